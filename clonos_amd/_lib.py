@@ -1,0 +1,185 @@
+"""ctypes binding of libclonos_engine.so (the C-ABI in include/clonos_engine.h).
+
+The library is the only compute path: there is no CPU fallback.  If the library is
+missing this module raises at import time; if no GPU is visible, engine creation fails
+with CLG_E_DEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libclonos_engine.so")
+
+# ---- status codes (clonos_engine.h) ------------------------------------------------
+CLG_OK = 0
+CLG_E_INVALID_ARG = -1
+CLG_E_CORRUPT_TAG = -2
+CLG_E_TRUNCATED = -3
+CLG_E_BAD_ENUM = -4
+CLG_E_NEG_LEN = -5
+CLG_E_BAD_SERIAL = -6
+CLG_E_CONSUMER_BACKWARDS = -7
+CLG_E_NO_CONSUMER = -8
+CLG_E_GAP = -9
+CLG_E_NOSPACE = -10
+CLG_E_CAPACITY = -11
+CLG_E_STATE = -12
+CLG_E_DEVICE = -13
+CLG_E_NO_LOG = -14
+
+STATUS_NAMES = {v: k for k, v in globals().items() if k.startswith("CLG_E_") or k == "CLG_OK"}
+
+CLG_MEM_HOST = 0
+CLG_MEM_DEVICE = 1
+CLG_F_TIMING = 1
+CLG_FULL_SHARING = -1
+
+EXPORTED = [
+    "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
+    "clg_engine_stream", "clg_sync", "clg_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find",
+    "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
+    "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
+    "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
+    "clg_slice_batch", "clg_consumer_seek", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
+    "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
+]
+
+
+class ClonosError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+class ChannelId(C.Structure):
+    _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
+
+
+class CausalLogIdC(C.Structure):
+    _fields_ = [
+        ("vertex_id", C.c_int16),
+        ("is_main", C.c_uint8),
+        ("subpartition", C.c_int8),
+        ("reserved", C.c_uint32),
+        ("irp_lower", C.c_int64),
+        ("irp_upper", C.c_int64),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("segment_bytes", C.c_uint32),
+        ("pool_segments", C.c_uint32),
+        ("device", C.c_int32),
+        ("sharing_depth", C.c_int32),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class LogState(C.Structure):
+    _fields_ = [("writer", C.c_int32), ("capacity", C.c_int32), ("n_components", C.c_int32), ("n_epochs", C.c_int32)]
+
+
+class SliceReq(C.Structure):
+    _fields_ = [("log", C.c_uint32), ("reserved", C.c_uint32), ("consumer", ChannelId), ("epoch", C.c_int64)]
+
+
+class SliceRes(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("has_delta", C.c_int32),
+        ("offset_from_epoch", C.c_int32),
+        ("len", C.c_int32),
+        ("out_off", C.c_uint64),
+    ]
+
+
+class Decoded(C.Structure):
+    _fields_ = [
+        ("off", C.c_void_p),
+        ("tag", C.c_void_p),
+        ("v0", C.c_void_p),
+        ("w_idx", C.c_void_p),
+        ("w_rc", C.c_void_p),
+        ("w_v1", C.c_void_p),
+        ("w_var_off", C.c_void_p),
+        ("w_var_len", C.c_void_p),
+        ("w_sub", C.c_void_p),
+        ("cap", C.c_uint64),
+        ("wcap", C.c_uint64),
+        ("out_kind", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("n_rec", C.c_uint64),
+        ("n_wide", C.c_uint64),
+        ("err_status", C.c_int32),
+        ("err_span", C.c_uint32),
+        ("err_off", C.c_int64),
+        ("err_tag", C.c_int32),
+        ("reserved2", C.c_uint32),
+    ]
+
+
+class KernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double), ("bytes", C.c_uint64)]
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m clonos_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    u32p, i32p, u64p, i64p = (C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
+                              C.POINTER(C.c_int64))
+    sig = {
+        "clg_config_default": (None, [C.POINTER(Config)]),
+        "clg_engine_create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+        "clg_engine_destroy": (None, [P]),
+        "clg_last_error": (C.c_char_p, []),
+        "clg_abi_version": (C.c_int, []),
+        "clg_engine_stream": (P, [P]),
+        "clg_sync": (C.c_int, [P]),
+        "clg_pool_stats": (C.c_int, [P, u32p, u32p]),
+        "clg_log_open": (C.c_int, [P, C.POINTER(CausalLogIdC), u32p]),
+        "clg_log_close": (C.c_int, [P, C.c_uint32]),
+        "clg_log_find": (C.c_int, [P, C.POINTER(CausalLogIdC), u32p]),
+        "clg_append": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_char_p, C.c_uint32]),
+        "clg_append_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P]),
+        "clg_upstream_delta": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_int32, C.c_char_p, C.c_uint32]),
+        "clg_log_length": (C.c_int, [P, C.c_uint32, i32p]),
+        "clg_has_delta": (C.c_int, [P, C.c_uint32, ChannelId, C.c_int64, i32p]),
+        "clg_offset_from_epoch": (C.c_int, [P, C.c_uint32, ChannelId, i32p]),
+        "clg_get_delta": (C.c_int, [P, C.c_uint32, ChannelId, C.c_int64, P, C.c_uint32, C.c_uint32, u32p]),
+        "clg_get_determinants": (C.c_int, [P, C.c_uint32, C.c_int64, P, C.c_uint32, C.c_uint32, u32p]),
+        "clg_notify_checkpoint_complete": (C.c_int, [P, C.c_uint32, C.c_int64]),
+        "clg_unregister_consumer": (C.c_int, [P, C.c_uint32, ChannelId]),
+        "clg_log_get_state": (C.c_int, [P, C.c_uint32, C.POINTER(LogState), P, P, C.c_int32]),
+        "clg_consumer_state": (C.c_int, [P, C.c_uint32, ChannelId, i32p, i64p, i32p]),
+        "clg_log_read_phys": (C.c_int, [P, C.c_uint32, C.c_int32, C.c_uint32, P]),
+        "clg_slice_batch": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, u64p]),
+        "clg_consumer_seek": (C.c_int, [P, C.c_uint32, ChannelId, C.c_int64, C.c_int32]),
+        "clg_truncate_all": (C.c_int, [P, C.c_int64, i32p]),
+        "clg_decode_host": (C.c_int, [P, P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
+        "clg_decode_logs": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
+        "clg_replay_prep": (C.c_int, [P, P, P, P, P, C.c_uint32, P, u32p, C.POINTER(Decoded), P]),
+        "clg_kernel_stats": (C.c_int, [P, C.POINTER(KernelStat), C.c_uint32, u32p]),
+        "clg_kernel_stats_reset": (C.c_int, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int) -> int:
+    if status != CLG_OK:
+        raise ClonosError(status, lib.clg_last_error().decode(errors="replace"))
+    return status

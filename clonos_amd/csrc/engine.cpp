@@ -1,0 +1,1034 @@
+// engine.cpp -- host side of the MI355X causal-log engine (implements include/clonos_engine.h).
+//
+// Owns: the HBM segment pool (components of determinantBufferSize bytes), the per-log
+// metadata with exactly the reference's semantics, host staging of appends, and the
+// batching of all byte work into gfx950 kernels (kernels.hip) on one HIP stream.
+//
+// R/ = /root/reference/flink-runtime/src/main/java/org/apache/flink/runtime/causal/.
+// The log metadata mirrors R/log/thread/ThreadCausalLogImpl.java:51-527 line for line in
+// behaviour (EpochStartOffset objects shared by reference with ConsumerOffset, Netty
+// component-granular discardReadComponents), but the bytes never leave HBM.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/clonos_engine.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return fail(CLG_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+#define CHK(x)                     \
+  do {                             \
+    int r_ = (x);                  \
+    if (r_ != CLG_OK) return r_;   \
+  } while (0)
+
+struct EpochStart {
+  int64_t id;
+  int32_t offset;
+};
+struct Consumer {
+  std::shared_ptr<EpochStart> es;  // ConsumerOffset.epochStart (a reference, may go stale)
+  int32_t offset;
+};
+struct ChKey {
+  uint64_t lo, hi;
+  bool operator==(const ChKey& o) const { return lo == o.lo && hi == o.hi; }
+};
+struct ChKeyHash {
+  size_t operator()(const ChKey& k) const { return std::hash<uint64_t>()(k.lo * 0x9E3779B97F4A7C15ull ^ k.hi); }
+};
+
+struct Log {
+  clg_causal_log_id id{};
+  bool open = false;
+  std::vector<uint32_t> segs;  // composite components
+  int32_t writer = 0;          // visibleWriterIndex (== composite writerIndex)
+  int32_t flushed = 0;         // physical bytes [0, flushed) are resident in HBM
+  std::vector<uint8_t> pending;  // staged bytes [flushed, writer)
+  std::map<int64_t, std::shared_ptr<EpochStart>> epochs;
+  std::unordered_map<ChKey, Consumer, ChKeyHash> consumers;
+};
+
+struct IdKey {
+  int16_t v;
+  uint8_t main;
+  int8_t sub;
+  int64_t lo, hi;
+  bool operator<(const IdKey& o) const {
+    if (v != o.v) return v < o.v;
+    if (main != o.main) return main < o.main;
+    if (main) return false;  // CausalLogID.equals: main logs compare by vertex only
+    if (lo != o.lo) return lo < o.lo;
+    if (hi != o.hi) return hi < o.hi;
+    return sub < o.sub;
+  }
+};
+IdKey key_of(const clg_causal_log_id& id) {
+  IdKey k{id.vertex_id, uint8_t(id.is_main ? 1 : 0), id.is_main ? int8_t(0) : id.subpartition,
+          id.is_main ? 0 : id.irp_lower, id.is_main ? 0 : id.irp_upper};
+  return k;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return CLG_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    size_t c = std::max(n, cap * 2);
+    c = (c + 255) & ~size_t(255);
+    hipError_t e = hipMalloc(&p, c + 64);
+    if (e != hipSuccess) {
+      cap = 0;
+      return fail(CLG_E_DEVICE, "hipMalloc(%zu) failed: %s", c, hipGetErrorString(e));
+    }
+    cap = c;
+    return CLG_OK;
+  }
+  ~DevBuf() {
+    if (p) hipFree(p);
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return CLG_OK;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    size_t c = std::max(n, cap * 2);
+    c = (c + 255) & ~size_t(255);
+    hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      cap = 0;
+      return fail(CLG_E_DEVICE, "hipHostMalloc(%zu) failed: %s", c, hipGetErrorString(e));
+    }
+    cap = c;
+    return CLG_OK;
+  }
+  ~PinBuf() {
+    if (p) hipHostFree(p);
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct Stat {
+  uint64_t launches = 0;
+  double ms = 0;
+  uint64_t bytes = 0;
+};
+struct PendingTiming {
+  std::string name;
+  hipEvent_t a, b;
+  uint64_t bytes;
+};
+
+}  // namespace
+
+struct clg_engine {
+  clg_config cfg{};
+  hipStream_t stream = nullptr;
+  uint8_t* pool = nullptr;
+  std::vector<uint32_t> free_segs;
+  std::vector<Log> logs;
+  std::map<IdKey, uint32_t> by_id;
+  int64_t latest_cp = 0;  // JobCausalLogImpl.latestCompletedCheckpoint (:92, :117)
+  std::recursive_mutex mu;
+
+  // staging / scratch
+  PinBuf h_stage, h_desc;
+  DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
+
+  // timing
+  std::map<std::string, Stat> stats;
+  std::vector<PendingTiming> timings;
+  std::vector<hipEvent_t> ev_pool;
+
+  uint32_t C() const { return cfg.segment_bytes; }
+  uint8_t* seg_addr(uint32_t s) const { return pool + size_t(s) * C(); }
+
+  // ---------------------------------------------------------------- timing helpers
+  hipEvent_t get_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+  }
+  template <class F>
+  int timed(const char* name, uint64_t bytes, F&& launch) {
+    if (!(cfg.flags & CLG_F_TIMING)) return launch();
+    hipEvent_t a = get_event(), b = get_event();
+    hipEventRecord(a, stream);
+    int r = launch();
+    hipEventRecord(b, stream);
+    timings.push_back(PendingTiming{name, a, b, bytes});
+    return r;
+  }
+  void collect_timings() {
+    for (auto& t : timings) {
+      float ms = 0;
+      hipEventSynchronize(t.b);
+      hipEventElapsedTime(&ms, t.a, t.b);
+      Stat& s = stats[t.name];
+      s.launches++;
+      s.ms += ms;
+      s.bytes += t.bytes;
+      ev_pool.push_back(t.a);
+      ev_pool.push_back(t.b);
+    }
+    timings.clear();
+  }
+  int sync() {
+    HIPCHK(hipStreamSynchronize(stream));
+    collect_timings();
+    return CLG_OK;
+  }
+
+  // ---------------------------------------------------------------- segments
+  int32_t capacity(const Log& l) const { return int32_t(l.segs.size()) * int32_t(C()); }
+  // notEnoughSpaceFor / addComponent (:351-353, :438-452): all-or-nothing.
+  int ensure_space(Log& l, int32_t n) {
+    int64_t need_bytes = int64_t(l.writer) + n - capacity(l);
+    if (need_bytes <= 0) return CLG_OK;
+    size_t need = size_t((need_bytes + C() - 1) / C());
+    if (need > free_segs.size())
+      return fail(CLG_E_NOSPACE, "segment pool exhausted (need %zu, free %zu)", need, free_segs.size());
+    for (size_t i = 0; i < need; ++i) {
+      l.segs.push_back(free_segs.back());
+      free_segs.pop_back();
+    }
+    return CLG_OK;
+  }
+  void write_pending(Log& l, const uint8_t* b, uint32_t n) {
+    l.pending.insert(l.pending.end(), b, b + n);
+    l.writer += int32_t(n);
+  }
+  std::shared_ptr<EpochStart> compute_if_absent(Log& l, int64_t e) {
+    auto it = l.epochs.find(e);
+    if (it != l.epochs.end()) return it->second;
+    auto es = std::make_shared<EpochStart>(EpochStart{e, l.writer});
+    l.epochs.emplace(e, es);
+    return es;
+  }
+  int32_t bytes_to_send(const Log& l, int64_t epoch, int32_t phys) const {  // :384-395
+    auto it = l.epochs.find(epoch + 1);
+    return (it != l.epochs.end() ? it->second->offset : l.writer) - phys;
+  }
+
+  int get_log(uint32_t h, Log** out) {
+    if (h >= logs.size() || !logs[h].open) return fail(CLG_E_NO_LOG, "unknown log handle %u", h);
+    *out = &logs[h];
+    return CLG_OK;
+  }
+
+  // ---------------------------------------------------------------- flush (append scatter)
+  int flush() {
+    size_t total = 0, nchunks = 0;
+    for (auto& l : logs)
+      if (l.open && !l.pending.empty()) {
+        total += l.pending.size();
+        nchunks += l.pending.size() / C() + 2;
+      }
+    if (total == 0) return CLG_OK;
+    const size_t desc_bytes = nchunks * sizeof(clg::ScatterChunk);
+    CHK(h_stage.ensure(total));
+    CHK(h_desc.ensure(desc_bytes));
+    CHK(d_stage.ensure(total));
+    CHK(d_desc.ensure(desc_bytes));
+    uint8_t* hs = h_stage.as<uint8_t>();
+    clg::ScatterChunk* ch = h_desc.as<clg::ScatterChunk>();
+    size_t off = 0, n = 0;
+    for (auto& l : logs) {
+      if (!l.open || l.pending.empty()) continue;
+      memcpy(hs + off, l.pending.data(), l.pending.size());
+      int32_t p = l.flushed;
+      size_t src = off;
+      size_t left = l.pending.size();
+      while (left) {
+        const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
+        const uint32_t take = uint32_t(std::min<size_t>(left, C() - so));
+        ch[n++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, 0};
+        p += int32_t(take);
+        src += take;
+        left -= take;
+      }
+      off += l.pending.size();
+      l.flushed = l.writer;
+      l.pending.clear();
+    }
+    HIPCHK(hipMemcpyAsync(d_stage.p, hs, total, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_desc.p, ch, n * sizeof(clg::ScatterChunk), hipMemcpyHostToDevice, stream));
+    CHK(timed("append_scatter", 2 * total, [&] {
+      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(n), d_stage.as<uint8_t>(), stream);
+    }));
+    // the pinned staging buffers are reused by the next flush: wait for the copies
+    HIPCHK(hipStreamSynchronize(stream));
+    return CLG_OK;
+  }
+
+  // ---------------------------------------------------------------- ThreadCausalLog ops
+  int append(uint32_t h, int64_t epoch, const uint8_t* b, uint32_t n) {  // :158-177
+    Log* l;
+    CHK(get_log(h, &l));
+    if (cfg.sharing_depth == 0) return CLG_OK;
+    if (n && !b) return fail(CLG_E_INVALID_ARG, "null record");
+    CHK(ensure_space(*l, int32_t(n)));
+    compute_if_absent(*l, epoch);
+    write_pending(*l, b, n);
+    return CLG_OK;
+  }
+
+  int upstream(uint32_t h, int64_t epoch, int32_t off_from_epoch, const uint8_t* d, uint32_t n) {  // :117-154
+    Log* l;
+    CHK(get_log(h, &l));
+    if (n == 0) return CLG_OK;
+    if (!d) return fail(CLG_E_INVALID_ARG, "null delta");
+    auto es = compute_if_absent(*l, epoch);
+    const int32_t cur = l->writer - es->offset;
+    const int32_t num_new = (off_from_epoch + int32_t(n)) - cur;
+    if (num_new > 0) {
+      if (num_new > int32_t(n))
+        return fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d", off_from_epoch,
+                    n, cur);
+      CHK(ensure_space(*l, num_new));
+      write_pending(*l, d + (n - uint32_t(num_new)), uint32_t(num_new));
+    }
+    return CLG_OK;
+  }
+
+  int has_delta(uint32_t h, ChKey k, int64_t epoch, int32_t* out) {  // :196-240
+    Log* l;
+    CHK(get_log(h, &l));
+    *out = 0;
+    if (cfg.sharing_depth == 0) return CLG_OK;
+    auto it = l->epochs.find(epoch);
+    if (it == l->epochs.end()) return CLG_OK;
+    auto ci = l->consumers.find(k);
+    if (ci == l->consumers.end()) ci = l->consumers.emplace(k, Consumer{it->second, 0}).first;
+    Consumer& c = ci->second;
+    if (c.es->id != epoch) {
+      if (c.es->id > epoch)
+        return fail(CLG_E_CONSUMER_BACKWARDS, "Consumer went backwards, current epoch %lld requested %lld",
+                    (long long)c.es->id, (long long)epoch);
+      c.es = it->second;
+      c.offset = 0;
+    }
+    *out = bytes_to_send(*l, epoch, c.es->offset + c.offset) != 0;
+    return CLG_OK;
+  }
+
+  int offset_from_epoch(uint32_t h, ChKey k, int32_t* out) {  // :243-246
+    Log* l;
+    CHK(get_log(h, &l));
+    auto ci = l->consumers.find(k);
+    if (ci == l->consumers.end()) return fail(CLG_E_NO_CONSUMER, "consumer not registered on log %u", h);
+    *out = ci->second.offset;
+    return CLG_OK;
+  }
+
+  // getDeltaForConsumer :249-277, metadata half: returns (phys, nb) and advances.
+  int take_delta(uint32_t h, ChKey k, int64_t epoch, int32_t* phys, int32_t* nb) {
+    Log* l;
+    CHK(get_log(h, &l));
+    auto ci = l->consumers.find(k);
+    if (ci == l->consumers.end()) return fail(CLG_E_NO_CONSUMER, "consumer not registered on log %u", h);
+    Consumer& c = ci->second;
+    const int32_t p = c.es->offset + c.offset;
+    const int32_t n = bytes_to_send(*l, epoch, p);
+    if (n < 0 || p < 0 || int64_t(p) + n > capacity(*l))
+      return fail(CLG_E_STATE, "delta [%d, %d) outside log of capacity %d", p, p + n, capacity(*l));
+    c.offset += n;
+    *phys = p;
+    *nb = n;
+    return CLG_OK;
+  }
+
+  // Pieces of [phys, phys+n) of a log, split at segment boundaries.
+  void add_pieces(const Log& l, int32_t phys, int32_t n, uint64_t dst, std::vector<clg::GatherPiece>& out) {
+    while (n > 0) {
+      const uint32_t si = uint32_t(phys) / C(), so = uint32_t(phys) % C();
+      const uint32_t take = std::min<uint32_t>(uint32_t(n), C() - so);
+      out.push_back(clg::GatherPiece{seg_addr(l.segs[si]) + so, dst, take, 0});
+      phys += int32_t(take);
+      dst += take;
+      n -= int32_t(take);
+    }
+  }
+
+  int run_gather(const std::vector<clg::GatherPiece>& pieces, uint64_t total, void* out, uint32_t out_kind) {
+    if (pieces.empty()) return CLG_OK;
+    const size_t db = pieces.size() * sizeof(clg::GatherPiece);
+    CHK(h_desc.ensure(db));
+    CHK(d_desc.ensure(db));
+    memcpy(h_desc.p, pieces.data(), db);
+    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, db, hipMemcpyHostToDevice, stream));
+    uint8_t* dout;
+    if (out_kind == CLG_MEM_DEVICE) {
+      dout = static_cast<uint8_t*>(out);
+    } else {
+      CHK(d_out.ensure(total));
+      dout = d_out.as<uint8_t>();
+    }
+    CHK(timed("slice_gather", 2 * total, [&] {
+      return clg::launch_gather(d_desc.as<clg::GatherPiece>(), uint32_t(pieces.size()), dout, stream);
+    }));
+    if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
+    return sync();
+  }
+
+  int get_delta(uint32_t h, ChKey k, int64_t epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
+    *n = 0;
+    Log* l;
+    CHK(get_log(h, &l));
+    auto ci = l->consumers.find(k);
+    if (ci == l->consumers.end()) return fail(CLG_E_NO_CONSUMER, "consumer not registered on log %u", h);
+    {
+      const int32_t p = ci->second.es->offset + ci->second.offset;
+      const int32_t nb = bytes_to_send(*l, epoch, p);
+      if (nb > 0 && uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
+    }
+    CHK(flush());
+    int32_t phys, nb;
+    CHK(take_delta(h, k, epoch, &phys, &nb));
+    std::vector<clg::GatherPiece> pieces;
+    add_pieces(*l, phys, nb, 0, pieces);
+    CHK(run_gather(pieces, uint64_t(nb), out, kind));
+    *n = uint32_t(nb);
+    return CLG_OK;
+  }
+
+  int determinants_range(const Log& l, int64_t start_epoch, int32_t* start, int32_t* nb) {  // :285-313
+    int32_t s = 0;
+    auto it = l.epochs.find(start_epoch);
+    if (it != l.epochs.end())
+      s = it->second->offset;
+    else if (!l.epochs.empty())
+      s = l.epochs.begin()->second->offset;
+    *start = s;
+    *nb = l.writer - s;
+    if (*nb < 0 || s < 0 || l.writer > capacity(l))  // makeDeltaUnsafe IndexOutOfBounds
+      return fail(CLG_E_STATE, "determinant range [%d, %d) outside the log", s, l.writer);
+    return CLG_OK;
+  }
+
+  int get_determinants(uint32_t h, int64_t start_epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
+    *n = 0;
+    Log* l;
+    CHK(get_log(h, &l));
+    if (cfg.sharing_depth == 0) return CLG_OK;
+    int32_t s, nb;
+    CHK(determinants_range(*l, start_epoch, &s, &nb));
+    if (uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "getDeterminants needs %d bytes", nb);
+    CHK(flush());
+    std::vector<clg::GatherPiece> pieces;
+    add_pieces(*l, s, nb, 0, pieces);
+    CHK(run_gather(pieces, uint64_t(nb), out, kind));
+    *n = uint32_t(nb);
+    return CLG_OK;
+  }
+
+  // notifyCheckpointComplete :398-435 (flushes first so no staged byte lives in a dropped
+  // component).
+  int checkpoint_complete(Log& l, int64_t cp) {
+    auto following = compute_if_absent(l, cp);
+    for (auto it = l.epochs.begin(); it != l.epochs.end();) {
+      if (it->first < cp)
+        it = l.epochs.erase(it);
+      else
+        ++it;
+    }
+    const int32_t R = following->offset;
+    if (R < 0 || R > l.writer) return fail(CLG_E_STATE, "readerIndex %d outside [0, %d]", R, l.writer);
+    int32_t move = 0;
+    if (R != 0) {
+      size_t drop;
+      if (R == l.writer && l.writer == capacity(l)) {  // discard-all case
+        drop = l.segs.size();
+        move = R;
+      } else {
+        drop = size_t(R) / C();
+        move = int32_t(drop * C());
+      }
+      for (size_t i = 0; i < drop; ++i) free_segs.push_back(l.segs[i]);
+      l.segs.erase(l.segs.begin(), l.segs.begin() + long(drop));
+    }
+    for (auto& e : l.epochs) e.second->offset -= move;
+    l.writer -= move;
+    l.flushed -= move;
+    return CLG_OK;
+  }
+
+  // ---------------------------------------------------------------- decode
+  struct DecodePlan {
+    std::vector<clg::TileDesc> tiles;
+    std::vector<clg::SpanDesc> spans;
+  };
+
+  void plan_host_span(DecodePlan& p, const uint8_t* dbase, uint64_t len, uint32_t s) {
+    clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, len};
+    uint64_t o = 0;
+    while (o < len) {
+      const uintptr_t addr = uintptr_t(dbase + o);
+      const uint32_t delta = uint32_t(addr & 15);
+      const uint32_t take = uint32_t(std::min<uint64_t>(len - o, uint64_t(clg::kTile - delta)));
+      p.tiles.push_back(clg::TileDesc{reinterpret_cast<const uint8_t*>(addr & ~uintptr_t(15)), delta, take, s, 0, o});
+      o += take;
+      sd.n_tiles++;
+    }
+    p.spans.push_back(sd);
+  }
+
+  void plan_log_span(DecodePlan& p, const Log& l, int32_t start, int32_t len, uint32_t s) {
+    clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, uint64_t(len)};
+    int32_t ph = start;
+    const int32_t end = start + len;
+    while (ph < end) {
+      const uint32_t si = uint32_t(ph) / C(), so = uint32_t(ph) % C();
+      const uint32_t take = std::min<uint32_t>(uint32_t(end - ph), C() - so);
+      // tiles never exceed kTile aligned bytes: split large segments
+      uint32_t done = 0;
+      while (done < take) {
+        const uint32_t o = so + done;
+        const uint32_t delta = o & 15;
+        const uint32_t t = std::min<uint32_t>(take - done, uint32_t(clg::kTile) - delta);
+        p.tiles.push_back(clg::TileDesc{seg_addr(l.segs[si]) + (o & ~15u), delta, t, s, 0, uint64_t(ph - start + int32_t(done))});
+        done += t;
+        sd.n_tiles++;
+      }
+      ph += int32_t(take);
+    }
+    p.spans.push_back(sd);
+  }
+
+  int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+    out->n_rec = out->n_wide = 0;
+    out->err_status = CLG_OK;
+    out->err_span = 0;
+    out->err_off = -1;
+    out->err_tag = 0;
+    const uint32_t nt = uint32_t(p.tiles.size()), ns = uint32_t(p.spans.size());
+    if (ns == 0) return CLG_OK;
+    CHK(d_tiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
+    CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
+    CHK(d_agg.ensure(std::max<size_t>(1, nt) * clg::kEntries * sizeof(uint64_t)));
+    CHK(d_conv.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileConv)));
+    CHK(d_tres.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileRes)));
+    CHK(d_sres.ensure(ns * sizeof(clg::SpanRes)));
+    CHK(d_totals.ensure(2 * sizeof(uint64_t)));
+    const size_t hb = nt * sizeof(clg::TileDesc) + ns * sizeof(clg::SpanDesc);
+    CHK(h_desc.ensure(hb + ns * sizeof(clg::SpanRes) + 64));
+    uint8_t* hd = h_desc.as<uint8_t>();
+    memcpy(hd, p.tiles.data(), nt * sizeof(clg::TileDesc));
+    memcpy(hd + nt * sizeof(clg::TileDesc), p.spans.data(), ns * sizeof(clg::SpanDesc));
+    if (nt) HIPCHK(hipMemcpyAsync(d_tiles.p, hd, nt * sizeof(clg::TileDesc), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_spans.p, hd + nt * sizeof(clg::TileDesc), ns * sizeof(clg::SpanDesc),
+                          hipMemcpyHostToDevice, stream));
+
+    // outputs
+    clg::DecodeOut o{};
+    const bool dev = out->out_kind == CLG_MEM_DEVICE;
+    if (dev) {
+      o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
+                         out->w_var_len, out->w_sub, out->cap, out->wcap};
+    } else {
+      const size_t cap = std::max<uint64_t>(1, out->cap), wcap = std::max<uint64_t>(1, out->wcap);
+      CHK(d_o_off.ensure(cap * 4));
+      CHK(d_o_tag.ensure(cap));
+      CHK(d_o_v0.ensure(cap * 8));
+      CHK(d_o_widx.ensure(wcap * 4));
+      CHK(d_o_wrc.ensure(wcap * 4));
+      CHK(d_o_wv1.ensure(wcap * 8));
+      CHK(d_o_wvo.ensure(wcap * 4));
+      CHK(d_o_wvl.ensure(wcap * 4));
+      CHK(d_o_wsub.ensure(wcap));
+      o = clg::DecodeOut{d_o_off.as<uint32_t>(), d_o_tag.as<uint8_t>(), d_o_v0.as<int64_t>(), d_o_widx.as<uint32_t>(),
+                         d_o_wrc.as<int32_t>(), d_o_wv1.as<int64_t>(), d_o_wvo.as<uint32_t>(), d_o_wvl.as<uint32_t>(),
+                         d_o_wsub.as<uint8_t>(), out->cap, out->wcap};
+    }
+    auto* dt = d_tiles.as<clg::TileDesc>();
+    auto* ds = d_spans.as<clg::SpanDesc>();
+    CHK(timed("decode_tables", log_bytes, [&] {
+      return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), stream);
+    }));
+    CHK(timed("decode_resolve", uint64_t(nt) * clg::kEntries * 8, [&] {
+      return clg::launch_decode_resolve(dt, ds, ns, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(),
+                                        d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), stream);
+    }));
+    CHK(timed("decode_spanscan", uint64_t(ns) * 48, [&] {
+      return clg::launch_decode_spanscan(d_sres.as<clg::SpanRes>(), ns, d_totals.as<uint64_t>(), stream);
+    }));
+    // emit bytes are attributed after the counts are known (below)
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (cfg.flags & CLG_F_TIMING) {
+      ea = get_event();
+      eb = get_event();
+      hipEventRecord(ea, stream);
+    }
+    CHK(clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
+                                d_sres.as<clg::SpanRes>(), o, stream));
+    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
+    clg::SpanRes* hres = reinterpret_cast<clg::SpanRes*>(hd + ((hb + 15) & ~size_t(15)));
+    HIPCHK(hipMemcpyAsync(hres, d_sres.p, ns * sizeof(clg::SpanRes), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    uint64_t nrec = 0, nwide = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (span_rec_base) span_rec_base[s] = hres[s].rec_base;
+      nrec += hres[s].n_rec;
+      nwide += hres[s].n_wide;
+      if (hres[s].status != CLG_OK && out->err_status == CLG_OK) {
+        out->err_status = hres[s].status;
+        out->err_span = s;
+        out->err_off = hres[s].err_off;
+        out->err_tag = hres[s].err_tag;
+      }
+    }
+    if (span_rec_base) span_rec_base[ns] = nrec;
+    if (cfg.flags & CLG_F_TIMING)
+      timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    out->n_rec = nrec;
+    out->n_wide = nwide;
+    if (!dev) {
+      const uint64_t r = std::min(nrec, out->cap), w = std::min(nwide, out->wcap);
+      if (r) {
+        HIPCHK(hipMemcpyAsync(out->off, d_o_off.p, r * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->tag, d_o_tag.p, r, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->v0, d_o_v0.p, r * 8, hipMemcpyDeviceToHost, stream));
+      }
+      if (w) {
+        HIPCHK(hipMemcpyAsync(out->w_idx, d_o_widx.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_rc, d_o_wrc.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_v1, d_o_wv1.p, w * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_var_off, d_o_wvo.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_var_len, d_o_wvl.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_sub, d_o_wsub.p, w, hipMemcpyDeviceToHost, stream));
+      }
+    }
+    CHK(sync());
+    if (nrec > out->cap || nwide > out->wcap)
+      return fail(CLG_E_CAPACITY, "decode produced %llu records / %llu wide rows, capacity %llu / %llu",
+                  (unsigned long long)nrec, (unsigned long long)nwide, (unsigned long long)out->cap,
+                  (unsigned long long)out->wcap);
+    if (out->err_status != CLG_OK)
+      return fail(out->err_status, "decode error %d in span %u at offset %lld (tag %d)", out->err_status, out->err_span,
+                  (long long)out->err_off, out->err_tag);
+    return CLG_OK;
+  }
+};
+
+// =======================================================================================
+// C-ABI
+// =======================================================================================
+extern "C" {
+
+#define ENGINE_GUARD(e)                                             \
+  if (!(e)) return fail(CLG_E_INVALID_ARG, "null engine");          \
+  std::lock_guard<std::recursive_mutex> guard_((e)->mu)
+
+void clg_config_default(clg_config* cfg) {
+  memset(cfg, 0, sizeof *cfg);
+  cfg->segment_bytes = 16384;  // NettyConfig.java:86-89
+  cfg->pool_segments = 16384;  // 256 MiB
+  cfg->device = 0;
+  cfg->sharing_depth = CLG_FULL_SHARING;
+}
+
+int clg_abi_version(void) { return CLG_ABI_VERSION; }
+
+const char* clg_last_error(void) { return g_err.c_str(); }
+
+int clg_engine_create(const clg_config* cfg, clg_engine** out) {
+  if (!cfg || !out) return fail(CLG_E_INVALID_ARG, "null argument");
+  *out = nullptr;
+  if (cfg->segment_bytes < 16 || (cfg->segment_bytes & 15) || cfg->pool_segments == 0)
+    return fail(CLG_E_INVALID_ARG, "segment_bytes must be a positive multiple of 16 and pool_segments > 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(CLG_E_DEVICE, "no HIP device visible (the engine has no CPU fallback)");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(CLG_E_INVALID_ARG, "device %d out of range", cfg->device);
+  std::unique_ptr<clg_engine> e(new clg_engine());
+  e->cfg = *cfg;
+  HIPCHK(hipSetDevice(cfg->device));
+  HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, pool_bytes + 256));  // +256: aligned over-reads past the last segment
+  e->pool = static_cast<uint8_t*>(p);
+  e->free_segs.resize(cfg->pool_segments);
+  for (uint32_t i = 0; i < cfg->pool_segments; ++i) e->free_segs[i] = cfg->pool_segments - 1 - i;
+  *out = e.release();
+  return CLG_OK;
+}
+
+void clg_engine_destroy(clg_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->cfg.device);
+  hipStreamSynchronize(e->stream);
+  for (auto& t : e->timings) {
+    hipEventDestroy(t.a);
+    hipEventDestroy(t.b);
+  }
+  for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  if (e->pool) hipFree(e->pool);
+  hipStreamDestroy(e->stream);
+  delete e;
+}
+
+void* clg_engine_stream(clg_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int clg_sync(clg_engine* e) {
+  ENGINE_GUARD(e);
+  CHK(e->flush());
+  return e->sync();
+}
+
+int clg_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments) {
+  ENGINE_GUARD(e);
+  *free_segments = uint32_t(e->free_segs.size());
+  *used = e->cfg.pool_segments - *free_segments;
+  return CLG_OK;
+}
+
+int clg_log_open(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle) {
+  ENGINE_GUARD(e);
+  if (!id || !handle) return fail(CLG_E_INVALID_ARG, "null argument");
+  const IdKey k = key_of(*id);
+  if (e->by_id.count(k)) return fail(CLG_E_INVALID_ARG, "log already open");
+  Log l;
+  l.id = *id;
+  l.open = true;
+  if (e->free_segs.empty()) return fail(CLG_E_NOSPACE, "segment pool exhausted");
+  l.segs.push_back(e->free_segs.back());  // ctor addComponent() :102
+  e->free_segs.pop_back();
+  const uint32_t h = uint32_t(e->logs.size());
+  e->logs.push_back(std::move(l));
+  e->by_id[k] = h;
+  *handle = h;
+  return CLG_OK;
+}
+
+int clg_log_close(clg_engine* e, uint32_t h) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  CHK(e->sync());
+  for (uint32_t s : l->segs) e->free_segs.push_back(s);
+  e->by_id.erase(key_of(l->id));
+  *l = Log();
+  return CLG_OK;
+}
+
+int clg_log_find(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle) {
+  ENGINE_GUARD(e);
+  auto it = e->by_id.find(key_of(*id));
+  if (it == e->by_id.end()) return fail(CLG_E_NO_LOG, "log not found");
+  *handle = it->second;
+  return CLG_OK;
+}
+
+int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n) {
+  ENGINE_GUARD(e);
+  return e->append(log, epoch, rec, n);
+}
+
+int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, const uint64_t* off,
+                     const uint32_t* len, uint32_t n, const uint8_t* bytes) {
+  ENGINE_GUARD(e);
+  for (uint32_t i = 0; i < n; ++i) CHK(e->append(log[i], epoch[i], bytes + off[i], len[i]));
+  return CLG_OK;
+}
+
+int clg_upstream_delta(clg_engine* e, uint32_t log, int64_t epoch, int32_t off, const uint8_t* d, uint32_t n) {
+  ENGINE_GUARD(e);
+  return e->upstream(log, epoch, off, d, n);
+}
+
+int clg_log_length(clg_engine* e, uint32_t h, int32_t* out) {  // :180-192
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  *out = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
+  return CLG_OK;
+}
+
+int clg_has_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t* out) {
+  ENGINE_GUARD(e);
+  return e->has_delta(log, ChKey{c.lo, c.hi}, epoch, out);
+}
+
+int clg_offset_from_epoch(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* out) {
+  ENGINE_GUARD(e);
+  return e->offset_from_epoch(log, ChKey{c.lo, c.hi}, out);
+}
+
+int clg_get_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, void* out, uint32_t cap,
+                  uint32_t kind, uint32_t* n) {
+  ENGINE_GUARD(e);
+  return e->get_delta(log, ChKey{c.lo, c.hi}, epoch, out, cap, kind, n);
+}
+
+int clg_get_determinants(clg_engine* e, uint32_t log, int64_t start_epoch, void* out, uint32_t cap, uint32_t kind,
+                         uint32_t* n) {
+  ENGINE_GUARD(e);
+  return e->get_determinants(log, start_epoch, out, cap, kind, n);
+}
+
+int clg_notify_checkpoint_complete(clg_engine* e, uint32_t h, int64_t cp) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  CHK(e->flush());
+  return e->checkpoint_complete(*l, cp);
+}
+
+int clg_unregister_consumer(clg_engine* e, uint32_t h, clg_channel_id c) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  l->consumers.erase(ChKey{c.lo, c.hi});
+  return CLG_OK;
+}
+
+int clg_log_get_state(clg_engine* e, uint32_t h, clg_log_state* st, int64_t* ids, int32_t* offs, int32_t cap) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  st->writer = l->writer;
+  st->capacity = e->capacity(*l);
+  st->n_components = int32_t(l->segs.size());
+  st->n_epochs = int32_t(l->epochs.size());
+  int32_t i = 0;
+  for (auto& ep : l->epochs) {
+    if (i < cap) {
+      if (ids) ids[i] = ep.first;
+      if (offs) offs[i] = ep.second->offset;
+    }
+    ++i;
+  }
+  return i > cap && (ids || offs) ? fail(CLG_E_CAPACITY, "%d epochs", i) : CLG_OK;
+}
+
+int clg_consumer_state(clg_engine* e, uint32_t h, clg_channel_id c, int32_t* exists, int64_t* epoch, int32_t* offset) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  auto ci = l->consumers.find(ChKey{c.lo, c.hi});
+  *exists = ci != l->consumers.end();
+  if (*exists) {
+    *epoch = ci->second.es->id;
+    *offset = ci->second.offset;
+  }
+  return CLG_OK;
+}
+
+int clg_log_read_phys(clg_engine* e, uint32_t h, int32_t phys, uint32_t n, uint8_t* host_out) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  if (phys < 0 || int64_t(phys) + n > e->capacity(*l)) return fail(CLG_E_STATE, "range outside log");
+  CHK(e->flush());
+  std::vector<clg::GatherPiece> pieces;
+  e->add_pieces(*l, phys, int32_t(n), 0, pieces);
+  return e->run_gather(pieces, n, host_out, CLG_MEM_HOST);
+}
+
+int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res, void* out, uint64_t cap,
+                    uint32_t out_kind, uint64_t* total) {
+  ENGINE_GUARD(e);
+  if (n && (!reqs || !res)) return fail(CLG_E_INVALID_ARG, "null argument");
+  CHK(e->flush());
+  std::vector<clg::GatherPiece> pieces;
+  pieces.reserve(n * 2);
+  uint64_t dst = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    clg_slice_res& r = res[i];
+    r = clg_slice_res{CLG_OK, 0, 0, 0, dst};
+    const ChKey k{reqs[i].consumer.lo, reqs[i].consumer.hi};
+    int32_t has = 0;
+    int st = e->has_delta(reqs[i].log, k, reqs[i].epoch, &has);
+    if (st != CLG_OK) {
+      r.status = st;
+      continue;
+    }
+    r.has_delta = has;
+    if (!has) continue;
+    st = e->offset_from_epoch(reqs[i].log, k, &r.offset_from_epoch);  // Abstract...:199 before :201
+    if (st != CLG_OK) {
+      r.status = st;
+      continue;
+    }
+    int32_t phys, nb;
+    st = e->take_delta(reqs[i].log, k, reqs[i].epoch, &phys, &nb);
+    if (st != CLG_OK) {
+      r.status = st;
+      continue;
+    }
+    if (dst + uint64_t(nb) > cap) {
+      // undo the consumer advance so the request can be retried with a bigger buffer
+      e->logs[reqs[i].log].consumers[k].offset -= nb;
+      r.status = CLG_E_CAPACITY;
+      continue;
+    }
+    r.len = nb;
+    e->add_pieces(e->logs[reqs[i].log], phys, nb, dst, pieces);
+    dst += uint64_t(nb);
+  }
+  if (total) *total = dst;
+  return e->run_gather(pieces, dst, out, out_kind);
+}
+
+int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch, int32_t offset) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  auto it = l->epochs.find(epoch);
+  if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)epoch);
+  l->consumers[ChKey{c.lo, c.hi}] = Consumer{it->second, offset};
+  return CLG_OK;
+}
+
+int clg_truncate_all(clg_engine* e, int64_t cp, int32_t* applied) {  // JobCausalLogImpl :230-246
+  ENGINE_GUARD(e);
+  if (applied) *applied = 0;
+  if (e->latest_cp >= cp) return CLG_OK;
+  e->latest_cp = cp;
+  CHK(e->flush());
+  for (auto& l : e->logs)
+    if (l.open) CHK(e->checkpoint_complete(l, cp));
+  if (applied) *applied = 1;
+  return CLG_OK;
+}
+
+int clg_decode_host(clg_engine* e, const uint8_t* bytes, const uint64_t* span_off, const uint64_t* span_len, uint32_t n,
+                    clg_decoded* out, uint64_t* span_rec_base) {
+  ENGINE_GUARD(e);
+  if (!out || (n && (!span_off || !span_len))) return fail(CLG_E_INVALID_ARG, "null argument");
+  uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (span_len[i] == 0) continue;
+    lo = std::min(lo, span_off[i]);
+    hi = std::max(hi, span_off[i] + span_len[i]);
+    total += span_len[i];
+  }
+  if (lo == UINT64_MAX) lo = hi = 0;
+  CHK(e->d_stage.ensure(hi - lo + 16));
+  CHK(e->h_stage.ensure(hi - lo + 16));
+  if (hi > lo) {
+    memcpy(e->h_stage.p, bytes + lo, hi - lo);
+    HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, hi - lo, hipMemcpyHostToDevice, e->stream));
+  }
+  clg_engine::DecodePlan p;
+  for (uint32_t i = 0; i < n; ++i)
+    e->plan_host_span(p, e->d_stage.as<uint8_t>() + (span_len[i] ? span_off[i] - lo : 0), span_len[i], i);
+  return e->run_decode(p, total, out, span_rec_base);
+}
+
+int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n, clg_decoded* out,
+                    uint64_t* span_rec_base) {
+  ENGINE_GUARD(e);
+  if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
+  CHK(e->flush());
+  clg_engine::DecodePlan p;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    Log* l;
+    CHK(e->get_log(log[i], &l));
+    int32_t s = 0, nb = 0;
+    if (e->cfg.sharing_depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &s, &nb));
+    e->plan_log_span(p, *l, s, nb, i);
+    total += uint64_t(nb);
+  }
+  return e->run_decode(p, total, out, span_rec_base);
+}
+
+int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off, const uint64_t* len,
+                    uint32_t n, uint32_t* winner, uint32_t* n_keys, clg_decoded* out, uint64_t* span_rec_base) {
+  ENGINE_GUARD(e);
+  if (n && (!key || !off || !len || !winner || !n_keys)) return fail(CLG_E_INVALID_ARG, "null argument");
+  // DeterminantResponseEvent.merge :136-146: per CausalLogID keep the longer buffer,
+  // ties -> the later one (v2).  Keys keep first-appearance order.
+  std::unordered_map<uint64_t, uint32_t> best;
+  std::vector<uint64_t> order;
+  for (uint32_t i = 0; i < n; ++i) {
+    auto it = best.find(key[i]);
+    if (it == best.end()) {
+      best.emplace(key[i], i);
+      order.push_back(key[i]);
+    } else if (!(len[it->second] > len[i])) {
+      it->second = i;
+    }
+  }
+  *n_keys = uint32_t(order.size());
+  std::vector<uint64_t> so(order.size()), sl(order.size());
+  for (size_t k = 0; k < order.size(); ++k) {
+    winner[k] = best[order[k]];
+    so[k] = off[winner[k]];
+    sl[k] = len[winner[k]];
+  }
+  if (!out) return CLG_OK;
+  return clg_decode_host(e, bytes, so.data(), sl.data(), uint32_t(order.size()), out, span_rec_base);
+}
+
+int clg_kernel_stats(clg_engine* e, clg_kernel_stat* out, uint32_t cap, uint32_t* n) {
+  ENGINE_GUARD(e);
+  CHK(e->sync());
+  uint32_t i = 0;
+  for (auto& kv : e->stats) {
+    if (i < cap) {
+      memset(&out[i], 0, sizeof out[i]);
+      snprintf(out[i].name, sizeof out[i].name, "%s", kv.first.c_str());
+      out[i].launches = kv.second.launches;
+      out[i].total_ms = kv.second.ms;
+      out[i].bytes = kv.second.bytes;
+    }
+    ++i;
+  }
+  *n = i;
+  return CLG_OK;
+}
+
+int clg_kernel_stats_reset(clg_engine* e) {
+  ENGINE_GUARD(e);
+  CHK(e->sync());
+  e->stats.clear();
+  return CLG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+// kernels.h -- descriptors shared by the host engine (engine.cpp) and the gfx950
+// kernels (kernels.hip).  Plain structs, no HIP types.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace clg {
+
+// ---- decode geometry ---------------------------------------------------------
+// A tile is one wave's unit of decode work: a contiguous run of at most kTile bytes
+// of one span, lying inside one HBM segment (or one 16 KiB window of a host-input
+// staging buffer).  The tile is split into kRegions regions of kRegion bytes; each
+// lane owns one region.  Coordinates inside a tile are "aligned coordinates":
+// a = delta + (byte offset from the tile's first valid byte), so that abase + a is
+// the byte's address and abase is 16-byte aligned.
+constexpr int kRegion = 256;
+constexpr int kRegions = 64;
+constexpr int kTile = kRegion * kRegions;  // 16384
+constexpr int kEntries = 64;               // transfer-table domain per region / per tile
+
+struct TileDesc {
+  const uint8_t* abase;  // 16-byte aligned
+  uint32_t delta;        // first valid byte is abase[delta]  (delta < 16)
+  uint32_t len;          // valid bytes (delta + len <= kTile)
+  uint32_t span;         // owning span
+  uint32_t pad;
+  uint64_t span_off;     // span offset of abase[delta]
+};
+
+struct SpanDesc {
+  uint32_t first_tile;
+  uint32_t n_tiles;
+  uint64_t len;
+};
+
+// Per-tile aggregate over tile entries e in [0, kEntries): e is the span offset of the
+// first record start at/after the tile start, relative to the tile start.
+// Packed u64: exit (u32, relative to the tile end; kExitErr / kExitFar sentinels) |
+// cnt (u16) << 32 | wcnt (u16) << 48.
+constexpr uint32_t kExitErr = 0xFFFFFFFFu;
+constexpr uint32_t kExitFar = 0xFFFFFFFEu;
+
+// Per-tile convergence info produced by the table kernel:
+//   conv_entry[l]: entry offset of region l (relative to the region's first valid byte)
+//                  shared by every live candidate path, or 0xFFFF if unknown;
+//   conv_suffix[l]: records (low 16) and wide records (high 16) on that shared path
+//                   from region l to the tile end.
+struct TileConv {
+  uint16_t entry[kRegions];
+  uint32_t suffix[kRegions];
+  uint32_t exit;       // tile exit (relative to tile end) of the shared path, or kExitErr
+  uint32_t valid;      // 1 if any region converged
+};
+
+// Resolution output per tile (filled by the resolve kernel).
+struct TileRes {
+  uint32_t entry;      // tile-relative offset of the first record start (>= len: none)
+  uint32_t limit;      // aligned coordinate where emission stops (failing record), or ~0
+  uint32_t flags;      // kResTableLive: entry < kEntries and its table path is live
+  uint32_t pad;
+  uint64_t rec_base;   // record index of the tile's first record (span-relative)
+  uint64_t wide_base;  // side-table index of the tile's first wide record (span-relative)
+};
+constexpr uint32_t kResTableLive = 1;
+
+struct SpanRes {
+  uint64_t n_rec;
+  uint64_t n_wide;
+  int32_t status;      // CLG_OK or decode error code
+  int32_t err_tag;
+  int64_t err_off;     // span offset of failing record
+  uint64_t rec_base;   // exclusive prefix over spans (filled by the span-scan kernel)
+  uint64_t wide_base;
+};
+
+struct DecodeOut {
+  uint32_t* off;
+  uint8_t* tag;
+  int64_t* v0;
+  uint32_t* w_idx;
+  int32_t* w_rc;
+  int64_t* w_v1;
+  uint32_t* w_var_off;
+  uint32_t* w_var_len;
+  uint8_t* w_sub;
+  uint64_t cap;
+  uint64_t wcap;
+};
+
+// ---- gather (delta slice) -------------------------------------------------------
+// A piece copies len bytes from src to out + dst; the source range lies inside one
+// segment.  Pieces are produced per slice request and split at segment boundaries.
+struct GatherPiece {
+  const uint8_t* src;
+  uint64_t dst;
+  uint32_t len;
+  uint32_t pad;
+};
+
+// ---- append scatter ---------------------------------------------------------------
+struct ScatterChunk {
+  uint8_t* dst;        // inside one segment
+  uint64_t src;        // offset into the staged upload buffer
+  uint32_t len;
+  uint32_t pad;
+};
+
+// ---- launchers (kernels.hip) -----------------------------------------------------------
+int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);
+int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream);
+int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
+                         uint64_t* d_agg, TileConv* d_conv, void* stream);
+int launch_decode_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                          const uint64_t* d_agg, const TileConv* d_conv, TileRes* d_tres,
+                          SpanRes* d_sres, void* stream);
+int launch_decode_spanscan(SpanRes* d_sres, uint32_t n_spans, uint64_t* d_totals, void* stream);
+int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
+                       const TileConv* d_conv, const TileRes* d_tres, const SpanRes* d_sres,
+                       DecodeOut out, void* stream);
+
+}  // namespace clg

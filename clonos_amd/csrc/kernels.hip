@@ -1,0 +1,839 @@
+// kernels.hip -- gfx950 kernels of the causal-log engine.
+//
+//  * k_scatter           batched append: staged host bytes -> HBM segments
+//  * k_gather            batched delta slice: segments -> packed per-consumer output
+//  * k_dec_tables        decode pass 1: per-lane backward DP over 256-byte regions of a
+//                        16 KiB tile -> per-region transfer tables -> tile aggregate
+//  * k_dec_resolve       decode pass 2: per-span walk over tile aggregates -> tile entries
+//  * k_dec_spanscan      decode pass 3: exclusive scan of per-span record counts
+//  * k_dec_emit          decode pass 4: per-lane forward parse of each region -> SoA
+//
+// Record lengths follow SimpleDeterminantEncoder.decodeNext (reference:
+// flink-runtime/.../causal/determinant/SimpleDeterminantEncoder.java:78-342).  The decode
+// design (speculative per-byte length, transfer functions over entry offsets, converged
+// region entries) is described in DESIGN.md section "Decode".
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/clonos_engine.h"
+#include "jser_device.h"
+#include "kernels.h"
+
+namespace clg {
+
+// ----------------------------------------------------------------------------------
+// Packed region-table entry: exit offset past the region end (16 bits, 0xFFFF = error,
+// 0xFFFE = far), record count (8 bits), wide-record count (8 bits).
+// ----------------------------------------------------------------------------------
+constexpr uint32_t kNsErr = 0xFFFFu;
+constexpr uint32_t kNsFar = 0xFFFEu;
+constexpr int kPitch = 65;  // dwords per region in the LDS tile image (64 + 1 pad)
+
+__device__ __forceinline__ uint32_t lds_byte_addr(uint32_t a) {
+  return ((a >> 8) * kPitch + ((a >> 2) & 63u)) * 4u + (a & 3u);
+}
+
+// Byte reader over a whole span (global memory, walks the span's tile list).
+struct SpanReader {
+  const TileDesc* tiles;
+  uint32_t t0, t1, cur;
+  uint64_t len;
+  __device__ int at(uint64_t o) {
+    if (o >= len) return -1;
+    while (cur > t0 && o < tiles[cur].span_off) --cur;
+    while (cur + 1 < t1 && o >= tiles[cur].span_off + tiles[cur].len) ++cur;
+    const TileDesc& t = tiles[cur];
+    return t.abase[t.delta + (o - t.span_off)];
+  }
+};
+
+// Byte reader for one tile: the LDS image for bytes inside the tile, the span reader
+// beyond it.  Coordinates are the tile's aligned coordinates.
+struct TileReader {
+  const uint8_t* lds;
+  uint32_t lo, hi;
+  uint64_t so;  // span offset of aligned coordinate lo
+  SpanReader* sr;
+  __device__ __forceinline__ int at(uint32_t a) {
+    if (a < hi) return lds[lds_byte_addr(a)];
+    return sr->at(so + (a - lo));
+  }
+  __device__ __forceinline__ uint64_t span_off(uint32_t a) const { return so + (a - lo); }
+};
+
+// Bytes relative to a record start, for the length / value parsers.
+template <class R>
+struct At {
+  R* r;
+  uint32_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + (uint32_t)k); }
+};
+struct AtSpan {
+  SpanReader* r;
+  uint64_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + k); }
+};
+
+template <class F>
+__device__ __forceinline__ uint32_t rd_be32(F& b, uint32_t k) {
+  return (uint32_t)b(k) << 24 | (uint32_t)b(k + 1) << 16 | (uint32_t)b(k + 2) << 8 | (uint32_t)b(k + 3);
+}
+template <class F>
+__device__ __forceinline__ uint64_t rd_be64(F& b, uint32_t k) {
+  return (uint64_t)rd_be32(b, k) << 32 | rd_be32(b, k + 4);
+}
+
+// Exact record length at a record start (decodeNext read order and error precedence).
+// `avail` = bytes from the record start to the span end (>= 1).  Returns L > 0 or a
+// negative CLG_E_* status.
+template <class F>
+__device__ __noinline__ int64_t rec_len_slow(F& b, uint64_t avail) {
+  const int tag = (int8_t)b(0);
+  int64_t L;
+  switch (tag) {
+    case CLG_TAG_ORDER: L = 2; break;
+    case CLG_TAG_TIMESTAMP: L = 9; break;
+    case CLG_TAG_RNG:
+    case CLG_TAG_BUFFER_BUILT: L = 5; break;
+    case CLG_TAG_IGNORE_CHECKPOINT: L = 13; break;
+    case CLG_TAG_TIMER_TRIGGER: {
+      if (avail < 14) return CLG_E_TRUNCATED;
+      const int ord = (int8_t)b(13);
+      if (ord < 0 || ord > 6) return CLG_E_BAD_ENUM;
+      if (ord == 6) {
+        if (avail < 18) return CLG_E_TRUNCATED;
+        const int32_t nl = (int32_t)rd_be32(b, 14);
+        if (nl < 0) return CLG_E_NEG_LEN;
+        L = 18 + (int64_t)nl;
+      } else {
+        L = 14;
+      }
+      break;
+    }
+    case CLG_TAG_SOURCE_CHECKPOINT: {
+      if (avail < 23) return CLG_E_TRUNCATED;
+      if (b(22) != 0) {
+        if (avail < 27) return CLG_E_TRUNCATED;
+        const int32_t rl = (int32_t)rd_be32(b, 23);
+        if (rl < 0) return CLG_E_NEG_LEN;
+        L = 27 + (int64_t)rl;
+      } else {
+        L = 23;
+      }
+      if ((uint64_t)L > avail) return CLG_E_TRUNCATED;
+      const int ord = (int8_t)b(21);
+      if (ord < 0 || ord > 1) return CLG_E_BAD_ENUM;
+      return L;
+    }
+    case CLG_TAG_SERIALIZABLE: {
+      struct Shift {
+        F* f;
+        __device__ int operator()(uint64_t k) { return (*f)(k + 1); }
+      } sh{&b};
+      const int64_t j = jser::stream_len(sh, avail - 1);
+      if (j < 0) return CLG_E_BAD_SERIAL;
+      L = 1 + j;
+      break;
+    }
+    default:
+      return CLG_E_CORRUPT_TAG;
+  }
+  if ((uint64_t)L > avail) return CLG_E_TRUNCATED;
+  return L;
+}
+
+// Fixed-length tags via a nibble LUT: 0->2, 1->9, 2->5, 6->13, 7->5; 0 = "slow" (3,4,5).
+__device__ __forceinline__ int fast_len(int tag) {
+  constexpr uint32_t lut = 2u | 9u << 4 | 5u << 8 | 0u << 12 | 0u << 16 | 0u << 20 | 13u << 24 | 5u << 28;
+  return (tag >= 0 && tag < 8) ? (int)((lut >> (4 * tag)) & 0xF) : -1;
+}
+__device__ __forceinline__ uint32_t is_wide(int tag) { return (tag >= 3 && tag <= 6) ? 1u : 0u; }
+
+// One decoded record (values + length), exact.
+struct Rec {
+  int64_t v0, v1;
+  int32_t rc;
+  uint32_t var_off, var_len;  // var_off relative to record start
+  uint32_t L;
+  uint8_t tag, sub, wide;
+};
+
+template <class F>
+__device__ int decode_rec(F& b, uint64_t avail, Rec& r) {
+  const int64_t L = rec_len_slow(b, avail);
+  if (L < 0) return (int)L;
+  const int tag = b(0);
+  r.tag = (uint8_t)tag;
+  r.L = (uint32_t)L;
+  r.wide = (uint8_t)is_wide(tag);
+  r.v1 = 0;
+  r.rc = 0;
+  r.var_off = 0;
+  r.var_len = 0;
+  r.sub = 0;
+  switch (tag) {
+    case CLG_TAG_ORDER: r.v0 = (int8_t)b(1); break;
+    case CLG_TAG_TIMESTAMP: r.v0 = (int64_t)rd_be64(b, 1); break;
+    case CLG_TAG_RNG:
+    case CLG_TAG_BUFFER_BUILT: r.v0 = (int32_t)rd_be32(b, 1); break;
+    case CLG_TAG_IGNORE_CHECKPOINT:
+      r.rc = (int32_t)rd_be32(b, 1);
+      r.v0 = (int64_t)rd_be64(b, 5);
+      break;
+    case CLG_TAG_TIMER_TRIGGER:
+      r.rc = (int32_t)rd_be32(b, 1);
+      r.v0 = (int64_t)rd_be64(b, 5);
+      r.sub = (uint8_t)b(13);
+      if (r.sub == 6) {
+        r.var_off = 18;
+        r.var_len = (uint32_t)(L - 18);
+      }
+      break;
+    case CLG_TAG_SOURCE_CHECKPOINT:
+      r.rc = (int32_t)rd_be32(b, 1);
+      r.v0 = (int64_t)rd_be64(b, 5);
+      r.v1 = (int64_t)rd_be64(b, 13);
+      r.sub = (uint8_t)b(21);
+      if (b(22) != 0) {
+        r.sub |= 0x80;
+        r.var_off = 27;
+        r.var_len = (uint32_t)(L - 27);
+      }
+      break;
+    case CLG_TAG_SERIALIZABLE:
+      r.v0 = L - 1;
+      r.var_off = 1;
+      r.var_len = (uint32_t)(L - 1);
+      break;
+  }
+  return CLG_OK;
+}
+
+// ==================================================================================
+// Append scatter: one wave per chunk.
+// ==================================================================================
+__global__ __launch_bounds__(256) void k_scatter(const ScatterChunk* __restrict__ chunks, uint32_t n,
+                                                 const uint8_t* __restrict__ src) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t c = wave; c < n; c += nwaves) {
+    const ScatterChunk ch = chunks[c];
+    for (uint32_t i = lane; i < ch.len; i += 64) ch.dst[i] = src[ch.src + i];
+  }
+}
+
+// ==================================================================================
+// Gather (delta slice): one block per piece; destination-aligned 16-byte chunks, the
+// source realigned in registers with v_alignbyte (shift is uniform per piece).
+// ==================================================================================
+__device__ __forceinline__ uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t s) {
+  return s ? __builtin_amdgcn_alignbyte(hi, lo, s) : lo;
+}
+// 16 bytes starting m bytes into the 32-byte window lo:hi (m in 1..15, uniform).
+__device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32_t m) {
+  const uint32_t s = m & 3;
+  switch (m >> 2) {
+    case 0: return make_uint4(fsh(lo.y, lo.x, s), fsh(lo.z, lo.y, s), fsh(lo.w, lo.z, s), fsh(hi.x, lo.w, s));
+    case 1: return make_uint4(fsh(lo.z, lo.y, s), fsh(lo.w, lo.z, s), fsh(hi.x, lo.w, s), fsh(hi.y, hi.x, s));
+    case 2: return make_uint4(fsh(lo.w, lo.z, s), fsh(hi.x, lo.w, s), fsh(hi.y, hi.x, s), fsh(hi.z, hi.y, s));
+    default: return make_uint4(fsh(hi.x, lo.w, s), fsh(hi.y, hi.x, s), fsh(hi.z, hi.y, s), fsh(hi.w, hi.z, s));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
+  const GatherPiece p = pieces[blockIdx.x];
+  if (p.len == 0) return;
+  uint8_t* dst = out + p.dst;
+  const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + p.len;
+  const uintptr_t a0 = d0 & ~(uintptr_t)15, a1 = (d1 - 1) & ~(uintptr_t)15;
+  const uintptr_t sdelta = (uintptr_t)p.src - d0;  // src address = dst address + sdelta
+  const uint32_t m = (uint32_t)(((uintptr_t)p.src - d0) & 15);
+  for (uintptr_t c = a0 + 16 * threadIdx.x; c <= a1; c += 16 * blockDim.x) {
+    if (c >= d0 && c + 16 <= d1) {
+      const uintptr_t s = c + sdelta;
+      const uintptr_t sa = s & ~(uintptr_t)15;
+      uint4 v;
+      if (m == 0) {
+        v = *reinterpret_cast<const uint4*>(sa);
+      } else {
+        const uint4 lo = *reinterpret_cast<const uint4*>(sa);
+        const uint4 hi = *reinterpret_cast<const uint4*>(sa + 16);
+        v = funnel16(lo, hi, m);
+      }
+      *reinterpret_cast<uint4*>(c) = v;
+    } else {
+      const uintptr_t b0 = c < d0 ? d0 : c, b1 = c + 16 > d1 ? d1 : c + 16;
+      for (uintptr_t x = b0; x < b1; ++x) *reinterpret_cast<uint8_t*>(x) = *reinterpret_cast<const uint8_t*>(x + sdelta);
+    }
+  }
+}
+
+// ==================================================================================
+// Decode, shared pieces.
+// ==================================================================================
+struct TileGeom {
+  uint32_t lo, hi;  // valid aligned coordinates
+  __device__ __forceinline__ uint32_t rs(int l) const { uint32_t s = (uint32_t)l * kRegion; return s < lo ? lo : s; }
+  __device__ __forceinline__ uint32_t re(int l) const { uint32_t e = (uint32_t)(l + 1) * kRegion; return e > hi ? hi : e; }
+};
+
+// Stage one tile into the padded LDS image (16-byte coalesced loads).
+__device__ __forceinline__ void stage_tile(uint32_t* s_tile, const TileDesc& td, uint32_t lane) {
+  const uint32_t words = (td.delta + td.len + 15) >> 4;
+  for (uint32_t w = lane; w < words; w += 64) {
+    const uint4 v = *reinterpret_cast<const uint4*>(td.abase + 16 * w);
+    const uint32_t a = 16 * w;
+    const uint32_t d = (a >> 8) * kPitch + ((a >> 2) & 63u);
+    s_tile[d + 0] = v.x;
+    s_tile[d + 1] = v.y;
+    s_tile[d + 2] = v.z;
+    s_tile[d + 3] = v.w;
+  }
+}
+
+// Forward parse of one region from an entry (aligned coordinate `a`) to the region end.
+// Returns the exit (aligned coordinate of the first record start >= re) and counts, or
+// a negative status.  Used for in-region long jumps and for concrete chain walks.
+__device__ int region_forward(TileReader& rd, uint64_t span_len, uint32_t a, uint32_t re, uint32_t* exit,
+                              uint32_t* cnt, uint32_t* wcnt) {
+  uint32_t c = 0, w = 0;
+  while (a < re) {
+    const uint64_t avail = span_len - rd.span_off(a);
+    At<TileReader> b{&rd, a};
+    const int64_t L = rec_len_slow(b, avail);
+    if (L < 0) return (int)L;
+    w += is_wide(rd.at(a));
+    ++c;
+    if ((uint64_t)a + (uint64_t)L > 0xFFFFFFF0ull) return CLG_E_STATE;
+    a += (uint32_t)L;
+  }
+  *exit = a;
+  *cnt = c;
+  *wcnt = w;
+  return CLG_OK;
+}
+
+// ==================================================================================
+// Pass 1: transfer tables.  One wave per tile; lane l owns region l.
+// ==================================================================================
+__global__ __launch_bounds__(64) void k_dec_tables(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                   uint64_t* __restrict__ agg, TileConv* __restrict__ conv) {
+  __shared__ uint32_t s_tile[kRegions * kPitch];
+  __shared__ uint32_t s_ring[kEntries * 64];  // [position mod 64][lane]
+  __shared__ uint32_t s_conv_lane[kRegions];
+  __shared__ uint32_t s_conv_cum[kRegions];
+  __shared__ uint16_t s_conv_entry[kRegions];
+
+  const uint32_t t = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const TileDesc td = tiles[t];
+  const SpanDesc sd = spans[td.span];
+  stage_tile(s_tile, td, lane);
+  __syncthreads();
+
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  TileReader rd{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
+  const TileGeom g{td.delta, td.delta + td.len};
+
+  // ---- backward DP over my region ----
+  const uint32_t rs = g.rs(lane), re = g.re(lane);
+  const int RL = re > rs ? (int)(re - rs) : 0;
+  for (int q = kRegion - 1; q >= 0; --q) {
+    if (q >= RL) continue;
+    const uint32_t a = rs + (uint32_t)q;
+    const int tag = rd.at(a);
+    int64_t L = fast_len(tag);
+    if (L <= 0) {
+      const uint64_t avail = sd.len - rd.span_off(a);
+      At<TileReader> b{&rd, a};
+      L = rec_len_slow(b, avail);
+    } else if ((uint64_t)L > sd.len - rd.span_off(a)) {
+      L = CLG_E_TRUNCATED;
+    }
+    uint32_t ns;
+    if (L < 0) {
+      ns = kNsErr;
+    } else {
+      const uint64_t t2 = (uint64_t)q + (uint64_t)L;
+      const uint32_t inc = (1u << 16) | (is_wide(tag) << 24);
+      if (t2 >= (uint64_t)RL) {
+        const uint64_t rel = t2 - (uint64_t)RL;
+        ns = (rel >= kNsFar ? kNsFar : (uint32_t)rel) | inc;
+      } else if (L < kEntries) {
+        const uint32_t x = s_ring[((uint32_t)t2 & 63u) * 64 + lane];
+        const uint32_t xr = x & 0xFFFFu;
+        ns = (xr >= kNsFar) ? xr : x + inc;
+      } else {
+        uint32_t ex, c, w;
+        const int st = region_forward(rd, sd.len, rs + (uint32_t)t2, re, &ex, &c, &w);
+        if (st != CLG_OK) {
+          ns = kNsErr;
+        } else {
+          const uint32_t rel = ex - re;
+          ns = (rel >= kNsFar ? kNsFar : rel) | ((c + 1) << 16) | ((w + is_wide(tag)) << 24);
+        }
+      }
+    }
+    s_ring[((uint32_t)q & 63u) * 64 + lane] = ns;
+  }
+  __syncthreads();
+
+  // ---- candidate walk: lane i follows tile entry i through all regions ----
+  uint32_t pos = td.delta + lane;  // aligned coordinate of the candidate's current record start
+  uint32_t cnt = 0, wcnt = 0;
+  uint32_t dead = 0;  // 0 live, 1 error, 2 far
+  bool any_conv = false;
+  for (int l = 0; l < kRegions; ++l) {
+    const uint32_t rsl = g.rs(l), rel_ = g.re(l);
+    if (rsl >= rel_) {
+      if (lane == 0) s_conv_entry[l] = 0xFFFF;
+      continue;
+    }
+    // convergence vote among live candidates
+    const uint64_t live = __ballot(dead == 0);
+    bool conv_here = false;
+    if (live) {
+      const int first = __builtin_ctzll(live);
+      const uint32_t p0 = __shfl(pos, first);
+      conv_here = __all(dead != 0 || pos == p0);
+      if (lane == 0) {
+        const bool ok = conv_here && p0 >= rsl && (p0 - rsl) < 0xFFFFu;
+        s_conv_entry[l] = ok ? (uint16_t)(p0 - rsl) : (uint16_t)0xFFFF;
+        s_conv_lane[l] = (uint32_t)first;
+      }
+      const uint32_t c0 = __shfl(cnt | (wcnt << 16), first);
+      if (lane == 0) s_conv_cum[l] = c0;
+      any_conv |= conv_here;
+    } else if (lane == 0) {
+      s_conv_entry[l] = 0xFFFF;
+    }
+    if (dead == 0 && pos < rel_) {
+      const uint32_t e = pos - rsl;
+      const uint32_t RLl = rel_ - rsl;
+      if (e < (uint32_t)kEntries && e < RLl) {
+        const uint32_t x = s_ring[e * 64 + (uint32_t)l];
+        const uint32_t xr = x & 0xFFFFu;
+        if (xr == kNsErr) {
+          dead = 1;
+        } else if (xr == kNsFar) {
+          dead = 2;
+        } else {
+          pos = rel_ + xr;
+          cnt += (x >> 16) & 0xFF;
+          wcnt += x >> 24;
+        }
+      } else {
+        uint32_t ex, c, w;
+        const int st = region_forward(rd, sd.len, pos, rel_, &ex, &c, &w);
+        if (st != CLG_OK) {
+          dead = 1;
+        } else {
+          pos = ex;
+          cnt += c;
+          wcnt += w;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const uint32_t tile_end = td.delta + td.len;
+  uint64_t a64;
+  if (dead == 1) {
+    a64 = kExitErr;
+  } else if (dead == 2) {
+    a64 = kExitFar;
+  } else {
+    a64 = (uint64_t)(pos - tile_end) | ((uint64_t)cnt << 32) | ((uint64_t)wcnt << 48);
+  }
+  agg[(uint64_t)t * kEntries + lane] = a64;
+
+  // ---- convergence info ----
+  TileConv* cv = conv + t;
+  const uint16_t ce = s_conv_entry[lane];
+  cv->entry[lane] = ce;
+  const uint32_t k_ref = (ce != 0xFFFF) ? s_conv_lane[lane] : 0u;
+  const uint32_t tot = __shfl(cnt | (wcnt << 16), (int)k_ref);  // executed by every lane
+  uint32_t suffix = 0;
+  if (ce != 0xFFFF) {
+    const uint32_t cum = s_conv_cum[lane];
+    suffix = ((tot & 0xFFFF) - (cum & 0xFFFF)) | (((tot >> 16) - (cum >> 16)) << 16);
+  }
+  cv->suffix[lane] = suffix;
+  const uint64_t live_end = __ballot(dead == 0);
+  if (lane == 0) {
+    uint32_t ex = kExitErr;
+    if (live_end) ex = 0;  // filled below by the first live lane
+    cv->valid = any_conv ? 1u : 0u;
+    cv->exit = ex;
+  }
+  if (live_end) {
+    const int first = __builtin_ctzll(live_end);
+    const uint32_t p0 = __shfl(pos, first);
+    const bool same = __all(dead != 0 || pos == p0);
+    if (lane == 0) cv->exit = same ? p0 - tile_end : kExitErr;
+  }
+}
+
+// ==================================================================================
+// Pass 2: resolve tile entries per span.  One block per span; thread 0 walks the
+// span's tiles over an LDS cache of their aggregates (loaded cooperatively).
+// ==================================================================================
+constexpr int kResolveChunk = 96;  // tiles cached in LDS per step (96*64*8 = 48 KiB)
+
+// Concrete evaluation of one tile from entry `e` (tile-relative offset), serial, exact.
+// Uses convergence info to short-cut once the path meets the shared path.
+__device__ int tile_eval_concrete(const TileDesc* tiles, const SpanDesc& sd, uint32_t t, const TileConv& cv,
+                                  uint32_t e, uint32_t* exit_rel, uint32_t* cnt, uint32_t* wcnt, int64_t* err_off,
+                                  int* err_tag, uint32_t* limit) {
+  const TileDesc td = tiles[t];
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  const uint32_t lo = td.delta, hi = td.delta + td.len;
+  uint32_t a = lo + e;
+  uint32_t c = 0, w = 0;
+  int region = -1;
+  while (a < hi) {
+    const int l = (int)(a >> 8);
+    if (l != region) {
+      region = l;
+      const uint32_t rsl = (uint32_t)l * kRegion < lo ? lo : (uint32_t)l * kRegion;
+      const uint16_t ce = cv.entry[l];
+      if (ce != 0xFFFF && rsl + ce == a && cv.exit != kExitErr) {
+        // Joined the shared path: the rest of the tile is known.
+        *exit_rel = cv.exit;
+        *cnt = c + (cv.suffix[l] & 0xFFFF);
+        *wcnt = w + (cv.suffix[l] >> 16);
+        *limit = 0xFFFFFFFFu;
+        return CLG_OK;
+      }
+    }
+    const uint64_t so = td.span_off + (a - lo);
+    AtSpan b{&sr, so};
+    const int64_t L = rec_len_slow(b, sd.len - so);
+    if (L < 0) {
+      *err_off = (int64_t)so;
+      *err_tag = (int8_t)sr.at(so);
+      *cnt = c;
+      *wcnt = w;
+      *limit = a;
+      return (int)L;
+    }
+    w += is_wide(sr.at(so));
+    ++c;
+    a += (uint32_t)L;
+  }
+  *exit_rel = a - hi;
+  *cnt = c;
+  *wcnt = w;
+  *limit = 0xFFFFFFFFu;
+  return CLG_OK;
+}
+
+__global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                     const uint64_t* __restrict__ agg, const TileConv* __restrict__ conv,
+                                                     TileRes* __restrict__ tres, SpanRes* __restrict__ sres) {
+  __shared__ uint64_t s_agg[kResolveChunk * kEntries];
+  __shared__ uint32_t s_len[kResolveChunk];
+  __shared__ uint64_t s_state[4];  // entry, rec, wide, done
+  const uint32_t s = blockIdx.x;
+  const SpanDesc sd = spans[s];
+  if (threadIdx.x == 0) {
+    s_state[0] = 0;
+    s_state[1] = 0;
+    s_state[2] = 0;
+    s_state[3] = 0;
+  }
+  int status = CLG_OK;
+  int64_t err_off = -1;
+  int err_tag = 0;
+  for (uint32_t base = 0; base < sd.n_tiles; base += kResolveChunk) {
+    const uint32_t nt = min((uint32_t)kResolveChunk, sd.n_tiles - base);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
+      s_agg[i] = agg[(uint64_t)(sd.first_tile + base) * kEntries + i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) s_len[i] = tiles[sd.first_tile + base + i].len;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t e = s_state[0], rec = s_state[1], wide = s_state[2];
+      bool done = s_state[3] != 0;
+      for (uint32_t i = 0; i < nt; ++i) {
+        const uint32_t t = sd.first_tile + base + i;
+        TileRes r;
+        r.rec_base = rec;
+        r.wide_base = wide;
+        r.limit = 0xFFFFFFFFu;
+        r.flags = 0;
+        r.pad = 0;
+        const uint32_t len = s_len[i];
+        if (done) {
+          r.entry = 0xFFFFFFFFu;
+          tres[t] = r;
+          continue;
+        }
+        r.entry = (uint32_t)min(e, (uint64_t)0xFFFFFFFFu);
+        if (e >= len) {  // a record started earlier covers the whole tile
+          e -= len;
+          tres[t] = r;
+          continue;
+        }
+        uint64_t x = (e < (uint64_t)kEntries) ? s_agg[i * kEntries + e] : (uint64_t)kExitFar;
+        uint32_t xr = (uint32_t)x;
+        uint32_t c, w;
+        if (xr == kExitErr || xr == kExitFar) {
+          uint32_t lim;
+          const int st = tile_eval_concrete(tiles, sd, t, conv[t], (uint32_t)e, &xr, &c, &w, &err_off, &err_tag, &lim);
+          r.limit = lim;
+          if (st != CLG_OK) {
+            status = st;
+            done = true;
+            rec += c;
+            wide += w;
+            tres[t] = r;
+            continue;
+          }
+        } else {
+          c = (uint32_t)(x >> 32) & 0xFFFF;
+          w = (uint32_t)(x >> 48);
+          r.flags = kResTableLive;
+        }
+        rec += c;
+        wide += w;
+        e = xr;
+        tres[t] = r;
+      }
+      s_state[0] = e;
+      s_state[1] = rec;
+      s_state[2] = wide;
+      s_state[3] = done ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    SpanRes sr_;
+    sr_.n_rec = s_state[1];
+    sr_.n_wide = s_state[2];
+    sr_.status = status;
+    sr_.err_tag = err_tag;
+    sr_.err_off = err_off;
+    if (status == CLG_OK && s_state[0] != 0) {
+      // The last record runs past the span end (cannot happen when tables flag
+      // truncation, kept as a guard).
+      sr_.status = CLG_E_TRUNCATED;
+    }
+    sr_.rec_base = 0;
+    sr_.wide_base = 0;
+    sres[s] = sr_;
+  }
+}
+
+// ==================================================================================
+// Pass 3: exclusive scan of span totals (single block).
+// ==================================================================================
+__global__ __launch_bounds__(1024) void k_dec_spanscan(SpanRes* __restrict__ sres, uint32_t n, uint64_t* __restrict__ totals) {
+  __shared__ uint64_t s_r[1024], s_w[1024];
+  __shared__ uint64_t carry_r, carry_w;
+  if (threadIdx.x == 0) {
+    carry_r = 0;
+    carry_w = 0;
+  }
+  __syncthreads();
+  for (uint32_t base = 0; base < n; base += 1024) {
+    const uint32_t i = base + threadIdx.x;
+    const uint64_t r = i < n ? sres[i].n_rec : 0, w = i < n ? sres[i].n_wide : 0;
+    s_r[threadIdx.x] = r;
+    s_w[threadIdx.x] = w;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+      const uint64_t ar = threadIdx.x >= off ? s_r[threadIdx.x - off] : 0;
+      const uint64_t aw = threadIdx.x >= off ? s_w[threadIdx.x - off] : 0;
+      __syncthreads();
+      s_r[threadIdx.x] += ar;
+      s_w[threadIdx.x] += aw;
+      __syncthreads();
+    }
+    if (i < n) {
+      sres[i].rec_base = carry_r + s_r[threadIdx.x] - r;
+      sres[i].wide_base = carry_w + s_w[threadIdx.x] - w;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      carry_r += s_r[1023];
+      carry_w += s_w[1023];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    totals[0] = carry_r;
+    totals[1] = carry_w;
+  }
+}
+
+// ==================================================================================
+// Pass 4: emit.  One wave per tile; region entries from the convergence info (or a
+// serial chain), then every lane parses its region forward twice (count, emit).
+// ==================================================================================
+__global__ __launch_bounds__(64) void k_dec_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                 const TileConv* __restrict__ conv, const TileRes* __restrict__ tres,
+                                                 const SpanRes* __restrict__ sres, DecodeOut out) {
+  __shared__ uint32_t s_tile[kRegions * kPitch];
+  __shared__ uint32_t s_entry[kRegions];
+  const uint32_t t = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const TileRes tr = tres[t];
+  const TileDesc td = tiles[t];
+  if (tr.entry >= td.len) return;  // no record starts in this tile (uniform)
+  const SpanDesc sd = spans[td.span];
+  const SpanRes sp = sres[td.span];
+  stage_tile(s_tile, td, lane);
+  __syncthreads();
+
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  TileReader rd{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
+  const TileGeom g{td.delta, td.delta + td.len};
+  const TileConv& cv = conv[t];
+  const uint32_t limit = tr.limit;  // emission stops at this aligned coordinate (error record)
+
+  // ---- region entries (lane 0, serial until the path joins the shared path) ----
+  // When the tile entry came from a live table path, that path is one of the candidates
+  // whose convergence k_dec_tables recorded, so it reaches the converged position of
+  // every later converged region: no serial parse is needed to get there.
+  if (lane == 0) {
+    const bool table_live = (tr.flags & kResTableLive) != 0;
+    uint32_t cur = td.delta + tr.entry;
+    bool joined = false;
+    for (int l = 0; l < kRegions; ++l) {
+      const uint32_t rsl = g.rs(l), rel_ = g.re(l);
+      const uint16_t ce = cv.entry[l];
+      if (!joined && ce != 0xFFFF && (table_live || rsl + ce == cur)) joined = true;
+      if (joined) {
+        const uint32_t p = (ce != 0xFFFF) ? rsl + ce : 0xFFFFFFFFu;
+        s_entry[l] = (rsl < rel_ && p < rel_ && p < limit) ? p : 0xFFFFFFFFu;
+        continue;
+      }
+      if (rsl >= rel_ || cur >= rel_ || cur >= limit) {
+        s_entry[l] = 0xFFFFFFFFu;
+        continue;
+      }
+      s_entry[l] = cur;
+      // Next region converged and our path is live: its entry is known, skip the parse.
+      if (table_live && l + 1 < kRegions && cv.entry[l + 1] != 0xFFFF) continue;
+      uint32_t ex, c, w;
+      const uint32_t stop = rel_ < limit ? rel_ : limit;
+      const int st = region_forward(rd, sd.len, cur, stop, &ex, &c, &w);
+      cur = (st == CLG_OK) ? ex : 0xFFFFFFFFu;
+    }
+  }
+  __syncthreads();
+
+  // ---- per-lane forward parse: count ----
+  const uint32_t my_entry = s_entry[lane];
+  const uint32_t my_re = g.re((int)lane);
+  const uint32_t stop = my_re < limit ? my_re : limit;
+  uint32_t c = 0, w = 0;
+  if (my_entry != 0xFFFFFFFFu) {
+    uint32_t a = my_entry;
+    while (a < stop) {
+      const uint64_t avail = sd.len - rd.span_off(a);
+      const int tag = rd.at(a);
+      int64_t L = fast_len(tag);
+      if (L <= 0) {
+        At<TileReader> b{&rd, a};
+        L = rec_len_slow(b, avail);
+      }
+      if (L <= 0) break;  // cannot happen before `limit` on a resolved path
+      ++c;
+      w += is_wide(tag);
+      a += (uint32_t)L;
+    }
+  }
+  // wave exclusive scan of (c, w)
+  uint32_t ic = c, iw = w;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t yc = __shfl_up(ic, off), yw = __shfl_up(iw, off);
+    if ((int)lane >= off) {
+      ic += yc;
+      iw += yw;
+    }
+  }
+  uint64_t rec = sp.rec_base + tr.rec_base + (ic - c);
+  uint64_t wide = sp.wide_base + tr.wide_base + (iw - w);
+
+  // ---- emit ----
+  if (my_entry != 0xFFFFFFFFu) {
+    uint32_t a = my_entry;
+    for (uint32_t k = 0; k < c; ++k) {
+      const uint64_t so = rd.span_off(a);
+      At<TileReader> b{&rd, a};
+      Rec r;
+      if (decode_rec(b, sd.len - so, r) != CLG_OK) break;
+      if (rec < out.cap) {
+        out.off[rec] = (uint32_t)so;
+        out.tag[rec] = r.tag;
+        out.v0[rec] = r.v0;
+      }
+      if (r.wide) {
+        if (wide < out.wcap) {
+          out.w_idx[wide] = (uint32_t)rec;
+          out.w_rc[wide] = r.rc;
+          out.w_v1[wide] = r.v1;
+          out.w_var_off[wide] = r.var_off ? (uint32_t)(so + r.var_off) : 0u;
+          out.w_var_len[wide] = r.var_len;
+          out.w_sub[wide] = r.sub;
+        }
+        ++wide;
+      }
+      ++rec;
+      a += r.L;
+    }
+  }
+}
+
+// ==================================================================================
+// Launchers.
+// ==================================================================================
+static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
+
+int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream) {
+  if (!n) return CLG_OK;
+  const uint32_t blocks = min((n + 3) / 4, 4096u);
+  hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_chunks, n, d_src);
+  return ok(hipGetLastError());
+}
+
+int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream) {
+  if (!n) return CLG_OK;
+  hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, (hipStream_t)stream, d_pieces, d_out);
+  return ok(hipGetLastError());
+}
+
+int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint64_t* d_agg,
+                         TileConv* d_conv, void* stream) {
+  if (!n_tiles) return CLG_OK;
+  hipLaunchKernelGGL(k_dec_tables, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_agg, d_conv);
+  return ok(hipGetLastError());
+}
+
+int launch_decode_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, const uint64_t* d_agg,
+                          const TileConv* d_conv, TileRes* d_tres, SpanRes* d_sres, void* stream) {
+  if (!n_spans) return CLG_OK;
+  hipLaunchKernelGGL(k_dec_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_agg, d_conv,
+                     d_tres, d_sres);
+  return ok(hipGetLastError());
+}
+
+int launch_decode_spanscan(SpanRes* d_sres, uint32_t n_spans, uint64_t* d_totals, void* stream) {
+  hipLaunchKernelGGL(k_dec_spanscan, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_sres, n_spans, d_totals);
+  return ok(hipGetLastError());
+}
+
+int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const TileConv* d_conv,
+                       const TileRes* d_tres, const SpanRes* d_sres, DecodeOut out, void* stream) {
+  if (!n_tiles) return CLG_OK;
+  hipLaunchKernelGGL(k_dec_emit, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_tres,
+                     d_sres, out);
+  return ok(hipGetLastError());
+}
+
+}  // namespace clg

@@ -1,0 +1,412 @@
+"""Host-side mirror of Clonos' ThreadCausalLog / DeterminantEncoder (decode) on top of the
+C-ABI of libclonos_engine.so.
+
+Method names follow the reference Java interfaces so parity tests read like the
+reference's own code:
+  ThreadCausalLog  reference flink-runtime/.../causal/log/thread/ThreadCausalLog.java:33-96
+  JobCausalLog     reference flink-runtime/.../causal/log/job/JobCausalLog.java:50-78 (see job.py)
+Errors surface as ClonosError carrying the C status (the Java side throws the matching
+exception: CorruptDeterminantArrayException, RuntimeException("Consumer went backwards"), ...).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from . import determinants as D
+
+ChannelLike = Union[Tuple[int, int], int]
+
+
+def _ch(c: ChannelLike) -> _lib.ChannelId:
+    if isinstance(c, tuple):
+        return _lib.ChannelId(c[0] & 0xFFFFFFFFFFFFFFFF, c[1] & 0xFFFFFFFFFFFFFFFF)
+    return _lib.ChannelId(int(c) & 0xFFFFFFFFFFFFFFFF, 0)
+
+
+@dataclass(frozen=True)
+class CausalLogID:
+    """CausalLogID.java:38-198: main-thread log or (partition, subpartition) log of a vertex."""
+    vertex_id: int
+    is_main: bool = True
+    irp_lower: int = 0
+    irp_upper: int = 0
+    subpartition: int = 0
+
+    @staticmethod
+    def main(vertex_id: int) -> "CausalLogID":
+        return CausalLogID(vertex_id, True)
+
+    @staticmethod
+    def sub(vertex_id: int, lower: int, upper: int, index: int) -> "CausalLogID":
+        return CausalLogID(vertex_id, False, lower, upper, index)
+
+    def key(self):
+        """equals/hashCode semantics (:128-163): main logs compare by vertex only."""
+        return (self.vertex_id, True) if self.is_main else (self.vertex_id, False, self.irp_lower, self.irp_upper,
+                                                            self.subpartition)
+
+    def to_c(self) -> _lib.CausalLogIdC:
+        return _lib.CausalLogIdC(self.vertex_id, 1 if self.is_main else 0, 0 if self.is_main else self.subpartition, 0,
+                                 0 if self.is_main else self.irp_lower, 0 if self.is_main else self.irp_upper)
+
+    def is_for_vertex(self, v: int) -> bool:
+        return self.vertex_id == v
+
+
+class DecodedBatch:
+    """Dense SoA produced by the GPU decode (layout: include/clonos_engine.h clg_decoded)."""
+
+    def __init__(self, off, tag, v0, w_idx, w_rc, w_v1, w_var_off, w_var_len, w_sub, span_rec_base, spans_bytes=None):
+        self.off, self.tag, self.v0 = off, tag, v0
+        self.w_idx, self.w_rc, self.w_v1 = w_idx, w_rc, w_v1
+        self.w_var_off, self.w_var_len, self.w_sub = w_var_off, w_var_len, w_sub
+        self.span_rec_base = span_rec_base
+        self.spans_bytes = spans_bytes  # optional: the raw span bytes, to materialise var fields
+
+    @property
+    def n_rec(self) -> int:
+        return int(self.tag.shape[0])
+
+    def span_slice(self, s: int) -> slice:
+        return slice(int(self.span_rec_base[s]), int(self.span_rec_base[s + 1]))
+
+    def determinants(self, s: int) -> List[D.Determinant]:
+        """Rebuild Determinant objects for span s (LogReplayer consumption order)."""
+        raw = self.spans_bytes[s] if self.spans_bytes is not None else None
+        sl = self.span_slice(s)
+        widx = {int(i): k for k, i in enumerate(self.w_idx)}
+        out: List[D.Determinant] = []
+        for i in range(sl.start, sl.stop):
+            t = int(self.tag[i])
+            v0 = int(self.v0[i])
+            if t == D.ORDER:
+                out.append(D.OrderDeterminant(v0))
+            elif t == D.TIMESTAMP:
+                out.append(D.TimestampDeterminant(v0))
+            elif t == D.RNG:
+                out.append(D.RNGDeterminant(v0))
+            elif t == D.BUFFER_BUILT:
+                out.append(D.BufferBuiltDeterminant(v0))
+            else:
+                k = widx[i]
+                rc, v1, vo, vl, sub = (int(self.w_rc[k]), int(self.w_v1[k]), int(self.w_var_off[k]),
+                                       int(self.w_var_len[k]), int(self.w_sub[k]))
+                var = bytes(raw[vo:vo + vl]) if raw is not None and vo else None
+                if t == D.IGNORE_CHECKPOINT:
+                    out.append(D.IgnoreCheckpointDeterminant(rc, v0))
+                elif t == D.TIMER_TRIGGER:
+                    out.append(D.TimerTriggerDeterminant(rc, v0, sub, var if sub == D.INTERNAL else None))
+                elif t == D.SOURCE_CHECKPOINT:
+                    out.append(D.SourceCheckpointDeterminant(rc, v0, v1, sub & 0x7F, var if sub & 0x80 else None))
+                elif t == D.SERIALIZABLE:
+                    out.append(D.SerializableDeterminant(var if var is not None else b""))
+        return out
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+class Engine:
+    """One engine per GPU (one process per GPU).  Owns the HBM segment pool."""
+
+    def __init__(self, segment_bytes: int = 16384, pool_segments: int = 16384, device: int = 0,
+                 sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False):
+        cfg = _lib.Config()
+        lib.clg_config_default(C.byref(cfg))
+        cfg.segment_bytes = segment_bytes
+        cfg.pool_segments = pool_segments
+        cfg.device = device
+        cfg.sharing_depth = sharing_depth
+        cfg.flags = _lib.CLG_F_TIMING if timing else 0
+        h = C.c_void_p()
+        check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.segment_bytes = segment_bytes
+        self.sharing_depth = sharing_depth
+        self.device = device
+        self._logs = {}
+
+    # ---- lifecycle ----------------------------------------------------------------
+    def close(self):
+        if self._h:
+            lib.clg_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return lib.clg_engine_stream(self._h) or 0
+
+    def sync(self):
+        check(lib.clg_sync(self._h))
+
+    def pool_stats(self) -> Tuple[int, int]:
+        u, f = C.c_uint32(), C.c_uint32()
+        check(lib.clg_pool_stats(self._h, C.byref(u), C.byref(f)))
+        return u.value, f.value
+
+    # ---- logs -----------------------------------------------------------------------
+    def open_log(self, cid: CausalLogID) -> "ThreadCausalLog":
+        h = C.c_uint32()
+        check(lib.clg_log_open(self._h, C.byref(cid.to_c()), C.byref(h)))
+        log = ThreadCausalLog(self, h.value, cid)
+        self._logs[cid.key()] = log
+        return log
+
+    def get_log(self, cid: CausalLogID) -> Optional["ThreadCausalLog"]:
+        return self._logs.get(cid.key())
+
+    def append_batch(self, logs: np.ndarray, epochs: np.ndarray, offs: np.ndarray, lens: np.ndarray,
+                     data: np.ndarray):
+        logs = np.ascontiguousarray(logs, np.uint32)
+        epochs = np.ascontiguousarray(epochs, np.int64)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        data = np.ascontiguousarray(data, np.uint8)
+        check(lib.clg_append_batch(self._h, _np_ptr(logs), _np_ptr(epochs), _np_ptr(offs), _np_ptr(lens),
+                                   len(logs), _np_ptr(data)))
+
+    # ---- batched slicing ----------------------------------------------------------------
+    def slice_batch(self, reqs: Sequence[Tuple["ThreadCausalLog", ChannelLike, int]], out=None,
+                    cap: Optional[int] = None):
+        """Batched hasDelta/getOffset/getDelta.  `out`: None (host bytes returned), a numpy
+        uint8 array, or a device pointer (int, CLG_MEM_DEVICE) with `cap`."""
+        n = len(reqs)
+        creq = (_lib.SliceReq * max(n, 1))()
+        for i, (log, ch, ep) in enumerate(reqs):
+            creq[i].log = log.handle
+            creq[i].consumer = _ch(ch)
+            creq[i].epoch = ep
+        cres = (_lib.SliceRes * max(n, 1))()
+        total = C.c_uint64()
+        if out is None or isinstance(out, np.ndarray):
+            if out is None:
+                out = np.empty(cap if cap is not None else self._slice_bound(reqs), np.uint8)
+            st = lib.clg_slice_batch(self._h, C.cast(creq, C.c_void_p), n, C.cast(cres, C.c_void_p), _np_ptr(out),
+                                     out.size, _lib.CLG_MEM_HOST, C.byref(total))
+        else:
+            st = lib.clg_slice_batch(self._h, C.cast(creq, C.c_void_p), n, C.cast(cres, C.c_void_p), int(out),
+                                     int(cap), _lib.CLG_MEM_DEVICE, C.byref(total))
+        check(st)
+        res = [(cres[i].status, bool(cres[i].has_delta), cres[i].offset_from_epoch, cres[i].len, cres[i].out_off)
+               for i in range(n)]
+        return res, out, total.value
+
+    def _slice_bound(self, reqs) -> int:
+        b = 0
+        for log in {id(r[0]): r[0] for r in reqs}.values():
+            b += log.state()["writer"] * sum(1 for r in reqs if r[0] is log)
+        return max(b, 1)
+
+    def slice_batch_raw(self, creq, cres, n: int, out_ptr: int, cap: int, device: bool = True) -> int:
+        """Zero-overhead variant for benchmarks: prebuilt ctypes request/result arrays."""
+        total = C.c_uint64()
+        check(lib.clg_slice_batch(self._h, C.cast(creq, C.c_void_p), n, C.cast(cres, C.c_void_p), out_ptr, cap,
+                                  _lib.CLG_MEM_DEVICE if device else _lib.CLG_MEM_HOST, C.byref(total)))
+        return total.value
+
+    # ---- checkpoint completion ---------------------------------------------------------
+    def truncate_all(self, checkpoint_id: int) -> bool:
+        applied = C.c_int32()
+        check(lib.clg_truncate_all(self._h, checkpoint_id, C.byref(applied)))
+        return bool(applied.value)
+
+    # ---- decode -------------------------------------------------------------------------
+    @staticmethod
+    def _host_outputs(cap: int, wcap: int):
+        arrs = dict(off=np.empty(cap, np.uint32), tag=np.empty(cap, np.uint8), v0=np.empty(cap, np.int64),
+                    w_idx=np.empty(wcap, np.uint32), w_rc=np.empty(wcap, np.int32), w_v1=np.empty(wcap, np.int64),
+                    w_var_off=np.empty(wcap, np.uint32), w_var_len=np.empty(wcap, np.uint32),
+                    w_sub=np.empty(wcap, np.uint8))
+        d = _lib.Decoded()
+        for k, a in arrs.items():
+            setattr(d, k, _np_ptr(a))
+        d.cap, d.wcap, d.out_kind = cap, wcap, _lib.CLG_MEM_HOST
+        return d, arrs
+
+    def _finish(self, st, d, arrs, base, n_spans, spans_bytes):
+        if st != _lib.CLG_OK:
+            err = _lib.ClonosError(st, lib.clg_last_error().decode(errors="replace"))
+            err.err_span, err.err_off, err.err_tag = d.err_span, d.err_off, d.err_tag
+            err.n_rec = d.n_rec
+            raise err
+        nr, nw = d.n_rec, d.n_wide
+        return DecodedBatch(arrs["off"][:nr], arrs["tag"][:nr], arrs["v0"][:nr], arrs["w_idx"][:nw],
+                            arrs["w_rc"][:nw], arrs["w_v1"][:nw], arrs["w_var_off"][:nw], arrs["w_var_len"][:nw],
+                            arrs["w_sub"][:nw], base[:n_spans + 1], spans_bytes)
+
+    def decode_host(self, data: Union[bytes, np.ndarray], spans: Optional[Sequence[Tuple[int, int]]] = None
+                    ) -> DecodedBatch:
+        """DeterminantEncoder.decodeNext over whole spans of host bytes, on the GPU."""
+        buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else np.ascontiguousarray(
+            data, np.uint8)
+        if spans is None:
+            spans = [(0, buf.size)]
+        so = np.array([s[0] for s in spans], np.uint64)
+        sl = np.array([s[1] for s in spans], np.uint64)
+        cap = int(sl.sum()) // 2 + len(spans) + 1
+        wcap = int(sl.sum()) // 6 + len(spans) + 1
+        d, arrs = self._host_outputs(cap, wcap)
+        base = np.zeros(len(spans) + 1, np.uint64)
+        st = lib.clg_decode_host(self._h, _np_ptr(buf), _np_ptr(so), _np_ptr(sl), len(spans), C.byref(d),
+                                 _np_ptr(base))
+        return self._finish(st, d, arrs, base, len(spans),
+                            [buf[int(o):int(o) + int(n)] for o, n in zip(so, sl)])
+
+    def decode_logs(self, logs: Sequence["ThreadCausalLog"], start_epochs: Sequence[int],
+                    keep_bytes: bool = False) -> DecodedBatch:
+        h = np.array([l.handle for l in logs], np.uint32)
+        ep = np.array(start_epochs, np.int64)
+        total = sum(l.state()["writer"] for l in logs)
+        cap = total // 2 + len(logs) + 1
+        wcap = total // 6 + len(logs) + 1
+        d, arrs = self._host_outputs(cap, wcap)
+        base = np.zeros(len(logs) + 1, np.uint64)
+        st = lib.clg_decode_logs(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base))
+        sb = [np.frombuffer(l.getDeterminants(e), np.uint8) for l, e in zip(logs, start_epochs)] if keep_bytes else None
+        return self._finish(st, d, arrs, base, len(logs), sb)
+
+    def decode_logs_device(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
+                           base: np.ndarray) -> None:
+        """Benchmark variant: outputs are caller-owned device arrays described by `dec`."""
+        check(lib.clg_decode_logs(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles), C.byref(dec),
+                                  _np_ptr(base)))
+
+    # ---- replay-prep ----------------------------------------------------------------------
+    def replay_prep(self, copies: Sequence[Tuple[int, bytes]]):
+        """DeterminantResponseEvent.merge (longest wins, ties -> later) + batched decode of
+        the winners.  Returns (winner indices, DecodedBatch over the winners)."""
+        keys = np.array([c[0] for c in copies], np.uint64)
+        blobs = [bytes(c[1]) for c in copies]
+        offs = np.zeros(len(blobs), np.uint64)
+        lens = np.array([len(b) for b in blobs], np.uint64)
+        if len(blobs):
+            offs[1:] = np.cumsum(lens)[:-1]
+        data = np.frombuffer(b"".join(blobs) or b"\0", np.uint8)
+        winner = np.zeros(max(len(blobs), 1), np.uint32)
+        nk = C.c_uint32()
+        total = int(lens.sum())
+        d, arrs = self._host_outputs(total // 2 + len(blobs) + 1, total // 6 + len(blobs) + 1)
+        base = np.zeros(len(blobs) + 1, np.uint64)
+        st = lib.clg_replay_prep(self._h, _np_ptr(keys), _np_ptr(data), _np_ptr(offs), _np_ptr(lens), len(blobs),
+                                 _np_ptr(winner), C.byref(nk), C.byref(d), _np_ptr(base))
+        k = nk.value
+        win = winner[:k].copy()
+        return win, self._finish(st, d, arrs, base, k, [np.frombuffer(blobs[i], np.uint8) for i in win])
+
+    # ---- instrumentation ---------------------------------------------------------------------
+    def kernel_stats(self):
+        arr = (_lib.KernelStat * 64)()
+        n = C.c_uint32()
+        check(lib.clg_kernel_stats(self._h, arr, 64, C.byref(n)))
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, ms=arr[i].total_ms, bytes=arr[i].bytes)
+                for i in range(min(n.value, 64))}
+
+    def kernel_stats_reset(self):
+        check(lib.clg_kernel_stats_reset(self._h))
+
+
+class ThreadCausalLog:
+    """Mirror of ThreadCausalLog (ThreadCausalLog.java:33-96) backed by the engine."""
+
+    def __init__(self, engine: Engine, handle: int, cid: CausalLogID):
+        self.engine = engine
+        self.handle = handle
+        self.cid = cid
+
+    def getCausalLogID(self) -> CausalLogID:
+        return self.cid
+
+    def appendDeterminant(self, det: Union[D.Determinant, bytes], epochID: int) -> None:
+        b = det if isinstance(det, (bytes, bytearray)) else D.encode(det)
+        check(lib.clg_append(self.engine.handle, self.handle, epochID, bytes(b), len(b)))
+
+    def processUpstreamDelta(self, delta: bytes, offsetFromEpoch: int, epochID: int) -> None:
+        check(lib.clg_upstream_delta(self.engine.handle, self.handle, epochID, offsetFromEpoch, bytes(delta),
+                                     len(delta)))
+
+    def logLength(self) -> int:
+        v = C.c_int32()
+        check(lib.clg_log_length(self.engine.handle, self.handle, C.byref(v)))
+        return v.value
+
+    def hasDeltaForConsumer(self, outputChannelID: ChannelLike, epochID: int) -> bool:
+        v = C.c_int32()
+        check(lib.clg_has_delta(self.engine.handle, self.handle, _ch(outputChannelID), epochID, C.byref(v)))
+        return bool(v.value)
+
+    def getOffsetFromEpochForConsumer(self, outputChannelID: ChannelLike, epochID: int) -> int:
+        v = C.c_int32()
+        check(lib.clg_offset_from_epoch(self.engine.handle, self.handle, _ch(outputChannelID), C.byref(v)))
+        return v.value
+
+    def getDeltaForConsumer(self, outputChannelID: ChannelLike, epochID: int) -> bytes:
+        cap = max(self.state()["capacity"], 1)
+        buf = np.empty(cap, np.uint8)
+        n = C.c_uint32()
+        check(lib.clg_get_delta(self.engine.handle, self.handle, _ch(outputChannelID), epochID, _np_ptr(buf), cap,
+                                _lib.CLG_MEM_HOST, C.byref(n)))
+        return buf[:n.value].tobytes()
+
+    def getDeterminants(self, startEpochID: int) -> bytes:
+        cap = max(self.state()["capacity"], 1)
+        buf = np.empty(cap, np.uint8)
+        n = C.c_uint32()
+        check(lib.clg_get_determinants(self.engine.handle, self.handle, startEpochID, _np_ptr(buf), cap,
+                                       _lib.CLG_MEM_HOST, C.byref(n)))
+        return buf[:n.value].tobytes()
+
+    def notifyCheckpointComplete(self, checkpointID: int) -> None:
+        check(lib.clg_notify_checkpoint_complete(self.engine.handle, self.handle, checkpointID))
+
+    def unregisterConsumer(self, toCancel: ChannelLike) -> None:
+        check(lib.clg_unregister_consumer(self.engine.handle, self.handle, _ch(toCancel)))
+
+    def close(self) -> None:
+        check(lib.clg_log_close(self.engine.handle, self.handle))
+        self.engine._logs.pop(self.cid.key(), None)
+
+    # ---- introspection (tests / safety assertions) ----
+    def state(self) -> dict:
+        st = _lib.LogState()
+        ids = np.zeros(4096, np.int64)
+        offs = np.zeros(4096, np.int32)
+        check(lib.clg_log_get_state(self.engine.handle, self.handle, C.byref(st), _np_ptr(ids), _np_ptr(offs), 4096))
+        n = st.n_epochs
+        return dict(writer=st.writer, capacity=st.capacity, n_components=st.n_components,
+                    epochs=list(zip(ids[:n].tolist(), offs[:n].tolist())))
+
+    def consumer_state(self, ch: ChannelLike):
+        ex, ep, off = C.c_int32(), C.c_int64(), C.c_int32()
+        check(lib.clg_consumer_state(self.engine.handle, self.handle, _ch(ch), C.byref(ex), C.byref(ep), C.byref(off)))
+        return (ep.value, off.value) if ex.value else None
+
+    def seek_consumer(self, ch: ChannelLike, epoch: int, offset: int) -> None:
+        check(lib.clg_consumer_seek(self.engine.handle, self.handle, _ch(ch), epoch, offset))
+
+    def read_phys(self, phys: int, n: int) -> bytes:
+        buf = np.empty(max(n, 1), np.uint8)
+        check(lib.clg_log_read_phys(self.engine.handle, self.handle, phys, n, _np_ptr(buf)))
+        return buf[:n].tobytes()

@@ -1,0 +1,241 @@
+/*
+ * clonos_engine.h -- C-ABI of the MI355X causal-log engine (libclonos_engine.so).
+ *
+ * This is the drop-in boundary a JNI layer binds.  Plain
+ * pointers and sizes only; no exceptions cross it; every entry point returns an
+ * int status (CLG_OK == 0).  clg_last_error() gives a thread-local message.
+ *
+ * Reference interfaces replaced (R/ = /root/reference/flink-runtime/src/main/java/
+ * org/apache/flink/runtime/causal/):
+ *   ThreadCausalLog      R/log/thread/ThreadCausalLog.java:33-96  (impl :51-527)
+ *   JobCausalLog         R/log/job/JobCausalLog.java:50-78        (impl JobCausalLogImpl.java:71-300)
+ *   DeterminantEncoder   R/determinant/DeterminantEncoder.java:28-65 (decode side; impl
+ *                        SimpleDeterminantEncoder.java:78-342)
+ *   DeterminantResponseEvent.merge  R/DeterminantResponseEvent.java:128-148
+ *
+ * Memory model: log bytes live in HBM in fixed-size segments (= Netty components of
+ * determinantBufferSize bytes, NettyConfig.java:86-89); log metadata (epoch start
+ * offsets, consumer offsets, visible writer index) lives in the host engine and is
+ * updated with exactly the reference's semantics.  Outputs go to caller-allocated
+ * buffers, either host (CLG_MEM_HOST) or device (CLG_MEM_DEVICE, a hipMalloc'd pointer
+ * on the engine's device).  Entry points are safe to call from any thread: the engine
+ * serialises on one mutex and issues all GPU work on one HIP stream.
+ */
+#ifndef CLONOS_ENGINE_H
+#define CLONOS_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLG_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------- */
+enum {
+  CLG_OK = 0,
+  CLG_E_INVALID_ARG = -1,
+  CLG_E_CORRUPT_TAG = -2,        /* CorruptDeterminantArrayException(tag)  SimpleDeterminantEncoder.java:92 */
+  CLG_E_TRUNCATED = -3,          /* record runs past the span (ByteBuf IndexOutOfBounds) */
+  CLG_E_BAD_ENUM = -4,           /* Type.values()[ord] / CheckpointType.values()[ord] out of range (:231, :285) */
+  CLG_E_NEG_LEN = -5,            /* negative name / reference length (NegativeArraySizeException, :235, :282) */
+  CLG_E_BAD_SERIAL = -6,         /* malformed Java serialization stream (type 3, :333-341) */
+  CLG_E_CONSUMER_BACKWARDS = -7, /* "Consumer went backwards"  ThreadCausalLogImpl.java:215-218 */
+  CLG_E_NO_CONSUMER = -8,        /* getOffset/getDelta before hasDelta (NPE at :245 / :256) */
+  CLG_E_GAP = -9,                /* upstream delta leaves a gap (delta.readerIndex(<0) at :143) */
+  CLG_E_NOSPACE = -10,           /* segment pool exhausted (Java side blocks: requestBufferBlocking :444) */
+  CLG_E_CAPACITY = -11,          /* caller output buffer too small; required size reported */
+  CLG_E_STATE = -12,             /* inconsistent log state (index out of bounds) */
+  CLG_E_DEVICE = -13,            /* HIP runtime error */
+  CLG_E_NO_LOG = -14             /* unknown / closed log handle */
+};
+
+enum { CLG_MEM_HOST = 0, CLG_MEM_DEVICE = 1 };
+
+/* Determinant tags (Determinant.java:23-34). */
+enum {
+  CLG_TAG_ORDER = 0, CLG_TAG_TIMESTAMP = 1, CLG_TAG_RNG = 2, CLG_TAG_SERIALIZABLE = 3,
+  CLG_TAG_TIMER_TRIGGER = 4, CLG_TAG_SOURCE_CHECKPOINT = 5, CLG_TAG_IGNORE_CHECKPOINT = 6,
+  CLG_TAG_BUFFER_BUILT = 7
+};
+
+#define CLG_FULL_SHARING (-1) /* ExecutionConfig.determinantSharingDepth default */
+
+/* ---- identities ---------------------------------------------------------------- */
+/* InputChannelID (an AbstractID: lower/upper longs). */
+typedef struct clg_channel_id { uint64_t lo, hi; } clg_channel_id;
+
+/* CausalLogID (CausalLogID.java:38-198): main-thread log of a vertex, or a
+ * subpartition log {vertex, intermediate result partition (lower, upper), index}. */
+typedef struct clg_causal_log_id {
+  int16_t vertex_id;
+  uint8_t is_main;
+  int8_t subpartition;
+  uint32_t reserved;
+  int64_t irp_lower;
+  int64_t irp_upper;
+} clg_causal_log_id;
+
+typedef struct clg_config {
+  uint32_t segment_bytes;  /* determinantBufferSize (NettyConfig.java:86-89); 16384 by default */
+  uint32_t pool_segments;  /* segments preallocated in HBM (pool = segment_bytes * pool_segments) */
+  int32_t device;          /* HIP device ordinal */
+  int32_t sharing_depth;   /* determinantSharingDepth (-1 = full sharing, 0 = logging off) */
+  uint32_t flags;          /* CLG_F_* */
+  uint32_t reserved;
+} clg_config;
+
+#define CLG_F_TIMING 1u /* record per-kernel HIP event timings (clg_kernel_stats) */
+
+typedef struct clg_engine clg_engine;
+
+/* ---- engine ---------------------------------------------------------------------- */
+void clg_config_default(clg_config* cfg);
+int clg_engine_create(const clg_config* cfg, clg_engine** out);
+void clg_engine_destroy(clg_engine* e);
+const char* clg_last_error(void);
+int clg_abi_version(void);
+/* The HIP stream (hipStream_t) all engine work is issued on. */
+void* clg_engine_stream(clg_engine* e);
+/* Flush staged appends to HBM and wait for all queued GPU work. */
+int clg_sync(clg_engine* e);
+/* Segments in use / free in the HBM pool. */
+int clg_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments);
+
+/* ---- ThreadCausalLog --------------------------------------------------------------- */
+/* Opens a log (ThreadCausalLogImpl ctor :94-112): one empty component is allocated. */
+int clg_log_open(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle);
+/* close() :317-328 (the engine does not wait for consumers; caller guarantees drain). */
+int clg_log_close(clg_engine* e, uint32_t log);
+int clg_log_find(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle);
+/* appendDeterminant :158-177.  `rec` holds ONE encoded determinant (encodeTo bytes;
+ * n == getEncodedSizeInBytes).  Staged on the host, flushed to HBM in batches. */
+int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n);
+/* Many appends at once: rec i = bytes[off[i], off[i]+len[i]) for log[i] in epoch[i]. */
+int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, const uint64_t* off,
+                     const uint32_t* len, uint32_t n, const uint8_t* bytes);
+/* processUpstreamDelta :117-154 (dedup by offsetFromEpoch, append the new suffix). */
+int clg_upstream_delta(clg_engine* e, uint32_t log, int64_t epoch, int32_t offset_from_epoch,
+                       const uint8_t* delta, uint32_t n);
+int clg_log_length(clg_engine* e, uint32_t log, int32_t* out);                                /* :180-192 */
+int clg_has_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t* out); /* :196-240 */
+int clg_offset_from_epoch(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* out);       /* :243-246 */
+/* getDeltaForConsumer :249-277: bytes copied into `out` (host or device). */
+int clg_get_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, void* out,
+                  uint32_t cap, uint32_t out_kind, uint32_t* n);
+/* getDeterminants(startEpoch) :285-313. */
+int clg_get_determinants(clg_engine* e, uint32_t log, int64_t start_epoch, void* out, uint32_t cap,
+                         uint32_t out_kind, uint32_t* n);
+int clg_notify_checkpoint_complete(clg_engine* e, uint32_t log, int64_t checkpoint_id); /* :398-435 */
+int clg_unregister_consumer(clg_engine* e, uint32_t log, clg_channel_id c);              /* :331-336 */
+
+/* State introspection (for parity tests and the JNI safety assertions). */
+typedef struct clg_log_state {
+  int32_t writer;        /* visibleWriterIndex */
+  int32_t capacity;      /* composite capacity = components * segment_bytes */
+  int32_t n_components;
+  int32_t n_epochs;
+} clg_log_state;
+int clg_log_get_state(clg_engine* e, uint32_t log, clg_log_state* st, int64_t* epoch_ids,
+                      int32_t* epoch_offsets, int32_t cap_epochs);
+int clg_consumer_state(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* exists,
+                       int64_t* epoch, int32_t* offset);
+/* Raw physical bytes of the log's composite (reads HBM). */
+int clg_log_read_phys(clg_engine* e, uint32_t log, int32_t phys, uint32_t n, uint8_t* host_out);
+
+/* ---- batched delta slicing (serializeThreadDelta loop, Flat/Grouping serde) ------------
+ * For each request, in order: hasDeltaForConsumer; if true, getOffsetFromEpochForConsumer
+ * then getDeltaForConsumer.  All deltas are gathered by ONE kernel into `out`
+ * (packed in request order).  res[i].status != 0 reports a per-request error
+ * (e.g. CLG_E_CONSUMER_BACKWARDS) without aborting the batch. */
+typedef struct clg_slice_req {
+  uint32_t log;
+  uint32_t reserved;
+  clg_channel_id consumer;
+  int64_t epoch;
+} clg_slice_req;
+typedef struct clg_slice_res {
+  int32_t status;
+  int32_t has_delta;
+  int32_t offset_from_epoch;
+  int32_t len;
+  uint64_t out_off;
+} clg_slice_res;
+int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res,
+                    void* out, uint64_t cap, uint32_t out_kind, uint64_t* total);
+/* Consumer offsets set directly (used to position consumers mid-epoch in benchmarks and
+ * when a standby takes over a channel); epoch must exist. */
+int clg_consumer_seek(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t offset);
+
+/* ---- checkpoint completion fan-out (JobCausalLogImpl.notifyCheckpointComplete :230-246) --
+ * CAS on the engine's latestCompletedCheckpoint; if newer, truncates every open log. */
+int clg_truncate_all(clg_engine* e, int64_t checkpoint_id, int32_t* applied);
+
+/* ---- batched decode (SimpleDeterminantEncoder.decodeNext over whole spans) -------------
+ * Output is a dense SoA over all spans (span order, record order):
+ *   off[i]  byte offset of record i inside its span;  tag[i];  v0[i] =
+ *   ORDER channel (sign-extended byte) | TIMESTAMP ts | RNG number | BUFFER_BUILT bytes |
+ *   TIMER_TRIGGER timestamp | SOURCE_CHECKPOINT checkpointID | IGNORE_CHECKPOINT
+ *   checkpointID | SERIALIZABLE java-stream length.
+ * Wide records (tags 3,4,5,6) also get a side-table row:
+ *   w_idx (global record index), w_rc (recordCount), w_v1 (SourceCheckpoint timestamp),
+ *   w_var_off/w_var_len (name, storage reference or java stream, span-relative),
+ *   w_sub (TimerTrigger type ordinal; SourceCheckpoint type | hasRef<<7). */
+typedef struct clg_decoded {
+  uint32_t* off;
+  uint8_t* tag;
+  int64_t* v0;
+  uint32_t* w_idx;
+  int32_t* w_rc;
+  int64_t* w_v1;
+  uint32_t* w_var_off;
+  uint32_t* w_var_len;
+  uint8_t* w_sub;
+  uint64_t cap;       /* capacity of the record arrays */
+  uint64_t wcap;      /* capacity of the side-table arrays */
+  uint32_t out_kind;  /* CLG_MEM_HOST / CLG_MEM_DEVICE */
+  uint32_t reserved;
+  /* results */
+  uint64_t n_rec;
+  uint64_t n_wide;
+  int32_t err_status; /* first decode error (lowest span), CLG_OK if none */
+  uint32_t err_span;
+  int64_t err_off;    /* span-relative offset of the failing record */
+  int32_t err_tag;
+  uint32_t reserved2;
+} clg_decoded;
+
+/* Decode spans of host memory: span i = bytes[span_off[i], span_off[i]+span_len[i]).
+ * span_rec_base (optional, n+1 entries) receives each span's first record index. */
+int clg_decode_host(clg_engine* e, const uint8_t* bytes, const uint64_t* span_off,
+                    const uint64_t* span_len, uint32_t n, clg_decoded* out, uint64_t* span_rec_base);
+/* Decode logs resident in HBM: span i = getDeterminants(start_epoch[i]) of log[i]
+ * (no copy: kernels read the segments in place). */
+int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
+                    clg_decoded* out, uint64_t* span_rec_base);
+
+/* ---- replay-prep (DeterminantResponseEvent.merge + LogReplayer decode) ----------------
+ * `n` candidate copies of logs (e.g. one per responding GPU / downstream):
+ * copy i is (key[i], bytes[off[i], off[i]+len[i])).  For every distinct key the LONGEST
+ * copy wins, ties going to the later copy (merge :137-146, v2 on ties).  winner[k] and
+ * the number of keys are returned; the winners are then decoded in one batch. */
+int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off,
+                    const uint64_t* len, uint32_t n, uint32_t* winner, uint32_t* n_keys,
+                    clg_decoded* out, uint64_t* span_rec_base);
+
+/* ---- instrumentation ---------------------------------------------------------------- */
+typedef struct clg_kernel_stat {
+  char name[32];
+  uint64_t launches;
+  double total_ms;
+  uint64_t bytes; /* algorithmic bytes attributed to the kernel */
+} clg_kernel_stat;
+int clg_kernel_stats(clg_engine* e, clg_kernel_stat* out, uint32_t cap, uint32_t* n);
+int clg_kernel_stats_reset(clg_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLONOS_ENGINE_H */
