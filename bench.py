@@ -1,0 +1,249 @@
+"""bench.py -- determinants/sec for decode + per-channel delta slice (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], SURVEY.md 8d "Config 2"), per GPU:
+  64 subtask logs x 1M Order+Timestamp determinants in one epoch (~352 MB resident in HBM
+  segments), 8 downstream consumers per log positioned at random record boundaries.
+One step = GPU decode of all 64 logs (getDeterminants spans, SoA output in HBM) +
+batched delta slice for all 512 (consumer, log) pairs (packed output in HBM).
+Multi-GPU: logs shard by vertex across ranks (weak scaling), no data-path collective.
+
+Prints ONE JSON line on rank 0 (contract in the task description), with a `roofline`
+object for the dominant kernel (HIP-event durations measured inside the engine on the
+stream the kernels run on) and a `cpu_baseline` object (the C++ oracle on host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_LOGS = 64
+N_REC = 1_000_000
+N_CONS = 8
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--logs", type=int, default=N_LOGS)
+    ap.add_argument("--records", type=int, default=N_REC)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from clonos_amd import CausalLogID, Engine, _lib, synth
+
+    # ---------------- synthetic shard (seeded per rank) ----------------
+    rng = np.random.default_rng(synth.SEED_CONFIG2 + rank)
+    bufs, offs = [], []
+    for _ in range(args.logs):
+        b, o = synth.config2_log(args.records, rng)
+        bufs.append(b)
+        offs.append(o)
+    log_bytes = [int(b.size) for b in bufs]
+    total_bytes = sum(log_bytes)
+    seg = 16384
+    pool = sum((n + seg - 1) // seg + 1 for n in log_bytes) + 64
+    eng = Engine(segment_bytes=seg, pool_segments=pool, device=local, timing=True)
+    logs = []
+    for v, b in enumerate(bufs):
+        vid = rank * args.logs + v  # VertexID sharding: this rank owns its vertices
+        log = eng.open_log(CausalLogID.main(vid))
+        log.processUpstreamDelta(b.tobytes(), 0, 1)  # one epoch, received whole
+        logs.append(log)
+    eng.sync()
+
+    # consumers at random record boundaries
+    cons = []  # (log index, channel, offset)
+    for i, o in enumerate(offs):
+        for c in range(N_CONS):
+            r = int(rng.integers(0, len(o)))
+            cons.append((i, (c + 1, rank * args.logs + i), int(o[r])))
+    slice_total = sum(log_bytes[i] - off for i, _, off in cons)
+    n_req = len(cons)
+    creq = (_lib.SliceReq * n_req)()
+    cres = (_lib.SliceRes * n_req)()
+    for k, (i, ch, _) in enumerate(cons):
+        creq[k].log = logs[i].handle
+        creq[k].consumer = _lib.ChannelId(ch[0], ch[1])
+        creq[k].epoch = 1
+
+    # ---------------- device outputs (HBM, caller-owned) ----------------
+    n_det = args.logs * args.records
+    dev = torch.device("cuda", local)
+    o_off = torch.empty(n_det, dtype=torch.int32, device=dev)
+    o_tag = torch.empty(n_det, dtype=torch.uint8, device=dev)
+    o_v0 = torch.empty(n_det, dtype=torch.int64, device=dev)
+    wcap = 1024
+    o_w = [torch.empty(wcap, dtype=t, device=dev) for t in
+           (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
+    o_slice = torch.empty(slice_total + 64, dtype=torch.uint8, device=dev)
+    dec = _lib.Decoded()
+    dec.off, dec.tag, dec.v0 = o_off.data_ptr(), o_tag.data_ptr(), o_v0.data_ptr()
+    dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len, dec.w_sub = [t.data_ptr() for t in o_w]
+    dec.cap, dec.wcap, dec.out_kind = n_det, wcap, _lib.CLG_MEM_DEVICE
+    handles = np.array([l.handle for l in logs], np.uint32)
+    starts = np.ones(len(logs), np.int64)
+    base = np.zeros(len(logs) + 1, np.uint64)
+
+    def step():
+        eng.decode_logs_device(handles, starts, dec, base)
+        for i, ch, off in cons:
+            logs[i].seek_consumer(ch, 1, off)
+        got = eng.slice_batch_raw(creq, cres, n_req, o_slice.data_ptr(), o_slice.numel(), device=True)
+        assert got == slice_total, (got, slice_total)
+
+    # correctness guard on the first step: record count and spot values
+    step()
+    assert dec.n_rec == n_det and dec.err_status == 0
+    torch.cuda.synchronize()
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    eng.kernel_stats_reset()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = eng.kernel_stats()
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = n_det * world / (elapsed / args.steps)
+
+    # ---------------- roofline of the dominant kernel ----------------
+    kern = {}
+    for name, s in stats.items():
+        if s["launches"]:
+            avg_ms = s["ms"] / s["launches"]
+            per_launch = s["bytes"] / s["launches"]
+            kern[name] = dict(launches=s["launches"], avg_ms=round(avg_ms, 5),
+                              algo_bytes_per_launch=int(per_launch),
+                              gbs=round(per_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None)
+    dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"]) if kern else None
+    roof = None
+    if dom:
+        ach = kern[dom]["gbs"]
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get(dom)
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic}
+    # decode pipeline as a whole (4 kernels) against its algorithmic bytes
+    dec_ms = sum(kern[k]["avg_ms"] for k in kern if k.startswith("decode_"))
+    dec_bytes = total_bytes + 13 * n_det
+    slice_bytes = 2 * slice_total + 16 * n_req
+
+    # ---------------- CPU baseline (rank 0, N=1 only) ----------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(bufs, log_bytes, cons, args)
+
+    if rank == 0:
+        line = {
+            "metric": "determinants/sec decode+delta-slice",
+            "value": round(value, 1),
+            "unit": "determinants/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded config-2 generator; SURVEY.md 8d)",
+            "config": {"workload": "config2: 64 subtasks x 1M Order+Timestamp determinants/epoch, decode + "
+                                   "per-channel delta slice (8 consumers/log)",
+                       "logs_per_gpu": args.logs, "records_per_log": args.records, "consumers_per_log": N_CONS,
+                       "log_bytes_per_gpu": total_bytes, "slice_bytes_per_gpu": slice_total,
+                       "segment_bytes": seg, "parallelism": f"shard-by-vertex x{world}"},
+            "log_gbs": round(total_bytes * world / (elapsed / args.steps) / 1e9, 2),
+            "decode_pipeline": {"avg_ms": round(dec_ms, 4), "algo_bytes": dec_bytes,
+                                "gbs": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1) if dec_ms else None},
+            "slice": {"algo_bytes": slice_bytes},
+            "kernels": kern,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(bufs, log_bytes, cons, args):
+    """The C++ oracle (sequential decodeNext loop + memcpy slicing) on host cores, same
+    workload as the GPU step.  Threads: one log per std::thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O  # the checker, timed here as the CPU baseline
+    host = np.concatenate(bufs)
+    starts = np.zeros(len(bufs), np.uint64)
+    starts[1:] = np.cumsum(np.array(log_bytes, np.uint64))[:-1]
+    lens = np.array(log_bytes, np.uint64)
+    src = np.array([int(starts[i]) + off for i, _, off in cons], np.uint64)
+    ln = np.array([log_bytes[i] - off for i, _, off in cons], np.uint64)
+    dst = np.zeros(len(cons), np.uint64)
+    dst[1:] = np.cumsum(ln)[:-1]
+    out = np.empty(int(ln.sum()), np.uint8)
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    nrec = O.lib.orc_bench_decode(O.ptr(host), O.ptr(starts), O.ptr(lens), len(bufs), threads)
+    t1 = time.perf_counter()
+    O.lib.orc_bench_slice(O.ptr(host), O.ptr(src), O.ptr(ln), O.ptr(dst), len(cons), O.ptr(out), threads)
+    t2 = time.perf_counter()
+    assert nrec == len(bufs) * args.records
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(nrec / (t2 - t0), 1), "unit": "determinants/s", "cores": threads, "kind": "port",
+            "sample": f"full config-2 step ({len(bufs)} logs x {args.records} records decode + {len(cons)} slices, "
+                      f"{int(ln.sum())} B) once; decode {t1 - t0:.3f}s slice {t2 - t1:.3f}s",
+            "cpu": cpu_model}
+
+
+if __name__ == "__main__":
+    main()

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -171,6 +172,7 @@ struct clg_engine {
   // staging / scratch
   PinBuf h_stage, h_desc;
   DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
 
   // timing
@@ -423,7 +425,9 @@ struct clg_engine {
     {
       const int32_t p = ci->second.es->offset + ci->second.offset;
       const int32_t nb = bytes_to_send(*l, epoch, p);
-      if (nb > 0 && uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
+      if (nb < 0 || p < 0 || int64_t(p) + nb > capacity(*l))
+        return fail(CLG_E_STATE, "delta [%d, %d) outside log of capacity %d", p, p + nb, capacity(*l));
+      if (uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
     }
     CHK(flush());
     int32_t phys, nb;
@@ -553,6 +557,11 @@ struct clg_engine {
     CHK(d_tres.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileRes)));
     CHK(d_sres.ensure(ns * sizeof(clg::SpanRes)));
     CHK(d_totals.ensure(2 * sizeof(uint64_t)));
+    CHK(d_fconv.ensure(std::max<size_t>(1, nt) * clg::kRegions * sizeof(uint32_t)));
+    CHK(d_lanes.ensure(std::max<size_t>(1, nt) * clg::kRegions * sizeof(clg::LaneSeg)));
+    CHK(d_sums.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileSum)));
+    CHK(d_fres.ensure(std::max<size_t>(1, nt) * sizeof(clg::FastRes)));
+    CHK(d_flags.ensure(ns * sizeof(uint32_t)));
     const size_t hb = nt * sizeof(clg::TileDesc) + ns * sizeof(clg::SpanDesc);
     CHK(h_desc.ensure(hb + ns * sizeof(clg::SpanRes) + 64));
     uint8_t* hd = h_desc.as<uint8_t>();
@@ -585,12 +594,29 @@ struct clg_engine {
     }
     auto* dt = d_tiles.as<clg::TileDesc>();
     auto* ds = d_spans.as<clg::SpanDesc>();
-    CHK(timed("decode_tables", log_bytes, [&] {
-      return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), stream);
+    auto* flags = d_flags.as<uint32_t>();
+    // fast path: convergence points -> segment counts -> per-span resolution
+    CHK(timed("decode_conv", log_bytes, [&] {
+      uint32_t* dbg = nullptr;
+      if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kRegions * 4) == CLG_OK)
+        dbg = d_dbg.as<uint32_t>();
+      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), dbg, stream);
     }));
-    CHK(timed("decode_resolve", uint64_t(nt) * clg::kEntries * 8, [&] {
+    CHK(timed("decode_count", log_bytes, [&] {
+      return clg::launch_fast_count(dt, nt, ds, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(),
+                                    d_sums.as<clg::TileSum>(), stream);
+    }));
+    CHK(timed("decode_resolve", uint64_t(nt) * 32, [&] {
+      return clg::launch_fast_resolve(dt, ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
+                                      d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags, stream);
+    }));
+    // robust DP pipeline for flagged spans only (early exit elsewhere)
+    CHK(timed("decode_dp_tables", 0, [&] {
+      return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), flags, stream);
+    }));
+    CHK(timed("decode_dp_resolve", 0, [&] {
       return clg::launch_decode_resolve(dt, ds, ns, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(),
-                                        d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), stream);
+                                        d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), flags, stream);
     }));
     CHK(timed("decode_spanscan", uint64_t(ns) * 48, [&] {
       return clg::launch_decode_spanscan(d_sres.as<clg::SpanRes>(), ns, d_totals.as<uint64_t>(), stream);
@@ -602,9 +628,33 @@ struct clg_engine {
       eb = get_event();
       hipEventRecord(ea, stream);
     }
-    CHK(clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
-                                d_sres.as<clg::SpanRes>(), o, stream));
+    CHK(clg::launch_fast_emit(dt, nt, ds, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(), d_fres.as<clg::FastRes>(),
+                              d_sres.as<clg::SpanRes>(), flags, o, stream));
     if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
+    CHK(timed("decode_dp_emit", 0, [&] {
+      return clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
+                                     d_sres.as<clg::SpanRes>(), flags, o, stream);
+    }));
+    if (const char* dump = getenv("CLONOS_DEBUG_DUMP")) {  // developer diagnostics only
+      std::vector<uint32_t> hc(size_t(nt) * clg::kRegions), hf(ns);
+      std::vector<clg::TileSum> hs(nt);
+      hipMemcpyAsync(hc.data(), d_fconv.p, hc.size() * 4, hipMemcpyDeviceToHost, stream);
+      hipMemcpyAsync(hs.data(), d_sums.p, hs.size() * sizeof(clg::TileSum), hipMemcpyDeviceToHost, stream);
+      hipMemcpyAsync(hf.data(), d_flags.p, hf.size() * 4, hipMemcpyDeviceToHost, stream);
+      hipStreamSynchronize(stream);
+      if (FILE* fp = fopen(dump, "wb")) {
+        fwrite(&nt, 4, 1, fp);
+        fwrite(&ns, 4, 1, fp);
+        fwrite(hc.data(), 4, hc.size(), fp);
+        fwrite(hs.data(), sizeof(clg::TileSum), hs.size(), fp);
+        fwrite(hf.data(), 4, hf.size(), fp);
+        fwrite(p.tiles.data(), sizeof(clg::TileDesc), nt, fp);
+        std::vector<uint32_t> hd(size_t(nt) * clg::kRegions);
+        hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
+        fwrite(hd.data(), 4, hd.size(), fp);
+        fclose(fp);
+      }
+    }
     clg::SpanRes* hres = reinterpret_cast<clg::SpanRes*>(hd + ((hb + 15) & ~size_t(15)));
     HIPCHK(hipMemcpyAsync(hres, d_sres.p, ns * sizeof(clg::SpanRes), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));

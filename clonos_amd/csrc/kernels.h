@@ -87,6 +87,50 @@ struct DecodeOut {
   uint64_t wcap;
 };
 
+// ---- fast decode: convergence points -----------------------------------------------
+// conv[t][l] = aligned coordinate (tile t) of region l's convergence point: the first
+// position that every live candidate parse from the region's first kEntries offsets
+// passes through; kConvUnknown if the candidates did not converge.
+constexpr uint32_t kConvUnknown = 0xFFFFFFFFu;
+constexpr int kFastHalo = 512;  // bytes of the span's next tile staged after a tile
+
+// Per-lane segment [conv[l], conv[end]) parsed by k_fast_count.  end in 1..127 indexes
+// this tile's points (< 64) or the next tile's (>= 64); kEndFail = parse failed/anomaly.
+struct LaneSeg {
+  uint8_t end;
+  uint8_t flags;
+  uint16_t cnt;
+  uint16_t wcnt;
+  uint16_t pad;
+};
+constexpr uint8_t kEndFail = 0xFF;
+
+// Tile summary assuming the tile's entry is its first known point f.
+struct TileSum {
+  uint32_t cnt, wcnt;
+  uint8_t f;      // first known point index (entry assumed)
+  uint8_t x;      // exit: index of the next tile's point the chain lands on; kEndFail = anomaly
+  uint8_t pad[2];
+  uint32_t pad2;
+  uint64_t valid; // lanes on the chain from f
+};
+
+struct FastRes {
+  uint64_t valid;      // lanes whose segments are on the resolved path
+  uint64_t rec_base;   // span-relative
+  uint64_t wide_base;
+};
+
+int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv,
+                     uint32_t* d_dbg, void* stream);
+int launch_fast_count(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
+                      LaneSeg* d_lanes, TileSum* d_sums, void* stream);
+int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes,
+                        const TileSum* d_sums, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
+int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
+                     const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
+                     const uint32_t* d_span_flags, DecodeOut out, void* stream);
+
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
 // segment.  Pieces are produced per slice request and split at segment boundaries.
@@ -108,14 +152,16 @@ struct ScatterChunk {
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream);
+// Robust pipeline (per-byte DP transfer tables); runs only on spans whose flag is set
+// (d_span_flags == nullptr: all spans).
 int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
-                         uint64_t* d_agg, TileConv* d_conv, void* stream);
+                         uint64_t* d_agg, TileConv* d_conv, const uint32_t* d_span_flags, void* stream);
 int launch_decode_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                           const uint64_t* d_agg, const TileConv* d_conv, TileRes* d_tres,
-                          SpanRes* d_sres, void* stream);
+                          SpanRes* d_sres, const uint32_t* d_span_flags, void* stream);
 int launch_decode_spanscan(SpanRes* d_sres, uint32_t n_spans, uint64_t* d_totals, void* stream);
 int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
                        const TileConv* d_conv, const TileRes* d_tres, const SpanRes* d_sres,
-                       DecodeOut out, void* stream);
+                       const uint32_t* d_span_flags, DecodeOut out, void* stream);
 
 }  // namespace clg

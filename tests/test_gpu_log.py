@@ -1,0 +1,156 @@
+"""GPU: the engine's ThreadCausalLog (HBM segments + host metadata) == the oracle's
+ThreadCausalLogImpl model, op by op, bytes and state.  Also the batched slice path."""
+import numpy as np
+import pytest
+
+import _oracle as O
+from clonos_amd import ClonosError, CausalLogID, Engine
+from clonos_amd import determinants as D
+from clonos_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def status_of(fn, *a):
+    try:
+        return 0, fn(*a)
+    except ClonosError as e:
+        return e.status, None
+
+
+@pytest.mark.parametrize("seed,comp", [(0, 16), (1, 32), (2, 64), (3, 256), (4, 16384)])
+def test_log_ops_match_oracle(seed, comp):
+    rng = np.random.default_rng(1000 + seed)
+    with Engine(segment_bytes=comp, pool_segments=1 << 14) as eng:
+        log = eng.open_log(CausalLogID.main(1))
+        ref = O.OracleLog(comp)
+        epoch, last_cp = 0, 0
+        chans = [(1, 9), (2, 9), (3, 9), (4, 9)]
+        for step in range(1500):
+            op = int(rng.integers(0, 12))
+            if op <= 4:
+                rec = D.encode(synth.random_determinant(rng))
+                log.appendDeterminant(rec, epoch)
+                assert ref.append(epoch, rec) == 0
+            elif op == 5:
+                # upstream delta overlapping what we have (dedup) or extending it
+                cur = ref.state()
+                rec = b"".join(D.encode(synth.random_determinant(rng)) for _ in range(int(rng.integers(1, 6))))
+                back = int(rng.integers(0, 3))
+                have = ref.get_determinants(epoch)[1] if epoch in dict(cur["epochs"]) else b""
+                delta = have[len(have) - min(back * 2, len(have)):] + rec if back else rec
+                off = len(have) - (len(delta) - len(rec))
+                st1, _ = status_of(log.processUpstreamDelta, delta, off, epoch)
+                assert st1 == ref.upstream(delta, off, epoch)
+            elif op == 6:
+                ch = chans[int(rng.integers(0, len(chans)))]
+                e = epoch - int(rng.integers(0, 2))
+                st1, v1 = status_of(log.hasDeltaForConsumer, ch, e)
+                st2, v2 = ref.has_delta(ch, e)
+                assert (st1, bool(v1) if st1 == 0 else False) == (st2, v2 if st2 == 0 else False)
+                if st1 == 0 and v1:
+                    assert log.getOffsetFromEpochForConsumer(ch, e) == ref.offset(ch)[1]
+                    st1, d1 = status_of(log.getDeltaForConsumer, ch, e)
+                    st2, d2 = ref.get_delta(ch, e)
+                    assert st1 == st2 and (st1 != 0 or d1 == d2)
+            elif op == 7:
+                epoch += 1
+            elif op == 8 and epoch - 1 > last_cp:
+                cp = epoch - int(rng.integers(0, 2))
+                last_cp = cp
+                st1, _ = status_of(log.notifyCheckpointComplete, cp)
+                assert st1 == ref.checkpoint_complete(cp)
+            elif op == 9:
+                e = epoch - int(rng.integers(0, 3))
+                st1, d1 = status_of(log.getDeterminants, e)
+                st2, d2 = ref.get_determinants(e)
+                assert st1 == st2 and (st1 != 0 or d1 == d2)
+            elif op == 10:
+                assert log.logLength() == ref.log_length()
+            else:
+                ch = chans[int(rng.integers(0, len(chans)))]
+                log.unregisterConsumer(ch)
+                ref.unregister(ch)
+            s1, s2 = log.state(), ref.state()
+            assert s1 == s2, (step, s1, s2)
+            for ch in chans:
+                assert log.consumer_state(ch) == ref.consumer(ch)
+        # physical bytes identical
+        s = ref.state()
+        if s["writer"]:
+            assert log.read_phys(0, s["writer"]) == ref.read_phys(0, s["writer"])[1]
+
+
+def test_nettytests_delta_over_components():
+    """NettyTests.CompositeFromCompositeComponentsTest (:144-186) with 16-byte components:
+    a delta straddling three components; truncation drops whole components only."""
+    with Engine(segment_bytes=16, pool_segments=64) as eng:
+        log = eng.open_log(CausalLogID.main(0))
+        for _ in range(5):
+            log.appendDeterminant(b"Hello world, hi!", 0)  # exactly one component each
+        ch = (7, 7)
+        assert log.hasDeltaForConsumer(ch, 0)
+        log.seek_consumer(ch, 0, 5)
+        assert log.getDeltaForConsumer(ch, 0) == (b"Hello world, hi!" * 5)[5:]
+        log.appendDeterminant(b"X" * 12, 1)  # epoch 1 starts at physical 80
+        log.notifyCheckpointComplete(1)
+        st = log.state()
+        assert st["capacity"] == 16 and st["n_components"] == 1 and st["epochs"] == [(1, 0)]
+
+
+def test_slice_batch_matches_sequential():
+    rng = np.random.default_rng(77)
+    with Engine(segment_bytes=512, pool_segments=1 << 14) as eng:
+        logs = [eng.open_log(CausalLogID.sub(v, 11, 22, v % 3)) for v in range(16)]
+        refs = [O.OracleLog(512) for _ in logs]
+        for ep in range(3):
+            for log, ref in zip(logs, refs):
+                for _ in range(int(rng.integers(0, 300))):
+                    rec = D.encode(synth.random_determinant(rng))
+                    log.appendDeterminant(rec, ep)
+                    ref.append(ep, rec)
+            reqs, expect = [], []
+            for i, (log, ref) in enumerate(zip(logs, refs)):
+                for c in range(4):
+                    ch = (c, i)
+                    reqs.append((log, ch, ep))
+                    st, has = ref.has_delta(ch, ep)
+                    if has:
+                        off = ref.offset(ch)[1]
+                        d = ref.get_delta(ch, ep)[1]
+                        expect.append((True, off, d))
+                    else:
+                        expect.append((False, 0, b""))
+            res, out, total = eng.slice_batch(reqs)
+            for (st, has, off, n, oo), (h2, off2, d2) in zip(res, expect):
+                assert st == 0 and has == h2
+                if has:
+                    assert off == off2 and out[oo:oo + n].tobytes() == d2
+
+
+def test_consumer_went_backwards():
+    with Engine(segment_bytes=64, pool_segments=64) as eng:
+        log = eng.open_log(CausalLogID.main(0))
+        log.appendDeterminant(D.OrderDeterminant(1), 0)
+        log.appendDeterminant(D.OrderDeterminant(2), 1)
+        assert log.hasDeltaForConsumer(1, 1)
+        with pytest.raises(ClonosError) as ex:
+            log.hasDeltaForConsumer(1, 0)
+        assert ex.value.status == -7
+
+
+def test_truncate_all_cas_and_pool_reuse():
+    with Engine(segment_bytes=64, pool_segments=256) as eng:
+        logs = [eng.open_log(CausalLogID.main(v)) for v in range(8)]
+        for ep in range(1, 6):
+            for log in logs:
+                for _ in range(40):
+                    log.appendDeterminant(D.TimestampDeterminant(ep), ep)
+        used0, _ = eng.pool_stats()
+        assert eng.truncate_all(4)
+        assert not eng.truncate_all(3)  # CAS: older checkpoint ignored (JobCausalLogImpl :234-235)
+        used1, _ = eng.pool_stats()
+        assert used1 < used0
+        for log in logs:
+            assert log.state()["epochs"][0][0] == 4
+            assert log.getDeterminants(4) == D.encode(D.TimestampDeterminant(4)) * 40 + D.encode(D.TimestampDeterminant(5)) * 40
