@@ -14,10 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libclonos_engine.so")
-SOURCES = [os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "kernels.hip")]
+SOURCES = [os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "decode_fast.hip")]
 HEADERS = [
     os.path.join(CSRC, "kernels.h"),
     os.path.join(CSRC, "jser_device.h"),
+    os.path.join(CSRC, "dev_common.h"),
+    os.path.join(CSRC, "dev_slow.h"),
     os.path.join(ROOT, "include", "clonos_engine.h"),
 ]
 ARCH = os.environ.get("CLONOS_OFFLOAD_ARCH", "gfx950")

@@ -172,7 +172,7 @@ struct clg_engine {
   // staging / scratch
   PinBuf h_stage, h_desc;
   DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
-  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg;
+  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
 
   // timing
@@ -562,6 +562,10 @@ struct clg_engine {
     CHK(d_sums.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileSum)));
     CHK(d_fres.ensure(std::max<size_t>(1, nt) * sizeof(clg::FastRes)));
     CHK(d_flags.ensure(ns * sizeof(uint32_t)));
+    CHK(d_jpos.ensure(std::max<size_t>(1, nt) * clg::kJserCap * sizeof(uint32_t)));
+    CHK(d_jlen.ensure(std::max<size_t>(1, nt) * clg::kJserCap * sizeof(uint32_t)));
+    CHK(d_jn.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
+    CHK(d_defer.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
     const size_t hb = nt * sizeof(clg::TileDesc) + ns * sizeof(clg::SpanDesc);
     CHK(h_desc.ensure(hb + ns * sizeof(clg::SpanRes) + 64));
     uint8_t* hd = h_desc.as<uint8_t>();
@@ -596,19 +600,25 @@ struct clg_engine {
     auto* ds = d_spans.as<clg::SpanDesc>();
     auto* flags = d_flags.as<uint32_t>();
     // fast path: convergence points -> segment counts -> per-span resolution
+    const clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>()};
+    uint32_t* dbg = nullptr;
+    if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kRegions * 4) == CLG_OK)
+      dbg = d_dbg.as<uint32_t>();
     CHK(timed("decode_conv", log_bytes, [&] {
-      uint32_t* dbg = nullptr;
-      if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kRegions * 4) == CLG_OK)
-        dbg = d_dbg.as<uint32_t>();
-      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), dbg, stream);
+      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), J, 0, dbg, stream);
+    }));
+    CHK(timed("decode_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
+    CHK(timed("decode_conv_deferred", 0, [&] {
+      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, dbg, stream);
     }));
     CHK(timed("decode_count", log_bytes, [&] {
-      return clg::launch_fast_count(dt, nt, ds, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(),
+      return clg::launch_fast_count(dt, nt, ds, d_fconv.as<uint32_t>(), J, d_lanes.as<clg::LaneSeg>(),
                                     d_sums.as<clg::TileSum>(), stream);
     }));
     CHK(timed("decode_resolve", uint64_t(nt) * 32, [&] {
-      return clg::launch_fast_resolve(dt, ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
-                                      d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags, stream);
+      return clg::launch_fast_resolve(ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
+                                      d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags,
+                                      stream);
     }));
     // robust DP pipeline for flagged spans only (early exit elsewhere)
     CHK(timed("decode_dp_tables", 0, [&] {
@@ -628,8 +638,8 @@ struct clg_engine {
       eb = get_event();
       hipEventRecord(ea, stream);
     }
-    CHK(clg::launch_fast_emit(dt, nt, ds, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(), d_fres.as<clg::FastRes>(),
-                              d_sres.as<clg::SpanRes>(), flags, o, stream));
+    CHK(clg::launch_fast_emit(dt, nt, ds, d_fconv.as<uint32_t>(), J, d_lanes.as<clg::LaneSeg>(),
+                              d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags, o, stream));
     if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     CHK(timed("decode_dp_emit", 0, [&] {
       return clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),

@@ -121,14 +121,28 @@ struct FastRes {
   uint64_t wide_base;
 };
 
-int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv,
-                     uint32_t* d_dbg, void* stream);
+constexpr int kCands = 32;     // candidate entries per region (covers every fixed-layout record)
+constexpr int kJserCap = 256;  // Serializable stream-length table entries per tile
+
+// Serializable stream lengths per tile, sorted by position (aligned coordinates):
+// pos/len[t * kJserCap + i], n[t] entries (n > kJserCap: overflow, span falls back);
+// defer[t] = 1 if the tile holds a "03 AC ED 00 05" pattern.
+struct JserTabs {
+  uint32_t* pos;
+  uint32_t* len;
+  uint32_t* n;
+  uint32_t* defer;
+};
+
+int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
+                     uint32_t mode, uint32_t* d_dbg, void* stream);
+int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream);
 int launch_fast_count(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                      LaneSeg* d_lanes, TileSum* d_sums, void* stream);
-int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes,
-                        const TileSum* d_sums, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
+                      JserTabs J, LaneSeg* d_lanes, TileSum* d_sums, void* stream);
+int launch_fast_resolve(const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes, const TileSum* d_sums,
+                        const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
 int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                     const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
+                     JserTabs J, const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
                      const uint32_t* d_span_flags, DecodeOut out, void* stream);
 
 // ---- gather (delta slice) -------------------------------------------------------

@@ -16,198 +16,9 @@
 #include <stdint.h>
 
 #include "../../include/clonos_engine.h"
-#include "jser_device.h"
-#include "kernels.h"
+#include "dev_slow.h"
 
 namespace clg {
-
-// ----------------------------------------------------------------------------------
-// Packed region-table entry: exit offset past the region end (16 bits, 0xFFFF = error,
-// 0xFFFE = far), record count (8 bits), wide-record count (8 bits).
-// ----------------------------------------------------------------------------------
-constexpr uint32_t kNsErr = 0xFFFFu;
-constexpr uint32_t kNsFar = 0xFFFEu;
-constexpr int kPitch = 65;  // dwords per region in the LDS tile image (64 + 1 pad)
-
-__device__ __forceinline__ uint32_t lds_byte_addr(uint32_t a) {
-  return ((a >> 8) * kPitch + ((a >> 2) & 63u)) * 4u + (a & 3u);
-}
-
-// Byte reader over a whole span (global memory, walks the span's tile list).
-struct SpanReader {
-  const TileDesc* tiles;
-  uint32_t t0, t1, cur;
-  uint64_t len;
-  __device__ int at(uint64_t o) {
-    if (o >= len) return -1;
-    while (cur > t0 && o < tiles[cur].span_off) --cur;
-    while (cur + 1 < t1 && o >= tiles[cur].span_off + tiles[cur].len) ++cur;
-    const TileDesc& t = tiles[cur];
-    return t.abase[t.delta + (o - t.span_off)];
-  }
-};
-
-// Byte reader for one tile: the LDS image for bytes inside the tile, the span reader
-// beyond it.  Coordinates are the tile's aligned coordinates.
-struct TileReader {
-  const uint8_t* lds;
-  uint32_t lo, hi;
-  uint64_t so;  // span offset of aligned coordinate lo
-  SpanReader* sr;
-  __device__ __forceinline__ int at(uint32_t a) {
-    if (a < hi) return lds[lds_byte_addr(a)];
-    return sr->at(so + (a - lo));
-  }
-  __device__ __forceinline__ uint64_t span_off(uint32_t a) const { return so + (a - lo); }
-};
-
-// Bytes relative to a record start, for the length / value parsers.
-template <class R>
-struct At {
-  R* r;
-  uint32_t base;
-  __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + (uint32_t)k); }
-};
-struct AtSpan {
-  SpanReader* r;
-  uint64_t base;
-  __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + k); }
-};
-
-template <class F>
-__device__ __forceinline__ uint32_t rd_be32(F& b, uint32_t k) {
-  return (uint32_t)b(k) << 24 | (uint32_t)b(k + 1) << 16 | (uint32_t)b(k + 2) << 8 | (uint32_t)b(k + 3);
-}
-template <class F>
-__device__ __forceinline__ uint64_t rd_be64(F& b, uint32_t k) {
-  return (uint64_t)rd_be32(b, k) << 32 | rd_be32(b, k + 4);
-}
-
-// Exact record length at a record start (decodeNext read order and error precedence).
-// `avail` = bytes from the record start to the span end (>= 1).  Returns L > 0 or a
-// negative CLG_E_* status.
-template <class F>
-__device__ __noinline__ int64_t rec_len_slow(F& b, uint64_t avail) {
-  const int tag = (int8_t)b(0);
-  int64_t L;
-  switch (tag) {
-    case CLG_TAG_ORDER: L = 2; break;
-    case CLG_TAG_TIMESTAMP: L = 9; break;
-    case CLG_TAG_RNG:
-    case CLG_TAG_BUFFER_BUILT: L = 5; break;
-    case CLG_TAG_IGNORE_CHECKPOINT: L = 13; break;
-    case CLG_TAG_TIMER_TRIGGER: {
-      if (avail < 14) return CLG_E_TRUNCATED;
-      const int ord = (int8_t)b(13);
-      if (ord < 0 || ord > 6) return CLG_E_BAD_ENUM;
-      if (ord == 6) {
-        if (avail < 18) return CLG_E_TRUNCATED;
-        const int32_t nl = (int32_t)rd_be32(b, 14);
-        if (nl < 0) return CLG_E_NEG_LEN;
-        L = 18 + (int64_t)nl;
-      } else {
-        L = 14;
-      }
-      break;
-    }
-    case CLG_TAG_SOURCE_CHECKPOINT: {
-      if (avail < 23) return CLG_E_TRUNCATED;
-      if (b(22) != 0) {
-        if (avail < 27) return CLG_E_TRUNCATED;
-        const int32_t rl = (int32_t)rd_be32(b, 23);
-        if (rl < 0) return CLG_E_NEG_LEN;
-        L = 27 + (int64_t)rl;
-      } else {
-        L = 23;
-      }
-      if ((uint64_t)L > avail) return CLG_E_TRUNCATED;
-      const int ord = (int8_t)b(21);
-      if (ord < 0 || ord > 1) return CLG_E_BAD_ENUM;
-      return L;
-    }
-    case CLG_TAG_SERIALIZABLE: {
-      struct Shift {
-        F* f;
-        __device__ int operator()(uint64_t k) { return (*f)(k + 1); }
-      } sh{&b};
-      const int64_t j = jser::stream_len(sh, avail - 1);
-      if (j < 0) return CLG_E_BAD_SERIAL;
-      L = 1 + j;
-      break;
-    }
-    default:
-      return CLG_E_CORRUPT_TAG;
-  }
-  if ((uint64_t)L > avail) return CLG_E_TRUNCATED;
-  return L;
-}
-
-// Fixed-length tags via a nibble LUT: 0->2, 1->9, 2->5, 6->13, 7->5; 0 = "slow" (3,4,5).
-__device__ __forceinline__ int fast_len(int tag) {
-  constexpr uint32_t lut = 2u | 9u << 4 | 5u << 8 | 0u << 12 | 0u << 16 | 0u << 20 | 13u << 24 | 5u << 28;
-  return (tag >= 0 && tag < 8) ? (int)((lut >> (4 * tag)) & 0xF) : -1;
-}
-__device__ __forceinline__ uint32_t is_wide(int tag) { return (tag >= 3 && tag <= 6) ? 1u : 0u; }
-
-// One decoded record (values + length), exact.
-struct Rec {
-  int64_t v0, v1;
-  int32_t rc;
-  uint32_t var_off, var_len;  // var_off relative to record start
-  uint32_t L;
-  uint8_t tag, sub, wide;
-};
-
-template <class F>
-__device__ int decode_rec(F& b, uint64_t avail, Rec& r) {
-  const int64_t L = rec_len_slow(b, avail);
-  if (L < 0) return (int)L;
-  const int tag = b(0);
-  r.tag = (uint8_t)tag;
-  r.L = (uint32_t)L;
-  r.wide = (uint8_t)is_wide(tag);
-  r.v1 = 0;
-  r.rc = 0;
-  r.var_off = 0;
-  r.var_len = 0;
-  r.sub = 0;
-  switch (tag) {
-    case CLG_TAG_ORDER: r.v0 = (int8_t)b(1); break;
-    case CLG_TAG_TIMESTAMP: r.v0 = (int64_t)rd_be64(b, 1); break;
-    case CLG_TAG_RNG:
-    case CLG_TAG_BUFFER_BUILT: r.v0 = (int32_t)rd_be32(b, 1); break;
-    case CLG_TAG_IGNORE_CHECKPOINT:
-      r.rc = (int32_t)rd_be32(b, 1);
-      r.v0 = (int64_t)rd_be64(b, 5);
-      break;
-    case CLG_TAG_TIMER_TRIGGER:
-      r.rc = (int32_t)rd_be32(b, 1);
-      r.v0 = (int64_t)rd_be64(b, 5);
-      r.sub = (uint8_t)b(13);
-      if (r.sub == 6) {
-        r.var_off = 18;
-        r.var_len = (uint32_t)(L - 18);
-      }
-      break;
-    case CLG_TAG_SOURCE_CHECKPOINT:
-      r.rc = (int32_t)rd_be32(b, 1);
-      r.v0 = (int64_t)rd_be64(b, 5);
-      r.v1 = (int64_t)rd_be64(b, 13);
-      r.sub = (uint8_t)b(21);
-      if (b(22) != 0) {
-        r.sub |= 0x80;
-        r.var_off = 27;
-        r.var_len = (uint32_t)(L - 27);
-      }
-      break;
-    case CLG_TAG_SERIALIZABLE:
-      r.v0 = L - 1;
-      r.var_off = 1;
-      r.var_len = (uint32_t)(L - 1);
-      break;
-  }
-  return CLG_OK;
-}
 
 // ==================================================================================
 // Append scatter: one wave per chunk.
@@ -267,136 +78,6 @@ __global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ 
       for (uintptr_t x = b0; x < b1; ++x) *reinterpret_cast<uint8_t*>(x) = *reinterpret_cast<const uint8_t*>(x + sdelta);
     }
   }
-}
-
-// ==================================================================================
-// Decode, shared pieces.
-//
-// LDS tile image: 65 rows of 65 dwords.  Row r holds aligned coordinates
-// [256 r, 256 r + 256) (one lane region) plus one pad dword, so that lanes reading
-// their own regions at the same offset hit distinct banks.  Row 64 and the area past
-// the tile's last valid byte hold a 32-byte halo copied from the span's next tile, so
-// every fixed-layout field (at most 27 bytes into a record) is read from LDS.
-// ==================================================================================
-constexpr int kHalo = 32;
-constexpr int kImageDwords = (kRegions + 1) * kPitch;
-constexpr int64_t kLenErr = -1;   // any decode error (exact code from the slow path)
-constexpr int64_t kLenSlow = 0;   // needs the slow path (Serializable stream walk)
-
-struct TileGeom {
-  uint32_t lo, hi;  // valid aligned coordinates
-  __device__ __forceinline__ uint32_t rs(int l) const { uint32_t s = (uint32_t)l * kRegion; return s < lo ? lo : s; }
-  __device__ __forceinline__ uint32_t re(int l) const { uint32_t e = (uint32_t)(l + 1) * kRegion; return e > hi ? hi : e; }
-};
-
-__device__ __forceinline__ uint32_t t_dw(const uint32_t* T, uint32_t k) { return T[(k >> 6) * kPitch + (k & 63u)]; }
-__device__ __forceinline__ int t_u8(const uint32_t* T, uint32_t a) {
-  return (int)((t_dw(T, a >> 2) >> (8 * (a & 3u))) & 0xFFu);
-}
-__device__ __forceinline__ uint32_t t_be32(const uint32_t* T, uint32_t a) {
-  const uint32_t k = a >> 2, s = a & 3u;
-  const uint32_t le = __builtin_amdgcn_alignbyte(t_dw(T, k + 1), t_dw(T, k), s);
-  return __builtin_bswap32(le);
-}
-__device__ __forceinline__ uint64_t t_be64(const uint32_t* T, uint32_t a) {
-  const uint32_t k = a >> 2, s = a & 3u;
-  const uint32_t d0 = t_dw(T, k), d1 = t_dw(T, k + 1), d2 = t_dw(T, k + 2);
-  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, s), hi = __builtin_amdgcn_alignbyte(d2, d1, s);
-  return __builtin_bswap64((uint64_t)hi << 32 | lo);
-}
-
-// Stage one tile (16-byte coalesced loads) plus its halo into the LDS image.
-__device__ __forceinline__ void stage_tile(uint32_t* s_tile, const TileDesc& td, SpanReader& sr, uint32_t lane) {
-  const uint32_t words = (td.delta + td.len + 15) >> 4;
-  for (uint32_t w = lane; w < words; w += 64) {
-    const uint4 v = *reinterpret_cast<const uint4*>(td.abase + 16 * w);
-    const uint32_t d = (w >> 4) * kPitch + ((w & 15u) << 2);
-    s_tile[d + 0] = v.x;
-    s_tile[d + 1] = v.y;
-    s_tile[d + 2] = v.z;
-    s_tile[d + 3] = v.w;
-  }
-  __syncthreads();
-  // halo: bytes [hi, hi + kHalo) of the span (zeros past the span end)
-  if (lane < (uint32_t)kHalo) {
-    const uint32_t a = td.delta + td.len + lane;
-    const int b = sr.at(td.span_off + td.len + lane);
-    reinterpret_cast<uint8_t*>(s_tile)[(a >> 8) * (kPitch * 4) + (a & 255u)] = (uint8_t)(b < 0 ? 0 : b);
-  }
-  __syncthreads();
-}
-
-// Record length at aligned coordinate a (a record start candidate, a < hi), using only
-// the LDS image.  end_a = aligned coordinate of the span end.
-__device__ __forceinline__ int64_t len_inline(const uint32_t* T, int tag, uint32_t a, uint64_t end_a) {
-  constexpr uint32_t lut = 2u | 9u << 4 | 5u << 8 | 13u << 24 | 5u << 28;
-  if ((uint32_t)tag > 7u) return kLenErr;
-  int64_t L = (int64_t)((lut >> (4 * tag)) & 0xFu);
-  if (L == 0) {
-    if (tag == CLG_TAG_TIMER_TRIGGER) {
-      const int ord = (int8_t)t_u8(T, a + 13);
-      if (ord < 0 || ord > 6) return kLenErr;
-      if (ord != 6) {
-        L = 14;
-      } else {
-        const int32_t nl = (int32_t)t_be32(T, a + 14);
-        if (nl < 0) return kLenErr;
-        L = 18 + (int64_t)nl;
-      }
-    } else if (tag == CLG_TAG_SOURCE_CHECKPOINT) {
-      const int ord = (int8_t)t_u8(T, a + 21);
-      if (ord < 0 || ord > 1) return kLenErr;
-      L = 23;
-      if (t_u8(T, a + 22) != 0) {
-        const int32_t rl = (int32_t)t_be32(T, a + 23);
-        if (rl < 0) return kLenErr;
-        L = 27 + (int64_t)rl;
-      }
-    } else {  // SERIALIZABLE: cheap magic check, the walk itself is out of line
-      if (t_be32(T, a + 1) != 0xACED0005u) return kLenErr;
-      return kLenSlow;
-    }
-  }
-  return ((uint64_t)a + (uint64_t)L > end_a) ? kLenErr : L;
-}
-
-// Exact length through the span reader (Serializable streams; error classification).
-__device__ __noinline__ int64_t len_slow_span(SpanReader* sr, uint64_t so) {
-  AtSpan b{sr, so};
-  return rec_len_slow(b, sr->len - so);
-}
-
-// Length of the record at aligned coordinate a (< hi), fast path + slow fallback.
-__device__ __forceinline__ int64_t rec_len_at(const uint32_t* T, SpanReader* sr, uint32_t a, uint32_t lo,
-                                              uint64_t tile_so, uint64_t end_a, int* tag_out) {
-  const int tag = t_u8(T, a);
-  *tag_out = tag;
-  int64_t L = len_inline(T, tag, a, end_a);
-  if (L == kLenSlow) {
-    L = len_slow_span(sr, tile_so + (a - lo));
-    if (L <= 0) L = kLenErr;
-  }
-  return L;
-}
-
-// Forward parse of one region from an entry (aligned coordinate `a`) to `stop`.
-// Returns the exit (first record start >= stop) and counts, or kLenErr.
-__device__ int region_forward(const uint32_t* T, SpanReader* sr, uint32_t lo, uint64_t tile_so, uint64_t end_a,
-                              uint32_t a, uint32_t stop, uint32_t* exit, uint32_t* cnt, uint32_t* wcnt) {
-  uint32_t c = 0, w = 0;
-  while (a < stop) {
-    int tag;
-    const int64_t L = rec_len_at(T, sr, a, lo, tile_so, end_a, &tag);
-    if (L < 0) return CLG_E_STATE;
-    w += is_wide(tag);
-    ++c;
-    if ((uint64_t)a + (uint64_t)L > 0xFFFFFFF0ull) return CLG_E_STATE;
-    a += (uint32_t)L;
-  }
-  *exit = a;
-  *cnt = c;
-  *wcnt = w;
-  return CLG_OK;
 }
 
 // ==================================================================================
@@ -930,467 +611,6 @@ __global__ __launch_bounds__(64) void k_dec_emit(const TileDesc* __restrict__ ti
 }
 
 // ==================================================================================
-// Fast decode: convergence points.
-//
-// For region l of a tile, start a parse at each of its first kEntries offsets (every
-// possible record start a record of < kEntries bytes can leave behind) and advance the
-// candidates in position order with a 64-bit frontier (paths that land on the same byte
-// merge; paths that hit an invalid record die).  The first position through which every
-// live candidate passes -- the region's convergence point -- is a record start on the
-// true path whenever the true entry is one of the candidates.  Lanes then parse the
-// segments between consecutive points; the chain of segments from a tile's entry point
-// is checked in-kernel (a lane that jumps over a point keeps going to the next one), so
-// a wrong point costs extra parsing, never a wrong answer.  Spans where the chain breaks
-// (no point reachable, a decode error) are flagged and re-decoded by the DP pipeline
-// above, which also reports exact error positions.
-// ==================================================================================
-constexpr int kFastRows = (kTile + kFastHalo) / kRegion + 1;
-constexpr int kFastImageDwords = kFastRows * kPitch;
-constexpr uint64_t kNoFar = ~0ull;
-constexpr int kMaxPops = 192;  // give up early: an unknown point only lengthens the previous segment
-constexpr int kMaxSegRecords = 1 << 15;
-
-// Stage the tile plus up to kFastHalo bytes of the span that follow it.
-__device__ __forceinline__ uint32_t stage_fast(uint32_t* s_tile, const TileDesc& td, SpanReader& sr, uint32_t lane) {
-  const uint32_t words = (td.delta + td.len + 15) >> 4;
-  for (uint32_t w = lane; w < words; w += 64) {
-    const uint4 v = *reinterpret_cast<const uint4*>(td.abase + 16 * w);
-    const uint32_t d = (w >> 4) * kPitch + ((w & 15u) << 2);
-    s_tile[d + 0] = v.x;
-    s_tile[d + 1] = v.y;
-    s_tile[d + 2] = v.z;
-    s_tile[d + 3] = v.w;
-  }
-  __syncthreads();
-  const uint32_t hi = td.delta + td.len;
-  const uint64_t after = td.span_off + td.len;  // span offset of the first halo byte
-  const uint64_t avail = sr.len > after ? sr.len - after : 0;
-  const uint32_t halo = (uint32_t)(avail < (uint64_t)kFastHalo ? avail : (uint64_t)kFastHalo);
-  uint8_t* b = reinterpret_cast<uint8_t*>(s_tile);
-  for (uint32_t k = lane; k < halo; k += 64) {
-    const uint32_t a = hi + k;
-    b[(a >> 8) * (kPitch * 4) + (a & 255u)] = (uint8_t)sr.at(after + k);
-  }
-  __syncthreads();
-  return hi + halo;  // image valid up to here (exclusive)
-}
-
-// Length of the record at aligned coordinate a (a < end_a): LDS image when the fixed
-// fields are staged, exact span-reader path otherwise.
-__device__ __forceinline__ int64_t len_any(const uint32_t* T, SpanReader* sr, uint32_t a, uint32_t img_end,
-                                           uint64_t end_a, uint32_t lo, uint64_t tile_so, int* tag) {
-  if (a + 27u < img_end) {
-    *tag = t_u8(T, a);
-    int64_t L = len_inline(T, *tag, a, end_a);
-    if (L == kLenSlow) {
-      L = len_slow_span(sr, tile_so + (a - lo));
-      if (L <= 0) L = kLenErr;
-    }
-    return L;
-  }
-  const uint64_t so = tile_so + (a - lo);
-  *tag = sr->at(so);
-  const int64_t L = len_slow_span(sr, so);
-  return L <= 0 ? kLenErr : L;
-}
-
-__device__ uint32_t converge(const uint32_t* T, SpanReader* sr, uint32_t rs, uint32_t ncand, uint32_t img_end,
-                             uint64_t end_a, uint32_t lo, uint64_t tile_so, uint32_t* pops) {
-  if (ncand == 0) return kConvUnknown;
-  struct PopCount {
-    int n;
-  } pc{0};
-  uint64_t M = ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull);
-  uint64_t W = rs;
-  uint64_t F = kNoFar;
-  bool sink = false;  // some candidate ended exactly at the span end
-  for (int it = 0; it < kMaxPops; ++it) {
-    const int n = __popcll(M) + (F != kNoFar ? 1 : 0) + (sink ? 1 : 0);
-    *pops = (uint32_t)pc.n | ((uint32_t)n << 16);
-    if (n == 0) return kConvUnknown;
-    if (n == 1) {
-      if (M) return (uint32_t)(W + (uint64_t)(__ffsll((long long)M) - 1));
-      if (F != kNoFar) return F > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)F;
-      return end_a > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)end_a;
-    }
-    if (M == 0) {  // only the far slot (and maybe the sink) left: jump the window
-      W = F;
-      M = 1;
-      F = kNoFar;
-      continue;
-    }
-    const int b = __ffsll((long long)M) - 1;
-    const uint64_t p = W + (uint64_t)b;
-    M &= M - 1;
-    ++pc.n;
-    if (p >= end_a) {
-      sink = true;
-    } else {
-      int tag;
-      const int64_t L = (p + 27 < img_end) ? len_inline(T, t_u8(T, (uint32_t)p), (uint32_t)p, end_a) : kLenSlow;
-      int64_t Lx = L;
-      if (L == kLenSlow) Lx = len_any(T, sr, (uint32_t)p, img_end, end_a, lo, tile_so, &tag);
-      if (Lx > 0) {
-        const uint64_t q = p + (uint64_t)Lx;
-        if (q < W + 64) {
-          M |= 1ull << (q - W);
-        } else if (F == kNoFar || F == q) {
-          F = q;
-        } else {
-          *pops |= 0x80000000u;
-          return kConvUnknown;  // two candidates far ahead: not tracked
-        }
-      }
-    }
-    if (M) {
-      const int s = __ffsll((long long)M) - 1;
-      if (s) {
-        M >>= s;
-        W += (uint64_t)s;
-      }
-    }
-    if (F != kNoFar && F < W + 64) {
-      M |= 1ull << (F - W);
-      F = kNoFar;
-    }
-  }
-  return kConvUnknown;
-}
-
-// ---- pass F1: convergence points -------------------------------------------------
-__global__ __launch_bounds__(64) void k_fast_conv(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                  uint32_t* __restrict__ conv, uint32_t* __restrict__ dbg) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  const uint32_t t = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const TileDesc td = tiles[t];
-  const SpanDesc sd = spans[td.span];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
-  const uint32_t img_end = stage_fast(s_tile, td, sr, lane);
-  const TileGeom g{td.delta, td.delta + td.len};
-  const uint64_t end_a = sd.len - td.span_off + td.delta;
-  const uint32_t rs = g.rs((int)lane), re = g.re((int)lane);
-  uint32_t c, pops = 0;
-  if (lane == 0 && t == sd.first_tile) {
-    c = td.delta;  // a span starts on a record boundary
-  } else {
-    const uint32_t RL = re > rs ? re - rs : 0;
-    c = converge(s_tile, &sr, rs, RL < (uint32_t)kEntries ? RL : (uint32_t)kEntries, img_end, end_a, td.delta,
-                 td.span_off, &pops);
-  }
-  conv[(uint64_t)t * kRegions + lane] = c;
-  if (dbg) dbg[(uint64_t)t * kRegions + lane] = pops;
-}
-
-// ---- pass F2: segment counts -----------------------------------------------------
-__device__ __forceinline__ int next_known(const uint32_t* s_c, int from) {
-  while (from < 2 * kRegions && s_c[from] == kConvUnknown) ++from;
-  return from;
-}
-
-// Points of this tile (0..63) and of the span's next tile (64..127) in this tile's
-// aligned coordinates; for the span's last tile the span end is point 64.
-__device__ __forceinline__ void load_points(uint32_t* s_c, const uint32_t* conv, const TileDesc* tiles,
-                                            const TileDesc& td, const SpanDesc& sd, uint32_t t, uint32_t lane,
-                                            uint64_t end_a) {
-  s_c[lane] = conv[(uint64_t)t * kRegions + lane];
-  const bool last = t + 1 == sd.first_tile + sd.n_tiles;
-  uint32_t x = kConvUnknown;
-  if (!last) {
-    const uint32_t c = conv[(uint64_t)(t + 1) * kRegions + lane];
-    if (c != kConvUnknown) {
-      const uint64_t v = (uint64_t)(td.delta + td.len) + (uint64_t)(c - tiles[t + 1].delta);
-      x = v > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)v;
-    }
-  } else if (lane == 0) {
-    x = end_a > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)end_a;
-  }
-  s_c[kRegions + lane] = x;
-  __syncthreads();
-  // Make both halves monotonic by dropping points that lie beyond a later point (a
-  // dropped point only means a longer segment for the lane before it).  The next
-  // tile's half is filtered on its own, exactly as that tile filters it, so both tiles
-  // agree on where the chain crosses the boundary; this tile's half is then filtered
-  // against everything after it.
-  if (lane == 0) {
-    uint32_t lim = kConvUnknown;
-    for (int l = 2 * kRegions - 1; l >= kRegions; --l) {
-      const uint32_t c = s_c[l];
-      if (c == kConvUnknown) continue;
-      if (c > lim) s_c[l] = kConvUnknown; else lim = c;
-    }
-    for (int l = kRegions - 1; l >= 0; --l) {
-      const uint32_t c = s_c[l];
-      if (c == kConvUnknown) continue;
-      if (c > lim) s_c[l] = kConvUnknown; else lim = c;
-    }
-  }
-  __syncthreads();
-}
-
-// Parse from point l until landing exactly on a later known point.  Returns the segment.
-__device__ LaneSeg parse_segment(const uint32_t* T, SpanReader* sr, const uint32_t* s_c, int l, uint32_t img_end,
-                                 uint64_t end_a, uint32_t lo, uint64_t tile_so) {
-  LaneSeg seg{kEndFail, 0, 0, 0, 0};
-  const uint32_t c0 = s_c[l];
-  if (c0 == kConvUnknown) return seg;
-  uint32_t pos = c0, cnt = 0, w = 0;
-  int m = next_known(s_c, l + 1);
-  for (int it = 0; it < kMaxSegRecords; ++it) {
-    while (m < 2 * kRegions && s_c[m] < pos) m = next_known(s_c, m + 1);
-    if (m >= 2 * kRegions) return seg;
-    if (s_c[m] == pos) {
-      seg.end = (uint8_t)m;
-      seg.cnt = (uint16_t)cnt;
-      seg.wcnt = (uint16_t)w;
-      return seg;
-    }
-    if ((uint64_t)pos >= end_a) return seg;
-    int tag;
-    const int64_t L = len_any(T, sr, pos, img_end, end_a, lo, tile_so, &tag);
-    if (L <= 0 || (uint64_t)pos + (uint64_t)L > 0xFFFFFFF0ull) return seg;
-    ++cnt;
-    w += is_wide(tag);
-    pos += (uint32_t)L;
-  }
-  return seg;
-}
-
-__global__ __launch_bounds__(64) void k_fast_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                   const uint32_t* __restrict__ conv, LaneSeg* __restrict__ lanes,
-                                                   TileSum* __restrict__ sums) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  __shared__ uint32_t s_c[2 * kRegions];
-  __shared__ LaneSeg s_seg[kRegions];
-  const uint32_t t = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const TileDesc td = tiles[t];
-  const SpanDesc sd = spans[td.span];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
-  const uint64_t end_a = sd.len - td.span_off + td.delta;
-  load_points(s_c, conv, tiles, td, sd, t, lane, end_a);
-  const uint32_t img_end = stage_fast(s_tile, td, sr, lane);  // contains __syncthreads
-
-  const LaneSeg seg = parse_segment(s_tile, &sr, s_c, (int)lane, img_end, end_a, td.delta, td.span_off);
-  s_seg[lane] = seg;
-  lanes[(uint64_t)t * kRegions + lane] = seg;
-  __syncthreads();
-  if (lane == 0) {
-    int f = 0;
-    while (f < kRegions && s_c[f] == kConvUnknown) ++f;
-    TileSum sm{};
-    sm.f = (uint8_t)f;
-    sm.x = kEndFail;
-    uint64_t valid = 0;
-    uint32_t cnt = 0, w = 0;
-    int v = f;
-    while (v < kRegions) {
-      const LaneSeg gs = s_seg[v];
-      if (gs.end == kEndFail) break;
-      valid |= 1ull << v;
-      cnt += gs.cnt;
-      w += gs.wcnt;
-      v = gs.end;
-    }
-    if (v >= kRegions && v < 2 * kRegions) sm.x = (uint8_t)(v - kRegions);
-    sm.cnt = cnt;
-    sm.wcnt = w;
-    sm.valid = valid;
-    sums[t] = sm;
-  }
-}
-
-// ---- pass F3: per-span resolution ----------------------------------------------------
-// Chain of segments from entry point e inside tile t (per-lane segments from pass F2).
-__device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* valid, uint32_t* cnt, uint32_t* wcnt,
-                           int* exit_idx) {
-  uint64_t vm = 0;
-  uint32_t c = 0, w = 0;
-  int v = e;
-  while (v < kRegions) {
-    const LaneSeg gs = lanes[(uint64_t)t * kRegions + v];
-    if (gs.end == kEndFail) return false;
-    vm |= 1ull << v;
-    c += gs.cnt;
-    w += gs.wcnt;
-    v = gs.end;
-  }
-  if (v >= 2 * kRegions) return false;
-  *valid = vm;
-  *cnt = c;
-  *wcnt = w;
-  *exit_idx = v - kRegions;
-  return true;
-}
-
-__global__ __launch_bounds__(256) void k_fast_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                      const LaneSeg* __restrict__ lanes, const TileSum* __restrict__ sums,
-                                                      FastRes* __restrict__ fres, SpanRes* __restrict__ sres,
-                                                      uint32_t* __restrict__ span_flags) {
-  __shared__ uint64_t s_r[256], s_w[256];
-  __shared__ uint32_t s_irregular;
-  __shared__ uint64_t s_carry_r, s_carry_w;
-  const uint32_t s = blockIdx.x;
-  const SpanDesc sd = spans[s];
-  if (threadIdx.x == 0) {
-    s_irregular = 0;
-    s_carry_r = 0;
-    s_carry_w = 0;
-  }
-  __syncthreads();
-  // regular: every tile's entry point is its first known point (f, 0 for the first tile)
-  // and the previous tile's chain lands on it; the last tile lands on the span end.
-  for (uint32_t i = threadIdx.x; i < sd.n_tiles; i += blockDim.x) {
-    const uint32_t t = sd.first_tile + i;
-    const TileSum sm = sums[t];
-    bool bad = sm.x == kEndFail || sm.f >= kRegions;
-    if (i == 0) bad |= sm.f != 0;
-    else bad |= sums[t - 1].x != sm.f;
-    if (i + 1 == sd.n_tiles) bad |= sm.x != 0;
-    if (bad) atomicOr(&s_irregular, 1u);
-  }
-  __syncthreads();
-  if (!s_irregular) {
-    for (uint32_t base = 0; base < sd.n_tiles; base += blockDim.x) {
-      const uint32_t i = base + threadIdx.x;
-      const TileSum sm = i < sd.n_tiles ? sums[sd.first_tile + i] : TileSum{};
-      const uint64_t r = i < sd.n_tiles ? sm.cnt : 0, w = i < sd.n_tiles ? sm.wcnt : 0;
-      s_r[threadIdx.x] = r;
-      s_w[threadIdx.x] = w;
-      __syncthreads();
-      for (uint32_t off = 1; off < blockDim.x; off <<= 1) {
-        const uint64_t ar = threadIdx.x >= off ? s_r[threadIdx.x - off] : 0;
-        const uint64_t aw = threadIdx.x >= off ? s_w[threadIdx.x - off] : 0;
-        __syncthreads();
-        s_r[threadIdx.x] += ar;
-        s_w[threadIdx.x] += aw;
-        __syncthreads();
-      }
-      if (i < sd.n_tiles) {
-        FastRes fr;
-        fr.valid = sm.valid;
-        fr.rec_base = s_carry_r + s_r[threadIdx.x] - r;
-        fr.wide_base = s_carry_w + s_w[threadIdx.x] - w;
-        fres[sd.first_tile + i] = fr;
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        s_carry_r += s_r[blockDim.x - 1];
-        s_carry_w += s_w[blockDim.x - 1];
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      SpanRes r{};
-      r.n_rec = s_carry_r;
-      r.n_wide = s_carry_w;
-      r.status = CLG_OK;
-      r.err_off = -1;
-      sres[s] = r;
-      span_flags[s] = 0;
-    }
-    return;
-  }
-  // irregular: serial walk with per-lane chains; give up to the DP pipeline on a break
-  if (threadIdx.x == 0) {
-    uint64_t rec = 0, wide = 0;
-    int e = 0;
-    bool fallback = sd.n_tiles == 0 ? false : false;
-    for (uint32_t i = 0; i < sd.n_tiles; ++i) {
-      const uint32_t t = sd.first_tile + i;
-      uint64_t vm;
-      uint32_t c, w;
-      int x;
-      if (!chain_from(lanes, t, e, &vm, &c, &w, &x)) {
-        fallback = true;
-        break;
-      }
-      fres[t] = FastRes{vm, rec, wide};
-      rec += c;
-      wide += w;
-      e = x;
-    }
-    if (!fallback && sd.n_tiles && e != 0) fallback = true;
-    SpanRes r{};
-    r.n_rec = rec;
-    r.n_wide = wide;
-    r.status = CLG_OK;
-    r.err_off = -1;
-    sres[s] = r;
-    span_flags[s] = fallback ? 1u : 0u;
-  }
-}
-
-// ---- pass F4: emit ---------------------------------------------------------------------
-__device__ __forceinline__ int decode_any(const uint32_t* T, SpanReader* sr, uint32_t a, uint32_t img_end,
-                                          uint32_t lo, uint64_t tile_so, uint64_t end_a, Rec& r) {
-  if (a + 27u < img_end) return decode_at(T, sr, a, lo, tile_so, end_a, r);
-  const uint64_t so = tile_so + (a - lo);
-  AtSpan b{sr, so};
-  return decode_rec(b, sr->len - so, r);
-}
-
-__global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                  const uint32_t* __restrict__ conv, const LaneSeg* __restrict__ lanes,
-                                                  const FastRes* __restrict__ fres, const SpanRes* __restrict__ sres,
-                                                  const uint32_t* __restrict__ span_flags, DecodeOut out) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  __shared__ uint32_t s_c[2 * kRegions];
-  const uint32_t t = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const TileDesc td = tiles[t];
-  if (span_flags[td.span]) return;  // decoded by the DP pipeline
-  const FastRes fr = fres[t];
-  if (fr.valid == 0) return;
-  const SpanDesc sd = spans[td.span];
-  const SpanRes sp = sres[td.span];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
-  const uint64_t end_a = sd.len - td.span_off + td.delta;
-  load_points(s_c, conv, tiles, td, sd, t, lane, end_a);
-  const uint32_t img_end = stage_fast(s_tile, td, sr, lane);
-
-  const bool mine = (fr.valid >> lane) & 1ull;
-  const LaneSeg seg = lanes[(uint64_t)t * kRegions + lane];
-  const uint32_t c = mine ? seg.cnt : 0u, w = mine ? seg.wcnt : 0u;
-  uint32_t ic = c, iw = w;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t yc = __shfl_up(ic, off), yw = __shfl_up(iw, off);
-    if ((int)lane >= off) {
-      ic += yc;
-      iw += yw;
-    }
-  }
-  uint64_t rec = sp.rec_base + fr.rec_base + (ic - c);
-  uint64_t wide = sp.wide_base + fr.wide_base + (iw - w);
-  if (!mine) return;
-  uint32_t a = s_c[lane];
-  for (uint32_t k = 0; k < c; ++k) {
-    Rec r;
-    if (decode_any(s_tile, &sr, a, img_end, td.delta, td.span_off, end_a, r) != CLG_OK) break;
-    const uint32_t so = (uint32_t)(td.span_off + (a - td.delta));
-    if (rec < out.cap) {
-      out.off[rec] = so;
-      out.tag[rec] = r.tag;
-      out.v0[rec] = r.v0;
-    }
-    if (r.wide) {
-      if (wide < out.wcap) {
-        out.w_idx[wide] = (uint32_t)rec;
-        out.w_rc[wide] = r.rc;
-        out.w_v1[wide] = r.v1;
-        out.w_var_off[wide] = r.var_off ? so + r.var_off : 0u;
-        out.w_var_len[wide] = r.var_len;
-        out.w_sub[wide] = r.sub;
-      }
-      ++wide;
-    }
-    ++rec;
-    a += r.L;
-  }
-}
-
-// ==================================================================================
 // Launchers.
 // ==================================================================================
 static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
@@ -1436,38 +656,6 @@ int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_dec_emit, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_tres,
                      d_sres, d_span_flags, out);
-  return ok(hipGetLastError());
-}
-
-int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv,
-                     uint32_t* d_dbg, void* stream) {
-  if (!n_tiles) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_conv, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_dbg);
-  return ok(hipGetLastError());
-}
-
-int launch_fast_count(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                      LaneSeg* d_lanes, TileSum* d_sums, void* stream) {
-  if (!n_tiles) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_count, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_lanes,
-                     d_sums);
-  return ok(hipGetLastError());
-}
-
-int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes,
-                        const TileSum* d_sums, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream) {
-  if (!n_spans) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_lanes,
-                     d_sums, d_fres, d_sres, d_span_flags);
-  return ok(hipGetLastError());
-}
-
-int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                     const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
-                     const uint32_t* d_span_flags, DecodeOut out, void* stream) {
-  if (!n_tiles) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_emit, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_lanes,
-                     d_fres, d_sres, d_span_flags, out);
   return ok(hipGetLastError());
 }
 
