@@ -12,37 +12,78 @@
 // decode error, an overflowing Serializable table) are flagged and re-decoded by the DP
 // pipeline in kernels.hip, which also reports exact error positions.
 //
-// Serializable records (tag 3) have no length prefix: their stream lengths come from a
-// per-tile table filled by k_jser_fill (the only kernel here that calls the out-of-line
-// grammar walker), so the hot kernels stay call-free.  k_fast_conv's first pass detects
-// tiles holding a "03 AC ED 00 05" pattern and defers them until the table exists.
+// Kernels:  k_fast_scan   stage tile -> points (BFS) -> filter -> segments -> chain
+//           k_jser_fill   Serializable stream lengths for deferred tiles (walker)
+//           k_fast_resolve  per span: tile entries/bases (regular: one scan)
+//           k_fast_emit   stage tile -> record starts into LDS by output index ->
+//                         decode + coalesced SoA stores
+// The hot kernels are call-free: Serializable lengths come from per-tile tables, and
+// tiles whose scan meets a "03 AC ED 00 05" pattern before the tables exist are deferred.
+//
+// LDS image: dense (byte a of the tile's aligned coordinates at LDS byte a), followed by
+// a halo of the span's next bytes.  Regions are 268 B = 67 dwords apart, an odd stride,
+// so lanes scanning their own regions in step hit 64 distinct banks.
 //
 // Record layouts: SimpleDeterminantEncoder.java:124-323 (reference flink-runtime).
 #include "dev_slow.h"
 
 namespace clg {
 
-constexpr int kFastRows = (kTile + kFastHalo) / kRegion + 1;
-constexpr int kFastImageDwords = kFastRows * kPitch;
-constexpr uint64_t kNoFar = ~0ull;
-constexpr int kMaxPops = 192;          // give up early: an unknown point only lengthens a segment
-constexpr int kMaxSegRecords = 1 << 15;
+constexpr uint32_t kScanHalo = 1024;  // covers the next tile's first kFNext regions + BFS overrun
+constexpr uint32_t kEmitHalo = 256;   // records crossing the tile end
+constexpr int kScanImgDwords = (kTile + kScanHalo + 64) / 4;
+constexpr int kEmitImgDwords = (kTile + kEmitHalo + 64) / 4;
+constexpr uint32_t kNoFar = 0xFFFFFFFFu;
+constexpr int kMaxPops = 96;          // give up early: an unknown point only lengthens a segment
+constexpr uint32_t kMaxSegRecords = 1u << 20;
 constexpr uint32_t kSerMagic = 0xACED0005u;
+constexpr int kLenRare = -2;          // lean_len: use the general path
+constexpr int kEmitCap = 3072;        // record starts staged per emit window
 
 // ---------------------------------------------------------------------------------
-// Per-tile context: LDS image + where everything else lives.
+// Dense LDS image accessors.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t d_u8(const uint32_t* T, uint32_t a) {
+  return reinterpret_cast<const uint8_t*>(T)[a];
+}
+__device__ __forceinline__ uint32_t d_be32(const uint32_t* T, uint32_t a) {
+  const uint32_t k = a >> 2;
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(T[k + 1], T[k], a & 3u));
+}
+__device__ __forceinline__ uint64_t d_be64(const uint32_t* T, uint32_t a) {
+  const uint32_t k = a >> 2, s = a & 3u;
+  const uint32_t d0 = T[k], d1 = T[k + 1], d2 = T[k + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, s), hi = __builtin_amdgcn_alignbyte(d2, d1, s);
+  return __builtin_bswap64((uint64_t)hi << 32 | lo);
+}
+struct DenseBytes {
+  const uint32_t* T;
+  uint32_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) const { return (int)d_u8(T, base + (uint32_t)k); }
+};
+__device__ __forceinline__ uint32_t fld_be32(const DenseBytes& b, uint32_t k) { return d_be32(b.T, b.base + k); }
+__device__ __forceinline__ uint64_t fld_be64(const DenseBytes& b, uint32_t k) { return d_be64(b.T, b.base + k); }
+
+// Region l of a tile with valid aligned coordinates [lo, hi).
+__device__ __forceinline__ void fregion(uint32_t lo, uint32_t hi, int l, uint32_t* rs, uint32_t* re) {
+  uint32_t s = (uint32_t)l * kFRegion;
+  uint32_t e = (l + 1 == kFOwn) ? (uint32_t)kTile : (uint32_t)(l + 1) * kFRegion;
+  *rs = s < lo ? lo : s;
+  *re = e > hi ? hi : e;
+}
+
+// ---------------------------------------------------------------------------------
+// Per-tile context.
 // ---------------------------------------------------------------------------------
 struct FastCtx {
   const uint32_t* T;  // LDS image
   uint32_t lo, hi, img_end;
-  uint64_t end_a;     // aligned coordinate of the span end
+  uint32_t end_a;     // aligned coordinate of the span end
   uint64_t so;        // span offset of coordinate lo
   const TileDesc* tiles;
   uint32_t t, t1;     // this tile, end of the span's tile range
-  const uint32_t* s_jpos;  // own Serializable table (LDS)
-  const uint32_t* s_jlen;
-  uint32_t s_jn;
-  JserTabs J;         // all tables (global)
+  uint32_t tables;    // Serializable tables exist (scan mode 1, emit)
+  JserTabs J;
 };
 
 // Span tile holding aligned coordinate a (a >= hi) and its local coordinate.
@@ -55,8 +96,8 @@ __device__ __forceinline__ uint32_t far_tile(const FastCtx& c, uint32_t a, uint3
 }
 
 __device__ __forceinline__ int fbyte(const FastCtx& c, uint32_t a) {
-  if (a < c.img_end) return t_u8(c.T, a);
-  if ((uint64_t)a >= c.end_a) return -1;
+  if (a < c.img_end) return (int)d_u8(c.T, a);
+  if (a >= c.end_a) return -1;
   uint32_t local;
   const uint32_t k = far_tile(c, a, &local);
   return c.tiles[k].abase[local];
@@ -71,17 +112,18 @@ __device__ __forceinline__ int64_t jfind(const uint32_t* pos, const uint32_t* le
   return (lo < n && pos[lo] == key) ? (int64_t)len[lo] : -1;
 }
 
-// Length of the Serializable record at a (magic already checked).
-__device__ __forceinline__ int64_t fser(const FastCtx& c, uint32_t a) {
-  int64_t j;
-  if (a < c.hi) {
-    j = jfind(c.s_jpos, c.s_jlen, c.s_jn, a);
-  } else {
-    uint32_t local;
-    const uint32_t k = far_tile(c, a, &local);
-    const uint32_t n = c.J.n[k];
-    j = jfind(c.J.pos + (uint64_t)k * kJserCap, c.J.len + (uint64_t)k * kJserCap, n < kJserCap ? n : kJserCap, local);
+// Length of the Serializable record at a (magic already checked): from the owning
+// tile's table; without tables the tile must be deferred.
+__device__ __forceinline__ int64_t fser_lookup(const FastCtx& c, uint32_t a, bool* defer) {
+  if (!c.tables) {
+    *defer = true;
+    return kLenErr;
   }
+  uint32_t k = c.t, local = a;
+  if (a >= c.hi) k = far_tile(c, a, &local);
+  const uint32_t n = c.J.n[k];
+  const int64_t j = jfind(c.J.pos + (uint64_t)k * kJserCap, c.J.len + (uint64_t)k * kJserCap,
+                          n < kJserCap ? n : kJserCap, local);
   if (j <= 0) return kLenErr;
   const int64_t L = 1 + j;
   return ((uint64_t)a + (uint64_t)L > c.end_a) ? kLenErr : L;
@@ -93,33 +135,64 @@ struct FarBytes {
   __device__ __forceinline__ int operator()(uint64_t k) const { return fbyte(*c, base + (uint32_t)k); }
 };
 
-// Record length at aligned coordinate a (< end_a); kLenErr for any decode error.
-__device__ __forceinline__ int64_t flen(const FastCtx& c, uint32_t a, int* tag) {
+// Lean length for the common case, branch-free: tag + the next 4 bytes from two LDS
+// dwords.  Tags 0,1,2,6,7 resolve here, as do bad tags and a 3 without the stream magic;
+// 4, 5, a magic-bearing 3 and anything near the image end return kLenRare.
+__device__ __forceinline__ int lean_len(const FastCtx& c, uint32_t a, int* tag) {
+  const bool in = a + 32u <= c.img_end;
+  const uint32_t ac = in ? a : 0u;
+  const uint32_t k = ac >> 2, sh = 8u * (ac & 3u);
+  const uint32_t d0 = c.T[k], d1 = c.T[k + 1];
+  const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);  // bytes a..a+3 (LE)
+  const uint32_t b4 = (d1 >> sh) & 0xFFu;                       // byte a+4
+  const uint32_t tg = x0 & 0xFFu;
+  *tag = (int)tg;
+  constexpr uint64_t lut = 2ull | 9ull << 4 | 5ull << 8 | 13ull << 24 | 5ull << 28;  // nibble per tag, 0 = special
+  const uint32_t L = (uint32_t)(lut >> (4u * (tg & 15u))) & 0xFu;
+  const bool magic = ((x0 >> 8) | (b4 << 24)) == 0x0500EDACu;  // LE of AC ED 00 05
+  const bool rare = !in || tg == 4u || tg == 5u || (tg == 3u && magic);
+  const bool err = tg > 7u || (tg == 3u && !magic) || a + L > c.end_a;
+  return rare ? kLenRare : (err ? (int)kLenErr : (int)L);
+}
+
+// General length (any tag, any position): kLenErr on any decode error.
+__device__ __forceinline__ int64_t full_len(const FastCtx& c, uint32_t a, int* tag, bool* defer) {
+  if (a >= c.end_a) return kLenErr;
   if (a + 27u < c.img_end) {
-    const int tg = t_u8(c.T, a);
+    DenseBytes b{c.T, a};
+    const int tg = b(0);
     *tag = tg;
-    const int64_t L = len_inline(c.T, tg, a, c.end_a);
-    return L == kLenSlow ? fser(c, a) : L;
+    const int64_t L = len_fields(b, tg, (uint64_t)(c.end_a - a));
+    if (L != kLenSlow) return L;
+    if (d_be32(c.T, a + 1) != kSerMagic) return kLenErr;
+    return fser_lookup(c, a, defer);
   }
   FarBytes b{&c, a};
   const int tg = b(0);
   *tag = tg;
-  const int64_t L = len_fields(b, tg, c.end_a - a);
+  const int64_t L = len_fields(b, tg, (uint64_t)(c.end_a - a));
   if (L != kLenSlow) return L;
   if (rd_be32(b, 1) != kSerMagic) return kLenErr;
-  return fser(c, a);
+  return fser_lookup(c, a, defer);
+}
+
+__device__ __forceinline__ int64_t flen(const FastCtx& c, uint32_t a, int* tag, bool* defer) {
+  const int L = lean_len(c, a, tag);
+  if (L != kLenRare) return L;
+  return full_len(c, a, tag, defer);
 }
 
 // Full record at a (a on the resolved path).
 __device__ __forceinline__ bool fdecode(const FastCtx& c, uint32_t a, Rec& r) {
   int tag;
-  const int64_t L = flen(c, a, &tag);
+  bool defer = false;
+  const int64_t L = flen(c, a, &tag, &defer);
   if (L <= 0) return false;
   r.tag = (uint8_t)tag;
   r.L = (uint32_t)L;
   r.wide = (uint8_t)is_wide(tag);
   if (a + 27u < c.img_end) {
-    LdsBytes b{c.T, a};
+    DenseBytes b{c.T, a};
     decode_fields(b, tag, L, r);
   } else {
     FarBytes b{&c, a};
@@ -128,59 +201,59 @@ __device__ __forceinline__ bool fdecode(const FastCtx& c, uint32_t a, Rec& r) {
   return true;
 }
 
-// Stage the tile plus up to kFastHalo bytes of the span that follow it.
-__device__ __forceinline__ uint32_t stage_fast(uint32_t* s_tile, const TileDesc& td, const TileDesc* tiles,
-                                               uint32_t t1, uint32_t t, uint64_t span_len, uint32_t lane) {
+// Stage the tile (dense) plus up to `halo` bytes of the span that follow it.
+__device__ __forceinline__ uint32_t stage_dense(uint32_t* T, const TileDesc& td, const TileDesc* tiles, uint32_t t1,
+                                                uint32_t t, uint64_t span_len, uint32_t halo_cap, uint32_t lane) {
   const uint32_t words = (td.delta + td.len + 15) >> 4;
-  for (uint32_t w = lane; w < words; w += 64) {
-    const uint4 v = *reinterpret_cast<const uint4*>(td.abase + 16 * w);
-    const uint32_t d = (w >> 4) * kPitch + ((w & 15u) << 2);
-    s_tile[d + 0] = v.x;
-    s_tile[d + 1] = v.y;
-    s_tile[d + 2] = v.z;
-    s_tile[d + 3] = v.w;
-  }
+  uint4* T4 = reinterpret_cast<uint4*>(T);
+  const uint4* src = reinterpret_cast<const uint4*>(td.abase);
+  for (uint32_t w = lane; w < words; w += 64) T4[w] = src[w];
   const uint32_t hi = td.delta + td.len;
   const uint64_t after = td.span_off + td.len;
   const uint64_t avail = span_len > after ? span_len - after : 0;
-  const uint32_t halo = (uint32_t)(avail < (uint64_t)kFastHalo ? avail : (uint64_t)kFastHalo);
-  __syncthreads();
+  const uint32_t halo = (uint32_t)(avail < (uint64_t)halo_cap ? avail : (uint64_t)halo_cap);
   if (halo) {
-    uint8_t* bb = reinterpret_cast<uint8_t*>(s_tile);
+    uint8_t* bb = reinterpret_cast<uint8_t*>(T);
     uint32_t k = t + 1, got = 0;  // the halo may span several (short) tiles
     while (got < halo && k < t1) {
       const TileDesc nt = tiles[k];
       const uint32_t take = nt.len < halo - got ? nt.len : halo - got;
       if (((hi + got) & 15u) == 0 && nt.delta == 0) {
-        for (uint32_t w = lane; w < (take + 15) / 16; w += 64) {
-          const uint4 v = *reinterpret_cast<const uint4*>(nt.abase + 16 * w);
-          const uint32_t a = hi + got + 16 * w;
-          const uint32_t d = (a >> 8) * kPitch + ((a >> 2) & 63u);
-          s_tile[d + 0] = v.x;
-          s_tile[d + 1] = v.y;
-          s_tile[d + 2] = v.z;
-          s_tile[d + 3] = v.w;
-        }
+        const uint4* ns = reinterpret_cast<const uint4*>(nt.abase);
+        uint4* dst = reinterpret_cast<uint4*>(bb + hi + got);
+        for (uint32_t w = lane; w < (take + 15) / 16; w += 64) dst[w] = ns[w];
       } else {
-        for (uint32_t i = lane; i < take; i += 64) {
-          const uint32_t a = hi + got + i;
-          bb[(a >> 8) * (kPitch * 4) + (a & 255u)] = nt.abase[nt.delta + i];
-        }
+        for (uint32_t i = lane; i < take; i += 64) bb[hi + got + i] = nt.abase[nt.delta + i];
       }
       got += take;
       ++k;
     }
-    __syncthreads();
   }
+  __syncthreads();
   return hi + halo;
 }
 
-// Serializable magic positions in [rs, re): count (and optionally list via callback).
+// Serializable magic patterns starting in [rs, re) (dense image).
+__device__ __forceinline__ uint32_t count_magic_dense(const uint32_t* T, uint32_t rs, uint32_t re) {
+  uint32_t n = 0;
+  for (uint32_t k = rs >> 2; k < (re + 3) >> 2; ++k) {
+    const uint32_t w = T[k] ^ 0x03030303u;
+    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;  // no 0x03 byte in this dword
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t a = 4 * k + i;
+      if (a < rs || a >= re) continue;
+      if (d_u8(T, a) == CLG_TAG_SERIALIZABLE && d_be32(T, a + 1) == kSerMagic) ++n;
+    }
+  }
+  return n;
+}
+
+// Same over the padded image of the DP pipeline (k_jser_fill).
 __device__ __forceinline__ uint32_t count_magic(const uint32_t* T, uint32_t rs, uint32_t re) {
   uint32_t n = 0;
   for (uint32_t k = rs >> 2; k < (re + 3) >> 2; ++k) {
     const uint32_t w = t_dw(T, k) ^ 0x03030303u;
-    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;  // no 0x03 byte in this dword
+    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
     for (uint32_t i = 0; i < 4; ++i) {
       const uint32_t a = 4 * k + i;
       if (a < rs || a >= re) continue;
@@ -193,135 +266,244 @@ __device__ __forceinline__ uint32_t count_magic(const uint32_t* T, uint32_t rs, 
 // ---------------------------------------------------------------------------------
 // Convergence (64-bit frontier BFS over candidate record starts).
 // ---------------------------------------------------------------------------------
-// Candidate starts whose tag byte is a valid tag (0..7): bit i <-> position rs + i.
-__device__ __forceinline__ uint64_t valid_tag_mask(const uint32_t* T, uint32_t rs, uint32_t ncand) {
+// Candidate starts in [rs, rs + n) whose byte is a valid tag (0..7): bit i <-> rs + i.
+__device__ __forceinline__ uint64_t cand_mask(const FastCtx& c, uint32_t rs, uint32_t n) {
   uint64_t m = 0;
-  const uint32_t k0 = rs >> 2, sh = rs & 3u;
-  for (uint32_t j = 0; j < 10; ++j) {  // 40 bytes cover 32 candidates at any alignment
-    const uint32_t y = t_dw(T, k0 + j) & 0xF8F8F8F8u;
-    const uint32_t z = (y - 0x01010101u) & ~y & 0x80808080u;  // exact: bytes of y are 0 or >= 8
-    const uint64_t bits = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-    m |= bits << (4 * j);
+  if (rs + 40u <= c.img_end) {
+    const uint32_t k0 = rs >> 2, sh = rs & 3u;
+    for (uint32_t j = 0; j < 9; ++j) {  // 36 bytes cover 32 candidates at any alignment
+      const uint32_t y = c.T[k0 + j] & 0xF8F8F8F8u;
+      const uint32_t z = (y - 0x01010101u) & ~y & 0x80808080u;  // exact: bytes of y are 0 or >= 8
+      const uint64_t bits = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+      m |= bits << (4 * j);
+    }
+    m >>= sh;
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      const int b = fbyte(c, rs + i);
+      if (b >= 0 && b <= 7) m |= 1ull << i;
+    }
   }
-  m >>= sh;
-  const uint64_t want = ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull);
-  return m & want;
+  return m & ((n >= 64) ? ~0ull : ((1ull << n) - 1ull));
 }
 
-__device__ uint32_t converge(const FastCtx& c, uint32_t rs, uint32_t ncand, uint32_t* pops) {
-  if (ncand == 0) return kConvUnknown;
-  uint64_t M = (rs + 40u + 4u < c.img_end) ? valid_tag_mask(c.T, rs, ncand)
-                                            : (ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull));
-  uint64_t W = rs;
-  uint64_t F = kNoFar;
-  bool sink = false;  // some candidate ended exactly at the span end
-  int npop = 0;
-  for (; npop < kMaxPops; ++npop) {
-    const int n = __popcll(M) + (F != kNoFar ? 1 : 0) + (sink ? 1 : 0);
-    if (n <= 1) {
-      *pops = (uint32_t)npop | ((uint32_t)n << 16);
-      if (n == 0) return kConvUnknown;
-      if (M) return (uint32_t)(W + (uint64_t)(__ffsll((long long)M) - 1));
-      if (F != kNoFar) return F > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)F;
-      return c.end_a > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)c.end_a;
+// Invariant inside the loop: the frontier's lowest position is W (bit 0 of M), so the
+// popped candidate is W itself and its successor lands at bit L.  F holds at most one
+// position >= W + 64; `sink` marks a path that ended exactly at the span end.  The common
+// path is straight-line (selects); only a rare record (or the image end) branches.
+__device__ uint32_t converge(const FastCtx& c, uint32_t rs, uint32_t ncand, uint32_t* pops, bool* defer) {
+  if (rs >= c.end_a) return kConvUnknown;
+  if (ncand > c.end_a - rs) ncand = c.end_a - rs;
+  uint64_t M = ncand ? cand_mask(c, rs, ncand) : 0;
+  if (M == 0) return kConvUnknown;
+  uint32_t W = rs + (uint32_t)__builtin_ctzll(M);
+  M >>= __builtin_ctzll(M);
+  uint32_t F = kNoFar;
+  bool sink = false;
+  uint32_t res = kConvUnknown;
+  int np = 0;
+  for (; np < kMaxPops; ++np) {
+    const bool m0 = M == 0, hasF = F != kNoFar;
+    // frontier empty apart from the far slot: jump the window there
+    W = m0 && hasF ? F : W;
+    M = m0 && hasF ? 1ull : M;
+    F = m0 ? kNoFar : F;
+    const bool dead = m0 && !hasF;                     // only the sink (or nothing) is left
+    const bool one = M == 1ull && F == kNoFar && !sink;  // a single live candidate: converged
+    if (dead || one) {
+      res = one ? W : (sink ? c.end_a : kConvUnknown);
+      break;
     }
-    if (M == 0) {  // only the far slot (and maybe the sink) left: jump the window
-      W = F;
-      M = 1;
-      F = kNoFar;
-      continue;
-    }
-    const int b = __ffsll((long long)M) - 1;
-    const uint64_t p = W + (uint64_t)b;
-    M &= M - 1;
-    if (p >= c.end_a) {
-      sink = true;
-    } else {
-      int tag;
-      const int64_t L = flen(c, (uint32_t)p, &tag);
-      if (L > 0) {
-        const uint64_t q = p + (uint64_t)L;
-        if (q < W + 64) {
-          M |= 1ull << (q - W);
-        } else if (F == kNoFar || F == q) {
-          F = q;
-        } else {
-          *pops = (uint32_t)npop | 0x80000000u;
-          return kConvUnknown;  // two candidates far ahead: not tracked
+    M ^= 1ull;  // pop W
+    const bool at_end = W >= c.end_a;
+    sink = sink || at_end;
+    int tag;
+    int L = lean_len(c, W, &tag);
+    L = at_end ? (int)kLenErr : L;
+    if (L == kLenRare) {
+      const int64_t LL = full_len(c, W, &tag, defer);
+      if (LL >= 64) {  // long record: its successor goes to the far slot
+        const uint32_t q = W + (uint32_t)LL;
+        if (F != kNoFar && F != q) {
+          np |= 0x4000;  // two far candidates: not tracked
+          break;
         }
+        F = q;
+        L = (int)kLenErr;
+      } else {
+        L = (int)LL;
       }
     }
-    if (M) {
-      const int s = __ffsll((long long)M) - 1;
-      if (s) {
-        M >>= s;
-        W += (uint64_t)s;
+    M |= L > 0 ? (1ull << (uint32_t)L) : 0ull;
+    const bool fm = F != kNoFar && F - W < 64u;
+    M |= fm ? (1ull << ((F - W) & 63u)) : 0ull;
+    F = fm ? kNoFar : F;
+    const uint32_t lo = (uint32_t)M, hi = (uint32_t)(M >> 32);
+    const uint32_t s = lo ? (uint32_t)__builtin_ctz(lo) : (hi ? 32u + (uint32_t)__builtin_ctz(hi) : 0u);
+    M >>= s;
+    W += s;
+  }
+  *pops = (uint32_t)np;
+  return res;
+}
+
+// ---------------------------------------------------------------------------------
+// Segments between kept points.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ int next_kept(const uint32_t* s_c, int from) {
+  while (from < kFPoints && s_c[from] == kConvUnknown) ++from;
+  return from;
+}
+
+// Parse from point l until landing exactly on a later kept point (jumping over a point
+// means it is off the path: aim at the next one).
+__device__ LaneSeg parse_segment(const FastCtx& c, const uint32_t* s_c, int l, bool* defer) {
+  LaneSeg seg{kEndFail, 0, 0, 0, 0};
+  const uint32_t c0 = s_c[l];
+  if (c0 == kConvUnknown) return seg;
+  uint32_t pos = c0, cnt = 0, w = 0;
+  int m = next_kept(s_c, l + 1);
+  uint32_t target = m < kFPoints ? s_c[m] : kConvUnknown;
+  for (uint32_t it = 0; it < kMaxSegRecords; ++it) {
+    if (target < pos) {
+      while (target < pos) {
+        m = next_kept(s_c, m + 1);
+        target = m < kFPoints ? s_c[m] : kConvUnknown;
       }
     }
-    if (F != kNoFar && F < W + 64) {
-      M |= 1ull << (F - W);
-      F = kNoFar;
+    int tag;
+    int L = lean_len(c, pos, &tag);
+    if (L == kLenRare) {
+      const int64_t LL = full_len(c, pos, &tag, defer);
+      L = LL > 0x7FFFFFF0ll ? (int)kLenErr : (int)LL;
     }
+    const bool hit = target == pos;
+    if (hit || L <= 0 || m >= kFPoints) {
+      if (hit) {
+        seg.end = (uint8_t)m;
+        seg.cnt = cnt;
+        seg.wcnt = w;
+      }
+      return seg;
+    }
+    ++cnt;
+    w += is_wide(tag);
+    pos += (uint32_t)L;
   }
-  *pops = (uint32_t)npop;
-  return kConvUnknown;
+  return seg;
 }
 
-__device__ __forceinline__ void load_jtab(uint32_t* s_jpos, uint32_t* s_jlen, uint32_t* s_jn, const JserTabs& J,
-                                          uint32_t t, uint32_t lane) {
-  const uint32_t n = J.n[t];
-  const uint32_t m = n < kJserCap ? n : kJserCap;
-  for (uint32_t i = lane; i < m; i += 64) {
-    s_jpos[i] = J.pos[(uint64_t)t * kJserCap + i];
-    s_jlen[i] = J.len[(uint64_t)t * kJserCap + i];
+// Kept points: known, inside the tile they belong to ([.., bound)), and above every
+// earlier kept point of the same tile (a running maximum, so the rule needs no later
+// points and the previous tile evaluates the next tile's first points exactly as it does).
+__device__ __forceinline__ uint32_t keep_points(uint32_t pt, uint32_t bound, uint32_t lane) {
+  const uint32_t v = (pt != kConvUnknown && pt < bound) ? pt : kConvUnknown;
+  uint32_t key = v == kConvUnknown ? 0u : v + 1u;
+  const uint32_t seg0 = lane < (uint32_t)kFOwn ? 0u : (uint32_t)kFOwn;
+  uint32_t incl = key;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if (lane >= seg0 + (uint32_t)off) incl = incl > y ? incl : y;
   }
-  if (lane == 0) *s_jn = m;
+  uint32_t excl = __shfl_up(incl, 1);
+  if (lane == seg0) excl = 0;
+  return (v != kConvUnknown && key > excl) ? v : kConvUnknown;
 }
 
-// ---- pass F1: convergence points (mode 0: every tile, tiles with Serializable
-// records are deferred; mode 1: the deferred tiles, tables filled) -----------------------
-__global__ __launch_bounds__(64) void k_fast_conv(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+// ---- pass F1: fused scan --------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   uint32_t* __restrict__ conv, JserTabs J, uint32_t mode,
+                                                  LaneSeg* __restrict__ lanes, TileSum* __restrict__ sums,
                                                   uint32_t* __restrict__ dbg) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  __shared__ uint32_t s_jpos[kJserCap], s_jlen[kJserCap];
-  __shared__ uint32_t s_jn;
+  __shared__ uint32_t s_img[kScanImgDwords];
+  __shared__ uint32_t s_c[kFPoints];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   if (mode == 1 && !J.defer[t]) return;
   const TileDesc td = tiles[t];
   const SpanDesc sd = spans[td.span];
   const uint32_t t1 = sd.first_tile + sd.n_tiles;
-  if (mode == 1) {
-    load_jtab(s_jpos, s_jlen, &s_jn, J, t, lane);
-  } else if (lane == 0) {
-    s_jn = 0;
-  }
-  const uint32_t img_end = stage_fast(s_tile, td, tiles, t1, t, sd.len, lane);
-  const TileGeom g{td.delta, td.delta + td.len};
-  const uint32_t rs = g.rs((int)lane), re = g.re((int)lane);
+  const bool last = t + 1 == t1;
+  const uint32_t hi = td.delta + td.len;
+  const uint64_t ea = sd.len - td.span_off + td.delta;
+  const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
+  const uint32_t img_end = stage_dense(s_img, td, tiles, t1, t, sd.len, kScanHalo, lane);
+  uint32_t rs = 0, re = 0;
+  if (lane < (uint32_t)kFOwn) fregion(td.delta, hi, (int)lane, &rs, &re);
   if (mode == 0) {
-    const uint32_t nm = re > rs ? count_magic(s_tile, rs, re) : 0u;
+    const uint32_t nm = re > rs ? count_magic_dense(s_img, rs, re) : 0u;
     if (__any(nm != 0)) {  // Serializable records here: wait for the stream-length table
       if (lane == 0) J.defer[t] = 1;
       return;
     }
-    if (lane == 0) {
-      J.defer[t] = 0;
-      J.n[t] = 0;
+  }
+  const FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J};
+  bool defer = false;
+
+  // ---- convergence points: own regions, then the next tile's first kFNext regions
+  uint32_t pt = kConvUnknown, pops = 0, bound = hi;
+  if (lane < (uint32_t)kFOwn) {
+    if (lane == 0 && t == sd.first_tile) pt = td.delta;  // a span starts on a record boundary
+    else if (re > rs) pt = converge(c, rs, re - rs < (uint32_t)kCands ? re - rs : (uint32_t)kCands, &pops, &defer);
+  } else if (!last) {
+    const TileDesc nd = tiles[t + 1];
+    uint32_t nrs, nre;
+    fregion(nd.delta, nd.delta + nd.len, (int)lane - kFOwn, &nrs, &nre);
+    bound = hi + nd.len;
+    if (nre > nrs) {
+      const uint32_t a = hi + (nrs - nd.delta), n = nre - nrs;
+      pt = converge(c, a, n < (uint32_t)kCands ? n : (uint32_t)kCands, &pops, &defer);
     }
+  } else if (lane == (uint32_t)kFOwn) {
+    pt = end_a;  // the span end closes the last tile
+    bound = end_a + 1;
   }
-  const FastCtx c{s_tile, td.delta, td.delta + td.len, img_end, sd.len - td.span_off + td.delta, td.span_off, tiles,
-                  t, t1, s_jpos, s_jlen, s_jn, J};
-  uint32_t pt, pops = 0;
-  if (lane == 0 && t == sd.first_tile) {
-    pt = td.delta;  // a span starts on a record boundary
-  } else {
-    const uint32_t RL = re > rs ? re - rs : 0;
-    pt = converge(c, rs, RL < (uint32_t)kCands ? RL : (uint32_t)kCands, &pops);
+  if (mode == 0 && __any(defer)) {
+    if (lane == 0) J.defer[t] = 1;
+    return;
   }
-  conv[(uint64_t)t * kRegions + lane] = pt;
-  if (dbg) dbg[(uint64_t)t * kRegions + lane] = pops;
+  const uint32_t kept = keep_points(pt, bound, lane);
+  s_c[lane] = kept;
+  conv[(uint64_t)t * kFPoints + lane] = kept;
+  if (dbg) dbg[(uint64_t)t * kFPoints + lane] = pops | (pt == kConvUnknown ? 0x80000000u : 0u);
+  __syncthreads();
+
+  // ---- segments and the chain from the first kept point
+  LaneSeg seg{kEndFail, 0, 0, 0, 0};
+  if (lane < (uint32_t)kFOwn) seg = parse_segment(c, s_c, (int)lane, &defer);
+  if (mode == 0 && __any(defer)) {
+    if (lane == 0) J.defer[t] = 1;
+    return;
+  }
+  if (mode == 0 && lane == 0) {
+    J.defer[t] = 0;
+    J.n[t] = 0;
+  }
+  lanes[(uint64_t)t * kFPoints + lane] = seg;
+  const uint64_t own_kept = __ballot(lane < (uint32_t)kFOwn && kept != kConvUnknown);
+  const int f = own_kept ? __builtin_ctzll(own_kept) : kFPoints;
+  const uint32_t g_end = seg.end, g_cnt = seg.cnt, g_w = seg.wcnt;
+  uint64_t valid = 0;
+  uint32_t cnt = 0, w = 0;
+  int v = f;
+  while (v < kFOwn) {
+    const uint32_t e = __builtin_amdgcn_readlane(g_end, v);
+    if (e == kEndFail) break;
+    valid |= 1ull << v;
+    cnt += __builtin_amdgcn_readlane(g_cnt, v);
+    w += __builtin_amdgcn_readlane(g_w, v);
+    v = (int)e;
+  }
+  if (lane == 0) {
+    TileSum sm{};
+    sm.f = f < kFOwn ? (uint8_t)f : kEndFail;
+    sm.x = (v >= kFOwn && v < kFPoints) ? (uint8_t)(v - kFOwn) : kEndFail;
+    sm.cnt = cnt;
+    sm.wcnt = w;
+    sm.valid = valid;
+    sums[t] = sm;
+  }
 }
 
 // ---- Serializable stream-length tables for deferred tiles --------------------------------
@@ -359,160 +541,25 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   }
 }
 
-// ---- pass F2: segment counts -----------------------------------------------------------
-__device__ __forceinline__ int next_known(const uint32_t* s_c, int from) {
-  while (from < 2 * kRegions && s_c[from] == kConvUnknown) ++from;
-  return from;
-}
-
-// Points of this tile (0..63) and of the span's next tile (64..127) in this tile's
-// aligned coordinates; for the span's last tile the span end is point 64.  Both halves
-// are then made monotonic by dropping points that lie beyond a later point (a dropped
-// point only means a longer segment for the lane before it).  The next tile's half is
-// filtered on its own, exactly as that tile filters it, so both tiles agree on where
-// the chain crosses the boundary; this tile's half is filtered against everything after.
-__device__ __forceinline__ void load_points(uint32_t* s_c, const uint32_t* conv, const TileDesc* tiles,
-                                            const TileDesc& td, const SpanDesc& sd, uint32_t t, uint32_t lane,
-                                            uint64_t end_a) {
-  const uint32_t own0 = conv[(uint64_t)t * kRegions + lane];
-  s_c[lane] = own0;
-  const bool last = t + 1 == sd.first_tile + sd.n_tiles;
-  uint32_t x = kConvUnknown;
-  if (!last) {
-    const uint32_t c = conv[(uint64_t)(t + 1) * kRegions + lane];
-    if (c != kConvUnknown) {
-      const uint64_t v = (uint64_t)(td.delta + td.len) + (uint64_t)(c - tiles[t + 1].delta);
-      x = v > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)v;
-    }
-  } else if (lane == 0) {
-    x = end_a > 0xFFFFFFF0ull ? kConvUnknown : (uint32_t)end_a;
-  }
-  // suffix minima over the known points (both halves in registers, wave-uniform loop)
-  uint32_t own = s_c[lane];
-  uint32_t lim = kConvUnknown;
-  uint32_t keep_next = x;
-  for (int l = kRegions - 1; l >= 0; --l) {  // next tile's half, filtered on its own
-    const uint32_t c = __builtin_amdgcn_readlane(x, l);
-    if (c == kConvUnknown) continue;
-    if (c > lim) {
-      if ((int)lane == l) keep_next = kConvUnknown;
-    } else {
-      lim = c;
-    }
-  }
-  uint32_t keep_own = own;
-  for (int l = kRegions - 1; l >= 0; --l) {  // this tile's half, filtered against everything after
-    const uint32_t c = __builtin_amdgcn_readlane(own, l);
-    if (c == kConvUnknown) continue;
-    if (c > lim) {
-      if ((int)lane == l) keep_own = kConvUnknown;
-    } else {
-      lim = c;
-    }
-  }
-  s_c[lane] = keep_own;
-  s_c[kRegions + lane] = keep_next;
-  __syncthreads();
-}
-
-// Parse from point l until landing exactly on a later known point.
-__device__ LaneSeg parse_segment(const FastCtx& c, const uint32_t* s_c, int l) {
-  LaneSeg seg{kEndFail, 0, 0, 0, 0};
-  const uint32_t c0 = s_c[l];
-  if (c0 == kConvUnknown) return seg;
-  uint32_t pos = c0, cnt = 0, w = 0;
-  int m = next_known(s_c, l + 1);
-  uint32_t target = m < 2 * kRegions ? s_c[m] : kConvUnknown;
-  for (int it = 0; it < kMaxSegRecords; ++it) {
-    while (target < pos) {  // jumped over a point: aim at the next one
-      m = next_known(s_c, m + 1);
-      target = m < 2 * kRegions ? s_c[m] : kConvUnknown;
-    }
-    if (m >= 2 * kRegions) return seg;
-    if (target == pos) {
-      seg.end = (uint8_t)m;
-      seg.cnt = (uint16_t)cnt;
-      seg.wcnt = (uint16_t)w;
-      return seg;
-    }
-    if ((uint64_t)pos >= c.end_a) return seg;
-    int tag;
-    const int64_t L = flen(c, pos, &tag);
-    if (L <= 0 || (uint64_t)pos + (uint64_t)L > 0xFFFFFFF0ull) return seg;
-    ++cnt;
-    w += is_wide(tag);
-    pos += (uint32_t)L;
-  }
-  return seg;
-}
-
-__global__ __launch_bounds__(64) void k_fast_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                   const uint32_t* __restrict__ conv, JserTabs J,
-                                                   LaneSeg* __restrict__ lanes, TileSum* __restrict__ sums) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  __shared__ uint32_t s_c[2 * kRegions];
-  __shared__ uint32_t s_jpos[kJserCap], s_jlen[kJserCap];
-  __shared__ uint32_t s_jn;
-  const uint32_t t = blockIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const TileDesc td = tiles[t];
-  const SpanDesc sd = spans[td.span];
-  const uint32_t t1 = sd.first_tile + sd.n_tiles;
-  const uint64_t end_a = sd.len - td.span_off + td.delta;
-  load_jtab(s_jpos, s_jlen, &s_jn, J, t, lane);
-  load_points(s_c, conv, tiles, td, sd, t, lane, end_a);
-  const uint32_t img_end = stage_fast(s_tile, td, tiles, t1, t, sd.len, lane);
-  const FastCtx c{s_tile, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, s_jpos, s_jlen,
-                  s_jn, J};
-
-  const LaneSeg seg = parse_segment(c, s_c, (int)lane);
-  lanes[(uint64_t)t * kRegions + lane] = seg;
-  // chain of segments from the first known point (wave-uniform walk over registers)
-  const uint32_t packed = (uint32_t)seg.end | ((uint32_t)seg.cnt << 8) | ((uint32_t)seg.wcnt << 20);
-  const uint64_t known = __ballot(s_c[lane] != kConvUnknown);
-  const int f = known ? __builtin_ctzll(known) : kRegions;
-  uint64_t valid = 0;
-  uint32_t cnt = 0, w = 0;
-  int v = f;
-  while (v < kRegions) {
-    const uint32_t g = __builtin_amdgcn_readlane(packed, v);
-    const uint32_t end = g & 0xFF;
-    if (end == kEndFail) break;
-    valid |= 1ull << v;
-    cnt += (g >> 8) & 0xFFF;
-    w += g >> 20;
-    v = (int)end;
-  }
-  if (lane == 0) {
-    TileSum sm{};
-    sm.f = (uint8_t)f;
-    sm.x = (v >= kRegions && v < 2 * kRegions) ? (uint8_t)(v - kRegions) : kEndFail;
-    sm.cnt = cnt;
-    sm.wcnt = w;
-    sm.valid = valid;
-    sums[t] = sm;
-  }
-}
-
-// ---- pass F3: per-span resolution ------------------------------------------------------
+// ---- pass F2: per-span resolution ------------------------------------------------------
 __device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* valid, uint32_t* cnt, uint32_t* wcnt,
                            int* exit_idx) {
   uint64_t vm = 0;
   uint32_t c = 0, w = 0;
   int v = e;
-  while (v < kRegions) {
-    const LaneSeg gs = lanes[(uint64_t)t * kRegions + v];
+  while (v < kFOwn) {
+    const LaneSeg gs = lanes[(uint64_t)t * kFPoints + v];
     if (gs.end == kEndFail) return false;
     vm |= 1ull << v;
     c += gs.cnt;
     w += gs.wcnt;
     v = gs.end;
   }
-  if (v >= 2 * kRegions) return false;
+  if (v >= kFPoints) return false;
   *valid = vm;
   *cnt = c;
   *wcnt = w;
-  *exit_idx = v - kRegions;
+  *exit_idx = v - kFOwn;
   return true;
 }
 
@@ -532,12 +579,13 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict
     s_carry_w = 0;
   }
   __syncthreads();
-  // regular: every tile's entry point is its first known point (0 for the first tile)
-  // and the previous tile's chain lands on it; the last tile lands on the span end.
+  // regular: every tile's entry is its first kept point (point 0 for the span's first
+  // tile), the previous tile's chain lands on exactly that point, and the last tile's
+  // chain lands on the span end (its point kFOwn + 0).
   for (uint32_t i = threadIdx.x; i < sd.n_tiles; i += blockDim.x) {
     const uint32_t t = sd.first_tile + i;
     const TileSum sm = sums[t];
-    bool bad = sm.x == kEndFail || sm.f >= kRegions;
+    bool bad = sm.x == kEndFail || sm.f == kEndFail;
     if (i == 0) bad |= sm.f != 0;
     else bad |= sums[t - 1].x != sm.f;
     if (i + 1 == sd.n_tiles) bad |= sm.x != 0;
@@ -585,7 +633,7 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict
     }
     return;
   }
-  // irregular: serial walk with per-lane chains; give up to the DP pipeline on a break
+  // irregular: serial walk over the per-lane chains; a break goes to the DP pipeline
   if (threadIdx.x == 0) {
     uint64_t rec = 0, wide = 0;
     int e = 0;
@@ -615,16 +663,17 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict
   }
 }
 
-// ---- pass F4: emit ---------------------------------------------------------------------
+// ---- pass F3: emit ---------------------------------------------------------------------
+// Phase A: each chain lane walks its segment and drops every record start (u16 image
+// coordinate) at its output index in LDS.  Phase B: lane i decodes the i-th record of the
+// window, so every SoA store of the wave covers consecutive output elements.
 __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   const uint32_t* __restrict__ conv, JserTabs J,
                                                   const LaneSeg* __restrict__ lanes, const FastRes* __restrict__ fres,
                                                   const SpanRes* __restrict__ sres, const uint32_t* __restrict__ span_flags,
                                                   DecodeOut out) {
-  __shared__ uint32_t s_tile[kFastImageDwords];
-  __shared__ uint32_t s_c[2 * kRegions];
-  __shared__ uint32_t s_jpos[kJserCap], s_jlen[kJserCap];
-  __shared__ uint32_t s_jn;
+  __shared__ uint32_t s_img[kEmitImgDwords];
+  __shared__ uint16_t s_pos[kEmitCap];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const TileDesc td = tiles[t];
@@ -634,51 +683,93 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
   const SpanDesc sd = spans[td.span];
   const SpanRes sp = sres[td.span];
   const uint32_t t1 = sd.first_tile + sd.n_tiles;
-  const uint64_t end_a = sd.len - td.span_off + td.delta;
-  load_jtab(s_jpos, s_jlen, &s_jn, J, t, lane);
-  load_points(s_c, conv, tiles, td, sd, t, lane, end_a);
-  const uint32_t img_end = stage_fast(s_tile, td, tiles, t1, t, sd.len, lane);
-  const FastCtx c{s_tile, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, s_jpos, s_jlen,
-                  s_jn, J};
-
+  const uint64_t ea = sd.len - td.span_off + td.delta;
+  const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   const bool mine = (fr.valid >> lane) & 1ull;
-  const LaneSeg seg = lanes[(uint64_t)t * kRegions + lane];
-  const uint32_t cn = mine ? seg.cnt : 0u, wn = mine ? seg.wcnt : 0u;
-  uint32_t ic = cn, iw = wn;
+  const LaneSeg seg = lanes[(uint64_t)t * kFPoints + lane];
+  uint32_t pos = conv[(uint64_t)t * kFPoints + lane];
+  const uint32_t img_end = stage_dense(s_img, td, tiles, t1, t, sd.len, kEmitHalo, lane);
+  const FastCtx c{s_img, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, 1u, J};
+
+  const uint32_t cn = mine ? seg.cnt : 0u;
+  uint32_t ic = cn;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t yc = __shfl_up(ic, off), yw = __shfl_up(iw, off);
-    if ((int)lane >= off) {
-      ic += yc;
-      iw += yw;
-    }
+    const uint32_t y = __shfl_up(ic, off);
+    if ((int)lane >= off) ic += y;
   }
-  uint64_t rec = sp.rec_base + fr.rec_base + (ic - cn);
-  uint64_t wide = sp.wide_base + fr.wide_base + (iw - wn);
-  if (!mine) return;
-  uint32_t a = s_c[lane];
-  for (uint32_t k = 0; k < cn; ++k) {
-    Rec r;
-    if (!fdecode(c, a, r)) break;
-    const uint32_t so = (uint32_t)(td.span_off + (a - td.delta));
-    if (rec < out.cap) {
-      out.off[rec] = so;
-      out.tag[rec] = r.tag;
-      out.v0[rec] = r.v0;
-    }
-    if (r.wide) {
-      if (wide < out.wcap) {
-        out.w_idx[wide] = (uint32_t)rec;
-        out.w_rc[wide] = r.rc;
-        out.w_v1[wide] = r.v1;
-        out.w_var_off[wide] = r.var_off ? so + r.var_off : 0u;
-        out.w_var_len[wide] = r.var_len;
-        out.w_sub[wide] = r.sub;
+  const uint32_t total = __shfl(ic, 63);
+  uint32_t idx = ic - cn, k = 0;
+  const uint64_t rec0 = sp.rec_base + fr.rec_base;
+  uint64_t wide = sp.wide_base + fr.wide_base;
+  for (uint32_t w0 = 0; w0 < total; w0 += kEmitCap) {
+    const uint32_t wend = w0 + kEmitCap;
+    while (k < cn && idx < wend) {  // phase A
+      s_pos[idx - w0] = (uint16_t)pos;
+      int tag;
+      int L = lean_len(c, pos, &tag);
+      if (L == kLenRare) {
+        bool defer = false;
+        const int64_t LL = full_len(c, pos, &tag, &defer);
+        L = LL > 0x7FFFFFF0ll ? (int)kLenErr : (int)LL;
       }
-      ++wide;
+      pos += L > 0 ? (uint32_t)L : 1u;
+      ++k;
+      ++idx;
     }
-    ++rec;
-    a += r.L;
+    __syncthreads();
+    const uint32_t nw = total - w0 < (uint32_t)kEmitCap ? total - w0 : (uint32_t)kEmitCap;
+    for (uint32_t i0 = 0; i0 < nw; i0 += 64) {  // phase B
+      const uint32_t i = i0 + lane;
+      const bool act = i < nw;
+      const uint32_t a = act ? (uint32_t)s_pos[i] : td.delta;
+      // narrow records (Order / Timestamp / RNG / BufferBuilt) straight from 3 dwords
+      const bool in = a + 16u <= img_end;
+      const uint32_t ac = in ? a : 0u;
+      const uint32_t kk = ac >> 2, sh = 8u * (ac & 3u);
+      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
+      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
+      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+      uint32_t tg = x0 & 0xFFu;
+      const uint32_t lo = (x0 >> 8) | (x1 << 24), hi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
+      int64_t v0 = tg == CLG_TAG_ORDER ? (int64_t)(int8_t)(lo & 0xFFu)
+                 : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)hi << 32 | lo)
+                                           : (int64_t)(int32_t)__builtin_bswap32(lo);
+      const bool narrow = in && (tg <= 2u || tg == 7u) && tg != CLG_TAG_SERIALIZABLE;
+      Rec r{};
+      bool wide_rec = false;
+      if (act && !narrow) {  // wide or near the image end: the general decoder
+        if (fdecode(c, a, r)) {
+          tg = r.tag;
+          v0 = r.v0;
+          wide_rec = r.wide;
+        }
+      }
+      const uint64_t wm = __ballot(act && wide_rec);
+      const uint64_t g = rec0 + w0 + i;
+      if (act) {
+        const uint32_t so = (uint32_t)(td.span_off + (a - td.delta));
+        if (g < out.cap) {
+          out.off[g] = so;
+          out.tag[g] = (uint8_t)tg;
+          out.v0[g] = v0;
+        }
+        if (wide_rec) {
+          const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+          if (wi < out.wcap) {
+            out.w_idx[wi] = (uint32_t)g;
+            out.w_rc[wi] = r.rc;
+            out.w_v1[wi] = r.v1;
+            out.w_var_off[wi] = r.var_off ? so + r.var_off : 0u;
+            out.w_var_len[wi] = r.var_len;
+            out.w_sub[wi] = r.sub;
+          }
+        }
+      }
+      wide += (uint64_t)__popcll(wm);
+    }
+    __syncthreads();
   }
 }
 
@@ -687,25 +778,17 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
 // ---------------------------------------------------------------------------------
 static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
 
-int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
-                     uint32_t mode, uint32_t* d_dbg, void* stream) {
+int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
+                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, void* stream) {
   if (!n_tiles) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_conv, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, J, mode,
-                     d_dbg);
+  hipLaunchKernelGGL(k_fast_scan, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, J, mode,
+                     d_lanes, d_sums, d_dbg);
   return ok(hipGetLastError());
 }
 
 int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream) {
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_jser_fill, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, J);
-  return ok(hipGetLastError());
-}
-
-int launch_fast_count(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                      JserTabs J, LaneSeg* d_lanes, TileSum* d_sums, void* stream) {
-  if (!n_tiles) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_count, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, J,
-                     d_lanes, d_sums);
   return ok(hipGetLastError());
 }
 

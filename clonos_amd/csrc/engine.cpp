@@ -557,8 +557,8 @@ struct clg_engine {
     CHK(d_tres.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileRes)));
     CHK(d_sres.ensure(ns * sizeof(clg::SpanRes)));
     CHK(d_totals.ensure(2 * sizeof(uint64_t)));
-    CHK(d_fconv.ensure(std::max<size_t>(1, nt) * clg::kRegions * sizeof(uint32_t)));
-    CHK(d_lanes.ensure(std::max<size_t>(1, nt) * clg::kRegions * sizeof(clg::LaneSeg)));
+    CHK(d_fconv.ensure(std::max<size_t>(1, nt) * clg::kFPoints * sizeof(uint32_t)));
+    CHK(d_lanes.ensure(std::max<size_t>(1, nt) * clg::kFPoints * sizeof(clg::LaneSeg)));
     CHK(d_sums.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileSum)));
     CHK(d_fres.ensure(std::max<size_t>(1, nt) * sizeof(clg::FastRes)));
     CHK(d_flags.ensure(ns * sizeof(uint32_t)));
@@ -599,21 +599,19 @@ struct clg_engine {
     auto* dt = d_tiles.as<clg::TileDesc>();
     auto* ds = d_spans.as<clg::SpanDesc>();
     auto* flags = d_flags.as<uint32_t>();
-    // fast path: convergence points -> segment counts -> per-span resolution
+    // fast path: fused scan (points + segments) -> per-span resolution -> emit
     const clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>()};
     uint32_t* dbg = nullptr;
-    if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kRegions * 4) == CLG_OK)
+    if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kFPoints * 4) == CLG_OK)
       dbg = d_dbg.as<uint32_t>();
-    CHK(timed("decode_conv", log_bytes, [&] {
-      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), J, 0, dbg, stream);
+    CHK(timed("decode_scan", log_bytes, [&] {
+      return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 0, d_lanes.as<clg::LaneSeg>(),
+                                   d_sums.as<clg::TileSum>(), dbg, stream);
     }));
     CHK(timed("decode_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
-    CHK(timed("decode_conv_deferred", 0, [&] {
-      return clg::launch_fast_conv(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, dbg, stream);
-    }));
-    CHK(timed("decode_count", log_bytes, [&] {
-      return clg::launch_fast_count(dt, nt, ds, d_fconv.as<uint32_t>(), J, d_lanes.as<clg::LaneSeg>(),
-                                    d_sums.as<clg::TileSum>(), stream);
+    CHK(timed("decode_scan_deferred", 0, [&] {
+      return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, d_lanes.as<clg::LaneSeg>(),
+                                   d_sums.as<clg::TileSum>(), dbg, stream);
     }));
     CHK(timed("decode_resolve", uint64_t(nt) * 32, [&] {
       return clg::launch_fast_resolve(ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
@@ -646,7 +644,7 @@ struct clg_engine {
                                      d_sres.as<clg::SpanRes>(), flags, o, stream);
     }));
     if (const char* dump = getenv("CLONOS_DEBUG_DUMP")) {  // developer diagnostics only
-      std::vector<uint32_t> hc(size_t(nt) * clg::kRegions), hf(ns);
+      std::vector<uint32_t> hc(size_t(nt) * clg::kFPoints), hf(ns);
       std::vector<clg::TileSum> hs(nt);
       hipMemcpyAsync(hc.data(), d_fconv.p, hc.size() * 4, hipMemcpyDeviceToHost, stream);
       hipMemcpyAsync(hs.data(), d_sums.p, hs.size() * sizeof(clg::TileSum), hipMemcpyDeviceToHost, stream);
@@ -659,7 +657,7 @@ struct clg_engine {
         fwrite(hs.data(), sizeof(clg::TileSum), hs.size(), fp);
         fwrite(hf.data(), 4, hf.size(), fp);
         fwrite(p.tiles.data(), sizeof(clg::TileDesc), nt, fp);
-        std::vector<uint32_t> hd(size_t(nt) * clg::kRegions);
+        std::vector<uint32_t> hd(size_t(nt) * clg::kFPoints);
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
         fwrite(hd.data(), 4, hd.size(), fp);
         fclose(fp);

@@ -87,32 +87,41 @@ struct DecodeOut {
   uint64_t wcap;
 };
 
-// ---- fast decode: convergence points -----------------------------------------------
-// conv[t][l] = aligned coordinate (tile t) of region l's convergence point: the first
-// position that every live candidate parse from the region's first kEntries offsets
-// passes through; kConvUnknown if the candidates did not converge.
+// ---- fast decode: convergence points (decode_fast.hip) ----------------------------
+// Fast-pipeline geometry: a tile's aligned coordinates [0, kTile) are split into kFOwn
+// regions of kFRegion bytes (the last one takes the remainder).  Lane l < kFOwn owns
+// region l; lanes kFOwn..63 compute the points of the span's NEXT tile's first kFNext
+// regions (the same deterministic function that tile evaluates for itself), so a tile
+// knows where its last segment must land without waiting for its neighbour.
+constexpr uint32_t kFRegion = 268;  // 67 dwords: odd, so lane-strided LDS scans are conflict-free
+constexpr int kFOwn = 61;
+constexpr int kFNext = 3;
+constexpr int kFPoints = kFOwn + kFNext;  // 64 = one wave
+//
+// conv[t * 64 + l] = aligned coordinate (tile t) of point l after filtering: a point is
+// kept iff its candidates converged, it lies inside its tile, and it exceeds every earlier
+// kept point of the same tile; kConvUnknown otherwise.
 constexpr uint32_t kConvUnknown = 0xFFFFFFFFu;
-constexpr int kFastHalo = 512;  // bytes of the span's next tile staged after a tile
 
-// Per-lane segment [conv[l], conv[end]) parsed by k_fast_count.  end in 1..127 indexes
-// this tile's points (< 64) or the next tile's (>= 64); kEndFail = parse failed/anomaly.
+// Per-lane segment [conv[l], conv[end]) parsed by k_fast_scan.  end in l+1..63 (>= kFOwn:
+// a point of the next tile); kEndFail = parse failed or no point reached.
 struct LaneSeg {
   uint8_t end;
   uint8_t flags;
-  uint16_t cnt;
-  uint16_t wcnt;
   uint16_t pad;
+  uint32_t cnt;
+  uint32_t wcnt;
 };
 constexpr uint8_t kEndFail = 0xFF;
 
-// Tile summary assuming the tile's entry is its first known point f.
+// Tile summary assuming the tile's entry is its first kept point f.
 struct TileSum {
   uint32_t cnt, wcnt;
-  uint8_t f;      // first known point index (entry assumed)
-  uint8_t x;      // exit: index of the next tile's point the chain lands on; kEndFail = anomaly
+  uint8_t f;      // first kept own point (kEndFail: none)
+  uint8_t x;      // exit: next tile's point index (0..kFNext-1) the chain lands on; kEndFail = none
   uint8_t pad[2];
   uint32_t pad2;
-  uint64_t valid; // lanes on the chain from f
+  uint64_t valid; // own lanes on the chain from f
 };
 
 struct FastRes {
@@ -126,7 +135,7 @@ constexpr int kJserCap = 256;  // Serializable stream-length table entries per t
 
 // Serializable stream lengths per tile, sorted by position (aligned coordinates):
 // pos/len[t * kJserCap + i], n[t] entries (n > kJserCap: overflow, span falls back);
-// defer[t] = 1 if the tile holds a "03 AC ED 00 05" pattern.
+// defer[t] = 1 if the tile's scan met a "03 AC ED 00 05" pattern before the tables existed.
 struct JserTabs {
   uint32_t* pos;
   uint32_t* len;
@@ -134,11 +143,11 @@ struct JserTabs {
   uint32_t* defer;
 };
 
-int launch_fast_conv(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
-                     uint32_t mode, uint32_t* d_dbg, void* stream);
+// Fused convergence + segment pass.  mode 0: every tile (tiles meeting a Serializable
+// record are deferred); mode 1: only deferred tiles, stream-length tables filled.
+int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
+                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, void* stream);
 int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream);
-int launch_fast_count(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
-                      JserTabs J, LaneSeg* d_lanes, TileSum* d_sums, void* stream);
 int launch_fast_resolve(const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes, const TileSum* d_sums,
                         const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
 int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Per-kernel hardware counters for the decode/slice kernels (one rocprofv3 pass per group;
+# counters only with --kernel-trace, never with sys/runtime traces).
+# usage: tools/pmc.sh <outdir> [bench args...]
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=${1:-gpurun_out/pmc}; shift || true
+ARGS=${*:---logs 16 --steps 2 --warmup 1 --no-cpu-baseline}
+mkdir -p "$OUT"
+rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+           "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+done
