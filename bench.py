@@ -111,10 +111,11 @@ def main():
     starts = np.ones(len(logs), np.int64)
     base = np.zeros(len(logs) + 1, np.uint64)
 
+    seek_offs = np.array([off for _, _, off in cons], np.int32)
+
     def step():
         eng.decode_logs_device(handles, starts, dec, base)
-        for i, ch, off in cons:
-            logs[i].seek_consumer(ch, 1, off)
+        eng.seek_consumers_raw(creq, seek_offs, n_req)  # rewind the consumers to their start offsets
         got = eng.slice_batch_raw(creq, cres, n_req, o_slice.data_ptr(), o_slice.numel(), device=True)
         assert got == slice_total, (got, slice_total)
 

@@ -18,7 +18,7 @@
 //           k_fast_emit   stage tile -> record starts into LDS by output index ->
 //                         decode + coalesced SoA stores
 // The hot kernels are call-free: Serializable lengths come from per-tile tables, and
-// tiles whose scan meets a "03 AC ED 00 05" pattern before the tables exist are deferred.
+// tiles whose scan meets a magic-bearing tag-3 record before the tables exist are deferred.
 //
 // LDS image: dense (byte a of the tile's aligned coordinates at LDS byte a), followed by
 // a halo of the span's next bytes.  Regions are 268 B = 67 dwords apart, an odd stride,
@@ -233,22 +233,7 @@ __device__ __forceinline__ uint32_t stage_dense(uint32_t* T, const TileDesc& td,
   return hi + halo;
 }
 
-// Serializable magic patterns starting in [rs, re) (dense image).
-__device__ __forceinline__ uint32_t count_magic_dense(const uint32_t* T, uint32_t rs, uint32_t re) {
-  uint32_t n = 0;
-  for (uint32_t k = rs >> 2; k < (re + 3) >> 2; ++k) {
-    const uint32_t w = T[k] ^ 0x03030303u;
-    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;  // no 0x03 byte in this dword
-    for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t a = 4 * k + i;
-      if (a < rs || a >= re) continue;
-      if (d_u8(T, a) == CLG_TAG_SERIALIZABLE && d_be32(T, a + 1) == kSerMagic) ++n;
-    }
-  }
-  return n;
-}
-
-// Same over the padded image of the DP pipeline (k_jser_fill).
+// Serializable magic patterns starting in [rs, re) of the padded DP image (k_jser_fill).
 __device__ __forceinline__ uint32_t count_magic(const uint32_t* T, uint32_t rs, uint32_t re) {
   uint32_t n = 0;
   for (uint32_t k = rs >> 2; k < (re + 3) >> 2; ++k) {
@@ -415,8 +400,10 @@ __device__ __forceinline__ uint32_t keep_points(uint32_t pt, uint32_t bound, uin
 __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   uint32_t* __restrict__ conv, JserTabs J, uint32_t mode,
                                                   LaneSeg* __restrict__ lanes, TileSum* __restrict__ sums,
-                                                  uint32_t* __restrict__ dbg) {
+                                                  uint32_t* __restrict__ dbg, uint64_t* __restrict__ prof) {
   __shared__ uint32_t s_img[kScanImgDwords];
+#define CLG_PHASE(i) \
+  if (prof && lane == 0) prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   __shared__ uint32_t s_c[kFPoints];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
@@ -428,41 +415,45 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   const uint32_t hi = td.delta + td.len;
   const uint64_t ea = sd.len - td.span_off + td.delta;
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
+  CLG_PHASE(0);
   const uint32_t img_end = stage_dense(s_img, td, tiles, t1, t, sd.len, kScanHalo, lane);
+  CLG_PHASE(1);
   uint32_t rs = 0, re = 0;
   if (lane < (uint32_t)kFOwn) fregion(td.delta, hi, (int)lane, &rs, &re);
-  if (mode == 0) {
-    const uint32_t nm = re > rs ? count_magic_dense(s_img, rs, re) : 0u;
-    if (__any(nm != 0)) {  // Serializable records here: wait for the stream-length table
-      if (lane == 0) J.defer[t] = 1;
-      return;
-    }
-  }
+  // No pre-scan for Serializable records: every record the BFS or the parse touches goes
+  // through fser_lookup, which (mode 0, no tables yet) defers the tile.
   const FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J};
   bool defer = false;
+  CLG_PHASE(2);
 
   // ---- convergence points: own regions, then the next tile's first kFNext regions
-  uint32_t pt = kConvUnknown, pops = 0, bound = hi;
+  // (one call site for every lane: the wave runs a single BFS loop)
+  uint32_t pt = kConvUnknown, pops = 0, bound = hi, brs = 0, bn = 0;
   if (lane < (uint32_t)kFOwn) {
     if (lane == 0 && t == sd.first_tile) pt = td.delta;  // a span starts on a record boundary
-    else if (re > rs) pt = converge(c, rs, re - rs < (uint32_t)kCands ? re - rs : (uint32_t)kCands, &pops, &defer);
+    else if (re > rs) {
+      brs = rs;
+      bn = re - rs;
+    }
   } else if (!last) {
     const TileDesc nd = tiles[t + 1];
     uint32_t nrs, nre;
     fregion(nd.delta, nd.delta + nd.len, (int)lane - kFOwn, &nrs, &nre);
     bound = hi + nd.len;
     if (nre > nrs) {
-      const uint32_t a = hi + (nrs - nd.delta), n = nre - nrs;
-      pt = converge(c, a, n < (uint32_t)kCands ? n : (uint32_t)kCands, &pops, &defer);
+      brs = hi + (nrs - nd.delta);
+      bn = nre - nrs;
     }
   } else if (lane == (uint32_t)kFOwn) {
     pt = end_a;  // the span end closes the last tile
     bound = end_a + 1;
   }
+  if (bn) pt = converge(c, brs, bn < (uint32_t)kCands ? bn : (uint32_t)kCands, &pops, &defer);
   if (mode == 0 && __any(defer)) {
     if (lane == 0) J.defer[t] = 1;
     return;
   }
+  CLG_PHASE(3);
   const uint32_t kept = keep_points(pt, bound, lane);
   s_c[lane] = kept;
   conv[(uint64_t)t * kFPoints + lane] = kept;
@@ -470,8 +461,10 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   __syncthreads();
 
   // ---- segments and the chain from the first kept point
+  CLG_PHASE(4);
   LaneSeg seg{kEndFail, 0, 0, 0, 0};
   if (lane < (uint32_t)kFOwn) seg = parse_segment(c, s_c, (int)lane, &defer);
+  CLG_PHASE(5);
   if (mode == 0 && __any(defer)) {
     if (lane == 0) J.defer[t] = 1;
     return;
@@ -504,6 +497,8 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
     sm.valid = valid;
     sums[t] = sm;
   }
+  CLG_PHASE(6);
+#undef CLG_PHASE
 }
 
 // ---- Serializable stream-length tables for deferred tiles --------------------------------
@@ -512,9 +507,11 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   __shared__ uint32_t s_tile[kImageDwords];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  if (!J.defer[t]) return;
   const TileDesc td = tiles[t];
   const SpanDesc sd = spans[td.span];
+  // deferred tiles, and the successor of a deferred tile (its segment crossing the tile
+  // end, and its next-tile points, may land on Serializable records there)
+  if (!J.defer[t] && !(t > sd.first_tile && J.defer[t - 1])) return;
   SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
   stage_tile(s_tile, td, sr, lane);
   const TileGeom g{td.delta, td.delta + td.len};
@@ -779,10 +776,10 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
 static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
 
 int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
-                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, void* stream) {
+                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, uint64_t* d_prof, void* stream) {
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_fast_scan, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, J, mode,
-                     d_lanes, d_sums, d_dbg);
+                     d_lanes, d_sums, d_dbg, d_prof);
   return ok(hipGetLastError());
 }
 

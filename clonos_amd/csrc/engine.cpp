@@ -171,8 +171,8 @@ struct clg_engine {
 
   // staging / scratch
   PinBuf h_stage, h_desc;
-  DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
-  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_jpos, d_jlen, d_jn, d_defer;
+  DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
 
   // timing
@@ -416,6 +416,35 @@ struct clg_engine {
     return sync();
   }
 
+  // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
+  int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
+                      uint64_t total, void* out, uint32_t out_kind) {
+    if (runs.empty() || !n_pieces) return CLG_OK;
+    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
+    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    CHK(h_desc.ensure(hb));
+    CHK(d_desc.ensure(hb));
+    CHK(d_pieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
+    memcpy(h_desc.p, runs.data(), rb);
+    memcpy(h_desc.as<uint8_t>() + o_seg, segtab.data(), gb);
+    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
+    CHK(clg::launch_expand_pieces(d_desc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
+                                  reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
+                                  d_pieces.as<clg::GatherPiece>(), stream));
+    uint8_t* dout;
+    if (out_kind == CLG_MEM_DEVICE) {
+      dout = static_cast<uint8_t*>(out);
+    } else {
+      CHK(d_out.ensure(total));
+      dout = d_out.as<uint8_t>();
+    }
+    CHK(timed("slice_gather", 2 * total, [&] {
+      return clg::launch_gather(d_pieces.as<clg::GatherPiece>(), n_pieces, dout, stream);
+    }));
+    if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
+    return sync();
+  }
+
   int get_delta(uint32_t h, ChKey k, int64_t epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
     *n = 0;
     Log* l;
@@ -502,9 +531,19 @@ struct clg_engine {
 
   // ---------------------------------------------------------------- decode
   struct DecodePlan {
-    std::vector<clg::TileDesc> tiles;
+    std::vector<clg::TileDesc> tiles;   // host-built tiles (staged host input)
     std::vector<clg::SpanDesc> spans;
+    std::vector<clg::SegSpan> runs;     // log spans: tiles generated on the device
+    std::vector<uint32_t> segtab;       // concatenated segment indices of the runs' logs
+    uint32_t n_tiles = 0;
   };
+
+  // Tile window for device planning: min(segment, kTile) when one divides the other.
+  uint32_t tile_unit() const {
+    const uint32_t c = C(), k = uint32_t(clg::kTile);
+    if (c <= k) return (k % c == 0) ? c : 0;
+    return (c % k == 0) ? k : 0;
+  }
 
   void plan_host_span(DecodePlan& p, const uint8_t* dbase, uint64_t len, uint32_t s) {
     clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, len};
@@ -518,9 +557,20 @@ struct clg_engine {
       sd.n_tiles++;
     }
     p.spans.push_back(sd);
+    p.n_tiles = uint32_t(p.tiles.size());
   }
 
   void plan_log_span(DecodePlan& p, const Log& l, int32_t start, int32_t len, uint32_t s) {
+    if (const uint32_t U = tile_unit()) {  // device planning
+      const uint32_t cnt = len > 0 ? (uint32_t(start + len - 1) / U - uint32_t(start) / U + 1) : 0;
+      p.spans.push_back(clg::SpanDesc{p.n_tiles, cnt, uint64_t(len)});
+      if (cnt) {
+        p.runs.push_back(clg::SegSpan{p.segtab.size(), uint32_t(start), uint32_t(len), s, p.n_tiles, 0});
+        p.segtab.insert(p.segtab.end(), l.segs.begin(), l.segs.end());
+      }
+      p.n_tiles += cnt;
+      return;
+    }
     clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, uint64_t(len)};
     int32_t ph = start;
     const int32_t end = start + len;
@@ -540,6 +590,7 @@ struct clg_engine {
       ph += int32_t(take);
     }
     p.spans.push_back(sd);
+    p.n_tiles = uint32_t(p.tiles.size());
   }
 
   int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
@@ -548,7 +599,7 @@ struct clg_engine {
     out->err_span = 0;
     out->err_off = -1;
     out->err_tag = 0;
-    const uint32_t nt = uint32_t(p.tiles.size()), ns = uint32_t(p.spans.size());
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     if (ns == 0) return CLG_OK;
     CHK(d_tiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
     CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
@@ -566,14 +617,28 @@ struct clg_engine {
     CHK(d_jlen.ensure(std::max<size_t>(1, nt) * clg::kJserCap * sizeof(uint32_t)));
     CHK(d_jn.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
     CHK(d_defer.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
-    const size_t hb = nt * sizeof(clg::TileDesc) + ns * sizeof(clg::SpanDesc);
+    // descriptors: host tiles (staged input) or runs + segment table (log spans)
+    const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
+                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
+    const size_t o_runs = (tb + 15) & ~size_t(15), o_seg = (o_runs + rb + 15) & ~size_t(15),
+                 o_spans = (o_seg + gb + 15) & ~size_t(15), hb = o_spans + sb;
     CHK(h_desc.ensure(hb + ns * sizeof(clg::SpanRes) + 64));
+    CHK(d_desc.ensure(hb));
     uint8_t* hd = h_desc.as<uint8_t>();
-    memcpy(hd, p.tiles.data(), nt * sizeof(clg::TileDesc));
-    memcpy(hd + nt * sizeof(clg::TileDesc), p.spans.data(), ns * sizeof(clg::SpanDesc));
-    if (nt) HIPCHK(hipMemcpyAsync(d_tiles.p, hd, nt * sizeof(clg::TileDesc), hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(d_spans.p, hd + nt * sizeof(clg::TileDesc), ns * sizeof(clg::SpanDesc),
-                          hipMemcpyHostToDevice, stream));
+    memcpy(hd, p.tiles.data(), tb);
+    memcpy(hd + o_runs, p.runs.data(), rb);
+    memcpy(hd + o_seg, p.segtab.data(), gb);
+    memcpy(hd + o_spans, p.spans.data(), sb);
+    HIPCHK(hipMemcpyAsync(d_desc.p, hd, hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_spans.p, d_desc.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
+    if (!p.runs.empty()) {
+      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_desc.as<uint8_t>() + o_runs),
+                                   uint32_t(p.runs.size()), nt,
+                                   reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
+                                   tile_unit(), d_tiles.as<clg::TileDesc>(), stream));
+    } else if (tb) {
+      HIPCHK(hipMemcpyAsync(d_tiles.p, d_desc.p, tb, hipMemcpyDeviceToDevice, stream));
+    }
 
     // outputs
     clg::DecodeOut o{};
@@ -604,14 +669,29 @@ struct clg_engine {
     uint32_t* dbg = nullptr;
     if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kFPoints * 4) == CLG_OK)
       dbg = d_dbg.as<uint32_t>();
+    uint64_t* prof = nullptr;  // developer diagnostics: per-phase s_memtime stamps of the scan
+    const char* prof_path = getenv("CLONOS_SCAN_PHASES");
+    if (prof_path && d_prof.ensure(std::max<size_t>(1, nt) * 8 * 8) == CLG_OK) {
+      prof = d_prof.as<uint64_t>();
+      hipMemsetAsync(prof, 0, size_t(nt) * 64, stream);
+    }
     CHK(timed("decode_scan", log_bytes, [&] {
       return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 0, d_lanes.as<clg::LaneSeg>(),
-                                   d_sums.as<clg::TileSum>(), dbg, stream);
+                                   d_sums.as<clg::TileSum>(), dbg, prof, stream);
     }));
+    if (prof) {
+      std::vector<uint64_t> hp(size_t(nt) * 8);
+      hipMemcpyAsync(hp.data(), prof, hp.size() * 8, hipMemcpyDeviceToHost, stream);
+      hipStreamSynchronize(stream);
+      if (FILE* fp = fopen(prof_path, "wb")) {
+        fwrite(hp.data(), 8, hp.size(), fp);
+        fclose(fp);
+      }
+    }
     CHK(timed("decode_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
     CHK(timed("decode_scan_deferred", 0, [&] {
       return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, d_lanes.as<clg::LaneSeg>(),
-                                   d_sums.as<clg::TileSum>(), dbg, stream);
+                                   d_sums.as<clg::TileSum>(), dbg, nullptr, stream);
     }));
     CHK(timed("decode_resolve", uint64_t(nt) * 32, [&] {
       return clg::launch_fast_resolve(ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
@@ -656,7 +736,9 @@ struct clg_engine {
         fwrite(hc.data(), 4, hc.size(), fp);
         fwrite(hs.data(), sizeof(clg::TileSum), hs.size(), fp);
         fwrite(hf.data(), 4, hf.size(), fp);
-        fwrite(p.tiles.data(), sizeof(clg::TileDesc), nt, fp);
+        std::vector<clg::TileDesc> ht(nt);
+        hipMemcpy(ht.data(), d_tiles.p, nt * sizeof(clg::TileDesc), hipMemcpyDeviceToHost);
+        fwrite(ht.data(), sizeof(clg::TileDesc), nt, fp);
         std::vector<uint32_t> hd(size_t(nt) * clg::kFPoints);
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
         fwrite(hd.data(), 4, hd.size(), fp);
@@ -932,8 +1014,12 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
   ENGINE_GUARD(e);
   if (n && (!reqs || !res)) return fail(CLG_E_INVALID_ARG, "null argument");
   CHK(e->flush());
-  std::vector<clg::GatherPiece> pieces;
-  pieces.reserve(n * 2);
+  std::vector<clg::SegSpan> runs;
+  std::vector<uint32_t> segtab;
+  std::unordered_map<uint32_t, uint64_t> tab_of;  // log -> its segment indices in segtab
+  runs.reserve(n);
+  uint32_t n_pieces = 0;
+  const uint32_t C = e->C();
   uint64_t dst = 0;
   for (uint32_t i = 0; i < n; ++i) {
     clg_slice_res& r = res[i];
@@ -965,11 +1051,20 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
       continue;
     }
     r.len = nb;
-    e->add_pieces(e->logs[reqs[i].log], phys, nb, dst, pieces);
+    if (nb > 0) {
+      auto ti = tab_of.find(reqs[i].log);
+      if (ti == tab_of.end()) {
+        const auto& segs = e->logs[reqs[i].log].segs;
+        ti = tab_of.emplace(reqs[i].log, segtab.size()).first;
+        segtab.insert(segtab.end(), segs.begin(), segs.end());
+      }
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(phys), uint32_t(nb), dst, n_pieces, 0});
+      n_pieces += uint32_t(phys + nb - 1) / C - uint32_t(phys) / C + 1;
+    }
     dst += uint64_t(nb);
   }
   if (total) *total = dst;
-  return e->run_gather(pieces, dst, out, out_kind);
+  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
 }
 
 int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch, int32_t offset) {
@@ -979,6 +1074,19 @@ int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch
   auto it = l->epochs.find(epoch);
   if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)epoch);
   l->consumers[ChKey{c.lo, c.hi}] = Consumer{it->second, offset};
+  return CLG_OK;
+}
+
+int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int32_t* offsets, uint32_t n) {
+  ENGINE_GUARD(e);
+  if (n && (!reqs || !offsets)) return fail(CLG_E_INVALID_ARG, "null argument");
+  for (uint32_t i = 0; i < n; ++i) {
+    Log* l;
+    CHK(e->get_log(reqs[i].log, &l));
+    auto it = l->epochs.find(reqs[i].epoch);
+    if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)reqs[i].epoch);
+    l->consumers[ChKey{reqs[i].consumer.lo, reqs[i].consumer.hi}] = Consumer{it->second, offsets[i]};
+  }
   return CLG_OK;
 }
 

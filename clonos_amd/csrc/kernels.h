@@ -146,7 +146,7 @@ struct JserTabs {
 // Fused convergence + segment pass.  mode 0: every tile (tiles meeting a Serializable
 // record are deferred); mode 1: only deferred tiles, stream-length tables filled.
 int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
-                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, void* stream);
+                     uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, uint64_t* d_prof, void* stream);
 int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream);
 int launch_fast_resolve(const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes, const TileSum* d_sums,
                         const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
@@ -171,6 +171,24 @@ struct ScatterChunk {
   uint32_t len;
   uint32_t pad;
 };
+
+// ---- device-side planning ---------------------------------------------------------
+// A run of a log's physical bytes.  Its gather pieces (one per segment it touches) or
+// decode tiles (one per min(segment, kTile) window) are generated on the device from the
+// log's segment-index table, uploaded once per call as one concatenated array, so host
+// work per call is O(requests + logs), not O(segments).
+struct SegSpan {
+  uint64_t segtab_off;  // first entry of the log's segment indices in the call's table
+  uint32_t phys;        // first physical byte of the run
+  uint32_t len;
+  uint64_t dst;         // gather: output offset of the run; decode: span index
+  uint32_t first;       // first piece / tile generated for the run
+  uint32_t pad;
+};
+int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pieces, const uint32_t* d_segtab,
+                         const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream);
+int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
+                        const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);

@@ -81,6 +81,46 @@ __global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ 
 }
 
 // ==================================================================================
+// Device-side planning: item g -> its run (binary search over first) -> window.
+// ==================================================================================
+__device__ __forceinline__ uint32_t find_run(const SegSpan* spans, uint32_t n, uint32_t g) {
+  uint32_t lo = 0, hi = n;  // last run with first <= g
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (spans[mid].first <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_expand_pieces(const SegSpan* __restrict__ spans, uint32_t n_spans,
+                                                       uint32_t n_pieces, const uint32_t* __restrict__ segtab,
+                                                       const uint8_t* __restrict__ pool, uint32_t C,
+                                                       GatherPiece* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_pieces) return;
+  const SegSpan r = spans[find_run(spans, n_spans, g)];
+  const uint32_t w = r.phys / C + (g - r.first);
+  const uint32_t s0 = w * C > r.phys ? w * C : r.phys;
+  const uint32_t e1 = (w + 1) * C < r.phys + r.len ? (w + 1) * C : r.phys + r.len;
+  out[g] = GatherPiece{pool + (size_t)segtab[r.segtab_off + w] * C + (s0 - w * C), r.dst + (s0 - r.phys), e1 - s0, 0};
+}
+
+__global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict__ spans, uint32_t n_spans,
+                                                      uint32_t n_tiles, const uint32_t* __restrict__ segtab,
+                                                      const uint8_t* __restrict__ pool, uint32_t C, uint32_t U,
+                                                      TileDesc* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_tiles) return;
+  const SegSpan r = spans[find_run(spans, n_spans, g)];
+  const uint32_t w = r.phys / U + (g - r.first);
+  const uint32_t s0 = w * U > r.phys ? w * U : r.phys;
+  const uint32_t e1 = (w + 1) * U < r.phys + r.len ? (w + 1) * U : r.phys + r.len;
+  const uint32_t si = s0 / C, so = s0 % C;
+  out[g] = TileDesc{pool + (size_t)segtab[r.segtab_off + si] * C + (so & ~15u), so & 15u, e1 - s0, (uint32_t)r.dst, 0,
+                    (uint64_t)(s0 - r.phys)};
+}
+
+// ==================================================================================
 // Pass 1: transfer tables.  One wave per tile; lane l owns region l and runs a backward
 // DP: ns(p) = (p + L(p) past the region end) ? that exit : ns(p + L(p)), with record
 // and wide counts.  ns for the last 64 positions lives in an LDS ring; after the DP the
@@ -620,6 +660,22 @@ int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_sr
   const uint32_t blocks = min((n + 3) / 4, 4096u);
   hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_chunks, n, d_src);
   return ok(hipGetLastError());
+}
+
+int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pieces, const uint32_t* d_segtab,
+                         const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream) {
+  if (!n_pieces) return CLG_OK;
+  hipLaunchKernelGGL(k_expand_pieces, dim3((n_pieces + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
+                     n_pieces, d_segtab, pool, seg_bytes, d_out);
+  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+}
+
+int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
+                        const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream) {
+  if (!n_tiles) return CLG_OK;
+  hipLaunchKernelGGL(k_expand_tiles, dim3((n_tiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
+                     n_tiles, d_segtab, pool, seg_bytes, unit, d_out);
+  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
 }
 
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream) {

@@ -227,6 +227,11 @@ class Engine:
                                   _lib.CLG_MEM_DEVICE if device else _lib.CLG_MEM_HOST, C.byref(total)))
         return total.value
 
+    def seek_consumers_raw(self, creq, offsets: np.ndarray, n: int) -> None:
+        """Batched consumer positioning over a prebuilt ctypes request array."""
+        offs = np.ascontiguousarray(offsets, dtype=np.int32)
+        check(lib.clg_consumer_seek_batch(self._h, C.cast(creq, C.c_void_p), offs.ctypes.data, n))
+
     # ---- checkpoint completion ---------------------------------------------------------
     def truncate_all(self, checkpoint_id: int) -> bool:
         applied = C.c_int32()

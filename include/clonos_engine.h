@@ -168,6 +168,9 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
 /* Consumer offsets set directly (used to position consumers mid-epoch in benchmarks and
  * when a standby takes over a channel); epoch must exist. */
 int clg_consumer_seek(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t offset);
+/* Batched form: consumer reqs[i] of log reqs[i].log positioned at offsets[i] of epoch
+ * reqs[i].epoch (stops at the first failing entry). */
+int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int32_t* offsets, uint32_t n);
 
 /* ---- checkpoint completion fan-out (JobCausalLogImpl.notifyCheckpointComplete :230-246) --
  * CAS on the engine's latestCompletedCheckpoint; if newer, truncates every open log. */

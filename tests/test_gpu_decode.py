@@ -142,3 +142,25 @@ def test_decode_logs_in_hbm(engine):
     dec = engine.decode_logs(logs, start)
     for s, b in enumerate(expect):
         assert_span_equal(dec, s, b)
+
+
+@pytest.mark.parametrize("seg", [48, 4096, 65536])
+def test_decode_logs_segment_sizes(seg):
+    """Tiles are planned on the device when the segment size and the 16 KiB tile divide
+    one another (4096, 65536) and on the host otherwise (48); both decode bit-exactly."""
+    from clonos_amd import Engine
+    rng = np.random.default_rng(seg)
+    with Engine(segment_bytes=seg, pool_segments=(1 << 22) // seg + 64) as eng:
+        logs, expect = [], []
+        for v in range(5):
+            log = eng.open_log(CausalLogID.main(v))
+            b, _ = synth.config2_log(int(rng.integers(1000, 60000)), rng)
+            log.processUpstreamDelta(b.tobytes(), 0, 0)
+            for _ in range(int(rng.integers(0, 400))):
+                log.appendDeterminant(synth.random_determinant(rng), 1)
+            logs.append(log)
+        start = [int(rng.integers(0, 2)) for _ in logs]
+        expect = [log.getDeterminants(e) for log, e in zip(logs, start)]
+        dec = eng.decode_logs(logs, start)
+        for s, b in enumerate(expect):
+            assert_span_equal(dec, s, b)

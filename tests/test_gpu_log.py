@@ -154,3 +154,41 @@ def test_truncate_all_cas_and_pool_reuse():
         for log in logs:
             assert log.state()["epochs"][0][0] == 4
             assert log.getDeterminants(4) == D.encode(D.TimestampDeterminant(4)) * 40 + D.encode(D.TimestampDeterminant(5)) * 40
+
+
+@pytest.mark.parametrize("seg", [16, 512, 16384, 65536])
+def test_seek_batch_then_slice(seg):
+    """clg_consumer_seek_batch positions consumers exactly like clg_consumer_seek; the
+    batched slice (pieces planned on the device) returns each consumer's suffix."""
+    from clonos_amd import _lib
+    rng = np.random.default_rng(seg + 3)
+    with Engine(segment_bytes=seg, pool_segments=(1 << 21) // seg + 64) as eng:
+        logs, bufs = [], []
+        for v in range(6):
+            log = eng.open_log(CausalLogID.main(v))
+            b, _ = synth.config2_log(int(rng.integers(10, 30000)), rng)
+            log.processUpstreamDelta(b.tobytes(), 0, 4)
+            logs.append(log)
+            bufs.append(b.tobytes())
+        reqs = []
+        for i in range(len(logs)):
+            for c in range(5):
+                reqs.append((i, (c + 1, i), int(rng.integers(0, len(bufs[i]) + 1))))
+        creq = (_lib.SliceReq * len(reqs))()
+        cres = (_lib.SliceRes * len(reqs))()
+        for k, (i, ch, _) in enumerate(reqs):
+            creq[k].log = logs[i].handle
+            creq[k].consumer = _lib.ChannelId(*ch)
+            creq[k].epoch = 4
+        eng.seek_consumers_raw(creq, np.array([o for _, _, o in reqs], np.int32), len(reqs))
+        for i, ch, off in reqs:
+            assert logs[i].consumer_state(ch)[1] == off
+        total = sum(len(bufs[i]) - off for i, _, off in reqs)
+        out = np.zeros(total + 16, np.uint8)
+        got = eng.slice_batch_raw(creq, cres, len(reqs), out.ctypes.data, out.size, device=False)
+        assert got == total
+        for k, (i, ch, off) in enumerate(reqs):
+            r = cres[k]
+            assert r.status == 0
+            exp = bufs[i][off:]
+            assert r.len == len(exp) and out[r.out_off:r.out_off + r.len].tobytes() == exp
