@@ -42,7 +42,7 @@ EXPORTED = [
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
     "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
-    "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
+    "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
 ]
 
@@ -85,6 +85,17 @@ class LogState(C.Structure):
 
 class SliceReq(C.Structure):
     _fields_ = [("log", C.c_uint32), ("reserved", C.c_uint32), ("consumer", ChannelId), ("epoch", C.c_int64)]
+
+
+class DeltaReq(C.Structure):
+    _fields_ = [
+        ("log", C.c_uint32),
+        ("offset_from_epoch", C.c_int32),
+        ("epoch", C.c_int64),
+        ("src_off", C.c_uint64),
+        ("len", C.c_uint32),
+        ("status", C.c_int32),
+    ]
 
 
 class SliceRes(C.Structure):
@@ -163,6 +174,7 @@ def _load() -> C.CDLL:
         "clg_slice_batch": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, u64p]),
         "clg_consumer_seek": (C.c_int, [P, C.c_uint32, ChannelId, C.c_int64, C.c_int32]),
         "clg_consumer_seek_batch": (C.c_int, [P, P, P, C.c_uint32]),
+        "clg_upstream_delta_batch": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32]),
         "clg_truncate_all": (C.c_int, [P, C.c_int64, i32p]),
         "clg_decode_host": (C.c_int, [P, P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_decode_logs": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),

@@ -25,6 +25,8 @@
 #include "../../include/clonos_engine.h"
 #include "kernels.h"
 
+static_assert(sizeof(clg_delta_req) == 32, "clg_delta_req layout");
+
 namespace {
 
 thread_local std::string g_err;
@@ -336,6 +338,60 @@ struct clg_engine {
     return CLG_OK;
   }
 
+  // Batched processUpstreamDelta (:117-154) over one input buffer.  Device input (e.g.
+  // an RCCL receive buffer) is scattered straight into the log segments: pending host
+  // bytes are flushed first, so the logs' byte order is preserved.
+  int upstream_batch(clg_delta_req* r, uint32_t n, const uint8_t* bytes, uint32_t in_kind) {
+    if (in_kind != CLG_MEM_DEVICE) {
+      for (uint32_t i = 0; i < n; ++i) {
+        r[i].status = upstream(r[i].log, r[i].epoch, r[i].offset_from_epoch, bytes + r[i].src_off, r[i].len);
+      }
+      return CLG_OK;
+    }
+    CHK(flush());
+    std::vector<clg::ScatterChunk> ch;
+    size_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      r[i].status = CLG_OK;
+      Log* l;
+      if ((r[i].status = get_log(r[i].log, &l)) != CLG_OK || r[i].len == 0) continue;
+      auto es = compute_if_absent(*l, r[i].epoch);
+      const int32_t cur = l->writer - es->offset;
+      const int32_t num_new = (r[i].offset_from_epoch + int32_t(r[i].len)) - cur;
+      if (num_new <= 0) continue;
+      if (num_new > int32_t(r[i].len)) {
+        r[i].status = fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d",
+                           r[i].offset_from_epoch, r[i].len, cur);
+        continue;
+      }
+      if ((r[i].status = ensure_space(*l, num_new)) != CLG_OK) continue;
+      int32_t p = l->writer;
+      uint64_t src = r[i].src_off + (r[i].len - uint32_t(num_new));
+      uint32_t left = uint32_t(num_new);
+      while (left) {
+        const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
+        const uint32_t take = std::min<uint32_t>(left, C() - so);
+        ch.push_back(clg::ScatterChunk{seg_addr(l->segs[si]) + so, src, take, 0});
+        p += int32_t(take);
+        src += take;
+        left -= take;
+      }
+      l->writer += num_new;
+      l->flushed = l->writer;
+      total += size_t(num_new);
+    }
+    if (ch.empty()) return CLG_OK;
+    const size_t db = ch.size() * sizeof(clg::ScatterChunk);
+    CHK(h_desc.ensure(db));
+    CHK(d_desc.ensure(db));
+    memcpy(h_desc.p, ch.data(), db);
+    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, db, hipMemcpyHostToDevice, stream));
+    CHK(timed("upstream_scatter", 2 * total, [&] {
+      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(ch.size()), bytes, stream);
+    }));
+    return sync();  // the caller's buffer and the pinned descriptors are free again
+  }
+
   int has_delta(uint32_t h, ChKey k, int64_t epoch, int32_t* out) {  // :196-240
     Log* l;
     CHK(get_log(h, &l));
@@ -456,7 +512,10 @@ struct clg_engine {
       const int32_t nb = bytes_to_send(*l, epoch, p);
       if (nb < 0 || p < 0 || int64_t(p) + nb > capacity(*l))
         return fail(CLG_E_STATE, "delta [%d, %d) outside log of capacity %d", p, p + nb, capacity(*l));
-      if (uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
+      if (uint32_t(nb) > cap) {
+        *n = uint32_t(nb);  // required size (the consumer does not advance)
+        return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
+      }
     }
     CHK(flush());
     int32_t phys, nb;
@@ -489,7 +548,10 @@ struct clg_engine {
     if (cfg.sharing_depth == 0) return CLG_OK;
     int32_t s, nb;
     CHK(determinants_range(*l, start_epoch, &s, &nb));
-    if (uint32_t(nb) > cap) return fail(CLG_E_CAPACITY, "getDeterminants needs %d bytes", nb);
+    if (uint32_t(nb) > cap) {
+      *n = uint32_t(nb);  // required size
+      return fail(CLG_E_CAPACITY, "getDeterminants needs %d bytes", nb);
+    }
     CHK(flush());
     std::vector<clg::GatherPiece> pieces;
     add_pieces(*l, s, nb, 0, pieces);
@@ -1075,6 +1137,12 @@ int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch
   if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)epoch);
   l->consumers[ChKey{c.lo, c.hi}] = Consumer{it->second, offset};
   return CLG_OK;
+}
+
+int clg_upstream_delta_batch(clg_engine* e, clg_delta_req* reqs, uint32_t n, const uint8_t* bytes, uint32_t in_kind) {
+  ENGINE_GUARD(e);
+  if (n && (!reqs || !bytes)) return fail(CLG_E_INVALID_ARG, "null argument");
+  return e->upstream_batch(reqs, n, bytes, in_kind);
 }
 
 int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int32_t* offsets, uint32_t n) {

@@ -227,6 +227,11 @@ class Engine:
                                   _lib.CLG_MEM_DEVICE if device else _lib.CLG_MEM_HOST, C.byref(total)))
         return total.value
 
+    def upstream_delta_batch(self, reqs, n: int, src_ptr: int, in_kind: int) -> None:
+        """Batched processUpstreamDelta over one buffer (host or device pointer); each
+        request's status is written back into `reqs` (clg_delta_req)."""
+        check(lib.clg_upstream_delta_batch(self._h, C.cast(reqs, C.c_void_p), n, src_ptr, in_kind))
+
     def seek_consumers_raw(self, creq, offsets: np.ndarray, n: int) -> None:
         """Batched consumer positioning over a prebuilt ctypes request array."""
         offs = np.ascontiguousarray(offsets, dtype=np.int32)

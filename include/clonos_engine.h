@@ -119,13 +119,27 @@ int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, c
 /* processUpstreamDelta :117-154 (dedup by offsetFromEpoch, append the new suffix). */
 int clg_upstream_delta(clg_engine* e, uint32_t log, int64_t epoch, int32_t offset_from_epoch,
                        const uint8_t* delta, uint32_t n);
+/* Batched processUpstreamDelta over one buffer (host or device memory): delta i is
+ * bytes[src_off, src_off + len) for log `log`; per-request status.  Device input (an
+ * RCCL receive buffer) is scattered into the log segments without a host round trip. */
+typedef struct clg_delta_req {
+  uint32_t log;
+  int32_t offset_from_epoch;
+  int64_t epoch;
+  uint64_t src_off;
+  uint32_t len;
+  int32_t status; /* out */
+} clg_delta_req;
+int clg_upstream_delta_batch(clg_engine* e, clg_delta_req* reqs, uint32_t n, const uint8_t* bytes,
+                             uint32_t in_kind);
 int clg_log_length(clg_engine* e, uint32_t log, int32_t* out);                                /* :180-192 */
 int clg_has_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t* out); /* :196-240 */
 int clg_offset_from_epoch(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* out);       /* :243-246 */
-/* getDeltaForConsumer :249-277: bytes copied into `out` (host or device). */
+/* getDeltaForConsumer :249-277: bytes copied into `out` (host or device).  With
+ * CLG_E_CAPACITY, *n is the required size and the consumer has not advanced. */
 int clg_get_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, void* out,
                   uint32_t cap, uint32_t out_kind, uint32_t* n);
-/* getDeterminants(startEpoch) :285-313. */
+/* getDeterminants(startEpoch) :285-313 (CLG_E_CAPACITY: *n = required size). */
 int clg_get_determinants(clg_engine* e, uint32_t log, int64_t start_epoch, void* out, uint32_t cap,
                          uint32_t out_kind, uint32_t* n);
 int clg_notify_checkpoint_complete(clg_engine* e, uint32_t log, int64_t checkpoint_id); /* :398-435 */

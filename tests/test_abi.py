@@ -32,6 +32,7 @@ def test_abi_version_and_struct_sizes():
     assert ctypes.sizeof(_lib.Config) == 24
     assert ctypes.sizeof(_lib.SliceReq) == 32
     assert ctypes.sizeof(_lib.SliceRes) == 24
+    assert ctypes.sizeof(_lib.DeltaReq) == 32
     assert ctypes.sizeof(_lib.Decoded) == 136
     assert ctypes.sizeof(_lib.KernelStat) == 56
 

@@ -192,3 +192,29 @@ def test_seek_batch_then_slice(seg):
             assert r.status == 0
             exp = bufs[i][off:]
             assert r.len == len(exp) and out[r.out_off:r.out_off + r.len].tobytes() == exp
+
+
+def test_capacity_reports_required_size():
+    """clg_get_delta / clg_get_determinants with a short buffer: CLG_E_CAPACITY, *n = the
+    size needed, consumer not advanced (the JNI layer sizes its direct buffer this way)."""
+    import ctypes as C
+    from clonos_amd._lib import lib
+    with Engine(segment_bytes=64, pool_segments=256) as eng:
+        log = eng.open_log(CausalLogID.main(3))
+        for i in range(40):
+            log.appendDeterminant(D.TimestampDeterminant(i), 0)
+        ch = (5, 6)
+        assert log.hasDeltaForConsumer(ch, 0)
+        n = C.c_uint32()
+        st = lib.clg_get_delta(eng.handle, log.handle, _lib_ch(ch), 0, None, 0, 0, C.byref(n))
+        assert st == -11 and n.value == 40 * 9
+        assert log.consumer_state(ch) == (0, 0)
+        st = lib.clg_get_determinants(eng.handle, log.handle, 0, None, 10, 0, C.byref(n))
+        assert st == -11 and n.value == 40 * 9
+        assert log.getDeltaForConsumer(ch, 0) == D.encode(D.TimestampDeterminant(0))[:0] + b"".join(
+            D.encode(D.TimestampDeterminant(i)) for i in range(40))
+
+
+def _lib_ch(ch):
+    from clonos_amd import _lib
+    return _lib.ChannelId(*ch)
