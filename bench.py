@@ -202,6 +202,7 @@ def main():
             "decode_pipeline": {"avg_ms": round(dec_ms, 4), "algo_bytes": dec_bytes,
                                 "gbs": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1) if dec_ms else None},
             "slice": {"algo_bytes": slice_bytes},
+            "decode_path": "robust (fused aborted)" if "decode_fallback" in stats else "fused single-pass",
             "kernels": kern,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -34,6 +34,7 @@ STATUS_NAMES = {v: k for k, v in globals().items() if k.startswith("CLG_E_") or 
 CLG_MEM_HOST = 0
 CLG_MEM_DEVICE = 1
 CLG_F_TIMING = 1
+CLG_F_ROBUST_DECODE = 2
 CLG_FULL_SHARING = -1
 
 EXPORTED = [

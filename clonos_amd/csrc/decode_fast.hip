@@ -40,30 +40,6 @@ constexpr uint32_t kSerMagic = 0xACED0005u;
 constexpr int kLenRare = -2;          // lean_len: use the general path
 constexpr int kEmitCap = 3072;        // record starts staged per emit window
 
-// ---------------------------------------------------------------------------------
-// Dense LDS image accessors.
-// ---------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t d_u8(const uint32_t* T, uint32_t a) {
-  return reinterpret_cast<const uint8_t*>(T)[a];
-}
-__device__ __forceinline__ uint32_t d_be32(const uint32_t* T, uint32_t a) {
-  const uint32_t k = a >> 2;
-  return __builtin_bswap32(__builtin_amdgcn_alignbyte(T[k + 1], T[k], a & 3u));
-}
-__device__ __forceinline__ uint64_t d_be64(const uint32_t* T, uint32_t a) {
-  const uint32_t k = a >> 2, s = a & 3u;
-  const uint32_t d0 = T[k], d1 = T[k + 1], d2 = T[k + 2];
-  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, s), hi = __builtin_amdgcn_alignbyte(d2, d1, s);
-  return __builtin_bswap64((uint64_t)hi << 32 | lo);
-}
-struct DenseBytes {
-  const uint32_t* T;
-  uint32_t base;
-  __device__ __forceinline__ int operator()(uint64_t k) const { return (int)d_u8(T, base + (uint32_t)k); }
-};
-__device__ __forceinline__ uint32_t fld_be32(const DenseBytes& b, uint32_t k) { return d_be32(b.T, b.base + k); }
-__device__ __forceinline__ uint64_t fld_be64(const DenseBytes& b, uint32_t k) { return d_be64(b.T, b.base + k); }
-
 // Region l of a tile with valid aligned coordinates [lo, hi).
 __device__ __forceinline__ void fregion(uint32_t lo, uint32_t hi, int l, uint32_t* rs, uint32_t* re) {
   uint32_t s = (uint32_t)l * kFRegion;

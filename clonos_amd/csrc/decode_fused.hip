@@ -1,0 +1,640 @@
+// decode_fused.hip -- single-pass batched decode (gfx950).
+//
+// SimpleDeterminantEncoder.decodeNext (reference flink-runtime
+// causal/determinant/SimpleDeterminantEncoder.java:78-342) applied to whole spans.  Record
+// starts form a chain p -> p + L(p) whose length function reads the tag byte (and, for
+// TimerTrigger / SourceCheckpoint, a field at a fixed offset), so the stream is not
+// self-synchronising.  One wave decodes one tile of kZTile bytes; lane l owns the kZRegion
+// bytes of region l:
+//
+//   1. speculative walk: from the region's first byte, follow the chain, stepping one
+//      byte past anything that is not a valid record (a 128-bit bitmap of the starts it
+//      visits stays in registers);
+//   2. merge: given the true entry e of the region, walk the true chain from e and the
+//      speculative chain from the region start in lock-step (two pointers) until they
+//      meet.  From the meeting point on the region's true starts ARE the speculative ones,
+//      so the region's exit is the speculative exit and its starts are the true prefix
+//      plus the speculative suffix.  Chains re-synchronise after a few records, so this
+//      costs a few steps per region;
+//   3. entries are the previous lane's exit; a lane whose entry changed re-merges
+//      (wave-uniform loop, at most one pass per lane);
+//   4. across tiles: every tile first computes its exit assuming the chain merges inside
+//      it ("canonical" exit, independent of its entry) and publishes it, then reads its
+//      predecessor's canonical exit as its entry, re-merges lane 0 and checks that its
+//      true exit is the one it published.  Record and wide-record bases come from a
+//      decoupled look-back over per-tile aggregates;
+//   5. emit: record starts are dropped into LDS by output index and decoded by
+//      consecutive lanes, so every SoA store of the wave is one contiguous run.
+//
+// Anything outside the fast path -- a decode error, a Serializable record (its length
+// needs the Java-serialization walker), a record that jumps a whole tile, a tile whose
+// true exit differs from the one it published -- raises the batch's abort flag; the
+// host then re-decodes the batch with the robust pipeline (decode_fast.hip +
+// kernels.hip), which also classifies errors exactly.  Abort never produces output the
+// host keeps.
+//
+// Cross-workgroup hand-offs are single 8-byte words written and polled with agent-scope
+// relaxed atomics (global_store/load ... sc1): the payload is the word itself.
+// Record layouts: SimpleDeterminantEncoder.java:124-323.
+#include "dev_common.h"
+
+namespace clg {
+
+// LDS image: row r holds aligned bytes [kZRegion r, kZRegion (r + 1)) at a pitch of kZPitch
+// dwords; the kZPad dwords after a row repeat the first kZPad dwords of the next row, so
+// up to four consecutive dwords read from any dword of a row stay inside its pitch.  Lane
+// l walks row l: with a pitch of 35 dwords (co-prime with the 32 banks) the lanes' reads
+// start on distinct banks.  Rows: the tile, then the halo + zero pad.
+constexpr uint32_t kZRowDw = kZRegion / 4;  // 32
+constexpr uint32_t kZPad = 3;
+constexpr uint32_t kZPitch = kZRowDw + kZPad;
+constexpr uint32_t kZRows = kZTile / kZRegion + 2;
+constexpr uint32_t kZImgDw = kZRows * kZPitch;
+#ifndef CLG_FUSED_PIPELINE
+#define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
+#endif
+constexpr uint32_t kZWin = 1024;                       // record starts staged per emit window
+constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // "canonical" entry marker (lane 0)
+constexpr int kZSer = -2;                              // Serializable stream: walker needed
+
+// ---------------------------------------------------------------------------------
+// 128-bit region bitmaps (bit i <-> region byte rs + i).
+// ---------------------------------------------------------------------------------
+struct Bits {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ void bset(Bits& b, uint32_t i) {
+  const uint64_t m = 1ull << (i & 63u);
+  b.lo |= i < 64u ? m : 0ull;
+  b.hi |= i < 64u ? 0ull : m;
+}
+// bits >= i
+__device__ __forceinline__ Bits bge(const Bits& b, uint32_t i) {
+  const uint64_t m = ~0ull << (i & 63u);
+  return Bits{i < 64u ? b.lo & m : 0ull, i < 64u ? b.hi : b.hi & m};
+}
+__device__ __forceinline__ Bits bor(const Bits& a, const Bits& b) { return Bits{a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ uint32_t bcount(const Bits& b) { return (uint32_t)(__popcll(b.lo) + __popcll(b.hi)); }
+
+__device__ __forceinline__ uint32_t rk(uint32_t k) { return k + kZPad * (k >> 5); }  // dword k -> LDS dword
+__device__ __forceinline__ uint32_t rb(uint32_t a) { return 4u * rk(a >> 2) + (a & 3u); }  // byte a -> LDS byte
+__device__ __forceinline__ uint32_t zb(const uint32_t* T, uint32_t a) { return (T[rk(a >> 2)] >> (8u * (a & 3u))) & 0xFFu; }
+__device__ __forceinline__ uint32_t zbe32(const uint32_t* T, uint32_t a) {
+  const uint32_t p = rk(a >> 2);
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(T[p + 1], T[p], a & 3u));
+}
+__device__ __forceinline__ uint64_t zbe64(const uint32_t* T, uint32_t a) {
+  const uint32_t p = rk(a >> 2), sh = a & 3u;
+  const uint32_t d0 = T[p], d1 = T[p + 1], d2 = T[p + 2];
+  return __builtin_bswap64((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32 | __builtin_amdgcn_alignbyte(d1, d0, sh));
+}
+// Bytes relative to a record start, for len_fields / decode_fields (dev_common.h).
+struct ZBytes {
+  const uint32_t* T;
+  uint32_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) const { return (int)zb(T, base + (uint32_t)k); }
+};
+__device__ __forceinline__ uint32_t fld_be32(const ZBytes& b, uint32_t k) { return zbe32(b.T, b.base + k); }
+__device__ __forceinline__ uint64_t fld_be64(const ZBytes& b, uint32_t k) { return zbe64(b.T, b.base + k); }
+
+// ---------------------------------------------------------------------------------
+// Record length at aligned coordinate a (< tile end): L > 0, kLenErr (-1) for a record
+// decodeNext rejects, kZSer for a Serializable record.  Reads only the LDS image (every
+// field a valid record needs lies within 27 bytes of its start, inside tile + halo).
+// Validity and length follow SimpleDeterminantEncoder readers :116-341 (len_fields).
+// ---------------------------------------------------------------------------------
+__device__ __noinline__ int zlen_rare(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t tg, uint32_t x0) {
+  if (tg == CLG_TAG_SERIALIZABLE)
+    return ((x0 >> 8) | (zb(T, a + 4) << 24)) == 0x0500EDACu ? kZSer : (int)kLenErr;  // AC ED 00 05
+  const ZBytes b{T, a};
+  const int64_t LL = len_fields(b, (int)tg, (uint64_t)(end_a - a));
+  return (LL <= 0 || LL > 0x7FFFFFF0ll) ? (int)kLenErr : (int)LL;
+}
+__device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t* tag) {
+  const uint32_t p = rk(a >> 2);
+  const uint32_t x0 = __builtin_amdgcn_alignbit(T[p + 1], T[p], 8u * (a & 3u));  // bytes a..a+3 (LE)
+  const uint32_t tg = x0 & 0xFFu;
+  *tag = tg;
+  constexpr uint64_t lut = 2ull | 9ull << 4 | 5ull << 8 | 13ull << 24 | 5ull << 28;  // 0: 3/4/5
+  const uint32_t L = (uint32_t)(lut >> (4u * (tg & 15u))) & 0xFu;
+  if (tg > 7u) return (int)kLenErr;
+  if (L != 0) return a + L > end_a ? (int)kLenErr : (int)L;
+  return zlen_rare(T, a, end_a, tg, x0);  // TimerTrigger, SourceCheckpoint, Serializable
+}
+
+// ---------------------------------------------------------------------------------
+// Walks.  Two step rules over the same length function:
+//   true step  -- follow the record (any length); an invalid record is an error;
+//   spec step  -- follow records of at most kZSpecMax bytes, step one byte past anything
+//                 else.  Speculative chains start at arbitrary bytes, and a garbage
+//                 TimerTrigger / SourceCheckpoint can claim a length of megabytes; the cap
+//                 keeps such a chain local.  A skip is recorded (Spec::bad) because from
+//                 a skipped byte on the speculative chain no longer follows the true one.
+// ---------------------------------------------------------------------------------
+constexpr int kZSpecMax = 256;
+
+__device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uint32_t end_a, int* L, uint32_t* tg) {
+  *L = zlen(T, q, end_a, tg);
+  return (*L > 0 && *L <= kZSpecMax) ? q + (uint32_t)*L : q + 1u;
+}
+
+struct Spec {
+  Bits bm, wb;         // followed starts in the region / followed wide starts
+  uint32_t first;      // first position >= rs
+  uint32_t exit;       // first position >= re
+  uint32_t bad;        // 1 + last position skipped, 0 if none
+};
+
+// The walk starts kZWarm bytes before the region (inside the previous one), so that by
+// the region start the chain has almost always re-synchronised with the true one; then
+// true chains meet it at their first step and entries rarely cascade across lanes.
+constexpr uint32_t kZWarm = 64;
+__device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a) {
+  Spec s{{0, 0}, {0, 0}, rs, rs, 0};
+  uint32_t q = ws;
+  while (q < rs) {  // warm-up: follow the rule, record nothing but skips
+    uint32_t tg;
+    int L;
+    const uint32_t nq = spec_step(T, q, end_a, &L, &tg);
+    if (nq == q + 1u && L != 1) s.bad = q + 1;
+    q = nq;
+  }
+  s.first = q;
+  while (q < re) {
+    uint32_t tg;
+    int L;
+    const uint32_t nq = spec_step(T, q, end_a, &L, &tg);
+    if (nq == q + 1u && L != 1) {
+      s.bad = q + 1;
+    } else {
+      bset(s.bm, q - rs);
+      if (is_wide((int)tg)) bset(s.wb, q - rs);
+    }
+    q = nq;
+  }
+  s.exit = q;
+  return s;
+}
+
+// Canonical chain: the speculative rule from entry e, merged with the region's
+// speculative chain (both follow the same rule, so meeting means identical from there).
+__device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
+                                               const Spec& s) {
+  if (e >= re) return e;
+  uint32_t p = e, q = s.first;
+  for (;;) {
+    if (p == q) return s.exit;
+    if (p >= re) return p;
+    int L;
+    uint32_t tg;
+    if (p < q) p = spec_step(T, p, end_a, &L, &tg);
+    else q = spec_step(T, q, end_a, &L, &tg);
+  }
+}
+
+struct Res {
+  Bits bm, wb;       // true record starts in the region / wide ones
+  uint32_t exit;     // first true start >= re (bad: the speculative exit)
+  uint32_t bad;      // true chain hits an invalid or Serializable record
+  uint32_t unclean;  // true chain follows a record longer than kZSpecMax
+};
+
+// True chain from entry e (e >= rs) merged with the speculative chain: they may only
+// merge at a position past the speculative chain's last skip.
+__device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
+                                          const Spec& s) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  if (e >= re) return r;  // no record starts in this region
+  uint32_t p = e, q = s.first;
+  Bits pb{0, 0}, pw{0, 0};
+  for (;;) {
+    if (p == q && p < re && p >= s.bad) {  // met: the speculative chain from here is the true one
+      r.bm = bor(pb, bge(s.bm, p - rs));
+      r.wb = bor(pw, bge(s.wb, p - rs));
+      r.exit = s.exit;
+      return r;
+    }
+    if (p >= re) break;
+    uint32_t tg;
+    int L;
+    if (p <= q) {
+      L = zlen(T, p, end_a, &tg);
+      if (L <= 0) {
+        r.bad = 1;
+        r.exit = s.exit;
+        return r;
+      }
+      bset(pb, p - rs);
+      if (is_wide((int)tg)) bset(pw, p - rs);
+      r.unclean |= L > kZSpecMax ? 1u : 0u;
+      p += (uint32_t)L;
+    } else {
+      q = spec_step(T, q, end_a, &L, &tg);
+    }
+  }
+  r.bm = pb;
+  r.wb = pw;
+  r.exit = p;
+  return r;
+}
+
+// ---------------------------------------------------------------------------------
+// Hand-off words.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// abort[0]: nonzero once any tile aborted (polled by waiting tiles); abort[r], r = 1..4:
+// ~(lowest tile that aborted for reason r), for diagnostics.
+__device__ __forceinline__ void raise_abort(const FusedCtl& c, uint32_t reason, uint32_t t) {
+  __hip_atomic_store(c.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(c.abort + reason, ~t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Polling backoff: every poll is an L2-bypassing load, and thousands of waves poll at
+// once, so waiting waves sleep 0.1-3 us between polls (doubling) to leave the memory
+// system to the waves that stage tiles.
+constexpr uint64_t kZSpinLimit = 1ull << 29;  // ~0.2 s of shader clock: give up and abort
+__device__ __forceinline__ bool backoff(uint32_t& n, uint64_t t0) {
+  for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(32);  // ~2k cycles each
+  n = n < 16u ? n * 2u : 16u;
+  return __builtin_amdgcn_s_memtime() - t0 < kZSpinLimit;
+}
+
+// Count words: [61:31] wide records | [30:0] records.
+__device__ __forceinline__ uint64_t pack_cnt(uint32_t rec, uint32_t wide) { return (uint64_t)wide << 31 | rec; }
+
+// Stage tile t into the padded row layout: the tile (16-byte loads, all in flight before
+// any LDS store), a halo of the span's next bytes, a zero pad, then every row's pad dwords.
+__device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
+                                            const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
+                                            const uint32_t hi) {
+  const uint32_t t1 = sd.first_tile + sd.n_tiles;
+  {
+    // every lane issues its 8 loads before any LDS store (the tile is at most 512 x 16 B)
+    const uint32_t words = (hi + 15) >> 4;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
+    constexpr int kLoads = (int)(kZTile / 16 / 64);
+    u32x4 v[kLoads];
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {  // branch-free: lanes past the tile re-read its last word
+      const uint32_t w = lane + 64u * (uint32_t)i;
+      v[i] = src[w < words ? w : words - 1u];
+    }
+#pragma unroll
+    for (int i = 0; i < kLoads; ++i) {
+      const uint32_t w = lane + 64u * (uint32_t)i;
+      if (w < words) {
+        uint32_t* d = s_img + (w >> 3) * kZPitch + 4u * (w & 7u);
+        d[0] = v[i].x;
+        d[1] = v[i].y;
+        d[2] = v[i].z;
+        d[3] = v[i].w;
+      }
+    }
+  }
+  const uint64_t after = td.span_off + td.len;
+  const uint64_t rem = sd.len > after ? sd.len - after : 0;
+  const uint32_t halo = rem < (uint64_t)kZHalo ? (uint32_t)rem : kZHalo;
+  const uint32_t img_end = hi + halo;
+  __syncthreads();
+  {
+    uint8_t* bb = reinterpret_cast<uint8_t*>(s_img);
+    if (lane < halo) {
+      uint64_t o = after + lane;  // span offset of the halo byte
+      uint32_t k = t + 1;
+      while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+      const TileDesc nt = tiles[k];
+      bb[rb(hi + lane)] = gp(nt.abase)[nt.delta + (uint32_t)(o - nt.span_off)];
+    }
+    bb[rb(img_end + lane)] = 0;  // zero pad (64 bytes) so 16-byte reads near the end are defined
+  }
+  __syncthreads();
+  for (uint32_t i = lane; i < (kZRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
+    const uint32_t row = i / kZPad, j = i - row * kZPad;
+    s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
+  }
+  __syncthreads();
+
+}
+
+// ---------------------------------------------------------------------------------
+// One 64-lane workgroup decodes one tile at a time (persistent grid, below).
+// ---------------------------------------------------------------------------------
+// Pass 1 for one tile: stage, chain, then the tile's record / wide-record counts and its
+// record-start bitmap (1 KiB) for the emit pass.  false once the batch has aborted.
+__device__ __forceinline__ bool count_tile(const uint32_t t, const TileDesc* __restrict__ tiles,
+                                           const SpanDesc* __restrict__ spans, const FusedCtl& ctl,
+                                           uint32_t* s_img, const uint32_t lane) {
+#define ZPHASE(i) \
+  if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
+  ZPHASE(0);
+  const TileDesc td = tiles[t];
+  const SpanDesc sd = spans[td.span];
+  const uint32_t t1 = sd.first_tile + sd.n_tiles;
+  const bool nodep = ctl.nodep != 0;  // developer timing mode: no cross-tile dependencies
+  const bool first = nodep || t == sd.first_tile, last = !nodep && t + 1 == t1;
+  const uint32_t lo = td.delta, hi = td.delta + td.len;
+  const uint64_t ea = sd.len - td.span_off + td.delta;
+  const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
+
+  stage_image(td, sd, t, tiles, s_img, lane, hi);
+
+  ZPHASE(1);
+  // ---- 1. speculative walk of the lane's region
+  const uint32_t r0 = lane * kZRegion;
+  const uint32_t rs = r0 < lo ? lo : (r0 > hi ? hi : r0);
+  const uint32_t re = r0 + kZRegion > hi ? hi : r0 + kZRegion;
+  const uint32_t ws = rs >= lo + kZWarm ? rs - kZWarm : lo;
+  const Spec sp = rs < re ? spec_walk(s_img, ws, rs, re, end_a) : Spec{{0, 0}, {0, 0}, rs, rs, 0};
+
+  ZPHASE(2);
+  // ---- 2. canonical exit: the speculative rule from the tile start, through every
+  // region (entries = previous lane's exit; lanes whose entry changed re-merge)
+  // Each lane keeps its true-rule merge result r (the canonical chain re-used by step 4
+  // unless its entry changes); the canonical exit cx follows the speculative rule only
+  // where r met a record the two rules treat differently (invalid, or longer than
+  // kZSpecMax).
+  uint32_t cx = sp.exit, x_pub = 0, entry = kZCanon;
+  Res r{sp.bm, sp.wb, sp.exit, 0, 0};
+  if (!first) {
+    for (int it = 0; it <= 64; ++it) {
+      const uint32_t prev = __shfl_up(cx, 1);
+      const uint32_t want = lane == 0 ? kZCanon : prev;
+      const bool ch = want != entry;
+      if (!__any(ch)) break;
+      if (ch) {
+        entry = want;
+        r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp) : Res{{0, 0}, {0, 0}, want, 0, 0};
+        cx = (r.bad | r.unclean) ? canon_walk(s_img, rs, re, end_a, want, sp) : r.exit;
+      }
+    }
+    x_pub = __shfl(cx, 63);
+    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (td.span_off + (x_pub - lo)));
+  }
+
+  ZPHASE(3);
+  // ---- 3. true entry: the span start, or the predecessor's published exit
+  uint32_t e_true;
+  if (first) {
+    e_true = lo;  // a span starts on a record boundary
+  } else {
+    uint64_t v;
+    uint32_t nb = 1;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (;;) {
+      v = ld_agent(&ctl.st_x[t - 1]);
+      if (v) break;
+      if (ld_agent32(ctl.abort)) return false;
+      if (!backoff(nb, t0)) {
+        if (lane == 0) raise_abort(ctl, 4, t);
+        return false;
+      }
+    }
+    const uint64_t xs = v & ~(1ull << 63);  // predecessor's exit, span offset (>= td.span_off)
+    const uint64_t ee = xs - td.span_off + lo;
+    e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+  }
+
+  ZPHASE(4);
+  // ---- 4. true chain: every lane merges from its guessed entry (the canonical one),
+  // then lanes whose entry changed re-merge until the chain is consistent
+  if (first) {  // no canonical pass: entries guessed from the speculative exits
+    const uint32_t guess = __shfl_up(sp.exit, 1);
+    entry = lane == 0 ? e_true : guess;
+    r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  }
+  for (int it = 0; it <= 64; ++it) {
+    const uint32_t prev = __shfl_up(r.exit, 1);
+    const uint32_t want = lane == 0 ? e_true : prev;
+    const bool ch = want != entry;
+    if (!__any(ch)) break;
+    if (ch) {
+      entry = want;
+      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp) : Res{{0, 0}, {0, 0}, want, 0, 0};
+    }
+  }
+  const uint32_t canon_exit = cx, canon_bad = 0;
+  const uint32_t x_true = __shfl(r.exit, 63);
+  uint32_t reason = __any(r.bad) ? 1u : 0u;  // the true chain meets an invalid / Serializable record
+  if (last) {
+    if (x_true != end_a) reason = reason ? reason : 2u;  // the last record must end at the span end
+  } else if (first) {
+    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (td.span_off + (x_true - lo)));
+  } else if (x_true != x_pub) {
+    reason = reason ? reason : 3u;  // the successor already entered at the published exit
+  }
+  if (reason && ctl.dbg) {  // developer diagnostics: the first aborting tile's lane state
+    uint32_t claim = 0;
+    if (lane == 0) claim = atomicCAS(ctl.dbg, 0u, 1u) == 0u ? 1u : 0u;
+    if (__shfl(claim, 0)) {
+      if (lane == 0) {
+        ctl.dbg[1] = t; ctl.dbg[2] = reason; ctl.dbg[3] = x_pub; ctl.dbg[4] = x_true; ctl.dbg[5] = e_true;
+        ctl.dbg[6] = lo; ctl.dbg[7] = hi; ctl.dbg[8] = end_a;
+      }
+      uint32_t* d = ctl.dbg + 16 + 8 * lane;
+      d[0] = rs; d[1] = re; d[2] = sp.exit; d[3] = sp.bad; d[4] = canon_exit; d[5] = canon_bad; d[6] = entry;
+      d[7] = r.exit | r.bad << 31;
+    }
+  }
+  if (reason && !nodep) {
+    if (lane == 0) raise_abort(ctl, reason, t);
+    return false;
+  }
+
+  ZPHASE(5);
+  // ---- counts and the record-start bitmap for the emit pass
+  uint32_t rec = bcount(r.bm), wide = bcount(r.wb);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    rec += __shfl_xor(rec, off);
+    wide += __shfl_xor(wide, off);
+  }
+  if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(rec, wide);
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  u64x2 bits;
+  bits.x = r.bm.lo;
+  bits.y = r.bm.hi;
+  gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = bits;
+  ZPHASE(6);
+#undef ZPHASE
+  return true;
+}
+
+// ---------------------------------------------------------------------------------
+// Pass 2: exclusive scan of the per-tile counts (one workgroup), and each span's range.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_decode_scan(const SpanDesc* __restrict__ spans, uint32_t n_spans,
+                                                      FusedCtl ctl) {
+  __shared__ uint64_t s_sum[1024];
+  if (ld_agent32(ctl.abort)) return;
+  const uint32_t nt = ctl.n_tiles, tid = threadIdx.x;
+  const uint32_t per = (nt + 1023u) / 1024u, b0 = tid * per, b1 = min(nt, b0 + per);
+  uint64_t sum = 0;
+  for (uint32_t i = b0; i < b1; ++i) sum += gp(ctl.cnt)[i];
+  s_sum[tid] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024u; off <<= 1) {
+    const uint64_t y = tid >= off ? s_sum[tid - off] : 0ull;
+    __syncthreads();
+    s_sum[tid] += y;
+    __syncthreads();
+  }
+  uint64_t run = s_sum[tid] - sum;  // exclusive
+  for (uint32_t i = b0; i < b1; ++i) {
+    gp(ctl.base)[i] = run;
+    run += gp(ctl.cnt)[i];
+  }
+  if (tid == 1023u) gp(ctl.base)[nt] = s_sum[1023];
+  __syncthreads();
+  __threadfence_block();
+  for (uint32_t sp = tid; sp < n_spans; sp += 1024u) {
+    const SpanDesc sd = spans[sp];
+    gp(ctl.span_lo)[sp] = gp(ctl.base)[sd.first_tile];
+    gp(ctl.span_hi)[sp] = gp(ctl.base)[sd.first_tile + sd.n_tiles];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Pass 3 for one tile: record starts dropped into LDS by output index (from the bitmap),
+// then consecutive lanes decode consecutive records, so each SoA store of the wave is one
+// contiguous run.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                    FusedCtl ctl, DecodeOut out) {
+  __shared__ uint32_t s_img[kZImgDw];
+  __shared__ uint16_t s_pos[kZWin];
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  if (ld_agent32(ctl.abort)) return;
+  const TileDesc td = tiles[t];
+  const SpanDesc sd = spans[td.span];
+  const uint32_t lo = td.delta, hi = td.delta + td.len;
+  const uint64_t ea = sd.len - td.span_off + td.delta;
+  const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
+  const uint64_t base = gp(ctl.base)[t];
+  stage_image(td, sd, t, tiles, s_img, lane, hi);
+  const uint32_t r0 = lane * kZRegion;
+  const uint32_t rs = r0 < lo ? lo : (r0 > hi ? hi : r0);
+  const uint32_t cnt = (uint32_t)(__popcll(bits.x) + __popcll(bits.y));
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += y;
+  }
+  const uint32_t total = __shfl(incl, 63);
+  const uint64_t rec0 = base & ((1ull << 31) - 1), wide0 = base >> 31;
+  Bits cur{bits.x, bits.y};
+  uint32_t idx = incl - cnt;
+  uint64_t wide = wide0;
+  for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
+    const uint32_t wend = w0 + kZWin;
+    while ((cur.lo | cur.hi) && idx < wend) {
+      const uint32_t i = cur.lo ? (uint32_t)__builtin_ctzll(cur.lo) : 64u + (uint32_t)__builtin_ctzll(cur.hi);
+      if (cur.lo) cur.lo &= cur.lo - 1; else cur.hi &= cur.hi - 1;
+      s_pos[idx - w0] = (uint16_t)(rs + i);
+      ++idx;
+    }
+    __syncthreads();
+    const uint32_t nw = total - w0 < kZWin ? total - w0 : kZWin;
+    for (uint32_t i0 = 0; i0 < nw; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool act = i < nw;
+      const uint32_t a = act ? (uint32_t)s_pos[i] : lo;
+      const uint32_t kk = rk(a >> 2), sh = 8u * (a & 3u);
+      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
+      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
+      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+      uint32_t tg = x0 & 0xFFu;
+      const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
+      int64_t v0 = tg == CLG_TAG_ORDER       ? (int64_t)(int8_t)(blo & 0xFFu)
+                   : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)bhi << 32 | blo)
+                                             : (int64_t)(int32_t)__builtin_bswap32(blo);
+      const bool wide_rec = act && is_wide((int)tg);
+      Rec rr{};
+      if (wide_rec) {
+        const ZBytes b{s_img, a};
+        int tagd;
+        uint32_t tgu;
+        const int L = zlen(s_img, a, end_a, &tgu);
+        tagd = (int)tgu;
+        decode_fields(b, tagd, (int64_t)L, rr);
+        v0 = rr.v0;
+      }
+      const uint64_t wm = __ballot(wide_rec);
+      const uint64_t g = rec0 + w0 + i;
+      if (act) {
+        const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+        if (g < out.cap) {
+          gp(out.off)[g] = so;
+          gp(out.tag)[g] = (uint8_t)tg;
+          gp(out.v0)[g] = v0;
+        }
+        if (wide_rec) {
+          const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+          if (wi < out.wcap) {
+            gp(out.w_idx)[wi] = (uint32_t)g;
+            gp(out.w_rc)[wi] = rr.rc;
+            gp(out.w_v1)[wi] = rr.v1;
+            gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
+            gp(out.w_var_len)[wi] = rr.var_len;
+            gp(out.w_sub)[wi] = rr.sub;
+          }
+        }
+      }
+      wide += (uint64_t)__popcll(wm);
+    }
+    __syncthreads();
+  }
+}
+
+// Persistent: the grid is at most what the device keeps resident (launch_decode_fused),
+// and block b takes tiles b, b + G, b + 2G, ...  Every wait is on a lower tile, whose
+// block is resident and never waits on a higher one, so the waits always end; a wait
+// that still runs past kZSpinLimit cycles aborts the batch instead of hanging.
+__global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                     FusedCtl ctl) {
+  __shared__ uint32_t s_img[kZImgDw];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
+    if (!count_tile(t, tiles, spans, ctl, s_img, lane)) return;
+    __syncthreads();  // the image is reused by the next tile
+  }
+}
+
+int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase) {
+  if (!n_tiles) return CLG_OK;
+  ctl.n_tiles = n_tiles;
+  hipStream_t st = (hipStream_t)stream;
+  if (phase == 0) {
+    static int resident = 0;  // blocks the device keeps resident for the count kernel
+    if (!resident) {
+      int dev = 0, per_cu = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count, 64, 0) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+        return CLG_E_DEVICE;
+      resident = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
+    }
+    const uint32_t grid = n_tiles < (uint32_t)resident ? n_tiles : (uint32_t)resident;
+    hipLaunchKernelGGL(k_decode_count, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+  } else if (phase == 1) {
+    hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, st, d_spans, n_spans, ctl);
+  } else {
+    hipLaunchKernelGGL(k_decode_emit, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+  }
+  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+}
+
+}  // namespace clg

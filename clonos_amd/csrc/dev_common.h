@@ -9,6 +9,19 @@
 
 namespace clg {
 
+// Global-address-space views of pointers that arrive inside structs: without them the
+// compiler emits flat loads/stores, whose counters force a full wait before every LDS
+// access and serialise staging and emission.
+#define CLG_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ CLG_GLOBAL T* gp(T* p) {
+  return (CLG_GLOBAL T*)(p);
+}
+template <class T>
+__device__ __forceinline__ const CLG_GLOBAL T* gp(const T* p) {
+  return (const CLG_GLOBAL T*)(p);
+}
+
 // ----------------------------------------------------------------------------------
 // Packed region-table entry: exit offset past the region end (16 bits, 0xFFFF = error,
 // 0xFFFE = far), record count (8 bits), wide-record count (8 bits).
@@ -194,6 +207,30 @@ __device__ __forceinline__ uint64_t fld_be64(const F& b, uint32_t k) {
 }
 __device__ __forceinline__ uint32_t fld_be32(const LdsBytes& b, uint32_t k) { return t_be32(b.T, b.base + k); }
 __device__ __forceinline__ uint64_t fld_be64(const LdsBytes& b, uint32_t k) { return t_be64(b.T, b.base + k); }
+
+// ---------------------------------------------------------------------------------
+// Dense LDS image accessors.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t d_u8(const uint32_t* T, uint32_t a) {
+  return reinterpret_cast<const uint8_t*>(T)[a];
+}
+__device__ __forceinline__ uint32_t d_be32(const uint32_t* T, uint32_t a) {
+  const uint32_t k = a >> 2;
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(T[k + 1], T[k], a & 3u));
+}
+__device__ __forceinline__ uint64_t d_be64(const uint32_t* T, uint32_t a) {
+  const uint32_t k = a >> 2, s = a & 3u;
+  const uint32_t d0 = T[k], d1 = T[k + 1], d2 = T[k + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, s), hi = __builtin_amdgcn_alignbyte(d2, d1, s);
+  return __builtin_bswap64((uint64_t)hi << 32 | lo);
+}
+struct DenseBytes {
+  const uint32_t* T;
+  uint32_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) const { return (int)d_u8(T, base + (uint32_t)k); }
+};
+__device__ __forceinline__ uint32_t fld_be32(const DenseBytes& b, uint32_t k) { return d_be32(b.T, b.base + k); }
+__device__ __forceinline__ uint64_t fld_be64(const DenseBytes& b, uint32_t k) { return d_be64(b.T, b.base + k); }
 
 // Exact length of a non-Serializable record through a byte accessor (inline, no calls):
 // L > 0, kLenErr on any decode error (truncation, bad enum, negative length, bad tag),

@@ -172,10 +172,12 @@ struct clg_engine {
   std::recursive_mutex mu;
 
   // staging / scratch
-  PinBuf h_stage, h_desc;
+  PinBuf h_stage, h_desc, h_sres, h_zres;
   DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
+  DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
+  bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
   // timing
   std::map<std::string, Stat> stats;
@@ -598,22 +600,23 @@ struct clg_engine {
     std::vector<clg::SegSpan> runs;     // log spans: tiles generated on the device
     std::vector<uint32_t> segtab;       // concatenated segment indices of the runs' logs
     uint32_t n_tiles = 0;
+    uint32_t unit = 0;                  // device-planning tile window
   };
 
-  // Tile window for device planning: min(segment, kTile) when one divides the other.
-  uint32_t tile_unit() const {
-    const uint32_t c = C(), k = uint32_t(clg::kTile);
+  // Tile window for device planning: min(segment, tile) when one divides the other.
+  uint32_t tile_unit(uint32_t k) const {
+    const uint32_t c = C();
     if (c <= k) return (k % c == 0) ? c : 0;
     return (c % k == 0) ? k : 0;
   }
 
-  void plan_host_span(DecodePlan& p, const uint8_t* dbase, uint64_t len, uint32_t s) {
+  void plan_host_span(DecodePlan& p, const uint8_t* dbase, uint64_t len, uint32_t s, uint32_t T) {
     clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, len};
     uint64_t o = 0;
     while (o < len) {
       const uintptr_t addr = uintptr_t(dbase + o);
       const uint32_t delta = uint32_t(addr & 15);
-      const uint32_t take = uint32_t(std::min<uint64_t>(len - o, uint64_t(clg::kTile - delta)));
+      const uint32_t take = uint32_t(std::min<uint64_t>(len - o, uint64_t(T - delta)));
       p.tiles.push_back(clg::TileDesc{reinterpret_cast<const uint8_t*>(addr & ~uintptr_t(15)), delta, take, s, 0, o});
       o += take;
       sd.n_tiles++;
@@ -622,8 +625,9 @@ struct clg_engine {
     p.n_tiles = uint32_t(p.tiles.size());
   }
 
-  void plan_log_span(DecodePlan& p, const Log& l, int32_t start, int32_t len, uint32_t s) {
-    if (const uint32_t U = tile_unit()) {  // device planning
+  void plan_log_span(DecodePlan& p, const Log& l, int32_t start, int32_t len, uint32_t s, uint32_t T) {
+    p.unit = tile_unit(T);
+    if (const uint32_t U = p.unit) {  // device planning
       const uint32_t cnt = len > 0 ? (uint32_t(start + len - 1) / U - uint32_t(start) / U + 1) : 0;
       p.spans.push_back(clg::SpanDesc{p.n_tiles, cnt, uint64_t(len)});
       if (cnt) {
@@ -644,7 +648,7 @@ struct clg_engine {
       while (done < take) {
         const uint32_t o = so + done;
         const uint32_t delta = o & 15;
-        const uint32_t t = std::min<uint32_t>(take - done, uint32_t(clg::kTile) - delta);
+        const uint32_t t = std::min<uint32_t>(take - done, T - delta);
         p.tiles.push_back(clg::TileDesc{seg_addr(l.segs[si]) + (o & ~15u), delta, t, s, 0, uint64_t(ph - start + int32_t(done))});
         done += t;
         sd.n_tiles++;
@@ -655,16 +659,213 @@ struct clg_engine {
     p.n_tiles = uint32_t(p.tiles.size());
   }
 
-  int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+  static void reset_result(clg_decoded* out) {
     out->n_rec = out->n_wide = 0;
     out->err_status = CLG_OK;
     out->err_span = 0;
     out->err_off = -1;
     out->err_tag = 0;
+  }
+
+  // Uploads the plan's descriptors (spans into d_spans) and materialises its tiles in
+  // `dtiles` (device planning from the segment table, or the host-built list).
+  int upload_plan(DecodePlan& p, DevBuf& dtiles) {
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    CHK(dtiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
+    CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
+    const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
+                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
+    const size_t o_runs = (tb + 15) & ~size_t(15), o_seg = (o_runs + rb + 15) & ~size_t(15),
+                 o_spans = (o_seg + gb + 15) & ~size_t(15), hb = o_spans + sb;
+    CHK(h_desc.ensure(hb + 64));
+    CHK(d_desc.ensure(hb));
+    uint8_t* hd = h_desc.as<uint8_t>();
+    memcpy(hd, p.tiles.data(), tb);
+    memcpy(hd + o_runs, p.runs.data(), rb);
+    memcpy(hd + o_seg, p.segtab.data(), gb);
+    memcpy(hd + o_spans, p.spans.data(), sb);
+    HIPCHK(hipMemcpyAsync(d_desc.p, hd, hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_spans.p, d_desc.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
+    if (!p.runs.empty()) {
+      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_desc.as<uint8_t>() + o_runs),
+                                   uint32_t(p.runs.size()), nt,
+                                   reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
+                                   p.unit, dtiles.as<clg::TileDesc>(), stream));
+    } else if (tb) {
+      HIPCHK(hipMemcpyAsync(dtiles.p, d_desc.p, tb, hipMemcpyDeviceToDevice, stream));
+    }
+    return CLG_OK;
+  }
+
+  // Output arrays the kernels write: the caller's device arrays, or engine scratch that
+  // finish_out copies to the caller's host arrays.
+  int prep_out(clg_decoded* out, clg::DecodeOut* o) {
+    const bool dev = out->out_kind == CLG_MEM_DEVICE;
+    if (dev) {
+      *o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
+                         out->w_var_len, out->w_sub, out->cap, out->wcap};
+    } else {
+      const size_t cap = std::max<uint64_t>(1, out->cap), wcap = std::max<uint64_t>(1, out->wcap);
+      CHK(d_o_off.ensure(cap * 4));
+      CHK(d_o_tag.ensure(cap));
+      CHK(d_o_v0.ensure(cap * 8));
+      CHK(d_o_widx.ensure(wcap * 4));
+      CHK(d_o_wrc.ensure(wcap * 4));
+      CHK(d_o_wv1.ensure(wcap * 8));
+      CHK(d_o_wvo.ensure(wcap * 4));
+      CHK(d_o_wvl.ensure(wcap * 4));
+      CHK(d_o_wsub.ensure(wcap));
+      *o = clg::DecodeOut{d_o_off.as<uint32_t>(), d_o_tag.as<uint8_t>(), d_o_v0.as<int64_t>(), d_o_widx.as<uint32_t>(),
+                         d_o_wrc.as<int32_t>(), d_o_wv1.as<int64_t>(), d_o_wvo.as<uint32_t>(), d_o_wvl.as<uint32_t>(),
+                         d_o_wsub.as<uint8_t>(), out->cap, out->wcap};
+    }
+    return CLG_OK;
+  }
+
+  int finish_out(clg_decoded* out, uint64_t nrec, uint64_t nwide) {
+    out->n_rec = nrec;
+    out->n_wide = nwide;
+    if (out->out_kind != CLG_MEM_DEVICE) {
+      const uint64_t r = std::min(nrec, out->cap), w = std::min(nwide, out->wcap);
+      if (r) {
+        HIPCHK(hipMemcpyAsync(out->off, d_o_off.p, r * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->tag, d_o_tag.p, r, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->v0, d_o_v0.p, r * 8, hipMemcpyDeviceToHost, stream));
+      }
+      if (w) {
+        HIPCHK(hipMemcpyAsync(out->w_idx, d_o_widx.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_rc, d_o_wrc.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_v1, d_o_wv1.p, w * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_var_off, d_o_wvo.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_var_len, d_o_wvl.p, w * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(out->w_sub, d_o_wsub.p, w, hipMemcpyDeviceToHost, stream));
+      }
+    }
+    CHK(sync());
+    if (nrec > out->cap || nwide > out->wcap)
+      return fail(CLG_E_CAPACITY, "decode produced %llu records / %llu wide rows, capacity %llu / %llu",
+                  (unsigned long long)nrec, (unsigned long long)nwide, (unsigned long long)out->cap,
+                  (unsigned long long)out->wcap);
+    return CLG_OK;
+  }
+
+  // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
+  // anything outside its fast path; the caller then runs the robust pipeline.
+  int run_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted) {
+    *aborted = false;
+    reset_result(out);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     if (ns == 0) return CLG_OK;
-    CHK(d_tiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
-    CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
+    CHK(upload_plan(p, d_ztiles));
+    clg::DecodeOut o{};
+    CHK(prep_out(out, &o));
+    // words: st_x[nt] cnt[nt] base[nt + 1] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
+    const size_t o_span = 3 * size_t(nt) + 1, o_ab = o_span + 2 * size_t(ns), words = o_ab + 4;
+    CHK(d_zctl.ensure(words * 8));
+    CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
+    CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
+    uint64_t* w = d_zctl.as<uint64_t>();
+    uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
+    const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
+    if (zdbg) {
+      CHK(d_dbg.ensure(16 * 4 + 64 * 32));
+      HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
+    }
+    const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
+    if (prof_path) {
+      CHK(d_prof.ensure(size_t(nt) * 64));
+      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
+    }
+    clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span, w + o_span + ns, ab,
+                      zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
+                      getenv("CLONOS_FUSED_NODEP") ? 1u : 0u};
+    HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
+    HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
+    auto* zt = d_ztiles.as<clg::TileDesc>();
+    auto* zs = d_spans.as<clg::SpanDesc>();
+    CHK(timed("decode_count", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 0); }));
+    CHK(timed("decode_offsets", 24 * uint64_t(nt), [&] {
+      return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 1);
+    }));
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (cfg.flags & CLG_F_TIMING) {
+      ea = get_event();
+      eb = get_event();
+      hipEventRecord(ea, stream);
+    }
+    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
+    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
+    uint64_t* hz = h_zres.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (prof_path) {
+      std::vector<uint64_t> hp(size_t(nt) * 8);
+      hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
+      if (FILE* fp = fopen(prof_path, "wb")) {
+        fwrite(hp.data(), 8, hp.size(), fp);
+        fclose(fp);
+      }
+    }
+    const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
+    if (hab[0]) {
+      *aborted = true;
+      if (getenv("CLONOS_FUSED_DEBUG"))
+        fprintf(stderr, "[clonos] fused decode aborted (%u tiles): first tile per reason bad=%d end=%d exit=%d timeout=%d\n",
+                nt, int(~hab[1]), int(~hab[2]), int(~hab[3]), int(~hab[4]));
+      if (zdbg) {
+        std::vector<uint32_t> hd(16 + 64 * 8);
+        hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
+        fprintf(stderr, "[clonos] tile %u reason %u x_pub %u x_true %u e_true %u lo %u hi %u end_a %u\n", hd[1], hd[2],
+                hd[3], hd[4], hd[5], hd[6], hd[7], hd[8]);
+        for (int l = 0; l < 64; ++l) {
+          const uint32_t* d = &hd[16 + 8 * l];
+          fprintf(stderr, "  lane %2d rs %5u re %5u spec_exit %5u spec_bad %5u canon_exit %5u canon_bad %u entry %5u exit %5u bad %u\n",
+                  l, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7] & 0x7FFFFFFFu, d[7] >> 31);
+        }
+      }
+      if (ea) {
+        ev_pool.push_back(ea);
+        ev_pool.push_back(eb);
+      }
+      return CLG_OK;
+    }
+    constexpr uint64_t kRecMask = (1ull << 31) - 1;
+    uint64_t nrec = 0, nwide = 0;
+    const std::vector<clg::SpanDesc>& sp = p.spans;
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (span_rec_base) span_rec_base[s] = nrec;
+      if (sp[s].n_tiles == 0) continue;
+      const uint64_t a = hz[s], b = hz[ns + s];
+      nrec += (b & kRecMask) - (a & kRecMask);
+      nwide += (b >> 31) - (a >> 31);
+    }
+    if (span_rec_base) span_rec_base[ns] = nrec;
+    if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    return finish_out(out, nrec, nwide);
+  }
+
+  // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
+  // tile_bytes)` fills a plan for the given tile geometry.
+  template <class Build>
+  int decode(Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+    // fused counts are packed in 31-bit fields: at most log_bytes / 2 records
+    if (fused_decode && log_bytes / 2 < (1ull << 31)) {
+      DecodePlan pf;
+      build(pf, clg::kZTile);
+      bool aborted = false;
+      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted));
+      if (!aborted) return CLG_OK;
+      stats["decode_fallback"].launches++;
+    }
+    DecodePlan p;
+    build(p, uint32_t(clg::kTile));
+    return run_decode(p, log_bytes, out, span_rec_base);
+  }
+
+  int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+    reset_result(out);
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    if (ns == 0) return CLG_OK;
     CHK(d_agg.ensure(std::max<size_t>(1, nt) * clg::kEntries * sizeof(uint64_t)));
     CHK(d_conv.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileConv)));
     CHK(d_tres.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileRes)));
@@ -679,50 +880,10 @@ struct clg_engine {
     CHK(d_jlen.ensure(std::max<size_t>(1, nt) * clg::kJserCap * sizeof(uint32_t)));
     CHK(d_jn.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
     CHK(d_defer.ensure(std::max<size_t>(1, nt) * sizeof(uint32_t)));
-    // descriptors: host tiles (staged input) or runs + segment table (log spans)
-    const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
-                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
-    const size_t o_runs = (tb + 15) & ~size_t(15), o_seg = (o_runs + rb + 15) & ~size_t(15),
-                 o_spans = (o_seg + gb + 15) & ~size_t(15), hb = o_spans + sb;
-    CHK(h_desc.ensure(hb + ns * sizeof(clg::SpanRes) + 64));
-    CHK(d_desc.ensure(hb));
-    uint8_t* hd = h_desc.as<uint8_t>();
-    memcpy(hd, p.tiles.data(), tb);
-    memcpy(hd + o_runs, p.runs.data(), rb);
-    memcpy(hd + o_seg, p.segtab.data(), gb);
-    memcpy(hd + o_spans, p.spans.data(), sb);
-    HIPCHK(hipMemcpyAsync(d_desc.p, hd, hb, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(d_spans.p, d_desc.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
-    if (!p.runs.empty()) {
-      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_desc.as<uint8_t>() + o_runs),
-                                   uint32_t(p.runs.size()), nt,
-                                   reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
-                                   tile_unit(), d_tiles.as<clg::TileDesc>(), stream));
-    } else if (tb) {
-      HIPCHK(hipMemcpyAsync(d_tiles.p, d_desc.p, tb, hipMemcpyDeviceToDevice, stream));
-    }
-
-    // outputs
+    CHK(upload_plan(p, d_tiles));
+    CHK(h_sres.ensure(ns * sizeof(clg::SpanRes) + 64));
     clg::DecodeOut o{};
-    const bool dev = out->out_kind == CLG_MEM_DEVICE;
-    if (dev) {
-      o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
-                         out->w_var_len, out->w_sub, out->cap, out->wcap};
-    } else {
-      const size_t cap = std::max<uint64_t>(1, out->cap), wcap = std::max<uint64_t>(1, out->wcap);
-      CHK(d_o_off.ensure(cap * 4));
-      CHK(d_o_tag.ensure(cap));
-      CHK(d_o_v0.ensure(cap * 8));
-      CHK(d_o_widx.ensure(wcap * 4));
-      CHK(d_o_wrc.ensure(wcap * 4));
-      CHK(d_o_wv1.ensure(wcap * 8));
-      CHK(d_o_wvo.ensure(wcap * 4));
-      CHK(d_o_wvl.ensure(wcap * 4));
-      CHK(d_o_wsub.ensure(wcap));
-      o = clg::DecodeOut{d_o_off.as<uint32_t>(), d_o_tag.as<uint8_t>(), d_o_v0.as<int64_t>(), d_o_widx.as<uint32_t>(),
-                         d_o_wrc.as<int32_t>(), d_o_wv1.as<int64_t>(), d_o_wvo.as<uint32_t>(), d_o_wvl.as<uint32_t>(),
-                         d_o_wsub.as<uint8_t>(), out->cap, out->wcap};
-    }
+    CHK(prep_out(out, &o));
     auto* dt = d_tiles.as<clg::TileDesc>();
     auto* ds = d_spans.as<clg::SpanDesc>();
     auto* flags = d_flags.as<uint32_t>();
@@ -737,7 +898,7 @@ struct clg_engine {
       prof = d_prof.as<uint64_t>();
       hipMemsetAsync(prof, 0, size_t(nt) * 64, stream);
     }
-    CHK(timed("decode_scan", log_bytes, [&] {
+    CHK(timed("robust_scan", log_bytes, [&] {
       return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 0, d_lanes.as<clg::LaneSeg>(),
                                    d_sums.as<clg::TileSum>(), dbg, prof, stream);
     }));
@@ -750,25 +911,25 @@ struct clg_engine {
         fclose(fp);
       }
     }
-    CHK(timed("decode_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
-    CHK(timed("decode_scan_deferred", 0, [&] {
+    CHK(timed("robust_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
+    CHK(timed("robust_scan_deferred", 0, [&] {
       return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, d_lanes.as<clg::LaneSeg>(),
                                    d_sums.as<clg::TileSum>(), dbg, nullptr, stream);
     }));
-    CHK(timed("decode_resolve", uint64_t(nt) * 32, [&] {
+    CHK(timed("robust_resolve", uint64_t(nt) * 32, [&] {
       return clg::launch_fast_resolve(ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
                                       d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags,
                                       stream);
     }));
     // robust DP pipeline for flagged spans only (early exit elsewhere)
-    CHK(timed("decode_dp_tables", 0, [&] {
+    CHK(timed("robust_dp_tables", 0, [&] {
       return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), flags, stream);
     }));
-    CHK(timed("decode_dp_resolve", 0, [&] {
+    CHK(timed("robust_dp_resolve", 0, [&] {
       return clg::launch_decode_resolve(dt, ds, ns, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(),
                                         d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), flags, stream);
     }));
-    CHK(timed("decode_spanscan", uint64_t(ns) * 48, [&] {
+    CHK(timed("robust_spanscan", uint64_t(ns) * 48, [&] {
       return clg::launch_decode_spanscan(d_sres.as<clg::SpanRes>(), ns, d_totals.as<uint64_t>(), stream);
     }));
     // emit bytes are attributed after the counts are known (below)
@@ -781,7 +942,7 @@ struct clg_engine {
     CHK(clg::launch_fast_emit(dt, nt, ds, d_fconv.as<uint32_t>(), J, d_lanes.as<clg::LaneSeg>(),
                               d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags, o, stream));
     if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
-    CHK(timed("decode_dp_emit", 0, [&] {
+    CHK(timed("robust_dp_emit", 0, [&] {
       return clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
                                      d_sres.as<clg::SpanRes>(), flags, o, stream);
     }));
@@ -807,7 +968,7 @@ struct clg_engine {
         fclose(fp);
       }
     }
-    clg::SpanRes* hres = reinterpret_cast<clg::SpanRes*>(hd + ((hb + 15) & ~size_t(15)));
+    clg::SpanRes* hres = h_sres.as<clg::SpanRes>();
     HIPCHK(hipMemcpyAsync(hres, d_sres.p, ns * sizeof(clg::SpanRes), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     uint64_t nrec = 0, nwide = 0;
@@ -824,30 +985,8 @@ struct clg_engine {
     }
     if (span_rec_base) span_rec_base[ns] = nrec;
     if (cfg.flags & CLG_F_TIMING)
-      timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
-    out->n_rec = nrec;
-    out->n_wide = nwide;
-    if (!dev) {
-      const uint64_t r = std::min(nrec, out->cap), w = std::min(nwide, out->wcap);
-      if (r) {
-        HIPCHK(hipMemcpyAsync(out->off, d_o_off.p, r * 4, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->tag, d_o_tag.p, r, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->v0, d_o_v0.p, r * 8, hipMemcpyDeviceToHost, stream));
-      }
-      if (w) {
-        HIPCHK(hipMemcpyAsync(out->w_idx, d_o_widx.p, w * 4, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->w_rc, d_o_wrc.p, w * 4, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->w_v1, d_o_wv1.p, w * 8, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->w_var_off, d_o_wvo.p, w * 4, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->w_var_len, d_o_wvl.p, w * 4, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(out->w_sub, d_o_wsub.p, w, hipMemcpyDeviceToHost, stream));
-      }
-    }
-    CHK(sync());
-    if (nrec > out->cap || nwide > out->wcap)
-      return fail(CLG_E_CAPACITY, "decode produced %llu records / %llu wide rows, capacity %llu / %llu",
-                  (unsigned long long)nrec, (unsigned long long)nwide, (unsigned long long)out->cap,
-                  (unsigned long long)out->wcap);
+      timings.push_back(PendingTiming{"robust_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    CHK(finish_out(out, nrec, nwide));
     if (out->err_status != CLG_OK)
       return fail(out->err_status, "decode error %d in span %u at offset %lld (tag %d)", out->err_status, out->err_span,
                   (long long)out->err_off, out->err_tag);
@@ -887,6 +1026,8 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   if (cfg->device < 0 || cfg->device >= ndev) return fail(CLG_E_INVALID_ARG, "device %d out of range", cfg->device);
   std::unique_ptr<clg_engine> e(new clg_engine());
   e->cfg = *cfg;
+  const char* dm = getenv("CLONOS_DECODE");
+  e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
@@ -1188,10 +1329,11 @@ int clg_decode_host(clg_engine* e, const uint8_t* bytes, const uint64_t* span_of
     memcpy(e->h_stage.p, bytes + lo, hi - lo);
     HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, hi - lo, hipMemcpyHostToDevice, e->stream));
   }
-  clg_engine::DecodePlan p;
-  for (uint32_t i = 0; i < n; ++i)
-    e->plan_host_span(p, e->d_stage.as<uint8_t>() + (span_len[i] ? span_off[i] - lo : 0), span_len[i], i);
-  return e->run_decode(p, total, out, span_rec_base);
+  auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
+    for (uint32_t i = 0; i < n; ++i)
+      e->plan_host_span(p, e->d_stage.as<uint8_t>() + (span_len[i] ? span_off[i] - lo : 0), span_len[i], i, T);
+  };
+  return e->decode(build, total, out, span_rec_base);
 }
 
 int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n, clg_decoded* out,
@@ -1199,17 +1341,18 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   ENGINE_GUARD(e);
   if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
   CHK(e->flush());
-  clg_engine::DecodePlan p;
+  std::vector<Log*> ls(n);
+  std::vector<int32_t> st(n), nb(n);
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    Log* l;
-    CHK(e->get_log(log[i], &l));
-    int32_t s = 0, nb = 0;
-    if (e->cfg.sharing_depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &s, &nb));
-    e->plan_log_span(p, *l, s, nb, i);
-    total += uint64_t(nb);
+    CHK(e->get_log(log[i], &ls[i]));
+    if (e->cfg.sharing_depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
+    total += uint64_t(nb[i]);
   }
-  return e->run_decode(p, total, out, span_rec_base);
+  auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
+    for (uint32_t i = 0; i < n; ++i) e->plan_log_span(p, *ls[i], st[i], nb[i], i, T);
+  };
+  return e->decode(build, total, out, span_rec_base);
 }
 
 int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off, const uint64_t* len,

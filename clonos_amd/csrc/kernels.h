@@ -154,6 +154,32 @@ int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
                      JserTabs J, const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
                      const uint32_t* d_span_flags, DecodeOut out, void* stream);
 
+// ---- fast decode (decode_fused.hip) -------------------------------------------------
+// Three passes over tiles of kZTile bytes (64 regions of kZRegion bytes, one per lane):
+// count (persistent grid, record chain + per-tile counts + record-start bitmaps), scan
+// (record / wide bases per tile and per span), emit (SoA).  Any anomaly raises *abort and
+// the host re-decodes the batch with the robust pipeline above.
+constexpr uint32_t kZRegion = 128;
+constexpr uint32_t kZTile = 64 * kZRegion;  // 8192
+constexpr uint32_t kZHalo = 64;             // bytes of the span's next tile staged after a tile
+
+struct FusedCtl {
+  uint64_t* st_x;     // per tile: 1<<63 | exit (span offset) the successor enters at
+  uint64_t* cnt;      // per tile: wide<<31 | records
+  uint64_t* base;     // per tile + 1: exclusive prefix of cnt
+  uint64_t* bits;     // per tile: 64 x 16 B record-start bitmaps (lane l: region l)
+  uint64_t* span_lo;  // per span: base at its first tile
+  uint64_t* span_hi;  // per span: base past its last tile
+  uint32_t* abort;    // [8]: flag, then ~(first tile) per abort reason 1..4 (4 = wait timed out)
+  uint32_t* dbg;      // optional diagnostics (CLONOS_FUSED_DEBUG): first aborting tile's lane state
+  uint64_t* prof;     // optional per-tile phase stamps (CLONOS_SCAN_PHASES): s_memtime x 8
+  uint32_t n_tiles;
+  uint32_t nodep;     // developer timing mode (CLONOS_FUSED_NODEP): tiles independent, output invalid
+};
+// phase 0: count, 1: scan, 2: emit
+int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
+
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
 // segment.  Pieces are produced per slice request and split at segment boundaries.

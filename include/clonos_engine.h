@@ -87,7 +87,9 @@ typedef struct clg_config {
   uint32_t reserved;
 } clg_config;
 
-#define CLG_F_TIMING 1u /* record per-kernel HIP event timings (clg_kernel_stats) */
+#define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
+#define CLG_F_ROBUST_DECODE 2u /* skip the single-pass decode kernel; always use the robust
+                                  multi-pass pipeline (the fallback the fused kernel aborts to) */
 
 typedef struct clg_engine clg_engine;
 

@@ -1,0 +1,148 @@
+"""GPU: the fast decode path (decode_fused.hip: count / offsets / emit) on its own.
+
+Every case checks bit-exactness against the CPU oracle's sequential decodeNext loop AND
+which path produced the output: logs without Serializable records must be decoded by the
+fast path itself (no `decode_fallback`), logs it cannot handle (Serializable streams,
+decode errors, chains that never re-synchronise across a tile) must fall back to the
+robust pipeline and still match.
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+from clonos_amd import CausalLogID, Engine
+from clonos_amd import determinants as D
+from clonos_amd import synth
+from test_gpu_decode import assert_span_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def fell_back(eng) -> bool:
+    return "decode_fallback" in eng.kernel_stats()
+
+
+@pytest.fixture(params=[256, 16384])
+def feng(request):
+    e = Engine(segment_bytes=request.param, pool_segments=(1 << 26) // request.param, timing=True)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fused_random_no_serializable(feng, seed):
+    rng = np.random.default_rng(100 + seed)
+    buf = synth.random_log(20000, rng, allow_serializable=False)
+    dec = feng.decode_host(buf)
+    assert_span_equal(dec, 0, buf)
+    assert "decode_count" in feng.kernel_stats() and not fell_back(feng)
+
+
+def test_fused_config2_multi_span(feng):
+    rng = np.random.default_rng(synth.SEED_CONFIG2)
+    parts, spans, blob = [], [], b""
+    for i in range(9):
+        b, _ = synth.config2_log(int(rng.integers(0, 60000)) if i != 4 else 0, rng)
+        pad = int(rng.integers(0, 17))
+        blob += bytes(pad)
+        spans.append((len(blob), b.size))
+        blob += b.tobytes()
+        parts.append(b.tobytes())
+    dec = feng.decode_host(blob, spans)
+    for s, p in enumerate(parts):
+        assert_span_equal(dec, s, p)
+    assert dec.span_rec_base[-1] == dec.n_rec
+    assert not fell_back(feng)
+
+
+def test_fused_far_garbage_lengths(feng):
+    """Timestamps whose bytes look like a TimerTrigger with a huge name length: a
+    speculative chain that starts inside them must not jump past the tile."""
+    ts = []
+    for i in range(40000):
+        # 04 .. at byte 1, type byte 06 at +13 and a name length of ~0x0002_0000
+        ts.append(D.TimestampDeterminant(0x0400000000000000 | (i & 0xFFFF)))
+        ts.append(D.OrderDeterminant(6))
+        ts.append(D.RNGDeterminant(0x00020000 + i))
+    buf = b"".join(D.encode(r) for r in ts)
+    dec = feng.decode_host(buf)
+    assert_span_equal(dec, 0, buf)
+    assert not fell_back(feng)
+
+
+def test_fused_logs_in_hbm_after_truncation(feng):
+    rng = np.random.default_rng(31)
+    logs = []
+    for v in range(10):
+        log = feng.open_log(CausalLogID.main(v))
+        b, _ = synth.config2_log(int(rng.integers(1000, 40000)), rng)
+        log.processUpstreamDelta(b.tobytes(), 0, 0)
+        for ep in range(1, 4):
+            for _ in range(int(rng.integers(10, 500))):
+                log.appendDeterminant(synth.random_determinant(rng, allow_serializable=False), ep)
+        if v % 3 == 0:
+            log.notifyCheckpointComplete(2)
+        logs.append(log)
+    start = [int(rng.integers(0, 4)) for _ in logs]
+    expect = [log.getDeterminants(e) for log, e in zip(logs, start)]
+    dec = feng.decode_logs(logs, start)
+    for s, b in enumerate(expect):
+        assert_span_equal(dec, s, b)
+    assert not fell_back(feng)
+
+
+def test_fused_wide_records_side_table(feng):
+    rng = np.random.default_rng(9)
+    recs = []
+    for i in range(6000):
+        k = i % 5
+        if k == 0:
+            recs.append(D.TimerTriggerDeterminant(i, i * 3, D.INTERNAL, b"PTS"))
+        elif k == 1:
+            recs.append(D.SourceCheckpointDeterminant(i, i, i + 1, D.CHECKPOINT, b"ref" * (i % 7)))
+        elif k == 2:
+            recs.append(D.IgnoreCheckpointDeterminant(i, i * 7))
+        else:
+            recs.append(synth.random_determinant(rng, allow_serializable=False))
+    buf = b"".join(D.encode(r) for r in recs)
+    dec = feng.decode_host(buf)
+    assert_span_equal(dec, 0, buf)
+    assert not fell_back(feng)
+
+
+def test_fused_serializable_falls_back(feng):
+    rng = np.random.default_rng(3)
+    buf, _ = synth.config3_epoch(20000, rng)
+    dec = feng.decode_host(buf.tobytes())
+    assert_span_equal(dec, 0, buf.tobytes())
+    assert fell_back(feng)
+
+
+@pytest.mark.parametrize("n", [100, 5000, 30000])
+def test_fused_odd_chain_never_merges(feng, n):
+    """Timestamp (9 bytes) then Order(0) runs: the true chain sits on odd offsets, every
+    speculative chain on even ones.  Single tiles still settle; multi-tile spans abort."""
+    buf = D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * n
+    dec = feng.decode_host(buf)
+    st, r, _, _ = O.decode(buf)
+    assert st == 0 and dec.n_rec == n + 1
+    np.testing.assert_array_equal(dec.off, r["off"])
+
+
+def test_fused_device_output_large(feng):
+    """Many tiles (the decoupled look-back chain); with 256-byte segments every tile is
+    one segment, too short for the speculative chains to re-synchronise reliably, so
+    only the 16 KiB configuration must stay on the fused path."""
+    rng = np.random.default_rng(77)
+    logs = []
+    for v in range(16):
+        log = feng.open_log(CausalLogID.main(v))
+        b, _ = synth.config2_log(200_000, rng)
+        log.processUpstreamDelta(b.tobytes(), 0, 1)
+        logs.append(log)
+    expect = [log.getDeterminants(1) for log in logs]
+    dec = feng.decode_logs(logs, [1] * len(logs))
+    for s, b in enumerate(expect):
+        assert_span_equal(dec, s, b)
+    if feng.segment_bytes >= 8192:
+        assert not fell_back(feng)

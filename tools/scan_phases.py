@@ -1,5 +1,6 @@
-"""Developer diagnostics: per-phase cycle breakdown of k_fast_scan (s_memtime stamps,
-CLONOS_SCAN_PHASES) on the config-2 workload.  Not part of the product or the tests."""
+"""Developer diagnostics: per-phase cycle breakdown of the decode count kernel
+(s_memtime stamps, CLONOS_SCAN_PHASES) on the config-2 workload.  Not part of the product
+or the tests."""
 import os
 import sys
 
@@ -7,6 +8,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 out = "gpurun_out/scan_phases.bin"
+os.makedirs("gpurun_out", exist_ok=True)
 os.environ["CLONOS_SCAN_PHASES"] = out
 from clonos_amd import CausalLogID, Engine, synth  # noqa: E402
 
@@ -20,13 +22,26 @@ with Engine(segment_bytes=16384, pool_segments=nlogs * 400, timing=True) as eng:
         lg.processUpstreamDelta(b.tobytes(), 0, 1)
         logs.append(lg)
     for _ in range(3):
-        dec = eng.decode_logs(logs, [1] * nlogs)
-    print("n_rec", dec.n_rec, {k: round(v["ms"] / max(1, v["launches"]), 4) for k, v in eng.kernel_stats().items() if v["launches"]})
+        try:
+            dec = eng.decode_logs(logs, [1] * nlogs)
+            print("n_rec", dec.n_rec)
+        except Exception as e:  # CLONOS_FUSED_NODEP: output is invalid by design
+            print("decode:", str(e)[:120])
+    print( {k: round(v["ms"] / max(1, v["launches"]), 4) for k, v in eng.kernel_stats().items() if v["launches"]})
 p = np.fromfile(out, np.uint64).reshape(-1, 8).astype(np.int64)
 ok = (p[:, 0] > 0) & (p[:, 6] > 0)
-d = np.diff(p[ok][:, :7], axis=1)
-names = ["stage", "magic", "bfs", "keep", "parse", "chain+store"]
-tot = d.sum(axis=1)
-print("tiles", ok.sum(), "cycles/tile mean %.0f p50 %.0f p99 %.0f" % (tot.mean(), np.median(tot), np.percentile(tot, 99)))
+print("tiles", len(p), "complete", ok.sum())
+q = p[ok][:, :7]
+d = np.diff(q, axis=1)
+names = ["stage", "spec", "canon", "wait_x", "true", "counts"]  # phases of k_decode_count
+tot = q[:, 6] - q[:, 0]
+print("cycles/tile mean %.0f p50 %.0f p99 %.0f" % (tot.mean(), np.median(tot), np.percentile(tot, 99)))
 for i, n in enumerate(names):
-    print(f"  {n:12s} mean {d[:, i].mean():9.0f}  p50 {np.median(d[:, i]):9.0f}  p99 {np.percentile(d[:, i], 99):9.0f}")
+    print(f"  {n:10s} mean {d[:, i].mean():9.0f}  p50 {np.median(d[:, i]):9.0f}  p99 {np.percentile(d[:, i], 99):9.0f}  max {d[:, i].max():9.0f}")
+t0 = q[:, 0].min()
+span = q[:, 6].max() - t0
+print("kernel span (cycles of s_memtime) %d" % span)
+idx = np.nonzero(ok)[0]
+for frac in (0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 1.0):
+    k = min(len(idx) - 1, int(frac * (len(idx) - 1)))
+    print(f"  tile {idx[k]:6d} start {q[k,0]-t0:10d} end {q[k,6]-t0:10d}")

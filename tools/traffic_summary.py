@@ -17,7 +17,8 @@ src, tag = sys.argv[1], sys.argv[2]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
-NAMES = {"k_fast_scan": "decode_scan", "k_fast_emit": "decode_emit", "k_gather": "slice_gather",
+NAMES = {"k_decode_count": "decode_count", "k_decode_scan": "decode_offsets", "k_decode_emit": "decode_emit",
+         "k_fast_scan": "robust_scan", "k_fast_emit": "robust_emit", "k_gather": "slice_gather",
          "k_fast_resolve": "decode_resolve", "k_expand_tiles": "plan_tiles", "k_expand_pieces": "plan_pieces"}
 
 
