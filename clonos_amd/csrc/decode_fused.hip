@@ -54,7 +54,8 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
 #endif
 constexpr uint32_t kZWin = 1024;                       // record starts staged per emit window
-constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // "canonical" entry marker (lane 0)
+constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
+constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
 
 // ---------------------------------------------------------------------------------
@@ -328,89 +329,78 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
 // ---------------------------------------------------------------------------------
 // One 64-lane workgroup decodes one tile at a time (persistent grid, below).
 // ---------------------------------------------------------------------------------
-// Pass 1 for one tile: stage, chain, then the tile's record / wide-record counts and its
-// record-start bitmap (1 KiB) for the emit pass.  false once the batch has aborted.
-__device__ __forceinline__ bool count_tile(const uint32_t t, const TileDesc* __restrict__ tiles,
-                                           const SpanDesc* __restrict__ spans, const FusedCtl& ctl,
-                                           uint32_t* s_img, const uint32_t lane) {
+// Tile geometry shared by the passes.
+struct ZTile {
+  TileDesc td;
+  SpanDesc sd;
+  uint32_t lo, hi, end_a, rs, re;
+  bool first, last;  // first / last tile of its span
+};
+__device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans, uint32_t t,
+                                       uint32_t lane) {
+  ZTile z;
+  z.td = tiles[t];
+  z.sd = spans[z.td.span];
+  z.first = t == z.sd.first_tile;
+  z.last = t + 1 == z.sd.first_tile + z.sd.n_tiles;
+  z.lo = z.td.delta;
+  z.hi = z.td.delta + z.td.len;
+  const uint64_t ea = z.sd.len - z.td.span_off + z.td.delta;
+  z.end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
+  const uint32_t r0 = lane * kZRegion;
+  z.rs = r0 < z.lo ? z.lo : (r0 > z.hi ? z.hi : r0);
+  z.re = r0 + kZRegion > z.hi ? z.hi : r0 + kZRegion;
+  return z;
+}
+
+// Canonical exit of tile t: the speculative rule's chain from region c0 = (last region -
+// kZCanonLanes + 1) to the tile end (entries = previous lane's exit; lanes whose entry
+// changed re-merge).  It depends only on the tile's last ~2 KiB and not on where the
+// true chain enters the tile, so a block publishes it for its chunk's last tile before
+// decoding anything; the true chain meets it inside those 2 KiB unless the data never
+// re-synchronises, and then the exit check in count_tile aborts the batch.
+__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t lane) {
+  const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
+  const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
+  const bool on = lane >= c0 && z.rs < z.re;
+  const uint32_t ws = z.rs >= z.lo + kZWarm ? z.rs - kZWarm : z.lo;
+  const Spec sp = on ? spec_walk(s_img, ws, z.rs, z.re, z.end_a) : Spec{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+  uint32_t cx = sp.exit, entry = kZCanon;
+  for (int it = 0; it <= 64; ++it) {
+    const uint32_t prev = __shfl_up(cx, 1);
+    const uint32_t want = lane <= c0 ? kZCanon : prev;
+    const bool ch = want != entry;
+    if (!__any(ch)) break;
+    if (ch) {
+      entry = want;
+      cx = on ? canon_walk(s_img, z.rs, z.re, z.end_a, want, sp) : want;
+    }
+  }
+  return __shfl(cx, 63);
+}
+
+// Pass 1 for one tile, given its true entry e_true (aligned coordinate): spec walks,
+// true chain, exit checks, then the tile's record / wide-record counts and its
+// record-start bitmap (1 KiB) for the emit pass.  *x_true = the tile's exit.  must_exit:
+// the exit the successor already uses (kZCanon: none).  false once the batch aborted.
+__device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
+                                           const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
+                                           const uint32_t lane, uint32_t* x_out) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
-  ZPHASE(0);
-  const TileDesc td = tiles[t];
-  const SpanDesc sd = spans[td.span];
-  const uint32_t t1 = sd.first_tile + sd.n_tiles;
-  const bool nodep = ctl.nodep != 0;  // developer timing mode: no cross-tile dependencies
-  const bool first = nodep || t == sd.first_tile, last = !nodep && t + 1 == t1;
-  const uint32_t lo = td.delta, hi = td.delta + td.len;
-  const uint64_t ea = sd.len - td.span_off + td.delta;
-  const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
-
-  stage_image(td, sd, t, tiles, s_img, lane, hi);
-
   ZPHASE(1);
-  // ---- 1. speculative walk of the lane's region
-  const uint32_t r0 = lane * kZRegion;
-  const uint32_t rs = r0 < lo ? lo : (r0 > hi ? hi : r0);
-  const uint32_t re = r0 + kZRegion > hi ? hi : r0 + kZRegion;
+  const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
+  // ---- speculative walk of the lane's region (with warm-up)
   const uint32_t ws = rs >= lo + kZWarm ? rs - kZWarm : lo;
   const Spec sp = rs < re ? spec_walk(s_img, ws, rs, re, end_a) : Spec{{0, 0}, {0, 0}, rs, rs, 0};
 
   ZPHASE(2);
-  // ---- 2. canonical exit: the speculative rule from the tile start, through every
-  // region (entries = previous lane's exit; lanes whose entry changed re-merge)
-  // Each lane keeps its true-rule merge result r (the canonical chain re-used by step 4
-  // unless its entry changes); the canonical exit cx follows the speculative rule only
-  // where r met a record the two rules treat differently (invalid, or longer than
-  // kZSpecMax).
-  uint32_t cx = sp.exit, x_pub = 0, entry = kZCanon;
-  Res r{sp.bm, sp.wb, sp.exit, 0, 0};
-  if (!first) {
-    for (int it = 0; it <= 64; ++it) {
-      const uint32_t prev = __shfl_up(cx, 1);
-      const uint32_t want = lane == 0 ? kZCanon : prev;
-      const bool ch = want != entry;
-      if (!__any(ch)) break;
-      if (ch) {
-        entry = want;
-        r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp) : Res{{0, 0}, {0, 0}, want, 0, 0};
-        cx = (r.bad | r.unclean) ? canon_walk(s_img, rs, re, end_a, want, sp) : r.exit;
-      }
-    }
-    x_pub = __shfl(cx, 63);
-    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (td.span_off + (x_pub - lo)));
-  }
-
-  ZPHASE(3);
-  // ---- 3. true entry: the span start, or the predecessor's published exit
-  uint32_t e_true;
-  if (first) {
-    e_true = lo;  // a span starts on a record boundary
-  } else {
-    uint64_t v;
-    uint32_t nb = 1;
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    for (;;) {
-      v = ld_agent(&ctl.st_x[t - 1]);
-      if (v) break;
-      if (ld_agent32(ctl.abort)) return false;
-      if (!backoff(nb, t0)) {
-        if (lane == 0) raise_abort(ctl, 4, t);
-        return false;
-      }
-    }
-    const uint64_t xs = v & ~(1ull << 63);  // predecessor's exit, span offset (>= td.span_off)
-    const uint64_t ee = xs - td.span_off + lo;
-    e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
-  }
-
-  ZPHASE(4);
-  // ---- 4. true chain: every lane merges from its guessed entry (the canonical one),
-  // then lanes whose entry changed re-merge until the chain is consistent
-  if (first) {  // no canonical pass: entries guessed from the speculative exits
-    const uint32_t guess = __shfl_up(sp.exit, 1);
-    entry = lane == 0 ? e_true : guess;
-    r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp) : Res{{0, 0}, {0, 0}, entry, 0, 0};
-  }
+  // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
+  // exit; lane 0 the true entry), then lanes whose entry changed re-merge until the chain
+  // is consistent (each pass fixes at least the lowest changed lane)
+  const uint32_t guess = __shfl_up(sp.exit, 1);
+  uint32_t entry = lane == 0 ? e_true : guess;
+  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp) : Res{{0, 0}, {0, 0}, entry, 0, 0};
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
     const uint32_t want = lane == 0 ? e_true : prev;
@@ -421,14 +411,12 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const TileDesc* __r
       r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp) : Res{{0, 0}, {0, 0}, want, 0, 0};
     }
   }
-  const uint32_t canon_exit = cx, canon_bad = 0;
   const uint32_t x_true = __shfl(r.exit, 63);
+  *x_out = x_true;
   uint32_t reason = __any(r.bad) ? 1u : 0u;  // the true chain meets an invalid / Serializable record
-  if (last) {
+  if (z.last) {
     if (x_true != end_a) reason = reason ? reason : 2u;  // the last record must end at the span end
-  } else if (first) {
-    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (td.span_off + (x_true - lo)));
-  } else if (x_true != x_pub) {
+  } else if (must_exit != kZCanon && x_true != must_exit) {
     reason = reason ? reason : 3u;  // the successor already entered at the published exit
   }
   if (reason && ctl.dbg) {  // developer diagnostics: the first aborting tile's lane state
@@ -436,20 +424,20 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const TileDesc* __r
     if (lane == 0) claim = atomicCAS(ctl.dbg, 0u, 1u) == 0u ? 1u : 0u;
     if (__shfl(claim, 0)) {
       if (lane == 0) {
-        ctl.dbg[1] = t; ctl.dbg[2] = reason; ctl.dbg[3] = x_pub; ctl.dbg[4] = x_true; ctl.dbg[5] = e_true;
-        ctl.dbg[6] = lo; ctl.dbg[7] = hi; ctl.dbg[8] = end_a;
+        ctl.dbg[1] = t; ctl.dbg[2] = reason; ctl.dbg[3] = must_exit; ctl.dbg[4] = x_true; ctl.dbg[5] = e_true;
+        ctl.dbg[6] = lo; ctl.dbg[7] = z.hi; ctl.dbg[8] = end_a;
       }
       uint32_t* d = ctl.dbg + 16 + 8 * lane;
-      d[0] = rs; d[1] = re; d[2] = sp.exit; d[3] = sp.bad; d[4] = canon_exit; d[5] = canon_bad; d[6] = entry;
+      d[0] = rs; d[1] = re; d[2] = sp.exit; d[3] = sp.bad; d[4] = sp.first; d[5] = 0; d[6] = entry;
       d[7] = r.exit | r.bad << 31;
     }
   }
-  if (reason && !nodep) {
+  if (reason && !ctl.nodep) {
     if (lane == 0) raise_abort(ctl, reason, t);
     return false;
   }
 
-  ZPHASE(5);
+  ZPHASE(3);
   // ---- counts and the record-start bitmap for the emit pass
   uint32_t rec = bcount(r.bm), wide = bcount(r.wb);
 #pragma unroll
@@ -463,7 +451,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const TileDesc* __r
   bits.x = r.bm.lo;
   bits.y = r.bm.hi;
   gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = bits;
-  ZPHASE(6);
+  ZPHASE(4);
 #undef ZPHASE
   return true;
 }
@@ -598,16 +586,61 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   }
 }
 
-// Persistent: the grid is at most what the device keeps resident (launch_decode_fused),
-// and block b takes tiles b, b + G, b + 2G, ...  Every wait is on a lower tile, whose
-// block is resident and never waits on a higher one, so the waits always end; a wait
-// that still runs past kZSpinLimit cycles aborts the batch instead of hanging.
+// Pass 1 kernel.  Persistent grid (at most what the device keeps resident, see
+// launch_decode_fused); block b decodes the contiguous chunk of tiles [b K, (b + 1) K).
+// Inside a chunk a tile's entry is its predecessor's true exit.  Across chunks: each block
+// first publishes the canonical exit of its chunk's last tile (no waiting before that),
+// and a chunk's first tile enters at the previous chunk's published exit, which that
+// chunk's last tile must then reproduce.  Blocks are all resident and publish first, so
+// the one wait always ends; a wait past kZSpinLimit cycles aborts the batch instead.
 __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
-    if (!count_tile(t, tiles, spans, ctl, s_img, lane)) return;
+  const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
+  const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
+  const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
+  if (t0 >= t1) return;
+  // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
+  uint32_t x_pub = kZCanon;
+  {
+    const ZTile z = ztile(tiles, spans, t1 - 1, lane);
+    if (!z.last && t1 < nt) {
+      stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
+      x_pub = canon_exit(z, s_img, lane);
+      if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
+      __syncthreads();
+    }
+  }
+  uint64_t x_prev = 0;  // previous tile's exit, span offset
+  for (uint32_t t = t0; t < t1; ++t) {
+    const ZTile z = ztile(tiles, spans, t, lane);
+    if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
+    uint64_t xs;
+    if (z.first || ctl.nodep) {
+      xs = z.td.span_off;  // a span starts on a record boundary
+    } else if (t > t0) {
+      xs = x_prev;
+    } else {  // chunk start: the previous chunk's published exit
+      uint64_t v;
+      uint32_t nb = 1;
+      const uint64_t w0 = __builtin_amdgcn_s_memtime();
+      for (;;) {
+        v = ld_agent(&ctl.st_x[t - 1]);
+        if (v) break;
+        if (ld_agent32(ctl.abort)) return;
+        if (!backoff(nb, w0)) {
+          if (lane == 0) raise_abort(ctl, 4, t);
+          return;
+        }
+      }
+      xs = v & ~(1ull << 63);
+    }
+    const uint64_t ee = xs - z.td.span_off + z.lo;
+    const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+    uint32_t x_true;
+    if (!count_tile(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true)) return;
+    x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
   }
 }

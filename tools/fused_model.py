@@ -3,7 +3,7 @@ checks of the speculation / merge / settle rules on real byte streams.  Develope
 not test infrastructure: it restates the KERNEL, not the reference."""
 import sys
 
-R, TILE, SPEC_MAX = 128, 8192, 256
+R, TILE, SPEC_MAX, CANON_LANES = 128, 8192, 256, 16
 LUT = {0: 2, 1: 9, 2: 5, 6: 13, 7: 5}
 
 
@@ -113,28 +113,36 @@ def decode_tile(b, lo, hi, end, first, e_true_fn):
         ws = rs - WARM if rs >= lo + WARM else lo
         regs.append((rs, re, spec_walk(b, ws, rs, re, end) if rs < re else dict(bm=set(), exit=rs, bad=0, first=rs)))
     cx = [g[2]["exit"] for g in regs]
-    x_pub = None
-    if not first:
-        ent = [None] * 64
-        for _ in range(65):
-            want = [None] + cx[:-1]
-            ch = [want[l] != ent[l] for l in range(64)]
-            if not any(ch):
-                break
-            for l in range(1, 64):
-                if ch[l]:
-                    rs, re, sp = regs[l]
-                    ent[l] = want[l]
-                    cx[l] = canon_walk(b, rs, re, end, want[l], sp) if rs < re else want[l]
-        x_pub = cx[63]
-    e_true = e_true_fn(x_pub)
-    entry = [e_true] + cx[:-1]
+    last_l = (hi - 1) >> 7 if hi > lo else 0
+    c0 = max(0, last_l - (CANON_LANES - 1))
 
     def mw(l, e):
         rs, re, sp = regs[l]
         return merge_walk(b, rs, re, end, e, sp) if rs < re else dict(bm=set(), exit=e, bad=0)
 
-    res = [mw(l, entry[l]) for l in range(64)]
+    ent = [None] * 64
+    res = [None] * 64
+    x_pub = None
+    if not first:
+        for _ in range(65):
+            want = [None if l <= c0 else cx[l - 1] for l in range(64)]
+            ch = [want[l] != ent[l] for l in range(64)]
+            if not any(ch):
+                break
+            for l in range(64):
+                if ch[l]:
+                    rs, re, sp = regs[l]
+                    ent[l] = want[l]
+                    res[l] = mw(l, want[l])
+                    cx[l] = canon_walk(b, rs, re, end, want[l], sp) if rs < re else want[l]
+        x_pub = cx[63]
+    e_true = e_true_fn(x_pub)
+    spx = [g[2]["exit"] for g in regs]
+    entry = list(ent)
+    for l in range(64):
+        if entry[l] is None:
+            entry[l] = e_true if l == 0 else spx[l - 1]
+            res[l] = mw(l, entry[l])
     for _ in range(65):
         want = [e_true] + [res[l - 1]["exit"] for l in range(1, 64)]
         ch = [want[l] != entry[l] for l in range(64)]

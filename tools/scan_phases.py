@@ -29,19 +29,19 @@ with Engine(segment_bytes=16384, pool_segments=nlogs * 400, timing=True) as eng:
             print("decode:", str(e)[:120])
     print( {k: round(v["ms"] / max(1, v["launches"]), 4) for k, v in eng.kernel_stats().items() if v["launches"]})
 p = np.fromfile(out, np.uint64).reshape(-1, 8).astype(np.int64)
-ok = (p[:, 0] > 0) & (p[:, 6] > 0)
+ok = (p[:, 0] > 0) & (p[:, 4] > 0)
 print("tiles", len(p), "complete", ok.sum())
-q = p[ok][:, :7]
+q = p[ok][:, :5]
 d = np.diff(q, axis=1)
-names = ["stage", "spec", "canon", "wait_x", "true", "counts"]  # phases of k_decode_count
-tot = q[:, 6] - q[:, 0]
+names = ["entry+stage", "spec", "true", "counts"]  # phases of k_decode_count
+tot = q[:, 4] - q[:, 0]
 print("cycles/tile mean %.0f p50 %.0f p99 %.0f" % (tot.mean(), np.median(tot), np.percentile(tot, 99)))
 for i, n in enumerate(names):
     print(f"  {n:10s} mean {d[:, i].mean():9.0f}  p50 {np.median(d[:, i]):9.0f}  p99 {np.percentile(d[:, i], 99):9.0f}  max {d[:, i].max():9.0f}")
 t0 = q[:, 0].min()
-span = q[:, 6].max() - t0
+span = q[:, 4].max() - t0
 print("kernel span (cycles of s_memtime) %d" % span)
 idx = np.nonzero(ok)[0]
 for frac in (0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 1.0):
     k = min(len(idx) - 1, int(frac * (len(idx) - 1)))
-    print(f"  tile {idx[k]:6d} start {q[k,0]-t0:10d} end {q[k,6]-t0:10d}")
+    print(f"  tile {idx[k]:6d} start {q[k,0]-t0:10d} end {q[k,4]-t0:10d}")
