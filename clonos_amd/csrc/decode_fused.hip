@@ -459,14 +459,34 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
 // ---------------------------------------------------------------------------------
 // Pass 2: exclusive scan of the per-tile counts (one workgroup), and each span's range.
 // ---------------------------------------------------------------------------------
+// Exclusive prefix at tile i (i <= nt) from the per-thread sums: the block's own base
+// writes are not re-read (no cross-thread global visibility needed inside the block).
+__device__ __forceinline__ uint64_t sum_before(const CLG_GLOBAL uint64_t* cnt, const CLG_GLOBAL uint64_t* base, uint32_t i,
+                                               uint32_t nt, const uint64_t* s_incl) {
+  (void)base;
+  const uint32_t per = (nt + 1023u) / 1024u;
+  if (i >= nt) return s_incl[1023];
+  const uint32_t th = i / per;
+  uint64_t run = th ? s_incl[th - 1] : 0ull;
+  for (uint32_t k = th * per; k < i; ++k) run += cnt[k];
+  return run;
+}
+
 __global__ __launch_bounds__(1024) void k_decode_scan(const SpanDesc* __restrict__ spans, uint32_t n_spans,
                                                       FusedCtl ctl) {
   __shared__ uint64_t s_sum[1024];
   if (ld_agent32(ctl.abort)) return;
   const uint32_t nt = ctl.n_tiles, tid = threadIdx.x;
   const uint32_t per = (nt + 1023u) / 1024u, b0 = tid * per, b1 = min(nt, b0 + per);
+  const CLG_GLOBAL uint64_t* cnt = gp(ctl.cnt);
   uint64_t sum = 0;
-  for (uint32_t i = b0; i < b1; ++i) sum += gp(ctl.cnt)[i];
+  for (uint32_t i = b0; i < b1; i += 8) {  // 8 independent loads in flight per thread
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = i + j < b1 ? cnt[i + j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += v[j];
+  }
   s_sum[tid] = sum;
   __syncthreads();
   for (uint32_t off = 1; off < 1024u; off <<= 1) {
@@ -476,17 +496,23 @@ __global__ __launch_bounds__(1024) void k_decode_scan(const SpanDesc* __restrict
     __syncthreads();
   }
   uint64_t run = s_sum[tid] - sum;  // exclusive
-  for (uint32_t i = b0; i < b1; ++i) {
-    gp(ctl.base)[i] = run;
-    run += gp(ctl.cnt)[i];
+  CLG_GLOBAL uint64_t* base = gp(ctl.base);
+  for (uint32_t i = b0; i < b1; i += 8) {
+    uint64_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = i + j < b1 ? cnt[i + j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i + j < b1) base[i + j] = run;
+      run += v[j];
+    }
   }
-  if (tid == 1023u) gp(ctl.base)[nt] = s_sum[1023];
+  if (tid == 1023u) base[nt] = s_sum[1023];
   __syncthreads();
-  __threadfence_block();
   for (uint32_t sp = tid; sp < n_spans; sp += 1024u) {
     const SpanDesc sd = spans[sp];
-    gp(ctl.span_lo)[sp] = gp(ctl.base)[sd.first_tile];
-    gp(ctl.span_hi)[sp] = gp(ctl.base)[sd.first_tile + sd.n_tiles];
+    gp(ctl.span_lo)[sp] = sum_before(cnt, base, sd.first_tile, nt, s_sum);
+    gp(ctl.span_hi)[sp] = sum_before(cnt, base, sd.first_tile + sd.n_tiles, nt, s_sum);
   }
 }
 
