@@ -102,25 +102,51 @@ __device__ __forceinline__ uint64_t fld_be64(const ZBytes& b, uint32_t k) { retu
 // Record length at aligned coordinate a (< tile end): L > 0, kLenErr (-1) for a record
 // decodeNext rejects, kZSer for a Serializable record.  Reads only the LDS image (every
 // field a valid record needs lies within 27 bytes of its start, inside tile + halo).
-// Validity and length follow SimpleDeterminantEncoder readers :116-341 (len_fields).
+// Validity and length follow the SimpleDeterminantEncoder readers (:116-341; the same
+// rules as len_fields in dev_common.h), all inline: the common tags cost one dword pair
+// and a nibble table.
 // ---------------------------------------------------------------------------------
-__device__ __noinline__ int zlen_rare(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t tg, uint32_t x0) {
+__device__ __forceinline__ int zlen_var(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t tg, uint32_t x0) {
   if (tg == CLG_TAG_SERIALIZABLE)
     return ((x0 >> 8) | (zb(T, a + 4) << 24)) == 0x0500EDACu ? kZSer : (int)kLenErr;  // AC ED 00 05
-  const ZBytes b{T, a};
-  const int64_t LL = len_fields(b, (int)tg, (uint64_t)(end_a - a));
-  return (LL <= 0 || LL > 0x7FFFFFF0ll) ? (int)kLenErr : (int)LL;
+  const uint32_t avail = end_a - a;
+  uint64_t L;
+  if (tg == CLG_TAG_TIMER_TRIGGER) {  // [04][rc i32][ts i64][type u8]{[len i32][name]}  (:202-242)
+    if (avail < 14u) return (int)kLenErr;
+    const int ord = (int8_t)zb(T, a + 13);
+    if (ord < 0 || ord > 6) return (int)kLenErr;  // ProcessingTimeCallbackID.Type (:33-34)
+    L = 14;
+    if (ord == 6) {
+      if (avail < 18u) return (int)kLenErr;
+      const int32_t nl = (int32_t)zbe32(T, a + 14);
+      if (nl < 0) return (int)kLenErr;
+      L = 18ull + (uint64_t)nl;
+    }
+  } else {  // SOURCE_CHECKPOINT [05][rc][cp i64][ts i64][type u8][hasRef u8]{[len][ref]}  (:244-287)
+    if (avail < 23u) return (int)kLenErr;
+    L = 23;
+    if (zb(T, a + 22) != 0) {
+      if (avail < 27u) return (int)kLenErr;
+      const int32_t rl = (int32_t)zbe32(T, a + 23);
+      if (rl < 0) return (int)kLenErr;
+      L = 27ull + (uint64_t)rl;
+    }
+    const int ord = (int8_t)zb(T, a + 21);
+    if (ord < 0 || ord > 1) return (int)kLenErr;  // CheckpointType (:27, :30)
+  }
+  return (L > avail || L > 0x7FFFFFF0ull) ? (int)kLenErr : (int)L;
 }
 __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t* tag) {
-  const uint32_t p = rk(a >> 2);
-  const uint32_t x0 = __builtin_amdgcn_alignbit(T[p + 1], T[p], 8u * (a & 3u));  // bytes a..a+3 (LE)
+  // byte address of LDS dword rk(a >> 2): rows of 32 dwords at a pitch of 35
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(T) + (a & ~3u) + 12u * (a >> 7));
+  const uint32_t x0 = __builtin_amdgcn_alignbit(d[1], d[0], a << 3);  // bytes a..a+3 (LE); shift uses bits 0-4
   const uint32_t tg = x0 & 0xFFu;
   *tag = tg;
-  constexpr uint64_t lut = 2ull | 9ull << 4 | 5ull << 8 | 13ull << 24 | 5ull << 28;  // 0: 3/4/5
-  const uint32_t L = (uint32_t)(lut >> (4u * (tg & 15u))) & 0xFu;
+  constexpr uint32_t lut = 2u | 9u << 4 | 5u << 8 | 13u << 24 | 5u << 28;  // nibble per tag 0..7; 0: 3, 4, 5
+  const uint32_t L = (lut >> ((tg & 7u) << 2)) & 0xFu;
   if (tg > 7u) return (int)kLenErr;
-  if (L != 0) return a + L > end_a ? (int)kLenErr : (int)L;
-  return zlen_rare(T, a, end_a, tg, x0);  // TimerTrigger, SourceCheckpoint, Serializable
+  if (L == 0) return zlen_var(T, a, end_a, tg, x0);  // TimerTrigger, SourceCheckpoint, Serializable
+  return a + L > end_a ? (int)kLenErr : (int)L;
 }
 
 // ---------------------------------------------------------------------------------
@@ -133,46 +159,42 @@ __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_
 //                 a skipped byte on the speculative chain no longer follows the true one.
 // ---------------------------------------------------------------------------------
 constexpr int kZSpecMax = 256;
-
-__device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uint32_t end_a, int* L, uint32_t* tg) {
-  *L = zlen(T, q, end_a, tg);
-  return (*L > 0 && *L <= kZSpecMax) ? q + (uint32_t)*L : q + 1u;
-}
+constexpr uint32_t kZNone = 0xFFFFFFFFu;
+constexpr uint32_t kZBitsPitch = 5;  // dwords per lane of the LDS spec bitmaps (4 + 1: banks)
 
 struct Spec {
-  Bits bm, wb;         // followed starts in the region / followed wide starts
-  uint32_t first;      // first position >= rs
-  uint32_t exit;       // first position >= re
-  uint32_t bad;        // 1 + last position skipped, 0 if none
+  Bits wb;         // followed wide starts in the region (the starts themselves: LDS bitmap)
+  uint32_t first;  // first position >= rs
+  uint32_t exit;   // first position >= re
+  uint32_t bad;    // 1 + last position skipped, 0 if none
 };
 
 // The walk starts kZWarm bytes before the region (inside the previous one), so that by
 // the region start the chain has almost always re-synchronised with the true one; then
-// true chains meet it at their first step and entries rarely cascade across lanes.
+// true chains meet it at their first step and entries rarely cascade across lanes.  The
+// region's followed starts are or-ed into the lane's LDS bitmap `bits` (zeroed by the
+// caller).
 constexpr uint32_t kZWarm = 64;
-__device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a) {
-  Spec s{{0, 0}, {0, 0}, rs, rs, 0};
+__device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
+                                          uint32_t* bits) {
+  Spec s{{0, 0}, kZNone, rs, 0};
   uint32_t q = ws;
-  while (q < rs) {  // warm-up: follow the rule, record nothing but skips
-    uint32_t tg;
-    int L;
-    const uint32_t nq = spec_step(T, q, end_a, &L, &tg);
-    if (nq == q + 1u && L != 1) s.bad = q + 1;
-    q = nq;
-  }
-  s.first = q;
   while (q < re) {
     uint32_t tg;
-    int L;
-    const uint32_t nq = spec_step(T, q, end_a, &L, &tg);
-    if (nq == q + 1u && L != 1) {
-      s.bad = q + 1;
-    } else {
-      bset(s.bm, q - rs);
-      if (is_wide((int)tg)) bset(s.wb, q - rs);
+    const int L = zlen(T, q, end_a, &tg);
+    const bool ok = L > 0 && L <= kZSpecMax;
+    if (q >= rs) {
+      s.first = s.first == kZNone ? q : s.first;
+      if (ok) {
+        const uint32_t i = q - rs;
+        atomicOr(&bits[i >> 5], 1u << (i & 31u));
+        if (tg - 4u < 3u) bset(s.wb, i);  // TimerTrigger, SourceCheckpoint, IgnoreCheckpoint
+      }
     }
-    q = nq;
+    s.bad = ok ? s.bad : q + 1;
+    q += ok ? (uint32_t)L : 1u;
   }
+  s.first = s.first == kZNone ? q : s.first;
   s.exit = q;
   return s;
 }
@@ -186,10 +208,11 @@ __device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, u
   for (;;) {
     if (p == q) return s.exit;
     if (p >= re) return p;
-    int L;
     uint32_t tg;
-    if (p < q) p = spec_step(T, p, end_a, &L, &tg);
-    else q = spec_step(T, q, end_a, &L, &tg);
+    const uint32_t x = p < q ? p : q;
+    const int L = zlen(T, x, end_a, &tg);
+    const uint32_t nx = x + ((L > 0 && L <= kZSpecMax) ? (uint32_t)L : 1u);
+    if (p < q) p = nx; else q = nx;
   }
 }
 
@@ -200,37 +223,39 @@ struct Res {
   uint32_t unclean;  // true chain follows a record longer than kZSpecMax
 };
 
-// True chain from entry e (e >= rs) merged with the speculative chain: they may only
-// merge at a position past the speculative chain's last skip.
+// True chain from entry e (e >= rs) merged with the speculative chain (starts in the LDS
+// bitmap `bits`): they may only merge at a position past the speculative chain's last
+// skip.
 __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
-                                          const Spec& s) {
+                                          const Spec& s, const uint32_t* bits) {
   Res r{{0, 0}, {0, 0}, e, 0, 0};
   if (e >= re) return r;  // no record starts in this region
   uint32_t p = e, q = s.first;
   Bits pb{0, 0}, pw{0, 0};
   for (;;) {
     if (p == q && p < re && p >= s.bad) {  // met: the speculative chain from here is the true one
-      r.bm = bor(pb, bge(s.bm, p - rs));
+      const Bits sb{(uint64_t)bits[1] << 32 | bits[0], (uint64_t)bits[3] << 32 | bits[2]};
+      r.bm = bor(pb, bge(sb, p - rs));
       r.wb = bor(pw, bge(s.wb, p - rs));
       r.exit = s.exit;
       return r;
     }
     if (p >= re) break;
     uint32_t tg;
-    int L;
     if (p <= q) {
-      L = zlen(T, p, end_a, &tg);
+      const int L = zlen(T, p, end_a, &tg);
       if (L <= 0) {
         r.bad = 1;
         r.exit = s.exit;
         return r;
       }
       bset(pb, p - rs);
-      if (is_wide((int)tg)) bset(pw, p - rs);
+      if (tg - 4u < 3u) bset(pw, p - rs);
       r.unclean |= L > kZSpecMax ? 1u : 0u;
       p += (uint32_t)L;
     } else {
-      q = spec_step(T, q, end_a, &L, &tg);
+      const int L = zlen(T, q, end_a, &tg);
+      q += (L > 0 && L <= kZSpecMax) ? (uint32_t)L : 1u;
     }
   }
   r.bm = pb;
@@ -359,12 +384,13 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
 // true chain enters the tile, so a block publishes it for its chunk's last tile before
 // decoding anything; the true chain meets it inside those 2 KiB unless the data never
 // re-synchronises, and then the exit check in count_tile aborts the batch.
-__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t lane) {
+__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t* s_bits, uint32_t lane) {
   const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
   const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
   const bool on = lane >= c0 && z.rs < z.re;
   const uint32_t ws = z.rs >= z.lo + kZWarm ? z.rs - kZWarm : z.lo;
-  const Spec sp = on ? spec_walk(s_img, ws, z.rs, z.re, z.end_a) : Spec{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+  uint32_t* bits = s_bits + lane * kZBitsPitch;
+  const Spec sp = on ? spec_walk(s_img, ws, z.rs, z.re, z.end_a, bits) : Spec{{0, 0}, z.rs, z.rs, 0};
   uint32_t cx = sp.exit, entry = kZCanon;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(cx, 1);
@@ -385,14 +411,16 @@ __device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s
 // the exit the successor already uses (kZCanon: none).  false once the batch aborted.
 __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
-                                           const uint32_t lane, uint32_t* x_out) {
+                                           uint32_t* s_bits, const uint32_t lane, uint32_t* x_out) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
   // ---- speculative walk of the lane's region (with warm-up)
   const uint32_t ws = rs >= lo + kZWarm ? rs - kZWarm : lo;
-  const Spec sp = rs < re ? spec_walk(s_img, ws, rs, re, end_a) : Spec{{0, 0}, {0, 0}, rs, rs, 0};
+  uint32_t* bits = s_bits + lane * kZBitsPitch;
+  bits[0] = bits[1] = bits[2] = bits[3] = 0;
+  const Spec sp = rs < re ? spec_walk(s_img, ws, rs, re, end_a, bits) : Spec{{0, 0}, rs, rs, 0};
 
   ZPHASE(2);
   // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
@@ -400,7 +428,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0};
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
     const uint32_t want = lane == 0 ? e_true : prev;
@@ -408,7 +436,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     if (!__any(ch)) break;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp) : Res{{0, 0}, {0, 0}, want, 0, 0};
+      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0};
     }
   }
   const uint32_t x_true = __shfl(r.exit, 63);
@@ -447,73 +475,65 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   }
   if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(rec, wide);
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  u64x2 bits;
-  bits.x = r.bm.lo;
-  bits.y = r.bm.hi;
-  gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = bits;
+  u64x2 out_bits;
+  out_bits.x = r.bm.lo;
+  out_bits.y = r.bm.hi;
+  gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = out_bits;
   ZPHASE(4);
 #undef ZPHASE
   return true;
 }
 
 // ---------------------------------------------------------------------------------
-// Pass 2: exclusive scan of the per-tile counts (one workgroup), and each span's range.
+// Pass 2: exclusive scan of the per-tile counts.  scan1: one 256-thread workgroup per
+// 1024 tiles (block-relative bases + the block's total); scan2: one workgroup scans the
+// block totals into block offsets.  The emit pass adds the two.
 // ---------------------------------------------------------------------------------
-// Exclusive prefix at tile i (i <= nt) from the per-thread sums: the block's own base
-// writes are not re-read (no cross-thread global visibility needed inside the block).
-__device__ __forceinline__ uint64_t sum_before(const CLG_GLOBAL uint64_t* cnt, const CLG_GLOBAL uint64_t* base, uint32_t i,
-                                               uint32_t nt, const uint64_t* s_incl) {
-  (void)base;
-  const uint32_t per = (nt + 1023u) / 1024u;
-  if (i >= nt) return s_incl[1023];
-  const uint32_t th = i / per;
-  uint64_t run = th ? s_incl[th - 1] : 0ull;
-  for (uint32_t k = th * per; k < i; ++k) run += cnt[k];
-  return run;
+constexpr uint32_t kZScanBlock = 1024;
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(v, off);
+    if ((int)lane >= off) v += y;
+  }
+  return v;
 }
 
-__global__ __launch_bounds__(1024) void k_decode_scan(const SpanDesc* __restrict__ spans, uint32_t n_spans,
-                                                      FusedCtl ctl) {
-  __shared__ uint64_t s_sum[1024];
+__global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
+  __shared__ uint64_t s_w[4];
   if (ld_agent32(ctl.abort)) return;
-  const uint32_t nt = ctl.n_tiles, tid = threadIdx.x;
-  const uint32_t per = (nt + 1023u) / 1024u, b0 = tid * per, b1 = min(nt, b0 + per);
-  const CLG_GLOBAL uint64_t* cnt = gp(ctl.cnt);
-  uint64_t sum = 0;
-  for (uint32_t i = b0; i < b1; i += 8) {  // 8 independent loads in flight per thread
-    uint64_t v[8];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t i0 = blockIdx.x * kZScanBlock + tid * 4u, nt = ctl.n_tiles;
+  uint64_t v[4], sum = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = i + j < b1 ? cnt[i + j] : 0ull;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sum += v[j];
+  for (int j = 0; j < 4; ++j) {
+    v[j] = i0 + j < nt ? gp(ctl.cnt)[i0 + j] : 0ull;
+    sum += v[j];
   }
-  s_sum[tid] = sum;
+  const uint64_t incl = wave_incl_scan(sum, lane);
+  if (lane == 63u) s_w[wv] = incl;
   __syncthreads();
-  for (uint32_t off = 1; off < 1024u; off <<= 1) {
-    const uint64_t y = tid >= off ? s_sum[tid - off] : 0ull;
-    __syncthreads();
-    s_sum[tid] += y;
-    __syncthreads();
-  }
-  uint64_t run = s_sum[tid] - sum;  // exclusive
-  CLG_GLOBAL uint64_t* base = gp(ctl.base);
-  for (uint32_t i = b0; i < b1; i += 8) {
-    uint64_t v[8];
+  uint64_t run = incl - sum;
+  for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = i + j < b1 ? cnt[i + j] : 0ull;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (i + j < b1) base[i + j] = run;
-      run += v[j];
-    }
+  for (int j = 0; j < 4; ++j) {
+    if (i0 + j < nt) gp(ctl.base)[i0 + j] = run;
+    run += v[j];
   }
-  if (tid == 1023u) base[nt] = s_sum[1023];
+  if (tid == 255u) gp(ctl.boff)[blockIdx.x] = run;  // block total (scan2 turns it into an offset)
+}
+
+__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_blocks) {
+  __shared__ uint64_t s_w[16];
+  if (ld_agent32(ctl.abort)) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint64_t v = tid < n_blocks ? gp(ctl.boff)[tid] : 0ull;
+  const uint64_t incl = wave_incl_scan(v, lane);
+  if (lane == 63u) s_w[wv] = incl;
   __syncthreads();
-  for (uint32_t sp = tid; sp < n_spans; sp += 1024u) {
-    const SpanDesc sd = spans[sp];
-    gp(ctl.span_lo)[sp] = sum_before(cnt, base, sd.first_tile, nt, s_sum);
-    gp(ctl.span_hi)[sp] = sum_before(cnt, base, sd.first_tile + sd.n_tiles, nt, s_sum);
-  }
+  uint64_t run = incl - v;
+  for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
+  if (tid < n_blocks) gp(ctl.boff)[tid] = run;
 }
 
 // ---------------------------------------------------------------------------------
@@ -534,7 +554,8 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
-  const uint64_t base = gp(ctl.base)[t];
+  const uint64_t cnt_t = gp(ctl.cnt)[t];
+  const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   stage_image(td, sd, t, tiles, s_img, lane, hi);
   const uint32_t r0 = lane * kZRegion;
   const uint32_t rs = r0 < lo ? lo : (r0 > hi ? hi : r0);
@@ -546,6 +567,10 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
     if ((int)lane >= off) incl += y;
   }
   const uint32_t total = __shfl(incl, 63);
+  if (lane == 0) {  // the span's record / wide-record range, at its first and last tiles
+    if (t == sd.first_tile) gp(ctl.span_lo)[td.span] = base;
+    if (t + 1 == sd.first_tile + sd.n_tiles) gp(ctl.span_hi)[td.span] = base + cnt_t;
+  }
   const uint64_t rec0 = base & ((1ull << 31) - 1), wide0 = base >> 31;
   Bits cur{bits.x, bits.y};
   uint32_t idx = incl - cnt;
@@ -622,6 +647,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
 __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
+  __shared__ uint32_t s_bits[64 * kZBitsPitch];  // speculative-start bitmaps, one row per lane
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
   const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
@@ -632,7 +658,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
-      x_pub = canon_exit(z, s_img, lane);
+      x_pub = canon_exit(z, s_img, s_bits, lane);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
@@ -665,7 +691,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
     stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
     uint32_t x_true;
-    if (!count_tile(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true)) return;
+    if (!count_tile(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, s_bits, lane, &x_true)) return;
     x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
   }
@@ -689,7 +715,10 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     const uint32_t grid = n_tiles < (uint32_t)resident ? n_tiles : (uint32_t)resident;
     hipLaunchKernelGGL(k_decode_count, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {
-    hipLaunchKernelGGL(k_decode_scan, dim3(1), dim3(1024), 0, st, d_spans, n_spans, ctl);
+    const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
+    if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
+    hipLaunchKernelGGL(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
+    hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
   } else {
     hipLaunchKernelGGL(k_decode_emit, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   }

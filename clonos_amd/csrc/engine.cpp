@@ -756,11 +756,16 @@ struct clg_engine {
     reset_result(out);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     if (ns == 0) return CLG_OK;
+    if (nt > (1u << 20)) {  // more than 8 GiB in one batch: the offsets pass covers 2^20 tiles
+      *aborted = true;
+      return CLG_OK;
+    }
     CHK(upload_plan(p, d_ztiles));
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
-    // words: st_x[nt] cnt[nt] base[nt + 1] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
-    const size_t o_span = 3 * size_t(nt) + 1, o_ab = o_span + 2 * size_t(ns), words = o_ab + 4;
+    // words: st_x[nt] cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
+    const size_t nbk = (size_t(nt) + 1023) / 1024;
+    const size_t o_span = 3 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), words = o_ab + 4;
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
@@ -776,7 +781,8 @@ struct clg_engine {
       CHK(d_prof.ensure(size_t(nt) * 64));
       HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
     }
-    clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span, w + o_span + ns, ab,
+    clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), w + 3 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
+                      w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u};
     HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));

@@ -166,7 +166,8 @@ constexpr uint32_t kZHalo = 64;             // bytes of the span's next tile sta
 struct FusedCtl {
   uint64_t* st_x;     // per tile: 1<<63 | exit (span offset) the successor enters at
   uint64_t* cnt;      // per tile: wide<<31 | records
-  uint64_t* base;     // per tile + 1: exclusive prefix of cnt
+  uint64_t* base;     // per tile: exclusive prefix of cnt inside its block of 1024 tiles
+  uint64_t* boff;     // per block of 1024 tiles: exclusive prefix of the block totals
   uint64_t* bits;     // per tile: 64 x 16 B record-start bitmaps (lane l: region l)
   uint64_t* span_lo;  // per span: base at its first tile
   uint64_t* span_hi;  // per span: base past its last tile
