@@ -59,7 +59,7 @@ constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the ca
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
 
 // ---------------------------------------------------------------------------------
-// 128-bit region bitmaps (bit i <-> region byte rs + i).
+// 128-bit region bitmaps (bit i <-> byte r0 + i of the lane's aligned region r0).
 // ---------------------------------------------------------------------------------
 struct Bits {
   uint64_t lo, hi;
@@ -97,6 +97,18 @@ struct ZBytes {
 };
 __device__ __forceinline__ uint32_t fld_be32(const ZBytes& b, uint32_t k) { return zbe32(b.T, b.base + k); }
 __device__ __forceinline__ uint64_t fld_be64(const ZBytes& b, uint32_t k) { return zbe64(b.T, b.base + k); }
+
+// LDS byte offset of aligned coordinate a (rows of 128 bytes at a pitch of 140 bytes):
+// a + 12 (a >> 7) in one full-rate op (left to itself the compiler picks v_mad_u64_u32).
+__device__ __forceinline__ uint32_t zoff(uint32_t a) {
+  uint32_t off;
+  asm("v_mad_u32_u24 %0, %1, 12, %2" : "=v"(off) : "v"(a >> 7), "v"(a));
+  return off;
+}
+typedef const __attribute__((address_space(3))) uint8_t lds_u8;
+typedef const __attribute__((address_space(3))) uint32_t lds_u32;
+// Byte a of the LDS image: one ds_read_u8.
+__device__ __forceinline__ uint32_t zb8(const uint32_t* T, uint32_t a) { return ((lds_u8*)(T))[zoff(a)]; }
 
 // ---------------------------------------------------------------------------------
 // Record length at aligned coordinate a (< tile end): L > 0, kLenErr (-1) for a record
@@ -137,8 +149,7 @@ __device__ __forceinline__ int zlen_var(const uint32_t* T, uint32_t a, uint32_t 
   return (L > avail || L > 0x7FFFFFF0ull) ? (int)kLenErr : (int)L;
 }
 __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t* tag) {
-  // byte address of LDS dword rk(a >> 2): rows of 32 dwords at a pitch of 35
-  const uint32_t* d = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(T) + (a & ~3u) + 12u * (a >> 7));
+  lds_u32* d = (lds_u32*)((lds_u8*)(T) + (zoff(a) & ~3u));  // LDS dword rk(a >> 2)
   const uint32_t x0 = __builtin_amdgcn_alignbit(d[1], d[0], a << 3);  // bytes a..a+3 (LE); shift uses bits 0-4
   const uint32_t tg = x0 & 0xFFu;
   *tag = tg;
@@ -159,42 +170,62 @@ __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_
 //                 a skipped byte on the speculative chain no longer follows the true one.
 // ---------------------------------------------------------------------------------
 constexpr int kZSpecMax = 256;
-constexpr uint32_t kZNone = 0xFFFFFFFFu;
 constexpr uint32_t kZBitsPitch = 5;  // dwords per lane of the LDS spec bitmaps (4 + 1: banks)
 
 struct Spec {
   Bits wb;         // followed wide starts in the region (the starts themselves: LDS bitmap)
   uint32_t first;  // first position >= rs
   uint32_t exit;   // first position >= re
-  uint32_t bad;    // 1 + last position skipped, 0 if none
+  uint32_t bad;    // 1 + last position skipped inside the region, 0 if none
 };
+
+// Speculative step length at a (< tile end): L in [1, kZSpecMax] to follow the record,
+// 0 to step one byte.  Fixed-length tags cost a nibble table (kZLut; 0: not followed,
+// 15: TimerTrigger / SourceCheckpoint / IgnoreCheckpoint, the out-of-line case);
+// Serializable and invalid tags are never followed.  *wide: the record is a wide one.
+constexpr uint32_t kZLut = 2u | 9u << 4 | 5u << 8 | 0u << 12 | 15u << 16 | 15u << 20 | 15u << 24 | 5u << 28;
+__device__ __forceinline__ uint32_t zspec_len(const uint32_t* T, uint32_t a, uint32_t end_a, bool* wide) {
+  const uint32_t tg = zb8(T, a);
+  uint32_t L = __builtin_amdgcn_ubfe(kZLut, tg << 2, 4);
+  *wide = false;
+  if (L == 15u && tg < 8u) {
+    *wide = true;
+    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
+      L = 13;
+    } else {
+      const int v = zlen_var(T, a, end_a, tg, 0);
+      L = (v > 0 && v <= kZSpecMax) ? (uint32_t)v : 0u;
+    }
+  }
+  return (tg < 8u && a + L <= end_a) ? L : 0u;
+}
 
 // The walk starts kZWarm bytes before the region (inside the previous one), so that by
 // the region start the chain has almost always re-synchronised with the true one; then
-// true chains meet it at their first step and entries rarely cascade across lanes.  The
-// region's followed starts are or-ed into the lane's LDS bitmap `bits` (zeroed by the
-// caller).
-constexpr uint32_t kZWarm = 64;
+// true chains meet it at their first step and entries rarely cascade across lanes.  Skips
+// in the warm-up never matter (true chains meet it at or after rs).  The region's
+// followed starts are or-ed into the lane's LDS bitmap `bits` (bit i <-> byte r0 + i,
+// r0 = rs & ~127; zeroed by the caller).
+constexpr uint32_t kZWarm = 96;
 __device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
                                           uint32_t* bits) {
-  Spec s{{0, 0}, kZNone, rs, 0};
+  Spec s{{0, 0}, rs, rs, 0};
   uint32_t q = ws;
-  while (q < re) {
-    uint32_t tg;
-    const int L = zlen(T, q, end_a, &tg);
-    const bool ok = L > 0 && L <= kZSpecMax;
-    if (q >= rs) {
-      s.first = s.first == kZNone ? q : s.first;
-      if (ok) {
-        const uint32_t i = q - rs;
-        atomicOr(&bits[i >> 5], 1u << (i & 31u));
-        if (tg - 4u < 3u) bset(s.wb, i);  // TimerTrigger, SourceCheckpoint, IgnoreCheckpoint
-      }
-    }
-    s.bad = ok ? s.bad : q + 1;
-    q += ok ? (uint32_t)L : 1u;
+  while (q < rs) {
+    bool w;
+    const uint32_t L = zspec_len(T, q, end_a, &w);
+    q += L > 1u ? L : 1u;
   }
-  s.first = s.first == kZNone ? q : s.first;
+  s.first = q;
+  while (q < re) {
+    bool w;
+    const uint32_t L = zspec_len(T, q, end_a, &w);
+    const uint32_t nq = q + (L > 1u ? L : 1u);
+    atomicOr(&bits[(q >> 5) & 3u], L ? 1u << (q & 31u) : 0u);
+    if (w && L) bset(s.wb, q & 127u);
+    s.bad = L ? s.bad : nq;
+    q = nq;
+  }
   s.exit = q;
   return s;
 }
@@ -221,42 +252,41 @@ struct Res {
   uint32_t exit;     // first true start >= re (bad: the speculative exit)
   uint32_t bad;      // true chain hits an invalid or Serializable record
   uint32_t unclean;  // true chain follows a record longer than kZSpecMax
+  uint32_t steps;    // pointer steps taken (diagnostics)
 };
 
-// True chain from entry e (e >= rs) merged with the speculative chain (starts in the LDS
-// bitmap `bits`): they may only merge at a position past the speculative chain's last
-// skip.
+// True chain from entry e (e >= rs) merged with the speculative chain (its starts are the
+// lane's LDS bitmap `bits`): walk the true chain until it lands on a speculative start
+// past the speculative chain's last skip; from there on the two chains are the same.
 __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
                                           const Spec& s, const uint32_t* bits) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  Res r{{0, 0}, {0, 0}, e, 0, 0, 0};
   if (e >= re) return r;  // no record starts in this region
-  uint32_t p = e, q = s.first;
+  const uint32_t b0 = bits[0], b1 = bits[1], b2 = bits[2], b3 = bits[3];
+  uint32_t p = e;
   Bits pb{0, 0}, pw{0, 0};
-  for (;;) {
-    if (p == q && p < re && p >= s.bad) {  // met: the speculative chain from here is the true one
-      const Bits sb{(uint64_t)bits[1] << 32 | bits[0], (uint64_t)bits[3] << 32 | bits[2]};
-      r.bm = bor(pb, bge(sb, p - rs));
-      r.wb = bor(pw, bge(s.wb, p - rs));
+  for (;; ++r.steps) {
+    if (p >= re) break;
+    const uint32_t i = p & 127u;
+    const uint32_t w = i < 64u ? (i < 32u ? b0 : b1) : (i < 96u ? b2 : b3);
+    if (((w >> (i & 31u)) & 1u) && p >= s.bad) {  // met the speculative chain
+      const Bits sb{(uint64_t)b1 << 32 | b0, (uint64_t)b3 << 32 | b2};
+      r.bm = bor(pb, bge(sb, i));
+      r.wb = bor(pw, bge(s.wb, i));
       r.exit = s.exit;
       return r;
     }
-    if (p >= re) break;
     uint32_t tg;
-    if (p <= q) {
-      const int L = zlen(T, p, end_a, &tg);
-      if (L <= 0) {
-        r.bad = 1;
-        r.exit = s.exit;
-        return r;
-      }
-      bset(pb, p - rs);
-      if (tg - 4u < 3u) bset(pw, p - rs);
-      r.unclean |= L > kZSpecMax ? 1u : 0u;
-      p += (uint32_t)L;
-    } else {
-      const int L = zlen(T, q, end_a, &tg);
-      q += (L > 0 && L <= kZSpecMax) ? (uint32_t)L : 1u;
+    const int L = zlen(T, p, end_a, &tg);
+    if (L <= 0) {
+      r.bad = 1;
+      r.exit = s.exit;
+      return r;
     }
+    bset(pb, i);
+    if (tg - 4u < 3u) bset(pw, i);
+    r.unclean |= L > kZSpecMax ? 1u : 0u;
+    p += (uint32_t)L;
   }
   r.bm = pb;
   r.wb = pw;
@@ -428,16 +458,28 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0, 0};
+  uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
     const uint32_t want = lane == 0 ? e_true : prev;
     const bool ch = want != entry;
     if (!__any(ch)) break;
+    ++iters;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0};
+      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0, 0};
+      steps_more += r.steps;
     }
+  }
+  if (ctl.prof) {  // diagnostics: max first-merge steps, max re-merge steps, fix-up passes
+    uint32_t m0 = steps0, m1 = steps_more;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      m0 = max(m0, (uint32_t)__shfl_xor(m0, off));
+      m1 = max(m1, (uint32_t)__shfl_xor(m1, off));
+    }
+    if (lane == 0) ctl.prof[(uint64_t)t * 8 + 5] = (uint64_t)m0 | (uint64_t)m1 << 20 | (uint64_t)iters << 40;
   }
   const uint32_t x_true = __shfl(r.exit, 63);
   *x_out = x_true;
@@ -558,7 +600,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   stage_image(td, sd, t, tiles, s_img, lane, hi);
   const uint32_t r0 = lane * kZRegion;
-  const uint32_t rs = r0 < lo ? lo : (r0 > hi ? hi : r0);
   const uint32_t cnt = (uint32_t)(__popcll(bits.x) + __popcll(bits.y));
   uint32_t incl = cnt;
 #pragma unroll
@@ -580,7 +621,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
     while ((cur.lo | cur.hi) && idx < wend) {
       const uint32_t i = cur.lo ? (uint32_t)__builtin_ctzll(cur.lo) : 64u + (uint32_t)__builtin_ctzll(cur.hi);
       if (cur.lo) cur.lo &= cur.lo - 1; else cur.hi &= cur.hi - 1;
-      s_pos[idx - w0] = (uint16_t)(rs + i);
+      s_pos[idx - w0] = (uint16_t)(r0 + i);
       ++idx;
     }
     __syncthreads();

@@ -50,7 +50,7 @@ def spec_step(b, q, end):
     return (q + L, True) if 0 < L <= SPEC_MAX else (q + 1, False)
 
 
-WARM = 64
+WARM = 96
 
 
 def spec_walk(b, ws, rs, re, end):
@@ -87,22 +87,19 @@ def canon_walk(b, rs, re, end, e, s):
 
 
 def merge_walk(b, rs, re, end, e, s):
+    """True chain from e until it lands on a speculative start past the last skip."""
     if e >= re:
         return dict(bm=set(), exit=e, bad=0)
-    p, q, pb = e, s["first"], set()
-    while True:
-        if p == q and p < re and p >= s["bad"]:
+    p, pb = e, set()
+    while p < re:
+        if p in s["bm"] and p >= s["bad"]:
             return dict(bm=pb | {x for x in s["bm"] if x >= p}, exit=s["exit"], bad=0)
-        if p >= re:
-            return dict(bm=pb, exit=p, bad=0)
-        if p <= q:
-            L = zlen(b, p, end)
-            if L <= 0:
-                return dict(bm=set(), exit=s["exit"], bad=1)
-            pb.add(p)
-            p += L
-        else:
-            q = spec_step(b, q, end)[0]
+        L = zlen(b, p, end)
+        if L <= 0:
+            return dict(bm=set(), exit=s["exit"], bad=1)
+        pb.add(p)
+        p += L
+    return dict(bm=pb, exit=p, bad=0)
 
 
 def decode_tile(b, lo, hi, end, first, e_true_fn):

@@ -45,3 +45,8 @@ idx = np.nonzero(ok)[0]
 for frac in (0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 1.0):
     k = min(len(idx) - 1, int(frac * (len(idx) - 1)))
     print(f"  tile {idx[k]:6d} start {q[k,0]-t0:10d} end {q[k,4]-t0:10d}")
+
+m = p[ok][:, 5]
+m0, m1, it = m & 0xFFFFF, (m >> 20) & 0xFFFFF, (m >> 40) & 0xFF
+for name, x in (("first-merge max steps", m0), ("re-merge max steps", m1), ("fix-up passes", it)):
+    print(f"  {name:22s} mean {x.mean():7.2f} p50 {np.median(x):5.0f} p90 {np.percentile(x, 90):5.0f} p99 {np.percentile(x, 99):5.0f} max {x.max()}")
