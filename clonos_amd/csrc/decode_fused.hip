@@ -239,28 +239,31 @@ __device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, u
   for (;;) {
     if (p == q) return s.exit;
     if (p >= re) return p;
-    uint32_t tg;
+    bool w;
     const uint32_t x = p < q ? p : q;
-    const int L = zlen(T, x, end_a, &tg);
-    const uint32_t nx = x + ((L > 0 && L <= kZSpecMax) ? (uint32_t)L : 1u);
+    const uint32_t L = zspec_len(T, x, end_a, &w);
+    const uint32_t nx = x + (L > 1u ? L : 1u);
     if (p < q) p = nx; else q = nx;
   }
 }
 
 struct Res {
-  Bits bm, wb;       // true record starts in the region / wide ones
-  uint32_t exit;     // first true start >= re (bad: the speculative exit)
-  uint32_t bad;      // true chain hits an invalid or Serializable record
-  uint32_t unclean;  // true chain follows a record longer than kZSpecMax
-  uint32_t steps;    // pointer steps taken (diagnostics)
+  Bits bm, wb;     // true record starts in the region / wide ones
+  uint32_t exit;   // first true start >= re (bad: the speculative exit)
+  uint32_t bad;    // true chain hits an invalid or Serializable record
+  uint32_t steps;  // true steps taken (diagnostics)
 };
+
+// True step lengths of the fixed-length tags (nibble per tag; 15: Serializable,
+// TimerTrigger, SourceCheckpoint, IgnoreCheckpoint, the out-of-line case).
+constexpr uint32_t kZLutTrue = 2u | 9u << 4 | 5u << 8 | 15u << 12 | 15u << 16 | 15u << 20 | 15u << 24 | 5u << 28;
 
 // True chain from entry e (e >= rs) merged with the speculative chain (its starts are the
 // lane's LDS bitmap `bits`): walk the true chain until it lands on a speculative start
 // past the speculative chain's last skip; from there on the two chains are the same.
-__device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
-                                          const Spec& s, const uint32_t* bits) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0, 0};
+__device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e, const Spec& s,
+                                          const uint32_t* bits) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0};
   if (e >= re) return r;  // no record starts in this region
   const uint32_t b0 = bits[0], b1 = bits[1], b2 = bits[2], b3 = bits[3];
   uint32_t p = e;
@@ -268,25 +271,35 @@ __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t rs, uint32
   for (;; ++r.steps) {
     if (p >= re) break;
     const uint32_t i = p & 127u;
-    const uint32_t w = i < 64u ? (i < 32u ? b0 : b1) : (i < 96u ? b2 : b3);
-    if (((w >> (i & 31u)) & 1u) && p >= s.bad) {  // met the speculative chain
+    const uint32_t w = (i & 64u) ? ((i & 32u) ? b3 : b2) : ((i & 32u) ? b1 : b0);
+    if (__builtin_amdgcn_ubfe(w, i, 1) && p >= s.bad) {  // met the speculative chain
       const Bits sb{(uint64_t)b1 << 32 | b0, (uint64_t)b3 << 32 | b2};
       r.bm = bor(pb, bge(sb, i));
       r.wb = bor(pw, bge(s.wb, i));
       r.exit = s.exit;
       return r;
     }
-    uint32_t tg;
-    const int L = zlen(T, p, end_a, &tg);
-    if (L <= 0) {
+    const uint32_t tg = zb8(T, p);
+    uint32_t L = __builtin_amdgcn_ubfe(kZLutTrue, tg << 2, 4);
+    if (L == 15u || tg >= 8u) {  // rare: wide, Serializable or invalid
+      const int v = (tg >= 8u || tg == CLG_TAG_SERIALIZABLE) ? (int)kLenErr
+                    : tg == CLG_TAG_IGNORE_CHECKPOINT    ? 13
+                                                         : zlen_var(T, p, end_a, tg, 0);
+      if (v <= 0) {
+        r.bad = 1;
+        r.exit = s.exit;
+        return r;
+      }
+      L = (uint32_t)v;
+      bset(pw, i);
+    }
+    if (p + L > end_a || p + L < p) {
       r.bad = 1;
       r.exit = s.exit;
       return r;
     }
     bset(pb, i);
-    if (tg - 4u < 3u) bset(pw, i);
-    r.unclean |= L > kZSpecMax ? 1u : 0u;
-    p += (uint32_t)L;
+    p += L;
   }
   r.bm = pb;
   r.wb = pw;
@@ -458,7 +471,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk(s_img, rs, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0, 0};
+  Res r = rs < re ? merge_walk(s_img, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0};
   uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
@@ -468,7 +481,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     ++iters;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk(s_img, rs, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0, 0};
+      r = rs < re ? merge_walk(s_img, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0};
       steps_more += r.steps;
     }
   }

@@ -159,11 +159,16 @@ struct PendingTiming {
   uint64_t bytes;
 };
 
+// Guard bytes either side of the segment pool: the gather and decode kernels issue aligned
+// 16-B loads that may start before a piece's first byte or end past its last.
+constexpr size_t kPoolGuard = 256;
+
 }  // namespace
 
 struct clg_engine {
   clg_config cfg{};
   hipStream_t stream = nullptr;
+  void* pool_alloc = nullptr;  // pool minus the guard bytes either side
   uint8_t* pool = nullptr;
   std::vector<uint32_t> free_segs;
   std::vector<Log> logs;
@@ -1038,8 +1043,9 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
   void* p = nullptr;
-  HIPCHK(hipMalloc(&p, pool_bytes + 256));  // +256: aligned over-reads past the last segment
-  e->pool = static_cast<uint8_t*>(p);
+  HIPCHK(hipMalloc(&p, pool_bytes + 2 * kPoolGuard));  // guards: aligned over-reads either side
+  e->pool_alloc = p;
+  e->pool = static_cast<uint8_t*>(p) + kPoolGuard;
   e->free_segs.resize(cfg->pool_segments);
   for (uint32_t i = 0; i < cfg->pool_segments; ++i) e->free_segs[i] = cfg->pool_segments - 1 - i;
   *out = e.release();
@@ -1055,7 +1061,7 @@ void clg_engine_destroy(clg_engine* e) {
     hipEventDestroy(t.b);
   }
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
-  if (e->pool) hipFree(e->pool);
+  if (e->pool_alloc) hipFree(e->pool_alloc);
   hipStreamDestroy(e->stream);
   delete e;
 }

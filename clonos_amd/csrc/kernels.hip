@@ -52,30 +52,47 @@ __device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32
   }
 }
 
+// Each thread takes up to kGatherK destination chunks (256 threads apart) and issues all
+// their source loads before any store.  Chunks that straddle the piece's ends are written
+// byte by byte from the same registers (no dependent loads).  Source reads may touch up to
+// 16 bytes either side of the piece's source range: the pool has guard bytes both ends.
+constexpr int kGatherK = 4;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
   const GatherPiece p = pieces[blockIdx.x];
   if (p.len == 0) return;
-  uint8_t* dst = out + p.dst;
-  const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + p.len;
-  const uintptr_t a0 = d0 & ~(uintptr_t)15, a1 = (d1 - 1) & ~(uintptr_t)15;
+  const uintptr_t d0 = (uintptr_t)(out + p.dst), d1 = d0 + p.len;
+  const uintptr_t a0 = d0 & ~(uintptr_t)15;
   const uintptr_t sdelta = (uintptr_t)p.src - d0;  // src address = dst address + sdelta
-  const uint32_t m = (uint32_t)(((uintptr_t)p.src - d0) & 15);
-  for (uintptr_t c = a0 + 16 * threadIdx.x; c <= a1; c += 16 * blockDim.x) {
-    if (c >= d0 && c + 16 <= d1) {
-      const uintptr_t s = c + sdelta;
-      const uintptr_t sa = s & ~(uintptr_t)15;
-      uint4 v;
-      if (m == 0) {
-        v = *reinterpret_cast<const uint4*>(sa);
-      } else {
-        const uint4 lo = *reinterpret_cast<const uint4*>(sa);
-        const uint4 hi = *reinterpret_cast<const uint4*>(sa + 16);
-        v = funnel16(lo, hi, m);
+  const uint32_t m = (uint32_t)(sdelta & 15);
+  const uint32_t nch = (uint32_t)((((d1 + 15) & ~(uintptr_t)15) - a0) >> 4);
+  for (uint32_t j0 = 0; j0 < nch; j0 += kGatherK * 256) {
+    uint4 lo[kGatherK], hi[kGatherK];
+#pragma unroll
+    for (int k = 0; k < kGatherK; ++k) {
+      const uint32_t j = j0 + threadIdx.x + 256u * (uint32_t)k;
+      if (j < nch) {
+        const uintptr_t sa = (a0 + 16u * (uintptr_t)j + sdelta) & ~(uintptr_t)15;
+        lo[k] = *reinterpret_cast<const uint4*>(sa);
+        if (m) hi[k] = *reinterpret_cast<const uint4*>(sa + 16);
       }
-      *reinterpret_cast<uint4*>(c) = v;
-    } else {
-      const uintptr_t b0 = c < d0 ? d0 : c, b1 = c + 16 > d1 ? d1 : c + 16;
-      for (uintptr_t x = b0; x < b1; ++x) *reinterpret_cast<uint8_t*>(x) = *reinterpret_cast<const uint8_t*>(x + sdelta);
+    }
+#pragma unroll
+    for (int k = 0; k < kGatherK; ++k) {
+      const uint32_t j = j0 + threadIdx.x + 256u * (uint32_t)k;
+      if (j < nch) {
+        const uintptr_t c = a0 + 16u * (uintptr_t)j;
+        const uint4 v = m ? funnel16(lo[k], hi[k], m) : lo[k];
+        if (c >= d0 && c + 16 <= d1) {
+          const u32x4 nv = {v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(nv, reinterpret_cast<u32x4*>(c));
+        } else {  // piece edge: the bytes inside [d0, d1)
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int x = 0; x < 16; ++x)
+            if (c + x >= d0 && c + x < d1) *reinterpret_cast<uint8_t*>(c + x) = (uint8_t)(w[x >> 2] >> (8 * (x & 3)));
+        }
+      }
     }
   }
 }
