@@ -28,6 +28,7 @@ CLG_E_CAPACITY = -11
 CLG_E_STATE = -12
 CLG_E_DEVICE = -13
 CLG_E_NO_LOG = -14
+CLG_E_NOT_BUFFER_BUILT = -15
 
 STATUS_NAMES = {v: k for k, v in globals().items() if k.startswith("CLG_E_") or k == "CLG_OK"}
 
@@ -45,6 +46,8 @@ EXPORTED = [
     "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
     "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
+    "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
+    "clg_replay_prepare",
 ]
 
 
@@ -134,6 +137,48 @@ class Decoded(C.Structure):
     ]
 
 
+class ResponseEntry(C.Structure):
+    _fields_ = [("id", CausalLogIdC), ("bytes", C.c_void_p), ("len", C.c_uint64)]
+
+
+class Response(C.Structure):
+    _fields_ = [
+        ("found", C.c_int32),
+        ("vertex_id", C.c_int16),
+        ("reserved", C.c_int16),
+        ("correlation_id", C.c_int64),
+        ("n", C.c_uint32),
+        ("cap", C.c_uint32),
+        ("table_cap", C.c_uint32),
+        ("reserved2", C.c_uint32),
+        ("entries", C.POINTER(ResponseEntry)),
+    ]
+
+
+class ReplayVertex(C.Structure):
+    _fields_ = [
+        ("acc", C.POINTER(Response)),
+        ("subpartitions", C.POINTER(CausalLogIdC)),
+        ("n_subpartitions", C.c_uint32),
+        ("vertex_id", C.c_int16),
+        ("reserved", C.c_int16),
+    ]
+
+
+class ReplayOut(C.Structure):
+    _fields_ = [
+        ("main", C.POINTER(Decoded)),
+        ("main_rec_base", C.c_void_p),
+        ("buffer_sizes", C.c_void_p),
+        ("sizes_cap", C.c_uint64),
+        ("sizes_base", C.c_void_p),
+        ("sub_count", C.c_void_p),
+        ("sub_status", C.c_void_p),
+        ("sub_err_off", C.c_void_p),
+        ("sub_err_tag", C.c_void_p),
+    ]
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double), ("bytes", C.c_uint64)]
 
@@ -182,6 +227,12 @@ def _load() -> C.CDLL:
         "clg_replay_prep": (C.c_int, [P, P, P, P, P, C.c_uint32, P, u32p, C.POINTER(Decoded), P]),
         "clg_kernel_stats": (C.c_int, [P, C.POINTER(KernelStat), C.c_uint32, u32p]),
         "clg_kernel_stats_reset": (C.c_int, [P]),
+        "clg_response_put": (C.c_int, [C.POINTER(Response), C.POINTER(CausalLogIdC), P, C.c_uint64]),
+        "clg_response_write": (C.c_int, [C.POINTER(Response), P, C.c_uint64, u64p]),
+        "clg_response_read": (C.c_int, [P, C.c_uint64, C.POINTER(Response), u64p]),
+        "clg_response_merge": (C.c_int, [C.POINTER(Response), C.POINTER(Response)]),
+        "clg_causal_log_id_hash": (C.c_int32, [C.POINTER(CausalLogIdC)]),
+        "clg_replay_prepare": (C.c_int, [P, C.POINTER(ReplayVertex), C.c_uint32, C.POINTER(ReplayOut)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

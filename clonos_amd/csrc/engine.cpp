@@ -165,6 +165,10 @@ constexpr size_t kPoolGuard = 256;
 
 }  // namespace
 
+namespace clg_internal {  // error text for the host-only translation units (response.cpp)
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace clg_internal
+
 struct clg_engine {
   clg_config cfg{};
   hipStream_t stream = nullptr;
@@ -182,6 +186,8 @@ struct clg_engine {
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
+  DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
+  PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
   // timing
@@ -1393,6 +1399,120 @@ int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, co
   }
   if (!out) return CLG_OK;
   return clg_decode_host(e, bytes, so.data(), sl.data(), uint32_t(order.size()), out, span_rec_base);
+}
+
+// ReplayingState (:58-66, :108-130) + SubpartitionRecoveryThread.run (:157-188) +
+// LogReplayerImpl (:51-158), batched over failed vertices.  Main logs go through the
+// batched decode; subpartition recovery buffers through k_bufsizes (5-byte BufferBuilt
+// records, no chain walk).  All inputs are staged to HBM in one copy.
+int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out) {
+  ENGINE_GUARD(e);
+  if (!out || !out->main || !out->main_rec_base || (n && !v)) return fail(CLG_E_INVALID_ARG, "null argument");
+  struct Piece {
+    const uint8_t* p;
+    uint64_t len;
+  };
+  std::vector<Piece> mains(n), subs;
+  auto lookup = [](const clg_response* r, const clg_causal_log_id& id) -> Piece {
+    if (!r) return Piece{nullptr, 0};
+    for (uint32_t i = 0; i < r->n; ++i) {
+      const clg_causal_log_id& k = r->entries[i].id;
+      const bool eq = k.vertex_id == id.vertex_id && (k.is_main != 0) == (id.is_main != 0) &&
+                      (id.is_main || (k.irp_lower == id.irp_lower && k.irp_upper == id.irp_upper &&
+                                      k.subpartition == id.subpartition));
+      if (eq) return Piece{r->entries[i].bytes, r->entries[i].len};
+    }
+    return Piece{nullptr, 0};
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    if (v[i].n_subpartitions && !v[i].subpartitions) return fail(CLG_E_INVALID_ARG, "null subpartition table");
+    clg_causal_log_id mid{};
+    mid.vertex_id = v[i].vertex_id;
+    mid.is_main = 1;
+    mains[i] = lookup(v[i].acc, mid);
+    for (uint32_t j = 0; j < v[i].n_subpartitions; ++j) {
+      clg_causal_log_id sid = v[i].subpartitions[j];
+      sid.vertex_id = v[i].vertex_id;  // id.replace(lower, upper, index) keeps the vertex (:114, :121)
+      sid.is_main = 0;
+      subs.push_back(lookup(v[i].acc, sid));
+    }
+  }
+  const uint32_t ns = uint32_t(subs.size());
+  if (ns && (!out->sizes_base || !out->sub_count || !out->sub_status || !out->sub_err_off || !out->sub_err_tag))
+    return fail(CLG_E_INVALID_ARG, "null subpartition output");
+  // sizes capacity: one slot per whole 5-byte record
+  uint64_t n_sizes = 0;
+  for (uint32_t j = 0; j < ns; ++j) {
+    out->sizes_base[j] = n_sizes;
+    n_sizes += subs[j].len / 5;
+  }
+  if (ns) out->sizes_base[ns] = n_sizes;
+  if (n_sizes > out->sizes_cap || (n_sizes && !out->buffer_sizes))
+    return fail(CLG_E_CAPACITY, "buffer_sizes needs %llu entries", (unsigned long long)n_sizes);
+  // stage main logs then subpartition buffers (16-byte aligned pieces) in one copy
+  std::vector<uint64_t> at(n + ns);
+  uint64_t total = 0, main_bytes = 0, sub_bytes = 0;
+  for (uint32_t i = 0; i < n + ns; ++i) {
+    const Piece& pc = i < n ? mains[i] : subs[i - n];
+    at[i] = total;
+    total += (pc.len + 15) & ~uint64_t(15);
+    (i < n ? main_bytes : sub_bytes) += pc.len;
+  }
+  CHK(e->d_stage.ensure(total + 16));
+  CHK(e->h_stage.ensure(total + 16));
+  for (uint32_t i = 0; i < n + ns; ++i) {
+    const Piece& pc = i < n ? mains[i] : subs[i - n];
+    if (pc.len) memcpy(e->h_stage.as<uint8_t>() + at[i], pc.p, pc.len);
+  }
+  if (total) HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
+  const uint8_t* dst = e->d_stage.as<uint8_t>();
+  // subpartition buffers first (their kernels only read the staged bytes)
+  if (ns) {
+    std::vector<clg::BufSpan> bs(ns);
+    std::vector<clg::BufChunk> bc;
+    constexpr uint64_t kRecPerChunk = 256;
+    for (uint32_t j = 0; j < ns; ++j) {
+      bs[j] = clg::BufSpan{dst + at[n + j], subs[j].len, out->sizes_base[j]};
+      const uint64_t nk = (subs[j].len + 4) / 5;  // records incl. a partial tail
+      for (uint64_t k = 0; k < nk; k += kRecPerChunk)
+        bc.push_back(clg::BufChunk{j, 0, k, std::min(nk, k + kRecPerChunk)});
+    }
+    const size_t o_spans = 0, o_chunks = (ns * sizeof(clg::BufSpan) + 15) & ~size_t(15);
+    const size_t o_res = (o_chunks + bc.size() * sizeof(clg::BufChunk) + 15) & ~size_t(15);
+    const size_t res_bytes = size_t(ns) * (8 + 8 + 4 + 8 + 4);  // first_bad, count, status, err_off, err_tag
+    CHK(e->h_rmeta.ensure(o_res + res_bytes + 64));
+    CHK(e->d_rmeta.ensure(o_res + res_bytes + 64));
+    uint8_t* hm = e->h_rmeta.as<uint8_t>();
+    memcpy(hm + o_spans, bs.data(), ns * sizeof(clg::BufSpan));
+    memcpy(hm + o_chunks, bc.data(), bc.size() * sizeof(clg::BufChunk));
+    HIPCHK(hipMemcpyAsync(e->d_rmeta.p, hm, o_res, hipMemcpyHostToDevice, e->stream));
+    uint8_t* dm = e->d_rmeta.as<uint8_t>();
+    uint64_t* d_first = reinterpret_cast<uint64_t*>(dm + o_res);
+    uint64_t* d_count = d_first + ns;
+    int64_t* d_eoff = reinterpret_cast<int64_t*>(d_count + ns);
+    int32_t* d_status = reinterpret_cast<int32_t*>(d_eoff + ns);
+    int32_t* d_etag = d_status + ns;
+    HIPCHK(hipMemsetAsync(d_first, 0xFF, ns * 8, e->stream));
+    CHK(e->d_rsizes.ensure(std::max<uint64_t>(1, n_sizes) * 4));
+    const auto* d_spans = reinterpret_cast<const clg::BufSpan*>(dm + o_spans);
+    CHK(e->timed("replay_bufsizes", sub_bytes + 4 * n_sizes, [&] {
+      return clg::launch_bufsizes(reinterpret_cast<const clg::BufChunk*>(dm + o_chunks), uint32_t(bc.size()), d_spans,
+                                  e->d_rsizes.as<int32_t>(), d_first, e->stream);
+    }));
+    CHK(clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, e->stream));
+    if (n_sizes)
+      HIPCHK(hipMemcpyAsync(out->buffer_sizes, e->d_rsizes.p, n_sizes * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out->sub_count, d_count, ns * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out->sub_err_off, d_eoff, ns * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out->sub_status, d_status, ns * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(out->sub_err_tag, d_etag, ns * 4, hipMemcpyDeviceToHost, e->stream));
+  }
+  // main logs: the batched decode (span i = vertex i)
+  auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
+    for (uint32_t i = 0; i < n; ++i) e->plan_host_span(p, dst + at[i], mains[i].len, i, T);
+  };
+  CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
+  return e->sync();
 }
 
 int clg_kernel_stats(clg_engine* e, clg_kernel_stat* out, uint32_t cap, uint32_t* n) {

@@ -232,4 +232,27 @@ int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc
                        const TileConv* d_conv, const TileRes* d_tres, const SpanRes* d_sres,
                        const uint32_t* d_span_flags, DecodeOut out, void* stream);
 
+
+// ---- replay preparation: subpartition recovery buffers ----------------------------
+// A recovery buffer may hold BufferBuilt determinants only (ReplayingState.java:172-177),
+// which are 5 bytes each, so record k of a well-formed buffer starts at 5k: no chain walk.
+struct BufSpan {
+  const uint8_t* src;  // device bytes
+  uint64_t len;
+  uint64_t out_base;   // first index in the sizes array
+};
+struct BufChunk {      // records [k0, k1) of span `span`
+  uint32_t span;
+  uint32_t pad;
+  uint64_t k0, k1;
+};
+// first_bad[s] = lowest k whose record is not a complete BufferBuilt (init ~0).
+int launch_bufsizes(const BufChunk* d_chunks, uint32_t n_chunks, const BufSpan* d_spans, int32_t* d_sizes,
+                    uint64_t* d_first_bad, void* stream);
+// Per span: the count of valid sizes, and the status SubpartitionRecoveryThread.run hits at
+// record first_bad (decodeNext's error, or CLG_E_NOT_BUFFER_BUILT for a valid other record).
+int launch_bufsizes_classify(const BufSpan* d_spans, uint32_t n_spans, const uint64_t* d_first_bad,
+                             uint64_t* d_count, int32_t* d_status, int64_t* d_err_off, int32_t* d_err_tag,
+                             void* stream);
+
 }  // namespace clg

@@ -1,0 +1,182 @@
+"""Host-side mirror of DeterminantResponseEvent and of the replay preparation done by the
+recovery states, on top of the C-ABI (libclonos_engine.so).
+
+  DeterminantResponseEvent  reference flink-runtime/.../causal/DeterminantResponseEvent.java:36-148
+                            (write :93-107, read :109-125, merge :128-148) -> clg_response_*
+  WaitingDeterminantsState  .../causal/recovery/WaitingDeterminantsState.java:57,97-108
+                            (accumulator (found=true, vertex), merge every direct response)
+  ReplayingState            .../causal/recovery/ReplayingState.java:58-214 and
+  LogReplayerImpl           .../causal/recovery/LogReplayerImpl.java:51-158
+                            -> clg_replay_prepare (main logs decoded on the GPU; subpartition
+                               recovery buffers turned into BufferBuilt size lists on the GPU)
+
+The event's map keeps java.util.HashMap iteration order (see include/clonos_engine.h), so
+write() produces the reference's bytes.  Entries reference Python-owned byte buffers that
+this object keeps alive.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+from .engine import CausalLogID, DecodedBatch, Engine, _np_ptr
+
+
+def _from_c(c: _lib.CausalLogIdC) -> CausalLogID:
+    if c.is_main:
+        return CausalLogID.main(c.vertex_id)
+    return CausalLogID.sub(c.vertex_id, c.irp_lower, c.irp_upper, c.subpartition)
+
+
+def causal_log_id_hash(lid: CausalLogID) -> int:
+    """CausalLogID.hashCode (CausalLogID.java:151-163)."""
+    c = lid.to_c()
+    return lib.clg_causal_log_id_hash(C.byref(c))
+
+
+class DeterminantResponseEvent:
+    """DeterminantResponseEvent (found, vertexID, correlationID, Map<CausalLogID, ByteBuf>)."""
+
+    def __init__(self, found: bool = False, vertex_id: int = 0, correlation_id: int = 0, capacity: int = 256):
+        self._entries = (_lib.ResponseEntry * max(1, capacity))()
+        self._c = _lib.Response(1 if found else 0, vertex_id, 0, correlation_id, 0, capacity, 0, 0, self._entries)
+        self._keep: List[object] = []  # buffers the entries point into
+
+    # ---- accessors (:71-89)
+    def isFound(self) -> bool:
+        return bool(self._c.found)
+
+    def getVertexID(self) -> int:
+        return int(self._c.vertex_id)
+
+    def getCorrelationID(self) -> int:
+        return int(self._c.correlation_id)
+
+    def setCorrelationID(self, v: int) -> None:
+        self._c.correlation_id = v
+
+    def getDeterminants(self) -> Dict[CausalLogID, bytes]:
+        """The map, in java.util.HashMap iteration order."""
+        out = {}
+        for i in range(self._c.n):
+            e = self._entries[i]
+            out[_from_c(e.id)] = C.string_at(e.bytes, e.len) if e.len else b""
+        return out
+
+    def __len__(self) -> int:
+        return int(self._c.n)
+
+    def _grow(self, need: int) -> None:
+        if need <= self._c.cap:
+            return
+        cap = max(need, 2 * self._c.cap)
+        new = (_lib.ResponseEntry * cap)()
+        C.memmove(new, self._entries, C.sizeof(_lib.ResponseEntry) * self._c.n)
+        self._entries, self._c.entries, self._c.cap = new, new, cap
+
+    # ---- map building (JobCausalLogImpl.respondToDeterminantRequest :197-199)
+    def put(self, lid: CausalLogID, data: bytes) -> None:
+        buf = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(1, np.uint8)
+        self._keep.append(buf)
+        self._grow(self._c.n + 1)
+        c = lid.to_c()
+        check(lib.clg_response_put(C.byref(self._c), C.byref(c), _np_ptr(buf), len(data)))
+
+    # ---- wire format
+    def write(self) -> bytes:
+        n = C.c_uint64()
+        st = lib.clg_response_write(C.byref(self._c), None, 0, C.byref(n))
+        if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+            check(st)
+        out = np.empty(max(1, n.value), np.uint8)
+        check(lib.clg_response_write(C.byref(self._c), _np_ptr(out), n.value, C.byref(n)))
+        return out[:n.value].tobytes()
+
+    @staticmethod
+    def read(data: bytes) -> Tuple["DeterminantResponseEvent", int]:
+        buf = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(0, np.uint8)
+        ev = DeterminantResponseEvent(capacity=max(1, len(data) // 7 + 1))
+        ev._keep.append(buf)
+        used = C.c_uint64()
+        check(lib.clg_response_read(_np_ptr(buf) if buf.size else None, len(data), C.byref(ev._c), C.byref(used)))
+        return ev, int(used.value)
+
+    def merge(self, other: "DeterminantResponseEvent") -> None:
+        self._grow(self._c.n + other._c.n)
+        self._keep.extend(other._keep)
+        check(lib.clg_response_merge(C.byref(self._c), C.byref(other._c)))
+
+
+def accumulate(vertex_id: int, responses: Sequence[DeterminantResponseEvent]) -> DeterminantResponseEvent:
+    """WaitingDeterminantsState: new DeterminantResponseEvent(true, vertex) (:57), then merge
+    every direct response in arrival order (:102)."""
+    acc = DeterminantResponseEvent(True, vertex_id)
+    for r in responses:
+        acc.merge(r)
+    return acc
+
+
+@dataclass
+class SubpartitionReplay:
+    """What SubpartitionRecoveryThread.run (ReplayingState.java:157-214) would rebuild."""
+    log_id: CausalLogID
+    buffer_sizes: np.ndarray  # buildAndLogBuffer(n) arguments, in order
+    status: int               # CLG_OK or the error the thread hits after those buffers
+    err_off: int
+    err_tag: int
+
+
+@dataclass
+class VertexReplay:
+    vertex_id: int
+    main: DecodedBatch          # LogReplayerImpl's record sequence (span 0 of this batch view)
+    main_slice: slice
+    subpartitions: List[SubpartitionReplay]
+
+
+def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, Sequence[CausalLogID]]]
+                   ) -> Tuple[DecodedBatch, List[VertexReplay]]:
+    """ReplayingState construction for a batch of failed vertices: jobs are
+    (vertex_id, merged response, subpartition table in the task's order)."""
+    n = len(jobs)
+    vs = (_lib.ReplayVertex * max(1, n))()
+    tables = []
+    main_bytes, sub_bytes = 0, 0
+    for i, (vid, acc, subs) in enumerate(jobs):
+        t = (_lib.CausalLogIdC * max(1, len(subs)))(*[s.to_c() for s in subs])
+        tables.append(t)
+        vs[i] = _lib.ReplayVertex(C.pointer(acc._c), t, len(subs), vid, 0)
+        dets = acc.getDeterminants()
+        main_bytes += len(dets.get(CausalLogID.main(vid), b""))
+        sub_bytes += sum(len(dets.get(CausalLogID.sub(vid, s.irp_lower, s.irp_upper, s.subpartition), b""))
+                         for s in subs)
+    n_sub = sum(len(j[2]) for j in jobs)
+    cap = main_bytes // 2 + n + 1
+    d, arrs = engine._host_outputs(cap, main_bytes // 6 + n + 1)
+    base = np.zeros(n + 1, np.uint64)
+    sizes = np.empty(max(1, sub_bytes // 5), np.int32)
+    sbase = np.zeros(n_sub + 1, np.uint64)
+    cnt = np.zeros(max(1, n_sub), np.uint64)
+    sst = np.zeros(max(1, n_sub), np.int32)
+    soff = np.zeros(max(1, n_sub), np.int64)
+    stag = np.zeros(max(1, n_sub), np.int32)
+    out = _lib.ReplayOut(C.pointer(d), _np_ptr(base), _np_ptr(sizes), sizes.size, _np_ptr(sbase), _np_ptr(cnt),
+                         _np_ptr(sst), _np_ptr(soff), _np_ptr(stag))
+    st = lib.clg_replay_prepare(engine.handle, vs, n, C.byref(out))
+    main = engine._finish(st, d, arrs, base, n, None)
+    res, j = [], 0
+    for i, (vid, acc, subs) in enumerate(jobs):
+        sp = []
+        for s in subs:
+            lid = CausalLogID.sub(vid, s.irp_lower, s.irp_upper, s.subpartition)
+            b0 = int(sbase[j])
+            sp.append(SubpartitionReplay(lid, sizes[b0:b0 + int(cnt[j])].copy(), int(sst[j]), int(soff[j]),
+                                         int(stag[j])))
+            j += 1
+        res.append(VertexReplay(vid, main, main.span_slice(i), sp))
+    return main, res

@@ -49,7 +49,9 @@ enum {
   CLG_E_CAPACITY = -11,          /* caller output buffer too small; required size reported */
   CLG_E_STATE = -12,             /* inconsistent log state (index out of bounds) */
   CLG_E_DEVICE = -13,            /* HIP runtime error */
-  CLG_E_NO_LOG = -14             /* unknown / closed log handle */
+  CLG_E_NO_LOG = -14,            /* unknown / closed log handle */
+  CLG_E_NOT_BUFFER_BUILT = -15   /* subpartition recovery buffer holds another determinant
+                                    (RuntimeException, ReplayingState.java:172-177) */
 };
 
 enum { CLG_MEM_HOST = 0, CLG_MEM_DEVICE = 1 };
@@ -243,6 +245,78 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
 int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off,
                     const uint64_t* len, uint32_t n, uint32_t* winner, uint32_t* n_keys,
                     clg_decoded* out, uint64_t* span_rec_base);
+
+/* ---- DeterminantResponseEvent (DeterminantResponseEvent.java:36-148) ---------------------
+ * The event's map CausalLogID -> log bytes is held as an entry array in the iteration
+ * order of the reference's java.util.HashMap (JDK 8: 2^k buckets from 16, load factor
+ * 0.75, bins keep insertion order); `table_cap` is that map's bucket count.  Entries
+ * point at caller memory (clg_response_read: into the wire bytes).  A zeroed struct with
+ * entries/cap set is an empty map. */
+typedef struct clg_response_entry {
+  clg_causal_log_id id;
+  const uint8_t* bytes;
+  uint64_t len;
+} clg_response_entry;
+
+typedef struct clg_response {
+  int32_t found;
+  int16_t vertex_id;
+  int16_t reserved;
+  int64_t correlation_id;
+  uint32_t n;          /* entries, map iteration order */
+  uint32_t cap;        /* capacity of `entries` */
+  uint32_t table_cap;  /* HashMap bucket count (0: fresh map, 16) */
+  uint32_t reserved2;
+  clg_response_entry* entries;
+} clg_response;
+
+/* HashMap.put (:54-63 constructors, JobCausalLogImpl.java:197-199): insert or replace. */
+int clg_response_put(clg_response* r, const clg_causal_log_id* id, const uint8_t* bytes, uint64_t len);
+/* write (:93-107).  *n_out = wire size (also on CLG_E_CAPACITY). */
+int clg_response_write(const clg_response* r, uint8_t* out, uint64_t cap, uint64_t* n_out);
+/* read (:109-125).  The count byte is signed: 128..255 entries read back as none, like the
+ * reference.  *consumed = bytes read.  Truncated input: CLG_E_TRUNCATED. */
+int clg_response_read(const uint8_t* in, uint64_t n, clg_response* r, uint64_t* consumed);
+/* acc.merge(other) (:128-148): nothing if neither is found; per CausalLogID the longer
+ * buffer wins, ties -> other's (v2). */
+int clg_response_merge(clg_response* acc, const clg_response* other);
+/* CausalLogID.hashCode (:151-163), for callers keeping their own maps. */
+int32_t clg_causal_log_id_hash(const clg_causal_log_id* id);
+
+/* ---- replay preparation (ReplayingState.java:58-214, LogReplayerImpl.java:51-158) --------
+ * For each failed vertex v: its merged response (WaitingDeterminantsState.java:57,102 --
+ * start from found=true and clg_response_merge every response in arrival order) and the
+ * task's subpartition table.  One batch on the GPU:
+ *   main logs  -- CausalLogID(v) of each vertex (absent: empty span), batched decode into
+ *                 `main` (span v; LogReplayerImpl replays that record sequence);
+ *   subpartition buffers -- for table entry j the response's log (absent: EMPTY_BUFFER),
+ *                 BufferBuilt sizes into buffer_sizes[sizes_base[j] ...]
+ *                 (SubpartitionRecoveryThread.run :161-188); sub_status[j] is CLG_OK or the
+ *                 error that thread hits first (decode error of the record at sub_err_off,
+ *                 or CLG_E_NOT_BUFFER_BUILT); sizes before the error are valid and
+ *                 sub_count[j] gives their number.  Entries are global over all vertices, in
+ *                 vertex order then table order. */
+typedef struct clg_replay_vertex {
+  const clg_response* acc;
+  const clg_causal_log_id* subpartitions;
+  uint32_t n_subpartitions;
+  int16_t vertex_id;
+  int16_t reserved;
+} clg_replay_vertex;
+
+typedef struct clg_replay_out {
+  clg_decoded* main;          /* host output (out_kind CLG_MEM_HOST) */
+  uint64_t* main_rec_base;    /* n_vertices + 1 */
+  int32_t* buffer_sizes;      /* capacity sizes_cap */
+  uint64_t sizes_cap;
+  uint64_t* sizes_base;       /* n_subpartitions_total + 1 */
+  uint64_t* sub_count;
+  int32_t* sub_status;
+  int64_t* sub_err_off;
+  int32_t* sub_err_tag;
+} clg_replay_out;
+
+int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out);
 
 /* ---- instrumentation ---------------------------------------------------------------- */
 typedef struct clg_kernel_stat {
