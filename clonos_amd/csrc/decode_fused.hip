@@ -37,6 +37,7 @@
 // relaxed atomics (global_store/load ... sc1): the payload is the word itself.
 // Record layouts: SimpleDeterminantEncoder.java:124-323.
 #include "dev_common.h"
+#include "jser_device.h"
 
 namespace clg {
 
@@ -121,31 +122,32 @@ __device__ __forceinline__ uint32_t zb8(const uint32_t* T, uint32_t a) { return 
 __device__ __forceinline__ int zlen_var(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t tg, uint32_t x0) {
   if (tg == CLG_TAG_SERIALIZABLE)
     return ((x0 >> 8) | (zb(T, a + 4) << 24)) == 0x0500EDACu ? kZSer : (int)kLenErr;  // AC ED 00 05
+  // TimerTrigger / SourceCheckpoint, branch-free: the fields both need lie in bytes
+  // a+13 .. a+26, read as five independent LDS dwords (one round trip) and selected by tag.
+  //   TIMER_TRIGGER     [04][rc i32][ts i64][type u8]{[len i32][name]}        (:202-242)
+  //   SOURCE_CHECKPOINT [05][rc][cp i64][ts i64][type u8][hasRef u8]{[len][ref]} (:244-287)
   const uint32_t avail = end_a - a;
+  const uint32_t b0 = a + 13, k0 = b0 >> 2, sh = b0 & 3u;
+  const uint32_t d0 = T[rk(k0)], d1 = T[rk(k0 + 1)], d2 = T[rk(k0 + 2)], d3 = T[rk(k0 + 3)], d4 = T[rk(k0 + 4)];
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);  // bytes a+13 .. a+16 (LE)
+  const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);  // a+17 .. a+20
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // a+21 .. a+24
+  const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);  // a+25 .. a+28
+  const int tt_ord = (int8_t)(w0 & 0xFFu);                                      // ProcessingTimeCallbackID.Type
+  const int32_t tt_nl = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, 1));  // a+14 .. a+17
+  const int sc_ord = (int8_t)(w2 & 0xFFu);                                      // CheckpointType (:27, :30)
+  const bool sc_ref = ((w2 >> 8) & 0xFFu) != 0u;
+  const int32_t sc_rl = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w3, w2, 2));  // a+23 .. a+26
   uint64_t L;
-  if (tg == CLG_TAG_TIMER_TRIGGER) {  // [04][rc i32][ts i64][type u8]{[len i32][name]}  (:202-242)
-    if (avail < 14u) return (int)kLenErr;
-    const int ord = (int8_t)zb(T, a + 13);
-    if (ord < 0 || ord > 6) return (int)kLenErr;  // ProcessingTimeCallbackID.Type (:33-34)
-    L = 14;
-    if (ord == 6) {
-      if (avail < 18u) return (int)kLenErr;
-      const int32_t nl = (int32_t)zbe32(T, a + 14);
-      if (nl < 0) return (int)kLenErr;
-      L = 18ull + (uint64_t)nl;
-    }
-  } else {  // SOURCE_CHECKPOINT [05][rc][cp i64][ts i64][type u8][hasRef u8]{[len][ref]}  (:244-287)
-    if (avail < 23u) return (int)kLenErr;
-    L = 23;
-    if (zb(T, a + 22) != 0) {
-      if (avail < 27u) return (int)kLenErr;
-      const int32_t rl = (int32_t)zbe32(T, a + 23);
-      if (rl < 0) return (int)kLenErr;
-      L = 27ull + (uint64_t)rl;
-    }
-    const int ord = (int8_t)zb(T, a + 21);
-    if (ord < 0 || ord > 1) return (int)kLenErr;  // CheckpointType (:27, :30)
+  bool ok;
+  if (tg == CLG_TAG_TIMER_TRIGGER) {
+    ok = avail >= 14u && tt_ord >= 0 && tt_ord <= 6 && (tt_ord != 6 || (avail >= 18u && tt_nl >= 0));
+    L = tt_ord == 6 ? 18ull + (uint64_t)(uint32_t)tt_nl : 14ull;
+  } else {
+    ok = avail >= 23u && sc_ord >= 0 && sc_ord <= 1 && (!sc_ref || (avail >= 27u && sc_rl >= 0));
+    L = sc_ref ? 27ull + (uint64_t)(uint32_t)sc_rl : 23ull;
   }
+  if (!ok) return (int)kLenErr;
   return (L > avail || L > 0x7FFFFFF0ull) ? (int)kLenErr : (int)L;
 }
 __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_a, uint32_t* tag) {
@@ -184,14 +186,35 @@ struct Spec {
 // 15: TimerTrigger / SourceCheckpoint / IgnoreCheckpoint, the out-of-line case);
 // Serializable and invalid tags are never followed.  *wide: the record is a wide one.
 constexpr uint32_t kZLut = 2u | 9u << 4 | 5u << 8 | 0u << 12 | 15u << 16 | 15u << 20 | 15u << 24 | 5u << 28;
-__device__ __forceinline__ uint32_t zspec_len(const uint32_t* T, uint32_t a, uint32_t end_a, bool* wide) {
+constexpr uint32_t kZLutJ = kZLut | 15u << 12;  // with tables: Serializable is a wide case too
+
+// Serializable record lengths of the tile (phase 3 tables), staged in LDS: a candidate
+// bitmap over aligned coordinates, the number of candidates before each bitmap dword, and
+// the record length per candidate (0: the stream is invalid).
+constexpr uint32_t kZJBitsDw = (kZTile + 16 + 31) / 32 + 3;  // 260
+struct JL {
+  const uint32_t* bits;
+  const uint32_t* rank;
+  const uint32_t* len;
+};
+__device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
+  const uint32_t w = j.bits[a >> 5], b = a & 31u;
+  if (!((w >> b) & 1u)) return 0u;
+  return j.len[j.rank[a >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))];
+}
+
+template <bool J>
+__device__ __forceinline__ uint32_t zspec_len(const uint32_t* T, uint32_t a, uint32_t end_a, bool* wide, const JL& jl) {
   const uint32_t tg = zb8(T, a);
-  uint32_t L = __builtin_amdgcn_ubfe(kZLut, tg << 2, 4);
+  uint32_t L = __builtin_amdgcn_ubfe(J ? kZLutJ : kZLut, tg << 2, 4);
   *wide = false;
   if (L == 15u && tg < 8u) {
     *wide = true;
     if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
       L = 13;
+    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
+      L = jl_len(jl, a);
+      L = L <= (uint32_t)kZSpecMax ? L : 0u;
     } else {
       const int v = zlen_var(T, a, end_a, tg, 0);
       L = (v > 0 && v <= kZSpecMax) ? (uint32_t)v : 0u;
@@ -207,19 +230,20 @@ __device__ __forceinline__ uint32_t zspec_len(const uint32_t* T, uint32_t a, uin
 // followed starts are or-ed into the lane's LDS bitmap `bits` (bit i <-> byte r0 + i,
 // r0 = rs & ~127; zeroed by the caller).
 constexpr uint32_t kZWarm = 96;
+template <bool J>
 __device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
-                                          uint32_t* bits) {
+                                          uint32_t* bits, const JL& jl) {
   Spec s{{0, 0}, rs, rs, 0};
   uint32_t q = ws;
   while (q < rs) {
     bool w;
-    const uint32_t L = zspec_len(T, q, end_a, &w);
+    const uint32_t L = zspec_len<J>(T, q, end_a, &w, jl);
     q += L > 1u ? L : 1u;
   }
   s.first = q;
   while (q < re) {
     bool w;
-    const uint32_t L = zspec_len(T, q, end_a, &w);
+    const uint32_t L = zspec_len<J>(T, q, end_a, &w, jl);
     const uint32_t nq = q + (L > 1u ? L : 1u);
     atomicOr(&bits[(q >> 5) & 3u], L ? 1u << (q & 31u) : 0u);
     if (w && L) bset(s.wb, q & 127u);
@@ -232,8 +256,9 @@ __device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32
 
 // Canonical chain: the speculative rule from entry e, merged with the region's
 // speculative chain (both follow the same rule, so meeting means identical from there).
+template <bool J>
 __device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
-                                               const Spec& s) {
+                                               const Spec& s, const JL& jl) {
   if (e >= re) return e;
   uint32_t p = e, q = s.first;
   for (;;) {
@@ -241,7 +266,7 @@ __device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, u
     if (p >= re) return p;
     bool w;
     const uint32_t x = p < q ? p : q;
-    const uint32_t L = zspec_len(T, x, end_a, &w);
+    const uint32_t L = zspec_len<J>(T, x, end_a, &w, jl);
     const uint32_t nx = x + (L > 1u ? L : 1u);
     if (p < q) p = nx; else q = nx;
   }
@@ -250,7 +275,7 @@ __device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, u
 struct Res {
   Bits bm, wb;     // true record starts in the region / wide ones
   uint32_t exit;   // first true start >= re (bad: the speculative exit)
-  uint32_t bad;    // true chain hits an invalid or Serializable record
+  uint32_t bad;    // true chain hits an invalid record (1) or, without tables, a Serializable one (2)
   uint32_t steps;  // true steps taken (diagnostics)
 };
 
@@ -261,8 +286,9 @@ constexpr uint32_t kZLutTrue = 2u | 9u << 4 | 5u << 8 | 15u << 12 | 15u << 16 | 
 // True chain from entry e (e >= rs) merged with the speculative chain (its starts are the
 // lane's LDS bitmap `bits`): walk the true chain until it lands on a speculative start
 // past the speculative chain's last skip; from there on the two chains are the same.
+template <bool J>
 __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e, const Spec& s,
-                                          const uint32_t* bits) {
+                                          const uint32_t* bits, const JL& jl) {
   Res r{{0, 0}, {0, 0}, e, 0, 0};
   if (e >= re) return r;  // no record starts in this region
   const uint32_t b0 = bits[0], b1 = bits[1], b2 = bits[2], b3 = bits[3];
@@ -282,11 +308,23 @@ __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t re, uint32
     const uint32_t tg = zb8(T, p);
     uint32_t L = __builtin_amdgcn_ubfe(kZLutTrue, tg << 2, 4);
     if (L == 15u || tg >= 8u) {  // rare: wide, Serializable or invalid
-      const int v = (tg >= 8u || tg == CLG_TAG_SERIALIZABLE) ? (int)kLenErr
-                    : tg == CLG_TAG_IGNORE_CHECKPOINT    ? 13
-                                                         : zlen_var(T, p, end_a, tg, 0);
+      int v;
+      uint32_t why = 1u;
+      if (tg >= 8u) {
+        v = (int)kLenErr;
+      } else if (tg == CLG_TAG_SERIALIZABLE) {
+        if (J) {
+          const uint32_t jv = jl_len(jl, p);
+          v = jv ? (int)jv : (int)kLenErr;
+        } else {  // a stream with the magic needs the tables (abort reason 5)
+          v = (int)kLenErr;
+          why = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
+        }
+      } else {
+        v = tg == CLG_TAG_IGNORE_CHECKPOINT ? 13 : zlen_var(T, p, end_a, tg, 0);
+      }
       if (v <= 0) {
-        r.bad = 1;
+        r.bad = why;
         r.exit = s.exit;
         return r;
       }
@@ -427,13 +465,15 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
 // true chain enters the tile, so a block publishes it for its chunk's last tile before
 // decoding anything; the true chain meets it inside those 2 KiB unless the data never
 // re-synchronises, and then the exit check in count_tile aborts the batch.
-__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t* s_bits, uint32_t lane) {
+template <bool J>
+__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t* s_bits, uint32_t lane,
+                                               const JL& jl) {
   const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
   const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
   const bool on = lane >= c0 && z.rs < z.re;
   const uint32_t ws = z.rs >= z.lo + kZWarm ? z.rs - kZWarm : z.lo;
   uint32_t* bits = s_bits + lane * kZBitsPitch;
-  const Spec sp = on ? spec_walk(s_img, ws, z.rs, z.re, z.end_a, bits) : Spec{{0, 0}, z.rs, z.rs, 0};
+  const Spec sp = on ? spec_walk<J>(s_img, ws, z.rs, z.re, z.end_a, bits, jl) : Spec{{0, 0}, z.rs, z.rs, 0};
   uint32_t cx = sp.exit, entry = kZCanon;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(cx, 1);
@@ -442,7 +482,7 @@ __device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s
     if (!__any(ch)) break;
     if (ch) {
       entry = want;
-      cx = on ? canon_walk(s_img, z.rs, z.re, z.end_a, want, sp) : want;
+      cx = on ? canon_walk<J>(s_img, z.rs, z.re, z.end_a, want, sp, jl) : want;
     }
   }
   return __shfl(cx, 63);
@@ -452,9 +492,10 @@ __device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s
 // true chain, exit checks, then the tile's record / wide-record counts and its
 // record-start bitmap (1 KiB) for the emit pass.  *x_true = the tile's exit.  must_exit:
 // the exit the successor already uses (kZCanon: none).  false once the batch aborted.
+template <bool J>
 __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
-                                           uint32_t* s_bits, const uint32_t lane, uint32_t* x_out) {
+                                           uint32_t* s_bits, const uint32_t lane, uint32_t* x_out, const JL& jl) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
@@ -463,7 +504,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   const uint32_t ws = rs >= lo + kZWarm ? rs - kZWarm : lo;
   uint32_t* bits = s_bits + lane * kZBitsPitch;
   bits[0] = bits[1] = bits[2] = bits[3] = 0;
-  const Spec sp = rs < re ? spec_walk(s_img, ws, rs, re, end_a, bits) : Spec{{0, 0}, rs, rs, 0};
+  const Spec sp = rs < re ? spec_walk<J>(s_img, ws, rs, re, end_a, bits, jl) : Spec{{0, 0}, rs, rs, 0};
 
   ZPHASE(2);
   // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
@@ -471,7 +512,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk(s_img, re, end_a, entry, sp, bits) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  Res r = rs < re ? merge_walk<J>(s_img, re, end_a, entry, sp, bits, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
   uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
@@ -481,7 +522,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     ++iters;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk(s_img, re, end_a, want, sp, bits) : Res{{0, 0}, {0, 0}, want, 0, 0};
+      r = rs < re ? merge_walk<J>(s_img, re, end_a, want, sp, bits, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
       steps_more += r.steps;
     }
   }
@@ -496,7 +537,10 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   }
   const uint32_t x_true = __shfl(r.exit, 63);
   *x_out = x_true;
-  uint32_t reason = __any(r.bad) ? 1u : 0u;  // the true chain meets an invalid / Serializable record
+  // the true chain meets an invalid record (1) or a Serializable one without tables (5):
+  // the lowest such lane decides (lanes above it may have run from guessed entries)
+  const uint64_t badm = __ballot(r.bad != 0u);
+  uint32_t reason = badm ? (__shfl(r.bad, (int)__builtin_ctzll(badm)) == 2u ? 5u : 1u) : 0u;
   if (z.last) {
     if (x_true != end_a) reason = reason ? reason : 2u;  // the last record must end at the span end
   } else if (must_exit != kZCanon && x_true != must_exit) {
@@ -596,6 +640,20 @@ __global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
 // contiguous run.
 // ---------------------------------------------------------------------------------
+// Record length of the Serializable record at aligned coordinate a of tile t (phase 3
+// table, sorted by position; 0 if absent or invalid -- the count pass has already
+// rejected such records).
+__device__ __forceinline__ uint32_t jtab_len(const FusedCtl& ctl, uint32_t t, uint32_t a) {
+  const CLG_GLOBAL uint32_t* pos = gp(ctl.jpos) + (uint64_t)t * kZJCap;
+  uint32_t lo = 0, hi = min(gp(ctl.jn)[t], kZJCap);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pos[mid] < a) lo = mid + 1; else hi = mid;
+  }
+  return (lo < min(gp(ctl.jn)[t], kZJCap) && pos[lo] == a) ? gp(ctl.jlen)[(uint64_t)t * kZJCap + lo] : 0u;
+}
+
+template <bool J>
 __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                     FusedCtl ctl, DecodeOut out) {
   __shared__ uint32_t s_img[kZImgDw];
@@ -659,8 +717,8 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
         const ZBytes b{s_img, a};
         int tagd;
         uint32_t tgu;
-        const int L = zlen(s_img, a, end_a, &tgu);
-        tagd = (int)tgu;
+        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jtab_len(ctl, t, a) : zlen(s_img, a, end_a, &tgu);
+        tagd = (int)tg;
         decode_fields(b, tagd, (int64_t)L, rr);
         v0 = rr.v0;
       }
@@ -698,11 +756,53 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
 // and a chunk's first tile enters at the previous chunk's published exit, which that
 // chunk's last tile must then reproduce.  Blocks are all resident and publish first, so
 // the one wait always ends; a wait past kZSpinLimit cycles aborts the batch instead.
+// Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
+__device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane) {
+  uint32_t* bits = s_j;
+  uint32_t* rank = s_j + kZJBitsDw;
+  uint32_t* len = s_j + 2 * kZJBitsDw;
+  for (uint32_t i = lane; i < kZJBitsDw; i += 64) bits[i] = 0;
+  __syncthreads();
+  const uint32_t n = min(gp(ctl.jn)[t], kZJCap);
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t a = gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
+    len[i] = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    atomicOr(&bits[a >> 5], 1u << (a & 31u));
+  }
+  __syncthreads();
+  // ranks: lane l takes dwords [5 l, 5 l + 5) (64 x 5 >= 260)
+  uint32_t c[5], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t i = 5 * lane + (uint32_t)k;
+    c[k] = i < kZJBitsDw ? (uint32_t)__popc(bits[i]) : 0u;
+    sum += c[k];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += y;
+  }
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t i = 5 * lane + (uint32_t)k;
+    if (i < kZJBitsDw) rank[i] = run;
+    run += c[k];
+  }
+  __syncthreads();
+  return JL{bits, rank, len};
+}
+
+template <bool J>
 __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_bits[64 * kZBitsPitch];  // speculative-start bitmaps, one row per lane
+  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
+  JL jl{nullptr, nullptr, nullptr};
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
   const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
   if (t0 >= t1) return;
@@ -712,7 +812,8 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
-      x_pub = canon_exit(z, s_img, s_bits, lane);
+      if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
+      x_pub = canon_exit<J>(z, s_img, s_bits, lane, jl);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
@@ -744,10 +845,141 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const uint64_t ee = xs - z.td.span_off + z.lo;
     const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
     stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+    if (J) jl = load_jl(ctl, t, s_j, lane);
     uint32_t x_true;
-    if (!count_tile(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, s_bits, lane, &x_true)) return;
+    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, s_bits, lane, &x_true, jl)) return;
     x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Phase 3 (only for batches holding Serializable records): per tile, the positions of
+// "03 AC ED 00 05" (tag + stream magic) and the record length there -- the length of one
+// Java serialization stream (jser_device.h walker; TC_STRING streams inline), 0 for an
+// invalid stream.  Streams may run past the tile: bytes beyond the LDS image are read
+// from the span's next tiles in HBM.
+// ---------------------------------------------------------------------------------
+struct ZStreamBytes {  // stream byte k = span byte at aligned coordinate base + k
+  const uint32_t* T;
+  uint32_t base, img_end, lo;
+  uint64_t so;  // span offset of aligned coordinate lo
+  const TileDesc* tiles;
+  uint32_t k, t1;  // tile searched last, end of the span's tiles
+  __device__ int operator()(uint64_t i) {
+    const uint64_t a = base + i;
+    if (a < img_end) return (int)zb(T, (uint32_t)a);
+    const uint64_t o = so + (a - lo);
+    while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+    const TileDesc d = tiles[k];
+    return (int)gp(d.abase)[d.delta + (uint32_t)(o - d.span_off)];
+  }
+};
+
+// Record length of the common stream shape, inline and call-free: one TC_OBJECT whose
+// class and superclasses are fresh TC_CLASSDESCs with flags SC_SERIALIZABLE only, primitive
+// fields only and an empty annotation (java.lang.Boolean, Integer, Long, ...); its class
+// data is then the fields' primitive values.  0: some other shape (the general walker
+// decides), or the stream leaves the LDS image.  Grammar: Java Object Serialization
+// Specification 6.4 (newObject, newClassDesc, classDescInfo, fieldDesc, nowrclass).
+__device__ __forceinline__ uint32_t jser_flat_len(const uint32_t* T, uint32_t a, uint32_t img_end) {
+  uint32_t p = a + 5;  // after the tag and AC ED 00 05
+  if (p + 1 > img_end || zb(T, p) != jser::TC_OBJECT) return 0u;
+  ++p;
+  uint32_t data = 0;
+  for (int depth = 0;; ++depth) {
+    if (p + 1 > img_end || depth > 8) return 0u;
+    const uint32_t b = zb(T, p);
+    if (b == jser::TC_NULL) {  // no (further) superclass
+      ++p;
+      break;
+    }
+    if (b != jser::TC_CLASSDESC || p + 3 > img_end) return 0u;
+    p += 3 + (zb(T, p + 1) << 8 | zb(T, p + 2)) + 8;  // className, serialVersionUID
+    if (p + 3 > img_end || zb(T, p) != jser::SC_SERIALIZABLE) return 0u;
+    const uint32_t nf = zb(T, p + 1) << 8 | zb(T, p + 2);
+    if (nf & 0x8000u) return 0u;
+    p += 3;
+    for (uint32_t i = 0; i < nf; ++i) {
+      if (p + 3 > img_end) return 0u;
+      const uint32_t tc = zb(T, p);
+      // primitive sizes: B 1, C 2, D 8, F 4, I 4, J 8, S 2, Z 1
+      const uint32_t sz = tc == 'B' || tc == 'Z' ? 1u : tc == 'C' || tc == 'S' ? 2u : tc == 'I' || tc == 'F' ? 4u
+                          : tc == 'J' || tc == 'D' ? 8u : 0u;
+      if (!sz) return 0u;
+      data += sz;
+      p += 3 + (zb(T, p + 1) << 8 | zb(T, p + 2));
+    }
+    if (p + 1 > img_end || zb(T, p) != jser::TC_ENDBLOCKDATA) return 0u;
+    ++p;
+  }
+  p += data;
+  return p <= img_end ? p - a : 0u;
+}
+
+__device__ __forceinline__ bool zmagic(const uint32_t* T, uint32_t a) {
+  return zb(T, a) == CLG_TAG_SERIALIZABLE && zbe32(T, a + 1) == 0xACED0005u;
+}
+
+__global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                    FusedCtl ctl) {
+  __shared__ uint32_t s_img[kZImgDw];
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  const ZTile z = ztile(tiles, spans, t, lane);
+  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+  const uint64_t after = z.td.span_off + z.td.len;
+  const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
+  const uint32_t img_end = z.hi + (rem < (uint64_t)kZHalo ? (uint32_t)rem : kZHalo);
+  // candidates in the lane's region: bytes equal to 03 (zero-byte test per dword), then the magic
+  uint32_t nm = 0;
+  for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
+    const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
+    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t a = 4 * k + i;
+      nm += (a >= z.rs && a < z.re && zmagic(s_img, a)) ? 1u : 0u;
+    }
+  }
+  uint32_t ex = nm;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(ex, off);
+    if ((int)lane >= off) ex += y;
+  }
+  const uint32_t total = __shfl(ex, 63);
+  if (lane == 0) {
+    gp(ctl.jn)[t] = total;
+    if (total) atomicAdd(ctl.abort + 7, total);
+    if (total > kZJCap) raise_abort(ctl, 6, t);
+  }
+  if (!nm) return;
+  uint32_t idx = ex - nm;
+  const uint32_t t1 = z.sd.first_tile + z.sd.n_tiles;
+  for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
+    const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
+    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t a = 4 * k + i;
+      if (a < z.rs || a >= z.re || !zmagic(s_img, a)) continue;
+      const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
+      uint64_t L;
+      const uint32_t fl = zb(s_img, a + 5) == jser::TC_OBJECT ? jser_flat_len(s_img, a, img_end) : 0u;
+      if (zb(s_img, a + 5) == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+        L = 8ull + (zb(s_img, a + 6) << 8 | zb(s_img, a + 7));
+        L = L <= avail ? L : 0ull;
+      } else if (fl) {
+        L = fl <= avail ? fl : 0ull;
+      } else {
+        ZStreamBytes acc{s_img, a + 1, img_end, z.lo, z.td.span_off, tiles, t + 1, t1};
+        const int64_t sl = jser::stream_len(acc, avail - 1);
+        L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
+      }
+      if (idx < kZJCap) {
+        gp(ctl.jpos)[(uint64_t)t * kZJCap + idx] = a;
+        gp(ctl.jlen)[(uint64_t)t * kZJCap + idx] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
+      }
+      ++idx;
+    }
   }
 }
 
@@ -757,24 +989,34 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
   ctl.n_tiles = n_tiles;
   hipStream_t st = (hipStream_t)stream;
   if (phase == 0) {
-    static int resident = 0;  // blocks the device keeps resident for the count kernel
-    if (!resident) {
+    static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
+    const int j = ctl.jser ? 1 : 0;
+    if (!resident[j]) {
       int dev = 0, per_cu = 0, cus = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count, 64, 0) != hipSuccess ||
+      const hipError_t oe = j ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<true>, 64, 0)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<false>, 64, 0);
+      if (hipGetDevice(&dev) != hipSuccess || oe != hipSuccess ||
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
         return CLG_E_DEVICE;
-      resident = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
+      resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
     }
-    const uint32_t grid = n_tiles < (uint32_t)resident ? n_tiles : (uint32_t)resident;
-    hipLaunchKernelGGL(k_decode_count, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    const uint32_t grid = n_tiles < (uint32_t)resident[j] ? n_tiles : (uint32_t)resident[j];
+    if (j)
+      hipLaunchKernelGGL(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    else
+      hipLaunchKernelGGL(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
     hipLaunchKernelGGL(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
     hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
+  } else if (phase == 2) {
+    if (ctl.jser)
+      hipLaunchKernelGGL(k_decode_emit<true>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+    else
+      hipLaunchKernelGGL(k_decode_emit<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else {
-    hipLaunchKernelGGL(k_decode_emit, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+    hipLaunchKernelGGL(k_decode_jser, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }
   return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
 }

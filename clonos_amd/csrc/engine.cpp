@@ -186,6 +186,8 @@ struct clg_engine {
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
+  DevBuf d_zjpos, d_zjlen, d_zjn;    // fast decode: Serializable length tables (phase 3)
+  bool jser_hint = false;            // the last batches held Serializable records: build tables first
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
@@ -762,8 +764,12 @@ struct clg_engine {
 
   // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
   // anything outside its fast path; the caller then runs the robust pipeline.
-  int run_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted) {
+  // jser: build the Serializable tables first (phase 3).  *need_jser: the batch aborted
+  // only because it met Serializable records without tables.
+  int run_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted,
+                bool jser, bool* need_jser) {
     *aborted = false;
+    *need_jser = false;
     reset_result(out);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     if (ns == 0) return CLG_OK;
@@ -792,14 +798,23 @@ struct clg_engine {
       CHK(d_prof.ensure(size_t(nt) * 64));
       HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
     }
+    if (jser) {
+      CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
+      CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
+      CHK(d_zjn.ensure(size_t(nt) * 4));
+    }
     clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), w + 3 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
-                      getenv("CLONOS_FUSED_NODEP") ? 1u : 0u};
+                      getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
+                      jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
+                      jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, 0u};
     HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
     HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
+    if (jser)
+      CHK(timed("decode_jser", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 3); }));
     CHK(timed("decode_count", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 0); }));
     CHK(timed("decode_offsets", 24 * uint64_t(nt), [&] {
       return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 1);
@@ -824,11 +839,16 @@ struct clg_engine {
       }
     }
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
+    if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[0]) {
       *aborted = true;
+      // Serializable records were met without tables: other aborts may be consequences
+      // (entries guessed across them), so the tables decide; a second abort goes robust
+      *need_jser = !jser && hab[5];
       if (getenv("CLONOS_FUSED_DEBUG"))
-        fprintf(stderr, "[clonos] fused decode aborted (%u tiles): first tile per reason bad=%d end=%d exit=%d timeout=%d\n",
-                nt, int(~hab[1]), int(~hab[2]), int(~hab[3]), int(~hab[4]));
+        fprintf(stderr, "[clonos] fused decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d exit=%d "
+                "timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]), int(~hab[3]),
+                int(~hab[4]), int(~hab[5]), int(~hab[6]));
       if (zdbg) {
         std::vector<uint32_t> hd(16 + 64 * 8);
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
@@ -869,8 +889,12 @@ struct clg_engine {
     if (fused_decode && log_bytes / 2 < (1ull << 31)) {
       DecodePlan pf;
       build(pf, clg::kZTile);
-      bool aborted = false;
-      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted));
+      bool aborted = false, need_jser = false;
+      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, jser_hint, &need_jser));
+      if (aborted && need_jser) {  // Serializable records: again with the length tables
+        stats["decode_jser_retry"].launches++;
+        CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &need_jser));
+      }
       if (!aborted) return CLG_OK;
       stats["decode_fallback"].launches++;
     }

@@ -176,8 +176,20 @@ struct FusedCtl {
   uint64_t* prof;     // optional per-tile phase stamps (CLONOS_SCAN_PHASES): s_memtime x 8
   uint32_t n_tiles;
   uint32_t nodep;     // developer timing mode (CLONOS_FUSED_NODEP): tiles independent, output invalid
+  // Serializable record lengths per tile (phase 3, k_decode_jser), sorted by position:
+  // jpos/jlen[t * kZJCap + i] (aligned coordinate, record length or 0 for an invalid
+  // stream), jn[t] entries.  jser = 1: the tables exist and the passes use them.
+  uint32_t* jpos;
+  uint32_t* jlen;
+  uint32_t* jn;
+  uint32_t jser;
+  uint32_t pad;
 };
-// phase 0: count, 1: scan, 2: emit
+constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
+// abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
+// 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
+// abort[7] = Serializable candidates found by phase 3 (all tiles)
+// phase 0: count, 1: scan, 2: emit, 3: Serializable tables
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 

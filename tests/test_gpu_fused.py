@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
-from clonos_amd import CausalLogID, Engine
+from clonos_amd import CausalLogID, ClonosError, Engine
 from clonos_amd import determinants as D
 from clonos_amd import synth
 from test_gpu_decode import assert_span_equal
@@ -110,12 +110,62 @@ def test_fused_wide_records_side_table(feng):
     assert not fell_back(feng)
 
 
-def test_fused_serializable_falls_back(feng):
+def test_fused_serializable_tables(feng):
+    """Serializable streams: the first batch aborts once (no tables), re-runs with the
+    phase-3 length tables and stays on the fast path; the next batch builds the tables
+    up front (no retry)."""
     rng = np.random.default_rng(3)
     buf, _ = synth.config3_epoch(20000, rng)
     dec = feng.decode_host(buf.tobytes())
     assert_span_equal(dec, 0, buf.tobytes())
-    assert fell_back(feng)
+    st = feng.kernel_stats()
+    if feng.segment_bytes == 16384:
+        assert not fell_back(feng)
+        assert st["decode_jser_retry"]["launches"] == 1
+    feng.kernel_stats_reset()
+    buf2, _ = synth.config3_epoch(30000, rng)
+    dec = feng.decode_host(buf2.tobytes())
+    assert_span_equal(dec, 0, buf2.tobytes())
+    st = feng.kernel_stats()
+    if feng.segment_bytes == 16384:  # 256-byte tiles re-synchronise too rarely: robust path
+        assert "decode_jser_retry" not in st and st["decode_jser"]["launches"] == 1
+        assert not fell_back(feng)
+
+
+def test_fused_serializable_long_streams(feng):
+    """Streams far longer than a tile (int[] of 6000 elements = 24 KiB) and strings placed
+    across tile boundaries: the table kernel reads past its LDS image from HBM."""
+    rng = np.random.default_rng(11)
+    parts = []
+    for i in range(40):
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            parts.append(D.encode(D.SerializableDeterminant(D.jser_int_array(
+                rng.integers(-2**31, 2**31, int(rng.integers(1000, 6000))).tolist()))))
+        elif k == 1:
+            parts.append(D.encode(D.SerializableDeterminant(D.jser_string("x" * int(rng.integers(0, 9000))))))
+        else:
+            parts.append(synth.random_log(int(rng.integers(1, 900)), rng, allow_serializable=(k == 2)))
+    buf = b"".join(parts)
+    dec = feng.decode_host(buf)
+    assert_span_equal(dec, 0, buf)
+
+
+@pytest.mark.parametrize("bad", ["magic_no_object", "truncated_stream", "bad_magic"])
+def test_fused_serializable_errors(feng, bad):
+    """Invalid Serializable records after valid ones: same status / offset / tag as the
+    oracle (the fast path falls back and the robust pipeline classifies)."""
+    rng = np.random.default_rng(12)
+    good, _ = synth.config3_epoch(3000, rng)
+    tail = {"magic_no_object": b"\x03\xac\xed\x00\x05\x70" [:-1] + b"\x99",
+            "truncated_stream": D.encode(D.SerializableDeterminant(D.jser_string("abcdef")))[:-2],
+            "bad_magic": b"\x03\xac\xed\x00\x06\x74\x00\x00"}[bad]
+    buf = good.tobytes() + tail
+    st, r, eo, et = O.decode(buf)
+    assert st != 0
+    with pytest.raises(ClonosError) as ei:
+        feng.decode_host(buf)
+    assert ei.value.status == st and ei.value.err_off == eo and ei.value.err_tag == et
 
 
 @pytest.mark.parametrize("n", [100, 5000, 30000])

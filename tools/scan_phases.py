@@ -1,5 +1,5 @@
 """Developer diagnostics: per-phase cycle breakdown of the decode count kernel
-(s_memtime stamps, CLONOS_SCAN_PHASES) on the config-2 workload.  Not part of the product
+(s_memtime stamps, CLONOS_SCAN_PHASES) on the config-2 workload (argv[2] = c3: config 3).  Not part of the product
 or the tests."""
 import os
 import sys
@@ -16,8 +16,12 @@ nlogs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 rng = np.random.default_rng(synth.SEED_CONFIG2)
 with Engine(segment_bytes=16384, pool_segments=nlogs * 400, timing=True) as eng:
     logs = []
+    c3 = len(sys.argv) > 2 and sys.argv[2].startswith("c3")
+    if len(sys.argv) > 2 and sys.argv[2] == "c3n":  # config 3 without Serializable records
+        synth.CONFIG3_MIX[:] = [(n, w) for n, w in synth.CONFIG3_MIX if not n.startswith("ser_")]
     for i in range(nlogs):
-        b, _ = synth.config2_log(1_000_000, rng)
+        b = np.concatenate([synth.config3_epoch(40000, rng, e)[0] for e in range(10)]) if c3 else \
+            synth.config2_log(1_000_000, rng)[0]
         lg = eng.open_log(CausalLogID.main(i))
         lg.processUpstreamDelta(b.tobytes(), 0, 1)
         logs.append(lg)
