@@ -379,9 +379,13 @@ __device__ __forceinline__ uint64_t pack_cnt(uint32_t rec, uint32_t wide) { retu
 
 // Stage tile t into the padded row layout: the tile (16-byte loads, all in flight before
 // any LDS store), a halo of the span's next bytes, a zero pad, then every row's pad dwords.
+// kHaloMax bytes of halo (kZHalo for count / emit; phase 3 stages more so that whole
+// Serializable streams near the tile end are in LDS); kRows rows of image.
+template <uint32_t kHaloMax = kZHalo, uint32_t kRows = kZRows>
 __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
                                             const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
                                             const uint32_t hi) {
+  static_assert((kZTile + 15 + kHaloMax + 64 + 127) / 128 <= kRows, "image rows: tile + halo + zero pad");
   const uint32_t t1 = sd.first_tile + sd.n_tiles;
   {
     // every lane issues its 8 loads before any LDS store (the tile is at most 512 x 16 B)
@@ -409,22 +413,37 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
   }
   const uint64_t after = td.span_off + td.len;
   const uint64_t rem = sd.len > after ? sd.len - after : 0;
-  const uint32_t halo = rem < (uint64_t)kZHalo ? (uint32_t)rem : kZHalo;
+  const uint32_t halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
   const uint32_t img_end = hi + halo;
   __syncthreads();
   {
     uint8_t* bb = reinterpret_cast<uint8_t*>(s_img);
-    if (lane < halo) {
-      uint64_t o = after + lane;  // span offset of the halo byte
+    const TileDesc n1 = halo ? tiles[t + 1] : td;
+    if (kHaloMax > 64u && halo > 64u && n1.span_off == after && n1.len >= halo) {
+      // the next tile holds the whole halo: 16-byte loads, byte stores
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      for (uint32_t c = lane; 16u * c < n1.delta + halo; c += 64) {
+        const u32x4 v = gp(reinterpret_cast<const u32x4*>(n1.abase))[c];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b) {
+          const uint32_t x = 16u * c + b;  // byte of the next tile's aligned coordinates
+          if (x >= n1.delta && x < n1.delta + halo) bb[rb(hi + x - n1.delta)] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
+        }
+      }
+    } else {
       uint32_t k = t + 1;
-      while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
-      const TileDesc nt = tiles[k];
-      bb[rb(hi + lane)] = gp(nt.abase)[nt.delta + (uint32_t)(o - nt.span_off)];
+      for (uint32_t i = lane; i < halo; i += 64) {
+        const uint64_t o = after + i;  // span offset of the halo byte
+        while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+        const TileDesc nt = tiles[k];
+        bb[rb(hi + i)] = gp(nt.abase)[nt.delta + (uint32_t)(o - nt.span_off)];
+      }
     }
     bb[rb(img_end + lane)] = 0;  // zero pad (64 bytes) so 16-byte reads near the end are defined
   }
   __syncthreads();
-  for (uint32_t i = lane; i < (kZRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
+  for (uint32_t i = lane; i < (kRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
     const uint32_t row = i / kZPad, j = i - row * kZPad;
     s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
   }
@@ -640,17 +659,43 @@ __global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
 // contiguous run.
 // ---------------------------------------------------------------------------------
-// Record length of the Serializable record at aligned coordinate a of tile t (phase 3
-// table, sorted by position; 0 if absent or invalid -- the count pass has already
-// rejected such records).
-__device__ __forceinline__ uint32_t jtab_len(const FusedCtl& ctl, uint32_t t, uint32_t a) {
-  const CLG_GLOBAL uint32_t* pos = gp(ctl.jpos) + (uint64_t)t * kZJCap;
-  uint32_t lo = 0, hi = min(gp(ctl.jn)[t], kZJCap);
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (pos[mid] < a) lo = mid + 1; else hi = mid;
+// Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
+__device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane) {
+  uint32_t* bits = s_j;
+  uint32_t* rank = s_j + kZJBitsDw;
+  uint32_t* len = s_j + 2 * kZJBitsDw;
+  for (uint32_t i = lane; i < kZJBitsDw; i += 64) bits[i] = 0;
+  __syncthreads();
+  const uint32_t n = min(gp(ctl.jn)[t], kZJCap);
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t a = gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
+    len[i] = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    atomicOr(&bits[a >> 5], 1u << (a & 31u));
   }
-  return (lo < min(gp(ctl.jn)[t], kZJCap) && pos[lo] == a) ? gp(ctl.jlen)[(uint64_t)t * kZJCap + lo] : 0u;
+  __syncthreads();
+  // ranks: lane l takes dwords [5 l, 5 l + 5) (64 x 5 >= 260)
+  uint32_t c[5], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t i = 5 * lane + (uint32_t)k;
+    c[k] = i < kZJBitsDw ? (uint32_t)__popc(bits[i]) : 0u;
+    sum += c[k];
+  }
+  uint32_t incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += y;
+  }
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t i = 5 * lane + (uint32_t)k;
+    if (i < kZJBitsDw) rank[i] = run;
+    run += c[k];
+  }
+  __syncthreads();
+  return JL{bits, rank, len};
 }
 
 template <bool J>
@@ -658,6 +703,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
                                                     FusedCtl ctl, DecodeOut out) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint16_t s_pos[kZWin];
+  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   const TileDesc td = tiles[t];
@@ -670,6 +716,8 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint64_t cnt_t = gp(ctl.cnt)[t];
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   stage_image(td, sd, t, tiles, s_img, lane, hi);
+  JL jl{nullptr, nullptr, nullptr};
+  if (J) jl = load_jl(ctl, t, s_j, lane);
   const uint32_t r0 = lane * kZRegion;
   const uint32_t cnt = (uint32_t)(__popcll(bits.x) + __popcll(bits.y));
   uint32_t incl = cnt;
@@ -717,7 +765,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
         const ZBytes b{s_img, a};
         int tagd;
         uint32_t tgu;
-        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jtab_len(ctl, t, a) : zlen(s_img, a, end_a, &tgu);
+        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
         tagd = (int)tg;
         decode_fields(b, tagd, (int64_t)L, rr);
         v0 = rr.v0;
@@ -756,45 +804,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
 // and a chunk's first tile enters at the previous chunk's published exit, which that
 // chunk's last tile must then reproduce.  Blocks are all resident and publish first, so
 // the one wait always ends; a wait past kZSpinLimit cycles aborts the batch instead.
-// Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
-__device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane) {
-  uint32_t* bits = s_j;
-  uint32_t* rank = s_j + kZJBitsDw;
-  uint32_t* len = s_j + 2 * kZJBitsDw;
-  for (uint32_t i = lane; i < kZJBitsDw; i += 64) bits[i] = 0;
-  __syncthreads();
-  const uint32_t n = min(gp(ctl.jn)[t], kZJCap);
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint32_t a = gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
-    len[i] = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
-    atomicOr(&bits[a >> 5], 1u << (a & 31u));
-  }
-  __syncthreads();
-  // ranks: lane l takes dwords [5 l, 5 l + 5) (64 x 5 >= 260)
-  uint32_t c[5], sum = 0;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const uint32_t i = 5 * lane + (uint32_t)k;
-    c[k] = i < kZJBitsDw ? (uint32_t)__popc(bits[i]) : 0u;
-    sum += c[k];
-  }
-  uint32_t incl = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += y;
-  }
-  uint32_t run = incl - sum;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const uint32_t i = 5 * lane + (uint32_t)k;
-    if (i < kZJBitsDw) rank[i] = run;
-    run += c[k];
-  }
-  __syncthreads();
-  return JL{bits, rank, len};
-}
-
 template <bool J>
 __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
@@ -921,23 +930,50 @@ __device__ __forceinline__ bool zmagic(const uint32_t* T, uint32_t a) {
   return zb(T, a) == CLG_TAG_SERIALIZABLE && zbe32(T, a + 1) == 0xACED0005u;
 }
 
+// Record length of the candidate at a: inline for TC_STRING and flat objects, 0 = needs
+// the general walker (*general set), or an invalid stream (0, *general clear).
+__device__ __forceinline__ uint32_t jser_inline_len(const uint32_t* T, uint32_t a, uint32_t img_end, uint64_t avail,
+                                                    bool* general) {
+  const uint32_t tc = zb(T, a + 5);
+  *general = false;
+  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+    const uint64_t L = 8ull + (zb(T, a + 6) << 8 | zb(T, a + 7));
+    return L <= avail ? (uint32_t)L : 0u;
+  }
+  const uint32_t fl = tc == jser::TC_OBJECT ? jser_flat_len(T, a, img_end) : 0u;
+  if (fl) return fl <= avail ? fl : 0u;
+  *general = true;
+  return 0u;
+}
+
+constexpr int kZJReg = 4;  // candidates a lane keeps in registers (more: second scan)
+constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser_general fills it
+constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
+constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
 __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                     FusedCtl ctl) {
-  __shared__ uint32_t s_img[kZImgDw];
+  __shared__ uint32_t s_img[kZJRows * kZPitch];
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const ZTile z = ztile(tiles, spans, t, lane);
-  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+  stage_image<kZJHalo, kZJRows>(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+  const uint64_t c1 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t after = z.td.span_off + z.td.len;
   const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
-  const uint32_t img_end = z.hi + (rem < (uint64_t)kZHalo ? (uint32_t)rem : kZHalo);
+  const uint32_t img_end = z.hi + (rem < (uint64_t)kZJHalo ? (uint32_t)rem : kZJHalo);
   // candidates in the lane's region: bytes equal to 03 (zero-byte test per dword), then the magic
-  uint32_t nm = 0;
+  uint32_t nm = 0, cand[kZJReg];
   for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
     const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
     if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
     for (uint32_t i = 0; i < 4; ++i) {
       const uint32_t a = 4 * k + i;
-      nm += (a >= z.rs && a < z.re && zmagic(s_img, a)) ? 1u : 0u;
+      if (a >= z.rs && a < z.re && zmagic(s_img, a)) {
+#pragma unroll
+        for (int r = 0; r < kZJReg; ++r)
+          if ((uint32_t)r == nm) cand[r] = a;
+        ++nm;
+      }
     }
   }
   uint32_t ex = nm;
@@ -949,37 +985,63 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   const uint32_t total = __shfl(ex, 63);
   if (lane == 0) {
     gp(ctl.jn)[t] = total;
-    if (total) atomicAdd(ctl.abort + 7, total);
+    if (total) __hip_atomic_store(ctl.abort + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (total > kZJCap) raise_abort(ctl, 6, t);
   }
-  if (!nm) return;
-  uint32_t idx = ex - nm;
   const uint32_t t1 = z.sd.first_tile + z.sd.n_tiles;
-  for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
-    const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
-    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
-    for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t a = 4 * k + i;
-      if (a < z.rs || a >= z.re || !zmagic(s_img, a)) continue;
-      const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
-      uint64_t L;
-      const uint32_t fl = zb(s_img, a + 5) == jser::TC_OBJECT ? jser_flat_len(s_img, a, img_end) : 0u;
-      if (zb(s_img, a + 5) == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
-        L = 8ull + (zb(s_img, a + 6) << 8 | zb(s_img, a + 7));
-        L = L <= avail ? L : 0ull;
-      } else if (fl) {
-        L = fl <= avail ? fl : 0ull;
-      } else {
-        ZStreamBytes acc{s_img, a + 1, img_end, z.lo, z.td.span_off, tiles, t + 1, t1};
-        const int64_t sl = jser::stream_len(acc, avail - 1);
-        L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
+  uint32_t idx = ex - nm;
+  (void)t1;
+  auto emit = [&](uint32_t a) {
+    const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
+    bool general;
+    const uint64_t L = jser_inline_len(s_img, a, img_end, avail, &general);
+    if (idx < kZJCap) {
+      gp(ctl.jpos)[(uint64_t)t * kZJCap + idx] = a;
+      gp(ctl.jlen)[(uint64_t)t * kZJCap + idx] = general ? kZJGeneral : (L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u);
+      if (general) {  // nested objects, arrays, ...: k_decode_jser_general walks the grammar
+        const uint32_t w = atomicAdd(ctl.jwork, 1u);
+        if (w < ctl.jwork_cap) ctl.jwork[1 + w] = t * kZJCap + idx;
+        else raise_abort(ctl, 6, t);
       }
-      if (idx < kZJCap) {
-        gp(ctl.jpos)[(uint64_t)t * kZJCap + idx] = a;
-        gp(ctl.jlen)[(uint64_t)t * kZJCap + idx] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
-      }
-      ++idx;
     }
+    ++idx;
+  };
+  if (nm <= (uint32_t)kZJReg) {
+#pragma unroll
+    for (int r = 0; r < kZJReg; ++r)
+      if ((uint32_t)r < nm) emit(cand[r]);
+  } else {  // rare: rescan the region
+    for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
+      const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
+      if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
+      for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t a = 4 * k + i;
+        if (a >= z.rs && a < z.re && zmagic(s_img, a)) emit(a);
+      }
+    }
+  }
+  if (ctl.prof && lane == 0) {  // developer diagnostics: stage / scan+lengths cycles
+    ctl.prof[(uint64_t)t * 8 + 6] = c1 - c0;
+    ctl.prof[(uint64_t)t * 8 + 7] = __builtin_amdgcn_s_memtime() - c1;
+  }
+}
+
+// Phase 3b: the candidates the inline shapes do not cover (nested objects, arrays,
+// block data, streams longer than the staged halo), one lane each, through the grammar
+// walker (jser_device.h) reading the span from HBM.  Persistent grid over the work list.
+__global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __restrict__ tiles,
+                                                            const SpanDesc* __restrict__ spans, FusedCtl ctl) {
+  const uint32_t n = min(ld_agent32(ctl.jwork), ctl.jwork_cap);
+  for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
+    const uint32_t item = ctl.jwork[1 + i], t = item / kZJCap;
+    const TileDesc td = tiles[t];
+    const SpanDesc sd = spans[td.span];
+    const uint32_t a = ctl.jpos[item];
+    const uint64_t so = td.span_off + (a - td.delta);  // span offset of the record
+    ZStreamBytes acc{nullptr, a + 1, 0u, td.delta, td.span_off, tiles, t, sd.first_tile + sd.n_tiles};
+    const int64_t sl = jser::stream_len(acc, sd.len - so - 1);
+    const uint64_t L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
+    ctl.jlen[item] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
   }
 }
 
@@ -1017,6 +1079,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
       hipLaunchKernelGGL(k_decode_emit<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else {
     hipLaunchKernelGGL(k_decode_jser, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    hipLaunchKernelGGL(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }
   return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
 }

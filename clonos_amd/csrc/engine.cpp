@@ -186,7 +186,7 @@ struct clg_engine {
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
-  DevBuf d_zjpos, d_zjlen, d_zjn;    // fast decode: Serializable length tables (phase 3)
+  DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   PinBuf h_rmeta;
@@ -802,13 +802,16 @@ struct clg_engine {
       CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
       CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
       CHK(d_zjn.ensure(size_t(nt) * 4));
+      CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
+      HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
     }
     clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), w + 3 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
-                      jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, 0u};
+                      jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
+                      jser ? d_zjwork.as<uint32_t>() : nullptr};
     HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
     HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
     auto* zt = d_ztiles.as<clg::TileDesc>();

@@ -183,12 +183,13 @@ struct FusedCtl {
   uint32_t* jlen;
   uint32_t* jn;
   uint32_t jser;
-  uint32_t pad;
+  uint32_t jwork_cap;  // capacity of the general-walker work list
+  uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
 // 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
-// abort[7] = Serializable candidates found by phase 3 (all tiles)
+// abort[7] != 0: phase 3 found Serializable candidates (any tile)
 // phase 0: count, 1: scan, 2: emit, 3: Serializable tables
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);

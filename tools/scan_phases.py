@@ -54,3 +54,7 @@ m = p[ok][:, 5]
 m0, m1, it = m & 0xFFFFF, (m >> 20) & 0xFFFFF, (m >> 40) & 0xFF
 for name, x in (("first-merge max steps", m0), ("re-merge max steps", m1), ("fix-up passes", it)):
     print(f"  {name:22s} mean {x.mean():7.2f} p50 {np.median(x):5.0f} p90 {np.percentile(x, 90):5.0f} p99 {np.percentile(x, 99):5.0f} max {x.max()}")
+
+j6, j7 = p[:, 6], p[:, 7]
+if (j7 > 0).any():  # k_decode_jser stamps (J runs): stage / scan + lengths
+    print(f"  jser stage mean {j6[j7 > 0].mean():9.0f}   scan+len mean {j7[j7 > 0].mean():9.0f}  p99 {np.percentile(j7[j7 > 0], 99):9.0f}")
