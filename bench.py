@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-config3", action="store_true", help="skip the secondary config-3 decode measurement")
     return ap.parse_args()
 
 
@@ -178,6 +179,13 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(bufs, log_bytes, cons, args)
+    # ---------------- secondary: config 3 decode (rank 0, N=1 only) ----------------
+    c3 = None
+    if rank == 0 and world == 1 and not args.no_config3:
+        eng.close()
+        del o_off, o_tag, o_v0, o_w, o_slice
+        torch.cuda.empty_cache()
+        c3 = config3(args, torch, dev)
 
     if rank == 0:
         line = {
@@ -206,11 +214,84 @@ def main():
             "kernels": kern,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "config3": c3,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5):
+    """BASELINE.json configs[2]: mixed variable-length determinants (Order, BufferBuilt,
+    TimerTrigger "PTS"/"87", Timestamp, RNG, Serializable String/Boolean/Integer,
+    SourceCheckpoint, IgnoreCheckpoint), 256 subtask logs x 10 epochs (~0.9 GB) resident in
+    HBM; one step = batched decode of every log from its first epoch.  Reported next to the
+    headline line (decode only; no consumers are defined for this config)."""
+    import time as _t
+    from clonos_amd import CausalLogID, Engine, _lib, synth
+    rng = np.random.default_rng(synth.SEED_CONFIG3)
+    epochs = [synth.config3_epoch(per_epoch, rng, e)[0] for e in range(n_epochs)]
+    per_log = sum(int(e.size) for e in epochs)
+    seg = 16384
+    eng = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
+                 timing=True)
+    logs = []
+    for v in range(n_logs):  # every log: the epoch sequence rotated, so layouts differ per log
+        log = eng.open_log(CausalLogID.main(v))
+        for e in range(n_epochs):
+            log.processUpstreamDelta(epochs[(e + v) % n_epochs].tobytes(), 0, e)
+        logs.append(log)
+    eng.sync()
+    total = per_log * n_logs
+    n_det = n_logs * per_epoch * n_epochs
+    o = [torch.empty(n_det, dtype=torch.int32, device=dev), torch.empty(n_det, dtype=torch.uint8, device=dev),
+         torch.empty(n_det, dtype=torch.int64, device=dev)]
+    wcap = n_det // 2 + 16
+    ow = [torch.empty(wcap, dtype=t, device=dev) for t in
+          (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
+    dec = _lib.Decoded()
+    dec.off, dec.tag, dec.v0 = [t.data_ptr() for t in o]
+    dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len, dec.w_sub = [t.data_ptr() for t in ow]
+    dec.cap, dec.wcap, dec.out_kind = n_det, wcap, _lib.CLG_MEM_DEVICE
+    handles = np.array([l.handle for l in logs], np.uint32)
+    starts = np.zeros(n_logs, np.int64)
+    base = np.zeros(n_logs + 1, np.uint64)
+    for _ in range(2):  # warm-up (the first batch also learns that the logs hold Serializable records)
+        eng.decode_logs_device(handles, starts, dec, base)
+    assert dec.n_rec == n_det and dec.err_status == 0
+    torch.cuda.synchronize()
+    eng.kernel_stats_reset()
+    t0 = _t.perf_counter()
+    for _ in range(steps):
+        eng.decode_logs_device(handles, starts, dec, base)
+    torch.cuda.synchronize()
+    el = (_t.perf_counter() - t0) / steps
+    st = eng.kernel_stats()
+    n_wide = int(dec.n_wide)
+    eng.close()
+    algo = total + 13 * n_det + 25 * n_wide
+    kern = {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5))
+            for k, v in st.items() if v["launches"]}
+    out = {"workload": f"config3: {n_logs} subtask logs x {n_epochs} epochs x {per_epoch} mixed determinants "
+                       "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
+           "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
+           "log_gbs": round(total / el / 1e9, 2), "algo_gbs": round(algo / el / 1e9, 1),
+           "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern}
+    if not args.no_cpu_baseline:  # the C++ oracle's decodeNext loop on host cores, whole workload once
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O  # the checker, timed here as the CPU baseline
+        host = np.concatenate([epochs[(e + v) % n_epochs] for v in range(n_logs) for e in range(n_epochs)])
+        lens = np.full(n_logs, per_log, np.uint64)
+        offs = np.arange(n_logs, dtype=np.uint64) * np.uint64(per_log)
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t0 = _t.perf_counter()
+        n1 = O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs), O.ptr(lens), n_logs, threads)
+        dt = _t.perf_counter() - t0
+        assert n1 == n_det, (n1, n_det)
+        out["cpu_baseline"] = {"value": round(n_det / dt, 1), "unit": "determinants/s", "cores": threads,
+                               "kind": "port", "sample": f"whole config-3 decode once ({total} B) in {dt:.2f}s"}
+    return out
 
 
 def cpu_baseline(bufs, log_bytes, cons, args):
