@@ -950,10 +950,9 @@ constexpr int kZJReg = 4;  // candidates a lane keeps in registers (more: second
 constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser_general fills it
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
-__global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                    FusedCtl ctl) {
-  __shared__ uint32_t s_img[kZJRows * kZPitch];
-  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+__device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                          const FusedCtl& ctl, uint32_t* s_img, const uint32_t t, const uint32_t lane,
+                                          bool* flagged) {
   const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const ZTile z = ztile(tiles, spans, t, lane);
   stage_image<kZJHalo, kZJRows>(z.td, z.sd, t, tiles, s_img, lane, z.hi);
@@ -961,14 +960,26 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   const uint64_t after = z.td.span_off + z.td.len;
   const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
   const uint32_t img_end = z.hi + (rem < (uint64_t)kZJHalo ? (uint32_t)rem : kZJHalo);
-  // candidates in the lane's region: bytes equal to 03 (zero-byte test per dword), then the magic
+  // candidates in the lane's region (row `lane` of the image, dwords 35 lane + j; j = 32..34
+  // are the row's pad = the next row's head): all 35 dwords loaded up front (independent
+  // LDS reads, no dependent round trips), then "03 AC ED 00 05" tested in registers where a
+  // dword pair holds an ED byte (rare outside the magic)
+  uint32_t D[kZRowDw + kZPad];
+#pragma unroll
+  for (uint32_t j = 0; j < kZRowDw + kZPad; ++j) D[j] = s_img[lane * kZPitch + j];
   uint32_t nm = 0, cand[kZJReg];
-  for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
-    const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
-    if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
-    for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t a = 4 * k + i;
-      if (a >= z.rs && a < z.re && zmagic(s_img, a)) {
+  const uint32_t r0 = lane * kZRegion;
+#pragma unroll
+  for (uint32_t j = 0; j < kZRowDw; ++j) {
+    const uint32_t x = D[j], y = D[j + 1], z2 = D[j + 2];
+    const uint32_t ex_ = x ^ 0xEDEDEDEDu, ey = y ^ 0xEDEDEDEDu;
+    if (!(((ex_ - 0x01010101u) & ~ex_ & 0x80808080u) | ((ey - 0x01010101u) & ~ey & 0x80808080u))) continue;
+#pragma unroll
+    for (uint32_t sh = 0; sh < 4; ++sh) {
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(y, x, sh);     // bytes a .. a+3 (LE)
+      const uint32_t w1 = __builtin_amdgcn_alignbyte(z2, y, sh);    // bytes a+4 .. a+7
+      const uint32_t a = r0 + 4u * j + sh;
+      if (w0 == 0x00EDAC03u && (w1 & 0xFFu) == 0x05u && a >= z.rs && a < z.re) {
 #pragma unroll
         for (int r = 0; r < kZJReg; ++r)
           if ((uint32_t)r == nm) cand[r] = a;
@@ -976,6 +987,7 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
       }
     }
   }
+  const uint64_t c2 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   uint32_t ex = nm;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -985,9 +997,10 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   const uint32_t total = __shfl(ex, 63);
   if (lane == 0) {
     gp(ctl.jn)[t] = total;
-    if (total) __hip_atomic_store(ctl.abort + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (total && !*flagged) __hip_atomic_store(ctl.abort + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (total > kZJCap) raise_abort(ctl, 6, t);
   }
+  *flagged = *flagged || total;  // one flag store per block
   const uint32_t t1 = z.sd.first_tile + z.sd.n_tiles;
   uint32_t idx = ex - nm;
   (void)t1;
@@ -1006,7 +1019,8 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
     }
     ++idx;
   };
-  if (nm <= (uint32_t)kZJReg) {
+  if (!nm) {
+  } else if (nm <= (uint32_t)kZJReg) {
 #pragma unroll
     for (int r = 0; r < kZJReg; ++r)
       if ((uint32_t)r < nm) emit(cand[r]);
@@ -1022,7 +1036,18 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   }
   if (ctl.prof && lane == 0) {  // developer diagnostics: stage / scan+lengths cycles
     ctl.prof[(uint64_t)t * 8 + 6] = c1 - c0;
-    ctl.prof[(uint64_t)t * 8 + 7] = __builtin_amdgcn_s_memtime() - c1;
+    ctl.prof[(uint64_t)t * 8 + 7] = (c2 - c1) | (__builtin_amdgcn_s_memtime() - c2) << 32;
+  }
+}
+
+// Persistent grid: block b takes tiles b, b + G, ...
+__global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                    FusedCtl ctl) {
+  __shared__ uint32_t s_img[kZJRows * kZPitch];
+  bool flagged = false;
+  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
+    jser_tile(tiles, spans, ctl, s_img, t, threadIdx.x, &flagged);
+    __syncthreads();  // the image is reused by the next tile
   }
 }
 
@@ -1078,7 +1103,17 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     else
       hipLaunchKernelGGL(k_decode_emit<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else {
-    hipLaunchKernelGGL(k_decode_jser, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    static int jres = 0;  // blocks the device keeps resident for the table kernel
+    if (!jres) {
+      int dev = 0, per_cu = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_jser, 64, 0) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+        return CLG_E_DEVICE;
+      jres = per_cu * cus;
+    }
+    hipLaunchKernelGGL(k_decode_jser, dim3(n_tiles < (uint32_t)jres ? n_tiles : (uint32_t)jres), dim3(64), 0, st,
+                       d_tiles, d_spans, ctl);
     hipLaunchKernelGGL(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }
   return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;

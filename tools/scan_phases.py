@@ -57,4 +57,5 @@ for name, x in (("first-merge max steps", m0), ("re-merge max steps", m1), ("fix
 
 j6, j7 = p[:, 6], p[:, 7]
 if (j7 > 0).any():  # k_decode_jser stamps (J runs): stage / scan + lengths
-    print(f"  jser stage mean {j6[j7 > 0].mean():9.0f}   scan+len mean {j7[j7 > 0].mean():9.0f}  p99 {np.percentile(j7[j7 > 0], 99):9.0f}")
+    sc, ln = j7[j7 > 0] & 0xFFFFFFFF, j7[j7 > 0] >> 32
+    print(f"  jser stage mean {j6[j7 > 0].mean():9.0f}   scan mean {sc.mean():9.0f}   lengths+stores mean {ln.mean():9.0f} p99 {np.percentile(ln, 99):9.0f}")
