@@ -161,3 +161,53 @@ def random_determinant(rng: np.random.Generator, allow_serializable: bool = True
 
 def random_log(n: int, rng: np.random.Generator, allow_serializable: bool = True) -> bytes:
     return b"".join(D.encode(random_determinant(rng, allow_serializable)) for _ in range(n))
+
+
+SEED_CONFIG1 = 0xC105
+
+
+def config1_job(rng: np.random.Generator, parallelism: int = 4, epoch_ms: int = 1000, checkpoints: int = 1):
+    """Config 1 (BASELINE.json configs[0]): WordCount + causal TimeService with a
+    processing-time window, parallelism 4, one epoch, modelled from the reference's producer
+    call sites (a JVM MiniCluster capture cannot run here):
+      every task's main log starts the epoch with Timestamp then RNG
+        (subscription order StreamTask.java:305-313, EpochTrackerImpl.java:99-100);
+      "PTS" TimerTrigger (21 B) every 5 ms of processing time (StreamTask.java:1519);
+      source main logs: SourceCheckpoint (27 B) per checkpoint;
+      window main logs: Order (2 B) per input buffer over 4 channels, window TimerTrigger
+        "87" (20 B) per firing (WindowOperator.java:203);
+      sink main logs: Order per input buffer;
+      every subpartition log: BufferBuilt (5 B) per output buffer (PipelinedSubpartition).
+    Returns (graph, {CausalLogID: bytes}) for stages source -> window -> sink."""
+    from . import job
+    from .engine import CausalLogID
+    g = job.JobGraph([job.JobVertex("source", parallelism), job.JobVertex("window", parallelism, ["source"]),
+                      job.JobVertex("sink", parallelism, ["window"])])
+    logs = {}
+    rc = 0
+    for name in ("source", "window", "sink"):
+        for i, vid in enumerate(g.vertex_ids(name)):
+            recs = [D.TimestampDeterminant(1_700_000_000_000 + int(rng.integers(0, 1000))),
+                    D.RNGDeterminant(int(rng.integers(-2**31, 2**31)))]
+            t, n_in = 0, 0
+            while t < epoch_ms:
+                step = int(rng.integers(1, 6))
+                t += step
+                if name != "source":
+                    for _ in range(int(rng.integers(0, 4))):
+                        recs.append(D.OrderDeterminant(int(rng.integers(0, parallelism))))
+                        n_in += 1
+                if t % 5 < step:
+                    recs.append(D.TimerTriggerDeterminant(n_in, 1_700_000_000_000 + t, D.INTERNAL, b"PTS"))
+                if name == "window" and t % 100 < step:
+                    recs.append(D.TimerTriggerDeterminant(n_in, 1_700_000_000_000 + t, D.INTERNAL, b"87"))
+                if name == "source" and checkpoints and t % (epoch_ms // checkpoints) < step:
+                    rc += 1
+                    recs.append(D.SourceCheckpointDeterminant(rc, rc, 1_700_000_000_000 + t, D.CHECKPOINT, b""))
+            logs[CausalLogID.main(vid)] = b"".join(D.encode(r) for r in recs)
+            if name != "sink":
+                for j in range(parallelism):  # one subpartition per downstream subtask
+                    n = int(rng.integers(5, 200))
+                    logs[CausalLogID.sub(vid, 0x5EED0000 + vid, 1, j)] = b"".join(
+                        D.encode(D.BufferBuiltDeterminant(int(x))) for x in rng.integers(1, 32768, n))
+    return g, logs
