@@ -47,7 +47,7 @@ EXPORTED = [
     "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
-    "clg_replay_prepare",
+    "clg_replay_prepare", "clg_encode_batch",
 ]
 
 
@@ -179,6 +179,15 @@ class ReplayOut(C.Structure):
     ]
 
 
+class EncodeIn(C.Structure):
+    _fields_ = [
+        ("tag", C.c_void_p), ("v0", C.c_void_p), ("n", C.c_uint64),
+        ("w_idx", C.c_void_p), ("w_rc", C.c_void_p), ("w_v1", C.c_void_p), ("w_var_off", C.c_void_p),
+        ("w_var_len", C.c_void_p), ("w_sub", C.c_void_p), ("n_wide", C.c_uint64),
+        ("var", C.c_void_p), ("var_len", C.c_uint64), ("in_kind", C.c_uint32), ("reserved", C.c_uint32),
+    ]
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double), ("bytes", C.c_uint64)]
 
@@ -233,6 +242,7 @@ def _load() -> C.CDLL:
         "clg_response_merge": (C.c_int, [C.POINTER(Response), C.POINTER(Response)]),
         "clg_causal_log_id_hash": (C.c_int32, [C.POINTER(CausalLogIdC)]),
         "clg_replay_prepare": (C.c_int, [P, C.POINTER(ReplayVertex), C.c_uint32, C.POINTER(ReplayOut)]),
+        "clg_encode_batch": (C.c_int, [P, C.POINTER(EncodeIn), P, C.c_uint64, C.c_uint32, u64p, u64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libclonos_engine.so")
 SOURCES = [os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "kernels.hip"), os.path.join(CSRC, "decode_fast.hip"),
-           os.path.join(CSRC, "decode_fused.hip"), os.path.join(CSRC, "replay.hip"),
+           os.path.join(CSRC, "decode_fused.hip"), os.path.join(CSRC, "replay.hip"), os.path.join(CSRC, "encode.hip"),
            os.path.join(CSRC, "response.cpp")]
 HEADERS = [
     os.path.join(CSRC, "kernels.h"),

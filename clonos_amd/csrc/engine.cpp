@@ -189,6 +189,7 @@ struct clg_engine {
   DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
+  DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
@@ -1539,6 +1540,74 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
     for (uint32_t i = 0; i < n; ++i) e->plan_host_span(p, dst + at[i], mains[i].len, i, T);
   };
   CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
+  return e->sync();
+}
+
+// SimpleDeterminantEncoder.encodeTo over a batch (encode.hip): sizes pass, one host read
+// of the total, write pass.
+int clg_encode_batch(clg_engine* e, const clg_encode_in* in, void* out, uint64_t cap, uint32_t out_kind,
+                     uint64_t* n_out, uint64_t* bad_index) {
+  ENGINE_GUARD(e);
+  if (!in || !n_out || (in->n && (!in->tag || !in->v0)) ||
+      (in->n_wide && (!in->w_idx || !in->w_rc || !in->w_v1 || !in->w_var_off || !in->w_var_len || !in->w_sub)) ||
+      (in->var_len && !in->var))
+    return fail(CLG_E_INVALID_ARG, "null argument");
+  *n_out = 0;
+  if (bad_index) *bad_index = UINT64_MAX;
+  if (in->n == 0) return CLG_OK;
+  const uint64_t n = in->n, nw = in->n_wide;
+  clg::EncodeIn d{in->tag, in->v0, in->w_idx, in->w_rc, in->w_v1, in->w_var_off, in->w_var_len, in->w_sub, in->var, n, nw};
+  if (in->in_kind != CLG_MEM_DEVICE) {  // stage the host arrays in one device buffer
+    const size_t sz[9] = {n, 8 * n, 4 * nw, 4 * nw, 8 * nw, 4 * nw, 4 * nw, nw, size_t(in->var_len)};
+    const void* src[9] = {in->tag, in->v0, in->w_idx, in->w_rc, in->w_v1, in->w_var_off, in->w_var_len, in->w_sub, in->var};
+    size_t off[9], tot = 0;
+    for (int i = 0; i < 9; ++i) {
+      off[i] = tot;
+      tot += (sz[i] + 15) & ~size_t(15);
+    }
+    CHK(e->d_encin.ensure(tot + 16));
+    uint8_t* b = e->d_encin.as<uint8_t>();
+    for (int i = 0; i < 9; ++i)
+      if (sz[i]) HIPCHK(hipMemcpyAsync(b + off[i], src[i], sz[i], hipMemcpyHostToDevice, e->stream));
+    d = clg::EncodeIn{b + off[0], reinterpret_cast<const int64_t*>(b + off[1]), reinterpret_cast<const uint32_t*>(b + off[2]),
+                      reinterpret_cast<const int32_t*>(b + off[3]), reinterpret_cast<const int64_t*>(b + off[4]),
+                      reinterpret_cast<const uint32_t*>(b + off[5]), reinterpret_cast<const uint32_t*>(b + off[6]),
+                      b + off[7], b + off[8], n, nw};
+  }
+  const uint64_t nb = (n + 1023) / 1024;
+  const size_t o_wsum = 0, o_wbase = (nb * 4 + 15) & ~size_t(15), o_bsum = o_wbase + (((nb + 1) * 8 + 15) & ~size_t(15)),
+               o_bbase = o_bsum + ((nb * 8 + 15) & ~size_t(15)), o_bad = o_bbase + (((nb + 1) * 8 + 15) & ~size_t(15));
+  CHK(e->d_encw.ensure(o_bad + 16));
+  uint8_t* w = e->d_encw.as<uint8_t>();
+  auto* wsum = reinterpret_cast<uint32_t*>(w + o_wsum);
+  auto* wbase = reinterpret_cast<uint64_t*>(w + o_wbase);
+  auto* bsum = reinterpret_cast<uint64_t*>(w + o_bsum);
+  auto* bbase = reinterpret_cast<uint64_t*>(w + o_bbase);
+  auto* bad = reinterpret_cast<uint32_t*>(w + o_bad);
+  HIPCHK(hipMemsetAsync(bad, 0xFF, 4, e->stream));
+  CHK(clg::launch_encode(d, wsum, wbase, bsum, bbase, bad, nullptr, 0, e->stream));
+  uint64_t hres[2] = {0, 0};  // total bytes, wide rows used
+  uint32_t hbad = 0;
+  HIPCHK(hipMemcpyAsync(&hres[0], bbase + nb, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&hres[1], wbase + nb, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, e->stream));
+  CHK(e->sync());
+  if (hbad != 0xFFFFFFFFu || hres[1] != nw) {
+    if (bad_index) *bad_index = hbad != 0xFFFFFFFFu ? hbad : n;
+    return fail(CLG_E_INVALID_ARG, "record %llu: invalid tag or side-table row (%llu wide rows given, %llu used)",
+                (unsigned long long)(hbad != 0xFFFFFFFFu ? hbad : n), (unsigned long long)nw,
+                (unsigned long long)hres[1]);
+  }
+  *n_out = hres[0];
+  if (hres[0] > cap || !out) return fail(CLG_E_CAPACITY, "encode needs %llu bytes", (unsigned long long)hres[0]);
+  uint8_t* dst = static_cast<uint8_t*>(out);
+  if (out_kind != CLG_MEM_DEVICE) {
+    CHK(e->d_encout.ensure(hres[0] + 16));
+    dst = e->d_encout.as<uint8_t>();
+  }
+  CHK(e->timed("encode_write", hres[0] + 9 * n + 25 * nw + in->var_len,
+               [&] { return clg::launch_encode(d, wsum, wbase, bsum, bbase, bad, dst, 1, e->stream); }));
+  if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dst, hres[0], hipMemcpyDeviceToHost, e->stream));
   return e->sync();
 }
 

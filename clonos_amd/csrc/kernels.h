@@ -246,6 +246,24 @@ int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc
                        const uint32_t* d_span_flags, DecodeOut out, void* stream);
 
 
+// ---- batched encode (encode.hip) -------------------------------------------------
+struct EncodeIn {  // device pointers, the decode's SoA layout (clg_decoded)
+  const uint8_t* tag;
+  const int64_t* v0;
+  const uint32_t* w_idx;
+  const int32_t* w_rc;
+  const int64_t* w_v1;
+  const uint32_t* w_var_off;  // into var
+  const uint32_t* w_var_len;
+  const uint8_t* w_sub;
+  const uint8_t* var;
+  uint64_t n, n_wide;
+};
+// phase 0: wide prefix per block (wsum -> wbase, nb + 1), bytes per block (bsum -> bbase,
+// nb + 1), *bad = lowest invalid record; phase 1: write.  nb = ceil(n / 1024).
+int launch_encode(const EncodeIn& in, uint32_t* d_wsum, uint64_t* d_wbase, uint64_t* d_bsum, uint64_t* d_bbase,
+                  uint32_t* d_bad, uint8_t* d_out, uint32_t phase, void* stream);
+
 // ---- replay preparation: subpartition recovery buffers ----------------------------
 // A recovery buffer may hold BufferBuilt determinants only (ReplayingState.java:172-177),
 // which are 5 bytes each, so record k of a well-formed buffer starts at 5k: no chain walk.

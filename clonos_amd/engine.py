@@ -308,6 +308,36 @@ class Engine:
         check(lib.clg_decode_logs(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles), C.byref(dec),
                                   _np_ptr(base)))
 
+    # ---- encode -----------------------------------------------------------------------------
+    def encode_batch(self, tag, v0, w_idx=None, w_rc=None, w_v1=None, w_var_off=None, w_var_len=None, w_sub=None,
+                     var: bytes = b"") -> bytes:
+        """SimpleDeterminantEncoder.encodeTo over a batch, on the GPU: records in the decode's
+        SoA layout (the side-table arrays for wide records; w_var_off indexes `var`)."""
+        tag = np.ascontiguousarray(tag, np.uint8)
+        v0 = np.ascontiguousarray(v0, np.int64)
+        nw = 0 if w_idx is None else len(w_idx)
+        arr = lambda a, t: np.ascontiguousarray(a if a is not None else np.zeros(0), t)  # noqa: E731
+        side = [arr(w_idx, np.uint32), arr(w_rc, np.int32), arr(w_v1, np.int64), arr(w_var_off, np.uint32),
+                arr(w_var_len, np.uint32), arr(w_sub, np.uint8)]
+        vb = np.frombuffer(bytes(var), np.uint8) if len(var) else np.zeros(1, np.uint8)
+        ein = _lib.EncodeIn(_np_ptr(tag), _np_ptr(v0), len(tag), *[_np_ptr(a) for a in side[:6]], nw,
+                            _np_ptr(vb), len(var), _lib.CLG_MEM_HOST, 0)
+        n_out, bad = C.c_uint64(), C.c_uint64()
+        st = lib.clg_encode_batch(self._h, C.byref(ein), None, 0, _lib.CLG_MEM_HOST, C.byref(n_out), C.byref(bad))
+        if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+            err = _lib.ClonosError(st, lib.clg_last_error().decode(errors="replace"))
+            err.bad_index = bad.value
+            raise err
+        out = np.empty(max(1, n_out.value), np.uint8)
+        check(lib.clg_encode_batch(self._h, C.byref(ein), _np_ptr(out), out.size, _lib.CLG_MEM_HOST, C.byref(n_out),
+                                   C.byref(bad)))
+        return out[:n_out.value].tobytes()
+
+    def encode_decoded(self, dec: "DecodedBatch", span_bytes: bytes) -> bytes:
+        """Round trip: re-encode a decoded span (its var fields index the span bytes)."""
+        return self.encode_batch(dec.tag, dec.v0, dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len,
+                                 dec.w_sub, span_bytes)
+
     # ---- replay-prep ----------------------------------------------------------------------
     def replay_prep(self, copies: Sequence[Tuple[int, bytes]]):
         """DeterminantResponseEvent.merge (longest wins, ties -> later) + batched decode of

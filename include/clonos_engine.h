@@ -246,6 +246,34 @@ int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, co
                     const uint64_t* len, uint32_t n, uint32_t* winner, uint32_t* n_keys,
                     clg_decoded* out, uint64_t* span_rec_base);
 
+/* ---- batched encode (SimpleDeterminantEncoder.encodeTo :56-75, writers :124-323) ---------
+ * The inverse of the decode: records given in the decode's SoA layout (tag, v0; a
+ * side-table row per wide record, rows in record order and w_idx naming the record;
+ * w_var_off indexes `var`, the payload bytes: TimerTrigger names, storage references,
+ * Serializable streams) are written back to back in record order -- exactly the bytes
+ * the reference's appendDeterminant sequence would produce.  *n_out = bytes (also on
+ * CLG_E_CAPACITY).  A record with tag > 7 or a side row naming another record:
+ * CLG_E_INVALID_ARG with the record index in *bad_index. */
+typedef struct clg_encode_in {
+  const uint8_t* tag;
+  const int64_t* v0;
+  uint64_t n;
+  const uint32_t* w_idx;
+  const int32_t* w_rc;
+  const int64_t* w_v1;
+  const uint32_t* w_var_off;
+  const uint32_t* w_var_len;
+  const uint8_t* w_sub;
+  uint64_t n_wide;
+  const uint8_t* var;
+  uint64_t var_len;
+  uint32_t in_kind; /* CLG_MEM_HOST / CLG_MEM_DEVICE (all input arrays) */
+  uint32_t reserved;
+} clg_encode_in;
+
+int clg_encode_batch(clg_engine* e, const clg_encode_in* in, void* out, uint64_t cap, uint32_t out_kind,
+                     uint64_t* n_out, uint64_t* bad_index);
+
 /* ---- DeterminantResponseEvent (DeterminantResponseEvent.java:36-148) ---------------------
  * The event's map CausalLogID -> log bytes is held as an entry array in the iteration
  * order of the reference's java.util.HashMap (JDK 8: 2^k buckets from 16, load factor
