@@ -47,7 +47,7 @@ EXPORTED = [
     "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
-    "clg_replay_prepare", "clg_encode_batch",
+    "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
 ]
 
 
@@ -188,6 +188,18 @@ class EncodeIn(C.Structure):
     ]
 
 
+class EnrichReq(C.Structure):
+    _fields_ = [
+        ("consumer", ChannelId), ("epoch", C.c_int64), ("first", C.c_uint32), ("count", C.c_uint32),
+        ("status", C.c_int32), ("header_bytes", C.c_uint32), ("out_off", C.c_uint64), ("out_len", C.c_uint64),
+    ]
+
+
+CLG_DELTA_FLAT = 0
+CLG_DELTA_HIERARCHICAL = 1
+CLG_DE_SEND = 1
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double), ("bytes", C.c_uint64)]
 
@@ -243,6 +255,9 @@ def _load() -> C.CDLL:
         "clg_causal_log_id_hash": (C.c_int32, [C.POINTER(CausalLogIdC)]),
         "clg_replay_prepare": (C.c_int, [P, C.POINTER(ReplayVertex), C.c_uint32, C.POINTER(ReplayOut)]),
         "clg_encode_batch": (C.c_int, [P, C.POINTER(EncodeIn), P, C.c_uint64, C.c_uint32, u64p, u64p]),
+        "clg_enrich_batch": (C.c_int, [P, C.c_uint32, C.POINTER(EnrichReq), C.c_uint32, P, P, P, C.c_uint64,
+                                       C.c_uint32, u64p]),
+        "clg_process_delta": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.c_uint32, i64p, P, C.c_uint32, u32p, u64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -190,6 +190,7 @@ struct clg_engine {
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
+  DevBuf d_hdr;                      // piggyback: delta headers staged for the gather
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
@@ -1609,6 +1610,269 @@ int clg_encode_batch(clg_engine* e, const clg_encode_in* in, void* out, uint64_t
                [&] { return clg::launch_encode(d, wsum, wbase, bsum, bbase, bad, dst, 1, e->stream); }));
   if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dst, hres[0], hipMemcpyDeviceToHost, e->stream));
   return e->sync();
+}
+
+namespace {
+void wr16(std::vector<uint8_t>& b, uint16_t v) { b.push_back(uint8_t(v >> 8)); b.push_back(uint8_t(v)); }
+void wr32(std::vector<uint8_t>& b, uint32_t v) { wr16(b, uint16_t(v >> 16)); wr16(b, uint16_t(v)); }
+void wr64(std::vector<uint8_t>& b, uint64_t v) { wr32(b, uint32_t(v >> 32)); wr32(b, uint32_t(v)); }
+uint32_t rd32(const uint8_t* p) { return uint32_t(p[0]) << 24 | uint32_t(p[1]) << 16 | uint32_t(p[2]) << 8 | p[3]; }
+uint64_t rd64(const uint8_t* p) { return uint64_t(rd32(p)) << 32 | rd32(p + 4); }
+}  // namespace
+
+// enrichWithCausalLogDelta (AbstractDeltaSerializerDeserializer.java:89-115) for a batch of
+// channels: host metadata (hasDelta / offset / take) and header bytes, then one gather
+// kernel writes headers and deltas into the output.
+int clg_enrich_batch(clg_engine* e, uint32_t strategy, clg_enrich_req* reqs, uint32_t n, const uint32_t* log,
+                     const uint8_t* flags, void* out, uint64_t cap, uint32_t out_kind, uint64_t* total) {
+  ENGINE_GUARD(e);
+  if ((n && (!reqs || !log)) || !total || strategy > CLG_DELTA_HIERARCHICAL)
+    return fail(CLG_E_INVALID_ARG, "null argument or unknown strategy");
+  CHK(e->flush());
+  struct Adv {
+    uint32_t log;
+    ChKey k;
+    int32_t nb;
+  };
+  struct Sent {
+    uint32_t log;
+    int32_t phys, nb;
+    uint64_t dst;
+  };
+  std::vector<Adv> advs;
+  std::vector<Sent> sent;
+  std::vector<uint8_t> hdr;          // all headers back to back
+  std::vector<uint64_t> hdr_at(n);   // request -> its header offset in hdr
+  uint64_t dst = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    clg_enrich_req& r = reqs[i];
+    r.status = CLG_OK;
+    r.out_off = dst;
+    const ChKey k{r.consumer.lo, r.consumer.hi};
+    const size_t h0 = hdr.size();
+    hdr_at[i] = h0;
+    wr32(hdr, 0);  // header size, patched below (:98, :103)
+    wr64(hdr, uint64_t(r.epoch));
+    uint64_t dlen = 0;
+    auto one = [&](uint32_t j, bool* has_out, int32_t* ofe, int32_t* nb) -> int {  // hasDelta, then take if sent
+      int32_t has = 0;
+      *has_out = false;
+      CHK(e->has_delta(log[j], k, r.epoch, &has));
+      if (!has || !(flags ? (flags[j] & CLG_DE_SEND) : 1)) return CLG_OK;
+      CHK(e->offset_from_epoch(log[j], k, ofe));
+      int32_t phys;
+      CHK(e->take_delta(log[j], k, r.epoch, &phys, nb));
+      advs.push_back(Adv{log[j], k, *nb});
+      sent.push_back(Sent{log[j], phys, *nb, dlen});  // dst relative to the request's deltas, fixed below
+      dlen += uint64_t(*nb);
+      *has_out = true;
+      return CLG_OK;
+    };
+    const size_t sent0 = sent.size();
+    int st = CLG_OK;
+    if (strategy == CLG_DELTA_FLAT) {  // [CausalLogID][offsetFromEpoch i32][len i32] per sent log (:80-84, :91-99)
+      for (uint32_t j = r.first; j < r.first + r.count && st == CLG_OK; ++j) {
+        bool has;
+        int32_t ofe = 0, nb = 0;
+        st = one(j, &has, &ofe, &nb);
+        if (st != CLG_OK || !has) continue;
+        const clg_causal_log_id& id = e->logs[log[j]].id;
+        wr16(hdr, uint16_t(id.vertex_id));
+        hdr.push_back(id.is_main ? 1 : 0);
+        if (!id.is_main) {
+          wr64(hdr, uint64_t(id.irp_lower));
+          wr64(hdr, uint64_t(id.irp_upper));
+          hdr.push_back(uint8_t(id.subpartition));
+        }
+        wr32(hdr, uint32_t(ofe));
+        wr32(hdr, uint32_t(nb));
+      }
+    } else {  // Grouping: per vertex [vertex i16][hasMain]{main}[numPartitions u8]{[lo][hi][numSub u8]{[sub][ofe][len]}}
+      uint32_t j = r.first;
+      const uint32_t end = r.first + r.count;
+      while (j < end && st == CLG_OK) {
+        const int16_t v = e->logs[log[j]].id.vertex_id;
+        const size_t vstart = hdr.size();
+        int updates = 0;
+        wr16(hdr, uint16_t(v));  // :113-115
+        bool has = false;
+        int32_t ofe = 0, nb = 0;
+        if (e->logs[log[j]].id.is_main) {  // :116-121
+          st = one(j, &has, &ofe, &nb);
+          ++j;
+        }
+        if (st != CLG_OK) break;
+        hdr.push_back(has ? 1 : 0);
+        if (has) {
+          wr32(hdr, uint32_t(ofe));
+          wr32(hdr, uint32_t(nb));
+          ++updates;
+        }
+        const size_t np_at = hdr.size();
+        hdr.push_back(0);  // numPartitionDeltas (:134-141)
+        int parts = 0;
+        while (j < end && st == CLG_OK && e->logs[log[j]].id.vertex_id == v && !e->logs[log[j]].id.is_main) {
+          const int64_t lo = e->logs[log[j]].id.irp_lower, hi = e->logs[log[j]].id.irp_upper;
+          const size_t pstart = hdr.size();
+          wr64(hdr, uint64_t(lo));  // :146-148
+          wr64(hdr, uint64_t(hi));
+          const size_t ns_at = hdr.size();
+          hdr.push_back(0);
+          int subs = 0;
+          while (j < end && e->logs[log[j]].id.vertex_id == v && !e->logs[log[j]].id.is_main &&
+                 e->logs[log[j]].id.irp_lower == lo && e->logs[log[j]].id.irp_upper == hi) {
+            bool hs;
+            int32_t o2 = 0, n2 = 0;
+            st = one(j, &hs, &o2, &n2);
+            if (st != CLG_OK) break;
+            if (hs) {  // :150-154
+              hdr.push_back(uint8_t(e->logs[log[j]].id.subpartition));
+              wr32(hdr, uint32_t(o2));
+              wr32(hdr, uint32_t(n2));
+              ++subs;
+            }
+            ++j;
+          }
+          if (subs == 0) {
+            hdr.resize(pstart);  // :156-158
+          } else {
+            hdr[ns_at] = uint8_t(subs);
+            ++parts;
+          }
+        }
+        hdr[np_at] = uint8_t(parts);
+        updates += parts;
+        if (updates == 0) hdr.resize(vstart);  // :125-126
+        if (j < end && st == CLG_OK && e->logs[log[j]].id.vertex_id != v) continue;
+        if (j < end && st == CLG_OK && e->logs[log[j]].id.vertex_id == v && e->logs[log[j]].id.is_main) {
+          st = fail(CLG_E_INVALID_ARG, "hierarchical entries: vertex %d repeats", int(v));
+        }
+      }
+    }
+    if (st != CLG_OK) {  // undo this request's takes; the request reports the error
+      for (size_t q = sent0; q < sent.size(); ++q) e->logs[sent[q].log].consumers[k].offset -= sent[q].nb;
+      advs.resize(advs.size() - (sent.size() - sent0));
+      sent.resize(sent0);
+      hdr.resize(h0);
+      r.status = st;
+      r.header_bytes = 0;
+      r.out_len = 0;
+      continue;
+    }
+    const uint32_t hb = uint32_t(hdr.size() - h0);
+    hdr[h0] = uint8_t(hb >> 24), hdr[h0 + 1] = uint8_t(hb >> 16), hdr[h0 + 2] = uint8_t(hb >> 8), hdr[h0 + 3] = uint8_t(hb);
+    for (size_t q = sent0; q < sent.size(); ++q) sent[q].dst += dst + hb;
+    r.header_bytes = hb;
+    r.out_len = hb + dlen;
+    dst += r.out_len;
+  }
+  *total = dst;
+  if (dst > cap || (dst && !out)) {  // nothing moves: undo every take
+    for (auto& a : advs) e->logs[a.log].consumers[a.k].offset -= a.nb;
+    return fail(CLG_E_CAPACITY, "enrich needs %llu bytes", (unsigned long long)dst);
+  }
+  if (dst == 0) return CLG_OK;
+  // headers staged in HBM (guard bytes either side for the gather's aligned reads)
+  constexpr size_t kG = 32;
+  CHK(e->d_hdr.ensure(hdr.size() + 2 * kG));
+  CHK(e->h_stage.ensure(hdr.size() + 16));
+  memcpy(e->h_stage.p, hdr.data(), hdr.size());
+  uint8_t* dh = e->d_hdr.as<uint8_t>() + kG;
+  HIPCHK(hipMemcpyAsync(dh, e->h_stage.p, hdr.size(), hipMemcpyHostToDevice, e->stream));
+  std::vector<clg::GatherPiece> pieces;
+  for (uint32_t i = 0; i < n; ++i)
+    if (reqs[i].status == CLG_OK && reqs[i].header_bytes)
+      pieces.push_back(clg::GatherPiece{dh + hdr_at[i], reqs[i].out_off, reqs[i].header_bytes, 0});
+  for (auto& q : sent)
+    if (q.nb > 0) e->add_pieces(e->logs[q.log], q.phys, q.nb, q.dst, pieces);
+  return e->run_gather(pieces, dst, out, out_kind);
+}
+
+// processCausalLogDelta (:117-163): header parsed on the host, deltas applied by the
+// batched upstream scatter straight from the message buffer.
+int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint64_t n, uint32_t in_kind,
+                      int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs, uint64_t* consumed) {
+  ENGINE_GUARD(e);
+  if (!msg || !epoch || !n_logs || strategy > CLG_DELTA_HIERARCHICAL) return fail(CLG_E_INVALID_ARG, "null argument");
+  *n_logs = 0;
+  if (n < 12) return fail(CLG_E_TRUNCATED, "delta header truncated");
+  std::vector<uint8_t> hb(12);
+  if (in_kind == CLG_MEM_DEVICE) HIPCHK(hipMemcpy(hb.data(), msg, 12, hipMemcpyDeviceToHost));
+  else memcpy(hb.data(), msg, 12);
+  const int32_t hsize = int32_t(rd32(hb.data()));
+  if (hsize < 12 || uint64_t(hsize) > n) return fail(CLG_E_TRUNCATED, "delta header size %d", hsize);
+  hb.resize(size_t(hsize));
+  if (in_kind == CLG_MEM_DEVICE) HIPCHK(hipMemcpy(hb.data(), msg, size_t(hsize), hipMemcpyDeviceToHost));
+  else memcpy(hb.data(), msg, size_t(hsize));
+  *epoch = int64_t(rd64(hb.data() + 4));
+  size_t p = 12;
+  uint64_t delta_at = uint64_t(hsize);
+  std::vector<clg_delta_req> reqs;
+  auto need = [&](size_t k) { return p + k <= size_t(hsize); };
+  auto apply = [&](const clg_causal_log_id& id) -> int {  // processThreadDelta :129-163
+    if (!need(8)) return fail(CLG_E_TRUNCATED, "delta record truncated");
+    const int32_t ofe = int32_t(rd32(&hb[p])), len = int32_t(rd32(&hb[p + 4]));
+    p += 8;
+    if (len < 0 || delta_at + uint64_t(len) > n) return fail(CLG_E_TRUNCATED, "delta past the message");
+    uint32_t h;
+    const IdKey key = key_of(id);
+    auto it = e->by_id.find(key);
+    if (it == e->by_id.end()) {
+      CHK(clg_log_open(e, &id, &h));  // insertNewUpstreamLog
+    } else {
+      h = it->second;
+    }
+    reqs.push_back(clg_delta_req{h, ofe, *epoch, delta_at, uint32_t(len), 0});
+    delta_at += uint64_t(len);
+    if (*n_logs < cap && handles) handles[*n_logs] = h;
+    ++*n_logs;
+    return CLG_OK;
+  };
+  while (p < size_t(hsize)) {
+    clg_causal_log_id id{};
+    if (!need(3)) return fail(CLG_E_TRUNCATED, "CausalLogID truncated");
+    id.vertex_id = int16_t(uint16_t(hb[p]) << 8 | hb[p + 1]);
+    const bool main = hb[p + 2] != 0;
+    p += 3;
+    if (strategy == CLG_DELTA_FLAT) {  // deserializeCausalLogID (Flat :107-119)
+      id.is_main = main ? 1 : 0;
+      if (!main) {
+        if (!need(17)) return fail(CLG_E_TRUNCATED, "CausalLogID truncated");
+        id.irp_lower = int64_t(rd64(&hb[p]));
+        id.irp_upper = int64_t(rd64(&hb[p + 8]));
+        id.subpartition = int8_t(hb[p + 16]);
+        p += 17;
+      }
+      CHK(apply(id));
+    } else {  // Grouping deserializeStrategyStep :66-88
+      if (main) {
+        id.is_main = 1;
+        CHK(apply(id));
+      }
+      if (!need(1)) return fail(CLG_E_TRUNCATED, "partition count truncated");
+      const int np = int(int8_t(hb[p++]));
+      for (int q = 0; q < np; ++q) {
+        if (!need(17)) return fail(CLG_E_TRUNCATED, "partition truncated");
+        clg_causal_log_id sid{};
+        sid.vertex_id = id.vertex_id;
+        sid.irp_lower = int64_t(rd64(&hb[p]));
+        sid.irp_upper = int64_t(rd64(&hb[p + 8]));
+        const int ns = int(int8_t(hb[p + 16]));
+        p += 17;
+        for (int t = 0; t < ns; ++t) {
+          if (!need(1)) return fail(CLG_E_TRUNCATED, "subpartition truncated");
+          sid.subpartition = int8_t(hb[p++]);
+          CHK(apply(sid));
+        }
+      }
+    }
+  }
+  if (consumed) *consumed = delta_at;
+  if (reqs.empty()) return CLG_OK;
+  CHK(e->upstream_batch(reqs.data(), uint32_t(reqs.size()), msg, in_kind));
+  for (auto& r : reqs)
+    if (r.status != CLG_OK) return fail(r.status, "processUpstreamDelta failed on log %u", r.log);
+  return CLG_OK;
 }
 
 int clg_kernel_stats(clg_engine* e, clg_kernel_stat* out, uint32_t cap, uint32_t* n) {

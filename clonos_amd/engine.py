@@ -180,7 +180,13 @@ class Engine:
         return log
 
     def get_log(self, cid: CausalLogID) -> Optional["ThreadCausalLog"]:
-        return self._logs.get(cid.key())
+        """The open log for `cid` (also logs the engine opened itself, e.g. by processCausalLogDelta)."""
+        log = self._logs.get(cid.key())
+        if log is None:
+            h = C.c_uint32()
+            if lib.clg_log_find(self._h, C.byref(cid.to_c()), C.byref(h)) == _lib.CLG_OK:
+                log = self._logs[cid.key()] = ThreadCausalLog(self, h.value, cid)
+        return log
 
     def append_batch(self, logs: np.ndarray, epochs: np.ndarray, offs: np.ndarray, lens: np.ndarray,
                      data: np.ndarray):
@@ -307,6 +313,39 @@ class Engine:
         """Benchmark variant: outputs are caller-owned device arrays described by `dec`."""
         check(lib.clg_decode_logs(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles), C.byref(dec),
                                   _np_ptr(base)))
+
+    # ---- piggybacked deltas (AbstractDeltaSerializerDeserializer) ---------------------------
+    def enrich_batch(self, strategy: int, reqs):
+        """enrichWithCausalLogDelta for many channels.  reqs: [(channel, epoch, [(log, send), ...])]
+        with the logs in the strategy's iteration order.  Returns [(status, header+deltas bytes)]."""
+        logs, flags, creq = [], [], (_lib.EnrichReq * max(1, len(reqs)))()
+        for i, (ch, ep, entries) in enumerate(reqs):
+            creq[i].consumer, creq[i].epoch, creq[i].first, creq[i].count = _ch(ch), ep, len(logs), len(entries)
+            for log, send in entries:
+                logs.append(log.handle)
+                flags.append(_lib.CLG_DE_SEND if send else 0)
+        la, fa = np.array(logs or [0], np.uint32), np.array(flags or [0], np.uint8)
+        total = C.c_uint64()
+        st = lib.clg_enrich_batch(self._h, strategy, creq, len(reqs), _np_ptr(la), _np_ptr(fa), None, 0,
+                                  _lib.CLG_MEM_HOST, C.byref(total))
+        if st == _lib.CLG_E_CAPACITY or (st == _lib.CLG_OK and total.value):
+            out = np.empty(max(1, total.value), np.uint8)
+            check(lib.clg_enrich_batch(self._h, strategy, creq, len(reqs), _np_ptr(la), _np_ptr(fa), _np_ptr(out),
+                                       out.size, _lib.CLG_MEM_HOST, C.byref(total)))
+        else:
+            check(st)
+            out = np.zeros(0, np.uint8)
+        return [(creq[i].status, out[creq[i].out_off:creq[i].out_off + creq[i].out_len].tobytes())
+                for i in range(len(reqs))]
+
+    def process_delta(self, strategy: int, msg: bytes):
+        """processCausalLogDelta: returns (epoch, logs touched in header order, bytes consumed)."""
+        buf = np.frombuffer(bytes(msg), np.uint8)
+        ep, nl, used = C.c_int64(), C.c_uint32(), C.c_uint64()
+        hs = np.zeros(4096, np.uint32)
+        check(lib.clg_process_delta(self._h, strategy, _np_ptr(buf), len(msg), _lib.CLG_MEM_HOST, C.byref(ep),
+                                    _np_ptr(hs), hs.size, C.byref(nl), C.byref(used)))
+        return ep.value, [int(h) for h in hs[:min(nl.value, hs.size)]], used.value
 
     # ---- encode -----------------------------------------------------------------------------
     def encode_batch(self, tag, v0, w_idx=None, w_rc=None, w_v1=None, w_var_off=None, w_var_len=None, w_sub=None,

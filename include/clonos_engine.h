@@ -246,6 +246,44 @@ int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, co
                     const uint64_t* len, uint32_t n, uint32_t* winner, uint32_t* n_keys,
                     clg_decoded* out, uint64_t* span_rec_base);
 
+/* ---- piggybacked deltas (AbstractDeltaSerializerDeserializer.java:89-163) -----------------
+ * enrichWithCausalLogDelta for a batch of outgoing buffers.  Request i covers entries
+ * [first, first + count) of log[] / flags[]: the logs the reference's strategy visits for
+ * that channel, in its iteration order, after the strategy's pre-hasDelta filters:
+ *   CLG_DELTA_FLAT          FlatDeltaSerializerDeserializer.serializeDataStrategy :57-90
+ *   CLG_DELTA_HIERARCHICAL  GroupingDeltaSerializerDeserializer.serializeDataStrategy
+ *                           :91-165 (vertex-major: the vertex's main log first, then its
+ *                           partitions' subpartition logs, each partition contiguous)
+ * hasDeltaForConsumer is called on every entry (with its side effects); the delta is sent
+ * when it has bytes and the entry's CLG_DE_SEND flag is set (the Grouping strategy's
+ * post-hasDelta subpartition filter, :148-151).  Output per request at out_off: the delta
+ * header ([size i32][epoch i64] + strategy records, :93-103) then the deltas back to back;
+ * out_len = header + deltas.  CLG_E_CAPACITY: *total = required, no consumer moved. */
+#define CLG_DELTA_FLAT 0u
+#define CLG_DELTA_HIERARCHICAL 1u
+#define CLG_DE_SEND 1u
+
+typedef struct clg_enrich_req {
+  clg_channel_id consumer;
+  int64_t epoch;
+  uint32_t first;
+  uint32_t count;
+  int32_t status;        /* out */
+  uint32_t header_bytes; /* out */
+  uint64_t out_off;      /* out */
+  uint64_t out_len;      /* out */
+} clg_enrich_req;
+
+int clg_enrich_batch(clg_engine* e, uint32_t strategy, clg_enrich_req* reqs, uint32_t n, const uint32_t* log,
+                     const uint8_t* flags, void* out, uint64_t cap, uint32_t out_kind, uint64_t* total);
+
+/* processCausalLogDelta (:117-163) + insertNewUpstreamLog (:165-194): parse one header +
+ * deltas (msg, host or device) and apply processUpstreamDelta to every log it names,
+ * opening the logs not seen before.  *epoch = the header's epoch; handles[] receives the
+ * logs in header order (*n_logs, up to cap); *consumed = header + delta bytes. */
+int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint64_t n, uint32_t in_kind,
+                      int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs, uint64_t* consumed);
+
 /* ---- batched encode (SimpleDeterminantEncoder.encodeTo :56-75, writers :124-323) ---------
  * The inverse of the decode: records given in the decode's SoA layout (tag, v0; a
  * side-table row per wide record, rows in record order and w_idx naming the record;
