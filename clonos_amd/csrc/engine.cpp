@@ -191,6 +191,14 @@ struct clg_engine {
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
   DevBuf d_hdr;                      // piggyback: delta headers staged for the gather
+  // Slices into device memory run on their own stream, overlapping the next decode: the
+  // gather only reads log segments, so every pool write (flush / upstream scatter) and
+  // every full sync first waits for it (gwait).
+  hipStream_t gstream = nullptr;
+  hipEvent_t gready = nullptr;
+  bool g_pending = false;
+  PinBuf h_gdesc;
+  DevBuf d_gdesc, d_gpieces;
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
@@ -214,12 +222,12 @@ struct clg_engine {
     return e;
   }
   template <class F>
-  int timed(const char* name, uint64_t bytes, F&& launch) {
+  int timed(const char* name, uint64_t bytes, F&& launch, hipStream_t on = nullptr) {
     if (!(cfg.flags & CLG_F_TIMING)) return launch();
     hipEvent_t a = get_event(), b = get_event();
-    hipEventRecord(a, stream);
+    hipEventRecord(a, on ? on : stream);
     int r = launch();
-    hipEventRecord(b, stream);
+    hipEventRecord(b, on ? on : stream);
     timings.push_back(PendingTiming{name, a, b, bytes});
     return r;
   }
@@ -237,7 +245,15 @@ struct clg_engine {
     }
     timings.clear();
   }
+  int gwait() {
+    if (g_pending) {
+      g_pending = false;
+      HIPCHK(hipStreamSynchronize(gstream));
+    }
+    return CLG_OK;
+  }
   int sync() {
+    CHK(gwait());
     HIPCHK(hipStreamSynchronize(stream));
     collect_timings();
     return CLG_OK;
@@ -289,6 +305,7 @@ struct clg_engine {
         nchunks += l.pending.size() / C() + 2;
       }
     if (total == 0) return CLG_OK;
+    CHK(gwait());  // an in-flight gather may still read the segments about to be written
     const size_t desc_bytes = nchunks * sizeof(clg::ScatterChunk);
     CHK(h_stage.ensure(total));
     CHK(h_desc.ensure(desc_bytes));
@@ -366,6 +383,7 @@ struct clg_engine {
       return CLG_OK;
     }
     CHK(flush());
+    CHK(gwait());  // the scatter below writes segments an in-flight gather may read
     std::vector<clg::ScatterChunk> ch;
     size_t total = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -493,6 +511,7 @@ struct clg_engine {
   int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                       uint64_t total, void* out, uint32_t out_kind) {
     if (runs.empty() || !n_pieces) return CLG_OK;
+    if (out_kind == CLG_MEM_DEVICE && gstream) return gather_runs_async(runs, segtab, n_pieces, total, out);
     const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
     const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
     CHK(h_desc.ensure(hb));
@@ -516,6 +535,32 @@ struct clg_engine {
     }));
     if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
     return sync();
+  }
+
+  // Device-output slice gather on gstream, after everything already queued on `stream`
+  // (appends); returns without waiting.  Its own descriptor buffers, so the next decode
+  // on `stream` does not touch them; the next gather waits for this one first.
+  int gather_runs_async(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
+                        uint64_t total, void* out) {
+    CHK(gwait());
+    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
+    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    CHK(h_gdesc.ensure(hb));
+    CHK(d_gdesc.ensure(hb));
+    CHK(d_gpieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
+    memcpy(h_gdesc.p, runs.data(), rb);
+    memcpy(h_gdesc.as<uint8_t>() + o_seg, segtab.data(), gb);
+    HIPCHK(hipEventRecord(gready, stream));
+    HIPCHK(hipStreamWaitEvent(gstream, gready, 0));
+    HIPCHK(hipMemcpyAsync(d_gdesc.p, h_gdesc.p, hb, hipMemcpyHostToDevice, gstream));
+    CHK(clg::launch_expand_pieces(d_gdesc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
+                                  reinterpret_cast<const uint32_t*>(d_gdesc.as<uint8_t>() + o_seg), pool, C(),
+                                  d_gpieces.as<clg::GatherPiece>(), gstream));
+    CHK(timed("slice_gather", 2 * total, [&] {
+      return clg::launch_gather(d_gpieces.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
+    }, gstream));
+    g_pending = true;
+    return CLG_OK;
   }
 
   int get_delta(uint32_t h, ChKey k, int64_t epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
@@ -1076,6 +1121,8 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&e->gready, hipEventDisableTiming));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, pool_bytes + 2 * kPoolGuard));  // guards: aligned over-reads either side
@@ -1091,6 +1138,7 @@ void clg_engine_destroy(clg_engine* e) {
   if (!e) return;
   hipSetDevice(e->cfg.device);
   hipStreamSynchronize(e->stream);
+  e->gwait();
   for (auto& t : e->timings) {
     hipEventDestroy(t.a);
     hipEventDestroy(t.b);
@@ -1098,6 +1146,8 @@ void clg_engine_destroy(clg_engine* e) {
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
   if (e->pool_alloc) hipFree(e->pool_alloc);
   hipStreamDestroy(e->stream);
+  if (e->gstream) hipStreamDestroy(e->gstream);
+  if (e->gready) hipEventDestroy(e->gready);
   delete e;
 }
 
