@@ -197,8 +197,12 @@ struct clg_engine {
   hipStream_t gstream = nullptr;
   hipEvent_t gready = nullptr;
   bool g_pending = false;
-  PinBuf h_gdesc;
-  DevBuf d_gdesc, d_gpieces;
+  // two descriptor sets, so a gather can be queued while the previous one still runs;
+  // gdone[s] marks the end of the last gather that used set s
+  PinBuf h_gdesc[2];
+  DevBuf d_gdesc[2], d_gpieces[2];
+  hipEvent_t gdone[2] = {nullptr, nullptr};
+  uint32_t gseq = 0;
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
 
@@ -542,23 +546,29 @@ struct clg_engine {
   // on `stream` does not touch them; the next gather waits for this one first.
   int gather_runs_async(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                         uint64_t total, void* out) {
-    CHK(gwait());
+    const uint32_t set = gseq++ & 1u;
+    if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
+    else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
     const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
     const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
-    CHK(h_gdesc.ensure(hb));
-    CHK(d_gdesc.ensure(hb));
-    CHK(d_gpieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
-    memcpy(h_gdesc.p, runs.data(), rb);
-    memcpy(h_gdesc.as<uint8_t>() + o_seg, segtab.data(), gb);
+    PinBuf& hd = h_gdesc[set];
+    DevBuf& dd = d_gdesc[set];
+    DevBuf& dp = d_gpieces[set];
+    CHK(hd.ensure(hb));
+    CHK(dd.ensure(hb));
+    CHK(dp.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
+    memcpy(hd.p, runs.data(), rb);
+    memcpy(hd.as<uint8_t>() + o_seg, segtab.data(), gb);
     HIPCHK(hipEventRecord(gready, stream));
     HIPCHK(hipStreamWaitEvent(gstream, gready, 0));
-    HIPCHK(hipMemcpyAsync(d_gdesc.p, h_gdesc.p, hb, hipMemcpyHostToDevice, gstream));
-    CHK(clg::launch_expand_pieces(d_gdesc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
-                                  reinterpret_cast<const uint32_t*>(d_gdesc.as<uint8_t>() + o_seg), pool, C(),
-                                  d_gpieces.as<clg::GatherPiece>(), gstream));
+    HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
+    CHK(clg::launch_expand_pieces(dd.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
+                                  reinterpret_cast<const uint32_t*>(dd.as<uint8_t>() + o_seg), pool, C(),
+                                  dp.as<clg::GatherPiece>(), gstream));
     CHK(timed("slice_gather", 2 * total, [&] {
-      return clg::launch_gather(d_gpieces.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
+      return clg::launch_gather(dp.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
     }, gstream));
+    HIPCHK(hipEventRecord(gdone[set], gstream));
     g_pending = true;
     return CLG_OK;
   }
@@ -1148,6 +1158,8 @@ void clg_engine_destroy(clg_engine* e) {
   hipStreamDestroy(e->stream);
   if (e->gstream) hipStreamDestroy(e->gstream);
   if (e->gready) hipEventDestroy(e->gready);
+  for (auto ev : e->gdone)
+    if (ev) hipEventDestroy(ev);
   delete e;
 }
 
