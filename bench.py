@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config3", action="store_true", help="skip the secondary config-3 decode measurement")
+    ap.add_argument("--no-isolated", action="store_true", help="skip the isolated per-kernel pass (profiling runs)")
     return ap.parse_args()
 
 
@@ -149,7 +150,7 @@ def main():
     # isolated pass (after the timed region): the same steps with the slice gather waited
     # for before the next decode, so every kernel's duration is its own (no overlap)
     eng.kernel_stats_reset()
-    for _ in range(min(args.steps, 5)):
+    for _ in range(0 if args.no_isolated else min(args.steps, 5)):
         step()
         eng.sync()
     torch.cuda.synchronize()

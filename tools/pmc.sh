@@ -6,7 +6,7 @@ set -euo pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${*:---logs 16 --steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${*:---logs 16 --steps 2 --warmup 1 --no-cpu-baseline --no-config3}
 mkdir -p "$OUT"
 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 i=0
