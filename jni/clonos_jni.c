@@ -8,6 +8,7 @@
  *      jni/clonos_jni.c -Lclonos_amd -lclonos_engine -o libclonos_jni.so
  */
 #include <jni.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "clonos_engine.h"
@@ -153,4 +154,169 @@ JNIEXPORT jint JNICALL FN(nTruncateAll)(JNIEnv* env, jclass cls, jlong e, jlong 
   int st = clg_truncate_all(ENG(e), cp, &a);
   put_int(env, applied, a);
   return st;
+}
+
+/* ---- batched paths ----------------------------------------------------------------
+ * Arrays of handles / ids come in as Java primitive arrays (copied by the JVM), bulk data
+ * as direct ByteBuffers (no copies).  Result words go back through long[] arrays. */
+
+/* clg_decode_logs: SoA into direct buffers; res = {n_rec, n_wide, err_status, err_span,
+ * err_off, err_tag}; spanRecBase has n + 1 entries. */
+JNIEXPORT jint JNICALL FN(nDecodeLogs)(JNIEnv* env, jclass cls, jlong e, jintArray logs, jlongArray starts,
+                                       jobject off, jobject tag, jobject v0, jobject w_idx, jobject w_rc, jobject w_v1,
+                                       jobject w_var_off, jobject w_var_len, jobject w_sub, jlongArray res,
+                                       jlongArray span_rec_base) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, logs);
+  jint* lg = (*env)->GetIntArrayElements(env, logs, NULL);
+  jlong* st = (*env)->GetLongArrayElements(env, starts, NULL);
+  jlong* base = (*env)->GetLongArrayElements(env, span_rec_base, NULL);
+  clg_decoded d;
+  memset(&d, 0, sizeof d);
+  d.off = (uint32_t*)addr(env, off, 0);
+  d.tag = addr(env, tag, 0);
+  d.v0 = (int64_t*)addr(env, v0, 0);
+  d.w_idx = (uint32_t*)addr(env, w_idx, 0);
+  d.w_rc = (int32_t*)addr(env, w_rc, 0);
+  d.w_v1 = (int64_t*)addr(env, w_v1, 0);
+  d.w_var_off = (uint32_t*)addr(env, w_var_off, 0);
+  d.w_var_len = (uint32_t*)addr(env, w_var_len, 0);
+  d.w_sub = addr(env, w_sub, 0);
+  d.cap = cap(env, tag);
+  d.wcap = cap(env, w_sub);
+  d.out_kind = CLG_MEM_HOST;
+  int s = clg_decode_logs(ENG(e), (const uint32_t*)lg, (const int64_t*)st, (uint32_t)n, &d, (uint64_t*)base);
+  jlong r[6] = {(jlong)d.n_rec, (jlong)d.n_wide, d.err_status, d.err_span, d.err_off, d.err_tag};
+  (*env)->SetLongArrayRegion(env, res, 0, 6, r);
+  (*env)->ReleaseLongArrayElements(env, span_rec_base, base, 0);
+  (*env)->ReleaseLongArrayElements(env, starts, st, JNI_ABORT);
+  (*env)->ReleaseIntArrayElements(env, logs, lg, JNI_ABORT);
+  return s;
+}
+
+/* clg_enrich_batch: reqs packed as 5 longs per request {chLo, chHi, epoch, first, count};
+ * res gets 4 longs per request {status, headerBytes, outOff, outLen}. */
+JNIEXPORT jint JNICALL FN(nEnrichBatch)(JNIEnv* env, jclass cls, jlong e, jint strategy, jlongArray reqs,
+                                        jintArray logs, jbyteArray flags, jobject out, jlongArray res,
+                                        jlongArray total) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, reqs) / 5;
+  jlong* rq = (*env)->GetLongArrayElements(env, reqs, NULL);
+  jint* lg = (*env)->GetIntArrayElements(env, logs, NULL);
+  jbyte* fl = (*env)->GetByteArrayElements(env, flags, NULL);
+  clg_enrich_req* r = (clg_enrich_req*)calloc(n ? (size_t)n : 1u, sizeof(clg_enrich_req));
+  for (jsize i = 0; i < n; ++i) {
+    r[i].consumer = ch(rq[5 * i], rq[5 * i + 1]);
+    r[i].epoch = rq[5 * i + 2];
+    r[i].first = (uint32_t)rq[5 * i + 3];
+    r[i].count = (uint32_t)rq[5 * i + 4];
+  }
+  uint64_t t = 0;
+  int s = clg_enrich_batch(ENG(e), (uint32_t)strategy, r, (uint32_t)n, (const uint32_t*)lg, (const uint8_t*)fl,
+                           addr(env, out, 0), cap(env, out), CLG_MEM_HOST, &t);
+  for (jsize i = 0; i < n; ++i) {
+    jlong w[4] = {r[i].status, (jlong)r[i].header_bytes, (jlong)r[i].out_off, (jlong)r[i].out_len};
+    (*env)->SetLongArrayRegion(env, res, 4 * i, 4, w);
+  }
+  jlong tt = (jlong)t;
+  (*env)->SetLongArrayRegion(env, total, 0, 1, &tt);
+  free(r);
+  (*env)->ReleaseByteArrayElements(env, flags, fl, JNI_ABORT);
+  (*env)->ReleaseIntArrayElements(env, logs, lg, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, reqs, rq, JNI_ABORT);
+  return s;
+}
+
+/* clg_process_delta on msg[off, off + len); res = {epoch, nLogs, consumed}. */
+JNIEXPORT jint JNICALL FN(nProcessDelta)(JNIEnv* env, jclass cls, jlong e, jint strategy, jobject msg, jint off,
+                                         jint len, jintArray handles, jlongArray res) {
+  (void)cls;
+  int64_t ep = 0;
+  uint32_t nl = 0;
+  uint64_t used = 0;
+  const jsize hc = (*env)->GetArrayLength(env, handles);
+  jint* hs = (*env)->GetIntArrayElements(env, handles, NULL);
+  int s = clg_process_delta(ENG(e), (uint32_t)strategy, addr(env, msg, off), (uint64_t)len, CLG_MEM_HOST, &ep,
+                            (uint32_t*)hs, (uint32_t)hc, &nl, &used);
+  (*env)->ReleaseIntArrayElements(env, handles, hs, 0);
+  jlong r[3] = {ep, (jlong)nl, (jlong)used};
+  (*env)->SetLongArrayRegion(env, res, 0, 3, r);
+  return s;
+}
+
+/* ReplayingState for one failed vertex: the merged DeterminantResponseEvent as written by
+ * its write() (DeterminantResponseEvent.java:93-107) in `event`, the subpartition table as
+ * 3 longs per entry {irpLower, irpUpper, index}.  Main-log SoA as in nDecodeLogs (res:
+ * 6 longs); per subpartition 4 longs {count, status, errOff, errTag} in subRes and the
+ * BufferBuilt sizes back to back in `sizes` (int32, native order). */
+JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jshort vertex, jobject event, jint len,
+                                          jlongArray subparts, jobject off, jobject tag, jobject v0, jobject w_idx,
+                                          jobject w_rc, jobject w_v1, jobject w_var_off, jobject w_var_len,
+                                          jobject w_sub, jlongArray res, jobject sizes, jlongArray sub_res) {
+  (void)cls;
+  clg_response_entry* ents = (clg_response_entry*)calloc((size_t)len / 7u + 1u, sizeof(clg_response_entry));
+  clg_response acc;
+  memset(&acc, 0, sizeof acc);
+  acc.entries = ents;
+  acc.cap = (uint32_t)len / 7u + 1u;
+  uint64_t used = 0;
+  int s = clg_response_read(addr(env, event, 0), (uint64_t)len, &acc, &used);
+  const jsize ns = (*env)->GetArrayLength(env, subparts) / 3;
+  jlong* sp = (*env)->GetLongArrayElements(env, subparts, NULL);
+  clg_causal_log_id* ids = (clg_causal_log_id*)calloc(ns ? (size_t)ns : 1u, sizeof(clg_causal_log_id));
+  uint64_t* sbase = (uint64_t*)calloc((size_t)ns + 1u, 8);
+  uint64_t* cnt = (uint64_t*)calloc((size_t)ns + 1u, 8);
+  int32_t* sst = (int32_t*)calloc((size_t)ns + 1u, 4);
+  int64_t* soff = (int64_t*)calloc((size_t)ns + 1u, 8);
+  int32_t* stg = (int32_t*)calloc((size_t)ns + 1u, 4);
+  for (jsize i = 0; i < ns; ++i) {
+    ids[i].vertex_id = vertex;
+    ids[i].irp_lower = sp[3 * i];
+    ids[i].irp_upper = sp[3 * i + 1];
+    ids[i].subpartition = (int8_t)sp[3 * i + 2];
+  }
+  clg_decoded d;
+  memset(&d, 0, sizeof d);
+  d.off = (uint32_t*)addr(env, off, 0);
+  d.tag = addr(env, tag, 0);
+  d.v0 = (int64_t*)addr(env, v0, 0);
+  d.w_idx = (uint32_t*)addr(env, w_idx, 0);
+  d.w_rc = (int32_t*)addr(env, w_rc, 0);
+  d.w_v1 = (int64_t*)addr(env, w_v1, 0);
+  d.w_var_off = (uint32_t*)addr(env, w_var_off, 0);
+  d.w_var_len = (uint32_t*)addr(env, w_var_len, 0);
+  d.w_sub = addr(env, w_sub, 0);
+  d.cap = cap(env, tag);
+  d.wcap = cap(env, w_sub);
+  d.out_kind = CLG_MEM_HOST;
+  uint64_t main_base[2] = {0, 0};
+  if (s == CLG_OK) {
+    clg_replay_vertex v;
+    memset(&v, 0, sizeof v);
+    v.acc = &acc;
+    v.subpartitions = ids;
+    v.n_subpartitions = (uint32_t)ns;
+    v.vertex_id = vertex;
+    clg_replay_out o;
+    memset(&o, 0, sizeof o);
+    o.main = &d;
+    o.main_rec_base = main_base;
+    o.buffer_sizes = (int32_t*)addr(env, sizes, 0);
+    o.sizes_cap = cap(env, sizes) / 4u;
+    o.sizes_base = sbase;
+    o.sub_count = cnt;
+    o.sub_status = sst;
+    o.sub_err_off = soff;
+    o.sub_err_tag = stg;
+    s = clg_replay_prepare(ENG(e), &v, 1, &o);
+  }
+  jlong r[6] = {(jlong)d.n_rec, (jlong)d.n_wide, d.err_status, d.err_span, d.err_off, d.err_tag};
+  (*env)->SetLongArrayRegion(env, res, 0, 6, r);
+  for (jsize i = 0; i < ns; ++i) {
+    jlong w[4] = {(jlong)cnt[i], sst[i], soff[i], stg[i]};
+    (*env)->SetLongArrayRegion(env, sub_res, 4 * i, 4, w);
+  }
+  (*env)->ReleaseLongArrayElements(env, subparts, sp, JNI_ABORT);
+  free(ids), free(sbase), free(cnt), free(sst), free(soff), free(stg), free(ents);
+  return s;
 }

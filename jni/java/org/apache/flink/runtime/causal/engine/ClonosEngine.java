@@ -94,4 +94,17 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nNotifyCheckpointComplete(long engine, int log, long checkpointId);
 	static native int nUnregisterConsumer(long engine, int log, long chLo, long chHi);
 	static native int nTruncateAll(long engine, long checkpointId, int[] applied);
+
+	// batched paths: LogReplayerImpl / ReplayingState decode, the piggyback serde, replay-prep
+	static native int nDecodeLogs(long engine, int[] logs, long[] startEpochs, ByteBuffer off, ByteBuffer tag,
+								  ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
+								  ByteBuffer wVarLen, ByteBuffer wSub, long[] result, long[] spanRecBase);
+	static native int nEnrichBatch(long engine, int strategy, long[] requests, int[] logs, byte[] flags,
+								   ByteBuffer out, long[] results, long[] total);
+	static native int nProcessDelta(long engine, int strategy, ByteBuffer msg, int off, int len, int[] handles,
+									long[] result);
+	static native int nReplayPrepare(long engine, short vertexId, ByteBuffer mergedEvent, int len, long[] subpartitions,
+									 ByteBuffer off, ByteBuffer tag, ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc,
+									 ByteBuffer wV1, ByteBuffer wVarOff, ByteBuffer wVarLen, ByteBuffer wSub,
+									 long[] result, ByteBuffer bufferSizes, long[] subpartitionResults);
 }
