@@ -54,10 +54,18 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # CLONOS_BENCH_REHEARSAL=1: every rank on cuda:0 with gloo, to rehearse the N>1 path on a
+    # one-GPU box (numbers meaningless); the real multi-GPU run is one rank per GPU over RCCL
+    rehearse = os.environ.get("CLONOS_BENCH_REHEARSAL") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from clonos_amd import CausalLogID, Engine, _lib, synth
 
@@ -143,7 +151,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = eng.kernel_stats()
