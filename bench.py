@@ -80,7 +80,7 @@ def main():
     total_bytes = sum(log_bytes)
     seg = 16384
     pool = sum((n + seg - 1) // seg + 1 for n in log_bytes) + 64
-    eng = Engine(segment_bytes=seg, pool_segments=pool, device=local, timing=True)
+    eng = Engine(segment_bytes=seg, pool_segments=pool, device=local, timing=True, async_slice=True)
     logs = []
     for v, b in enumerate(bufs):
         vid = rank * args.logs + v  # VertexID sharding: this rank owns its vertices

@@ -36,11 +36,12 @@ CLG_MEM_HOST = 0
 CLG_MEM_DEVICE = 1
 CLG_F_TIMING = 1
 CLG_F_ROBUST_DECODE = 2
+CLG_F_ASYNC_SLICE = 4
 CLG_FULL_SHARING = -1
 
 EXPORTED = [
     "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
-    "clg_engine_stream", "clg_sync", "clg_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find",
+    "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find",
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
     "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
@@ -220,6 +221,7 @@ def _load() -> C.CDLL:
         "clg_last_error": (C.c_char_p, []),
         "clg_abi_version": (C.c_int, []),
         "clg_engine_stream": (P, [P]),
+        "clg_gather_stream": (P, [P]),
         "clg_sync": (C.c_int, [P]),
         "clg_pool_stats": (C.c_int, [P, u32p, u32p]),
         "clg_log_open": (C.c_int, [P, C.POINTER(CausalLogIdC), u32p]),

@@ -515,7 +515,8 @@ struct clg_engine {
   int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                       uint64_t total, void* out, uint32_t out_kind) {
     if (runs.empty() || !n_pieces) return CLG_OK;
-    if (out_kind == CLG_MEM_DEVICE && gstream) return gather_runs_async(runs, segtab, n_pieces, total, out);
+    if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
+      return gather_runs_async(runs, segtab, n_pieces, total, out);
     const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
     const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
     CHK(h_desc.ensure(hb));
@@ -1164,6 +1165,7 @@ void clg_engine_destroy(clg_engine* e) {
 }
 
 void* clg_engine_stream(clg_engine* e) { return e ? (void*)e->stream : nullptr; }
+void* clg_gather_stream(clg_engine* e) { return e ? (void*)e->gstream : nullptr; }
 
 int clg_sync(clg_engine* e) {
   ENGINE_GUARD(e);

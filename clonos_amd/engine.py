@@ -117,9 +117,12 @@ class Engine:
     """One engine per GPU (one process per GPU).  Owns the HBM segment pool."""
 
     def __init__(self, segment_bytes: int = 16384, pool_segments: int = 16384, device: int = 0,
-                 sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto"):
+                 sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto",
+                 async_slice: bool = False):
         """decode: "auto" = single-pass fused kernel, robust multi-pass pipeline on abort;
-        "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE)."""
+        "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
+        slices return once queued on the gather stream (CLG_F_ASYNC_SLICE); sync() before
+        reading them."""
         if decode not in ("auto", "robust"):
             raise ValueError(f"decode must be 'auto' or 'robust', not {decode!r}")
         cfg = _lib.Config()
@@ -128,7 +131,8 @@ class Engine:
         cfg.pool_segments = pool_segments
         cfg.device = device
         cfg.sharing_depth = sharing_depth
-        cfg.flags = (_lib.CLG_F_TIMING if timing else 0) | (_lib.CLG_F_ROBUST_DECODE if decode == "robust" else 0)
+        cfg.flags = ((_lib.CLG_F_TIMING if timing else 0) | (_lib.CLG_F_ROBUST_DECODE if decode == "robust" else 0)
+                     | (_lib.CLG_F_ASYNC_SLICE if async_slice else 0))
         h = C.c_void_p()
         check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))
         self._h = h

@@ -92,6 +92,10 @@ typedef struct clg_config {
 #define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
 #define CLG_F_ROBUST_DECODE 2u /* skip the single-pass decode kernel; always use the robust
                                   multi-pass pipeline (the fallback the fused kernel aborts to) */
+#define CLG_F_ASYNC_SLICE 4u   /* slices into device memory (clg_slice_batch, CLG_MEM_DEVICE)
+                                  return once queued on the engine's gather stream and overlap
+                                  later decodes; the output is ready after clg_sync or once
+                                  clg_gather_stream's work completes.  Default: synchronous */
 
 typedef struct clg_engine clg_engine;
 
@@ -103,6 +107,8 @@ const char* clg_last_error(void);
 int clg_abi_version(void);
 /* The HIP stream (hipStream_t) all engine work is issued on. */
 void* clg_engine_stream(clg_engine* e);
+/* The stream CLG_F_ASYNC_SLICE gathers run on (hipStream_t). */
+void* clg_gather_stream(clg_engine* e);
 /* Flush staged appends to HBM and wait for all queued GPU work. */
 int clg_sync(clg_engine* e);
 /* Segments in use / free in the HBM pool. */
