@@ -654,6 +654,19 @@ __global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_
   if (tid < n_blocks) gp(ctl.boff)[tid] = run;
 }
 
+// Each span's record / wide-record range from the scan (the host reads them before the
+// emit pass, so an asynchronous caller knows its record counts while emit still runs).
+__global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict__ spans, uint32_t n_spans,
+                                                      FusedCtl ctl) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= n_spans || ld_agent32(ctl.abort)) return;
+  const SpanDesc sd = spans[s];
+  if (!sd.n_tiles) return;
+  const uint32_t t0 = sd.first_tile, t1 = sd.first_tile + sd.n_tiles - 1;
+  gp(ctl.span_lo)[s] = gp(ctl.base)[t0] + gp(ctl.boff)[t0 / kZScanBlock];
+  gp(ctl.span_hi)[s] = gp(ctl.base)[t1] + gp(ctl.boff)[t1 / kZScanBlock] + gp(ctl.cnt)[t1];
+}
+
 // ---------------------------------------------------------------------------------
 // Pass 3 for one tile: record starts dropped into LDS by output index (from the bitmap),
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
@@ -713,7 +726,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
-  const uint64_t cnt_t = gp(ctl.cnt)[t];
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   stage_image(td, sd, t, tiles, s_img, lane, hi);
   JL jl{nullptr, nullptr, nullptr};
@@ -727,10 +739,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
     if ((int)lane >= off) incl += y;
   }
   const uint32_t total = __shfl(incl, 63);
-  if (lane == 0) {  // the span's record / wide-record range, at its first and last tiles
-    if (t == sd.first_tile) gp(ctl.span_lo)[td.span] = base;
-    if (t + 1 == sd.first_tile + sd.n_tiles) gp(ctl.span_hi)[td.span] = base + cnt_t;
-  }
   const uint64_t rec0 = base & ((1ull << 31) - 1), wide0 = base >> 31;
   Bits cur{bits.x, bits.y};
   uint32_t idx = incl - cnt;
@@ -1097,6 +1105,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
     hipLaunchKernelGGL(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
     hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
+    hipLaunchKernelGGL(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
   } else if (phase == 2) {
     if (ctl.jser)
       hipLaunchKernelGGL(k_decode_emit<true>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);

@@ -560,8 +560,8 @@ struct clg_engine {
     CHK(dp.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
     memcpy(hd.p, runs.data(), rb);
     memcpy(hd.as<uint8_t>() + o_seg, segtab.data(), gb);
-    HIPCHK(hipEventRecord(gready, stream));
-    HIPCHK(hipStreamWaitEvent(gstream, gready, 0));
+    // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
+    // its call returned, and decodes only read the pool
     HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
     CHK(clg::launch_expand_pieces(dd.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
                                   reinterpret_cast<const uint32_t*>(dd.as<uint8_t>() + o_seg), pool, C(),
@@ -880,14 +880,7 @@ struct clg_engine {
     CHK(timed("decode_offsets", 24 * uint64_t(nt), [&] {
       return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 1);
     }));
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (cfg.flags & CLG_F_TIMING) {
-      ea = get_event();
-      eb = get_event();
-      hipEventRecord(ea, stream);
-    }
-    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
-    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
+    // span ranges + abort words are known after the scan: read them, then emit
     uint64_t* hz = h_zres.as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -921,12 +914,16 @@ struct clg_engine {
                   l, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7] & 0x7FFFFFFFu, d[7] >> 31);
         }
       }
-      if (ea) {
-        ev_pool.push_back(ea);
-        ev_pool.push_back(eb);
-      }
       return CLG_OK;
     }
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (cfg.flags & CLG_F_TIMING) {
+      ea = get_event();
+      eb = get_event();
+      hipEventRecord(ea, stream);
+    }
+    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
+    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     constexpr uint64_t kRecMask = (1ull << 31) - 1;
     uint64_t nrec = 0, nwide = 0;
     const std::vector<clg::SpanDesc>& sp = p.spans;

@@ -257,3 +257,49 @@ def test_async_slice_overlaps_and_orders():
                     assert st == 0 and host[oo:oo + n] == w
         finally:
             hip.hipFree(dptr)
+
+
+def test_async_decode_device_output():
+    """Decode into device memory on an engine with CLG_F_ASYNC_SLICE (the decode itself stays
+    synchronous): counts final on return, SoA equal to the oracle's decode."""
+    import ctypes
+    from clonos_amd import _lib
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    rng = np.random.default_rng(92)
+    with Engine(segment_bytes=16384, pool_segments=1 << 12, async_slice=True) as eng:
+        bufs = [synth.config2_log(int(rng.integers(1000, 200_000)), rng)[0].tobytes() for _ in range(6)]
+        logs = []
+        for v, b in enumerate(bufs):
+            lg = eng.open_log(CausalLogID.main(v))
+            lg.appendDeterminant(b, 0)
+            logs.append(lg)
+        cap = sum(len(b) for b in bufs) // 2 + 8
+        sizes = dict(off=4 * cap, tag=cap, v0=8 * cap, w_idx=64, w_rc=64, w_v1=64, w_var_off=64, w_var_len=64, w_sub=64)
+        ptrs = {}
+        for k, n in sizes.items():
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n)) == 0
+            ptrs[k] = p
+        try:
+            dec = _lib.Decoded()
+            for k, p in ptrs.items():
+                setattr(dec, k, p.value)
+            dec.cap, dec.wcap, dec.out_kind = cap, 8, _lib.CLG_MEM_DEVICE
+            base = np.zeros(len(logs) + 1, np.uint64)
+            eng.decode_logs_device(np.array([l.handle for l in logs], np.uint32), np.zeros(len(logs), np.int64), dec,
+                                   base)
+            want = [O.decode(b)[1] for b in bufs]
+            assert dec.n_rec == sum(len(w["tag"]) for w in want)
+            eng.sync()
+            got = {}
+            for k, dt in (("off", np.uint32), ("tag", np.uint8), ("v0", np.int64)):
+                a = np.empty(dec.n_rec, dt)
+                assert hip.hipMemcpy(ctypes.c_void_p(a.ctypes.data), ptrs[k], ctypes.c_size_t(a.nbytes), 2) == 0
+                got[k] = a
+            for s, w in enumerate(want):
+                sl = slice(int(base[s]), int(base[s + 1]))
+                for k in ("off", "tag", "v0"):
+                    np.testing.assert_array_equal(got[k][sl], w[k])
+        finally:
+            for p in ptrs.values():
+                hip.hipFree(p)

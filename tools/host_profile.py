@@ -14,7 +14,7 @@ from clonos_amd import CausalLogID, Engine, _lib, synth  # noqa: E402
 nlogs = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 rng = np.random.default_rng(synth.SEED_CONFIG2)
 bufs = [synth.config2_log(1_000_000, rng) for _ in range(nlogs)]
-eng = Engine(segment_bytes=16384, pool_segments=nlogs * 360, timing=False)
+eng = Engine(segment_bytes=16384, pool_segments=nlogs * 360, timing=False, async_slice=True)
 logs = []
 for i, (b, _) in enumerate(bufs):
     lg = eng.open_log(CausalLogID.main(i))
@@ -42,19 +42,19 @@ for k, (i, ch, _) in enumerate(cons):
     creq[k].log = logs[i].handle
     creq[k].consumer = _lib.ChannelId(ch[0], ch[1])
     creq[k].epoch = 1
-T = {"decode": [], "seek": [], "slice": [], "step": []}
+seek_offs = np.array([off for _, _, off in cons], np.int32)
+T = {"decode_call": [], "seek_call": [], "slice_call(async)": [], "step": []}
 for it in range(12):
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     eng.decode_logs_device(handles, starts, dec, base)
     t1 = time.perf_counter()
-    for i, ch, off in cons:
-        logs[i].seek_consumer(ch, 1, off)
+    eng.seek_consumers_raw(creq, seek_offs, len(cons))
     t2 = time.perf_counter()
     eng.slice_batch_raw(creq, cres, len(cons), o_slice.data_ptr(), o_slice.numel(), device=True)
-    torch.cuda.synchronize()
     t3 = time.perf_counter()
     if it >= 2:
-        T["decode"].append(t1 - t0); T["seek"].append(t2 - t1); T["slice"].append(t3 - t2); T["step"].append(t3 - t0)
+        T["decode_call"].append(t1 - t0); T["seek_call"].append(t2 - t1); T["slice_call(async)"].append(t3 - t2)
+        T["step"].append(t3 - t0)
+torch.cuda.synchronize()
 print({k: round(1e3 * float(np.mean(v)), 3) for k, v in T.items()}, "ms")
 eng.close()
