@@ -301,6 +301,12 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     el = (_t.perf_counter() - t0) / steps
     st = eng.kernel_stats()
     n_wide = int(dec.n_wide)
+    # checkpoint-complete epoch truncation of every log (JobCausalLogImpl.notifyCheckpointComplete
+    # fan-out, ThreadCausalLogImpl :398-435): metadata + segment release, reported as latency
+    t0 = _t.perf_counter()
+    applied = eng.truncate_all(n_epochs // 2)
+    trunc_ms = (_t.perf_counter() - t0) * 1e3
+    assert applied
     eng.close()
     algo = total + 13 * n_det + 25 * n_wide
     kern = {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5))
@@ -309,7 +315,8 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
                        "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
            "log_gbs": round(total / el / 1e9, 2), "algo_gbs": round(algo / el / 1e9, 1),
-           "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern}
+           "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern,
+           "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)}}
     if not args.no_cpu_baseline:  # the C++ oracle's decodeNext loop on host cores, whole workload once
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import _oracle as O  # the checker, timed here as the CPU baseline
