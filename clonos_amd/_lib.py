@@ -29,6 +29,7 @@ CLG_E_STATE = -12
 CLG_E_DEVICE = -13
 CLG_E_NO_LOG = -14
 CLG_E_NOT_BUFFER_BUILT = -15
+CLG_E_EPOCH_GAP = -16
 
 STATUS_NAMES = {v: k for k, v in globals().items() if k.startswith("CLG_E_") or k == "CLG_OK"}
 
@@ -49,6 +50,8 @@ EXPORTED = [
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
+    "clg_ifl_open", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
+    "clg_ifl_replay_batch",
 ]
 
 
@@ -201,6 +204,17 @@ CLG_DELTA_HIERARCHICAL = 1
 CLG_DE_SEND = 1
 
 
+class IflReplayReq(C.Structure):
+    _fields_ = [("ifl", C.c_uint32), ("ignore_buffers", C.c_uint32), ("start_epoch", C.c_int64)]
+
+
+class IflReplayRes(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32), ("n_buffers", C.c_uint32), ("remaining", C.c_uint32), ("reserved", C.c_uint32),
+        ("out_off", C.c_uint64), ("len", C.c_uint64), ("sizes_off", C.c_uint64),
+    ]
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("total_ms", C.c_double), ("bytes", C.c_uint64)]
 
@@ -260,6 +274,13 @@ def _load() -> C.CDLL:
         "clg_enrich_batch": (C.c_int, [P, C.c_uint32, C.POINTER(EnrichReq), C.c_uint32, P, P, P, C.c_uint64,
                                        C.c_uint32, u64p]),
         "clg_process_delta": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.c_uint32, i64p, P, C.c_uint32, u32p, u64p]),
+        "clg_ifl_open": (C.c_int, [P, u32p]),
+        "clg_ifl_close": (C.c_int, [P, C.c_uint32]),
+        "clg_ifl_log_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P, C.c_uint32]),
+        "clg_ifl_notify_checkpoint_complete": (C.c_int, [P, C.c_uint32, C.c_int64]),
+        "clg_ifl_state": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, u32p]),
+        "clg_ifl_replay_batch": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, u64p,
+                                           u64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

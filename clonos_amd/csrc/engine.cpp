@@ -80,6 +80,17 @@ struct Log {
   std::unordered_map<ChKey, Consumer, ChKeyHash> consumers;
 };
 
+// In-flight (data) log of one subpartition (InMemorySubpartitionInFlightLogger.java:28-207):
+// SortedMap<epoch, List<Buffer>>; each buffer's bytes occupy whole pool segments.
+struct IflBuf {
+  std::vector<uint32_t> segs;
+  uint32_t len;
+};
+struct InFlight {
+  bool open = false;
+  std::map<int64_t, std::vector<IflBuf>> epochs;
+};
+
 struct IdKey {
   int16_t v;
   uint8_t main;
@@ -176,6 +187,7 @@ struct clg_engine {
   uint8_t* pool = nullptr;
   std::vector<uint32_t> free_segs;
   std::vector<Log> logs;
+  std::vector<InFlight> ifls;
   std::map<IdKey, uint32_t> by_id;
   int64_t latest_cp = 0;  // JobCausalLogImpl.latestCompletedCheckpoint (:92, :117)
   std::recursive_mutex mu;
@@ -490,7 +502,8 @@ struct clg_engine {
     }
   }
 
-  int run_gather(const std::vector<clg::GatherPiece>& pieces, uint64_t total, void* out, uint32_t out_kind) {
+  int run_gather(const std::vector<clg::GatherPiece>& pieces, uint64_t total, void* out, uint32_t out_kind,
+                 const char* stat = "slice_gather") {
     if (pieces.empty()) return CLG_OK;
     const size_t db = pieces.size() * sizeof(clg::GatherPiece);
     CHK(h_desc.ensure(db));
@@ -504,7 +517,7 @@ struct clg_engine {
       CHK(d_out.ensure(total));
       dout = d_out.as<uint8_t>();
     }
-    CHK(timed("slice_gather", 2 * total, [&] {
+    CHK(timed(stat, 2 * total, [&] {
       return clg::launch_gather(d_desc.as<clg::GatherPiece>(), uint32_t(pieces.size()), dout, stream);
     }));
     if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
@@ -1934,6 +1947,211 @@ int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint
   for (auto& r : reqs)
     if (r.status != CLG_OK) return fail(r.status, "processUpstreamDelta failed on log %u", r.log);
   return CLG_OK;
+}
+
+// ---- in-flight (data) log (inflightlogging/InMemorySubpartitionInFlightLogger.java) ------
+static int ifl_get(clg_engine* e, uint32_t h, InFlight** out) {
+  if (h >= e->ifls.size() || !e->ifls[h].open) return fail(CLG_E_NO_LOG, "unknown in-flight log handle %u", h);
+  *out = &e->ifls[h];
+  return CLG_OK;
+}
+
+static void ifl_release(clg_engine* e, std::vector<IflBuf>& bufs) {  // Buffer.recycleBuffer
+  for (auto& b : bufs) e->free_segs.insert(e->free_segs.end(), b.segs.rbegin(), b.segs.rend());
+  bufs.clear();
+}
+
+int clg_ifl_open(clg_engine* e, uint32_t* handle) {
+  ENGINE_GUARD(e);
+  if (!handle) return fail(CLG_E_INVALID_ARG, "null argument");
+  for (uint32_t i = 0; i < e->ifls.size(); ++i)
+    if (!e->ifls[i].open) {
+      e->ifls[i].open = true;
+      *handle = i;
+      return CLG_OK;
+    }
+  e->ifls.emplace_back();
+  e->ifls.back().open = true;
+  *handle = uint32_t(e->ifls.size() - 1);
+  return CLG_OK;
+}
+
+int clg_ifl_close(clg_engine* e, uint32_t h) {  // close() :90-94
+  ENGINE_GUARD(e);
+  InFlight* f;
+  CHK(ifl_get(e, h, &f));
+  for (auto& kv : f->epochs) ifl_release(e, kv.second);
+  f->epochs.clear();
+  f->open = false;
+  return CLG_OK;
+}
+
+// log(buffer, epochID, isFinished) :44-48 -- computeIfAbsent(epoch).add(buffer), batched.
+// Segments are taken for the whole batch first (all-or-nothing), then one scatter copies
+// every buffer into its segments.
+int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, const uint64_t* off,
+                      const uint32_t* len, uint32_t n, const uint8_t* bytes, uint32_t in_kind) {
+  ENGINE_GUARD(e);
+  if (n == 0) return CLG_OK;
+  if (!ifl || !epoch || !off || !len || !bytes) return fail(CLG_E_INVALID_ARG, "null argument");
+  if (in_kind != CLG_MEM_HOST && in_kind != CLG_MEM_DEVICE) return fail(CLG_E_INVALID_ARG, "bad in_kind");
+  const uint32_t C = e->C();
+  size_t need = 0, total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    InFlight* f;
+    CHK(ifl_get(e, ifl[i], &f));
+    need += (size_t(len[i]) + C - 1) / C;
+    total += len[i];
+  }
+  if (need > e->free_segs.size())
+    return fail(CLG_E_NOSPACE, "segment pool exhausted (in-flight log needs %zu, free %zu)", need, e->free_segs.size());
+  CHK(e->gwait());  // a queued gather may still read segments that were freed and are reused now
+  std::vector<clg::ScatterChunk> ch;
+  ch.reserve(need);
+  const uint8_t* dsrc = bytes;
+  if (in_kind == CLG_MEM_HOST) {  // pack the buffers into pinned staging, one upload
+    CHK(e->h_stage.ensure(total ? total : 1));
+    CHK(e->d_stage.ensure(total ? total : 1));
+    dsrc = e->d_stage.as<uint8_t>();
+  }
+  uint64_t packed = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    IflBuf b{{}, len[i]};
+    const uint64_t src = in_kind == CLG_MEM_HOST ? packed : off[i];
+    if (in_kind == CLG_MEM_HOST && len[i]) memcpy(e->h_stage.as<uint8_t>() + packed, bytes + off[i], len[i]);
+    for (uint32_t o = 0; o < len[i]; o += C) {
+      const uint32_t s = e->free_segs.back();
+      e->free_segs.pop_back();
+      b.segs.push_back(s);
+      ch.push_back(clg::ScatterChunk{e->seg_addr(s), src + o, std::min(C, len[i] - o), 0});
+    }
+    packed += len[i];
+    e->ifls[ifl[i]].epochs[epoch[i]].push_back(std::move(b));
+  }
+  if (ch.empty()) return CLG_OK;
+  const size_t db = ch.size() * sizeof(clg::ScatterChunk);
+  CHK(e->h_desc.ensure(db));
+  CHK(e->d_desc.ensure(db));
+  memcpy(e->h_desc.p, ch.data(), db);
+  if (in_kind == CLG_MEM_HOST)
+    HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(e->d_desc.p, e->h_desc.p, db, hipMemcpyHostToDevice, e->stream));
+  CHK(e->timed("ifl_scatter", 2 * total, [&] {
+    return clg::launch_scatter(e->d_desc.as<clg::ScatterChunk>(), uint32_t(ch.size()), dsrc, e->stream);
+  }));
+  HIPCHK(hipStreamSynchronize(e->stream));  // staging buffers are reused; device input is the caller's
+  return CLG_OK;
+}
+
+int clg_ifl_notify_checkpoint_complete(clg_engine* e, uint32_t h, int64_t cp) {  // :51-70
+  ENGINE_GUARD(e);
+  InFlight* f;
+  CHK(ifl_get(e, h, &f));
+  for (auto it = f->epochs.begin(); it != f->epochs.end() && it->first < cp;) {
+    ifl_release(e, it->second);
+    it = f->epochs.erase(it);
+  }
+  return CLG_OK;
+}
+
+int clg_ifl_state(clg_engine* e, uint32_t h, int64_t* ids, uint32_t* nb, uint32_t cap, uint32_t* n_epochs) {
+  ENGINE_GUARD(e);
+  InFlight* f;
+  CHK(ifl_get(e, h, &f));
+  uint32_t k = 0;
+  for (auto& kv : f->epochs) {
+    if (k < cap) {
+      if (ids) ids[k] = kv.first;
+      if (nb) nb[k] = uint32_t(kv.second.size());
+    }
+    ++k;
+  }
+  if (n_epochs) *n_epochs = k;
+  return CLG_OK;
+}
+
+// getInFlightIterator(start, ignore) :73-82 and a full drain of the ReplayIterator
+// (:114-167).  The iterator walks tailMap(start) by ++currentKey, so it only yields
+// contiguous epochs from `start`; a missing key throws inside next() right after the last
+// buffer before it was taken (:156 -> :133), so that buffer is lost to the caller.
+int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t n, clg_ifl_replay_res* res,
+                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, uint64_t sizes_cap,
+                         uint64_t* total, uint64_t* total_buffers) {
+  ENGINE_GUARD(e);
+  if (n && (!reqs || !res)) return fail(CLG_E_INVALID_ARG, "null argument");
+  if (out_kind != CLG_MEM_HOST && out_kind != CLG_MEM_DEVICE) return fail(CLG_E_INVALID_ARG, "bad out_kind");
+  struct Pick {
+    const IflBuf* b;
+    uint64_t dst;
+  };
+  std::vector<Pick> picks;
+  uint64_t dst = 0, nbuf = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    clg_ifl_replay_res& r = res[i];
+    r = clg_ifl_replay_res{CLG_OK, 0, 0, 0, dst, 0, nbuf};
+    InFlight* f;
+    int st = ifl_get(e, reqs[i].ifl, &f);
+    if (st != CLG_OK) {
+      r.status = st;
+      continue;
+    }
+    const int64_t start = reqs[i].start_epoch;
+    const uint64_t ign = reqs[i].ignore_buffers;
+    auto it = f->epochs.find(start);
+    if (it == f->epochs.end()) {  // :121-127 -- currentIterator == null, nothing left
+      if (ign) r.status = fail(CLG_E_STATE, "skip of %llu buffers on an empty iterator", (unsigned long long)ign);
+      continue;
+    }
+    uint64_t tail = 0, k = 0;  // tail: numberOfBuffersLeft (:123); k: buffers before a gap
+    bool gap = false;
+    int64_t expect = start;
+    for (auto jt = it; jt != f->epochs.end(); ++jt) {
+      tail += jt->second.size();
+      if (!gap && jt->first == expect) {
+        k += jt->second.size();
+        ++expect;
+      } else {
+        gap = true;
+      }
+    }
+    const uint64_t deliver = gap ? k - 1 : k;  // buffers next() returns
+    if (gap) {
+      r.status = CLG_E_EPOCH_GAP;
+      if (ign >= k) continue;  // the skip loop itself throws at the gap (:78-79)
+    } else if (ign > deliver) {
+      r.status = fail(CLG_E_STATE, "skip of %llu buffers past the %llu logged", (unsigned long long)ign,
+                      (unsigned long long)deliver);
+      continue;
+    }
+    r.remaining = uint32_t(tail >= ign ? tail - ign : 0);
+    uint64_t idx = 0;
+    for (auto jt = it; jt != f->epochs.end() && idx < deliver; ++jt)
+      for (const IflBuf& b : jt->second) {
+        if (idx >= deliver) break;
+        if (idx++ < ign) continue;
+        picks.push_back(Pick{&b, dst});
+        if (sizes && nbuf < sizes_cap) sizes[nbuf] = b.len;
+        dst += b.len;
+        r.len += b.len;
+        ++nbuf;
+        ++r.n_buffers;
+      }
+  }
+  if (total) *total = dst;
+  if (total_buffers) *total_buffers = nbuf;
+  if (dst > cap || nbuf > sizes_cap || (nbuf && !sizes) || (dst && !out))
+    return fail(CLG_E_CAPACITY, "in-flight replay needs %llu bytes / %llu sizes (cap %llu / %llu)",
+                (unsigned long long)dst, (unsigned long long)nbuf, (unsigned long long)cap,
+                (unsigned long long)sizes_cap);
+  std::vector<clg::GatherPiece> pieces;
+  const uint32_t C = e->C();
+  for (const Pick& p : picks)
+    for (size_t s = 0; s < p.b->segs.size(); ++s) {
+      const uint32_t o = uint32_t(s) * C;
+      pieces.push_back(clg::GatherPiece{e->seg_addr(p.b->segs[s]), p.dst + o, std::min(C, p.b->len - o), 0});
+    }
+  CHK(e->flush());
+  return e->run_gather(pieces, dst, out, out_kind, "ifl_gather");
 }
 
 int clg_kernel_stats(clg_engine* e, clg_kernel_stat* out, uint32_t cap, uint32_t* n) {

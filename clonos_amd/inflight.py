@@ -1,0 +1,180 @@
+"""In-flight (data) log on the engine: host-side mirror of the reference's InFlightLog.
+
+Reference (I/ = flink-runtime/src/main/java/org/apache/flink/runtime/inflightlogging/):
+  InFlightLog                          I/InFlightLog.java:32-55
+  InMemorySubpartitionInFlightLogger   I/InMemorySubpartitionInFlightLogger.java:28-207
+    log(buffer, epochID, isFinished)   :44-48
+    notifyCheckpointComplete(cp)       :51-70
+    getInFlightIterator(epoch, ignore) :73-82   (ReplayIterator :107-201)
+    close()                            :90-94
+
+The buffers live in HBM (the engine's segment pool); replays of many subpartitions are one
+batched gather on the GPU (clg_ifl_replay_batch).  The Java refcount bookkeeping
+(retainBuffer / recycleBuffer) stays on the Java side: the engine owns the bytes until the
+epoch is truncated or the log is closed.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import ClonosError, check, lib
+
+
+class InFlightReplay:
+    """Result of one replay request: the buffers getInFlightIterator(start, ignore) yields.
+
+    `status` is CLG_OK, CLG_E_EPOCH_GAP (the reference's iterator throws after the buffers
+    listed here) or a request error.  `remaining` is numberRemaining() right after the skip."""
+
+    def __init__(self, status: int, buffers: List[bytes], remaining: int):
+        self.status = status
+        self.buffers = buffers
+        self.remaining = remaining
+
+
+class InFlightLogIterator:
+    """ReplayIterator (:107-201) over a replay already gathered from HBM: next / hasNext /
+    peekNext / numberRemaining; raises where the reference's iterator throws (an epoch gap)."""
+
+    def __init__(self, rep: InFlightReplay, start_epoch: int):
+        self._rep = rep
+        self._i = 0
+        self._left = rep.remaining
+        self._epoch = start_epoch
+
+    def has_next(self) -> bool:
+        if self._i < len(self._rep.buffers):
+            return True
+        if self._rep.status == _lib.CLG_E_EPOCH_GAP:
+            raise ClonosError(_lib.CLG_E_EPOCH_GAP, "in-flight log epoch gap (ReplayIterator :133)")
+        return False
+
+    def next(self) -> bytes:
+        if not self.has_next():
+            raise StopIteration
+        b = self._rep.buffers[self._i]
+        self._i += 1
+        self._left -= 1
+        return b
+
+    def peek_next(self) -> bytes:
+        if not self.has_next():
+            raise StopIteration
+        return self._rep.buffers[self._i]
+
+    def number_remaining(self) -> int:
+        return self._left
+
+    def __iter__(self):
+        while self.has_next():
+            yield self.next()
+
+
+class InFlightLog:
+    """InMemorySubpartitionInFlightLogger over the engine's HBM pool."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        h = C.c_uint32()
+        check(lib.clg_ifl_open(engine.handle, C.byref(h)))
+        self.handle = h.value
+
+    def log(self, buffer: bytes, epoch_id: int, is_finished: bool = True) -> None:  # :44-48
+        log_batch(self.engine, [(self, epoch_id, buffer)])
+
+    def notify_checkpoint_complete(self, checkpoint_id: int) -> None:  # :51-70
+        check(lib.clg_ifl_notify_checkpoint_complete(self.engine.handle, self.handle, checkpoint_id))
+
+    def epochs(self) -> List[Tuple[int, int]]:
+        """[(epochID, buffers)] ascending (the slicedLog map)."""
+        n = C.c_uint32()
+        check(lib.clg_ifl_state(self.engine.handle, self.handle, None, None, 0, C.byref(n)))
+        ids = np.zeros(max(n.value, 1), np.int64)
+        cnt = np.zeros(max(n.value, 1), np.uint32)
+        check(lib.clg_ifl_state(self.engine.handle, self.handle, ids.ctypes.data, cnt.ctypes.data, n.value,
+                                C.byref(n)))
+        return [(int(ids[i]), int(cnt[i])) for i in range(n.value)]
+
+    def replay(self, start_epoch: int, ignore_buffers: int = 0) -> InFlightReplay:
+        return replay_batch(self.engine, [(self, start_epoch, ignore_buffers)])[0]
+
+    def get_in_flight_iterator(self, epoch_id: int, ignore_buffers: int = 0) -> InFlightLogIterator:  # :73-82
+        rep = self.replay(epoch_id, ignore_buffers)
+        if rep.status not in (_lib.CLG_OK, _lib.CLG_E_EPOCH_GAP):
+            check(rep.status)
+        if rep.status == _lib.CLG_E_EPOCH_GAP and not rep.buffers and ignore_buffers:
+            check(rep.status)  # the skip loop itself crossed the gap (:78-79)
+        return InFlightLogIterator(rep, epoch_id)
+
+    def close(self) -> None:  # :90-94
+        if self.handle is not None:
+            check(lib.clg_ifl_close(self.engine.handle, self.handle))
+            self.handle = None
+
+
+def log_batch(engine, items: Sequence[Tuple[InFlightLog, int, bytes]]) -> None:
+    """log() for many (log, epoch, buffer) at once: one upload + one scatter kernel."""
+    n = len(items)
+    if n == 0:
+        return
+    h = np.array([it[0].handle for it in items], np.uint32)
+    ep = np.array([it[1] for it in items], np.int64)
+    lens = np.array([len(it[2]) for it in items], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(bytes(it[2]) for it in items) or b"\0", np.uint8)
+    check(lib.clg_ifl_log_batch(engine.handle, h.ctypes.data, ep.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                n, blob.ctypes.data, _lib.CLG_MEM_HOST))
+
+
+def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=None, sizes=None, cap: int = 0):
+    """One batched replay.  Returns (status, res array, out, sizes, total, total_buffers);
+    out / sizes are host numpy arrays unless given; an int `out` is a device pointer
+    (hipMalloc on the engine's device) of `cap` bytes, written in place."""
+    n = len(reqs)
+    creq = (_lib.IflReplayReq * max(n, 1))()
+    for i, (f, start, ign) in enumerate(reqs):
+        creq[i].ifl = f.handle
+        creq[i].start_epoch = start
+        creq[i].ignore_buffers = ign
+    cres = (_lib.IflReplayRes * max(n, 1))()
+    total, nbuf = C.c_uint64(), C.c_uint64()
+    # sizing pass: capacity 0 reports the totals without gathering
+    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, 0,
+                                  C.byref(total), C.byref(nbuf))
+    if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+        check(st)
+    kind = _lib.CLG_MEM_HOST
+    if out is None:
+        out = np.zeros(max(total.value, 1), np.uint8)
+        out_ptr, cap = out.ctypes.data, out.size
+    elif isinstance(out, np.ndarray):
+        out_ptr, cap = out.ctypes.data, out.nbytes
+    else:  # device pointer
+        out_ptr, kind = int(out), _lib.CLG_MEM_DEVICE
+    if sizes is None:
+        sizes = np.zeros(max(nbuf.value, 1), np.uint32)
+    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, out_ptr, cap, kind, sizes.ctypes.data, sizes.size,
+                                  C.byref(total), C.byref(nbuf))
+    return st, cres, out, sizes, total.value, nbuf.value
+
+
+def replay_batch(engine, reqs: Sequence[Tuple[InFlightLog, int, int]]) -> List[InFlightReplay]:
+    """getInFlightIterator + drain for many subpartitions: one gather kernel for all of them."""
+    st, cres, out, sizes, _, _ = replay_batch_raw(engine, reqs)
+    check(st)
+    reps = []
+    for i in range(len(reqs)):
+        r = cres[i]
+        bufs, o = [], r.out_off
+        for k in range(r.n_buffers):
+            sz = int(sizes[r.sizes_off + k])
+            bufs.append(out[o:o + sz].tobytes())
+            o += sz
+        reps.append(InFlightReplay(r.status, bufs, r.remaining))
+    return reps

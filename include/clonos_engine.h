@@ -50,8 +50,10 @@ enum {
   CLG_E_STATE = -12,             /* inconsistent log state (index out of bounds) */
   CLG_E_DEVICE = -13,            /* HIP runtime error */
   CLG_E_NO_LOG = -14,            /* unknown / closed log handle */
-  CLG_E_NOT_BUFFER_BUILT = -15   /* subpartition recovery buffer holds another determinant
+  CLG_E_NOT_BUFFER_BUILT = -15,  /* subpartition recovery buffer holds another determinant
                                     (RuntimeException, ReplayingState.java:172-177) */
+  CLG_E_EPOCH_GAP = -16          /* in-flight replay reaches an epoch with no buffers (the reference's
+                                    ReplayIterator NPEs at logToReplay.get(++currentKey), :133) */
 };
 
 enum { CLG_MEM_HOST = 0, CLG_MEM_DEVICE = 1 };
@@ -389,6 +391,55 @@ typedef struct clg_replay_out {
 } clg_replay_out;
 
 int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out);
+
+/* ---- in-flight (data) log (RT/inflightlogging/, I/ below) -------------------------------------
+ * InFlightLog I/InFlightLog.java:32-55, implementation InMemorySubpartitionInFlightLogger
+ * I/InMemorySubpartitionInFlightLogger.java:28-207: per subpartition, the data buffers sent in
+ * each epoch, kept in HBM (the engine's segment pool; a buffer spans ceil(len / segment_bytes)
+ * segments) until a checkpoint completes.  The Java side keeps refcounts; the engine owns
+ * the bytes. */
+int clg_ifl_open(clg_engine* e, uint32_t* handle);
+/* close() :90-94: all buffers released. */
+int clg_ifl_close(clg_engine* e, uint32_t ifl);
+/* log(buffer, epochID, isFinished) :44-48, batched: buffer i = bytes[off[i], off[i] + len[i])
+ * appended to ifl[i] in epoch[i], in order (host or device input). */
+int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, const uint64_t* off,
+                      const uint32_t* len, uint32_t n, const uint8_t* bytes, uint32_t in_kind);
+/* notifyCheckpointComplete :51-70: epochs < checkpoint_id are dropped, their segments freed. */
+int clg_ifl_notify_checkpoint_complete(clg_engine* e, uint32_t ifl, int64_t checkpoint_id);
+/* Epochs and buffer counts (ascending epoch), for parity tests. */
+int clg_ifl_state(clg_engine* e, uint32_t ifl, int64_t* epoch_ids, uint32_t* n_buffers, uint32_t cap,
+                  uint32_t* n_epochs);
+/* getInFlightIterator(startEpochID, ignoreBuffers) :73-82 + draining the ReplayIterator
+ * (:107-201), batched: for request i the buffers the iterator yields after skipping
+ * ignore_buffers are gathered by one kernel, back to back in request order, into `out`
+ * at out_off (len bytes); their sizes go to sizes[sizes_off ...] (n_buffers entries).
+ * remaining = the iterator's numberRemaining() after the skip: the buffers of every epoch
+ * >= start when start itself holds buffers, else 0 (:121-127: a start epoch that is absent,
+ * e.g. already truncated, yields nothing).  An epoch without buffers between start and
+ * the last epoch (K buffers before it): next() advances past each returned buffer (:156)
+ * and throws at the gap (:133), so the K-th buffer is never delivered -- buffers
+ * [ignore_buffers, K-1) are gathered and status is CLG_E_EPOCH_GAP.  Without a gap,
+ * ignore_buffers beyond the buffers available (or any skip when start is absent) is the
+ * iterator's NoSuchElement/NPE: CLG_E_STATE, nothing gathered.  CLG_E_CAPACITY (bytes or sizes): *total /
+ * *total_buffers hold the required sizes and no bytes are gathered. */
+typedef struct clg_ifl_replay_req {
+  uint32_t ifl;
+  uint32_t ignore_buffers;
+  int64_t start_epoch;
+} clg_ifl_replay_req;
+typedef struct clg_ifl_replay_res {
+  int32_t status;
+  uint32_t n_buffers;
+  uint32_t remaining;
+  uint32_t reserved;
+  uint64_t out_off;
+  uint64_t len;
+  uint64_t sizes_off;
+} clg_ifl_replay_res;
+int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t n, clg_ifl_replay_res* res,
+                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, uint64_t sizes_cap,
+                         uint64_t* total, uint64_t* total_buffers);
 
 /* ---- instrumentation ---------------------------------------------------------------- */
 typedef struct clg_kernel_stat {

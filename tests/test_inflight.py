@@ -1,0 +1,73 @@
+"""CPU: the in-flight log oracle (oracle/inflight_ref.py) against the reference's own
+InFlightLogTest (flink-runtime/src/test/java/org/apache/flink/runtime/inflightlogging/
+InFlightLogTest.java) and hand-derived iterator cases; the host mirror's API surface."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from inflight_ref import InFlightLogRef, IteratorNPE  # noqa: E402
+import pytest  # noqa: E402
+
+
+def populate(log):  # InFlightLogTest.populate: 3 epochs x (5 + 1) buffers of 64 B
+    for epoch in range(3):
+        for i in range(6):
+            log.log(bytes([epoch, i]) * 32, epoch)
+
+
+def test_iterator_count():  # InFlightLogTest.iteratorCountTest
+    log = InFlightLogRef()
+    populate(log)
+    assert log.get_in_flight_iterator(0, 0).number_remaining() == 15 + 3
+
+
+def test_checkpoint_complete_then_iterate_from_truncated_epoch():
+    # InFlightLogTest.logCheckpointCompleteTest / logIterationTest assert 12 remaining and
+    # hasNext() == true here, but InMemorySubpartitionInFlightLogger.ReplayIterator
+    # (:121-127) builds an empty iterator when the start epoch is not a key: the code
+    # yields 0 / false, and that code is what the engine follows.
+    log = InFlightLogRef()
+    populate(log)
+    log.notify_checkpoint_complete(1)
+    assert sorted(log.sliced) == [1, 2]
+    it = log.get_in_flight_iterator(0, 0)
+    assert it.number_remaining() == 0 and not it.has_next()
+    it = log.get_in_flight_iterator(1, 0)
+    assert it.number_remaining() == 12 and it.has_next()
+
+
+def test_replay_order_and_skip():
+    log = InFlightLogRef()
+    populate(log)
+    st, bufs, rem = log.replay(1, 4)
+    assert st == "ok" and rem == 12 - 4
+    assert bufs == [bytes([1, i]) * 32 for i in range(4, 6)] + [bytes([2, i]) * 32 for i in range(6)]
+    assert log.replay(2, 6) == ("ok", [], 0)
+    assert log.replay(2, 7)[0] == "state"
+    assert log.replay(5, 0) == ("ok", [], 0)
+    assert log.replay(5, 1)[0] == "state"
+
+
+def test_epoch_gap_loses_last_buffer_before_it():
+    log = InFlightLogRef()
+    for e, n in ((0, 3), (2, 2)):
+        for i in range(n):
+            log.log(bytes([e, i]), e)
+    st, bufs, rem = log.replay(0, 0)
+    assert st == "gap" and bufs == [bytes([0, 0]), bytes([0, 1])] and rem == 5
+    st, bufs, rem = log.replay(0, 3)  # the skip loop reaches the gap
+    assert st == "gap" and bufs == [] and rem == 0
+    assert log.replay(2, 0) == ("ok", [bytes([2, 0]), bytes([2, 1])], 2)
+    it = log.get_in_flight_iterator(0, 0)
+    it.next()
+    it.next()
+    with pytest.raises(IteratorNPE):  # fetches buffer 2, then advances into the gap
+        it.next()
+
+
+def test_host_mirror_exports():
+    from clonos_amd import inflight
+    for name in ("InFlightLog", "InFlightLogIterator", "log_batch", "replay_batch", "replay_batch_raw"):
+        assert hasattr(inflight, name)
