@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config3", action="store_true", help="skip the secondary config-3 decode measurement")
+    ap.add_argument("--no-inflight", action="store_true", help="skip the secondary in-flight log replay measurement")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated per-kernel pass (profiling runs)")
     return ap.parse_args()
 
@@ -213,6 +214,9 @@ def main():
         del o_off, o_tag, o_v0, o_w, o_slice
         torch.cuda.empty_cache()
         c3 = config3(args, torch, dev)
+    ifl = None
+    if rank == 0 and world == 1 and not args.no_inflight:
+        ifl = inflight_replay(args, torch, dev)
 
     if rank == 0:
         line = {
@@ -247,11 +251,71 @@ def main():
             "roofline_isolated": roof_iso,
             "cpu_baseline": cpu,
             "config3": c3,
+            "inflight_replay": ifl,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def inflight_replay(args, torch, dev, n_sub=256, n_epochs=4, per_epoch=8, buf_bytes=32768, steps=5):
+    """in-flight (data) log replay.  n_sub subpartition logs, each holding
+    per_epoch network buffers (32 KiB, the default memory segment) per epoch in HBM; one step
+    = getInFlightIterator(1, 1) + drain for every subpartition (a recovering downstream
+    replays from epoch 1 after skipping one buffer), gathered into one device buffer by one
+    kernel.  Algorithmic bytes: 2 x replayed bytes (read + packed write)."""
+    import time as _t
+    from clonos_amd import Engine, inflight as IF
+    rng = np.random.default_rng(0xC105_0F40)
+    seg = 16384
+    segs = n_sub * n_epochs * per_epoch * ((buf_bytes + seg - 1) // seg)
+    eng = Engine(segment_bytes=seg, pool_segments=segs + 64, timing=True)
+    logs = [IF.InFlightLog(eng) for _ in range(n_sub)]
+    pat = rng.integers(0, 256, buf_bytes + 4096, dtype=np.uint8).tobytes()
+    for e in range(n_epochs):  # one batched log() call per epoch; ragged tail buffers
+        items = []
+        for i, f in enumerate(logs):
+            for k in range(per_epoch):
+                n = buf_bytes if k < per_epoch - 1 else 1 + (i * 977 + e * 131) % buf_bytes
+                o = (i * 31 + k * 7 + e) % 4096
+                items.append((f, e, pat[o:o + n]))
+        IF.log_batch(eng, items)
+    reqs = [(f, 1, 1) for f in logs]
+    st, cres, _, _, total, nbuf = IF.replay_batch_raw(eng, reqs, out=np.zeros(1, np.uint8))
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        st, *_ = IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total)
+        assert st == 0
+    torch.cuda.synchronize()
+    eng.kernel_stats_reset()
+    t0 = _t.perf_counter()
+    for _ in range(steps):
+        IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total)
+    torch.cuda.synchronize()
+    el = (_t.perf_counter() - t0) / steps
+    k = eng.kernel_stats().get("ifl_gather", {})
+    kms = k["ms"] / k["launches"] if k.get("launches") else None
+    # spot check against the logged bytes: the first replayed buffer of subpartition 0
+    first = pat[(0 * 31 + 1 * 7 + 1) % 4096:][:buf_bytes]
+    assert out[:buf_bytes].cpu().numpy().tobytes() == first
+    eng.close()
+    res = {"workload": f"in-flight log replay: {n_sub} subpartitions x {n_epochs} epochs x {per_epoch} buffers "
+                       f"(32 KiB), replay from epoch 1 skipping 1", "replayed_bytes": total, "buffers": nbuf,
+           "ms_per_step": round(el * 1e3, 4), "kernel_avg_ms": round(kms, 5) if kms else None,
+           "kernel_gbs": round(2 * total / (kms * 1e-3) / 1e9, 1) if kms else None,
+           "hbm_frac": round(2 * total / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if kms else None}
+    if not args.no_cpu_baseline:  # host memcpy of the same buffers (the Java drain copies nothing;
+        bufs = [np.frombuffer(b, np.uint8) for (_, _, b) in items]  # this is the byte-move floor)
+        t0 = _t.perf_counter()
+        reps = 0
+        while _t.perf_counter() - t0 < 2.0 or reps == 0:
+            np.concatenate(bufs)
+            reps += 1
+        dt = (_t.perf_counter() - t0) / reps
+        res["cpu_baseline"] = {"value": round(sum(b.size for b in bufs) / dt / 1e9, 2), "unit": "GB/s", "cores": 1,
+                               "kind": "port", "sample": f"memcpy gather of one epoch's {len(bufs)} buffers, x{reps}"}
+    return res
 
 
 def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5):

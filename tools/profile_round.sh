@@ -11,8 +11,8 @@ OUT=${1:-gpurun_out/round}
 mkdir -p "$OUT"
 timeout -k 10 420 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-isolated > "$OUT/trace.log" 2>&1 &&
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-inflight --no-isolated > "$OUT/trace.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-isolated > "$OUT/fetch.log" 2>&1 &&
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-inflight --no-isolated > "$OUT/fetch.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-isolated > "$OUT/write.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 --no-inflight --no-isolated > "$OUT/write.log" 2>&1
