@@ -320,3 +320,58 @@ JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jsho
   free(ids), free(sbase), free(cnt), free(sst), free(soff), free(stg), free(ents);
   return s;
 }
+
+/* ---- in-flight (data) log: InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207) ---- */
+JNIEXPORT jint JNICALL FN(nIflOpen)(JNIEnv* env, jclass cls, jlong e, jintArray out) {
+  (void)cls;
+  uint32_t h = 0;
+  int s = clg_ifl_open(ENG(e), &h);
+  put_int(env, out, (jint)h);
+  return s;
+}
+
+JNIEXPORT jint JNICALL FN(nIflClose)(JNIEnv* env, jclass cls, jlong e, jint ifl) {
+  (void)env;
+  (void)cls;
+  return clg_ifl_close(ENG(e), (uint32_t)ifl);
+}
+
+/* log(buffer, epochID, isFinished) :44-48 -- the buffer's readable bytes, copied to HBM. */
+JNIEXPORT jint JNICALL FN(nIflLog)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong epoch, jobject buf, jint off,
+                                   jint len) {
+  (void)cls;
+  const uint8_t* p = addr(env, buf, off);
+  if (!p) return CLG_E_INVALID_ARG;
+  uint32_t h = (uint32_t)ifl;
+  int64_t ep = epoch;
+  uint64_t o = 0;
+  uint32_t n = (uint32_t)len;
+  return clg_ifl_log_batch(ENG(e), &h, &ep, &o, &n, 1, p, CLG_MEM_HOST);
+}
+
+JNIEXPORT jint JNICALL FN(nIflNotifyCheckpointComplete)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong cp) {
+  (void)env;
+  (void)cls;
+  return clg_ifl_notify_checkpoint_complete(ENG(e), (uint32_t)ifl, cp);
+}
+
+/* getInFlightIterator(epoch, ignoreBuffers) :73-82 drained into `out` (buffers back to back)
+ * and `sizes` (i32 per buffer).  res = {status, buffers, numberRemaining, bytes, required
+ * bytes, required buffers}; the call's status is CLG_E_CAPACITY when out/sizes are short. */
+JNIEXPORT jint JNICALL FN(nIflReplay)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong start, jint ignore,
+                                      jobject out, jobject sizes, jlongArray res) {
+  (void)cls;
+  clg_ifl_replay_req q;
+  memset(&q, 0, sizeof q);
+  q.ifl = (uint32_t)ifl;
+  q.ignore_buffers = (uint32_t)ignore;
+  q.start_epoch = start;
+  clg_ifl_replay_res r;
+  memset(&r, 0, sizeof r);
+  uint64_t total = 0, nbuf = 0;
+  int s = clg_ifl_replay_batch(ENG(e), &q, 1, &r, addr(env, out, 0), cap(env, out), CLG_MEM_HOST,
+                               (uint32_t*)addr(env, sizes, 0), cap(env, sizes) / 4u, &total, &nbuf);
+  jlong w[6] = {r.status, (jlong)r.n_buffers, (jlong)r.remaining, (jlong)r.len, (jlong)total, (jlong)nbuf};
+  (*env)->SetLongArrayRegion(env, res, 0, 6, w);
+  return s;
+}

@@ -24,6 +24,8 @@ public final class ClonosEngine implements AutoCloseable {
 	public static final int CLG_E_NO_CONSUMER = -8;
 	public static final int CLG_E_NOSPACE = -10;
 	public static final int CLG_E_CAPACITY = -11;
+	public static final int CLG_E_STATE = -12;
+	public static final int CLG_E_EPOCH_GAP = -16;
 
 	private final long handle; // clg_engine*
 
@@ -68,6 +70,9 @@ public final class ClonosEngine implements AutoCloseable {
 				throw new NullPointerException(msg); // :245 / :256 dereference a missing ConsumerOffset
 			case CLG_E_CORRUPT_TAG:
 				throw new IllegalStateException("corrupt determinant array: " + msg);
+			case CLG_E_EPOCH_GAP: // InMemorySubpartitionInFlightLogger.ReplayIterator :133
+			case CLG_E_STATE:
+				throw new NullPointerException(msg);
 			default:
 				throw new IllegalStateException("clonos engine status " + status + ": " + msg);
 		}
@@ -80,6 +85,13 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nLogOpen(long engine, short vertexId, boolean isMain, long irpLower, long irpUpper,
 							   byte subpartition, int[] out);
 	static native int nLogClose(long engine, int log);
+	// in-flight (data) log, InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207)
+	static native int nIflOpen(long engine, int[] out);
+	static native int nIflClose(long engine, int ifl);
+	static native int nIflLog(long engine, int ifl, long epoch, ByteBuffer direct, int off, int len);
+	static native int nIflNotifyCheckpointComplete(long engine, int ifl, long checkpointId);
+	static native int nIflReplay(long engine, int ifl, long startEpoch, int ignoreBuffers, ByteBuffer out,
+		ByteBuffer sizes, long[] res);
 	/** bytes = direct buffer holding encoded records (SimpleDeterminantEncoder.encodeTo). */
 	static native int nAppend(long engine, int log, long epoch, ByteBuffer direct, int off, int len);
 	static native int nUpstreamDelta(long engine, int log, long epoch, int offsetFromEpoch, ByteBuffer direct,

@@ -1,0 +1,165 @@
+/*
+ * InFlightLog over the MI355X engine (C-ABI clg_ifl_*, jni/clonos_jni.c): a drop-in for
+ * InMemorySubpartitionInFlightLogger (InMemorySubpartitionInFlightLogger.java:28-207).
+ * Buffer bytes are copied into HBM on log() and the Java Buffer is recycled at once; a
+ * replay gathers every buffer from the start epoch in one GPU call and hands them out as
+ * Buffers taken from the in-flight buffer pool.  Wiring: InMemoryInFlightLogFactory
+ * returns `new EngineInFlightLog(engine)` instead of the in-memory logger.
+ */
+package org.apache.flink.runtime.inflightlogging;
+
+import org.apache.flink.runtime.causal.engine.ClonosEngine;
+import org.apache.flink.runtime.io.network.buffer.Buffer;
+import org.apache.flink.runtime.io.network.buffer.BufferPool;
+
+import java.io.IOException;
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+
+import static org.apache.flink.runtime.causal.engine.ClonosEngine.*;
+
+public class EngineInFlightLog implements InFlightLog {
+
+	private final ClonosEngine engine;
+	private final int ifl;
+	private BufferPool inFlightBufferPool;
+
+	public EngineInFlightLog(ClonosEngine engine) {
+		this.engine = engine;
+		int[] h = new int[1];
+		check(nIflOpen(engine.handle(), h));
+		this.ifl = h[0];
+	}
+
+	@Override
+	public void registerBufferPool(BufferPool bufferPool) {
+		this.inFlightBufferPool = bufferPool;
+	}
+
+	@Override
+	public synchronized void log(Buffer buffer, long epochID, boolean isFinished) { // :44-48
+		ByteBuffer nio = buffer.getNioBufferReadable();
+		ByteBuffer direct = nio.isDirect() ? nio : ByteBuffer.allocateDirect(nio.remaining()).put(nio.duplicate());
+		int off = nio.isDirect() ? nio.position() : 0;
+		check(nIflLog(engine.handle(), ifl, epochID, direct, off, nio.remaining()));
+	}
+
+	@Override
+	public synchronized void notifyCheckpointComplete(long checkpointId) { // :51-70
+		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
+	}
+
+	@Override
+	public synchronized InFlightLogIterator<Buffer> getInFlightIterator(long startEpochID, int ignoreBuffers) {
+		long[] res = new long[6];
+		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, null, null, res);
+		if (st != CLG_OK && st != CLG_E_CAPACITY) {
+			check(st);
+		}
+		ByteBuffer out = ByteBuffer.allocateDirect((int) Math.max(1, res[4]));
+		ByteBuffer sizes = ByteBuffer.allocateDirect((int) Math.max(4, 4 * res[5])).order(ByteOrder.nativeOrder());
+		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, out, sizes, res));
+		int status = (int) res[0];
+		if (status != CLG_OK && !(status == CLG_E_EPOCH_GAP && res[1] > 0)) {
+			check(status); // the skip loop itself failed (:78-79)
+		}
+		return new Replay(out, sizes, (int) res[1], (int) res[2], startEpochID, status);
+	}
+
+	@Override
+	public void destroyBufferPools() {
+	}
+
+	@Override
+	public synchronized void close() { // :90-94
+		check(nIflClose(engine.handle(), ifl));
+	}
+
+	@Override
+	public BufferPool getInFlightBufferPool() {
+		return inFlightBufferPool;
+	}
+
+	/** The drained ReplayIterator (:107-201): buffers materialised from the gathered bytes. */
+	private final class Replay extends InFlightLogIterator<Buffer> {
+		private final ByteBuffer bytes;
+		private final ByteBuffer sizes;
+		private final int count;
+		private final long epoch;
+		private final int status;
+		private int next;
+		private int left;
+		private int pos;
+
+		Replay(ByteBuffer bytes, ByteBuffer sizes, int count, int remaining, long epoch, int status) {
+			this.bytes = bytes;
+			this.sizes = sizes;
+			this.count = count;
+			this.left = remaining;
+			this.epoch = epoch;
+			this.status = status;
+		}
+
+		@Override
+		public boolean hasNext() {
+			if (next < count) {
+				return true;
+			}
+			if (status == CLG_E_EPOCH_GAP) {
+				check(status);
+			}
+			return false;
+		}
+
+		private Buffer materialise(boolean advance) {
+			int n = sizes.getInt(4 * next);
+			Buffer b;
+			try {
+				b = inFlightBufferPool.requestBufferBlocking();
+			} catch (IOException | InterruptedException e) {
+				throw new RuntimeException(e);
+			}
+			ByteBuffer src = bytes.duplicate();
+			src.position(pos).limit(pos + n);
+			b.getMemorySegment().put(0, src, n);
+			b.setSize(n);
+			if (advance) {
+				pos += n;
+				next++;
+				left--;
+			}
+			return b;
+		}
+
+		@Override
+		public Buffer next() {
+			if (!hasNext()) {
+				throw new java.util.NoSuchElementException();
+			}
+			return materialise(true);
+		}
+
+		@Override
+		public Buffer peekNext() {
+			if (!hasNext()) {
+				throw new java.util.NoSuchElementException();
+			}
+			return materialise(false);
+		}
+
+		@Override
+		public int numberRemaining() {
+			return left;
+		}
+
+		@Override
+		public long getEpoch() {
+			return epoch;
+		}
+
+		@Override
+		public void close() {
+			next = count;
+		}
+	}
+}
