@@ -122,3 +122,27 @@ def test_inflight_device_output_and_capacity():
         # per log: drop the first buffer (ignore_buffers=1)
         exp = b"".join(b"".join([b for (g, ee, b) in items if g is f][1:]) for f in logs)
         assert host == exp
+
+
+def test_inflight_golden_fixture():
+    """The engine replays tests/golden/inflight_ops.json byte for byte (64-B segments, so
+    buffers span several segments)."""
+    import json
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "inflight_ops.json")))
+    with Engine(segment_bytes=d["segment_bytes"], pool_segments=1 << 14) as eng:
+        for c in d["cases"]:
+            logs = [IF.InFlightLog(eng) for _ in range(c["n_sub"])]
+            got = []
+            for op in c["ops"]:
+                if op[0] == "log":
+                    logs[op[1]].log(bytes.fromhex(op[3]), op[2])
+                elif op[0] == "cp":
+                    logs[op[1]].notify_checkpoint_complete(op[2])
+                else:
+                    reps = IF.replay_batch(eng, [(logs[s], st, ign) for s, st, ign in op[1]])
+                    got.append([[{v: k for k, v in STATUS.items()}[r.status], [b.hex() for b in r.buffers],
+                                 r.remaining if r.status != _lib.CLG_E_STATE else None] for r in reps])
+            assert got == c["expect"]
+            for f in logs:
+                f.close()
+        assert eng.pool_stats()[0] == 0

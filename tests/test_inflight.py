@@ -71,3 +71,16 @@ def test_host_mirror_exports():
     from clonos_amd import inflight
     for name in ("InFlightLog", "InFlightLogIterator", "log_batch", "replay_batch", "replay_batch_raw"):
         assert hasattr(inflight, name)
+
+
+def test_golden_fixture_matches_oracle():
+    """tests/golden/inflight_ops.json (committed) == a fresh run of the oracle."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_inflight_golden import run_script
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "inflight_ops.json")))
+    kinds = set()
+    for c in d["cases"]:
+        assert run_script(c["ops"], c["n_sub"]) == c["expect"]
+        kinds |= {r[0] for e in c["expect"] for r in e}
+    assert kinds == {"ok", "state", "gap"}
