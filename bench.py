@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config3", action="store_true", help="skip the secondary config-3 decode measurement")
     ap.add_argument("--no-inflight", action="store_true", help="skip the secondary in-flight log replay measurement")
+    ap.add_argument("--inflight-only", action="store_true",
+                    help="profiling aid: run only the in-flight replay leg and print its JSON object")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated per-kernel pass (profiling runs)")
     return ap.parse_args()
 
@@ -69,6 +71,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from clonos_amd import CausalLogID, Engine, _lib, synth
+
+    if args.inflight_only:
+        print(json.dumps(inflight_replay(args, torch, torch.device("cuda", local))), flush=True)
+        return
 
     # ---------------- synthetic shard (seeded per rank) ----------------
     rng = np.random.default_rng(synth.SEED_CONFIG2 + rank)
