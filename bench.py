@@ -287,17 +287,18 @@ def inflight_replay(args, torch, dev, n_sub=256, n_epochs=4, per_epoch=8, buf_by
                 o = (i * 31 + k * 7 + e) % 4096
                 items.append((f, e, pat[o:o + n]))
         IF.log_batch(eng, items)
-    reqs = [(f, 1, 1) for f in logs]
-    st, cres, _, _, total, nbuf = IF.replay_batch_raw(eng, reqs, out=np.zeros(1, np.uint8))
+    reqs = IF.make_requests([(f, 1, 1) for f in logs])
+    st, cres, _, sizes, total, nbuf = IF.replay_batch_raw(eng, reqs, out=np.zeros(1, np.uint8))
     out = torch.empty(total, dtype=torch.uint8, device=dev)
+    sizes = np.zeros(nbuf, np.uint32)  # caller-sized outputs: one engine call per step
     for _ in range(2):
-        st, *_ = IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total)
+        st, *_ = IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total, sizes=sizes)
         assert st == 0
     torch.cuda.synchronize()
     eng.kernel_stats_reset()
     t0 = _t.perf_counter()
     for _ in range(steps):
-        IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total)
+        IF.replay_batch_raw(eng, reqs, out=out.data_ptr(), cap=total, sizes=sizes)
     torch.cuda.synchronize()
     el = (_t.perf_counter() - t0) / steps
     k = eng.kernel_stats().get("ifl_gather", {})

@@ -110,8 +110,8 @@ class InFlightLog:
             check(rep.status)  # the skip loop itself crossed the gap (:78-79)
         return InFlightLogIterator(rep, epoch_id)
 
-    def close(self) -> None:  # :90-94
-        if self.handle is not None:
+    def close(self) -> None:  # :90-94 (a no-op once the engine itself is closed)
+        if self.handle is not None and self.engine.handle:
             check(lib.clg_ifl_close(self.engine.handle, self.handle))
             self.handle = None
 
@@ -132,23 +132,31 @@ def log_batch(engine, items: Sequence[Tuple[InFlightLog, int, bytes]]) -> None:
                                 n, blob.ctypes.data, _lib.CLG_MEM_HOST))
 
 
-def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=None, sizes=None, cap: int = 0):
-    """One batched replay.  Returns (status, res array, out, sizes, total, total_buffers);
-    out / sizes are host numpy arrays unless given; an int `out` is a device pointer
-    (hipMalloc on the engine's device) of `cap` bytes, written in place."""
-    n = len(reqs)
-    creq = (_lib.IflReplayReq * max(n, 1))()
+def make_requests(reqs: Sequence[Tuple[InFlightLog, int, int]]):
+    """The C request array for (log, start_epoch, ignore_buffers) triples; build it once to
+    replay the same subpartitions repeatedly."""
+    creq = (_lib.IflReplayReq * max(len(reqs), 1))()
     for i, (f, start, ign) in enumerate(reqs):
         creq[i].ifl = f.handle
         creq[i].start_epoch = start
         creq[i].ignore_buffers = ign
+    return creq
+
+
+def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=None, sizes=None, cap: int = 0):
+    """One batched replay.  Returns (status, res array, out, sizes, total, total_buffers);
+    out / sizes are host numpy arrays unless given; an int `out` is a device pointer
+    (hipMalloc on the engine's device) of `cap` bytes, written in place."""
+    creq = reqs if isinstance(reqs, C.Array) else make_requests(reqs)
+    n = len(creq) if len(reqs) else 0
     cres = (_lib.IflReplayRes * max(n, 1))()
     total, nbuf = C.c_uint64(), C.c_uint64()
-    # sizing pass: capacity 0 reports the totals without gathering
-    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, 0,
-                                  C.byref(total), C.byref(nbuf))
-    if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
-        check(st)
+    if out is None or sizes is None:
+        # sizing pass: capacity 0 reports the totals without gathering
+        st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, 0,
+                                      C.byref(total), C.byref(nbuf))
+        if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+            check(st)
     kind = _lib.CLG_MEM_HOST
     if out is None:
         out = np.zeros(max(total.value, 1), np.uint8)
