@@ -47,14 +47,13 @@ class InFlightLogIterator:
         self._epoch = start_epoch
 
     def has_next(self) -> bool:
-        if self._i < len(self._rep.buffers):
-            return True
-        if self._rep.status == _lib.CLG_E_EPOCH_GAP:
-            raise ClonosError(_lib.CLG_E_EPOCH_GAP, "in-flight log epoch gap (ReplayIterator :133)")
-        return False
+        # at a gap the reference still sees the last buffer before it (:146-149) ...
+        return self._i < len(self._rep.buffers) or self._rep.status == _lib.CLG_E_EPOCH_GAP
 
     def next(self) -> bytes:
-        if not self.has_next():
+        if self._i >= len(self._rep.buffers):
+            if self._rep.status == _lib.CLG_E_EPOCH_GAP:  # ... and next() throws taking it (:156 -> :133)
+                raise ClonosError(_lib.CLG_E_EPOCH_GAP, "in-flight log epoch gap (ReplayIterator :133)")
             raise StopIteration
         b = self._rep.buffers[self._i]
         self._i += 1
@@ -62,14 +61,14 @@ class InFlightLogIterator:
         return b
 
     def peek_next(self) -> bytes:
-        if not self.has_next():
+        if self._i >= len(self._rep.buffers):
             raise StopIteration
         return self._rep.buffers[self._i]
 
     def number_remaining(self) -> int:
         return self._left
 
-    def __iter__(self):
+    def __iter__(self):  # raises ClonosError at an epoch gap, like draining the reference's iterator
         while self.has_next():
             yield self.next()
 

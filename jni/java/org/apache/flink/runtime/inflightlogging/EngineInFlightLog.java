@@ -102,13 +102,8 @@ public class EngineInFlightLog implements InFlightLog {
 
 		@Override
 		public boolean hasNext() {
-			if (next < count) {
-				return true;
-			}
-			if (status == CLG_E_EPOCH_GAP) {
-				check(status);
-			}
-			return false;
+			// at a gap the reference still sees the last buffer before it (:146-149); next() throws (:156 -> :133)
+			return next < count || status == CLG_E_EPOCH_GAP;
 		}
 
 		private Buffer materialise(boolean advance) {
@@ -133,7 +128,8 @@ public class EngineInFlightLog implements InFlightLog {
 
 		@Override
 		public Buffer next() {
-			if (!hasNext()) {
+			if (next >= count) {
+				check(status); // CLG_E_EPOCH_GAP -> the reference's NullPointerException
 				throw new java.util.NoSuchElementException();
 			}
 			return materialise(true);
@@ -141,7 +137,7 @@ public class EngineInFlightLog implements InFlightLog {
 
 		@Override
 		public Buffer peekNext() {
-			if (!hasNext()) {
+			if (next >= count) {
 				throw new java.util.NoSuchElementException();
 			}
 			return materialise(false);

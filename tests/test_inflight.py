@@ -84,3 +84,37 @@ def test_golden_fixture_matches_oracle():
         assert run_script(c["ops"], c["n_sub"]) == c["expect"]
         kinds |= {r[0] for e in c["expect"] for r in e}
     assert kinds == {"ok", "state", "gap"}
+
+
+def test_host_iterator_mirrors_reference_iterator():
+    """clonos_amd.inflight.InFlightLogIterator over a replay result behaves like the
+    oracle's ReplayIterator: same buffers, numberRemaining, and the throw at a gap."""
+    from clonos_amd import ClonosError, _lib
+    from clonos_amd.inflight import InFlightLogIterator, InFlightReplay
+    log = InFlightLogRef()
+    for e, n in ((0, 3), (1, 2), (3, 2)):
+        for i in range(n):
+            log.log(bytes([e, i]), e)
+    code = {"ok": _lib.CLG_OK, "gap": _lib.CLG_E_EPOCH_GAP}
+    for start, ign in ((0, 0), (0, 2), (3, 0), (3, 1)):
+        st, bufs, rem = log.replay(start, ign)
+        mine = InFlightLogIterator(InFlightReplay(code[st], bufs, rem), start)
+        ref = log.get_in_flight_iterator(start, ign)
+        while True:
+            assert mine.number_remaining() == ref.number_remaining()
+            try:
+                has = ref.has_next()
+            except IteratorNPE:
+                with pytest.raises(ClonosError):
+                    mine.has_next()
+                break
+            assert mine.has_next() == has
+            if not has:
+                break
+            try:
+                want = ref.next()
+            except IteratorNPE:  # the reference loses this buffer; the engine never hands it out
+                with pytest.raises(ClonosError):
+                    mine.next()
+                break
+            assert mine.next() == want
