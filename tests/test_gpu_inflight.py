@@ -146,3 +146,33 @@ def test_inflight_golden_fixture():
             for f in logs:
                 f.close()
         assert eng.pool_stats()[0] == 0
+
+
+def test_inflight_log_from_device_memory():
+    """clg_ifl_log_batch with CLG_MEM_DEVICE input (a buffer already in HBM, e.g. the
+    network stack's output) == the same buffers logged from host memory."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    rng = np.random.default_rng(11)
+    bufs = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in (0, 1, 16383, 16384, 16385, 40000, 7)]
+    blob = np.frombuffer(b"".join(bufs), np.uint8).copy()
+    lens = np.array([len(b) for b in bufs], np.uint32)
+    offs = np.zeros(len(bufs), np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    with Engine(segment_bytes=16384, pool_segments=256) as eng:
+        f = IF.InFlightLog(eng)
+        dptr = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(dptr), ctypes.c_size_t(blob.size)) == 0
+        try:
+            assert hip.hipMemcpy(dptr, ctypes.c_void_p(blob.ctypes.data), ctypes.c_size_t(blob.size), 1) == 0
+            h = np.full(len(bufs), f.handle, np.uint32)
+            ep = np.array([0, 0, 0, 1, 1, 2, 2], np.int64)
+            _lib.check(_lib.lib.clg_ifl_log_batch(eng.handle, h.ctypes.data, ep.ctypes.data, offs.ctypes.data,
+                                                  lens.ctypes.data, len(bufs), dptr.value, _lib.CLG_MEM_DEVICE))
+        finally:
+            hip.hipFree(dptr)
+        assert f.epochs() == [(0, 3), (1, 2), (2, 2)]
+        rep = f.replay(0, 0)
+        assert rep.status == _lib.CLG_OK and rep.buffers == bufs and rep.remaining == len(bufs)
+        f.close()
+        assert eng.pool_stats()[0] == 0
