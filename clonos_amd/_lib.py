@@ -211,7 +211,7 @@ class IflReplayReq(C.Structure):
 class IflReplayRes(C.Structure):
     _fields_ = [
         ("status", C.c_int32), ("n_buffers", C.c_uint32), ("remaining", C.c_uint32), ("reserved", C.c_uint32),
-        ("out_off", C.c_uint64), ("len", C.c_uint64), ("sizes_off", C.c_uint64),
+        ("out_off", C.c_uint64), ("len", C.c_uint64), ("sizes_off", C.c_uint64), ("end_epoch", C.c_int64),
     ]
 
 
@@ -279,8 +279,8 @@ def _load() -> C.CDLL:
         "clg_ifl_log_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P, C.c_uint32]),
         "clg_ifl_notify_checkpoint_complete": (C.c_int, [P, C.c_uint32, C.c_int64]),
         "clg_ifl_state": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32, u32p]),
-        "clg_ifl_replay_batch": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, C.c_uint64, u64p,
-                                           u64p]),
+        "clg_ifl_replay_batch": (C.c_int, [P, P, C.c_uint32, P, P, C.c_uint64, C.c_uint32, P, P, C.c_uint64,
+                                           u64p, u64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -41,30 +41,42 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
 
 
+def _compile_cmd(src: str, obj: str) -> list:
+    return [
+        hipcc(),
+        "-x", "hip",
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-Wall",
+        "-Wno-unused-function",
+        "-Wno-unused-value",
+        "-I", os.path.join(ROOT, "include"),
+        "-c", src,
+        "-o", obj,
+    ]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every source whose object is older than it or any header (all of them with
+    force), in parallel, then link."""
     if not force and not needs_build():
         return LIB
-    objs = []
+    hdr_t = max(os.path.getmtime(h) for h in HEADERS)
+    objs, procs = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, os.path.basename(src) + ".o")
-        cmd = [
-            hipcc(),
-            "-x", "hip" if src.endswith(".hip") else "hip",
-            f"--offload-arch={ARCH}",
-            "-O3",
-            "-std=c++17",
-            "-fPIC",
-            "-Wall",
-            "-Wno-unused-function",
-            "-Wno-unused-value",
-            "-I", os.path.join(ROOT, "include"),
-            "-c", src,
-            "-o", obj,
-        ]
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(src)):
+            continue
+        cmd = _compile_cmd(src, obj)
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
+        procs.append((src, subprocess.Popen(cmd)))
+    bad = [src for src, p in procs if p.wait() != 0]
+    if bad:
+        raise RuntimeError(f"hipcc failed for {bad}")
     link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
     if verbose:
         print(" ".join(link), flush=True)

@@ -379,10 +379,11 @@ struct clg_engine {
     const int32_t cur = l->writer - es->offset;
     const int32_t num_new = (off_from_epoch + int32_t(n)) - cur;
     if (num_new > 0) {
+      // :136-137 add components before delta.readerIndex(<0) throws (:143): capacity grows
+      CHK(ensure_space(*l, num_new));
       if (num_new > int32_t(n))
         return fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d", off_from_epoch,
                     n, cur);
-      CHK(ensure_space(*l, num_new));
       write_pending(*l, d + (n - uint32_t(num_new)), uint32_t(num_new));
     }
     return CLG_OK;
@@ -410,12 +411,12 @@ struct clg_engine {
       const int32_t cur = l->writer - es->offset;
       const int32_t num_new = (r[i].offset_from_epoch + int32_t(r[i].len)) - cur;
       if (num_new <= 0) continue;
+      if ((r[i].status = ensure_space(*l, num_new)) != CLG_OK) continue;  // before the gap check (:136-143)
       if (num_new > int32_t(r[i].len)) {
         r[i].status = fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d",
                            r[i].offset_from_epoch, r[i].len, cur);
         continue;
       }
-      if ((r[i].status = ensure_space(*l, num_new)) != CLG_OK) continue;
       int32_t p = l->writer;
       uint64_t src = r[i].src_off + (r[i].len - uint32_t(num_new));
       uint32_t left = uint32_t(num_new);
@@ -2075,8 +2076,8 @@ int clg_ifl_state(clg_engine* e, uint32_t h, int64_t* ids, uint32_t* nb, uint32_
 // contiguous epochs from `start`; a missing key throws inside next() right after the last
 // buffer before it was taken (:156 -> :133), so that buffer is lost to the caller.
 int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t n, clg_ifl_replay_res* res,
-                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, uint64_t sizes_cap,
-                         uint64_t* total, uint64_t* total_buffers) {
+                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, int64_t* epochs,
+                         uint64_t sizes_cap, uint64_t* total, uint64_t* total_buffers) {
   ENGINE_GUARD(e);
   if (n && (!reqs || !res)) return fail(CLG_E_INVALID_ARG, "null argument");
   if (out_kind != CLG_MEM_HOST && out_kind != CLG_MEM_DEVICE) return fail(CLG_E_INVALID_ARG, "bad out_kind");
@@ -2088,17 +2089,17 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
   uint64_t dst = 0, nbuf = 0;
   for (uint32_t i = 0; i < n; ++i) {
     clg_ifl_replay_res& r = res[i];
-    r = clg_ifl_replay_res{CLG_OK, 0, 0, 0, dst, 0, nbuf};
+    const int64_t start = reqs[i].start_epoch;
+    r = clg_ifl_replay_res{CLG_OK, 0, 0, 0, dst, 0, nbuf, start};
     InFlight* f;
     int st = ifl_get(e, reqs[i].ifl, &f);
     if (st != CLG_OK) {
       r.status = st;
       continue;
     }
-    const int64_t start = reqs[i].start_epoch;
     const uint64_t ign = reqs[i].ignore_buffers;
     auto it = f->epochs.find(start);
-    if (it == f->epochs.end()) {  // :121-127 -- currentIterator == null, nothing left
+    if (it == f->epochs.end()) {  // :121-127 -- currentIterator == null, nothing left, currentKey = start
       if (ign) r.status = fail(CLG_E_STATE, "skip of %llu buffers on an empty iterator", (unsigned long long)ign);
       continue;
     }
@@ -2115,22 +2116,26 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
       }
     }
     const uint64_t deliver = gap ? k - 1 : k;  // buffers next() returns
-    if (gap) {
-      r.status = CLG_E_EPOCH_GAP;
-      if (ign >= k) continue;  // the skip loop itself throws at the gap (:78-79)
-    } else if (ign > deliver) {
-      r.status = fail(CLG_E_STATE, "skip of %llu buffers past the %llu logged", (unsigned long long)ign,
+    if (ign > deliver) {  // the skip loop inside getInFlightIterator throws (:78-79)
+      r.status = fail(CLG_E_STATE, "skip of %llu buffers past the %llu the iterator yields", (unsigned long long)ign,
                       (unsigned long long)deliver);
       continue;
     }
-    r.remaining = uint32_t(tail >= ign ? tail - ign : 0);
+    if (gap) r.status = CLG_E_EPOCH_GAP;  // the next() after the last delivered buffer throws (:156 -> :133)
+    // after the last successful next() the iterator sits on the last contiguous epoch: that
+    // epoch holds the final buffer (no gap) or the K-th buffer the gap swallows
+    r.end_epoch = expect - 1;
+    r.remaining = uint32_t(tail - ign);
     uint64_t idx = 0;
     for (auto jt = it; jt != f->epochs.end() && idx < deliver; ++jt)
       for (const IflBuf& b : jt->second) {
         if (idx >= deliver) break;
         if (idx++ < ign) continue;
         picks.push_back(Pick{&b, dst});
-        if (sizes && nbuf < sizes_cap) sizes[nbuf] = b.len;
+        if (nbuf < sizes_cap) {
+          if (sizes) sizes[nbuf] = b.len;
+          if (epochs) epochs[nbuf] = jt->first;  // getEpoch() before this next()
+        }
         dst += b.len;
         r.len += b.len;
         ++nbuf;

@@ -28,23 +28,30 @@ class InFlightReplay:
     """Result of one replay request: the buffers getInFlightIterator(start, ignore) yields.
 
     `status` is CLG_OK, CLG_E_EPOCH_GAP (the reference's iterator throws after the buffers
-    listed here) or a request error.  `remaining` is numberRemaining() right after the skip."""
+    listed here) or a request error.  `remaining` is numberRemaining() right after the skip.
+    `epochs[i]` is getEpoch() right before the next() that returns buffers[i] (the epoch
+    PipelinedSubpartition.getReplayedBufferUnsafe :306-320 stamps on it); `end_epoch` is
+    getEpoch() once the last buffer was taken."""
 
-    def __init__(self, status: int, buffers: List[bytes], remaining: int):
+    def __init__(self, status: int, buffers: List[bytes], remaining: int, epochs: Optional[List[int]] = None,
+                 end_epoch: int = 0):
         self.status = status
         self.buffers = buffers
         self.remaining = remaining
+        self.epochs = list(epochs) if epochs is not None else []
+        self.end_epoch = end_epoch
 
 
 class InFlightLogIterator:
     """ReplayIterator (:107-201) over a replay already gathered from HBM: next / hasNext /
-    peekNext / numberRemaining; raises where the reference's iterator throws (an epoch gap)."""
+    peekNext / numberRemaining / getEpoch; raises where the reference's iterator throws (an
+    epoch gap)."""
 
     def __init__(self, rep: InFlightReplay, start_epoch: int):
         self._rep = rep
         self._i = 0
         self._left = rep.remaining
-        self._epoch = start_epoch
+        self._start = start_epoch
 
     def has_next(self) -> bool:
         # at a gap the reference still sees the last buffer before it (:146-149) ...
@@ -67,6 +74,11 @@ class InFlightLogIterator:
 
     def number_remaining(self) -> int:
         return self._left
+
+    def get_epoch(self) -> int:  # :181-183 currentKey
+        if self._i < len(self._rep.epochs):
+            return self._rep.epochs[self._i]
+        return self._rep.end_epoch
 
     def __iter__(self):  # raises ClonosError at an epoch gap, like draining the reference's iterator
         while self.has_next():
@@ -104,9 +116,7 @@ class InFlightLog:
     def get_in_flight_iterator(self, epoch_id: int, ignore_buffers: int = 0) -> InFlightLogIterator:  # :73-82
         rep = self.replay(epoch_id, ignore_buffers)
         if rep.status not in (_lib.CLG_OK, _lib.CLG_E_EPOCH_GAP):
-            check(rep.status)
-        if rep.status == _lib.CLG_E_EPOCH_GAP and not rep.buffers and ignore_buffers:
-            check(rep.status)  # the skip loop itself crossed the gap (:78-79)
+            check(rep.status)  # CLG_E_STATE: the skip loop itself threw (:78-79)
         return InFlightLogIterator(rep, epoch_id)
 
     def close(self) -> None:  # :90-94 (a no-op once the engine itself is closed)
@@ -142,17 +152,19 @@ def make_requests(reqs: Sequence[Tuple[InFlightLog, int, int]]):
     return creq
 
 
-def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=None, sizes=None, cap: int = 0):
+def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=None, sizes=None, cap: int = 0,
+                     epochs=None):
     """One batched replay.  Returns (status, res array, out, sizes, total, total_buffers);
     out / sizes are host numpy arrays unless given; an int `out` is a device pointer
-    (hipMalloc on the engine's device) of `cap` bytes, written in place."""
+    (hipMalloc on the engine's device) of `cap` bytes, written in place.  `epochs` (int64,
+    sized like `sizes`) optionally receives each buffer's epoch."""
     creq = reqs if isinstance(reqs, C.Array) else make_requests(reqs)
     n = len(creq) if len(reqs) else 0
     cres = (_lib.IflReplayRes * max(n, 1))()
     total, nbuf = C.c_uint64(), C.c_uint64()
     if out is None or sizes is None:
         # sizing pass: capacity 0 reports the totals without gathering
-        st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, 0,
+        st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, None, 0,
                                       C.byref(total), C.byref(nbuf))
         if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
             check(st)
@@ -166,22 +178,37 @@ def replay_batch_raw(engine, reqs: Sequence[Tuple[InFlightLog, int, int]], out=N
         out_ptr, kind = int(out), _lib.CLG_MEM_DEVICE
     if sizes is None:
         sizes = np.zeros(max(nbuf.value, 1), np.uint32)
-    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, out_ptr, cap, kind, sizes.ctypes.data, sizes.size,
+    if epochs is not None:
+        assert epochs.dtype == np.int64 and epochs.size >= sizes.size
+    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, out_ptr, cap, kind, sizes.ctypes.data,
+                                  epochs.ctypes.data if epochs is not None else None, sizes.size,
                                   C.byref(total), C.byref(nbuf))
     return st, cres, out, sizes, total.value, nbuf.value
 
 
 def replay_batch(engine, reqs: Sequence[Tuple[InFlightLog, int, int]]) -> List[InFlightReplay]:
     """getInFlightIterator + drain for many subpartitions: one gather kernel for all of them."""
-    st, cres, out, sizes, _, _ = replay_batch_raw(engine, reqs)
+    creq = make_requests(reqs)
+    n = len(reqs)
+    cres = (_lib.IflReplayRes * max(n, 1))()
+    total, nbuf = C.c_uint64(), C.c_uint64()
+    st = lib.clg_ifl_replay_batch(engine.handle, creq, n, cres, None, 0, _lib.CLG_MEM_HOST, None, None, 0,
+                                  C.byref(total), C.byref(nbuf))
+    if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+        check(st)
+    epochs = np.zeros(max(nbuf.value, 1), np.int64)
+    st, cres, out, sizes, _, _ = replay_batch_raw(engine, creq if n else [], sizes=np.zeros(max(nbuf.value, 1),
+                                                  np.uint32), out=np.zeros(max(total.value, 1), np.uint8),
+                                                  epochs=epochs)
     check(st)
     reps = []
-    for i in range(len(reqs)):
+    for i in range(n):
         r = cres[i]
         bufs, o = [], r.out_off
         for k in range(r.n_buffers):
             sz = int(sizes[r.sizes_off + k])
             bufs.append(out[o:o + sz].tobytes())
             o += sz
-        reps.append(InFlightReplay(r.status, bufs, r.remaining))
+        eps = [int(x) for x in epochs[r.sizes_off:r.sizes_off + r.n_buffers]]
+        reps.append(InFlightReplay(r.status, bufs, r.remaining, eps, int(r.end_epoch)))
     return reps

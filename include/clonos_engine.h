@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 1
+#define CLG_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -419,10 +419,16 @@ int clg_ifl_state(clg_engine* e, uint32_t ifl, int64_t* epoch_ids, uint32_t* n_b
  * e.g. already truncated, yields nothing).  An epoch without buffers between start and
  * the last epoch (K buffers before it): next() advances past each returned buffer (:156)
  * and throws at the gap (:133), so the K-th buffer is never delivered -- buffers
- * [ignore_buffers, K-1) are gathered and status is CLG_E_EPOCH_GAP.  Without a gap,
- * ignore_buffers beyond the buffers available (or any skip when start is absent) is the
- * iterator's NoSuchElement/NPE: CLG_E_STATE, nothing gathered.  CLG_E_CAPACITY (bytes or sizes): *total /
- * *total_buffers hold the required sizes and no bytes are gathered. */
+ * [ignore_buffers, K-1) are gathered and status is CLG_E_EPOCH_GAP: getInFlightIterator
+ * itself succeeds and only the next() after the last gathered buffer throws.  A skip that
+ * throws inside getInFlightIterator (:78-79) -- ignore_buffers >= K at a gap, beyond the
+ * buffers available without one, or any skip when start is absent -- is CLG_E_STATE, nothing
+ * gathered.  epochs (optional, indexed like sizes) receives each buffer's epoch: the
+ * iterator's getEpoch() (:181-183, its currentKey) right before the next() that returns
+ * it, which PipelinedSubpartition.getReplayedBufferUnsafe (:306-320) stamps on the
+ * BufferAndBacklog; end_epoch is getEpoch() after the last buffer was taken (or after the
+ * skip when none is).  CLG_E_CAPACITY (bytes or sizes): *total / *total_buffers hold the
+ * required sizes and no bytes are gathered. */
 typedef struct clg_ifl_replay_req {
   uint32_t ifl;
   uint32_t ignore_buffers;
@@ -436,10 +442,11 @@ typedef struct clg_ifl_replay_res {
   uint64_t out_off;
   uint64_t len;
   uint64_t sizes_off;
+  int64_t end_epoch;
 } clg_ifl_replay_res;
 int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t n, clg_ifl_replay_res* res,
-                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, uint64_t sizes_cap,
-                         uint64_t* total, uint64_t* total_buffers);
+                         void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, int64_t* epochs,
+                         uint64_t sizes_cap, uint64_t* total, uint64_t* total_buffers);
 
 /* ---- instrumentation ---------------------------------------------------------------- */
 typedef struct clg_kernel_stat {

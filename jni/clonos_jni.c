@@ -359,7 +359,7 @@ JNIEXPORT jint JNICALL FN(nIflNotifyCheckpointComplete)(JNIEnv* env, jclass cls,
  * and `sizes` (i32 per buffer).  res = {status, buffers, numberRemaining, bytes, required
  * bytes, required buffers}; the call's status is CLG_E_CAPACITY when out/sizes are short. */
 JNIEXPORT jint JNICALL FN(nIflReplay)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong start, jint ignore,
-                                      jobject out, jobject sizes, jlongArray res) {
+                                      jobject out, jobject sizes, jobject epochs, jlongArray res) {
   (void)cls;
   clg_ifl_replay_req q;
   memset(&q, 0, sizeof q);
@@ -369,9 +369,14 @@ JNIEXPORT jint JNICALL FN(nIflReplay)(JNIEnv* env, jclass cls, jlong e, jint ifl
   clg_ifl_replay_res r;
   memset(&r, 0, sizeof r);
   uint64_t total = 0, nbuf = 0;
+  /* sizes (i32) and epochs (i64) are sized for the same number of buffers */
+  uint64_t n_sizes = cap(env, sizes) / 4u;
+  if (epochs && cap(env, epochs) / 8u < n_sizes) n_sizes = cap(env, epochs) / 8u;
   int s = clg_ifl_replay_batch(ENG(e), &q, 1, &r, addr(env, out, 0), cap(env, out), CLG_MEM_HOST,
-                               (uint32_t*)addr(env, sizes, 0), cap(env, sizes) / 4u, &total, &nbuf);
-  jlong w[6] = {r.status, (jlong)r.n_buffers, (jlong)r.remaining, (jlong)r.len, (jlong)total, (jlong)nbuf};
-  (*env)->SetLongArrayRegion(env, res, 0, 6, w);
+                               (uint32_t*)addr(env, sizes, 0), (int64_t*)addr(env, epochs, 0), n_sizes, &total,
+                               &nbuf);
+  jlong w[7] = {r.status, (jlong)r.n_buffers, (jlong)r.remaining, (jlong)r.len, (jlong)total, (jlong)nbuf,
+                (jlong)r.end_epoch};
+  (*env)->SetLongArrayRegion(env, res, 0, 7, w);
   return s;
 }

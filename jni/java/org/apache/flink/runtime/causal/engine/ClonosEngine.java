@@ -90,8 +90,10 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nIflClose(long engine, int ifl);
 	static native int nIflLog(long engine, int ifl, long epoch, ByteBuffer direct, int off, int len);
 	static native int nIflNotifyCheckpointComplete(long engine, int ifl, long checkpointId);
+	/** res = {status, n_buffers, remaining, len, total, total_buffers, end_epoch}; sizes (i32) and
+	 *  epochs (i64, native order) receive one entry per buffer. */
 	static native int nIflReplay(long engine, int ifl, long startEpoch, int ignoreBuffers, ByteBuffer out,
-		ByteBuffer sizes, long[] res);
+		ByteBuffer sizes, ByteBuffer epochs, long[] res);
 	/** bytes = direct buffer holding encoded records (SimpleDeterminantEncoder.encodeTo). */
 	static native int nAppend(long engine, int log, long epoch, ByteBuffer direct, int off, int len);
 	static native int nUpstreamDelta(long engine, int log, long epoch, int offsetFromEpoch, ByteBuffer direct,

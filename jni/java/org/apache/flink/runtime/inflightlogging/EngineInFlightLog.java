@@ -51,19 +51,20 @@ public class EngineInFlightLog implements InFlightLog {
 
 	@Override
 	public synchronized InFlightLogIterator<Buffer> getInFlightIterator(long startEpochID, int ignoreBuffers) {
-		long[] res = new long[6];
-		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, null, null, res);
+		long[] res = new long[7];
+		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, null, null, null, res);
 		if (st != CLG_OK && st != CLG_E_CAPACITY) {
 			check(st);
 		}
 		ByteBuffer out = ByteBuffer.allocateDirect((int) Math.max(1, res[4]));
 		ByteBuffer sizes = ByteBuffer.allocateDirect((int) Math.max(4, 4 * res[5])).order(ByteOrder.nativeOrder());
-		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, out, sizes, res));
+		ByteBuffer epochs = ByteBuffer.allocateDirect((int) Math.max(8, 8 * res[5])).order(ByteOrder.nativeOrder());
+		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, out, sizes, epochs, res));
 		int status = (int) res[0];
-		if (status != CLG_OK && !(status == CLG_E_EPOCH_GAP && res[1] > 0)) {
-			check(status); // the skip loop itself failed (:78-79)
+		if (status != CLG_OK && status != CLG_E_EPOCH_GAP) {
+			check(status); // CLG_E_STATE: the skip loop inside getInFlightIterator threw (:78-79)
 		}
-		return new Replay(out, sizes, (int) res[1], (int) res[2], startEpochID, status);
+		return new Replay(out, sizes, epochs, (int) res[1], (int) res[2], res[6], status);
 	}
 
 	@Override
@@ -84,19 +85,22 @@ public class EngineInFlightLog implements InFlightLog {
 	private final class Replay extends InFlightLogIterator<Buffer> {
 		private final ByteBuffer bytes;
 		private final ByteBuffer sizes;
+		private final ByteBuffer epochs;
 		private final int count;
-		private final long epoch;
+		private final long endEpoch;
 		private final int status;
 		private int next;
 		private int left;
 		private int pos;
 
-		Replay(ByteBuffer bytes, ByteBuffer sizes, int count, int remaining, long epoch, int status) {
+		Replay(ByteBuffer bytes, ByteBuffer sizes, ByteBuffer epochs, int count, int remaining, long endEpoch,
+			int status) {
 			this.bytes = bytes;
 			this.sizes = sizes;
+			this.epochs = epochs;
 			this.count = count;
 			this.left = remaining;
-			this.epoch = epoch;
+			this.endEpoch = endEpoch;
 			this.status = status;
 		}
 
@@ -148,9 +152,12 @@ public class EngineInFlightLog implements InFlightLog {
 			return left;
 		}
 
+		/** ReplayIterator.getEpoch (:181-183): currentKey, i.e. the epoch of the buffer the next
+		 *  next() returns -- PipelinedSubpartition.getReplayedBufferUnsafe (:306-320) stamps it on
+		 *  the BufferAndBacklog -- and, once drained, the epoch the iterator stopped in. */
 		@Override
 		public long getEpoch() {
-			return epoch;
+			return next < count ? epochs.getLong(8 * next) : endEpoch;
 		}
 
 		@Override

@@ -550,8 +550,8 @@ int orc_log_upstream(orc_log* l, const uint8_t* delta, uint32_t n, int32_t off_f
   int32_t cur = l->writer - es->offset;                          // :130
   int32_t num_new = (off_from_epoch + int32_t(n)) - cur;         // :132
   if (num_new > 0) {
+    l->ensure(num_new);  // :136-137 -- components are added before the reader index is set
     if (num_new > int32_t(n)) return ORC_E_GAP;  // delta.readerIndex(negative) -> IndexOutOfBounds (:143)
-    l->ensure(num_new);
     l->write(delta + (n - uint32_t(num_new)), uint32_t(num_new));  // :143-146
   }
   return ORC_OK;

@@ -82,23 +82,31 @@ class InFlightLogRef:
 
     def replay(self, start: int, ignore: int):
         """(status, buffers, remaining) as clg_ifl_replay_batch reports them:
-        status 'ok', 'gap' (the iterator threw after `buffers`) or 'state' (the skip threw)."""
+        status 'ok', 'gap' (the iterator threw after `buffers`) or 'state' (the skip inside
+        getInFlightIterator threw, :78-79)."""
+        return self.replay_full(start, ignore)[:3]
+
+    def replay_full(self, start: int, ignore: int):
+        """(status, buffers, remaining, epochs, end_epoch): epochs[i] is getEpoch()
+        (:181-183, currentKey) right before the next() that returned buffers[i] -- the value
+        PipelinedSubpartition.getReplayedBufferUnsafe (:306-320) reads; end_epoch is
+        getEpoch() after the last successful next() (or after the skip)."""
         try:
             it = ReplayIterator(start, self.sliced)
             for _ in range(ignore):
                 it.next()
         except IteratorNPE:
-            gap = self._has_gap(start)
-            return ("gap" if gap else "state"), [], 0
+            return "state", [], 0, [], None
         remaining = it.number_remaining()
-        out = []
+        out, eps = [], []
+        end = it.current_key
         try:
             while it.has_next():
-                out.append(it.next())
+                e = it.current_key
+                b = it.next()
+                out.append(b)
+                eps.append(e)
+                end = it.current_key
         except IteratorNPE:
-            return "gap", out, remaining
-        return "ok", out, remaining
-
-    def _has_gap(self, start: int) -> bool:
-        keys = sorted(k for k in self.sliced if k >= start)
-        return bool(keys) and keys[0] == start and keys != list(range(start, start + len(keys)))
+            return "gap", out, remaining, eps, end
+        return "ok", out, remaining, eps, it.current_key

@@ -369,9 +369,9 @@ class ThreadLog:
         cur = self.writer - es.offset
         num_new = off_from_epoch + n - cur
         if num_new > 0:
+            self._ensure(num_new)  # :136-137: components are added before readerIndex throws
             if num_new > n:
                 raise LogError(E_GAP)
-            self._ensure(num_new)
             self._write(delta[n - num_new:])
 
     def has_delta(self, ch, epoch) -> bool:

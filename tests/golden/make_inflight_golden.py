@@ -29,8 +29,8 @@ def run_script(ops, n_sub):
         else:
             res = []
             for sub, start, ign in op[1]:
-                st, bufs, rem = refs[sub].replay(start, ign)
-                res.append([st, [b.hex() for b in bufs], rem if st != "state" else None])
+                st, bufs, rem, eps, end = refs[sub].replay_full(start, ign)
+                res.append([st, [b.hex() for b in bufs], rem if st != "state" else None, eps, end])
             out.append(res)
     return out
 

@@ -22,11 +22,11 @@ EDGE_SIZES = [0, 1, 15, 16, 255, 256, 257, 4095, 4096, 32768]
 
 def _check(reps, refs, reqs):
     for rep, (ref, start, ign) in zip(reps, [(refs[f], s, i) for f, s, i in reqs]):
-        st, bufs, rem = ref.replay(start, ign)
+        st, bufs, rem, eps, end = ref.replay_full(start, ign)
         assert rep.status == STATUS[st], (start, ign, rep.status, st)
         assert rep.buffers == bufs
         if st != "state":
-            assert rep.remaining == rem
+            assert rep.remaining == rem and rep.epochs == eps and rep.end_epoch == end
 
 
 @pytest.mark.parametrize("seg", [256, 16384])
@@ -141,7 +141,9 @@ def test_inflight_golden_fixture():
                 else:
                     reps = IF.replay_batch(eng, [(logs[s], st, ign) for s, st, ign in op[1]])
                     got.append([[{v: k for k, v in STATUS.items()}[r.status], [b.hex() for b in r.buffers],
-                                 r.remaining if r.status != _lib.CLG_E_STATE else None] for r in reps])
+                                 r.remaining if r.status != _lib.CLG_E_STATE else None,
+                                 r.epochs if r.status != _lib.CLG_E_STATE else [],
+                                 r.end_epoch if r.status != _lib.CLG_E_STATE else None] for r in reps])
             assert got == c["expect"]
             for f in logs:
                 f.close()

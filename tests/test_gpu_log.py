@@ -40,6 +40,9 @@ def test_log_ops_match_oracle(seed, comp):
                 have = ref.get_determinants(epoch)[1] if epoch in dict(cur["epochs"]) else b""
                 delta = have[len(have) - min(back * 2, len(have)):] + rec if back else rec
                 off = len(have) - (len(delta) - len(rec))
+                if rng.integers(0, 6) == 0:
+                    # a gap: components are added before the reader index throws (:136-143)
+                    off += int(rng.integers(1, 40))
                 st1, _ = status_of(log.processUpstreamDelta, delta, off, epoch)
                 assert st1 == ref.upstream(delta, off, epoch)
             elif op == 6:

@@ -57,9 +57,18 @@ def test_epoch_gap_loses_last_buffer_before_it():
             log.log(bytes([e, i]), e)
     st, bufs, rem = log.replay(0, 0)
     assert st == "gap" and bufs == [bytes([0, 0]), bytes([0, 1])] and rem == 5
-    st, bufs, rem = log.replay(0, 3)  # the skip loop reaches the gap
-    assert st == "gap" and bufs == [] and rem == 0
+    st, bufs, rem = log.replay(0, 3)  # the skip loop inside getInFlightIterator reaches the gap
+    assert st == "state" and bufs == [] and rem == 0
+    # a skip that stops right before the gap succeeds; only the next next() throws
+    st, bufs, rem, eps, end = log.replay_full(0, 2)
+    assert (st, bufs, rem, eps, end) == ("gap", [], 3, [], 0)
     assert log.replay(2, 0) == ("ok", [bytes([2, 0]), bytes([2, 1])], 2)
+    # one buffer before the gap (K = 1): the iterator is built, and next() throws at once
+    one = InFlightLogRef()
+    one.log(b"a", 0)
+    one.log(b"b", 2)
+    assert one.replay_full(0, 0) == ("gap", [], 2, [], 0)
+    assert one.replay_full(0, 1)[0] == "state"
     it = log.get_in_flight_iterator(0, 0)
     it.next()
     it.next()
@@ -82,6 +91,9 @@ def test_golden_fixture_matches_oracle():
     kinds = set()
     for c in d["cases"]:
         assert run_script(c["ops"], c["n_sub"]) == c["expect"]
+        for e in c["expect"]:  # every replay carries one epoch per buffer, non-decreasing
+            for r in e:
+                assert r[0] == "state" or (len(r[3]) == len(r[1]) and r[3] == sorted(r[3]))
         kinds |= {r[0] for e in c["expect"] for r in e}
     assert kinds == {"ok", "state", "gap"}
 
@@ -96,12 +108,13 @@ def test_host_iterator_mirrors_reference_iterator():
         for i in range(n):
             log.log(bytes([e, i]), e)
     code = {"ok": _lib.CLG_OK, "gap": _lib.CLG_E_EPOCH_GAP}
-    for start, ign in ((0, 0), (0, 2), (3, 0), (3, 1)):
-        st, bufs, rem = log.replay(start, ign)
-        mine = InFlightLogIterator(InFlightReplay(code[st], bufs, rem), start)
+    for start, ign in ((0, 0), (0, 2), (0, 4), (3, 0), (3, 1), (1, 0), (1, 1)):
+        st, bufs, rem, eps, end = log.replay_full(start, ign)
+        mine = InFlightLogIterator(InFlightReplay(code[st], bufs, rem, eps, end), start)
         ref = log.get_in_flight_iterator(start, ign)
         while True:
             assert mine.number_remaining() == ref.number_remaining()
+            assert mine.get_epoch() == ref.current_key  # getEpoch() (:181-183)
             try:
                 has = ref.has_next()
             except IteratorNPE:

@@ -156,8 +156,24 @@ def test_oracle_log_matches_pyref(seed):
     last_cp = 0  # JobCausalLogImpl's CAS (:231-238) only lets newer checkpoints through
     chans = [(1, 1), (2, 2), (3, 3)]
     for step in range(400):
-        op = rng.integers(0, 10)
-        if op <= 4:
+        op = rng.integers(0, 11)
+        if op == 10:
+            # upstream delta: dedup overlap, extension, or a gap (components are added
+            # before the reader index throws, ThreadCausalLogImpl.java:136-143)
+            rec = b"".join(D.encode(synth.random_determinant(rng, allow_serializable=False))
+                           for _ in range(int(rng.integers(1, 4))))
+            cur = dict(a.state()["epochs"])
+            have = a.get_determinants(epoch)[1] if epoch in cur else b""
+            off = len(have) - int(rng.integers(0, min(len(have), 6) + 1)) + int(rng.integers(-1, 2)) * 3
+            off = max(off, 0)
+            st = a.upstream(rec, off, epoch)
+            try:
+                b.upstream(rec, off, epoch)
+                st2 = 0
+            except pyref.LogError as ex:
+                st2 = ex.status
+            assert st == st2
+        elif op <= 4:
             rec = D.encode(synth.random_determinant(rng, allow_serializable=False))
             assert a.append(epoch, rec) == 0
             b.append(epoch, rec)
