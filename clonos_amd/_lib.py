@@ -43,6 +43,7 @@ CLG_FULL_SHARING = -1
 EXPORTED = [
     "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
     "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find",
+    "clg_job_open", "clg_job_close",
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
     "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
@@ -238,9 +239,11 @@ def _load() -> C.CDLL:
         "clg_gather_stream": (P, [P]),
         "clg_sync": (C.c_int, [P]),
         "clg_pool_stats": (C.c_int, [P, u32p, u32p]),
-        "clg_log_open": (C.c_int, [P, C.POINTER(CausalLogIdC), u32p]),
+        "clg_log_open": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),
         "clg_log_close": (C.c_int, [P, C.c_uint32]),
-        "clg_log_find": (C.c_int, [P, C.POINTER(CausalLogIdC), u32p]),
+        "clg_log_find": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),
+        "clg_job_open": (C.c_int, [P, C.c_uint64, C.c_uint64, C.c_int32, u32p]),
+        "clg_job_close": (C.c_int, [P, C.c_uint32]),
         "clg_append": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_char_p, C.c_uint32]),
         "clg_append_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P]),
         "clg_upstream_delta": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_int32, C.c_char_p, C.c_uint32]),
@@ -258,7 +261,7 @@ def _load() -> C.CDLL:
         "clg_consumer_seek": (C.c_int, [P, C.c_uint32, ChannelId, C.c_int64, C.c_int32]),
         "clg_consumer_seek_batch": (C.c_int, [P, P, P, C.c_uint32]),
         "clg_upstream_delta_batch": (C.c_int, [P, P, C.c_uint32, P, C.c_uint32]),
-        "clg_truncate_all": (C.c_int, [P, C.c_int64, i32p]),
+        "clg_truncate_all": (C.c_int, [P, C.c_uint32, C.c_int64, i32p]),
         "clg_decode_host": (C.c_int, [P, P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_decode_logs": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_replay_prep": (C.c_int, [P, P, P, P, P, C.c_uint32, P, u32p, C.POINTER(Decoded), P]),
@@ -273,7 +276,8 @@ def _load() -> C.CDLL:
         "clg_encode_batch": (C.c_int, [P, C.POINTER(EncodeIn), P, C.c_uint64, C.c_uint32, u64p, u64p]),
         "clg_enrich_batch": (C.c_int, [P, C.c_uint32, C.POINTER(EnrichReq), C.c_uint32, P, P, P, C.c_uint64,
                                        C.c_uint32, u64p]),
-        "clg_process_delta": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.c_uint32, i64p, P, C.c_uint32, u32p, u64p]),
+        "clg_process_delta": (C.c_int, [P, C.c_uint32, C.c_uint32, P, C.c_uint64, C.c_uint32, i64p, P, C.c_uint32, u32p,
+                                        u64p]),
         "clg_ifl_open": (C.c_int, [P, u32p]),
         "clg_ifl_close": (C.c_int, [P, C.c_uint32]),
         "clg_ifl_log_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P, C.c_uint32]),

@@ -69,8 +69,20 @@ struct ChKeyHash {
   size_t operator()(const ChKey& k) const { return std::hash<uint64_t>()(k.lo * 0x9E3779B97F4A7C15ull ^ k.hi); }
 };
 
+// JobCausalLogImpl (one per job per TaskManager, JobCausalLogFactory.java:56-67): the
+// job's sharing depth (ExecutionConfig.determinantSharingDepth) and its
+// latestCompletedCheckpoint, whose CAS gates the fan-out of truncation (:230-246).
+struct Job {
+  bool open = false;
+  uint64_t lo = 0, hi = 0;  // JobID (an AbstractID)
+  int32_t depth = CLG_FULL_SHARING;
+  int64_t latest_cp = 0;  // JobCausalLogImpl.latestCompletedCheckpoint (:92, :117)
+};
+
 struct Log {
   clg_causal_log_id id{};
+  uint32_t job = 0;
+  int32_t depth = CLG_FULL_SHARING;  // the owning job's sharing depth
   bool open = false;
   std::vector<uint32_t> segs;  // composite components
   int32_t writer = 0;          // visibleWriterIndex (== composite writerIndex)
@@ -91,12 +103,14 @@ struct InFlight {
   std::map<int64_t, std::vector<IflBuf>> epochs;
 };
 
-struct IdKey {
+struct IdKey {  // (job, CausalLogID): logs of different jobs never alias
+  uint32_t job;
   int16_t v;
   uint8_t main;
   int8_t sub;
   int64_t lo, hi;
   bool operator<(const IdKey& o) const {
+    if (job != o.job) return job < o.job;
     if (v != o.v) return v < o.v;
     if (main != o.main) return main < o.main;
     if (main) return false;  // CausalLogID.equals: main logs compare by vertex only
@@ -105,8 +119,8 @@ struct IdKey {
     return sub < o.sub;
   }
 };
-IdKey key_of(const clg_causal_log_id& id) {
-  IdKey k{id.vertex_id, uint8_t(id.is_main ? 1 : 0), id.is_main ? int8_t(0) : id.subpartition,
+IdKey key_of(uint32_t job, const clg_causal_log_id& id) {
+  IdKey k{job, id.vertex_id, uint8_t(id.is_main ? 1 : 0), id.is_main ? int8_t(0) : id.subpartition,
           id.is_main ? 0 : id.irp_lower, id.is_main ? 0 : id.irp_upper};
   return k;
 }
@@ -189,7 +203,7 @@ struct clg_engine {
   std::vector<Log> logs;
   std::vector<InFlight> ifls;
   std::map<IdKey, uint32_t> by_id;
-  int64_t latest_cp = 0;  // JobCausalLogImpl.latestCompletedCheckpoint (:92, :117)
+  std::vector<Job> jobs;  // jobs[0]: the default job (cfg.sharing_depth)
   std::recursive_mutex mu;
 
   // staging / scratch
@@ -362,7 +376,7 @@ struct clg_engine {
   int append(uint32_t h, int64_t epoch, const uint8_t* b, uint32_t n) {  // :158-177
     Log* l;
     CHK(get_log(h, &l));
-    if (cfg.sharing_depth == 0) return CLG_OK;
+    if (l->depth == 0) return CLG_OK;
     if (n && !b) return fail(CLG_E_INVALID_ARG, "null record");
     CHK(ensure_space(*l, int32_t(n)));
     compute_if_absent(*l, epoch);
@@ -448,7 +462,7 @@ struct clg_engine {
     Log* l;
     CHK(get_log(h, &l));
     *out = 0;
-    if (cfg.sharing_depth == 0) return CLG_OK;
+    if (l->depth == 0) return CLG_OK;
     auto it = l->epochs.find(epoch);
     if (it == l->epochs.end()) return CLG_OK;
     auto ci = l->consumers.find(k);
@@ -632,7 +646,7 @@ struct clg_engine {
     *n = 0;
     Log* l;
     CHK(get_log(h, &l));
-    if (cfg.sharing_depth == 0) return CLG_OK;
+    if (l->depth == 0) return CLG_OK;
     int32_t s, nb;
     CHK(determinants_range(*l, start_epoch, &s, &nb));
     if (uint32_t(nb) > cap) {
@@ -1152,6 +1166,9 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->pool = static_cast<uint8_t*>(p) + kPoolGuard;
   e->free_segs.resize(cfg->pool_segments);
   for (uint32_t i = 0; i < cfg->pool_segments; ++i) e->free_segs[i] = cfg->pool_segments - 1 - i;
+  e->jobs.emplace_back();  // job 0: the default job
+  e->jobs[0].open = true;
+  e->jobs[0].depth = cfg->sharing_depth;
   *out = e.release();
   return CLG_OK;
 }
@@ -1191,18 +1208,53 @@ int clg_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments) {
   return CLG_OK;
 }
 
-int clg_log_open(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle) {
+int clg_job_open(clg_engine* e, uint64_t job_lo, uint64_t job_hi, int32_t sharing_depth, uint32_t* job) {
+  ENGINE_GUARD(e);
+  if (!job) return fail(CLG_E_INVALID_ARG, "null argument");
+  for (uint32_t j = 0; j < e->jobs.size(); ++j)
+    if (e->jobs[j].open && e->jobs[j].lo == job_lo && e->jobs[j].hi == job_hi && j != 0)
+      return fail(CLG_E_INVALID_ARG, "job already open");
+  Job nj;
+  nj.open = true;
+  nj.lo = job_lo;
+  nj.hi = job_hi;
+  nj.depth = sharing_depth;
+  for (uint32_t j = 1; j < e->jobs.size(); ++j)
+    if (!e->jobs[j].open) {
+      e->jobs[j] = nj;
+      *job = j;
+      return CLG_OK;
+    }
+  e->jobs.push_back(nj);
+  *job = uint32_t(e->jobs.size() - 1);
+  return CLG_OK;
+}
+
+int clg_job_close(clg_engine* e, uint32_t job) {
+  ENGINE_GUARD(e);
+  if (job >= e->jobs.size() || !e->jobs[job].open) return fail(CLG_E_NO_LOG, "unknown job %u", job);
+  for (uint32_t h = 0; h < e->logs.size(); ++h)
+    if (e->logs[h].open && e->logs[h].job == job) CHK(clg_log_close(e, h));
+  if (job != 0) e->jobs[job] = Job();
+  else e->jobs[0].latest_cp = 0;
+  return CLG_OK;
+}
+
+int clg_log_open(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint32_t* handle) {
   ENGINE_GUARD(e);
   if (!id || !handle) return fail(CLG_E_INVALID_ARG, "null argument");
-  const IdKey k = key_of(*id);
+  if (job >= e->jobs.size() || !e->jobs[job].open) return fail(CLG_E_NO_LOG, "unknown job %u", job);
+  const IdKey k = key_of(job, *id);
   if (e->by_id.count(k)) return fail(CLG_E_INVALID_ARG, "log already open");
   Log l;
   l.id = *id;
+  l.job = job;
+  l.depth = e->jobs[job].depth;
   l.open = true;
   if (e->free_segs.empty()) return fail(CLG_E_NOSPACE, "segment pool exhausted");
   l.segs.push_back(e->free_segs.back());  // ctor addComponent() :102
   e->free_segs.pop_back();
-  const uint32_t h = uint32_t(e->logs.size());
+  const uint32_t h = uint32_t(e->logs.size());  // handles are never reused: a stale one is CLG_E_NO_LOG
   e->logs.push_back(std::move(l));
   e->by_id[k] = h;
   *handle = h;
@@ -1215,14 +1267,14 @@ int clg_log_close(clg_engine* e, uint32_t h) {
   CHK(e->get_log(h, &l));
   CHK(e->sync());
   for (uint32_t s : l->segs) e->free_segs.push_back(s);
-  e->by_id.erase(key_of(l->id));
+  e->by_id.erase(key_of(l->job, l->id));
   *l = Log();
   return CLG_OK;
 }
 
-int clg_log_find(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle) {
+int clg_log_find(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint32_t* handle) {
   ENGINE_GUARD(e);
-  auto it = e->by_id.find(key_of(*id));
+  auto it = e->by_id.find(key_of(job, *id));
   if (it == e->by_id.end()) return fail(CLG_E_NO_LOG, "log not found");
   *handle = it->second;
   return CLG_OK;
@@ -1421,14 +1473,16 @@ int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int3
   return CLG_OK;
 }
 
-int clg_truncate_all(clg_engine* e, int64_t cp, int32_t* applied) {  // JobCausalLogImpl :230-246
+int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) {  // JobCausalLogImpl :230-246
   ENGINE_GUARD(e);
   if (applied) *applied = 0;
-  if (e->latest_cp >= cp) return CLG_OK;
-  e->latest_cp = cp;
+  if (job >= e->jobs.size() || !e->jobs[job].open) return fail(CLG_E_NO_LOG, "unknown job %u", job);
+  Job& j = e->jobs[job];
+  if (j.latest_cp >= cp) return CLG_OK;  // the CAS: only a newer checkpoint fans out
+  j.latest_cp = cp;
   CHK(e->flush());
   for (auto& l : e->logs)
-    if (l.open) CHK(e->checkpoint_complete(l, cp));
+    if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
   if (applied) *applied = 1;
   return CLG_OK;
 }
@@ -1468,7 +1522,7 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) {
     CHK(e->get_log(log[i], &ls[i]));
-    if (e->cfg.sharing_depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
+    if (ls[i]->depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
     total += uint64_t(nb[i]);
   }
   auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
@@ -1865,9 +1919,11 @@ int clg_enrich_batch(clg_engine* e, uint32_t strategy, clg_enrich_req* reqs, uin
 
 // processCausalLogDelta (:117-163): header parsed on the host, deltas applied by the
 // batched upstream scatter straight from the message buffer.
-int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint64_t n, uint32_t in_kind,
-                      int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs, uint64_t* consumed) {
+int clg_process_delta(clg_engine* e, uint32_t job, uint32_t strategy, const uint8_t* msg, uint64_t n,
+                      uint32_t in_kind, int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs,
+                      uint64_t* consumed) {
   ENGINE_GUARD(e);
+  if (job >= e->jobs.size() || !e->jobs[job].open) return fail(CLG_E_NO_LOG, "unknown job %u", job);
   if (!msg || !epoch || !n_logs || strategy > CLG_DELTA_HIERARCHICAL) return fail(CLG_E_INVALID_ARG, "null argument");
   *n_logs = 0;
   if (n < 12) return fail(CLG_E_TRUNCATED, "delta header truncated");
@@ -1890,10 +1946,10 @@ int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint
     p += 8;
     if (len < 0 || delta_at + uint64_t(len) > n) return fail(CLG_E_TRUNCATED, "delta past the message");
     uint32_t h;
-    const IdKey key = key_of(id);
+    const IdKey key = key_of(job, id);
     auto it = e->by_id.find(key);
     if (it == e->by_id.end()) {
-      CHK(clg_log_open(e, &id, &h));  // insertNewUpstreamLog
+      CHK(clg_log_open(e, job, &id, &h));  // insertNewUpstreamLog
     } else {
       h = it->second;
     }

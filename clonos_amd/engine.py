@@ -175,21 +175,33 @@ class Engine:
         check(lib.clg_pool_stats(self._h, C.byref(u), C.byref(f)))
         return u.value, f.value
 
+    # ---- jobs (JobCausalLogImpl scope) ----------------------------------------------------
+    def open_job(self, job_id: Tuple[int, int], sharing_depth: int = _lib.CLG_FULL_SHARING) -> int:
+        """A further JobCausalLog on this engine (job 0 is the engine's default job): its own
+        logs, sharing depth and latestCompletedCheckpoint CAS."""
+        j = C.c_uint32()
+        check(lib.clg_job_open(self._h, job_id[0], job_id[1], sharing_depth, C.byref(j)))
+        return j.value
+
+    def close_job(self, job: int) -> None:
+        check(lib.clg_job_close(self._h, job))
+        self._logs = {k: v for k, v in self._logs.items() if k[0] != job}
+
     # ---- logs -----------------------------------------------------------------------
-    def open_log(self, cid: CausalLogID) -> "ThreadCausalLog":
+    def open_log(self, cid: CausalLogID, job: int = 0) -> "ThreadCausalLog":
         h = C.c_uint32()
-        check(lib.clg_log_open(self._h, C.byref(cid.to_c()), C.byref(h)))
-        log = ThreadCausalLog(self, h.value, cid)
-        self._logs[cid.key()] = log
+        check(lib.clg_log_open(self._h, job, C.byref(cid.to_c()), C.byref(h)))
+        log = ThreadCausalLog(self, h.value, cid, job)
+        self._logs[(job, cid.key())] = log
         return log
 
-    def get_log(self, cid: CausalLogID) -> Optional["ThreadCausalLog"]:
+    def get_log(self, cid: CausalLogID, job: int = 0) -> Optional["ThreadCausalLog"]:
         """The open log for `cid` (also logs the engine opened itself, e.g. by processCausalLogDelta)."""
-        log = self._logs.get(cid.key())
+        log = self._logs.get((job, cid.key()))
         if log is None:
             h = C.c_uint32()
-            if lib.clg_log_find(self._h, C.byref(cid.to_c()), C.byref(h)) == _lib.CLG_OK:
-                log = self._logs[cid.key()] = ThreadCausalLog(self, h.value, cid)
+            if lib.clg_log_find(self._h, job, C.byref(cid.to_c()), C.byref(h)) == _lib.CLG_OK:
+                log = self._logs[(job, cid.key())] = ThreadCausalLog(self, h.value, cid, job)
         return log
 
     def append_batch(self, logs: np.ndarray, epochs: np.ndarray, offs: np.ndarray, lens: np.ndarray,
@@ -252,9 +264,10 @@ class Engine:
         check(lib.clg_consumer_seek_batch(self._h, C.cast(creq, C.c_void_p), offs.ctypes.data, n))
 
     # ---- checkpoint completion ---------------------------------------------------------
-    def truncate_all(self, checkpoint_id: int) -> bool:
+    def truncate_all(self, checkpoint_id: int, job: int = 0) -> bool:
+        """JobCausalLogImpl.notifyCheckpointComplete (:230-246) for `job`: CAS, then every log of it."""
         applied = C.c_int32()
-        check(lib.clg_truncate_all(self._h, checkpoint_id, C.byref(applied)))
+        check(lib.clg_truncate_all(self._h, job, checkpoint_id, C.byref(applied)))
         return bool(applied.value)
 
     # ---- decode -------------------------------------------------------------------------
@@ -342,12 +355,12 @@ class Engine:
         return [(creq[i].status, out[creq[i].out_off:creq[i].out_off + creq[i].out_len].tobytes())
                 for i in range(len(reqs))]
 
-    def process_delta(self, strategy: int, msg: bytes):
+    def process_delta(self, strategy: int, msg: bytes, job: int = 0):
         """processCausalLogDelta: returns (epoch, logs touched in header order, bytes consumed)."""
         buf = np.frombuffer(bytes(msg), np.uint8)
         ep, nl, used = C.c_int64(), C.c_uint32(), C.c_uint64()
         hs = np.zeros(4096, np.uint32)
-        check(lib.clg_process_delta(self._h, strategy, _np_ptr(buf), len(msg), _lib.CLG_MEM_HOST, C.byref(ep),
+        check(lib.clg_process_delta(self._h, job, strategy, _np_ptr(buf), len(msg), _lib.CLG_MEM_HOST, C.byref(ep),
                                     _np_ptr(hs), hs.size, C.byref(nl), C.byref(used)))
         return ep.value, [int(h) for h in hs[:min(nl.value, hs.size)]], used.value
 
@@ -418,10 +431,11 @@ class Engine:
 class ThreadCausalLog:
     """Mirror of ThreadCausalLog (ThreadCausalLog.java:33-96) backed by the engine."""
 
-    def __init__(self, engine: Engine, handle: int, cid: CausalLogID):
+    def __init__(self, engine: Engine, handle: int, cid: CausalLogID, job: int = 0):
         self.engine = engine
         self.handle = handle
         self.cid = cid
+        self.job = job
 
     def getCausalLogID(self) -> CausalLogID:
         return self.cid
@@ -449,21 +463,28 @@ class ThreadCausalLog:
         check(lib.clg_offset_from_epoch(self.engine.handle, self.handle, _ch(outputChannelID), C.byref(v)))
         return v.value
 
-    def getDeltaForConsumer(self, outputChannelID: ChannelLike, epochID: int) -> bytes:
-        cap = max(self.state()["capacity"], 1)
-        buf = np.empty(cap, np.uint8)
+    @staticmethod
+    def _probe_fetch(call) -> bytes:
+        """Size probe, then fetch; CLG_E_CAPACITY (the log grew in between: another thread
+        appended) reports the new size without moving anything, so fetch again."""
         n = C.c_uint32()
-        check(lib.clg_get_delta(self.engine.handle, self.handle, _ch(outputChannelID), epochID, _np_ptr(buf), cap,
-                                _lib.CLG_MEM_HOST, C.byref(n)))
+        st = call(None, 0, C.byref(n))
+        buf = np.empty(1, np.uint8)
+        while st == _lib.CLG_E_CAPACITY:
+            buf = np.empty(n.value + 256, np.uint8)
+            st = call(_np_ptr(buf), buf.size, C.byref(n))
+        check(st)
         return buf[:n.value].tobytes()
 
+    def getDeltaForConsumer(self, outputChannelID: ChannelLike, epochID: int) -> bytes:
+        ch = _ch(outputChannelID)
+        return self._probe_fetch(lambda p, cap, n: lib.clg_get_delta(self.engine.handle, self.handle, ch, epochID, p,
+                                                                     cap, _lib.CLG_MEM_HOST, n))
+
     def getDeterminants(self, startEpochID: int) -> bytes:
-        cap = max(self.state()["capacity"], 1)
-        buf = np.empty(cap, np.uint8)
-        n = C.c_uint32()
-        check(lib.clg_get_determinants(self.engine.handle, self.handle, startEpochID, _np_ptr(buf), cap,
-                                       _lib.CLG_MEM_HOST, C.byref(n)))
-        return buf[:n.value].tobytes()
+        return self._probe_fetch(lambda p, cap, n: lib.clg_get_determinants(self.engine.handle, self.handle,
+                                                                            startEpochID, p, cap, _lib.CLG_MEM_HOST,
+                                                                            n))
 
     def notifyCheckpointComplete(self, checkpointID: int) -> None:
         check(lib.clg_notify_checkpoint_complete(self.engine.handle, self.handle, checkpointID))
@@ -473,7 +494,7 @@ class ThreadCausalLog:
 
     def close(self) -> None:
         check(lib.clg_log_close(self.engine.handle, self.handle))
-        self.engine._logs.pop(self.cid.key(), None)
+        self.engine._logs.pop((self.job, self.cid.key()), None)
 
     # ---- introspection (tests / safety assertions) ----
     def state(self) -> dict:

@@ -116,12 +116,23 @@ int clg_sync(clg_engine* e);
 /* Segments in use / free in the HBM pool. */
 int clg_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments);
 
+/* ---- JobCausalLog scope ------------------------------------------------------------
+ * One JobCausalLogImpl per job per TaskManager (JobCausalLogFactory.java:56-67,
+ * JobCausalLogImpl.java:71-122): a job owns its thread logs, its sharing depth
+ * (ExecutionConfig.determinantSharingDepth) and its latestCompletedCheckpoint.  Job 0 is
+ * the engine's default job (sharing depth from clg_config); clg_job_open adds others, so
+ * that several jobs on one TaskManager share an engine without sharing log identities or
+ * checkpoint CAS state.  Log handles are global to the engine. */
+int clg_job_open(clg_engine* e, uint64_t job_lo, uint64_t job_hi, int32_t sharing_depth, uint32_t* job);
+/* Closes every log of the job (JobCausalLogImpl.close :277-283); job 0 stays open. */
+int clg_job_close(clg_engine* e, uint32_t job);
+
 /* ---- ThreadCausalLog --------------------------------------------------------------- */
-/* Opens a log (ThreadCausalLogImpl ctor :94-112): one empty component is allocated. */
-int clg_log_open(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle);
+/* Opens a log of `job` (ThreadCausalLogImpl ctor :94-112): one empty component is allocated. */
+int clg_log_open(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint32_t* handle);
 /* close() :317-328 (the engine does not wait for consumers; caller guarantees drain). */
 int clg_log_close(clg_engine* e, uint32_t log);
-int clg_log_find(clg_engine* e, const clg_causal_log_id* id, uint32_t* handle);
+int clg_log_find(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint32_t* handle);
 /* appendDeterminant :158-177.  `rec` holds ONE encoded determinant (encodeTo bytes;
  * n == getEncodedSizeInBytes).  Staged on the host, flushed to HBM in batches. */
 int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n);
@@ -199,8 +210,9 @@ int clg_consumer_seek(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epo
 int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int32_t* offsets, uint32_t n);
 
 /* ---- checkpoint completion fan-out (JobCausalLogImpl.notifyCheckpointComplete :230-246) --
- * CAS on the engine's latestCompletedCheckpoint; if newer, truncates every open log. */
-int clg_truncate_all(clg_engine* e, int64_t checkpoint_id, int32_t* applied);
+ * CAS on the job's latestCompletedCheckpoint; if newer, truncates every open log of that
+ * job (other jobs' logs are untouched). */
+int clg_truncate_all(clg_engine* e, uint32_t job, int64_t checkpoint_id, int32_t* applied);
 
 /* ---- batched decode (SimpleDeterminantEncoder.decodeNext over whole spans) -------------
  * Output is a dense SoA over all spans (span order, record order):
@@ -287,10 +299,11 @@ int clg_enrich_batch(clg_engine* e, uint32_t strategy, clg_enrich_req* reqs, uin
 
 /* processCausalLogDelta (:117-163) + insertNewUpstreamLog (:165-194): parse one header +
  * deltas (msg, host or device) and apply processUpstreamDelta to every log it names,
- * opening the logs not seen before.  *epoch = the header's epoch; handles[] receives the
+ * opening the logs not seen before (in `job`).  *epoch = the header's epoch; handles[] receives the
  * logs in header order (*n_logs, up to cap); *consumed = header + delta bytes. */
-int clg_process_delta(clg_engine* e, uint32_t strategy, const uint8_t* msg, uint64_t n, uint32_t in_kind,
-                      int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs, uint64_t* consumed);
+int clg_process_delta(clg_engine* e, uint32_t job, uint32_t strategy, const uint8_t* msg, uint64_t n,
+                      uint32_t in_kind, int64_t* epoch, uint32_t* handles, uint32_t cap, uint32_t* n_logs,
+                      uint64_t* consumed);
 
 /* ---- batched encode (SimpleDeterminantEncoder.encodeTo :56-75, writers :124-323) ---------
  * The inverse of the decode: records given in the decode's SoA layout (tag, v0; a

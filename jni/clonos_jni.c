@@ -58,8 +58,23 @@ JNIEXPORT jstring JNICALL FN(nLastError)(JNIEnv* env, jclass cls) {
   return (*env)->NewStringUTF(env, clg_last_error());
 }
 
-JNIEXPORT jint JNICALL FN(nLogOpen)(JNIEnv* env, jclass cls, jlong e, jshort vid, jboolean is_main, jlong lo,
-                                    jlong hi, jbyte sub, jintArray out) {
+JNIEXPORT jint JNICALL FN(nJobOpen)(JNIEnv* env, jclass cls, jlong e, jlong job_lo, jlong job_hi, jint depth,
+                                    jintArray out) {
+  (void)cls;
+  uint32_t j = 0;
+  int st = clg_job_open(ENG(e), (uint64_t)job_lo, (uint64_t)job_hi, depth, &j);
+  put_int(env, out, (jint)j);
+  return st;
+}
+
+JNIEXPORT jint JNICALL FN(nJobClose)(JNIEnv* env, jclass cls, jlong e, jint job) {
+  (void)env;
+  (void)cls;
+  return clg_job_close(ENG(e), (uint32_t)job);
+}
+
+JNIEXPORT jint JNICALL FN(nLogOpen)(JNIEnv* env, jclass cls, jlong e, jint job, jshort vid, jboolean is_main,
+                                    jlong lo, jlong hi, jbyte sub, jintArray out) {
   (void)cls;
   clg_causal_log_id id;
   memset(&id, 0, sizeof id);
@@ -69,7 +84,7 @@ JNIEXPORT jint JNICALL FN(nLogOpen)(JNIEnv* env, jclass cls, jlong e, jshort vid
   id.irp_upper = hi;
   id.subpartition = sub;
   uint32_t h = 0;
-  int st = clg_log_open(ENG(e), &id, &h);
+  int st = clg_log_open(ENG(e), (uint32_t)job, &id, &h);
   put_int(env, out, (jint)h);
   return st;
 }
@@ -148,10 +163,10 @@ JNIEXPORT jint JNICALL FN(nUnregisterConsumer)(JNIEnv* env, jclass cls, jlong e,
   return clg_unregister_consumer(ENG(e), (uint32_t)log, ch(lo, hi));
 }
 
-JNIEXPORT jint JNICALL FN(nTruncateAll)(JNIEnv* env, jclass cls, jlong e, jlong cp, jintArray applied) {
+JNIEXPORT jint JNICALL FN(nTruncateAll)(JNIEnv* env, jclass cls, jlong e, jint job, jlong cp, jintArray applied) {
   (void)cls;
   int32_t a = 0;
-  int st = clg_truncate_all(ENG(e), cp, &a);
+  int st = clg_truncate_all(ENG(e), (uint32_t)job, cp, &a);
   put_int(env, applied, a);
   return st;
 }
@@ -228,15 +243,15 @@ JNIEXPORT jint JNICALL FN(nEnrichBatch)(JNIEnv* env, jclass cls, jlong e, jint s
 }
 
 /* clg_process_delta on msg[off, off + len); res = {epoch, nLogs, consumed}. */
-JNIEXPORT jint JNICALL FN(nProcessDelta)(JNIEnv* env, jclass cls, jlong e, jint strategy, jobject msg, jint off,
-                                         jint len, jintArray handles, jlongArray res) {
+JNIEXPORT jint JNICALL FN(nProcessDelta)(JNIEnv* env, jclass cls, jlong e, jint job, jint strategy, jobject msg,
+                                         jint off, jint len, jintArray handles, jlongArray res) {
   (void)cls;
   int64_t ep = 0;
   uint32_t nl = 0;
   uint64_t used = 0;
   const jsize hc = (*env)->GetArrayLength(env, handles);
   jint* hs = (*env)->GetIntArrayElements(env, handles, NULL);
-  int s = clg_process_delta(ENG(e), (uint32_t)strategy, addr(env, msg, off), (uint64_t)len, CLG_MEM_HOST, &ep,
+  int s = clg_process_delta(ENG(e), (uint32_t)job, (uint32_t)strategy, addr(env, msg, off), (uint64_t)len, CLG_MEM_HOST, &ep,
                             (uint32_t*)hs, (uint32_t)hc, &nl, &used);
   (*env)->ReleaseIntArrayElements(env, handles, hs, 0);
   jlong r[3] = {ep, (jlong)nl, (jlong)used};

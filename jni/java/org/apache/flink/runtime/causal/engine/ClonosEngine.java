@@ -10,7 +10,10 @@
  */
 package org.apache.flink.runtime.causal.engine;
 
+import org.apache.flink.runtime.causal.determinant.CorruptDeterminantArrayException;
+
 import java.nio.ByteBuffer;
+import java.util.NoSuchElementException;
 
 public final class ClonosEngine implements AutoCloseable {
 
@@ -19,13 +22,25 @@ public final class ClonosEngine implements AutoCloseable {
 	}
 
 	public static final int CLG_OK = 0;
+	public static final int CLG_E_INVALID_ARG = -1;
 	public static final int CLG_E_CORRUPT_TAG = -2;
+	public static final int CLG_E_TRUNCATED = -3;
+	public static final int CLG_E_BAD_ENUM = -4;
+	public static final int CLG_E_NEG_LEN = -5;
+	public static final int CLG_E_BAD_SERIAL = -6;
 	public static final int CLG_E_CONSUMER_BACKWARDS = -7;
 	public static final int CLG_E_NO_CONSUMER = -8;
+	public static final int CLG_E_GAP = -9;
 	public static final int CLG_E_NOSPACE = -10;
 	public static final int CLG_E_CAPACITY = -11;
 	public static final int CLG_E_STATE = -12;
+	public static final int CLG_E_DEVICE = -13;
+	public static final int CLG_E_NO_LOG = -14;
+	public static final int CLG_E_NOT_BUFFER_BUILT = -15;
 	public static final int CLG_E_EPOCH_GAP = -16;
+
+	/** The engine's default job (clg_config sharing depth). */
+	public static final int DEFAULT_JOB = 0;
 
 	private final long handle; // clg_engine*
 
@@ -39,17 +54,29 @@ public final class ClonosEngine implements AutoCloseable {
 		return handle;
 	}
 
-	/** CausalLogID fields (CausalLogID.java:38-60) -> u32 log handle. */
-	public int openLog(short vertexId, boolean isMain, long irpLower, long irpUpper, byte subpartition) {
+	/** A JobCausalLog's scope on this engine (JobCausalLogFactory.java:56-67): JobID + its
+	 *  ExecutionConfig.determinantSharingDepth.  Returns the job slot. */
+	public int openJob(long jobIdLower, long jobIdUpper, int sharingDepth) {
 		int[] out = new int[1];
-		check(nLogOpen(handle, vertexId, isMain, irpLower, irpUpper, subpartition, out));
+		check(nJobOpen(handle, jobIdLower, jobIdUpper, sharingDepth, out));
 		return out[0];
 	}
 
-	/** JobCausalLogImpl.notifyCheckpointComplete :230-246 (CAS + fan-out). */
-	public boolean truncateAll(long checkpointId) {
+	public void closeJob(int job) {
+		check(nJobClose(handle, job));
+	}
+
+	/** CausalLogID fields (CausalLogID.java:38-60) of a log of `job` -> u32 log handle. */
+	public int openLog(int job, short vertexId, boolean isMain, long irpLower, long irpUpper, byte subpartition) {
+		int[] out = new int[1];
+		check(nLogOpen(handle, job, vertexId, isMain, irpLower, irpUpper, subpartition, out));
+		return out[0];
+	}
+
+	/** JobCausalLogImpl.notifyCheckpointComplete :230-246: the job's CAS + fan-out to its logs. */
+	public boolean truncateAll(int job, long checkpointId) {
 		int[] applied = new int[1];
-		check(nTruncateAll(handle, checkpointId, applied));
+		check(nTruncateAll(handle, job, checkpointId, applied));
 		return applied[0] != 0;
 	}
 
@@ -62,27 +89,71 @@ public final class ClonosEngine implements AutoCloseable {
 		if (status == CLG_OK) {
 			return;
 		}
-		String msg = nLastError();
+		throw toException(status, nLastError());
+	}
+
+	/** The exception the reference throws at the point the status stands for. */
+	public static RuntimeException toException(int status, String msg) {
 		switch (status) {
-			case CLG_E_CONSUMER_BACKWARDS:
-				throw new RuntimeException("Consumer went backwards: " + msg); // ThreadCausalLogImpl.java:216
-			case CLG_E_NO_CONSUMER:
-				throw new NullPointerException(msg); // :245 / :256 dereference a missing ConsumerOffset
-			case CLG_E_CORRUPT_TAG:
-				throw new IllegalStateException("corrupt determinant array: " + msg);
+			case CLG_E_CORRUPT_TAG: // SimpleDeterminantEncoder.decodeNext :92
+				return new CorruptDeterminantArrayException(tagOf(msg));
+			case CLG_E_BAD_ENUM: // ProcessingTimeCallbackID.Type.values()[ord] / CheckpointType.values()[ord]
+				return new ArrayIndexOutOfBoundsException(msg);
+			case CLG_E_NEG_LEN: // new byte[negative] (:235, :282)
+				return new NegativeArraySizeException(msg);
+			case CLG_E_TRUNCATED: // ByteBuf.readX past writerIndex
+			case CLG_E_GAP: // ThreadCausalLogImpl.processUpstreamDelta: delta.readerIndex(< 0) (:143)
+			case CLG_E_STATE: // makeDeltaUnsafe / getDeterminants index checks
+				return new IndexOutOfBoundsException(msg);
+			case CLG_E_CONSUMER_BACKWARDS: // ThreadCausalLogImpl.java:215-218
+				return new RuntimeException("Consumer went backwards: " + msg);
+			case CLG_E_NO_CONSUMER: // :245 / :256 dereference a missing ConsumerOffset
 			case CLG_E_EPOCH_GAP: // InMemorySubpartitionInFlightLogger.ReplayIterator :133
-			case CLG_E_STATE:
-				throw new NullPointerException(msg);
-			default:
-				throw new IllegalStateException("clonos engine status " + status + ": " + msg);
+			case CLG_E_NO_LOG: // flatThreadCausalLogs.get(id) == null
+				return new NullPointerException(msg);
+			case CLG_E_NOT_BUFFER_BUILT: // ReplayingState.SubpartitionRecoveryThread :172-177
+				return new RuntimeException("Subpartition has corrupt recovery buffer, expected buffer built: " + msg);
+			case CLG_E_INVALID_ARG:
+				return new IllegalArgumentException(msg);
+			default: // CLG_E_NOSPACE (callers retry), CLG_E_CAPACITY (callers resize), CLG_E_DEVICE
+				return new IllegalStateException("clonos engine status " + status + ": " + msg);
 		}
+	}
+
+	/** The tag byte clg_last_error reports for CLG_E_CORRUPT_TAG ("... (tag N)"). */
+	private static byte tagOf(String msg) {
+		int i = msg.lastIndexOf("tag ");
+		if (i < 0) {
+			return 0;
+		}
+		int j = i + 4;
+		while (j < msg.length() && (Character.isDigit(msg.charAt(j)) || msg.charAt(j) == '-')) {
+			j++;
+		}
+		try {
+			return (byte) Integer.parseInt(msg.substring(i + 4, j));
+		} catch (NumberFormatException e) {
+			return 0;
+		}
+	}
+
+	/** In-flight iterator statuses (InMemorySubpartitionInFlightLogger.ReplayIterator): a skip past
+	 *  the end is ListIterator.next()'s NoSuchElementException, a start epoch that is absent or a
+	 *  gap the NullPointerException of logToReplay.get(..).listIterator(). */
+	public static RuntimeException inFlightException(int status, boolean startPresent, String msg) {
+		if (status == CLG_E_STATE && startPresent) {
+			return new NoSuchElementException(msg);
+		}
+		return new NullPointerException(msg);
 	}
 
 	// ---- natives (jni/clonos_jni.c) ------------------------------------------------------
 	static native int nCreate(int segmentBytes, int poolSegments, int device, int sharingDepth, long[] out);
 	static native void nDestroy(long engine);
 	static native String nLastError();
-	static native int nLogOpen(long engine, short vertexId, boolean isMain, long irpLower, long irpUpper,
+	static native int nJobOpen(long engine, long jobIdLower, long jobIdUpper, int sharingDepth, int[] out);
+	static native int nJobClose(long engine, int job);
+	static native int nLogOpen(long engine, int job, short vertexId, boolean isMain, long irpLower, long irpUpper,
 							   byte subpartition, int[] out);
 	static native int nLogClose(long engine, int log);
 	// in-flight (data) log, InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207)
@@ -107,7 +178,7 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nGetDeterminants(long engine, int log, long startEpoch, ByteBuffer direct, int[] out);
 	static native int nNotifyCheckpointComplete(long engine, int log, long checkpointId);
 	static native int nUnregisterConsumer(long engine, int log, long chLo, long chHi);
-	static native int nTruncateAll(long engine, long checkpointId, int[] applied);
+	static native int nTruncateAll(long engine, int job, long checkpointId, int[] applied);
 
 	// batched paths: LogReplayerImpl / ReplayingState decode, the piggyback serde, replay-prep
 	static native int nDecodeLogs(long engine, int[] logs, long[] startEpochs, ByteBuffer off, ByteBuffer tag,
@@ -115,8 +186,8 @@ public final class ClonosEngine implements AutoCloseable {
 								  ByteBuffer wVarLen, ByteBuffer wSub, long[] result, long[] spanRecBase);
 	static native int nEnrichBatch(long engine, int strategy, long[] requests, int[] logs, byte[] flags,
 								   ByteBuffer out, long[] results, long[] total);
-	static native int nProcessDelta(long engine, int strategy, ByteBuffer msg, int off, int len, int[] handles,
-									long[] result);
+	static native int nProcessDelta(long engine, int job, int strategy, ByteBuffer msg, int off, int len,
+									int[] handles, long[] result);
 	static native int nReplayPrepare(long engine, short vertexId, ByteBuffer mergedEvent, int len, long[] subpartitions,
 									 ByteBuffer off, ByteBuffer tag, ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc,
 									 ByteBuffer wV1, ByteBuffer wVarOff, ByteBuffer wVarLen, ByteBuffer wSub,

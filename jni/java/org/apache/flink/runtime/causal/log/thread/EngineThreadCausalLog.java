@@ -36,13 +36,13 @@ public class EngineThreadCausalLog implements ThreadCausalLog {
 	// per-thread scratch for encoding one determinant (largest fixed record is 27 B)
 	private final ThreadLocal<ByteBuf> scratch;
 
-	public EngineThreadCausalLog(ClonosEngine engine, CausalLogID id, DeterminantEncoder encoder,
+	public EngineThreadCausalLog(ClonosEngine engine, int job, CausalLogID id, DeterminantEncoder encoder,
 								 ByteBufAllocator alloc) {
 		this.engine = engine;
 		this.causalLogID = id;
 		this.encoder = encoder;
 		this.alloc = alloc;
-		this.log = engine.openLog(id.getVertexID(), id.isMainThread(), id.getIntermediateResultPartitionLower(),
+		this.log = engine.openLog(job, id.getVertexID(), id.isMainThread(), id.getIntermediateResultPartitionLower(),
 			id.getIntermediateResultPartitionUpper(), id.getSubpartitionIndex());
 		this.scratch = ThreadLocal.withInitial(() -> Unpooled.directBuffer(256));
 	}
@@ -52,19 +52,46 @@ public class EngineThreadCausalLog implements ThreadCausalLog {
 		return causalLogID;
 	}
 
+	/** The engine handle of this log (batched natives take handles). */
+	public int handle() {
+		return log;
+	}
+
 	@Override
 	public ByteBuf getDeterminants(long startEpochID) {
 		int[] n = new int[1];
 		int st = nGetDeterminants(engine.handle(), log, startEpochID, null, n);
-		if (st == CLG_OK && n[0] == 0) {
-			return Unpooled.EMPTY_BUFFER;
+		ByteBuf out = null;
+		// an append may land between the size probe and the fetch (the task thread appends
+		// while a Netty thread slices): CLG_E_CAPACITY reports the new size, nothing moved, retry
+		while (st == CLG_E_CAPACITY) {
+			if (out != null) {
+				out.release();
+			}
+			int want = n[0] + SLACK;
+			out = alloc.directBuffer(want);
+			st = nGetDeterminants(engine.handle(), log, startEpochID, out.nioBuffer(0, want), n);
 		}
-		if (st != CLG_E_CAPACITY) {
+		return finish(st, out, n[0]);
+	}
+
+	/** Extra room per fetch so a concurrent append rarely forces a second round. */
+	private static final int SLACK = 256;
+
+	private static ByteBuf finish(int st, ByteBuf out, int n) {
+		if (st != CLG_OK) {
+			if (out != null) {
+				out.release();
+			}
 			check(st);
 		}
-		ByteBuf out = alloc.directBuffer(n[0]);
-		check(nGetDeterminants(engine.handle(), log, startEpochID, out.nioBuffer(0, n[0]), n));
-		return out.writerIndex(n[0]);
+		if (n == 0) {
+			if (out != null) {
+				out.release();
+			}
+			return Unpooled.EMPTY_BUFFER; // :265 / :287
+		}
+		return out.writerIndex(n);
 	}
 
 	@Override
@@ -120,15 +147,18 @@ public class EngineThreadCausalLog implements ThreadCausalLog {
 		long lo = outputChannelID.getLowerPart(), hi = outputChannelID.getUpperPart();
 		int[] n = new int[1];
 		int st = nGetDelta(engine.handle(), log, lo, hi, epochID, null, n); // size probe, no advance
-		if (st == CLG_OK && n[0] == 0) {
-			return Unpooled.EMPTY_BUFFER;
+		ByteBuf out = null;
+		// CLG_E_CAPACITY never advances the consumer, so a delta that grew since the probe
+		// (a concurrent appendDeterminant) is fetched again at its new size
+		while (st == CLG_E_CAPACITY) {
+			if (out != null) {
+				out.release();
+			}
+			int want = n[0] + SLACK;
+			out = alloc.directBuffer(want);
+			st = nGetDelta(engine.handle(), log, lo, hi, epochID, out.nioBuffer(0, want), n);
 		}
-		if (st != CLG_E_CAPACITY) {
-			check(st);
-		}
-		ByteBuf out = alloc.directBuffer(n[0]);
-		check(nGetDelta(engine.handle(), log, lo, hi, epochID, out.nioBuffer(0, n[0]), n));
-		return out.writerIndex(n[0]);
+		return finish(st, out, n[0]);
 	}
 
 	@Override

@@ -306,3 +306,74 @@ def test_async_decode_device_output():
         finally:
             for p in ptrs.values():
                 hip.hipFree(p)
+
+
+def test_two_jobs_on_one_engine():
+    """JobCausalLogImpl is per job (JobCausalLogFactory.java:56-67): two jobs on one
+    TaskManager's engine keep separate logs for the same CausalLogID, separate sharing
+    depths, and separate latestCompletedCheckpoint CAS states (:230-246)."""
+    with Engine(segment_bytes=64, pool_segments=1 << 10) as eng:
+        ja = 0
+        jb = eng.open_job((0xA, 0xB), sharing_depth=-1)
+        jz = eng.open_job((0xC, 0xD), sharing_depth=0)  # logging switched off for this job
+        cid = CausalLogID.main(3)
+        la, lb, lz = eng.open_log(cid, ja), eng.open_log(cid, jb), eng.open_log(cid, jz)
+        assert len({la.handle, lb.handle, lz.handle}) == 3
+        ra, rb = O.OracleLog(64), O.OracleLog(64)
+        for e in range(4):
+            for k in range(30):
+                a = bytes([0, k % 4])
+                b = bytes([1]) + (e * 1000 + k).to_bytes(8, "big")
+                la.appendDeterminant(a, e)
+                ra.append(e, a)
+                lb.appendDeterminant(b, e)
+                rb.append(e, b)
+                lz.appendDeterminant(b, e)  # depth 0: a no-op (:160-161)
+        assert lz.state()["writer"] == 0
+        assert eng.get_log(cid, jb).handle == lb.handle and eng.get_log(cid, ja).handle == la.handle
+        # job A completes checkpoint 3: only its logs are truncated
+        assert eng.truncate_all(3, ja)
+        assert ra.checkpoint_complete(3) == 0
+        assert la.state() == ra.state() and lb.state() == rb.state()
+        # job B has not seen any checkpoint yet: an older id than A's still fans out
+        assert eng.truncate_all(2, jb)
+        assert rb.checkpoint_complete(2) == 0
+        assert lb.state() == rb.state()
+        assert not eng.truncate_all(2, jb) and not eng.truncate_all(1, ja)  # CAS per job
+        assert la.getDeterminants(3) == ra.get_determinants(3)[1]
+        assert lb.getDeterminants(2) == rb.get_determinants(2)[1]
+        eng.close_job(jb)
+        assert eng.get_log(cid, jb) is None and eng.get_log(cid, ja) is not None
+
+
+def test_get_delta_with_concurrent_appender():
+    """getDeltaForConsumer on one thread while appendDeterminant runs on another (the
+    Netty thread vs the task thread, ThreadCausalLogImpl's epochReadLock + synchronized(buf)):
+    the size probe and the fetch are two calls, so a delta that grew in between must be
+    re-fetched (CLG_E_CAPACITY never advances the consumer).  The deltas a consumer receives
+    concatenate to exactly the log."""
+    import threading
+    with Engine(segment_bytes=256, pool_segments=1 << 12) as eng:
+        log = eng.open_log(CausalLogID.main(9))
+        recs = [bytes([1]) + i.to_bytes(8, "big") for i in range(4000)]
+        log.appendDeterminant(recs[0], 0)
+        done = threading.Event()
+
+        def appender():
+            for r in recs[1:]:
+                log.appendDeterminant(r, 0)
+            done.set()
+
+        t = threading.Thread(target=appender)
+        t.start()
+        ch = (5, 5)
+        got = []
+        assert log.hasDeltaForConsumer(ch, 0)
+        while True:
+            fin = done.is_set()
+            got.append(log.getDeltaForConsumer(ch, 0))
+            if fin:
+                break
+        t.join()
+        got.append(log.getDeltaForConsumer(ch, 0))
+        assert b"".join(got) == b"".join(recs)
