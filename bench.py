@@ -320,8 +320,11 @@ def inflight_replay(args, torch, dev, n_sub=256, n_epochs=4, per_epoch=8, buf_by
             np.concatenate(bufs)
             reps += 1
         dt = (_t.perf_counter() - t0) / reps
+        hc = host_cpu()
         res["cpu_baseline"] = {"value": round(sum(b.size for b in bufs) / dt / 1e9, 2), "unit": "GB/s", "cores": 1,
-                               "kind": "port", "sample": f"memcpy gather of one epoch's {len(bufs)} buffers, x{reps}"}
+                               "kind": "port", "sample": f"memcpy gather of one epoch's {len(bufs)} buffers, x{reps} "
+                                                         "(one thread: the Java drain is one thread per subpartition)",
+                               **{k2: v for k2, v in hc.items() if k2 != "cores"}}
     return res
 
 
@@ -394,14 +397,48 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
         host = np.concatenate([epochs[(e + v) % n_epochs] for v in range(n_logs) for e in range(n_epochs)])
         lens = np.full(n_logs, per_log, np.uint64)
         offs = np.arange(n_logs, dtype=np.uint64) * np.uint64(per_log)
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        hc = host_cpu()
+        threads = args.cpu_threads or hc["cores"]
         t0 = _t.perf_counter()
         n1 = O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs), O.ptr(lens), n_logs, threads)
         dt = _t.perf_counter() - t0
         assert n1 == n_det, (n1, n_det)
+        k = 8  # one core: the first 8 logs
+        t0 = _t.perf_counter()
+        nk = O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs), O.ptr(lens), k, 1)
+        d1 = _t.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(n_det / dt, 1), "unit": "determinants/s", "cores": threads,
-                               "kind": "port", "sample": f"whole config-3 decode once ({total} B) in {dt:.2f}s"}
+                               "kind": "port", "sample": f"whole config-3 decode once ({total} B) in {dt:.2f}s",
+                               "cores_1": {"value": round(nk / d1, 1), "unit": "determinants/s",
+                                           "sample": f"{k} logs decode, one thread, {d1:.2f}s"},
+                               **{k2: v for k2, v in hc.items() if k2 != "cores"}}
     return out
+
+
+def host_cpu():
+    """The host cores this process may use: its affinity mask, capped by a cgroup CPU quota
+    when one is set (a GPU box shares its host between GPUs), and the CPU model."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"cores": usable, "affinity": affinity, "cgroup_quota_cpus": quota, "cpu": model}
 
 
 def cpu_baseline(bufs, log_bytes, cons, args):
@@ -418,7 +455,8 @@ def cpu_baseline(bufs, log_bytes, cons, args):
     dst = np.zeros(len(cons), np.uint64)
     dst[1:] = np.cumsum(ln)[:-1]
     out = np.empty(int(ln.sum()), np.uint8)
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    hc = host_cpu()
+    threads = args.cpu_threads or hc["cores"]
     # repeat the full step until at least args.cpu_seconds of CPU wall time (bounded sample)
     reps, td, ts, nrec = 0, 0.0, 0.0, 0
     while td + ts < args.cpu_seconds or reps == 0:
@@ -432,18 +470,24 @@ def cpu_baseline(bufs, log_bytes, cons, args):
         td += t1 - t0
         ts += t2 - t1
         reps += 1
-    cpu_model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu_model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    # 1 core: the same per-log work for the first 4 logs and their consumers, once
+    k = min(4, len(bufs))
+    kc = [j for j, (i, _, _) in enumerate(cons) if i < k]
+    t0 = time.perf_counter()
+    n1 = O.lib.orc_bench_decode(O.ptr(host), O.ptr(starts), O.ptr(lens), k, 1)
+    t1 = time.perf_counter()
+    src1, ln1 = np.ascontiguousarray(src[kc]), np.ascontiguousarray(ln[kc])
+    dst1 = np.zeros(len(kc), np.uint64)
+    dst1[1:] = np.cumsum(ln1)[:-1]
+    O.lib.orc_bench_slice(O.ptr(host), O.ptr(src1), O.ptr(ln1), O.ptr(dst1), len(kc), O.ptr(out), 1)
+    t2 = time.perf_counter()
     return {"value": round(nrec / (td + ts), 1), "unit": "determinants/s", "cores": threads, "kind": "port",
             "sample": f"full config-2 step ({len(bufs)} logs x {args.records} records decode + {len(cons)} slices, "
                       f"{int(ln.sum())} B) x {reps}; decode {td:.2f}s slice {ts:.2f}s on {threads} threads",
-            "cpu": cpu_model}
+            "cores_1": {"value": round(n1 / (t2 - t0), 1), "unit": "determinants/s",
+                        "sample": f"{k} logs decode ({t1 - t0:.2f}s) + their {len(kc)} slices ({t2 - t1:.2f}s), "
+                                  "one thread"},
+            **{k2: v for k2, v in hc.items() if k2 != "cores"}}
 
 
 if __name__ == "__main__":

@@ -296,6 +296,34 @@ def decode_one(b: bytes, pos: int):
     raise DecodeError(E_CORRUPT_TAG, pos, tag)
 
 
+def encode_one(tag: int, v0: int, rc: int = 0, v1: int = 0, sub: int = 0, var: bytes = b"") -> bytes:
+    """SimpleDeterminantEncoder.encodeTo (:56-75) with the per-type writers: Order :124-127,
+    Timestamp :145-148, RNG :167-170, BufferBuilt :189-192, TimerTrigger :202-213,
+    SourceCheckpoint :244-257, IgnoreCheckpoint :289-293, Serializable :316-323 (the
+    stream bytes are given).  Fields are in the decode's record layout (decode_one)."""
+    w = lambda fmt, *a: struct.pack(">" + fmt, *a)  # noqa: E731  (Netty ByteBuf: big-endian)
+    m32 = lambda x: ((x + (1 << 31)) % (1 << 32)) - (1 << 31)  # noqa: E731  (int cast)
+    m64 = lambda x: ((x + (1 << 63)) % (1 << 64)) - (1 << 63)  # noqa: E731  (long cast)
+    if tag == 0:
+        return w("bb", 0, ((v0 + 128) % 256) - 128)
+    if tag == 1:
+        return w("bq", 1, m64(v0))
+    if tag in (2, 7):
+        return w("bi", tag, m32(v0))
+    if tag == 6:
+        return w("biq", 6, m32(rc), m64(v0))
+    if tag == 4:
+        head = w("biqb", 4, m32(rc), m64(v0), sub)
+        return head + (w("i", len(var)) + var if sub == 6 else b"")
+    if tag == 5:
+        has = 1 if sub & 0x80 else 0
+        head = w("biqqbB", 5, m32(rc), m64(v0), m64(v1), sub & 0x7F, has)
+        return head + (w("i", len(var)) + var if has else b"")
+    if tag == 3:
+        return b"\x03" + bytes(var)
+    raise ValueError(f"unknown tag {tag}")
+
+
 def decode_all(b: bytes) -> List[dict]:
     out, pos = [], 0
     while pos < len(b):

@@ -51,6 +51,13 @@ for n, a in {
 }.items():
     getattr(lib, n).restype = C.c_int
     getattr(lib, n).argtypes = a
+class OrcDet(C.Structure):
+    _fields_ = [("tag", C.c_uint8), ("v0", C.c_int64), ("record_count", C.c_int32), ("v1", C.c_int64),
+                ("sub", C.c_uint8), ("var", C.c_void_p), ("var_len", C.c_uint32)]
+
+
+lib.orc_encode.restype = C.c_int64
+lib.orc_encode.argtypes = [C.POINTER(OrcDet), C.c_void_p, C.c_size_t]
 lib.orc_bench_decode.restype = C.c_int64
 lib.orc_bench_decode.argtypes = [P, P, P, C.c_uint32, C.c_uint32]
 lib.orc_bench_slice.restype = C.c_int64
@@ -59,6 +66,32 @@ lib.orc_bench_slice.argtypes = [P, P, P, P, C.c_uint32, P, C.c_uint32]
 
 def ptr(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
+
+
+def encode_soa(tag, v0, w_idx=(), w_rc=(), w_v1=(), w_var_off=(), w_var_len=(), w_sub=(), var: bytes = b"") -> bytes:
+    """orc_encode (SimpleDeterminantEncoder.encodeTo) record by record over the decode's SoA
+    layout: side row k belongs to record w_idx[k]; payloads are var[w_var_off, +w_var_len)."""
+    side = {int(w_idx[k]): k for k in range(len(w_idx))}
+    vb = np.frombuffer(bytes(var) or b"\0", np.uint8)
+    base = vb.ctypes.data
+    out = bytearray()
+    buf = np.zeros(64, np.uint8)
+    d = OrcDet()
+    for i in range(len(tag)):
+        d.tag, d.v0 = int(tag[i]), int(v0[i])
+        k = side.get(i)
+        d.record_count = int(w_rc[k]) if k is not None else 0
+        d.v1 = int(w_v1[k]) if k is not None else 0
+        d.sub = int(w_sub[k]) if k is not None else 0
+        vl = int(w_var_len[k]) if k is not None else 0
+        d.var, d.var_len = (base + int(w_var_off[k])) if vl else None, vl
+        if buf.size < 64 + vl:
+            buf = np.zeros(64 + vl, np.uint8)
+        n = lib.orc_encode(C.byref(d), buf.ctypes.data, buf.size)
+        if n < 0:
+            raise ValueError(f"orc_encode status {n} at record {i}")
+        out += buf[:n].tobytes()
+    return bytes(out)
 
 
 def jser_len(b: bytes) -> int:

@@ -1,10 +1,11 @@
 """GPU: batched encode (clg_encode_batch, encode.hip) == SimpleDeterminantEncoder.encodeTo
 (SimpleDeterminantEncoder.java:56-75, writers :124-323) record by record.
 
-Two independent checks: (1) determinant objects turned into the SoA layout by hand and
-encoded on the GPU give exactly the bytes of the per-record encoder (determinants.encode,
-pinned by the KATs in test_oracle_kat.py); (2) encode(decode(log)) == log for the mixed
-config-3 stream and for logs with long payloads (blocks that do not fit the LDS stage).
+Every check compares the GPU with the CPU oracle (orc_encode, oracle/clonos_oracle.cpp,
+pinned by the hand KATs in test_oracle_kat.py and cross-checked against the Python
+restatement pyref.encode_one): (1) determinant objects turned into the SoA layout by hand;
+(2) the oracle's decode of the mixed config-3 stream, re-encoded (== the original bytes as
+well); (3) logs with long payloads (blocks that do not fit the LDS stage).
 """
 import numpy as np
 import pytest
@@ -67,16 +68,23 @@ def soa_of(dets):
 def test_encode_matches_encoder(eng, seed):
     rng = np.random.default_rng(seed)
     dets = [synth.random_determinant(rng) for _ in range(int(rng.integers(1, 5000)))]
-    want = b"".join(D.encode(d) for d in dets)
-    got = eng.encode_batch(*soa_of(dets))
+    soa = soa_of(dets)
+    want = O.encode_soa(*soa)
+    got = eng.encode_batch(*soa)
     assert got == want
 
 
 def test_encode_roundtrip_config3(eng):
     rng = np.random.default_rng(33)
     buf = synth.config3_epoch(100_000, rng)[0].tobytes()
-    dec = eng.decode_host(buf)
-    assert eng.encode_decoded(dec, buf) == buf
+    st, r, _, _ = O.decode(buf)
+    assert st == 0
+    soa = (r["tag"], r["v0"], r["w_idx"], r["w_rc"], r["w_v1"], r["w_var_off"], r["w_var_len"], r["w_sub"], buf)
+    want = O.encode_soa(*soa)
+    assert want == buf
+    assert eng.encode_batch(*soa) == want
+    dec = eng.decode_host(buf)  # the GPU decode's SoA re-encodes to the same bytes
+    assert eng.encode_decoded(dec, buf) == want
     assert eng.kernel_stats()["encode_write"]["launches"] >= 1
 
 
@@ -92,8 +100,10 @@ def test_encode_long_payloads(eng):
     buf = b"".join(parts)
     st, r, _, _ = O.decode(buf)
     assert st == 0
-    assert eng.encode_batch(r["tag"], r["v0"], r["w_idx"], r["w_rc"], r["w_v1"], r["w_var_off"], r["w_var_len"],
-                            r["w_sub"], buf) == buf
+    soa = (r["tag"], r["v0"], r["w_idx"], r["w_rc"], r["w_v1"], r["w_var_off"], r["w_var_len"], r["w_sub"], buf)
+    want = O.encode_soa(*soa)
+    assert want == buf
+    assert eng.encode_batch(*soa) == want
 
 
 def test_encode_errors(eng):

@@ -36,6 +36,15 @@ BOOLEAN_TRUE = bytes.fromhex("aced0005737200116a6176612e6c616e672e426f6f6c65616e
 @pytest.mark.parametrize("det,hexs", KAT_ENCODE)
 def test_encode_kat(det, hexs):
     assert D.encode(det).hex() == hexs
+    # both oracle encoders reproduce the hand-derived bytes from the decoded fields
+    raw = bytes.fromhex(hexs)
+    st, r, _, _ = O.decode(raw)
+    assert st == 0 and len(r["tag"]) == 1
+    assert O.encode_soa(r["tag"], r["v0"], r["w_idx"], r["w_rc"], r["w_v1"], r["w_var_off"], r["w_var_len"],
+                        r["w_sub"], raw) == raw
+    d = pyref.decode_all(raw)[0]
+    assert pyref.encode_one(d["tag"], d["v0"], d["rc"], d["v1"], d["sub"],
+                            raw[d["var_off"]:d["var_off"] + d["var_len"]]) == raw
 
 
 def test_record_sizes_match_reference():
@@ -217,3 +226,18 @@ def test_oracle_log_matches_pyref(seed):
         else:
             assert a.log_length() == b.log_length()
         assert a.state() == b.state()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_oracle_encode_matches_pyref(seed):
+    """orc_encode (C++) == pyref.encode_one (Python) on random records of every tag, and
+    both invert the decoder (encode(decode(x)) == x)."""
+    rng = np.random.default_rng(500 + seed)
+    buf = synth.random_log(3000, rng)
+    st, r, _, _ = O.decode(buf)
+    assert st == 0
+    soa = (r["tag"], r["v0"], r["w_idx"], r["w_rc"], r["w_v1"], r["w_var_off"], r["w_var_len"], r["w_sub"], buf)
+    assert O.encode_soa(*soa) == buf
+    py = b"".join(pyref.encode_one(d["tag"], d["v0"], d["rc"], d["v1"], d["sub"],
+                                   buf[d["var_off"]:d["var_off"] + d["var_len"]]) for d in pyref.decode_all(buf))
+    assert py == buf
