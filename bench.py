@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--inflight-only", action="store_true",
                     help="profiling aid: run only the in-flight replay leg and print its JSON object")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated per-kernel pass (profiling runs)")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 replication leg")
+    ap.add_argument("--config4-only", action="store_true",
+                    help="profiling aid: run only the config-4 leg and print its JSON object")
+    ap.add_argument("--config4-steps", type=int, default=6)
     return ap.parse_args()
 
 
@@ -74,6 +78,13 @@ def main():
 
     if args.inflight_only:
         print(json.dumps(inflight_replay(args, torch, torch.device("cuda", local))), flush=True)
+        return
+    if args.config4_only:
+        c4 = config4(args, torch, torch.device("cuda", local), rank, world, dist, rehearse)
+        if rank == 0:
+            print(json.dumps(c4), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
         return
 
     # ---------------- synthetic shard (seeded per rank) ----------------
@@ -223,6 +234,11 @@ def main():
     ifl = None
     if rank == 0 and world == 1 and not args.no_inflight:
         ifl = inflight_replay(args, torch, dev)
+    c4 = None
+    if not args.no_config4:  # every rank: the exchange is a collective
+        if world == 1:
+            eng.close()
+        c4 = config4(args, torch, dev, rank, world, dist, rehearse)
 
     if rank == 0:
         line = {
@@ -258,11 +274,140 @@ def main():
             "cpu_baseline": cpu,
             "config3": c3,
             "inflight_replay": ifl,
+            "config4": c4,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, sub_records=64):
+    """BASELINE.json configs[3]: full sharing depth on a 5-stage DAG at parallelism 128
+    (640 VertexIDs; per producing vertex 1 main + 128 subpartition logs; 66 176 logs), logs
+    sharded by VertexID across the ranks (job.owner_rank).  One step, on every rank:
+      1. the new epoch of every owned log lands in HBM (batched device-input append);
+      2. batched decode of that epoch of every owned log (SoA in HBM);
+      3. replication (dist.Replicator.exchange): batched slice of the new bytes of every
+         owned log another rank wants -> all-gather over RCCL -> batched device-input
+         processUpstreamDelta into the replicas;
+      4. checkpoint completion of the previous epoch (job CAS + truncation of owned logs and
+         replicas).
+    At N=1 every log is local: the replication moves nothing (its collective still runs on a
+    one-rank group).  Timing: K steps between barriers + device syncs, max over ranks."""
+    import time as _t
+    from clonos_amd import Engine, _lib, job as J, synth, dist as X
+    own_group = None
+    if world == 1:  # a one-rank group so the exchange's collectives run (and are timed)
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 2000)))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+            own_group = True
+    g = J.dag(5, 128)
+    table = J.LogTable(g)
+    need = J.replication_masks(g, -1, world)
+    plan = X.ReplicationPlan(table, -1, rank, world, need)
+    rng = np.random.default_rng(synth.SEED_CONFIG4 + rank)
+    gids = plan.owned
+    host, offs = synth.config4_epoch(table, gids, rng, main_records, sub_records)
+    seg = 16384
+    per_log = np.diff(offs).astype(np.int64)
+    segs = int(((2 * per_log + seg - 1) // seg + 2).sum())
+    # replicas: the owners' epoch sizes are the same shapes (main / subpartition)
+    main_b = int(per_log[[table.ids[int(x)].is_main for x in gids]].max()) if len(gids) else 0
+    sub_b = sub_records * 5
+    rep_segs = sum(((2 * (main_b if table.ids[int(x)].is_main else sub_b) + seg - 1) // seg + 2)
+                   for x in plan.wanted)
+    eng = Engine(segment_bytes=seg, pool_segments=segs + rep_segs + 64, device=dev.index or 0, timing=True)
+    owned = {int(x): eng.open_log(table.ids[int(x)]).handle for x in gids}
+    sendset = set(plan.send.tolist())
+    rep = X.Replicator(X.EngineIO(eng), plan, dev, {k: v for k, v in owned.items() if k in sendset})
+    d_epoch = torch.from_numpy(host).to(dev)
+    areq = np.zeros(len(gids), X.DELTA_REQ)
+    areq["log"] = [owned[int(x)] for x in gids]
+    areq["src_off"] = offs[:-1]
+    areq["len"] = per_log
+    handles = np.array([owned[int(x)] for x in gids], np.uint32)
+    n_rec = int(sum(main_records if table.ids[int(x)].is_main else sub_records for x in gids))
+    o = [torch.empty(max(n_rec, 1), dtype=t, device=dev) for t in (torch.int32, torch.uint8, torch.int64)]
+    ow = [torch.empty(16, dtype=t, device=dev) for t in
+          (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
+    dec = _lib.Decoded()
+    dec.off, dec.tag, dec.v0 = [t.data_ptr() for t in o]
+    dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len, dec.w_sub = [t.data_ptr() for t in ow]
+    dec.cap, dec.wcap, dec.out_kind = max(n_rec, 1), 16, _lib.CLG_MEM_DEVICE
+    base = np.zeros(len(gids) + 1, np.uint64)
+    bytes_owned = int(host.size)
+    payload_cap = int(per_log[np.isin(gids, plan.send)].sum()) + 64
+    phase = {"append": 0.0, "decode": 0.0, "exchange": 0.0, "truncate": 0.0}
+    ex_tot = X.ExchangeStats()
+
+    def step(e, timed):
+        t0 = _t.perf_counter()
+        areq["epoch"] = e
+        areq["status"] = 0
+        _lib.check(_lib.lib.clg_upstream_delta_batch(eng.handle, areq.ctypes.data, len(areq), d_epoch.data_ptr(),
+                                                     _lib.CLG_MEM_DEVICE))
+        t1 = _t.perf_counter()
+        starts = np.full(len(gids), e, np.int64)
+        eng.decode_logs_device(handles, starts, dec, base)
+        assert dec.n_rec == n_rec and dec.err_status == 0, (dec.n_rec, n_rec)
+        t2 = _t.perf_counter()
+        st = rep.exchange(e, payload_cap)
+        t3 = _t.perf_counter()
+        if e > 0:
+            assert eng.truncate_all(e)
+        t4 = _t.perf_counter()
+        if timed:
+            for k, v in zip(phase, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+                phase[k] += v
+            for f in ("sent_bytes", "recv_bytes", "applied", "applied_bytes", "skipped"):
+                setattr(ex_tot, f, getattr(ex_tot, f) + getattr(st, f))
+
+    warm = 2
+    for e in range(warm):
+        step(e, False)
+    torch.cuda.synchronize()
+    eng.kernel_stats_reset()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = _t.perf_counter()
+    K = args.config4_steps
+    for e in range(warm, warm + K):
+        step(e, True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = _t.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64, device="cpu" if rehearse else dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el = float(tt.item())
+    tot = torch.tensor([n_rec, bytes_owned, ex_tot.applied_bytes, ex_tot.sent_bytes], dtype=torch.float64,
+                       device="cpu" if rehearse else dev)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    tot_rec, tot_bytes, tot_applied, tot_sent = [float(x) for x in tot.cpu()]
+    st = eng.kernel_stats()
+    kern = {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5),
+                    gbs=round(v["bytes"] / v["launches"] / (v["ms"] / v["launches"] * 1e-3) / 1e9, 1)
+                    if v["ms"] > 0 else None) for k, v in st.items() if v["launches"]}
+    eng.close()
+    if own_group:
+        dist.destroy_process_group()
+    ms = el * 1e3 / K
+    return {"workload": "config4: 5-stage DAG, p=128, full sharing (640 VertexIDs, 66176 logs: 1 main + 128 "
+                        f"subpartition logs per producing vertex); per epoch {main_records} Order/Timestamp per main "
+                        f"log, {sub_records} BufferBuilt per subpartition log; step = append + decode of owned logs "
+                        "+ replication exchange (slice -> all-gather -> processUpstreamDelta) + truncation",
+            "n_gpus": world, "steps": K, "ms_per_step": round(ms, 4),
+            "determinants_per_s": round(tot_rec / (el / K), 1), "log_gbs": round(tot_bytes / (el / K) / 1e9, 2),
+            "logs_per_rank": {"owned": len(gids), "sent": int(len(plan.send)), "replicas": int(len(plan.wanted))},
+            "exchange": {"sent_bytes_per_step_all_ranks": int(tot_sent / K),
+                         "applied_bytes_per_step_all_ranks": int(tot_applied / K),
+                         "applied_deltas_per_step_rank0": int(ex_tot.applied / K),
+                         "replicated_gbs": round(tot_applied / el / 1e9, 2)},
+            "phase_ms_rank0": {k: round(v * 1e3 / K, 3) for k, v in phase.items()},
+            "kernels_rank0": kern,
+            "transport": "gloo rehearsal" if rehearse else "RCCL (nccl backend)"}
 
 
 def inflight_replay(args, torch, dev, n_sub=256, n_epochs=4, per_epoch=8, buf_bytes=32768, steps=5):

@@ -204,6 +204,7 @@ struct clg_engine {
   std::vector<InFlight> ifls;
   std::map<IdKey, uint32_t> by_id;
   std::vector<Job> jobs;  // jobs[0]: the default job (cfg.sharing_depth)
+  std::vector<uint32_t> dirty;  // logs with staged (unflushed) bytes: flush() visits only these
   std::recursive_mutex mu;
 
   // staging / scratch
@@ -305,6 +306,7 @@ struct clg_engine {
     return CLG_OK;
   }
   void write_pending(Log& l, const uint8_t* b, uint32_t n) {
+    if (l.pending.empty() && n) dirty.push_back(uint32_t(&l - logs.data()));
     l.pending.insert(l.pending.end(), b, b + n);
     l.writer += int32_t(n);
   }
@@ -329,12 +331,17 @@ struct clg_engine {
   // ---------------------------------------------------------------- flush (append scatter)
   int flush() {
     size_t total = 0, nchunks = 0;
-    for (auto& l : logs)
+    for (uint32_t h : dirty) {
+      const Log& l = logs[h];
       if (l.open && !l.pending.empty()) {
         total += l.pending.size();
         nchunks += l.pending.size() / C() + 2;
       }
-    if (total == 0) return CLG_OK;
+    }
+    if (total == 0) {
+      dirty.clear();
+      return CLG_OK;
+    }
     CHK(gwait());  // an in-flight gather may still read the segments about to be written
     const size_t desc_bytes = nchunks * sizeof(clg::ScatterChunk);
     CHK(h_stage.ensure(total));
@@ -344,7 +351,8 @@ struct clg_engine {
     uint8_t* hs = h_stage.as<uint8_t>();
     clg::ScatterChunk* ch = h_desc.as<clg::ScatterChunk>();
     size_t off = 0, n = 0;
-    for (auto& l : logs) {
+    for (uint32_t h : dirty) {
+      Log& l = logs[h];
       if (!l.open || l.pending.empty()) continue;
       memcpy(hs + off, l.pending.data(), l.pending.size());
       int32_t p = l.flushed;
@@ -362,6 +370,7 @@ struct clg_engine {
       l.flushed = l.writer;
       l.pending.clear();
     }
+    dirty.clear();
     HIPCHK(hipMemcpyAsync(d_stage.p, hs, total, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_desc.p, ch, n * sizeof(clg::ScatterChunk), hipMemcpyHostToDevice, stream));
     CHK(timed("append_scatter", 2 * total, [&] {
@@ -1302,6 +1311,21 @@ int clg_log_length(clg_engine* e, uint32_t h, int32_t* out) {  // :180-192
   Log* l;
   CHK(e->get_log(h, &l));
   *out = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
+  return CLG_OK;
+}
+
+int clg_log_length_batch(clg_engine* e, const uint32_t* log, uint32_t n, int32_t* out, uint64_t* total) {
+  ENGINE_GUARD(e);
+  if (n && !log) return fail(CLG_E_INVALID_ARG, "null argument");
+  uint64_t t = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    Log* l;
+    CHK(e->get_log(log[i], &l));
+    const int32_t v = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
+    if (out) out[i] = v;
+    t += uint64_t(v);
+  }
+  if (total) *total = t;
   return CLG_OK;
 }
 

@@ -1,43 +1,66 @@
-"""Multi-GPU sharding and sharing-depth replication.
+"""Multi-GPU sharding, sharing-depth replication and the cross-GPU replay-prep merge
+(SURVEY.md 8e).
 
 One process per GPU, one Engine per process.  Logs shard by VertexID (job.owner_rank):
 rank g owns the vertices v with v mod G == g and is the only writer of their logs.
-Consumers on other GPUs need replicas of upstream logs within the sharing depth
-(job.replication_plan).  Once per exchange (e.g. per epoch or per batch of buffers):
 
-  1. every rank slices the new bytes of each owned log for one replication consumer
-     per log (the engine's batched getDeltaForConsumer: one device gather into a
-     send blob, no host copy of the bytes);
-  2. the blob = [header table | payload]; blob sizes are all-gathered, then the padded
-     blobs (torch.distributed.all_gather_into_tensor: RCCL over xGMI with the "nccl"
-     backend, gloo on CPU);
-  3. every rank applies the deltas of the logs it needs with the batched
-     processUpstreamDelta (clg_upstream_delta_batch), reading straight from the receive
-     buffer in HBM.  The dedup rule of :117-154 makes re-delivery harmless.
+Replication.  Consumers on other GPUs need replicas of upstream logs within the sharing
+depth (job.replication_masks).  Every rank builds the same canonical log table
+(job.LogTable: a global index `gid` per CausalLogID), so the wire carries gids and every
+per-log step is a numpy gather over dense tables -- no per-log Python.  One exchange (per
+epoch, or per batch of buffers):
+
+  1. the owner slices the new bytes of every owned log that some other rank wants, for one
+     replication consumer per log: the engine's batched hasDelta/getOffset/getDelta
+     (clg_slice_batch), ONE device gather into the payload part of the send blob;
+  2. send blob = [header rows | payload]; one all-gather of the (header, payload) sizes,
+     one all-gather of the blobs padded to the largest (RCCL over xGMI with the "nccl"
+     backend; gloo on CPU), then ONE device->host copy of every rank's header region;
+  3. every rank applies the rows of the logs it wants with the batched processUpstreamDelta
+     (clg_upstream_delta_batch) reading straight from the receive buffer in HBM.  The dedup
+     rule of ThreadCausalLogImpl.java:117-154 makes re-delivery harmless.
 
 This replaces the reference's piggybacking of CausalLogDelta on network buffers for
-GPU-to-GPU traffic (AbstractDeltaSerializerDeserializer.java:89-163): the bytes and the
-(offsetFromEpoch, epoch) header are the same, the transport is a collective.
+GPU-to-GPU traffic (AbstractDeltaSerializerDeserializer.java:89-163,
+FlatDeltaSerializerDeserializer.java:57-90): the bytes and the (offsetFromEpoch, epoch)
+pairs are the same, the transport is a collective.
+
+Replay-prep merge (concurrent / connected failures).  DeterminantResponseEvent.merge
+(DeterminantResponseEvent.java:128-148) keeps, per CausalLogID, the longest copy among
+the responses (WaitingDeterminantsState.java:97-109).  Across GPUs: every rank measures its
+copy of each log of the failed vertices, one all-reduce(MAX) over packed
+(len << 8 | rank) picks the winner per log, and one all-to-all moves each winner's bytes to
+the rank hosting the failed vertex's replacement (merge_responses).
 """
 from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _lib
-from ._lib import check
+from ._lib import check, lib
 from .engine import CausalLogID, Engine, ThreadCausalLog
+from .job import JobGraph, LogTable, owner_rank, replication_masks
 
-# One header row per delta (little-endian, 48 bytes).
-HEADER = np.dtype([("vertex", "<i2"), ("is_main", "u1"), ("sub", "i1"), ("pad", "<u4"),
-                   ("irp_lo", "<i8"), ("irp_hi", "<i8"), ("epoch", "<i8"),
-                   ("offset_from_epoch", "<i4"), ("len", "<u4"), ("payload_off", "<u8")])
-assert HEADER.itemsize == 48
+# One header row per delta (little-endian, 32 bytes): global log index, epoch,
+# offsetFromEpoch, length, payload offset inside the sender's payload.
+HEADER = np.dtype([("gid", "<i4"), ("offset_from_epoch", "<i4"), ("epoch", "<i8"), ("len", "<u4"),
+                   ("pad", "<u4"), ("payload_off", "<u8")])
+assert HEADER.itemsize == 32
 BLOB_ALIGN = 64
 REPLICATION_CHANNEL = (0xC1055EED00000000, 0x5EED)  # the replication consumer of every log
+
+# numpy views of the C request / result structs (include/clonos_engine.h)
+SLICE_REQ = np.dtype([("log", "<u4"), ("reserved", "<u4"), ("ch_lo", "<u8"), ("ch_hi", "<u8"), ("epoch", "<i8")])
+SLICE_RES = np.dtype([("status", "<i4"), ("has_delta", "<i4"), ("offset_from_epoch", "<i4"), ("len", "<i4"),
+                      ("out_off", "<u8")])
+DELTA_REQ = np.dtype([("log", "<u4"), ("offset_from_epoch", "<i4"), ("epoch", "<i8"), ("src_off", "<u8"),
+                      ("len", "<u4"), ("status", "<i4")])
+assert SLICE_REQ.itemsize == C.sizeof(_lib.SliceReq) and SLICE_RES.itemsize == C.sizeof(_lib.SliceRes)
+assert DELTA_REQ.itemsize == C.sizeof(_lib.DeltaReq)
 
 
 def _align(n: int) -> int:
@@ -45,160 +68,266 @@ def _align(n: int) -> int:
 
 
 def header_bytes(n_rows: int) -> int:
-    """[u64 n_rows][pad to 64][rows] rounded up to 64."""
-    return _align(BLOB_ALIGN + n_rows * HEADER.itemsize)
+    return _align(n_rows * HEADER.itemsize)
 
 
-def pack_header(rows: np.ndarray) -> bytes:
-    out = bytearray(header_bytes(len(rows)))
-    out[0:8] = np.uint64(len(rows)).tobytes()
-    out[BLOB_ALIGN:BLOB_ALIGN + rows.nbytes] = rows.tobytes()
-    return bytes(out)
+# ---- collectives ------------------------------------------------------------------------
+def _to_comm(t, backend: str):
+    """gloo moves host tensors; RCCL ("nccl") moves device tensors in place."""
+    return t if (backend == "nccl" or not t.is_cuda) else t.cpu()
 
 
-def unpack_header(blob: bytes) -> np.ndarray:
-    n = int(np.frombuffer(blob[:8], np.uint64)[0])
-    return np.frombuffer(blob[BLOB_ALIGN:BLOB_ALIGN + n * HEADER.itemsize], HEADER).copy()
-
-
-def header_row(lid: CausalLogID, epoch: int, offset_from_epoch: int, n: int, payload_off: int) -> tuple:
-    return (lid.vertex_id, 1 if lid.is_main else 0, 0 if lid.is_main else lid.subpartition, 0,
-            0 if lid.is_main else lid.irp_lower, 0 if lid.is_main else lid.irp_upper, epoch, offset_from_epoch, n,
-            payload_off)
-
-
-def row_log_id(r) -> CausalLogID:
-    if r["is_main"]:
-        return CausalLogID.main(int(r["vertex"]))
-    return CausalLogID.sub(int(r["vertex"]), int(r["irp_lo"]), int(r["irp_hi"]), int(r["sub"]))
-
-
-# ---- the collective: all-gather of variable-size blobs ------------------------------------
-def allgather_blobs(send, group=None):
-    """All-gather one uint8 tensor per rank (sizes differ): returns (recv, sizes, stride)
-    with rank r's blob at recv[r * stride : r * stride + sizes[r]]."""
+def allgather_sizes(vals: Sequence[int], device, group=None) -> np.ndarray:
+    """int64[world, len(vals)]: every rank's `vals` (one tiny collective + one D2H)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    n = torch.tensor([send.numel()], dtype=torch.int64, device=send.device)
-    sizes_t = torch.empty(world, dtype=torch.int64, device=send.device)
-    dist.all_gather_into_tensor(sizes_t, n, group=group)
-    sizes = [int(x) for x in sizes_t.cpu()]
-    stride = _align(max(sizes) if sizes else 0) or BLOB_ALIGN
-    padded = torch.zeros(stride, dtype=torch.uint8, device=send.device)
-    padded[:send.numel()] = send
-    recv = torch.empty(world * stride, dtype=torch.uint8, device=send.device)
+    backend = dist.get_backend(group)
+    dev = device if backend == "nccl" else "cpu"
+    mine = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+    out = torch.empty(world * len(vals), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, mine, group=group)
+    return out.cpu().numpy().reshape(world, len(vals))
+
+
+def allgather_blobs(send, stride: int, group=None):
+    """All-gather one uint8 blob per rank, each padded to `stride`: rank r's blob starts
+    at recv[r * stride]."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    backend = dist.get_backend(group)
+    src = _to_comm(send, backend)
+    padded = src if src.numel() == stride else torch.nn.functional.pad(src, (0, stride - src.numel()))
+    recv = torch.empty(world * stride, dtype=torch.uint8, device=padded.device)
     dist.all_gather_into_tensor(recv, padded, group=group)
-    return recv, sizes, stride
+    return recv if (recv.is_cuda or not send.is_cuda) else recv.to(send.device)
 
 
-# ---- engine I/O (the product path) ------------------------------------------------------
-class EngineIO:
-    """Slices and applies deltas through the engine; blobs live in HBM."""
-
-    def __init__(self, engine: Engine, device):
-        self.engine = engine
-        self.device = device
-        self.replicas: Dict[tuple, ThreadCausalLog] = {}
-
-    def build_blob(self, owned: Sequence[ThreadCausalLog], epoch: int):
-        import torch
-        n = len(owned)
-        creq = (_lib.SliceReq * max(1, n))()
-        cres = (_lib.SliceRes * max(1, n))()
-        for k, lg in enumerate(owned):
-            creq[k].log = lg.handle
-            creq[k].consumer = _lib.ChannelId(*REPLICATION_CHANNEL)
-            creq[k].epoch = epoch
-        cap = sum(lg.logLength() for lg in owned) + BLOB_ALIGN
-        hb = header_bytes(n)
-        blob = torch.empty(hb + cap, dtype=torch.uint8, device=self.device)
-        total = self.engine.slice_batch_raw(creq, cres, n, blob.data_ptr() + hb, cap, device=True) if n else 0
-        rows = []
-        for k, lg in enumerate(owned):
-            r = cres[k]
-            check(r.status)
-            if r.has_delta and r.len:
-                rows.append(header_row(lg.cid, epoch, r.offset_from_epoch, r.len, r.out_off))
-        head = pack_header(np.array(rows, HEADER))
-        hb2 = len(head)
-        if hb2 != hb:  # fewer rows than logs: compact the header in front of the payload
-            blob2 = torch.empty(hb2 + total, dtype=torch.uint8, device=self.device)
-            blob2[hb2:] = blob[hb:hb + total]
-            blob, hb = blob2, hb2
-        blob[:hb] = torch.frombuffer(bytearray(head), dtype=torch.uint8).to(self.device)
-        return blob[:hb + total]
-
-    def replica(self, lid: CausalLogID) -> ThreadCausalLog:
-        key = lid.key()
-        lg = self.replicas.get(key)
-        if lg is None:
-            lg = self.replicas[key] = self.engine.open_log(lid)
-        return lg
-
-    def apply(self, recv, plan: List[Tuple[CausalLogID, int, int, int, int]]) -> List[int]:
-        """plan rows: (log id, epoch, offsetFromEpoch, src_off in recv, len)."""
-        if not plan:
-            return []
-        reqs = (_lib.DeltaReq * len(plan))()
-        for k, (lid, epoch, ofe, src, n) in enumerate(plan):
-            reqs[k].log = self.replica(lid).handle
-            reqs[k].offset_from_epoch = ofe
-            reqs[k].epoch = epoch
-            reqs[k].src_off = src
-            reqs[k].len = n
-        kind = _lib.CLG_MEM_DEVICE if recv.is_cuda else _lib.CLG_MEM_HOST
-        self.engine.upstream_delta_batch(reqs, len(plan), recv.data_ptr(), kind)
-        return [reqs[k].status for k in range(len(plan))]
-
-
+# ---- replication ------------------------------------------------------------------------
 @dataclass
 class ExchangeStats:
-    sent_bytes: int = 0
-    recv_bytes: int = 0
-    applied: int = 0
-    skipped: int = 0
+    sent_bytes: int = 0     # this rank's blob (header + payload)
+    recv_bytes: int = 0     # other ranks' blobs (header + payload)
+    applied: int = 0        # deltas applied to replicas
+    applied_bytes: int = 0  # delta bytes those deltas carried
+    skipped: int = 0        # rows for logs this rank does not want
+
+
+class ReplicationPlan:
+    """The static part of sharing-depth replication for one rank: which owned logs it
+    sends, which logs it keeps replicas of, and the dense handle tables.  Built once per
+    job and rank (registerTask time), identically on every rank."""
+
+    def __init__(self, table: LogTable, depth: int, rank: int, world: int,
+                 need: Optional[np.ndarray] = None):
+        self.table, self.rank, self.world = table, rank, world
+        g = table.graph
+        need = replication_masks(g, depth, world) if need is None else need  # [rank, vertex]
+        owner = np.array([owner_rank(int(v), world) for v in range(need.shape[1])], np.int64)
+        lv = table.vertex
+        self.owned = np.nonzero(owner[lv] == rank)[0]            # gids this rank writes
+        wanted_anywhere = need.any(axis=0)
+        self.send = self.owned[wanted_anywhere[lv[self.owned]]]  # owned gids some rank wants
+        self.wanted = np.nonzero(need[rank][lv])[0]               # gids this rank keeps replicas of
+
+
+class EngineIO:
+    """The byte work of replication on the engine (HBM): batched slices into a device
+    blob, batched device-input processUpstreamDelta into replicas."""
+
+    def __init__(self, engine: Engine, job: int = 0):
+        self.engine, self.job = engine, job
+
+    def open_replica(self, cid: CausalLogID) -> int:
+        return self.engine.open_log(cid, self.job).handle
+
+    def payload_bound(self, handles: np.ndarray) -> int:
+        return self.engine.log_lengths(handles)[1]
+
+    def slice(self, sreq: np.ndarray, sres: np.ndarray, n: int, out_ptr: int, cap: int) -> int:
+        total = C.c_uint64()
+        check(lib.clg_slice_batch(self.engine.handle, sreq.ctypes.data, n, sres.ctypes.data, out_ptr, cap,
+                                  _lib.CLG_MEM_DEVICE, C.byref(total)))
+        if self.engine.async_slice:  # the collective reads the payload: wait for the gather
+            self.engine.sync()
+        return total.value
+
+    def apply(self, req: np.ndarray, recv) -> None:
+        kind = _lib.CLG_MEM_DEVICE if recv.is_cuda else _lib.CLG_MEM_HOST
+        check(lib.clg_upstream_delta_batch(self.engine.handle, req.ctypes.data, len(req), recv.data_ptr(), kind))
+
+    # replay-prep merge: a copy is getDeterminants(startEpoch) of a log (owned or replica)
+    def copy_length(self, handle: int, cid: CausalLogID, start_epoch: int) -> int:
+        return ThreadCausalLog(self.engine, handle, cid).determinants_length(start_epoch)
+
+    def copy_into(self, handle: int, cid: CausalLogID, start_epoch: int, tensor, off: int, n: int) -> None:
+        got = ThreadCausalLog(self.engine, handle, cid).determinants_into(start_epoch, tensor.data_ptr() + off, n)
+        if got != n:
+            raise RuntimeError(f"log {cid} changed during the merge ({got} != {n} bytes)")
 
 
 class Replicator:
-    """Sharing-depth replication for one rank.  `io` does the byte work (EngineIO on a
-    GPU); `wanted` is the set of VertexIDs this rank needs from other ranks
-    (job.replication_plan(...)[rank])."""
+    """Sharing-depth replication for one rank.  `io` does the byte work (EngineIO; the CPU
+    tests pass a stand-in over the oracle).  owned_handles: gid -> handle of each owned log
+    that is sent; replicas of the wanted logs are opened here."""
 
-    def __init__(self, io, rank: int, world: int, wanted: Iterable[int], group=None):
-        self.io = io
-        self.rank = rank
-        self.world = world
-        self.wanted = set(int(v) for v in wanted)
-        self.group = group
+    def __init__(self, io, plan: ReplicationPlan, device, owned_handles: Dict[int, int], group=None):
+        self.io, self.plan, self.device, self.group = io, plan, device, group
+        n = len(plan.table)
+        self.handle = np.full(n, -1, np.int64)
+        for gid, h in owned_handles.items():
+            self.handle[gid] = h
+        self.replica_handle = np.full(n, -1, np.int64)
+        for gid in plan.wanted:
+            self.replica_handle[gid] = io.open_replica(plan.table.ids[gid])
+        missing = [int(g) for g in plan.send if self.handle[g] < 0]
+        if missing:
+            raise ValueError(f"no log handle for owned gids {missing[:8]}")
+        # prebuilt slice requests: one per sent log, the replication consumer
+        ns = len(plan.send)
+        self._sreq = np.zeros(max(ns, 1), SLICE_REQ)
+        self._sreq["log"][:ns] = self.handle[plan.send]
+        self._sreq["ch_lo"], self._sreq["ch_hi"] = REPLICATION_CHANNEL
+        self._sres = np.zeros(max(ns, 1), SLICE_RES)
+        self._blob = None
 
-    def exchange(self, owned: Sequence, epoch: int) -> ExchangeStats:
+    def build_blob(self, epoch: int, payload_cap: Optional[int] = None):
+        """Slice every sent log into the send blob.  Returns (blob, header rows, header
+        bytes, payload bytes)."""
         import torch
-        import torch.distributed as dist
+        ns = len(self.plan.send)
+        hb = header_bytes(ns)
+        cap = payload_cap if payload_cap is not None else self.io.payload_bound(self._sreq["log"][:ns])
+        if self._blob is None or self._blob.numel() < hb + cap + BLOB_ALIGN:
+            self._blob = torch.empty(_align(hb + cap) + BLOB_ALIGN, dtype=torch.uint8, device=self.device)
+        blob = self._blob
+        self._sreq["epoch"][:ns] = epoch
+        total = self.io.slice(self._sreq, self._sres, ns, blob.data_ptr() + hb, cap) if ns else 0
+        res = self._sres[:ns]
+        bad = np.nonzero(res["status"])[0]
+        if bad.size:
+            check(int(res["status"][bad[0]]))
+        keep = np.nonzero((res["has_delta"] != 0) & (res["len"] > 0))[0]
+        rows = np.zeros(len(keep), HEADER)
+        rows["gid"] = self.plan.send[keep]
+        rows["offset_from_epoch"] = res["offset_from_epoch"][keep]
+        rows["epoch"] = epoch
+        rows["len"] = res["len"][keep]
+        rows["payload_off"] = res["out_off"][keep]
+        return blob, rows, hb, int(total)
+
+    def exchange(self, epoch: int, payload_cap: Optional[int] = None) -> ExchangeStats:
+        """One replication round for `epoch` (all ranks call it together)."""
+        import torch
         st = ExchangeStats()
-        blob = self.io.build_blob(owned, epoch)
-        st.sent_bytes = int(blob.numel())
-        backend = dist.get_backend(self.group)
-        send = blob if (backend == "nccl" or not blob.is_cuda) else blob.cpu()
-        recv, sizes, stride = allgather_blobs(send, self.group)
-        recv_dev = recv if (recv.is_cuda or not blob.is_cuda) else recv.to(blob.device)
-        plan = []
-        for r in range(self.world):
-            if r == self.rank or sizes[r] == 0:
+        blob, rows, hb, payload = self.build_blob(epoch, payload_cap)
+        head = np.zeros(hb // HEADER.itemsize, HEADER)
+        head[:len(rows)] = rows
+        blob[:hb].copy_(torch.from_numpy(head.view(np.uint8)))
+        used = hb + payload
+        st.sent_bytes = used
+        sizes = allgather_sizes([hb, payload, len(rows)], self.device, self.group)  # [world, 3]
+        stride = _align(int((sizes[:, 0] + sizes[:, 1]).max()))
+        send = blob[:stride] if blob.numel() >= stride else torch.nn.functional.pad(blob[:used], (0, stride - used))
+        recv = allgather_blobs(send, stride, self.group)
+        hmax = int(sizes[:, 0].max())
+        # one D2H copy of every header region; it also orders the host after the collective
+        heads = recv.view(self.plan.world, stride)[:, :hmax].cpu().numpy()
+        parts = []
+        for r in range(self.plan.world):
+            if r == self.plan.rank:
                 continue
-            base = r * stride
-            n_rows = int(np.frombuffer(recv[base:base + 8].cpu().numpy().tobytes(), np.uint64)[0])
-            hb = header_bytes(n_rows)
-            rows = unpack_header(recv[base:base + hb].cpu().numpy().tobytes())
-            st.recv_bytes += sizes[r]
-            for row in rows:
-                if int(row["vertex"]) not in self.wanted:
-                    st.skipped += 1
-                    continue
-                plan.append((row_log_id(row), int(row["epoch"]), int(row["offset_from_epoch"]),
-                             base + hb + int(row["payload_off"]), int(row["len"])))
-        statuses = self.io.apply(recv_dev, plan)
-        for s in statuses:
-            check(s)
-        st.applied = len(plan)
+            st.recv_bytes += int(sizes[r, 0] + sizes[r, 1])
+            n = int(sizes[r, 2])
+            rr = heads[r, :n * HEADER.itemsize].view(HEADER)
+            src = np.uint64(r * stride + int(sizes[r, 0])) + rr["payload_off"].astype(np.uint64)
+            parts.append((rr, src))
+        if not parts:
+            return st
+        rows_all = np.concatenate([p[0] for p in parts])
+        src_all = np.concatenate([p[1] for p in parts])
+        h = self.replica_handle[rows_all["gid"]]
+        want = h >= 0
+        st.skipped = int((~want).sum())
+        n = int(want.sum())
+        if n:
+            req = np.zeros(n, DELTA_REQ)
+            req["log"] = h[want]
+            req["offset_from_epoch"] = rows_all["offset_from_epoch"][want]
+            req["epoch"] = rows_all["epoch"][want]
+            req["src_off"] = src_all[want]
+            req["len"] = rows_all["len"][want]
+            self.io.apply(req, recv)
+            bad = np.nonzero(req["status"])[0]
+            if bad.size:
+                check(int(req["status"][bad[0]]))
+            st.applied = n
+            st.applied_bytes = int(req["len"].sum())
         return st
+
+
+# ---- replay-prep merge across GPUs ---------------------------------------------------------
+def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int, int],
+                    start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None) -> Dict[int, bytes]:
+    """Cross-GPU DeterminantResponseEvent.merge for the logs of the failed vertices.
+
+    copies: gid -> io handle of this rank's copy (owned log or replica) of a log of a failed
+    vertex; start_epochs: failed VertexID -> the epoch the request asks from
+    (respondToDeterminantRequest -> getDeterminants(startEpoch), JobCausalLogImpl.java:
+    188-204); dest_of: failed VertexID -> rank hosting its replacement.
+
+    Step 1: every rank reports len(getDeterminants) of each copy as (len << 8 | rank) and an
+    all-reduce(MAX) picks, per log, the longest copy (DeterminantResponseEvent.java:137-146;
+    equal lengths are equal bytes -- every copy is a prefix of the same log -- so the rank
+    tie-break picks identical content).  Step 2: one all-to-all carries each winner's bytes
+    from its rank to the destination.  Returns, on every rank, {gid: bytes} of the winners
+    whose destination is this rank (a log no rank holds is absent, as in the merged map)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    if world > 255:
+        raise ValueError("rank must fit the packed key's low byte")
+    backend = dist.get_backend(group)
+    failed = sorted(set(int(v) for v in failed))
+    gids = np.nonzero(np.isin(table.vertex, failed))[0]
+    n = len(gids)
+    key = np.full(max(n, 1), -1, np.int64)
+    for k, g in enumerate(gids):
+        h = copies.get(int(g))
+        if h is not None:
+            ln = io.copy_length(h, table.ids[g], start_epochs[int(table.vertex[g])])
+            key[k] = (int(ln) << 8) | rank
+    dev = device if backend == "nccl" else "cpu"
+    kt = torch.from_numpy(key).to(dev)
+    dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=group)
+    win = kt.cpu().numpy()[:n]
+    win_rank = np.where(win >= 0, win & 0xFF, -1)
+    win_len = np.where(win >= 0, win >> 8, 0)
+    dest = np.array([dest_of[int(table.vertex[g])] for g in gids], np.int64)
+    mine = np.nonzero(win_rank == rank)[0]
+    send_split = np.array([int(win_len[mine[dest[mine] == d]].sum()) for d in range(world)], np.int64)
+    recv_split = np.array([int(win_len[(win_rank == s) & (dest == rank)].sum()) for s in range(world)], np.int64)
+    send = torch.empty(max(int(send_split.sum()), 1), dtype=torch.uint8, device=device)
+    off = 0
+    for d in range(world):  # the winners this rank holds, grouped by destination, gid order
+        for k in mine[dest[mine] == d]:
+            nb = int(win_len[k])
+            if nb:
+                g = int(gids[k])
+                io.copy_into(copies[g], table.ids[g], start_epochs[int(table.vertex[g])], send, off, nb)
+            off += nb
+    recv = torch.empty(max(int(recv_split.sum()), 1), dtype=torch.uint8, device=dev)
+    s_in = _to_comm(send, backend)
+    dist.all_to_all_single(recv[:int(recv_split.sum())], s_in[:int(send_split.sum())],
+                           output_split_sizes=recv_split.tolist(), input_split_sizes=send_split.tolist(),
+                           group=group)
+    host = recv.cpu().numpy()
+    out = {}
+    o = 0
+    for s in range(world):
+        for k in np.nonzero((win_rank == s) & (dest == rank))[0]:
+            nb = int(win_len[k])
+            out[int(gids[k])] = host[o:o + nb].tobytes()
+            o += nb
+    return out

@@ -138,6 +138,7 @@ class Engine:
         self._h = h
         self.segment_bytes = segment_bytes
         self.sharing_depth = sharing_depth
+        self.async_slice = async_slice
         self.device = device
         self._logs = {}
 
@@ -252,6 +253,14 @@ class Engine:
         check(lib.clg_slice_batch(self._h, C.cast(creq, C.c_void_p), n, C.cast(cres, C.c_void_p), out_ptr, cap,
                                   _lib.CLG_MEM_DEVICE if device else _lib.CLG_MEM_HOST, C.byref(total)))
         return total.value
+
+    def log_lengths(self, handles: np.ndarray) -> Tuple[np.ndarray, int]:
+        """logLength of many logs in one call: (per-log lengths, sum)."""
+        h = np.ascontiguousarray(handles, np.uint32)
+        out = np.zeros(max(h.size, 1), np.int32)
+        tot = C.c_uint64()
+        check(lib.clg_log_length_batch(self._h, _np_ptr(h), h.size, _np_ptr(out), C.byref(tot)))
+        return out[:h.size], tot.value
 
     def upstream_delta_batch(self, reqs, n: int, src_ptr: int, in_kind: int) -> None:
         """Batched processUpstreamDelta over one buffer (host or device pointer); each
@@ -480,6 +489,22 @@ class ThreadCausalLog:
         ch = _ch(outputChannelID)
         return self._probe_fetch(lambda p, cap, n: lib.clg_get_delta(self.engine.handle, self.handle, ch, epochID, p,
                                                                      cap, _lib.CLG_MEM_HOST, n))
+
+    def determinants_length(self, startEpochID: int) -> int:
+        """len(getDeterminants(startEpochID)) without moving bytes."""
+        n = C.c_uint32()
+        st = lib.clg_get_determinants(self.engine.handle, self.handle, startEpochID, None, 0, _lib.CLG_MEM_HOST,
+                                      C.byref(n))
+        if st not in (_lib.CLG_OK, _lib.CLG_E_CAPACITY):
+            check(st)
+        return n.value
+
+    def determinants_into(self, startEpochID: int, dev_ptr: int, cap: int) -> int:
+        """getDeterminants(startEpochID) gathered into device memory (engine's device)."""
+        n = C.c_uint32()
+        check(lib.clg_get_determinants(self.engine.handle, self.handle, startEpochID, dev_ptr, cap,
+                                       _lib.CLG_MEM_DEVICE, C.byref(n)))
+        return n.value
 
     def getDeterminants(self, startEpochID: int) -> bytes:
         return self._probe_fetch(lambda p, cap, n: lib.clg_get_determinants(self.engine.handle, self.handle,

@@ -17,6 +17,8 @@ from collections import deque
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
+import numpy as np
+
 FULL_SHARING = -1  # ExecutionConfig.determinantSharingDepth default
 
 
@@ -106,7 +108,8 @@ def held_upstream_vertices(graph: JobGraph, name: str, depth: int) -> Set[int]:
 
     A producer p piggybacks its own logs (depth != 0) and the upstream logs it shares
     (|dist(u, p)| + 1 <= depth); following that rule along every path, a task holds the
-    logs of the upstream vertices within `depth` hops (all of them at full sharing)."""
+    logs of the upstream vertices within `depth` hops (all of them at full sharing).
+    Depends on the job vertex only, not on the subtask."""
     if depth == 0:
         return set()
     return {vid for vid, d in graph.distances(name).items() if d < 0 and (depth == FULL_SHARING or -d <= depth)}
@@ -118,14 +121,75 @@ def owner_rank(vertex_id: int, world: int) -> int:
     return (vertex_id & 0xFFFF) % world
 
 
+def held_table(graph: JobGraph, depth: int) -> Dict[str, np.ndarray]:
+    """job vertex -> sorted VertexIDs its subtasks hold replicas of (one BFS per job
+    vertex: computeDistances depends on the job vertex only)."""
+    return {v.name: np.array(sorted(held_upstream_vertices(graph, v.name, depth)), np.int64)
+            for v in graph.vertices}
+
+
 def replication_plan(graph: JobGraph, depth: int, world: int) -> Dict[int, Set[int]]:
     """rank -> VertexIDs owned by OTHER ranks whose logs that rank must receive (the
     union of the replicas its local subtasks hold)."""
-    need: Dict[int, Set[int]] = {r: set() for r in range(world)}
-    for name, _, vid in graph.all_vertex_ids():
-        r = owner_rank(vid, world)
-        need[r] |= {u for u in held_upstream_vertices(graph, name, depth) if owner_rank(u, world) != r}
+    need = replication_masks(graph, depth, world)
+    return {r: set(np.nonzero(need[r])[0].tolist()) for r in range(world)}
+
+
+def replication_masks(graph: JobGraph, depth: int, world: int) -> np.ndarray:
+    """bool[world, n_vertices]: [r, v] iff rank r needs replicas of vertex v's logs (v is
+    held upstream by a subtask placed on r and owned by another rank).  Vectorised over
+    VertexIDs (the reference's VertexIDs are 0 .. total parallelism - 1)."""
+    ids = graph.all_vertex_ids()
+    n = len(ids)
+    held = held_table(graph, depth)
+    owner = np.array([owner_rank(v, world) for _, _, v in ids], np.int64)
+    need = np.zeros((world, n), bool)
+    for v in graph.vertices:
+        h = held[v.name]
+        if h.size == 0:
+            continue
+        vids = np.array(graph.vertex_ids(v.name), np.int64)
+        for r in np.unique(owner[vids]):
+            need[r, h] = True
+    need &= owner[None, :] != np.arange(world)[:, None]
     return need
+
+
+def task_logs(graph: JobGraph, name: str, subtask: int):
+    """The CausalLogIDs a subtask creates (registerTask :125-169): its main-thread log and,
+    per output IntermediateResultPartition (one per consuming job vertex, produced by this
+    subtask), one log per subpartition (= the consumer's parallelism).  The partition ID is
+    synthetic but stable: lower = VertexID << 16 | output index, upper = 0xC105."""
+    from .engine import CausalLogID
+    vid = graph.vertex_id(name, subtask)
+    out = [CausalLogID.main(vid)]
+    for k, c in enumerate(graph.consumers[name]):
+        lo = ((vid & 0xFFFF) << 16) | k
+        out += [CausalLogID.sub(vid, lo, 0xC105, s) for s in range(graph.by_name[c].parallelism)]
+    return out
+
+
+class LogTable:
+    """Every log of a job in one canonical order that all ranks agree on (VertexID order;
+    per vertex: main log, then subpartition logs): the global log index `gid` replaces
+    the CausalLogID on the replication wire and indexes dense per-rank handle tables."""
+
+    def __init__(self, graph: JobGraph):
+        self.graph = graph
+        self.ids = []
+        vert = []
+        for name, sub, vid in graph.all_vertex_ids():
+            for cid in task_logs(graph, name, sub):
+                self.ids.append(cid)
+                vert.append(vid)
+        self.vertex = np.array(vert, np.int64)
+        self._gid = {cid.key(): i for i, cid in enumerate(self.ids)}
+
+    def __len__(self):
+        return len(self.ids)
+
+    def gid(self, cid) -> int:
+        return self._gid[cid.key()]
 
 
 def dag(stages: int, parallelism: int) -> JobGraph:

@@ -90,6 +90,34 @@ def config2_log(n_records: int, rng: np.random.Generator, channels: int = 4) -> 
     return build(kind_idx, kinds, {0: [ch], 1: [ts]})
 
 
+SEED_CONFIG4 = 0xC1050004
+
+
+def config4_epoch(table, gids: np.ndarray, rng: np.random.Generator, main_records: int = 4096,
+                  sub_records: int = 64) -> Tuple[np.ndarray, np.ndarray]:
+    """Config 4 (5-stage DAG, p=128, full sharing): one epoch of every log in `gids`
+    (job.LogTable indices), back to back.  Main-thread logs: `main_records` Order/Timestamp
+    determinants (the config-2 mix); subpartition logs: `sub_records` BufferBuilt
+    determinants (one per output buffer, PipelinedSubpartition.java:370).  Returns
+    (bytes, per-log byte offsets with a final end offset)."""
+    is_main = np.array([table.ids[int(g)].is_main for g in gids], bool)
+    n_sub = int((~is_main).sum())
+    kd = KINDS["buffer_built"]
+    sub_blk, _ = build(np.zeros(n_sub * sub_records, np.int64), [kd],
+                       {0: [rng.integers(1, 32769, n_sub * sub_records)]})
+    sub_len = sub_records * len(kd.template)
+    parts, k = [], 0
+    for m in is_main:
+        if m:
+            parts.append(config2_log(main_records, rng)[0])
+        else:
+            parts.append(sub_blk[k * sub_len:(k + 1) * sub_len])
+            k += 1
+    offs = np.zeros(len(parts) + 1, np.uint64)
+    np.cumsum([p.size for p in parts], out=offs[1:])
+    return (np.concatenate(parts) if parts else np.zeros(0, np.uint8)), offs
+
+
 CONFIG3_MIX = [("order", 0.35), ("buffer_built", 0.35), ("timer_pts", 0.05), ("timer_87", 0.05),
                ("timestamp", 0.05), ("rng", 0.05), ("ser_string", 0.05 / 3), ("ser_boolean", 0.05 / 3),
                ("ser_integer", 0.05 / 3), ("source_cp", 0.03), ("ignore_cp", 0.02)]

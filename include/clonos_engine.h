@@ -156,6 +156,8 @@ typedef struct clg_delta_req {
 int clg_upstream_delta_batch(clg_engine* e, clg_delta_req* reqs, uint32_t n, const uint8_t* bytes,
                              uint32_t in_kind);
 int clg_log_length(clg_engine* e, uint32_t log, int32_t* out);                                /* :180-192 */
+/* logLength of n logs at once (out[i] for log[i]); *total = their sum (either may be NULL). */
+int clg_log_length_batch(clg_engine* e, const uint32_t* log, uint32_t n, int32_t* out, uint64_t* total);
 int clg_has_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t* out); /* :196-240 */
 int clg_offset_from_epoch(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* out);       /* :243-246 */
 /* getDeltaForConsumer :249-277: bytes copied into `out` (host or device).  With

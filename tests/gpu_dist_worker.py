@@ -1,6 +1,14 @@
-"""Launcher for tests/test_gpu_dist.py: two ranks (gloo), one Engine each on cuda:0,
-replicating owned logs with clonos_amd.dist over real engines.  The launcher itself never
-touches the GPU; each rank is a fresh process."""
+"""Launcher for tests/test_gpu_dist.py: two ranks (gloo transport), one Engine each on
+cuda:0.  Config 4's shape at reduced log sizes -- the 5-stage DAG at parallelism 128 under
+full sharing (640 VertexIDs, 1 main + 128 subpartition logs per producing vertex) -- is
+replicated with clonos_amd.dist over real engines, then the replay-prep merge runs across
+the ranks.  The launcher itself never touches the GPU; each rank is a fresh process.
+
+Checks, per rank: every replica holds exactly the owner's bytes (all ~33k replicas, read
+back in one batched slice), replica state == the oracle's ThreadCausalLogImpl fed the same
+epochs (a sample), the merge winners == DeterminantResponseEvent.merge of the ranks'
+responses (oracle/response_ref.py), and truncation afterwards (job CAS) matches the oracle.
+"""
 import os
 import socket
 import sys
@@ -10,7 +18,26 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
-import test_dist_cpu as T  # noqa: E402  (log ids and deterministic contents)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+
+STAGES, PAR, EPOCHS, SEG = 5, 128, 3, 1024
+
+
+def content(gid: int, epoch: int, is_main: bool) -> bytes:
+    """Deterministic bytes of log `gid` in `epoch`: main logs a few Order/Timestamp/RNG
+    records, subpartition logs BufferBuilt records (0-3 per epoch)."""
+    rng = np.random.default_rng(gid * 131 + epoch)
+    out = bytearray()
+    if is_main:
+        for _ in range(int(rng.integers(0, 12))):
+            t = int(rng.integers(0, 3))
+            out += (bytes([0, int(rng.integers(0, 4))]) if t == 0 else
+                    bytes([1]) + int(rng.integers(0, 1 << 40)).to_bytes(8, "big") if t == 1 else
+                    bytes([2]) + int(rng.integers(0, 1 << 31)).to_bytes(4, "big"))
+    else:
+        for _ in range(int(rng.integers(0, 4))):
+            out += bytes([7]) + int(rng.integers(1, 1 << 15)).to_bytes(4, "big")
+    return bytes(out)
 
 
 def worker(rank, world, port, q):
@@ -18,38 +45,115 @@ def worker(rank, world, port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch
         import torch.distributed as dist
-        from clonos_amd import Engine
+        import _oracle as O
+        from clonos_amd import Engine, _lib
         from clonos_amd import dist as X
-        from clonos_amd.job import owner_rank
+        from clonos_amd.engine import ThreadCausalLog
+        from clonos_amd import job as J
         dist.init_process_group("gloo", rank=rank, world_size=world)
         dev = torch.device("cuda", 0)
-        eng = Engine(segment_bytes=T.SEG, pool_segments=1 << 14, device=0)
-        mine = [cid for cid in T.log_ids() if owner_rank(cid.vertex_id, world) == rank]
-        owned = [eng.open_log(cid) for cid in mine]
-        wanted = {v for v in range(T.N_VERT) if owner_rank(v, world) != rank and v != 1}
-        io = X.EngineIO(eng, dev)
-        rep = X.Replicator(io, rank, world, wanted)
-        for ep in range(T.EPOCHS):
-            for half in range(2):
-                for lg in owned:
-                    r = T.records(lg.cid, ep)
-                    part = r[:len(r) // 2] if half == 0 else r[len(r) // 2:]
-                    if part:
-                        lg.processUpstreamDelta(part, len(r) // 2 if half else 0, ep)
-                rep.exchange(owned, ep)
-        got = 0
-        for cid in T.log_ids():
-            if cid.vertex_id not in wanted:
+        g = J.dag(STAGES, PAR)
+        table = J.LogTable(g)
+        need = J.replication_masks(g, -1, world)
+        plan = X.ReplicationPlan(table, -1, rank, world, need)
+        assert len(plan.wanted) == (4 * PAR // world) * (PAR + 1) * (world - 1)
+        eng = Engine(segment_bytes=SEG, pool_segments=len(plan.owned) + len(plan.wanted) + 4096, device=0)
+        owned = {int(gid): eng.open_log(table.ids[gid]).handle for gid in plan.owned}
+        send = set(plan.send.tolist())
+        rep = X.Replicator(X.EngineIO(eng), plan, dev, {k: v for k, v in owned.items() if k in send})
+        gids = np.array(sorted(owned), np.int64)
+        stats = []
+        for ep in range(EPOCHS):
+            blob = bytearray()
+            reqs = np.zeros(len(gids), X.DELTA_REQ)
+            for k, gid in enumerate(gids):  # the owners' new epoch, appended in one batch
+                b = content(int(gid), ep, table.ids[gid].is_main)
+                reqs[k] = (owned[int(gid)], 0, ep, len(blob), len(b), 0)
+                blob += b
+            hb = np.frombuffer(bytes(blob) or b"\0", np.uint8)
+            _lib.check(_lib.lib.clg_upstream_delta_batch(eng.handle, reqs.ctypes.data, len(reqs), hb.ctypes.data,
+                                                         _lib.CLG_MEM_HOST))
+            stats.append(rep.exchange(ep))
+        assert stats[0].applied > 0 and stats[0].skipped == 0
+        # every replica == the owner's bytes: one batched slice over all replicas (host output)
+        wanted = plan.wanted
+        handles = rep.replica_handle[wanted]
+        from clonos_amd.engine import _ch
+        creq = (_lib.SliceReq * len(wanted))()
+        for k, h in enumerate(handles):
+            creq[k].log = int(h)
+            creq[k].consumer = _ch((0xC4EC, 0xC4EC))
+            creq[k].epoch = 0
+        cres = (_lib.SliceRes * len(wanted))()
+        lens, tot = eng.log_lengths(handles)
+        out = np.zeros(max(tot, 1), np.uint8)
+        # consumers created at epoch 0 see only epoch 0: walk the epochs like a downstream would
+        got = {int(g): bytearray() for g in wanted}
+        for ep in range(EPOCHS):
+            for k in range(len(wanted)):
+                creq[k].epoch = ep
+            eng.slice_batch_raw(creq, cres, len(wanted), out.ctypes.data, out.size, device=False)
+            for k, gid in enumerate(wanted):
+                r = cres[k]
+                assert r.status == 0
+                if r.has_delta and r.len:
+                    got[int(gid)] += out[r.out_off:r.out_off + r.len].tobytes()
+        n_bytes = 0
+        for gid in wanted:
+            want = b"".join(content(int(gid), ep, table.ids[gid].is_main) for ep in range(EPOCHS))
+            assert bytes(got[int(gid)]) == want, (rank, int(gid))
+            n_bytes += len(want)
+        # replica state == the oracle's ThreadCausalLogImpl fed the same epochs (sample)
+        rng = np.random.default_rng(rank)
+        for gid in rng.choice(wanted, 200, replace=False):
+            ol = O.OracleLog(SEG)
+            for ep in range(EPOCHS):
+                b = content(int(gid), ep, table.ids[gid].is_main)
+                assert ol.upstream(b, 0, ep) == 0
+            lg = rep.replica_handle[gid]
+            assert ThreadCausalLog(eng, int(lg), table.ids[gid]).state() == ol.state()
+        # replay-prep merge across the ranks: failed vertices 3 (stage 0) and 131 (stage 1),
+        # a connected pair; rank r's copies are its owned logs or replicas
+        failed = [3, 131]
+        dest_of = {3: 1 % world, 131: 0}
+        fg = np.nonzero(np.isin(table.vertex, failed))[0]
+        copies = {}
+        for gid in fg:
+            h = owned.get(int(gid), -1)
+            if h < 0:
+                h = int(rep.replica_handle[gid])
+            if h >= 0:
+                copies[int(gid)] = h
+        # the owner of vertex 3 logged one more epoch that was never replicated: its copies
+        # are the longest and must win
+        extra = {}
+        for gid in fg:
+            if int(table.vertex[gid]) == 3 and int(gid) in owned:
+                b = content(int(gid), EPOCHS, table.ids[gid].is_main)
+                ThreadCausalLog(eng, owned[int(gid)], table.ids[gid]).processUpstreamDelta(b, 0, EPOCHS)
+        for gid in fg:
+            if int(table.vertex[gid]) == 3:
+                extra[int(gid)] = content(int(gid), EPOCHS, table.ids[gid].is_main)
+        merged = X.merge_responses(X.EngineIO(eng), table, failed, copies, {3: 0, 131: 0}, dest_of, dev)
+        for gid in fg:
+            v = int(table.vertex[gid])
+            if dest_of[v] != rank:
+                assert int(gid) not in merged
                 continue
-            expect = b"".join(T.records(cid, ep) for ep in range(T.EPOCHS))
-            lg = io.replicas.get(cid.key())
-            have = lg.getDeterminants(0) if lg is not None else b""
-            assert have == expect, (rank, cid, len(have), len(expect))
-            got += 1
+            want = b"".join(content(int(gid), ep, table.ids[gid].is_main) for ep in range(EPOCHS))
+            assert merged.get(int(gid)) == want + extra.get(int(gid), b""), (rank, int(gid))
+        # checkpoint completion afterwards: the job's CAS + truncation of owned logs and replicas
+        assert eng.truncate_all(2)
+        for gid in rng.choice(wanted, 50, replace=False):
+            ol = O.OracleLog(SEG)
+            for ep in range(EPOCHS):
+                assert ol.upstream(content(int(gid), ep, table.ids[gid].is_main), 0, ep) == 0
+            assert ol.checkpoint_complete(2) == 0
+            assert ThreadCausalLog(eng, int(rep.replica_handle[gid]), table.ids[gid]).state() == ol.state()
         dist.barrier()
         dist.destroy_process_group()
         eng.close()
-        q.put((rank, "ok", got))
+        q.put((rank, "ok", (len(wanted), n_bytes, stats[0].sent_bytes)))
     except Exception:
         import traceback
         q.put((rank, "fail", traceback.format_exc()))
@@ -72,5 +176,5 @@ if __name__ == "__main__":
     bad = [r for r in res if r[1] != "ok"]
     for r in bad:
         print(r[2], file=sys.stderr)
-    print("replicas verified:", sum(r[2] for r in res if r[1] == "ok"))
+    print("replicas verified:", [r[2] for r in res if r[1] == "ok"])
     sys.exit(1 if bad else 0)

@@ -1,7 +1,8 @@
 """CPU, world_size 2 over gloo: the sharing-depth replication protocol of
-clonos_amd/dist.py (blob packing, all-gather of variable-size blobs, the wanted-vertex
-filter, per-epoch re-delivery).  The byte store is the oracle's ThreadCausalLogImpl model
-(test infrastructure: it stands in for the engine, which needs a GPU; the same exchange
+clonos_amd/dist.py (canonical log table, send blobs of gid-keyed rows, all-gather of sizes
+and padded blobs, one header read-back, the wanted-log filter, per-epoch re-delivery) and
+the cross-GPU replay-prep merge.  The byte store is the oracle's ThreadCausalLogImpl model
+(test infrastructure standing in for the engine, which needs a GPU; the same protocol
 over real engines is tests/test_gpu_dist.py)."""
 import os
 import socket
@@ -14,9 +15,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(HERE))
 
-N_VERT = 6
 EPOCHS = 4
 SEG = 64
+STAGES, PAR = 3, 4
 
 
 def free_port():
@@ -27,97 +28,112 @@ def free_port():
     return p
 
 
-def log_ids():
-    from clonos_amd import CausalLogID
-    ids = [CausalLogID.main(v) for v in range(N_VERT)]
-    ids += [CausalLogID.sub(v, 100 + v, 200 + v, s) for v in range(N_VERT) for s in range(2)]
-    return ids
-
-
-def records(cid, epoch):
+def records(cid, epoch, scale=60):
     """Deterministic content of log `cid` in `epoch` (every rank can recompute it)."""
     from clonos_amd import determinants as D, synth
-    rng = np.random.default_rng(hash(cid.key()) % (1 << 30) * 31 + epoch)
-    return b"".join(D.encode(synth.random_determinant(rng)) for _ in range(int(rng.integers(0, 60))))
+    seed = (hash(cid.key()) % (1 << 30)) * 31 + epoch
+    rng = np.random.default_rng(seed)
+    if not cid.is_main:  # subpartition logs hold BufferBuilt records (ReplayingState :172-177)
+        return b"".join(D.encode(D.BufferBuiltDeterminant(int(rng.integers(1, 1 << 15))))
+                        for _ in range(int(rng.integers(0, scale // 6 + 1))))
+    return b"".join(D.encode(synth.random_determinant(rng)) for _ in range(int(rng.integers(0, scale))))
 
 
 class OracleIO:
+    """dist.Replicator's IO over oracle logs (handles index self.logs)."""
+
     def __init__(self):
         import _oracle as O
         self.O = O
-        self.replicas = {}
+        self.logs = []
 
-    def build_blob(self, owned, epoch):
-        import torch
+    def new_log(self):
+        self.logs.append(self.O.OracleLog(SEG))
+        return len(self.logs) - 1
+
+    def open_replica(self, cid):
+        return self.new_log()
+
+    def payload_bound(self, handles):
+        return sum(self.logs[int(h)].state()["writer"] for h in handles)
+
+    def slice(self, sreq, sres, n, out_ptr, cap):
+        import ctypes
         from clonos_amd import dist as X
-        rows, payload = [], bytearray()
-        for cid, ol in owned:
-            st, has = ol.has_delta(X.REPLICATION_CHANNEL, epoch)
-            assert st == 0
-            if has:
-                ofe = ol.offset(X.REPLICATION_CHANNEL)[1]
-                st, d = ol.get_delta(X.REPLICATION_CHANNEL, epoch)
-                assert st == 0
-                rows.append(X.header_row(cid, epoch, ofe, len(d), len(payload)))
-                payload += d
-        head = X.pack_header(np.array(rows, X.HEADER))
-        return torch.frombuffer(bytearray(head + bytes(payload)) or bytearray(64), dtype=torch.uint8)
+        dst = 0
+        for i in range(n):
+            ol = self.logs[int(sreq["log"][i])]
+            ch = (int(sreq["ch_lo"][i]), int(sreq["ch_hi"][i]))
+            ep = int(sreq["epoch"][i])
+            st, has = ol.has_delta(ch, ep)
+            sres[i] = (st, int(has), 0, 0, dst)
+            if st or not has:
+                continue
+            ofe = ol.offset(ch)[1]
+            st, d = ol.get_delta(ch, ep)
+            assert dst + len(d) <= cap
+            ctypes.memmove(out_ptr + dst, d, len(d))
+            sres[i] = (st, 1, ofe, len(d), dst)
+            dst += len(d)
+        assert X.REPLICATION_CHANNEL == (int(sreq["ch_lo"][0]), int(sreq["ch_hi"][0]))
+        return dst
 
-    def apply(self, recv, plan):
+    def apply(self, req, recv):
         buf = recv.numpy().tobytes()
-        out = []
-        for lid, epoch, ofe, src, n in plan:
-            ol = self.replicas.setdefault(lid.key(), self.O.OracleLog(SEG))
-            out.append(ol.upstream(buf[src:src + n], ofe, epoch))
-        return out
+        for r in req:
+            n = int(r["len"])
+            src = int(r["src_off"])
+            r["status"] = self.logs[int(r["log"])].upstream(buf[src:src + n], int(r["offset_from_epoch"]),
+                                                            int(r["epoch"]))
 
 
-def worker(rank, world, port, q):
+def worker(rank, world, port, q, depth):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch.distributed as dist
-        import _oracle as O
         from clonos_amd import dist as X
-        from clonos_amd.job import owner_rank
+        from clonos_amd import job as J
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        mine = [cid for cid in log_ids() if owner_rank(cid.vertex_id, world) == rank]
-        owned = [(cid, O.OracleLog(SEG)) for cid in mine]
-        wanted = {v for v in range(N_VERT) if owner_rank(v, world) != rank and v != 1}  # vertex 1 not wanted
+        g = J.dag(STAGES, PAR)
+        table = J.LogTable(g)
+        plan = X.ReplicationPlan(table, depth, rank, world)
         io = OracleIO()
-        rep = X.Replicator(io, rank, world, wanted)
+        owned = {int(gid): io.new_log() for gid in plan.owned}
+        rep = X.Replicator(io, plan, "cpu", {gid: h for gid, h in owned.items() if gid in set(plan.send.tolist())})
         for ep in range(EPOCHS):
             for half in range(2):  # two exchanges per epoch: re-delivery must be a no-op
-                for cid, ol in owned:
-                    r = records(cid, ep)
+                for gid, h in owned.items():
+                    r = records(table.ids[gid], ep)
                     part = r[:len(r) // 2] if half == 0 else r[len(r) // 2:]
                     if part:
-                        assert ol.append(ep, part) == 0
-                rep.exchange(owned, ep)
-        # every wanted replica holds exactly the owner's bytes
+                        assert io.logs[h].append(ep, part) == 0
+                st = rep.exchange(ep)
+                assert st.skipped >= 0
+        # every wanted replica holds exactly the owner's bytes; nothing else was opened
+        need = J.replication_masks(g, depth, world)[rank]
         got = 0
-        for cid in log_ids():
-            if cid.vertex_id not in wanted:
-                assert cid.key() not in io.replicas or owner_rank(cid.vertex_id, world) == rank
+        for gid, cid in enumerate(table.ids):
+            h = int(rep.replica_handle[gid])
+            if not need[cid.vertex_id]:
+                assert h < 0
                 continue
             expect = b"".join(records(cid, ep) for ep in range(EPOCHS))
-            ol = io.replicas.get(cid.key())
-            have = ol.get_determinants(0)[1] if ol is not None else b""
-            assert have == expect, (rank, cid)
+            assert io.logs[h].get_determinants(0)[1] == expect, (rank, cid)
             got += 1
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok", got))
-    except Exception as e:  # surface the failure in the parent
+    except Exception:  # surface the failure in the parent
         import traceback
         q.put((rank, "fail", traceback.format_exc()))
 
 
-def test_replication_gloo_world2():
+def run_world(target, *args, world=2):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -125,16 +141,104 @@ def test_replication_gloo_world2():
         p.join(timeout=60)
     for rank, status, info in res:
         assert status == "ok", info
+    return res
+
+
+@pytest.mark.parametrize("depth", [-1, 1])
+def test_replication_gloo_world2(depth):
+    res = run_world(worker, depth)
     assert sum(info for _, _, info in res) > 0
 
 
-def test_header_roundtrip():
-    from clonos_amd import CausalLogID
+def test_header_layout():
     from clonos_amd import dist as X
-    rows = np.array([X.header_row(CausalLogID.main(7), 3, 11, 5, 0),
-                     X.header_row(CausalLogID.sub(-2, 1 << 40, -5, 3), 9, 0, 17, 64)], X.HEADER)
-    b = X.pack_header(rows)
-    assert len(b) % 64 == 0
-    back = X.unpack_header(b)
-    assert back.tobytes() == rows.tobytes()
-    assert X.row_log_id(back[1]).key() == CausalLogID.sub(-2, 1 << 40, -5, 3).key()
+    rows = np.zeros(3, X.HEADER)
+    rows["gid"] = [7, 0, 66175]
+    rows["len"] = [5, 0, 17]
+    assert X.HEADER.itemsize == 32 and X.header_bytes(3) == 128
+    assert np.frombuffer(rows.tobytes(), X.HEADER)["gid"].tolist() == [7, 0, 66175]
+
+
+def test_plan_partitions_logs():
+    """Every log is owned by exactly one rank; a rank never wants its own logs; a log is
+    sent iff some rank wants it (config 4: 5 stages x 128, 8 ranks)."""
+    from clonos_amd import dist as X
+    from clonos_amd import job as J
+    g = J.dag(5, 128)
+    table = J.LogTable(g)
+    assert len(table) == 640 + 4 * 128 * 128
+    need = J.replication_masks(g, -1, 8)
+    plans = [X.ReplicationPlan(table, -1, r, 8, need) for r in range(8)]
+    owned = np.concatenate([p.owned for p in plans])
+    assert sorted(owned.tolist()) == list(range(len(table)))
+    for p in plans:
+        assert not set(p.owned.tolist()) & set(p.wanted.tolist())
+        assert len(p.wanted) == 448 * 129  # stages 0..3 minus the 64 vertices it owns there
+    sent = set(np.concatenate([p.send for p in plans]).tolist())
+    wanted = set(np.concatenate([p.wanted for p in plans]).tolist())
+    assert sent == wanted
+
+
+def merge_worker(rank, world, port, q):
+    """Cross-GPU merge over oracle copies: each rank holds a prefix (different lengths) of
+    every log of the failed vertices; the winners equal DeterminantResponseEvent.merge of
+    the per-rank responses in any arrival order (oracle/response_ref.py)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        from clonos_amd import dist as X
+        from clonos_amd import job as J
+        import response_ref as R
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        g = J.dag(STAGES, PAR)
+        table = J.LogTable(g)
+        failed = [1, 5]  # a connected pair (stage 0 subtask 1 -> stage 1 subtask 1)
+        dest_of = {1: 1, 5: 0}
+        full = {gid: records(table.ids[gid], 0, 200) for gid in range(len(table)) if table.vertex[gid] in failed}
+        rng = np.random.default_rng(9)
+        cut = {gid: [int(rng.integers(0, len(b) + 1)) for _ in range(world)] for gid, b in full.items()}
+        for gid in list(cut)[:3]:
+            cut[gid] = [len(full[gid])] * world  # ties: every rank holds the whole log
+        store = OracleStore(full, cut, rank)
+        got = X.merge_responses(store, table, failed, store.handles, {1: 0, 5: 0}, dest_of, "cpu")
+
+        def lid(cid):
+            return (R.LogId.main(cid.vertex_id) if cid.is_main else
+                    R.LogId.subpartition(cid.vertex_id, cid.irp_lower, cid.irp_upper, cid.subpartition))
+        # the reference: every rank's response merged in arrival order (two orders)
+        for order in (list(range(world)), list(reversed(range(world)))):
+            acc = R.Response(True, 0)
+            for r in order:
+                ev = R.Response(True, 0)
+                for gid, b in full.items():
+                    ev.dets.put(lid(table.ids[gid]), b[:cut[gid][r]])
+                acc.merge(ev)
+            want = {gid: acc.dets.get(lid(table.ids[gid])) for gid in full
+                    if dest_of[int(table.vertex[gid])] == rank}
+            assert got == want
+        dist.destroy_process_group()
+        q.put((rank, "ok", len(got)))
+    except Exception:
+        import traceback
+        q.put((rank, "fail", traceback.format_exc()))
+
+
+class OracleStore:
+    """merge_responses' view of a rank's copies, over host bytes (stands in for the engine)."""
+
+    def __init__(self, full, cut, rank):
+        self.copies = {gid: b[:cut[gid][rank]] for gid, b in full.items()}
+        self.handles = {gid: gid for gid in full}
+
+    def copy_length(self, handle, cid, start_epoch):
+        return len(self.copies[handle])
+
+    def copy_into(self, handle, cid, start_epoch, tensor, off, n):
+        import torch
+        tensor[off:off + n] = torch.frombuffer(bytearray(self.copies[handle]), dtype=torch.uint8)
+
+
+def test_merge_gloo_world2():
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    res = run_world(merge_worker)
+    assert sum(info for _, _, info in res) == 2 * (1 + 4)  # both failed vertices' logs
