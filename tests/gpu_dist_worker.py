@@ -75,29 +75,10 @@ def worker(rank, world, port, q):
                                                          _lib.CLG_MEM_HOST))
             stats.append(rep.exchange(ep))
         assert stats[0].applied > 0 and stats[0].skipped == 0
-        # every replica == the owner's bytes: one batched slice over all replicas (host output)
+        # every replica == the owner's bytes (getDeterminants from the first epoch)
         wanted = plan.wanted
-        handles = rep.replica_handle[wanted]
-        from clonos_amd.engine import _ch
-        creq = (_lib.SliceReq * len(wanted))()
-        for k, h in enumerate(handles):
-            creq[k].log = int(h)
-            creq[k].consumer = _ch((0xC4EC, 0xC4EC))
-            creq[k].epoch = 0
-        cres = (_lib.SliceRes * len(wanted))()
-        lens, tot = eng.log_lengths(handles)
-        out = np.zeros(max(tot, 1), np.uint8)
-        # consumers created at epoch 0 see only epoch 0: walk the epochs like a downstream would
-        got = {int(g): bytearray() for g in wanted}
-        for ep in range(EPOCHS):
-            for k in range(len(wanted)):
-                creq[k].epoch = ep
-            eng.slice_batch_raw(creq, cres, len(wanted), out.ctypes.data, out.size, device=False)
-            for k, gid in enumerate(wanted):
-                r = cres[k]
-                assert r.status == 0
-                if r.has_delta and r.len:
-                    got[int(gid)] += out[r.out_off:r.out_off + r.len].tobytes()
+        got = {int(gid): ThreadCausalLog(eng, int(rep.replica_handle[gid]), table.ids[gid]).getDeterminants(0)
+               for gid in wanted}
         n_bytes = 0
         for gid in wanted:
             want = b"".join(content(int(gid), ep, table.ids[gid].is_main) for ep in range(EPOCHS))
