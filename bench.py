@@ -266,7 +266,9 @@ def main():
                                       "next decode on a second stream)", "achieved": round(step_gbs, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
             "slice": {"algo_bytes": slice_bytes},
-            "decode_path": "robust (fused aborted)" if "decode_fallback" in stats else "fused single-pass",
+            "decode_path": ("robust (fast path aborted)" if "decode_fallback" in stats else
+                            "one-pass (k_decode_one)" if "decode_one" in stats else
+                            "three-pass (count -> scan -> emit)"),
             "kernels": kern,
             "kernels_isolated": kern_iso,
             "roofline": roof,

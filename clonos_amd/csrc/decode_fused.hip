@@ -345,6 +345,174 @@ __device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t re, uint32
   return r;
 }
 
+struct SpecR {
+  Bits sb, wb;     // followed starts in the region / wide ones (registers)
+  uint32_t first;  // first position >= rs
+  uint32_t exit;   // first position >= re
+  uint32_t bad;    // 1 + last position skipped inside the region, 0 if none
+};
+
+// Speculative length of a TimerTrigger (tg 4) / SourceCheckpoint (tg 5) at q: only the
+// bytes that decide the length are read (type / hasRef byte, then the name / reference
+// length when there is one); 0 (step one byte) for an ordinal decodeNext would reject or a
+// length past kZSpecMax or the span end.  Speculation only: the true chain re-checks every
+// record with the full rules (zlen_var).
+__device__ __forceinline__ uint32_t zspec_var(const uint32_t* T, uint32_t q, uint32_t end_a, uint32_t tg) {
+  const bool tt = tg == CLG_TAG_TIMER_TRIGGER;
+  const uint32_t b = zb8(T, q + (tt ? 13u : 22u));  // TT type ordinal / SC hasRef
+  uint32_t L, var_at;
+  bool var;
+  if (tt) {
+    L = b < 6u ? 14u : (b == 6u ? 18u : 0u);
+    var = b == 6u;
+    var_at = q + 14u;
+  } else {
+    const uint32_t ord = zb8(T, q + 21u);
+    L = ord > 1u ? 0u : (b ? 27u : 23u);
+    var = ord <= 1u && b;
+    var_at = q + 23u;
+  }
+  if (var) {  // a name / reference follows: its big-endian length
+    const uint32_t n = zbe32(T, var_at);
+    L = n <= (uint32_t)kZSpecMax - L ? L + n : 0u;
+  }
+  return q + L <= end_a ? L : 0u;
+}
+
+template <bool J>
+__device__ __forceinline__ uint32_t spec_len_fast(const uint32_t* T, uint32_t q, uint32_t end_a, bool safe, const JL& jl,
+                                                  bool* wide) {
+  constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16 | (J ? 0x40u : 0u) << 24;  // tags 0..3
+  constexpr uint32_t kHi = 0x40u | 0x40u << 8 | 0x40u << 16 | 5u << 24;       // tags 4..7
+  const uint32_t tg = zb8(T, q);
+  const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
+  uint32_t L = c;
+  *wide = false;
+  if (c & 0x40u) {  // rare: the length needs fields of the record
+    *wide = true;
+    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
+      L = 13;
+    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
+      L = jl_len(jl, q);
+      L = L <= (uint32_t)kZSpecMax ? L : 0u;
+    } else {
+      L = zspec_var(T, q, end_a, tg);
+    }
+  }
+  if (!safe) L = q + L <= end_a ? L : 0u;
+  return L;
+}
+
+template <bool J>
+__device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
+                                                uint32_t r0, const JL& jl) {
+  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
+  const bool safe = re + 16u <= end_a;
+  uint32_t q = ws;
+  bool w;
+  while (q < rs) {
+    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
+    q += L > 1u ? L : 1u;
+  }
+  s.first = q;
+  const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
+  while (q < mid) {
+    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
+    const uint64_t m = (uint64_t)(L ? 1u : 0u) << (q & 63u);
+    s.sb.lo |= m;
+    if (w) s.wb.lo |= m;
+    s.bad = L ? s.bad : q + 1u;
+    q += L > 1u ? L : 1u;
+  }
+  while (q < re) {
+    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
+    const uint64_t m = (uint64_t)(L ? 1u : 0u) << (q & 63u);
+    s.sb.hi |= m;
+    if (w) s.wb.hi |= m;
+    s.bad = L ? s.bad : q + 1u;
+    q += L > 1u ? L : 1u;
+  }
+  s.exit = q;
+  return s;
+}
+
+// Canonical chain through region: the speculative rule from entry e merged with the
+// region's speculative chain (same rule, so meeting means identical from there on).
+template <bool J>
+__device__ __forceinline__ uint32_t canon_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
+                                                 const SpecR& s, const JL& jl) {
+  if (e >= re) return e;
+  uint32_t p = e, q = s.first;
+  for (;;) {
+    if (p == q) return s.exit;
+    if (p >= re) return p;
+    bool w;
+    const uint32_t x = p < q ? p : q;
+    const uint32_t L = spec_len_fast<J>(T, x, end_a, false, jl, &w);
+    const uint32_t nx = x + (L > 1u ? L : 1u);
+    if (p < q) p = nx; else q = nx;
+  }
+}
+
+// True chain from entry e (e >= rs) merged with the speculative chain: walk until the true
+// chain lands on a speculative start past the speculative chain's last skip.
+template <bool J>
+__device__ __forceinline__ Res merge_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s,
+                                            const JL& jl) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  if (e >= re) return r;
+  uint32_t p = e;
+  Bits pb{0, 0}, pw{0, 0};
+  for (;; ++r.steps) {
+    if (p >= re) break;
+    const uint32_t i = p & 127u;
+    const uint64_t word = i < 64u ? s.sb.lo : s.sb.hi;
+    if (((word >> (i & 63u)) & 1ull) && p >= s.bad) {
+      r.bm = bor(pb, bge(s.sb, i));
+      r.wb = bor(pw, bge(s.wb, i));
+      r.exit = s.exit;
+      return r;
+    }
+    const uint32_t tg = zb8(T, p);
+    uint32_t L = __builtin_amdgcn_ubfe(kZLutTrue, tg << 2, 4);
+    if (L == 15u || tg >= 8u) {
+      int v;
+      uint32_t why = 1u;
+      if (tg >= 8u) {
+        v = (int)kLenErr;
+      } else if (tg == CLG_TAG_SERIALIZABLE) {
+        if (J) {
+          const uint32_t jv = jl_len(jl, p);
+          v = jv ? (int)jv : (int)kLenErr;
+        } else {
+          v = (int)kLenErr;
+          why = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
+        }
+      } else {
+        v = tg == CLG_TAG_IGNORE_CHECKPOINT ? 13 : zlen_var(T, p, end_a, tg, 0);
+      }
+      if (v <= 0) {
+        r.bad = why;
+        r.exit = s.exit;
+        return r;
+      }
+      L = (uint32_t)v;
+      bset(pw, i);
+    }
+    if (p + L > end_a || p + L < p) {
+      r.bad = 1;
+      r.exit = s.exit;
+      return r;
+    }
+    bset(pb, i);
+    p += L;
+  }
+  r.bm = pb;
+  r.wb = pw;
+  r.exit = p;
+  return r;
+}
+
 // ---------------------------------------------------------------------------------
 // Hand-off words.
 // ---------------------------------------------------------------------------------
@@ -478,6 +646,29 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
   return z;
 }
 
+// Canonical exit of the tile from the lanes' speculative walks: lanes >= c0 (the last
+// kZCanonLanes regions) chain their speculative exits, lane c0 starting from its own
+// speculative chain; lanes whose entry changed merge again.
+template <bool J>
+__device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t* s_img, const SpecR& sp, uint32_t lane,
+                                                 const JL& jl) {
+  const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
+  const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
+  const bool on = lane >= c0 && z.rs < z.re;
+  uint32_t cx = on ? sp.exit : z.rs, entry = kZCanon;
+  for (int it = 0; it <= 64; ++it) {
+    const uint32_t prev = __shfl_up(cx, 1);
+    const uint32_t want = lane <= c0 ? kZCanon : prev;
+    const bool ch = want != entry;
+    if (!__any(ch)) break;
+    if (ch) {
+      entry = want;
+      cx = on ? canon_walk_r<J>(s_img, z.re, z.end_a, want, sp, jl) : want;
+    }
+  }
+  return __shfl(cx, 63);
+}
+
 // Canonical exit of tile t: the speculative rule's chain from region c0 = (last region -
 // kZCanonLanes + 1) to the tile end (entries = previous lane's exit; lanes whose entry
 // changed re-merge).  It depends only on the tile's last ~2 KiB and not on where the
@@ -518,12 +709,12 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
+  (void)s_bits;
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
-  // ---- speculative walk of the lane's region (with warm-up)
-  const uint32_t ws = rs >= lo + kZWarm ? rs - kZWarm : lo;
-  uint32_t* bits = s_bits + lane * kZBitsPitch;
-  bits[0] = bits[1] = bits[2] = bits[3] = 0;
-  const Spec sp = rs < re ? spec_walk<J>(s_img, ws, rs, re, end_a, bits, jl) : Spec{{0, 0}, rs, rs, 0};
+  // ---- speculative walk of the lane's region (with warm-up), starts in registers
+  const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
+  const SpecR sp = rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
+                           : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
 
   ZPHASE(2);
   // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
@@ -531,7 +722,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk<J>(s_img, re, end_a, entry, sp, bits, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  Res r = rs < re ? merge_walk_r<J>(s_img, re, end_a, entry, sp, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
   uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
@@ -541,7 +732,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     ++iters;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk<J>(s_img, re, end_a, want, sp, bits, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
+      r = rs < re ? merge_walk_r<J>(s_img, re, end_a, want, sp, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
       steps_more += r.steps;
     }
   }
@@ -830,7 +1021,10 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
       if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
-      x_pub = canon_exit<J>(z, s_img, s_bits, lane, jl);
+      const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
+      const SpecR sp = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
+                                   : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+      x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
@@ -1076,6 +1270,278 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
     const uint64_t L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
     ctl.jlen[item] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
   }
+}
+
+// =================================================================================
+// One-pass decode (k_decode_one): every tile is staged once, its record chain found and
+// its records emitted by the same wave.  Tiles are taken in order from a ticket, so every
+// tile a wave waits for is held by a wave that already runs:
+//   * a tile publishes its canonical exit (entry-independent, canon_exit_r) before it
+//     waits for anything; its successor enters there and the tile later checks that its
+//     true exit is that value (else the batch aborts to the robust pipeline);
+//   * record / wide-record bases come from a decoupled look-back over per-tile words
+//     (flag 1: the tile's own counts, flag 2: the inclusive prefix), 64 predecessors per
+//     wave step.
+// Input bytes are read once; the only other traffic is the SoA output.
+// =================================================================================
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+template <bool J>
+__global__ __launch_bounds__(64) void k_decode_one(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                   FusedCtl ctl, DecodeOut out) {
+  __shared__ uint32_t s_img[kZImgDw];
+  __shared__ uint16_t s_pos[kZWin];
+  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
+  __shared__ uint32_t s_tk;
+  const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
+  if (lane == 0) s_tk = (ctl.nodep & 8u) ? atomicAdd(ctl.ticket, 1u) : blockIdx.x;
+  __syncthreads();
+  const uint32_t t = s_tk;
+  if (t >= nt || ld_agent32(ctl.abort)) return;
+#define OPHASE(i) \
+  if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
+  OPHASE(0);
+  const ZTile z = ztile(tiles, spans, t, lane);
+  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+  OPHASE(1);
+  JL jl{nullptr, nullptr, nullptr};
+  if (J) jl = load_jl(ctl, t, s_j, lane);
+  const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
+  const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
+  const SpecR sp = rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
+                           : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
+  OPHASE(2);
+
+  // ---- publish the canonical exit, then take the entry from the predecessor's
+  uint32_t x_pub = kZCanon;
+  if (!z.last) {
+    x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl);
+    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (z.td.span_off + (x_pub - lo)));
+  }
+  OPHASE(3);
+  uint64_t xs;
+  if (z.first || (ctl.nodep & 1u)) {
+    xs = z.td.span_off;  // a span starts on a record boundary
+  } else {
+    uint64_t v;
+    const uint64_t w0 = __builtin_amdgcn_s_memtime();
+    for (;;) {
+      v = ld_agent(&ctl.st_x[t - 1]);
+      if (v) break;
+      if (ld_agent32(ctl.abort)) return;
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
+        if (lane == 0) raise_abort(ctl, 4, t);
+        return;
+      }
+    }
+    xs = v & ~(1ull << 63);
+  }
+  const uint64_t ee = xs - z.td.span_off + lo;
+  const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+  OPHASE(4);
+
+  // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
+  // exit; lane 0 the true entry); lanes whose entry changed re-merge until consistent
+  uint32_t entry = lane == 0 ? e_true : __shfl_up(sp.exit, 1);
+  Res r = rs < re ? merge_walk_r<J>(s_img, re, end_a, entry, sp, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  for (int it = 0; it <= 64; ++it) {
+    const uint32_t prev = __shfl_up(r.exit, 1);
+    const uint32_t want = lane == 0 ? e_true : prev;
+    const bool ch = want != entry;
+    if (!__any(ch)) break;
+    if (ch) {
+      entry = want;
+      r = rs < re ? merge_walk_r<J>(s_img, re, end_a, want, sp, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
+    }
+  }
+  const uint32_t x_true = __shfl(r.exit, 63);
+  const uint64_t badm = __ballot(r.bad != 0u);
+  uint32_t reason = badm ? (__shfl(r.bad, (int)__builtin_ctzll(badm)) == 2u ? 5u : 1u) : 0u;
+  if (z.last) {
+    if (x_true != end_a) reason = reason ? reason : 2u;
+  } else if (x_true != x_pub) {
+    reason = reason ? reason : 3u;  // the successor already entered at the published exit
+  }
+  if (reason && !ctl.nodep) {
+    if (lane == 0) raise_abort(ctl, reason, t);
+    return;
+  }
+
+  // ---- counts, then the exclusive prefix by decoupled look-back
+  uint32_t rec = bcount(r.bm), wide = bcount(r.wb);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    rec += __shfl_xor(rec, off);
+    wide += __shfl_xor(wide, off);
+  }
+  const uint64_t agg = (uint64_t)wide << 32 | rec;
+  if (lane == 0) {
+    gp(ctl.cnt)[t] = agg;
+    st_agent(&ctl.look[t], kZLookAgg | agg);
+  }
+  OPHASE(5);
+  // two-level look-back: the tile's offset inside its group of kZGroup tiles (one read of
+  // the group mates' words), then the group's offset from the group words (64 groups per
+  // read; the last tile of a group publishes the group's counts, then its inclusive prefix)
+  const uint32_t g = t / kZGroup, g0 = g * kZGroup;
+  const uint32_t g1 = min(g0 + kZGroup, nt) - 1;
+  uint64_t ingrp = 0, excl = 0;
+  if (!(ctl.nodep & 2u)) {
+    const uint64_t w0 = __builtin_amdgcn_s_memtime();
+    for (;;) {
+      const uint32_t k = g0 + lane;
+      const uint64_t v = k < t ? ld_agent(&ctl.look[k]) : kZLookAgg;
+      if (!__any((v >> 62) == 0u)) {
+        ingrp = wave_sum64(k < t ? (v & kZLookVal) : 0ull);
+        break;
+      }
+      if (ld_agent32(ctl.abort)) return;
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
+        if (lane == 0) raise_abort(ctl, 4, t);
+        return;
+      }
+    }
+  }
+  if (t == g1 && lane == 0) st_agent(&ctl.glook[g], kZLookAgg | (ingrp + agg));
+  if (!(ctl.nodep & 2u)) {
+    int64_t j = (int64_t)g - 1;
+    const uint64_t w0 = __builtin_amdgcn_s_memtime();
+    while (j >= 0) {
+      const int64_t k = j - (int64_t)lane;
+      const uint64_t v = k >= 0 ? ld_agent(&ctl.glook[k]) : kZLookInc;  // before group 0: an inclusive 0
+      const uint64_t f = v >> 62;
+      const uint64_t incm = __ballot(f == 2u);
+      const uint64_t zm = __ballot(f == 0u);
+      const uint32_t stop = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;
+      const uint64_t upto = stop >= 63u ? ~0ull : ((2ull << stop) - 1ull);  // lanes 0 .. stop
+      if (zm & upto) {  // an earlier group is not complete yet
+        if (ld_agent32(ctl.abort)) return;
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
+          if (lane == 0) raise_abort(ctl, 4, t);
+          return;
+        }
+        continue;
+      }
+      excl += wave_sum64(lane <= stop ? (v & kZLookVal) : 0ull);
+      if (incm) break;
+      j -= 64;
+    }
+  }
+  if (t == g1 && lane == 0) st_agent(&ctl.glook[g], kZLookInc | (excl + ingrp + agg));
+  excl += ingrp;
+  if (lane == 0) gp(ctl.base)[t] = excl;  // look[] keeps the tile's own counts for its group mates
+  OPHASE(6);
+
+  // ---- emit: record starts into LDS by output index, consecutive lanes decode
+  // consecutive records (each SoA store of the wave is one contiguous run)
+  const uint32_t r0 = lane * kZRegion;
+  const uint32_t cnt = bcount(r.bm);
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += y;
+  }
+  const uint32_t total = (ctl.nodep & 4u) ? 0u : __shfl(incl, 63);
+  const uint64_t rec0 = excl & 0xFFFFFFFFull;
+  uint64_t wbase = (excl >> 32) & ((1ull << 30) - 1);
+  Bits cur = r.bm;
+  uint32_t idx = incl - cnt;
+  for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
+    const uint32_t wend = w0 + kZWin;
+    while ((cur.lo | cur.hi) && idx < wend) {
+      const uint32_t i = cur.lo ? (uint32_t)__builtin_ctzll(cur.lo) : 64u + (uint32_t)__builtin_ctzll(cur.hi);
+      if (cur.lo) cur.lo &= cur.lo - 1; else cur.hi &= cur.hi - 1;
+      s_pos[idx - w0] = (uint16_t)(r0 + i);
+      ++idx;
+    }
+    __syncthreads();
+    const uint32_t nw = total - w0 < kZWin ? total - w0 : kZWin;
+    for (uint32_t i0 = 0; i0 < nw; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool act = i < nw;
+      const uint32_t a = act ? (uint32_t)s_pos[i] : lo;
+      const uint32_t kk = rk(a >> 2), sh = 8u * (a & 3u);
+      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
+      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
+      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+      const uint32_t tg = x0 & 0xFFu;
+      const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
+      int64_t v0 = tg == CLG_TAG_ORDER       ? (int64_t)(int8_t)(blo & 0xFFu)
+                   : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)bhi << 32 | blo)
+                                             : (int64_t)(int32_t)__builtin_bswap32(blo);
+      const bool wide_rec = act && is_wide((int)tg);
+      Rec rr{};
+      if (wide_rec) {
+        const ZBytes b{s_img, a};
+        uint32_t tgu;
+        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
+        decode_fields(b, (int)tg, (int64_t)L, rr);
+        v0 = rr.v0;
+      }
+      const uint64_t wm = __ballot(wide_rec);
+      const uint64_t g = rec0 + w0 + i;
+      if (act) {
+        const uint32_t so = (uint32_t)(z.td.span_off + (a - lo));
+        if (g < out.cap) {
+          gp(out.off)[g] = so;
+          gp(out.tag)[g] = (uint8_t)tg;
+          gp(out.v0)[g] = v0;
+        }
+        if (wide_rec) {
+          const uint64_t wi = wbase + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+          if (wi < out.wcap) {
+            gp(out.w_idx)[wi] = (uint32_t)g;
+            gp(out.w_rc)[wi] = rr.rc;
+            gp(out.w_v1)[wi] = rr.v1;
+            gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
+            gp(out.w_var_len)[wi] = rr.var_len;
+            gp(out.w_sub)[wi] = rr.sub;
+          }
+        }
+      }
+      wbase += (uint64_t)__popcll(wm);
+    }
+    __syncthreads();
+  }
+  OPHASE(7);
+#undef OPHASE
+}
+
+// Each span's record / wide-record range from the one-pass look-back words.
+__global__ __launch_bounds__(256) void k_decode_spans1(const SpanDesc* __restrict__ spans, uint32_t n_spans,
+                                                       FusedCtl ctl) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= n_spans || ld_agent32(ctl.abort)) return;
+  const SpanDesc sd = spans[s];
+  if (!sd.n_tiles) return;
+  const uint32_t t0 = sd.first_tile, t1 = sd.first_tile + sd.n_tiles - 1;
+  gp(ctl.span_lo)[s] = gp(ctl.base)[t0];
+  gp(ctl.span_hi)[s] = gp(ctl.base)[t1] + gp(ctl.cnt)[t1];
+}
+
+int launch_decode_one(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                      FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase) {
+  if (!n_tiles) return CLG_OK;
+  ctl.n_tiles = n_tiles;
+  hipStream_t st = (hipStream_t)stream;
+  if (phase == 0) {
+    if (ctl.jser)
+      hipLaunchKernelGGL(k_decode_one<true>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+    else
+      hipLaunchKernelGGL(k_decode_one<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+  } else {
+    hipLaunchKernelGGL(k_decode_spans1, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
+  }
+  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
 }
 
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,

@@ -232,6 +232,7 @@ struct clg_engine {
   uint32_t gseq = 0;
   PinBuf h_rmeta;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
+  bool three_pass = true;    // CLONOS_DECODE=onepass: the experimental one-pass kernel instead of count/scan/emit
 
   // timing
   std::map<std::string, Stat> stats;
@@ -857,6 +858,15 @@ struct clg_engine {
     return CLG_OK;
   }
 
+  // Speculative warm-up bytes before each lane's region (CLONOS_WARM overrides; tuning aid).
+  static uint32_t spec_warm() {
+    static const uint32_t w = [] {
+      const char* v = getenv("CLONOS_WARM");
+      return v ? uint32_t(atoi(v)) : 96u;
+    }();
+    return w;
+  }
+
   // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
   // anything outside its fast path; the caller then runs the robust pipeline.
   // jser: build the Serializable tables first (phase 3).  *need_jser: the batch aborted
@@ -906,7 +916,7 @@ struct clg_engine {
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
-                      jser ? d_zjwork.as<uint32_t>() : nullptr};
+                      jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr, spec_warm()};
     HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
     HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -976,6 +986,122 @@ struct clg_engine {
     return finish_out(out, nrec, nwide);
   }
 
+  // One-pass decode (k_decode_one): stage, chain, look-back and emit per tile in one
+  // kernel; then the span ranges.  *aborted / *need_jser as in run_fused.
+  int run_one(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted, bool jser,
+              bool* need_jser) {
+    *aborted = false;
+    *need_jser = false;
+    reset_result(out);
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    if (ns == 0) return CLG_OK;
+    if (nt > (1u << 19)) {  // > 4 GiB in one batch: the look-back words hold 32-bit record prefixes
+      *aborted = true;
+      return CLG_OK;
+    }
+    CHK(upload_plan(p, d_ztiles));
+    clg::DecodeOut o{};
+    CHK(prep_out(out, &o));
+    // words: st_x[nt] cnt[nt] look[nt] glook[ng] base[nt] | span_lo[ns] span_hi[ns] | abort[8] (u32) | ticket
+    const size_t ng = (size_t(nt) + clg::kZGroup - 1) / clg::kZGroup;
+    const size_t o_span = 4 * size_t(nt) + ng, o_ab = o_span + 2 * size_t(ns), words = o_ab + 5;
+    CHK(d_zctl.ensure(words * 8));
+    CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
+    uint64_t* w = d_zctl.as<uint64_t>();
+    uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
+    if (jser) {
+      CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
+      CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
+      CHK(d_zjn.ensure(size_t(nt) * 4));
+      CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
+      HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
+    }
+    clg::FusedCtl ctl{};
+    ctl.st_x = w;
+    ctl.cnt = w + nt;
+    ctl.look = w + 2 * size_t(nt);
+    ctl.glook = w + 3 * size_t(nt);
+    ctl.base = w + 3 * size_t(nt) + ng;  // per tile: exclusive record / wide prefix
+    ctl.span_lo = w + o_span;
+    ctl.span_hi = w + o_span + ns;
+    ctl.abort = ab;
+    ctl.n_tiles = nt;
+    ctl.jpos = jser ? d_zjpos.as<uint32_t>() : nullptr;
+    ctl.jlen = jser ? d_zjlen.as<uint32_t>() : nullptr;
+    ctl.jn = jser ? d_zjn.as<uint32_t>() : nullptr;
+    ctl.jser = jser ? 1u : 0u;
+    ctl.jwork_cap = uint32_t(nt) * 16 + 1024;
+    ctl.jwork = jser ? d_zjwork.as<uint32_t>() : nullptr;
+    ctl.ticket = reinterpret_cast<uint32_t*>(w + o_ab + 4);
+    ctl.warm = spec_warm();
+    // developer timing probe (CLONOS_ONE_PROBE bits: 1 no entry wait, 2 no look-back, 4 no
+    // emit); output invalid
+    static const uint32_t probe = [] {
+      const char* v = getenv("CLONOS_ONE_PROBE");
+      return v ? uint32_t(atoi(v)) : 0u;
+    }();
+    ctl.nodep = probe;
+    const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
+    if (prof_path) {
+      CHK(d_prof.ensure(size_t(nt) * 64));
+      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
+      ctl.prof = d_prof.as<uint64_t>();
+    }
+    HIPCHK(hipMemsetAsync(w, 0, (4 * size_t(nt) + ng) * 8, stream));
+    HIPCHK(hipMemsetAsync(ab, 0, 40, stream));
+    auto* zt = d_ztiles.as<clg::TileDesc>();
+    auto* zs = d_spans.as<clg::SpanDesc>();
+    if (jser)
+      CHK(timed("decode_jser", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 3); }));
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (cfg.flags & CLG_F_TIMING) {
+      ea = get_event();
+      eb = get_event();
+      hipEventRecord(ea, stream);
+    }
+    CHK(clg::launch_decode_one(zt, nt, zs, ns, ctl, o, stream, 0));
+    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
+    CHK(clg::launch_decode_one(zt, nt, zs, ns, ctl, o, stream, 1));
+    uint64_t* hz = h_zres.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (prof_path) {
+      std::vector<uint64_t> hp(size_t(nt) * 8);
+      hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
+      if (FILE* fp = fopen(prof_path, "wb")) {
+        fwrite(hp.data(), 8, hp.size(), fp);
+        fclose(fp);
+      }
+    }
+    const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
+    if (jser) jser_hint = hab[7] != 0;
+    if (hab[0]) {
+      if (ea) {
+        ev_pool.push_back(ea);
+        ev_pool.push_back(eb);
+      }
+      *aborted = true;
+      *need_jser = !jser && hab[5];
+      if (getenv("CLONOS_FUSED_DEBUG"))
+        fprintf(stderr, "[clonos] one-pass decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d "
+                "exit=%d timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]),
+                int(~hab[3]), int(~hab[4]), int(~hab[5]), int(~hab[6]));
+      return CLG_OK;
+    }
+    constexpr uint64_t kRecMask = 0xFFFFFFFFull;
+    uint64_t nrec = 0, nwide = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (span_rec_base) span_rec_base[s] = nrec;
+      if (p.spans[s].n_tiles == 0) continue;
+      const uint64_t a = hz[s], b = hz[ns + s];
+      nrec += (b & kRecMask) - (a & kRecMask);
+      nwide += (b >> 32) - (a >> 32);
+    }
+    if (span_rec_base) span_rec_base[ns] = nrec;
+    if (ea) timings.push_back(PendingTiming{"decode_one", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    return finish_out(out, nrec, nwide);
+  }
+
   // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
   // tile_bytes)` fills a plan for the given tile geometry.
   template <class Build>
@@ -985,10 +1111,14 @@ struct clg_engine {
       DecodePlan pf;
       build(pf, clg::kZTile);
       bool aborted = false, need_jser = false;
-      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, jser_hint, &need_jser));
+      auto run = [&](bool j) {
+        return three_pass ? run_fused(pf, log_bytes, out, span_rec_base, &aborted, j, &need_jser)
+                          : run_one(pf, log_bytes, out, span_rec_base, &aborted, j, &need_jser);
+      };
+      CHK(run(jser_hint));
       if (aborted && need_jser) {  // Serializable records: again with the length tables
         stats["decode_jser_retry"].launches++;
-        CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &need_jser));
+        CHK(run(true));
       }
       if (!aborted) return CLG_OK;
       stats["decode_fallback"].launches++;
@@ -1164,6 +1294,7 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->cfg = *cfg;
   const char* dm = getenv("CLONOS_DECODE");
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
+  e->three_pass = !(dm && !strcmp(dm, "onepass"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));

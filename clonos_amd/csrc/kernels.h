@@ -185,7 +185,19 @@ struct FusedCtl {
   uint32_t jser;
   uint32_t jwork_cap;  // capacity of the general-walker work list
   uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
+  // one-pass kernel (k_decode_one): tiles taken in order from a ticket; per tile a
+  // look-back word flag<<62 | wide<<32 | records (flag 1: the tile's own counts, 2: the
+  // inclusive prefix); cnt[t] = the tile's own counts in the same packing
+  uint32_t* ticket;
+  uint64_t* look;   // per tile
+  uint64_t* glook;  // per group of kZGroup tiles: flag<<62 | the group's counts / inclusive prefix
+  uint32_t warm;    // speculative warm-up bytes before each region
 };
+constexpr uint32_t kZGroup = 64;
+constexpr uint64_t kZLookAgg = 1ull << 62, kZLookInc = 2ull << 62, kZLookVal = (1ull << 62) - 1;
+// one-pass decode: kernel (phase 0) then span ranges (phase 1) from the look-back words
+int launch_decode_one(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                      FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
 // 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
