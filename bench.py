@@ -550,10 +550,12 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
         n1 = O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs), O.ptr(lens), n_logs, threads)
         dt = _t.perf_counter() - t0
         assert n1 == n_det, (n1, n_det)
-        k = 8  # one core: the first 8 logs
-        t0 = _t.perf_counter()
-        nk = O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs), O.ptr(lens), k, 1)
-        d1 = _t.perf_counter() - t0
+        k, nk, d1 = 0, 0, 0.0  # one core: log after log for about a quarter of the multi-core time
+        while k < n_logs and (d1 < max(2.0, dt / 4) or k == 0):
+            t0 = _t.perf_counter()
+            nk += O.lib.orc_bench_decode(O.ptr(host), O.ptr(offs[k:]), O.ptr(lens[k:]), 1, 1)
+            d1 += _t.perf_counter() - t0
+            k += 1
         out["cpu_baseline"] = {"value": round(n_det / dt, 1), "unit": "determinants/s", "cores": threads,
                                "kind": "port", "sample": f"whole config-3 decode once ({total} B) in {dt:.2f}s",
                                "cores_1": {"value": round(nk / d1, 1), "unit": "determinants/s",
@@ -617,17 +619,25 @@ def cpu_baseline(bufs, log_bytes, cons, args):
         td += t1 - t0
         ts += t2 - t1
         reps += 1
-    # 1 core: the same per-log work for the first 4 logs and their consumers, once
-    k = min(4, len(bufs))
+    # 1 core: the same per-log work (decode + that log's consumers' slices), one thread, log
+    # after log until about a quarter of the multi-core sample's time has passed
+    src1_all, ln1_all = src, ln
+    n1, k, d1, s1 = 0, 0, 0.0, 0.0
+    while k < len(bufs) and (d1 + s1 < args.cpu_seconds / 4 or k == 0):
+        kc = [j for j, (i, _, _) in enumerate(cons) if i == k]
+        t0 = time.perf_counter()
+        n1 += O.lib.orc_bench_decode(O.ptr(host), O.ptr(starts[k:]), O.ptr(lens[k:]), 1, 1)
+        t1 = time.perf_counter()
+        src1, ln1 = np.ascontiguousarray(src1_all[kc]), np.ascontiguousarray(ln1_all[kc])
+        dst1 = np.zeros(len(kc), np.uint64)
+        dst1[1:] = np.cumsum(ln1)[:-1]
+        O.lib.orc_bench_slice(O.ptr(host), O.ptr(src1), O.ptr(ln1), O.ptr(dst1), len(kc), O.ptr(out), 1)
+        t2 = time.perf_counter()
+        d1 += t1 - t0
+        s1 += t2 - t1
+        k += 1
     kc = [j for j, (i, _, _) in enumerate(cons) if i < k]
-    t0 = time.perf_counter()
-    n1 = O.lib.orc_bench_decode(O.ptr(host), O.ptr(starts), O.ptr(lens), k, 1)
-    t1 = time.perf_counter()
-    src1, ln1 = np.ascontiguousarray(src[kc]), np.ascontiguousarray(ln[kc])
-    dst1 = np.zeros(len(kc), np.uint64)
-    dst1[1:] = np.cumsum(ln1)[:-1]
-    O.lib.orc_bench_slice(O.ptr(host), O.ptr(src1), O.ptr(ln1), O.ptr(dst1), len(kc), O.ptr(out), 1)
-    t2 = time.perf_counter()
+    t0, t1, t2 = 0.0, d1, d1 + s1
     return {"value": round(nrec / (td + ts), 1), "unit": "determinants/s", "cores": threads, "kind": "port",
             "sample": f"full config-2 step ({len(bufs)} logs x {args.records} records decode + {len(cons)} slices, "
                       f"{int(ln.sum())} B) x {reps}; decode {td:.2f}s slice {ts:.2f}s on {threads} threads",

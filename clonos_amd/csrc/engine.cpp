@@ -927,7 +927,16 @@ struct clg_engine {
     CHK(timed("decode_offsets", 24 * uint64_t(nt), [&] {
       return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 1);
     }));
-    // span ranges + abort words are known after the scan: read them, then emit
+    // emit right behind the scan (it returns at once when the batch aborted; its stores are
+    // bounded by the output capacity), then read the span ranges and abort words
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (cfg.flags & CLG_F_TIMING) {
+      ea = get_event();
+      eb = get_event();
+      hipEventRecord(ea, stream);
+    }
+    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
+    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     uint64_t* hz = h_zres.as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -942,6 +951,10 @@ struct clg_engine {
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[0]) {
+      if (ea) {
+        ev_pool.push_back(ea);
+        ev_pool.push_back(eb);
+      }
       *aborted = true;
       // Serializable records were met without tables: other aborts may be consequences
       // (entries guessed across them), so the tables decide; a second abort goes robust
@@ -963,14 +976,6 @@ struct clg_engine {
       }
       return CLG_OK;
     }
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (cfg.flags & CLG_F_TIMING) {
-      ea = get_event();
-      eb = get_event();
-      hipEventRecord(ea, stream);
-    }
-    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
-    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     constexpr uint64_t kRecMask = (1ull << 31) - 1;
     uint64_t nrec = 0, nwide = 0;
     const std::vector<clg::SpanDesc>& sp = p.spans;
