@@ -98,7 +98,8 @@ def main():
     total_bytes = sum(log_bytes)
     seg = 16384
     pool = sum((n + seg - 1) // seg + 1 for n in log_bytes) + 64
-    eng = Engine(segment_bytes=seg, pool_segments=pool, device=local, timing=True, async_slice=True)
+    eng = Engine(segment_bytes=seg, pool_segments=pool, device=local, timing=True, async_slice=True,
+                 ifl_pool_segments=16)
     logs = []
     for v, b in enumerate(bufs):
         vid = rank * args.logs + v  # VertexID sharding: this rank owns its vertices
@@ -321,7 +322,8 @@ def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, su
     sub_b = sub_records * 5
     rep_segs = sum(((2 * (main_b if table.ids[int(x)].is_main else sub_b) + seg - 1) // seg + 2)
                    for x in plan.wanted)
-    eng = Engine(segment_bytes=seg, pool_segments=segs + rep_segs + 64, device=dev.index or 0, timing=True)
+    eng = Engine(segment_bytes=seg, pool_segments=segs + rep_segs + 64, device=dev.index or 0, timing=True,
+                 ifl_pool_segments=16)
     owned = {int(x): eng.open_log(table.ids[int(x)]).handle for x in gids}
     sendset = set(plan.send.tolist())
     rep = X.Replicator(X.EngineIO(eng), plan, dev, {k: v for k, v in owned.items() if k in sendset})
@@ -423,7 +425,7 @@ def inflight_replay(args, torch, dev, n_sub=256, n_epochs=4, per_epoch=8, buf_by
     rng = np.random.default_rng(0xC105_0F40)
     seg = 16384
     segs = n_sub * n_epochs * per_epoch * ((buf_bytes + seg - 1) // seg)
-    eng = Engine(segment_bytes=seg, pool_segments=segs + 64, timing=True)
+    eng = Engine(segment_bytes=seg, pool_segments=64, ifl_segment_bytes=seg, ifl_pool_segments=segs + 64, timing=True)
     logs = [IF.InFlightLog(eng) for _ in range(n_sub)]
     pat = rng.integers(0, 256, buf_bytes + 4096, dtype=np.uint8).tobytes()
     for e in range(n_epochs):  # one batched log() call per epoch; ragged tail buffers
@@ -488,7 +490,7 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     per_log = sum(int(e.size) for e in epochs)
     seg = 16384
     eng = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
-                 timing=True)
+                 timing=True, ifl_pool_segments=16)
     logs = []
     for v in range(n_logs):  # every log: the epoch sequence rotated, so layouts differ per log
         log = eng.open_log(CausalLogID.main(v))

@@ -42,7 +42,7 @@ CLG_FULL_SHARING = -1
 
 EXPORTED = [
     "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
-    "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find", "clg_log_length_batch",
+    "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_ifl_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find", "clg_log_length_batch",
     "clg_job_open", "clg_job_close",
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
@@ -85,6 +85,8 @@ class Config(C.Structure):
         ("sharing_depth", C.c_int32),
         ("flags", C.c_uint32),
         ("reserved", C.c_uint32),
+        ("ifl_segment_bytes", C.c_uint32),
+        ("ifl_pool_segments", C.c_uint32),
     ]
 
 
@@ -239,6 +241,7 @@ def _load() -> C.CDLL:
         "clg_gather_stream": (P, [P]),
         "clg_sync": (C.c_int, [P]),
         "clg_pool_stats": (C.c_int, [P, u32p, u32p]),
+        "clg_ifl_pool_stats": (C.c_int, [P, u32p, u32p]),
         "clg_log_open": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),
         "clg_log_close": (C.c_int, [P, C.c_uint32]),
         "clg_log_find": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),

@@ -200,6 +200,12 @@ struct clg_engine {
   void* pool_alloc = nullptr;  // pool minus the guard bytes either side
   uint8_t* pool = nullptr;
   std::vector<uint32_t> free_segs;
+  // the in-flight (data) log's own pool (clg_config.ifl_*)
+  void* ifl_alloc = nullptr;
+  uint8_t* ifl_pool = nullptr;
+  uint32_t ifl_C = 0;
+  std::vector<uint32_t> ifl_free;
+  uint8_t* ifl_addr(uint32_t s) const { return ifl_pool + size_t(s) * ifl_C; }
   std::vector<Log> logs;
   std::vector<InFlight> ifls;
   std::map<IdKey, uint32_t> by_id;
@@ -1280,6 +1286,8 @@ void clg_config_default(clg_config* cfg) {
   cfg->pool_segments = 16384;  // 256 MiB
   cfg->device = 0;
   cfg->sharing_depth = CLG_FULL_SHARING;
+  cfg->ifl_segment_bytes = 32768;  // the in-flight log's pool: Flink's 32 KiB memory segments
+  cfg->ifl_pool_segments = 4096;   // 128 MiB
 }
 
 int clg_abi_version(void) { return CLG_ABI_VERSION; }
@@ -1311,6 +1319,16 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->pool = static_cast<uint8_t*>(p) + kPoolGuard;
   e->free_segs.resize(cfg->pool_segments);
   for (uint32_t i = 0; i < cfg->pool_segments; ++i) e->free_segs[i] = cfg->pool_segments - 1 - i;
+  e->ifl_C = cfg->ifl_segment_bytes ? cfg->ifl_segment_bytes : 32768u;
+  const uint32_t ifl_n = cfg->ifl_pool_segments ? cfg->ifl_pool_segments : 4096u;
+  if (e->ifl_C % 16) return fail(CLG_E_INVALID_ARG, "ifl_segment_bytes must be a multiple of 16");
+  e->cfg.ifl_segment_bytes = e->ifl_C;
+  e->cfg.ifl_pool_segments = ifl_n;
+  HIPCHK(hipMalloc(&p, size_t(e->ifl_C) * ifl_n + 2 * kPoolGuard));
+  e->ifl_alloc = p;
+  e->ifl_pool = static_cast<uint8_t*>(p) + kPoolGuard;
+  e->ifl_free.resize(ifl_n);
+  for (uint32_t i = 0; i < ifl_n; ++i) e->ifl_free[i] = ifl_n - 1 - i;
   e->jobs.emplace_back();  // job 0: the default job
   e->jobs[0].open = true;
   e->jobs[0].depth = cfg->sharing_depth;
@@ -1329,6 +1347,7 @@ void clg_engine_destroy(clg_engine* e) {
   }
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
   if (e->pool_alloc) hipFree(e->pool_alloc);
+  if (e->ifl_alloc) hipFree(e->ifl_alloc);
   hipStreamDestroy(e->stream);
   if (e->gstream) hipStreamDestroy(e->gstream);
   if (e->gready) hipEventDestroy(e->gready);
@@ -1382,6 +1401,13 @@ int clg_job_close(clg_engine* e, uint32_t job) {
     if (e->logs[h].open && e->logs[h].job == job) CHK(clg_log_close(e, h));
   if (job != 0) e->jobs[job] = Job();
   else e->jobs[0].latest_cp = 0;
+  return CLG_OK;
+}
+
+int clg_ifl_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments) {
+  ENGINE_GUARD(e);
+  *free_segments = uint32_t(e->ifl_free.size());
+  *used = e->cfg.ifl_pool_segments - *free_segments;
   return CLG_OK;
 }
 
@@ -2174,7 +2200,7 @@ static int ifl_get(clg_engine* e, uint32_t h, InFlight** out) {
 }
 
 static void ifl_release(clg_engine* e, std::vector<IflBuf>& bufs) {  // Buffer.recycleBuffer
-  for (auto& b : bufs) e->free_segs.insert(e->free_segs.end(), b.segs.rbegin(), b.segs.rend());
+  for (auto& b : bufs) e->ifl_free.insert(e->ifl_free.end(), b.segs.rbegin(), b.segs.rend());
   bufs.clear();
 }
 
@@ -2212,7 +2238,7 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
   if (n == 0) return CLG_OK;
   if (!ifl || !epoch || !off || !len || !bytes) return fail(CLG_E_INVALID_ARG, "null argument");
   if (in_kind != CLG_MEM_HOST && in_kind != CLG_MEM_DEVICE) return fail(CLG_E_INVALID_ARG, "bad in_kind");
-  const uint32_t C = e->C();
+  const uint32_t C = e->ifl_C;
   size_t need = 0, total = 0;
   for (uint32_t i = 0; i < n; ++i) {
     InFlight* f;
@@ -2220,8 +2246,8 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
     need += (size_t(len[i]) + C - 1) / C;
     total += len[i];
   }
-  if (need > e->free_segs.size())
-    return fail(CLG_E_NOSPACE, "segment pool exhausted (in-flight log needs %zu, free %zu)", need, e->free_segs.size());
+  if (need > e->ifl_free.size())
+    return fail(CLG_E_NOSPACE, "in-flight pool exhausted (needs %zu segments, free %zu)", need, e->ifl_free.size());
   CHK(e->gwait());  // a queued gather may still read segments that were freed and are reused now
   std::vector<clg::ScatterChunk> ch;
   ch.reserve(need);
@@ -2237,10 +2263,10 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
     const uint64_t src = in_kind == CLG_MEM_HOST ? packed : off[i];
     if (in_kind == CLG_MEM_HOST && len[i]) memcpy(e->h_stage.as<uint8_t>() + packed, bytes + off[i], len[i]);
     for (uint32_t o = 0; o < len[i]; o += C) {
-      const uint32_t s = e->free_segs.back();
-      e->free_segs.pop_back();
+      const uint32_t s = e->ifl_free.back();
+      e->ifl_free.pop_back();
       b.segs.push_back(s);
-      ch.push_back(clg::ScatterChunk{e->seg_addr(s), src + o, std::min(C, len[i] - o), 0});
+      ch.push_back(clg::ScatterChunk{e->ifl_addr(s), src + o, std::min(C, len[i] - o), 0});
     }
     packed += len[i];
     e->ifls[ifl[i]].epochs[epoch[i]].push_back(std::move(b));
@@ -2333,8 +2359,10 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
     }
     const uint64_t deliver = gap ? k - 1 : k;  // buffers next() returns
     if (ign > deliver) {  // the skip loop inside getInFlightIterator throws (:78-79)
-      r.status = fail(CLG_E_STATE, "skip of %llu buffers past the %llu the iterator yields", (unsigned long long)ign,
-                      (unsigned long long)deliver);
+      r.status = gap ? fail(CLG_E_STATE, "skip of %llu buffers reaches an epoch gap after %llu", (unsigned long long)ign,
+                            (unsigned long long)deliver)
+                     : fail(CLG_E_STATE, "skip of %llu buffers past the end (%llu)", (unsigned long long)ign,
+                            (unsigned long long)deliver);
       continue;
     }
     if (gap) r.status = CLG_E_EPOCH_GAP;  // the next() after the last delivered buffer throws (:156 -> :133)
@@ -2365,11 +2393,11 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
                 (unsigned long long)dst, (unsigned long long)nbuf, (unsigned long long)cap,
                 (unsigned long long)sizes_cap);
   std::vector<clg::GatherPiece> pieces;
-  const uint32_t C = e->C();
+  const uint32_t C = e->ifl_C;
   for (const Pick& p : picks)
     for (size_t s = 0; s < p.b->segs.size(); ++s) {
       const uint32_t o = uint32_t(s) * C;
-      pieces.push_back(clg::GatherPiece{e->seg_addr(p.b->segs[s]), p.dst + o, std::min(C, p.b->len - o), 0});
+      pieces.push_back(clg::GatherPiece{e->ifl_addr(p.b->segs[s]), p.dst + o, std::min(C, p.b->len - o), 0});
     }
   CHK(e->flush());
   return e->run_gather(pieces, dst, out, out_kind, "ifl_gather");

@@ -118,11 +118,13 @@ class Engine:
 
     def __init__(self, segment_bytes: int = 16384, pool_segments: int = 16384, device: int = 0,
                  sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto",
-                 async_slice: bool = False):
+                 async_slice: bool = False, ifl_segment_bytes: Optional[int] = None,
+                 ifl_pool_segments: Optional[int] = None):
         """decode: "auto" = single-pass fused kernel, robust multi-pass pipeline on abort;
         "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
         slices return once queued on the gather stream (CLG_F_ASYNC_SLICE); sync() before
-        reading them."""
+        reading them.  ifl_*: the in-flight log's own pool (default: the same geometry as the
+        determinant pool)."""
         if decode not in ("auto", "robust"):
             raise ValueError(f"decode must be 'auto' or 'robust', not {decode!r}")
         cfg = _lib.Config()
@@ -131,6 +133,8 @@ class Engine:
         cfg.pool_segments = pool_segments
         cfg.device = device
         cfg.sharing_depth = sharing_depth
+        cfg.ifl_segment_bytes = ifl_segment_bytes if ifl_segment_bytes is not None else segment_bytes
+        cfg.ifl_pool_segments = ifl_pool_segments if ifl_pool_segments is not None else pool_segments
         cfg.flags = ((_lib.CLG_F_TIMING if timing else 0) | (_lib.CLG_F_ROBUST_DECODE if decode == "robust" else 0)
                      | (_lib.CLG_F_ASYNC_SLICE if async_slice else 0))
         h = C.c_void_p()
@@ -174,6 +178,11 @@ class Engine:
     def pool_stats(self) -> Tuple[int, int]:
         u, f = C.c_uint32(), C.c_uint32()
         check(lib.clg_pool_stats(self._h, C.byref(u), C.byref(f)))
+        return u.value, f.value
+
+    def ifl_pool_stats(self) -> Tuple[int, int]:
+        u, f = C.c_uint32(), C.c_uint32()
+        check(lib.clg_ifl_pool_stats(self._h, C.byref(u), C.byref(f)))
         return u.value, f.value
 
     # ---- jobs (JobCausalLogImpl scope) ----------------------------------------------------

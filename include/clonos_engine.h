@@ -89,6 +89,12 @@ typedef struct clg_config {
   int32_t sharing_depth;   /* determinantSharingDepth (-1 = full sharing, 0 = logging off) */
   uint32_t flags;          /* CLG_F_* */
   uint32_t reserved;
+  /* The in-flight (data) log's own HBM pool (InMemorySubpartitionInFlightLogger keeps the
+   * network buffers it was given; here their bytes are copied into this pool, apart from
+   * the determinant segments so that data volume never starves appendDeterminant).  0:
+   * defaults (32 KiB segments = Flink's memory segment size, 4096 of them). */
+  uint32_t ifl_segment_bytes;
+  uint32_t ifl_pool_segments;
 } clg_config;
 
 #define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
@@ -115,6 +121,8 @@ void* clg_gather_stream(clg_engine* e);
 int clg_sync(clg_engine* e);
 /* Segments in use / free in the HBM pool. */
 int clg_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments);
+/* Segments in use / free in the in-flight log's pool. */
+int clg_ifl_pool_stats(clg_engine* e, uint32_t* used, uint32_t* free_segments);
 
 /* ---- JobCausalLog scope ------------------------------------------------------------
  * One JobCausalLogImpl per job per TaskManager (JobCausalLogFactory.java:56-67,
@@ -410,9 +418,10 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
 /* ---- in-flight (data) log (RT/inflightlogging/, I/ below) -------------------------------------
  * InFlightLog I/InFlightLog.java:32-55, implementation InMemorySubpartitionInFlightLogger
  * I/InMemorySubpartitionInFlightLogger.java:28-207: per subpartition, the data buffers sent in
- * each epoch, kept in HBM (the engine's segment pool; a buffer spans ceil(len / segment_bytes)
- * segments) until a checkpoint completes.  The Java side keeps refcounts; the engine owns
- * the bytes. */
+ * each epoch, kept in HBM (the engine's in-flight pool, clg_config.ifl_*; a buffer spans
+ * ceil(len / ifl_segment_bytes) segments) until a checkpoint completes.  The Java side keeps
+ * refcounts; the engine owns the bytes.  A full pool is CLG_E_NOSPACE with nothing logged:
+ * the caller applies backpressure (waits for a checkpoint to free epochs) and retries. */
 int clg_ifl_open(clg_engine* e, uint32_t* handle);
 /* close() :90-94: all buffers released. */
 int clg_ifl_close(clg_engine* e, uint32_t ifl);

@@ -32,12 +32,14 @@ static clg_channel_id ch(jlong lo, jlong hi) {
 }
 
 JNIEXPORT jint JNICALL FN(nCreate)(JNIEnv* env, jclass cls, jint seg, jint pool, jint dev, jint depth,
-                                   jlongArray out) {
+                                   jint ifl_seg, jint ifl_pool, jlongArray out) {
   (void)cls;
   clg_config cfg;
   clg_config_default(&cfg);
   cfg.segment_bytes = (uint32_t)seg;
   cfg.pool_segments = (uint32_t)pool;
+  cfg.ifl_segment_bytes = (uint32_t)ifl_seg;
+  cfg.ifl_pool_segments = (uint32_t)ifl_pool;
   cfg.device = dev;
   cfg.sharing_depth = depth;
   clg_engine* e = NULL;
@@ -362,6 +364,34 @@ JNIEXPORT jint JNICALL FN(nIflLog)(JNIEnv* env, jclass cls, jlong e, jint ifl, j
   uint64_t o = 0;
   uint32_t n = (uint32_t)len;
   return clg_ifl_log_batch(ENG(e), &h, &ep, &o, &n, 1, p, CLG_MEM_HOST);
+}
+
+/* n buffers of one in-flight log, staged back to back in `buf`: lens[i] bytes each, epochs[i]. */
+JNIEXPORT jint JNICALL FN(nIflLogBatch)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlongArray epochs, jintArray lens,
+                                        jobject buf, jint n) {
+  (void)cls;
+  if (n <= 0) return CLG_OK;
+  const uint8_t* p = addr(env, buf, 0);
+  if (!p) return CLG_E_INVALID_ARG;
+  jlong* ep = (*env)->GetLongArrayElements(env, epochs, NULL);
+  jint* ln = (*env)->GetIntArrayElements(env, lens, NULL);
+  uint32_t* h = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+  uint64_t* off = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+  int st = CLG_E_INVALID_ARG;
+  if (h && off) {
+    uint64_t o = 0;
+    for (jint i = 0; i < n; ++i) {
+      h[i] = (uint32_t)ifl;
+      off[i] = o;
+      o += (uint32_t)ln[i];
+    }
+    st = clg_ifl_log_batch(ENG(e), h, (const int64_t*)ep, off, (const uint32_t*)ln, (uint32_t)n, p, CLG_MEM_HOST);
+  }
+  free(h);
+  free(off);
+  (*env)->ReleaseIntArrayElements(env, lens, ln, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, epochs, ep, JNI_ABORT);
+  return st;
 }
 
 JNIEXPORT jint JNICALL FN(nIflNotifyCheckpointComplete)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong cp) {

@@ -45,8 +45,14 @@ public final class ClonosEngine implements AutoCloseable {
 	private final long handle; // clg_engine*
 
 	public ClonosEngine(int segmentBytes, int poolSegments, int device, int sharingDepth) {
+		this(segmentBytes, poolSegments, device, sharingDepth, 0, 0);
+	}
+
+	/** inFlightSegmentBytes / inFlightPoolSegments: the in-flight log's own HBM pool (0: 32 KiB x 4096). */
+	public ClonosEngine(int segmentBytes, int poolSegments, int device, int sharingDepth, int inFlightSegmentBytes,
+						int inFlightPoolSegments) {
 		long[] out = new long[1];
-		check(nCreate(segmentBytes, poolSegments, device, sharingDepth, out));
+		check(nCreate(segmentBytes, poolSegments, device, sharingDepth, inFlightSegmentBytes, inFlightPoolSegments, out));
 		this.handle = out[0];
 	}
 
@@ -138,17 +144,22 @@ public final class ClonosEngine implements AutoCloseable {
 	}
 
 	/** In-flight iterator statuses (InMemorySubpartitionInFlightLogger.ReplayIterator): a skip past
-	 *  the end is ListIterator.next()'s NoSuchElementException, a start epoch that is absent or a
-	 *  gap the NullPointerException of logToReplay.get(..).listIterator(). */
-	public static RuntimeException inFlightException(int status, boolean startPresent, String msg) {
-		if (status == CLG_E_STATE && startPresent) {
+	 *  the end is ListIterator.next()'s NoSuchElementException; a start epoch that is absent
+	 *  (currentIterator == null) or a gap (logToReplay.get(++currentKey) == null) is a
+	 *  NullPointerException.  clg_last_error names the case. */
+	public static RuntimeException inFlightException(int status, String msg) {
+		if (status == CLG_E_STATE && msg.contains("past the end")) {
 			return new NoSuchElementException(msg);
 		}
-		return new NullPointerException(msg);
+		if (status == CLG_E_STATE || status == CLG_E_EPOCH_GAP) {
+			return new NullPointerException(msg);
+		}
+		return toException(status, msg);
 	}
 
 	// ---- natives (jni/clonos_jni.c) ------------------------------------------------------
-	static native int nCreate(int segmentBytes, int poolSegments, int device, int sharingDepth, long[] out);
+	static native int nCreate(int segmentBytes, int poolSegments, int device, int sharingDepth, int iflSegmentBytes,
+							  int iflPoolSegments, long[] out);
 	static native void nDestroy(long engine);
 	static native String nLastError();
 	static native int nJobOpen(long engine, long jobIdLower, long jobIdUpper, int sharingDepth, int[] out);
@@ -160,6 +171,8 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nIflOpen(long engine, int[] out);
 	static native int nIflClose(long engine, int ifl);
 	static native int nIflLog(long engine, int ifl, long epoch, ByteBuffer direct, int off, int len);
+	/** n buffers staged back to back in `direct` (lens[i] bytes, epoch epochs[i]), logged in order. */
+	static native int nIflLogBatch(long engine, int ifl, long[] epochs, int[] lens, ByteBuffer direct, int n);
 	static native int nIflNotifyCheckpointComplete(long engine, int ifl, long checkpointId);
 	/** res = {status, n_buffers, remaining, len, total, total_buffers, end_epoch}; sizes (i32) and
 	 *  epochs (i64, native order) receive one entry per buffer. */

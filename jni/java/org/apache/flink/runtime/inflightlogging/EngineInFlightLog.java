@@ -24,6 +24,16 @@ public class EngineInFlightLog implements InFlightLog {
 	private final int ifl;
 	private BufferPool inFlightBufferPool;
 
+	// log() stages buffers host-side and hands them to the engine in batches (one upload and
+	// one scatter kernel per batch instead of a GPU round trip per network buffer); every other
+	// operation flushes first, so the engine always sees the buffers in log() order
+	private static final int STAGE_BYTES = 1 << 20;
+	private static final int STAGE_BUFFERS = 256;
+	private final ByteBuffer stage = ByteBuffer.allocateDirect(STAGE_BYTES);
+	private final long[] stagedEpochs = new long[STAGE_BUFFERS];
+	private final int[] stagedLens = new int[STAGE_BUFFERS];
+	private int staged;
+
 	public EngineInFlightLog(ClonosEngine engine) {
 		this.engine = engine;
 		int[] h = new int[1];
@@ -39,18 +49,55 @@ public class EngineInFlightLog implements InFlightLog {
 	@Override
 	public synchronized void log(Buffer buffer, long epochID, boolean isFinished) { // :44-48
 		ByteBuffer nio = buffer.getNioBufferReadable();
-		ByteBuffer direct = nio.isDirect() ? nio : ByteBuffer.allocateDirect(nio.remaining()).put(nio.duplicate());
-		int off = nio.isDirect() ? nio.position() : 0;
-		check(nIflLog(engine.handle(), ifl, epochID, direct, off, nio.remaining()));
+		int n = nio.remaining();
+		if (n > stage.remaining() || staged == STAGE_BUFFERS) {
+			flush();
+		}
+		if (n > STAGE_BYTES) { // larger than the stage: a batch of its own
+			ByteBuffer direct = nio.isDirect() ? nio.slice() : ByteBuffer.allocateDirect(n).put(nio.duplicate());
+			logBatch(new long[]{epochID}, new int[]{n}, direct, 1);
+			return;
+		}
+		stage.put(nio.duplicate());
+		stagedEpochs[staged] = epochID;
+		stagedLens[staged] = n;
+		staged++;
+	}
+
+	private void flush() {
+		if (staged == 0) {
+			return;
+		}
+		logBatch(stagedEpochs, stagedLens, stage, staged);
+		stage.clear();
+		staged = 0;
+	}
+
+	// Backpressure: a full in-flight pool (CLG_E_NOSPACE, nothing logged) waits until a
+	// checkpoint completes and frees epochs (notifyCheckpointComplete wakes us), then retries.
+	private void logBatch(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
+		int st;
+		while ((st = nIflLogBatch(engine.handle(), ifl, epochs, lens, bytes, n)) == CLG_E_NOSPACE) {
+			try {
+				wait(10);
+			} catch (InterruptedException e) {
+				Thread.currentThread().interrupt();
+				throw new RuntimeException(e);
+			}
+		}
+		check(st);
 	}
 
 	@Override
 	public synchronized void notifyCheckpointComplete(long checkpointId) { // :51-70
+		flush();
 		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
+		notifyAll();
 	}
 
 	@Override
 	public synchronized InFlightLogIterator<Buffer> getInFlightIterator(long startEpochID, int ignoreBuffers) {
+		flush();
 		long[] res = new long[7];
 		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, null, null, null, res);
 		if (st != CLG_OK && st != CLG_E_CAPACITY) {
@@ -61,8 +108,8 @@ public class EngineInFlightLog implements InFlightLog {
 		ByteBuffer epochs = ByteBuffer.allocateDirect((int) Math.max(8, 8 * res[5])).order(ByteOrder.nativeOrder());
 		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, out, sizes, epochs, res));
 		int status = (int) res[0];
-		if (status != CLG_OK && status != CLG_E_EPOCH_GAP) {
-			check(status); // CLG_E_STATE: the skip loop inside getInFlightIterator threw (:78-79)
+		if (status != CLG_OK && status != CLG_E_EPOCH_GAP) { // the skip loop inside getInFlightIterator threw (:78-79)
+			throw inFlightException(status, nLastError());
 		}
 		return new Replay(out, sizes, epochs, (int) res[1], (int) res[2], res[6], status);
 	}
@@ -73,6 +120,8 @@ public class EngineInFlightLog implements InFlightLog {
 
 	@Override
 	public synchronized void close() { // :90-94
+		staged = 0;
+		stage.clear();
 		check(nIflClose(engine.handle(), ifl));
 	}
 

@@ -57,7 +57,8 @@ def worker(rank, world, port, q):
         need = J.replication_masks(g, -1, world)
         plan = X.ReplicationPlan(table, -1, rank, world, need)
         assert len(plan.wanted) == (4 * PAR // world) * (PAR + 1) * (world - 1)
-        eng = Engine(segment_bytes=SEG, pool_segments=len(plan.owned) + len(plan.wanted) + 4096, device=0)
+        eng = Engine(segment_bytes=SEG, pool_segments=len(plan.owned) + len(plan.wanted) + 4096, device=0,
+                     ifl_pool_segments=16)
         owned = {int(gid): eng.open_log(table.ids[gid]).handle for gid in plan.owned}
         send = set(plan.send.tolist())
         rep = X.Replicator(X.EngineIO(eng), plan, dev, {k: v for k, v in owned.items() if k in send})

@@ -30,7 +30,7 @@ def test_abi_version_and_struct_sizes():
     assert _lib.lib.clg_abi_version() == 2
     assert ctypes.sizeof(_lib.IflReplayRes) == 48
     assert ctypes.sizeof(_lib.CausalLogIdC) == 24
-    assert ctypes.sizeof(_lib.Config) == 24
+    assert ctypes.sizeof(_lib.Config) == 32
     assert ctypes.sizeof(_lib.SliceReq) == 32
     assert ctypes.sizeof(_lib.SliceRes) == 24
     assert ctypes.sizeof(_lib.DeltaReq) == 32

@@ -65,8 +65,8 @@ def test_inflight_random_vs_oracle(seg, seed):
             _check(IF.replay_batch(eng, reqs), refs, reqs)
         for f in logs:
             f.close()
-        used, _ = eng.pool_stats()
-        assert used == 0
+        used, _ = eng.ifl_pool_stats()
+        assert used == 0 and eng.pool_stats()[0] == 0  # the determinant pool was never touched
 
 
 def test_inflight_reference_scenario_and_gap():
@@ -147,7 +147,27 @@ def test_inflight_golden_fixture():
             assert got == c["expect"]
             for f in logs:
                 f.close()
-        assert eng.pool_stats()[0] == 0
+        assert eng.ifl_pool_stats()[0] == 0
+
+
+def test_inflight_pool_is_separate_and_reports_nospace():
+    """The in-flight log has its own pool: a full in-flight pool is CLG_E_NOSPACE with
+    nothing logged (the caller waits for a checkpoint: backpressure), and it never takes
+    the segments appendDeterminant needs."""
+    with Engine(segment_bytes=64, pool_segments=8, ifl_segment_bytes=1024, ifl_pool_segments=4) as eng:
+        f = IF.InFlightLog(eng)
+        f.log(b"a" * 2048, 0)  # two segments
+        with pytest.raises(ClonosError) as ei:
+            f.log(b"b" * 3000, 1)  # three more: the pool holds four
+        assert ei.value.status == _lib.CLG_E_NOSPACE
+        assert f.epochs() == [(0, 1)] and eng.ifl_pool_stats() == (2, 2)
+        from clonos_amd import CausalLogID
+        log = eng.open_log(CausalLogID.main(1))  # the determinant pool is untouched
+        for _ in range(7):
+            log.appendDeterminant(b"\x00\x01" * 32, 0)
+        f.notify_checkpoint_complete(1)  # frees epoch 0: the retry fits
+        f.log(b"b" * 3000, 1)
+        assert f.epochs() == [(1, 1)] and eng.ifl_pool_stats() == (3, 1)
 
 
 def test_inflight_log_from_device_memory():
@@ -177,4 +197,4 @@ def test_inflight_log_from_device_memory():
         rep = f.replay(0, 0)
         assert rep.status == _lib.CLG_OK and rep.buffers == bufs and rep.remaining == len(bufs)
         f.close()
-        assert eng.pool_stats()[0] == 0
+        assert eng.ifl_pool_stats()[0] == 0
