@@ -84,7 +84,7 @@ class Config(C.Structure):
         ("device", C.c_int32),
         ("sharing_depth", C.c_int32),
         ("flags", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("host_tail_bytes", C.c_uint32),
         ("ifl_segment_bytes", C.c_uint32),
         ("ifl_pool_segments", C.c_uint32),
     ]

@@ -87,7 +87,14 @@ struct Log {
   std::vector<uint32_t> segs;  // composite components
   int32_t writer = 0;          // visibleWriterIndex (== composite writerIndex)
   int32_t flushed = 0;         // physical bytes [0, flushed) are resident in HBM
-  std::vector<uint8_t> pending;  // staged bytes [flushed, writer)
+  // Host copy of physical bytes [tail_start, writer): the staged bytes [flushed, writer)
+  // plus the most recent flushed ones (clg_config.host_tail_bytes), so a slice of the log's
+  // tail -- a consumer keeping up with its producer -- is served without a GPU round trip.
+  // tail_start <= flushed <= writer.
+  std::vector<uint8_t> tail;
+  int32_t tail_start = 0;
+  uint32_t pending_bytes() const { return uint32_t(writer - flushed); }
+  const uint8_t* pending_data() const { return tail.data() + (flushed - tail_start); }
   std::map<int64_t, std::shared_ptr<EpochStart>> epochs;
   std::unordered_map<ChKey, Consumer, ChKeyHash> consumers;
 };
@@ -313,8 +320,8 @@ struct clg_engine {
     return CLG_OK;
   }
   void write_pending(Log& l, const uint8_t* b, uint32_t n) {
-    if (l.pending.empty() && n) dirty.push_back(uint32_t(&l - logs.data()));
-    l.pending.insert(l.pending.end(), b, b + n);
+    if (l.flushed == l.writer && n) dirty.push_back(uint32_t(&l - logs.data()));
+    l.tail.insert(l.tail.end(), b, b + n);
     l.writer += int32_t(n);
   }
   std::shared_ptr<EpochStart> compute_if_absent(Log& l, int64_t e) {
@@ -336,13 +343,28 @@ struct clg_engine {
   }
 
   // ---------------------------------------------------------------- flush (append scatter)
+  // Drops flushed bytes from the front of a log's host tail beyond the configured keep.
+  void trim_tail(Log& l) {
+    const size_t keep = cfg.host_tail_bytes;
+    const size_t flushed_in_tail = size_t(l.flushed - l.tail_start);
+    if (flushed_in_tail <= 2 * keep) return;  // amortised: trim to `keep` once it doubled
+    const size_t drop = flushed_in_tail - keep;
+    l.tail.erase(l.tail.begin(), l.tail.begin() + long(drop));
+    l.tail_start += int32_t(drop);
+  }
+  // Forget the host tail (bytes were written to HBM behind its back).
+  static void reset_tail(Log& l) {
+    l.tail.clear();
+    l.tail_start = l.writer;
+  }
+
   int flush() {
     size_t total = 0, nchunks = 0;
     for (uint32_t h : dirty) {
       const Log& l = logs[h];
-      if (l.open && !l.pending.empty()) {
-        total += l.pending.size();
-        nchunks += l.pending.size() / C() + 2;
+      if (l.open && l.pending_bytes()) {
+        total += l.pending_bytes();
+        nchunks += l.pending_bytes() / C() + 2;
       }
     }
     if (total == 0) {
@@ -360,11 +382,12 @@ struct clg_engine {
     size_t off = 0, n = 0;
     for (uint32_t h : dirty) {
       Log& l = logs[h];
-      if (!l.open || l.pending.empty()) continue;
-      memcpy(hs + off, l.pending.data(), l.pending.size());
+      const uint32_t pb = l.open ? l.pending_bytes() : 0u;
+      if (!pb) continue;
+      memcpy(hs + off, l.pending_data(), pb);
       int32_t p = l.flushed;
       size_t src = off;
-      size_t left = l.pending.size();
+      size_t left = pb;
       while (left) {
         const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
         const uint32_t take = uint32_t(std::min<size_t>(left, C() - so));
@@ -373,9 +396,9 @@ struct clg_engine {
         src += take;
         left -= take;
       }
-      off += l.pending.size();
+      off += pb;
       l.flushed = l.writer;
-      l.pending.clear();
+      trim_tail(l);
     }
     dirty.clear();
     HIPCHK(hipMemcpyAsync(d_stage.p, hs, total, hipMemcpyHostToDevice, stream));
@@ -460,6 +483,7 @@ struct clg_engine {
       }
       l->writer += num_new;
       l->flushed = l->writer;
+      reset_tail(*l);  // these bytes go to HBM only
       total += size_t(num_new);
     }
     if (ch.empty()) return CLG_OK;
@@ -633,6 +657,13 @@ struct clg_engine {
         *n = uint32_t(nb);  // required size (the consumer does not advance)
         return fail(CLG_E_CAPACITY, "delta needs %d bytes", nb);
       }
+      if (kind == CLG_MEM_HOST && p >= l->tail_start && p + nb <= l->writer) {  // the host tail holds it
+        int32_t phys, nb2;
+        CHK(take_delta(h, k, epoch, &phys, &nb2));
+        if (nb2) memcpy(out, l->tail.data() + (phys - l->tail_start), size_t(nb2));
+        *n = uint32_t(nb2);
+        return CLG_OK;
+      }
     }
     CHK(flush());
     int32_t phys, nb;
@@ -668,6 +699,11 @@ struct clg_engine {
     if (uint32_t(nb) > cap) {
       *n = uint32_t(nb);  // required size
       return fail(CLG_E_CAPACITY, "getDeterminants needs %d bytes", nb);
+    }
+    if (kind == CLG_MEM_HOST && s >= l->tail_start) {  // the host tail holds it
+      if (nb) memcpy(out, l->tail.data() + (s - l->tail_start), size_t(nb));
+      *n = uint32_t(nb);
+      return CLG_OK;
     }
     CHK(flush());
     std::vector<clg::GatherPiece> pieces;
@@ -705,6 +741,12 @@ struct clg_engine {
     for (auto& e : l.epochs) e.second->offset -= move;
     l.writer -= move;
     l.flushed -= move;
+    l.tail_start -= move;
+    if (l.tail_start < 0) {  // bytes of dropped components
+      l.tail.erase(l.tail.begin(), l.tail.begin() + std::min<long>(long(l.tail.size()), long(-l.tail_start)));
+      l.tail_start = 0;
+      if (l.tail_start + int32_t(l.tail.size()) != l.writer) reset_tail(l);
+    }
     return CLG_OK;
   }
 
@@ -1286,6 +1328,7 @@ void clg_config_default(clg_config* cfg) {
   cfg->pool_segments = 16384;  // 256 MiB
   cfg->device = 0;
   cfg->sharing_depth = CLG_FULL_SHARING;
+  cfg->host_tail_bytes = 16384;    // one component of each log's tail kept on the host
   cfg->ifl_segment_bytes = 32768;  // the in-flight log's pool: Flink's 32 KiB memory segments
   cfg->ifl_pool_segments = 4096;   // 128 MiB
 }

@@ -88,7 +88,9 @@ typedef struct clg_config {
   int32_t device;          /* HIP device ordinal */
   int32_t sharing_depth;   /* determinantSharingDepth (-1 = full sharing, 0 = logging off) */
   uint32_t flags;          /* CLG_F_* */
-  uint32_t reserved;
+  uint32_t host_tail_bytes; /* flushed bytes of each log's tail also kept in host memory (16384 by
+                               default): host-output slices / getDeterminants inside the tail are
+                               served by memcpy, without a GPU round trip; 0: every slice gathers */
   /* The in-flight (data) log's own HBM pool (InMemorySubpartitionInFlightLogger keeps the
    * network buffers it was given; here their bytes are copied into this pool, apart from
    * the determinant segments so that data volume never starves appendDeterminant).  0:

@@ -18,10 +18,11 @@ def status_of(fn, *a):
         return e.status, None
 
 
+@pytest.mark.parametrize("tail", [0, 100, 16384])  # host tail: none (every slice gathers), short, default
 @pytest.mark.parametrize("seed,comp", [(0, 16), (1, 32), (2, 64), (3, 256), (4, 16384)])
-def test_log_ops_match_oracle(seed, comp):
+def test_log_ops_match_oracle(seed, comp, tail):
     rng = np.random.default_rng(1000 + seed)
-    with Engine(segment_bytes=comp, pool_segments=1 << 14) as eng:
+    with Engine(segment_bytes=comp, pool_segments=1 << 14, host_tail_bytes=tail) as eng:
         log = eng.open_log(CausalLogID.main(1))
         ref = O.OracleLog(comp)
         epoch, last_cp = 0, 0
