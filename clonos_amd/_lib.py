@@ -42,7 +42,7 @@ CLG_FULL_SHARING = -1
 
 EXPORTED = [
     "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
-    "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_ifl_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find", "clg_log_length_batch",
+    "clg_engine_stream", "clg_gather_stream", "clg_sync", "clg_pool_stats", "clg_ifl_pool_stats", "clg_log_open", "clg_log_close", "clg_log_find", "clg_log_length_batch", "clg_log_get_id",
     "clg_job_open", "clg_job_close",
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
@@ -247,6 +247,7 @@ def _load() -> C.CDLL:
         "clg_log_find": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),
         "clg_job_open": (C.c_int, [P, C.c_uint64, C.c_uint64, C.c_int32, u32p]),
         "clg_log_length_batch": (C.c_int, [P, P, C.c_uint32, P, u64p]),
+        "clg_log_get_id": (C.c_int, [P, C.c_uint32, C.POINTER(CausalLogIdC), u32p]),
         "clg_job_close": (C.c_int, [P, C.c_uint32]),
         "clg_append": (C.c_int, [P, C.c_uint32, C.c_int64, C.c_char_p, C.c_uint32]),
         "clg_append_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P]),

@@ -1494,6 +1494,15 @@ int clg_log_find(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint3
   return CLG_OK;
 }
 
+int clg_log_get_id(clg_engine* e, uint32_t h, clg_causal_log_id* id, uint32_t* job) {
+  ENGINE_GUARD(e);
+  Log* l;
+  CHK(e->get_log(h, &l));
+  if (id) *id = l->id;
+  if (job) *job = l->job;
+  return CLG_OK;
+}
+
 int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n) {
   ENGINE_GUARD(e);
   return e->append(log, epoch, rec, n);

@@ -143,6 +143,8 @@ int clg_log_open(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint3
 /* close() :317-328 (the engine does not wait for consumers; caller guarantees drain). */
 int clg_log_close(clg_engine* e, uint32_t log);
 int clg_log_find(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint32_t* handle);
+/* The CausalLogID and job of an open log (e.g. one clg_process_delta opened). */
+int clg_log_get_id(clg_engine* e, uint32_t log, clg_causal_log_id* id, uint32_t* job);
 /* appendDeterminant :158-177.  `rec` holds ONE encoded determinant (encodeTo bytes;
  * n == getEncodedSizeInBytes).  Staged on the host, flushed to HBM in batches. */
 int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n);

@@ -211,6 +211,45 @@ JNIEXPORT jint JNICALL FN(nDecodeLogs)(JNIEnv* env, jclass cls, jlong e, jintArr
   return s;
 }
 
+/* clg_decode_host over bytes[off, off + len): one span; results as nDecodeLogs. */
+JNIEXPORT jint JNICALL FN(nDecodeHost)(JNIEnv* env, jclass cls, jlong e, jobject bytes, jint off, jint len, jobject o_off,
+                                       jobject tag, jobject v0, jobject w_idx, jobject w_rc, jobject w_v1,
+                                       jobject w_var_off, jobject w_var_len, jobject w_sub, jlongArray res) {
+  (void)cls;
+  clg_decoded d;
+  memset(&d, 0, sizeof d);
+  d.off = (uint32_t*)addr(env, o_off, 0);
+  d.tag = addr(env, tag, 0);
+  d.v0 = (int64_t*)addr(env, v0, 0);
+  d.w_idx = (uint32_t*)addr(env, w_idx, 0);
+  d.w_rc = (int32_t*)addr(env, w_rc, 0);
+  d.w_v1 = (int64_t*)addr(env, w_v1, 0);
+  d.w_var_off = (uint32_t*)addr(env, w_var_off, 0);
+  d.w_var_len = (uint32_t*)addr(env, w_var_len, 0);
+  d.w_sub = addr(env, w_sub, 0);
+  d.cap = cap(env, tag);
+  d.wcap = cap(env, w_sub);
+  d.out_kind = CLG_MEM_HOST;
+  uint64_t so = 0, sl = (uint64_t)len;
+  uint64_t base[2] = {0, 0};
+  int s = clg_decode_host(ENG(e), addr(env, bytes, off), &so, &sl, 1, &d, base);
+  jlong r[6] = {(jlong)d.n_rec, (jlong)d.n_wide, d.err_status, d.err_span, d.err_off, d.err_tag};
+  (*env)->SetLongArrayRegion(env, res, 0, 6, r);
+  return s;
+}
+
+/* clg_log_get_id: out = {vertexId, isMain, irpLower, irpUpper, subpartition, job}. */
+JNIEXPORT jint JNICALL FN(nLogGetId)(JNIEnv* env, jclass cls, jlong e, jint log, jlongArray out) {
+  (void)cls;
+  clg_causal_log_id id;
+  uint32_t job = 0;
+  memset(&id, 0, sizeof id);
+  int s = clg_log_get_id(ENG(e), (uint32_t)log, &id, &job);
+  jlong w[6] = {id.vertex_id, id.is_main, id.irp_lower, id.irp_upper, id.subpartition, (jlong)job};
+  (*env)->SetLongArrayRegion(env, out, 0, 6, w);
+  return s;
+}
+
 /* clg_enrich_batch: reqs packed as 5 longs per request {chLo, chHi, epoch, first, count};
  * res gets 4 longs per request {status, headerBytes, outOff, outLen}. */
 JNIEXPORT jint JNICALL FN(nEnrichBatch)(JNIEnv* env, jclass cls, jlong e, jint strategy, jlongArray reqs,

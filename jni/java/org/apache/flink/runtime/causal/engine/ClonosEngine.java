@@ -197,6 +197,12 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nDecodeLogs(long engine, int[] logs, long[] startEpochs, ByteBuffer off, ByteBuffer tag,
 								  ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
 								  ByteBuffer wVarLen, ByteBuffer wSub, long[] result, long[] spanRecBase);
+	/** One span of host bytes decoded on the GPU (clg_decode_host); result as nDecodeLogs. */
+	static native int nDecodeHost(long engine, ByteBuffer bytes, int off, int len, ByteBuffer recOff, ByteBuffer tag,
+								  ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
+								  ByteBuffer wVarLen, ByteBuffer wSub, long[] result);
+	/** out = {vertexId, isMain, irpLower, irpUpper, subpartition, job}. */
+	static native int nLogGetId(long engine, int log, long[] out);
 	static native int nEnrichBatch(long engine, int strategy, long[] requests, int[] logs, byte[] flags,
 								   ByteBuffer out, long[] results, long[] total);
 	static native int nProcessDelta(long engine, int job, int strategy, ByteBuffer msg, int off, int len,

@@ -38,12 +38,24 @@ public class EngineThreadCausalLog implements ThreadCausalLog {
 
 	public EngineThreadCausalLog(ClonosEngine engine, int job, CausalLogID id, DeterminantEncoder encoder,
 								 ByteBufAllocator alloc) {
+		this(engine, engine.openLog(job, id.getVertexID(), id.isMainThread(), id.getIntermediateDataSetLower(),
+			id.getIntermediateDataSetUpper(), id.getSubpartitionIndex()), id, encoder, alloc);
+	}
+
+	/** A log the engine already opened (clg_process_delta's insertNewUpstreamLog,
+	 *  AbstractDeltaSerializerDeserializer.java:165-194). */
+	public static EngineThreadCausalLog wrap(ClonosEngine engine, int handle, CausalLogID id, DeterminantEncoder encoder,
+											 ByteBufAllocator alloc) {
+		return new EngineThreadCausalLog(engine, handle, id, encoder, alloc);
+	}
+
+	private EngineThreadCausalLog(ClonosEngine engine, int handle, CausalLogID id, DeterminantEncoder encoder,
+								  ByteBufAllocator alloc) {
 		this.engine = engine;
 		this.causalLogID = id;
 		this.encoder = encoder;
 		this.alloc = alloc;
-		this.log = engine.openLog(job, id.getVertexID(), id.isMainThread(), id.getIntermediateResultPartitionLower(),
-			id.getIntermediateResultPartitionUpper(), id.getSubpartitionIndex());
+		this.log = handle;
 		this.scratch = ThreadLocal.withInitial(() -> Unpooled.directBuffer(256));
 	}
 
