@@ -17,8 +17,10 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -195,6 +197,48 @@ struct PendingTiming {
 // 16-B loads that may start before a piece's first byte or end past its last.
 constexpr size_t kPoolGuard = 256;
 
+// Two-level engine lock.  The per-call ThreadCausalLog operations of the drop-in (append,
+// hasDelta, offset, slices the host tail holds, logLength, a host-input upstream delta) take
+// only the stripe of their log, so task threads appending and Netty threads slicing
+// different logs run in parallel -- as on the reference's per-log objects -- without
+// touching a shared cache line.  Everything that touches the GPU, the log table or several
+// logs at once takes the engine mutex and then every stripe (EXCLUSIVE).  Exclusive is
+// re-entrant (clg_job_close -> clg_log_close), and a per-log request from the exclusive
+// holder passes through.
+constexpr uint32_t kLogStripes = 64;
+struct alignas(64) Stripe {
+  std::mutex m;
+};
+struct EngineLock {
+  std::mutex m;
+  std::atomic<std::thread::id> owner{};
+  int depth = 0;
+  Stripe stripe[kLogStripes];
+  bool owned() const { return owner.load(std::memory_order_relaxed) == std::this_thread::get_id(); }
+  void lock() {
+    if (owned()) {
+      ++depth;
+      return;
+    }
+    m.lock();
+    for (auto& s : stripe) s.m.lock();
+    owner.store(std::this_thread::get_id(), std::memory_order_relaxed);
+    depth = 1;
+  }
+  void unlock() {
+    if (--depth == 0) {
+      owner.store(std::thread::id(), std::memory_order_relaxed);
+      for (uint32_t i = kLogStripes; i-- > 0;) stripe[i].m.unlock();
+      m.unlock();
+    }
+  }
+};
+struct XGuard {
+  EngineLock& l;
+  explicit XGuard(EngineLock& l_) : l(l_) { l.lock(); }
+  ~XGuard() { l.unlock(); }
+};
+
 }  // namespace
 
 namespace clg_internal {  // error text for the host-only translation units (response.cpp)
@@ -218,7 +262,9 @@ struct clg_engine {
   std::map<IdKey, uint32_t> by_id;
   std::vector<Job> jobs;  // jobs[0]: the default job (cfg.sharing_depth)
   std::vector<uint32_t> dirty;  // logs with staged (unflushed) bytes: flush() visits only these
-  std::recursive_mutex mu;
+  EngineLock mu;
+  std::mutex pool_mu;   // free_segs, taken by appends holding only their stripe
+  std::mutex dirty_mu;  // dirty, idem
 
   // staging / scratch
   PinBuf h_stage, h_desc, h_sres, h_zres;
@@ -311,6 +357,7 @@ struct clg_engine {
     int64_t need_bytes = int64_t(l.writer) + n - capacity(l);
     if (need_bytes <= 0) return CLG_OK;
     size_t need = size_t((need_bytes + C() - 1) / C());
+    std::lock_guard<std::mutex> g(pool_mu);
     if (need > free_segs.size())
       return fail(CLG_E_NOSPACE, "segment pool exhausted (need %zu, free %zu)", need, free_segs.size());
     for (size_t i = 0; i < need; ++i) {
@@ -320,7 +367,10 @@ struct clg_engine {
     return CLG_OK;
   }
   void write_pending(Log& l, const uint8_t* b, uint32_t n) {
-    if (l.flushed == l.writer && n) dirty.push_back(uint32_t(&l - logs.data()));
+    if (l.flushed == l.writer && n) {
+      std::lock_guard<std::mutex> g(dirty_mu);
+      dirty.push_back(uint32_t(&l - logs.data()));
+    }
     l.tail.insert(l.tail.end(), b, b + n);
     l.writer += int32_t(n);
   }
@@ -351,6 +401,12 @@ struct clg_engine {
     const size_t drop = flushed_in_tail - keep;
     l.tail.erase(l.tail.begin(), l.tail.begin() + long(drop));
     l.tail_start += int32_t(drop);
+  }
+  // Staged (unflushed) bytes of one log are bounded: past this the append that crossed it
+  // flushes (the host holds at most ~this + host_tail_bytes per log).
+  bool over_stage_limit(uint32_t h) const {
+    const uint32_t lim = std::max<uint32_t>(65536u, 2u * cfg.host_tail_bytes);
+    return h < logs.size() && logs[h].open && logs[h].pending_bytes() > lim;
   }
   // Forget the host tail (bytes were written to HBM behind its back).
   static void reset_tail(Log& l) {
@@ -642,7 +698,11 @@ struct clg_engine {
     return CLG_OK;
   }
 
-  int get_delta(uint32_t h, ChKey k, int64_t epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
+  // host_only: serve the slice from the host tail or return kNeedGpu with nothing changed
+  // (the caller holds only the shared lock and retries under the exclusive one).
+  static constexpr int kNeedGpu = 1;
+  int get_delta(uint32_t h, ChKey k, int64_t epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n,
+                bool host_only = false) {
     *n = 0;
     Log* l;
     CHK(get_log(h, &l));
@@ -665,6 +725,7 @@ struct clg_engine {
         return CLG_OK;
       }
     }
+    if (host_only) return kNeedGpu;
     CHK(flush());
     int32_t phys, nb;
     CHK(take_delta(h, k, epoch, &phys, &nb));
@@ -689,7 +750,8 @@ struct clg_engine {
     return CLG_OK;
   }
 
-  int get_determinants(uint32_t h, int64_t start_epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n) {
+  int get_determinants(uint32_t h, int64_t start_epoch, void* out, uint32_t cap, uint32_t kind, uint32_t* n,
+                       bool host_only = false) {
     *n = 0;
     Log* l;
     CHK(get_log(h, &l));
@@ -705,6 +767,7 @@ struct clg_engine {
       *n = uint32_t(nb);
       return CLG_OK;
     }
+    if (host_only) return kNeedGpu;
     CHK(flush());
     std::vector<clg::GatherPiece> pieces;
     add_pieces(*l, s, nb, 0, pieces);
@@ -1320,7 +1383,21 @@ extern "C" {
 
 #define ENGINE_GUARD(e)                                             \
   if (!(e)) return fail(CLG_E_INVALID_ARG, "null engine");          \
-  std::lock_guard<std::recursive_mutex> guard_((e)->mu)
+  XGuard guard_((e)->mu)
+
+// A per-log call: only the log's stripe (see EngineLock).
+struct LogGuard {
+  std::mutex* s;
+  LogGuard(clg_engine* e, uint32_t h) : s(e->mu.owned() ? nullptr : &e->mu.stripe[h % kLogStripes].m) {
+    if (s) s->lock();
+  }
+  ~LogGuard() {
+    if (s) s->unlock();
+  }
+};
+#define LOG_GUARD(e, h)                                    \
+  if (!(e)) return fail(CLG_E_INVALID_ARG, "null engine"); \
+  LogGuard lguard_((e), (h))
 
 void clg_config_default(clg_config* cfg) {
   memset(cfg, 0, sizeof *cfg);
@@ -1504,8 +1581,15 @@ int clg_log_get_id(clg_engine* e, uint32_t h, clg_causal_log_id* id, uint32_t* j
 }
 
 int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n) {
-  ENGINE_GUARD(e);
-  return e->append(log, epoch, rec, n);
+  bool spill;
+  {
+    LOG_GUARD(e, log);
+    CHK(e->append(log, epoch, rec, n));
+    spill = e->over_stage_limit(log);
+  }
+  if (!spill) return CLG_OK;
+  ENGINE_GUARD(e);  // bounded write-behind: this log's staged bytes go to HBM now
+  return e->flush();
 }
 
 int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, const uint64_t* off,
@@ -1516,12 +1600,19 @@ int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, c
 }
 
 int clg_upstream_delta(clg_engine* e, uint32_t log, int64_t epoch, int32_t off, const uint8_t* d, uint32_t n) {
+  bool spill;
+  {
+    LOG_GUARD(e, log);
+    CHK(e->upstream(log, epoch, off, d, n));
+    spill = e->over_stage_limit(log);
+  }
+  if (!spill) return CLG_OK;
   ENGINE_GUARD(e);
-  return e->upstream(log, epoch, off, d, n);
+  return e->flush();
 }
 
 int clg_log_length(clg_engine* e, uint32_t h, int32_t* out) {  // :180-192
-  ENGINE_GUARD(e);
+  LOG_GUARD(e, h);
   Log* l;
   CHK(e->get_log(h, &l));
   *out = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
@@ -1544,23 +1635,33 @@ int clg_log_length_batch(clg_engine* e, const uint32_t* log, uint32_t n, int32_t
 }
 
 int clg_has_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, int32_t* out) {
-  ENGINE_GUARD(e);
+  LOG_GUARD(e, log);
   return e->has_delta(log, ChKey{c.lo, c.hi}, epoch, out);
 }
 
 int clg_offset_from_epoch(clg_engine* e, uint32_t log, clg_channel_id c, int32_t* out) {
-  ENGINE_GUARD(e);
+  LOG_GUARD(e, log);
   return e->offset_from_epoch(log, ChKey{c.lo, c.hi}, out);
 }
 
 int clg_get_delta(clg_engine* e, uint32_t log, clg_channel_id c, int64_t epoch, void* out, uint32_t cap,
                   uint32_t kind, uint32_t* n) {
+  {  // the host tail holds it: no GPU, only this log's stripe
+    LOG_GUARD(e, log);
+    const int r = e->get_delta(log, ChKey{c.lo, c.hi}, epoch, out, cap, kind, n, true);
+    if (r != clg_engine::kNeedGpu) return r;
+  }
   ENGINE_GUARD(e);
   return e->get_delta(log, ChKey{c.lo, c.hi}, epoch, out, cap, kind, n);
 }
 
 int clg_get_determinants(clg_engine* e, uint32_t log, int64_t start_epoch, void* out, uint32_t cap, uint32_t kind,
                          uint32_t* n) {
+  {
+    LOG_GUARD(e, log);
+    const int r = e->get_determinants(log, start_epoch, out, cap, kind, n, true);
+    if (r != clg_engine::kNeedGpu) return r;
+  }
   ENGINE_GUARD(e);
   return e->get_determinants(log, start_epoch, out, cap, kind, n);
 }
@@ -1574,7 +1675,7 @@ int clg_notify_checkpoint_complete(clg_engine* e, uint32_t h, int64_t cp) {
 }
 
 int clg_unregister_consumer(clg_engine* e, uint32_t h, clg_channel_id c) {
-  ENGINE_GUARD(e);
+  LOG_GUARD(e, h);
   Log* l;
   CHK(e->get_log(h, &l));
   l->consumers.erase(ChKey{c.lo, c.hi});

@@ -378,3 +378,70 @@ def test_get_delta_with_concurrent_appender():
         t.join()
         got.append(log.getDeltaForConsumer(ch, 0))
         assert b"".join(got) == b"".join(recs)
+
+
+@pytest.mark.parametrize("tail", [0, 64, 16384])
+def test_many_threads_many_logs(tail):
+    """Eight task/Netty thread pairs on eight logs at once (the lock split: per-log calls
+    take the engine lock shared + the log's stripe) while another thread keeps forcing
+    whole-engine work (sync = flush + GPU, log_lengths).  Every consumer's deltas
+    concatenate to exactly its log, and every log ends byte-identical to the oracle's
+    ThreadCausalLogImpl fed the same records."""
+    import threading
+    import _oracle as O
+    T, N = 8, 1500
+    with Engine(segment_bytes=256, pool_segments=1 << 13, host_tail_bytes=tail) as eng:
+        logs = [eng.open_log(CausalLogID.main(100 + t)) for t in range(T)]
+        recs = [[bytes([1]) + (t * N + i).to_bytes(8, "big") for i in range(N)] for t in range(T)]
+        got = [[] for _ in range(T)]
+        errs = []
+        stop = threading.Event()
+
+        done_n = [0] * T
+
+        def appender(t):
+            try:
+                for i, r in enumerate(recs[t]):
+                    logs[t].appendDeterminant(r, i // 500)
+                    done_n[t] += 1
+            except Exception as ex:  # pragma: no cover - surfaced below
+                errs.append(ex)
+
+        def slicer(t, app):
+            # moves to epoch ep+1 only once a record of it was appended before the last
+            # drain of ep (a consumer moving on abandons the rest of its epoch, :204-214)
+            try:
+                ch = (7, t)
+                ep = 0
+                while True:
+                    n = done_n[t]
+                    if logs[t].hasDeltaForConsumer(ch, ep):
+                        got[t].append(logs[t].getDeltaForConsumer(ch, ep))
+                    if n >= N and ep == (N - 1) // 500:
+                        break
+                    if n > 500 * (ep + 1):
+                        ep += 1
+            except Exception as ex:  # pragma: no cover
+                errs.append(ex)
+
+        def whole_engine():
+            while not stop.is_set():
+                eng.sync()
+                eng.log_lengths(np.array([lg.handle for lg in logs], np.uint32))
+
+        apps = [threading.Thread(target=appender, args=(t,)) for t in range(T)]
+        slis = [threading.Thread(target=slicer, args=(t, apps[t])) for t in range(T)]
+        w = threading.Thread(target=whole_engine)
+        for th in apps + slis + [w]:
+            th.start()
+        for th in apps + slis:
+            th.join(timeout=120)
+        stop.set()
+        w.join(timeout=60)
+        assert not errs, errs
+        for t in range(T):
+            assert b"".join(got[t]) == b"".join(recs[t]), t
+            ol = O.OracleLog(256)
+            for i, r in enumerate(recs[t]):
+                ol.append(i // 500, r)
+            assert logs[t].getDeterminants(0) == ol.get_determinants(0)[1]
