@@ -144,11 +144,13 @@ def main():
     seek_offs = np.array([off for _, _, off in cons], np.int32)
 
     def step():
-        # the slice gather runs on the engine's second stream and overlaps the next step's
-        # decode (it only reads log segments); the timed region ends with a device-wide sync
-        eng.decode_logs_device(handles, starts, dec, base)
+        # the decode is queued asynchronously, so planning the slices overlaps it on the GPU;
+        # the slice gather runs on the engine's second stream beside the decode and the next
+        # step's (it only reads log segments); the timed region ends with a device-wide sync
+        eng.decode_logs_device_async(handles, starts, dec, base)
         eng.seek_consumers_raw(creq, seek_offs, n_req)  # rewind the consumers to their start offsets
         got = eng.slice_batch_raw(creq, cres, n_req, o_slice.data_ptr(), o_slice.numel(), device=True)
+        eng.decode_wait()
         assert got == slice_total, (got, slice_total)
 
     # correctness guard on the first step: record count and spot values

@@ -47,7 +47,7 @@ EXPORTED = [
     "clg_append", "clg_append_batch", "clg_upstream_delta", "clg_log_length", "clg_has_delta",
     "clg_offset_from_epoch", "clg_get_delta", "clg_get_determinants", "clg_notify_checkpoint_complete",
     "clg_unregister_consumer", "clg_log_get_state", "clg_consumer_state", "clg_log_read_phys",
-    "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs",
+    "clg_slice_batch", "clg_consumer_seek", "clg_consumer_seek_batch", "clg_upstream_delta_batch", "clg_truncate_all", "clg_decode_host", "clg_decode_logs", "clg_decode_logs_async", "clg_decode_wait",
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
@@ -227,6 +227,15 @@ def _load() -> C.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -m clonos_amd.build` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (same SONAME as
+    # /opt/rocm's) and loads it by a different file name, so whichever of the two comes
+    # second would be a second runtime in the process -- and torch's device init then
+    # fails ("No HIP GPUs are available") once the engine's has initialised.  Importing
+    # torch first makes its runtime the one the engine's NEEDED libamdhip64.so.7 resolves to.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # a torch-less host: /opt/rocm's runtime
+        pass
     lib = C.CDLL(LIB_PATH)
     P = C.c_void_p
     u32p, i32p, u64p, i64p = (C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
@@ -269,6 +278,8 @@ def _load() -> C.CDLL:
         "clg_truncate_all": (C.c_int, [P, C.c_uint32, C.c_int64, i32p]),
         "clg_decode_host": (C.c_int, [P, P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_decode_logs": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
+        "clg_decode_logs_async": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
+        "clg_decode_wait": (C.c_int, [P]),
         "clg_replay_prep": (C.c_int, [P, P, P, P, P, C.c_uint32, P, u32p, C.POINTER(Decoded), P]),
         "clg_kernel_stats": (C.c_int, [P, C.POINTER(KernelStat), C.c_uint32, u32p]),
         "clg_kernel_stats_reset": (C.c_int, [P]),

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <atomic>
@@ -290,6 +291,8 @@ struct clg_engine {
   hipEvent_t gdone[2] = {nullptr, nullptr};
   uint32_t gseq = 0;
   PinBuf h_rmeta;
+  PinBuf h_plan;  // decode plans (upload_plan)
+  DevBuf d_plan;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
   bool three_pass = true;    // CLONOS_DECODE=onepass: the experimental one-pass kernel instead of count/scan/emit
 
@@ -897,22 +900,24 @@ struct clg_engine {
                  gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
     const size_t o_runs = (tb + 15) & ~size_t(15), o_seg = (o_runs + rb + 15) & ~size_t(15),
                  o_spans = (o_seg + gb + 15) & ~size_t(15), hb = o_spans + sb;
-    CHK(h_desc.ensure(hb + 64));
-    CHK(d_desc.ensure(hb));
-    uint8_t* hd = h_desc.as<uint8_t>();
+    // the plan has buffers of its own: an asynchronous decode may still be uploading it
+    // while later calls (flush, slices) stage their descriptors
+    CHK(h_plan.ensure(hb + 64));
+    CHK(d_plan.ensure(hb));
+    uint8_t* hd = h_plan.as<uint8_t>();
     memcpy(hd, p.tiles.data(), tb);
     memcpy(hd + o_runs, p.runs.data(), rb);
     memcpy(hd + o_seg, p.segtab.data(), gb);
     memcpy(hd + o_spans, p.spans.data(), sb);
-    HIPCHK(hipMemcpyAsync(d_desc.p, hd, hb, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(d_spans.p, d_desc.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_plan.p, hd, hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_spans.p, d_plan.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
     if (!p.runs.empty()) {
-      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_desc.as<uint8_t>() + o_runs),
+      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + o_runs),
                                    uint32_t(p.runs.size()), nt,
-                                   reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
+                                   reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + o_seg), pool, C(),
                                    p.unit, dtiles.as<clg::TileDesc>(), stream));
     } else if (tb) {
-      HIPCHK(hipMemcpyAsync(dtiles.p, d_desc.p, tb, hipMemcpyDeviceToDevice, stream));
+      HIPCHK(hipMemcpyAsync(dtiles.p, d_plan.p, tb, hipMemcpyDeviceToDevice, stream));
     }
     return CLG_OK;
   }
@@ -987,12 +992,29 @@ struct clg_engine {
     *aborted = false;
     *need_jser = false;
     reset_result(out);
-    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
-    if (ns == 0) return CLG_OK;
-    if (nt > (1u << 20)) {  // more than 8 GiB in one batch: the offsets pass covers 2^20 tiles
+    if (p.spans.empty()) return CLG_OK;
+    if (!fused_fits(p)) {
       *aborted = true;
       return CLG_OK;
     }
+    FusedRun r;
+    CHK(launch_fused(p, log_bytes, out, jser, &r));
+    return finish_fused(p, r, out, span_rec_base, aborted, need_jser);
+  }
+  // more than 8 GiB in one batch: the offsets pass covers 2^20 tiles
+  static bool fused_fits(const DecodePlan& p) { return p.n_tiles <= (1u << 20); }
+
+  // One queued three-pass decode: launch_fused queues everything up to the read-back of the
+  // span ranges and abort words; finish_fused waits for it and turns it into the result.
+  struct FusedRun {
+    uint64_t log_bytes = 0;
+    bool jser = false;
+    hipEvent_t ea = nullptr, eb = nullptr;
+  };
+  int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    r->log_bytes = log_bytes;
+    r->jser = jser;
     CHK(upload_plan(p, d_ztiles));
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
@@ -1050,8 +1072,22 @@ struct clg_engine {
     if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     uint64_t* hz = h_zres.as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+    r->ea = ea;
+    r->eb = eb;
+    return CLG_OK;
+  }
+
+  int finish_fused(const DecodePlan& p, FusedRun& r, clg_decoded* out, uint64_t* span_rec_base, bool* aborted,
+                   bool* need_jser) {
+    *aborted = false;
+    *need_jser = false;
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    const bool jser = r.jser, zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
+    const uint64_t log_bytes = r.log_bytes;
+    hipEvent_t ea = r.ea, eb = r.eb;
+    uint64_t* hz = h_zres.as<uint64_t>();
     HIPCHK(hipStreamSynchronize(stream));
-    if (prof_path) {
+    if (const char* prof_path = getenv("CLONOS_SCAN_PHASES")) {
       std::vector<uint64_t> hp(size_t(nt) * 8);
       hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
       if (FILE* fp = fopen(prof_path, "wb")) {
@@ -1232,16 +1268,80 @@ struct clg_engine {
                           : run_one(pf, log_bytes, out, span_rec_base, &aborted, j, &need_jser);
       };
       CHK(run(jser_hint));
-      if (aborted && need_jser) {  // Serializable records: again with the length tables
-        stats["decode_jser_retry"].launches++;
-        CHK(run(true));
-      }
       if (!aborted) return CLG_OK;
-      stats["decode_fallback"].launches++;
+      return after_abort(pf, build, log_bytes, out, span_rec_base, need_jser);
     }
     DecodePlan p;
     build(p, uint32_t(clg::kTile));
     return run_decode(p, log_bytes, out, span_rec_base);
+  }
+
+  // The fast path aborted: again with the Serializable length tables when that was the
+  // reason, then the robust pipeline.
+  template <class Build>
+  int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
+                  bool need_jser) {
+    bool aborted = true, nj = false;
+    if (need_jser) {
+      stats["decode_jser_retry"].launches++;
+      CHK(three_pass ? run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &nj)
+                     : run_one(pf, log_bytes, out, span_rec_base, &aborted, true, &nj));
+      if (!aborted) return CLG_OK;
+    }
+    stats["decode_fallback"].launches++;
+    DecodePlan p;
+    build(p, uint32_t(clg::kTile));
+    return run_decode(p, log_bytes, out, span_rec_base);
+  }
+
+  // ---------------------------------------------------------------- asynchronous decode
+  // clg_decode_logs_async: the three-pass decode is queued and the call returns; settle()
+  // completes it (result, fallbacks) in clg_decode_wait or first thing in any other call
+  // that needs the engine exclusively (see ENGINE_GUARD), so a pending decode never sees
+  // its inputs change.  Slices into device memory on the gather stream and consumer seeks
+  // leave it pending: they only read log segments and move consumer offsets.
+  struct PendingDecode {
+    bool active = false;
+    DecodePlan plan;
+    FusedRun run;
+    clg_decoded* out = nullptr;
+    uint64_t* span_rec_base = nullptr;
+    std::function<void(DecodePlan&, uint32_t)> build;
+    int status = CLG_OK;  // result of the last settled decode, for clg_decode_wait
+    std::string err;      // and its error text
+  } pend;
+
+  int decode_async(std::function<void(DecodePlan&, uint32_t)> build, uint64_t log_bytes, clg_decoded* out,
+                   uint64_t* span_rec_base) {
+    pend.status = CLG_OK;
+    if (!(fused_decode && three_pass && log_bytes / 2 < (1ull << 31))) return decode(build, log_bytes, out, span_rec_base);
+    DecodePlan pf;
+    build(pf, clg::kZTile);
+    reset_result(out);
+    if (pf.spans.empty()) return CLG_OK;
+    if (!fused_fits(pf)) return decode(build, log_bytes, out, span_rec_base);
+    FusedRun r;
+    CHK(launch_fused(pf, log_bytes, out, jser_hint, &r));
+    pend.active = true;
+    pend.plan = std::move(pf);
+    pend.run = r;
+    pend.out = out;
+    pend.span_rec_base = span_rec_base;
+    pend.build = std::move(build);
+    return CLG_OK;
+  }
+
+  int settle() {
+    if (!pend.active) return CLG_OK;
+    pend.active = false;
+    bool aborted = false, need_jser = false;
+    int st = finish_fused(pend.plan, pend.run, pend.out, pend.span_rec_base, &aborted, &need_jser);
+    if (st == CLG_OK && aborted)
+      st = after_abort(pend.plan, pend.build, pend.run.log_bytes, pend.out, pend.span_rec_base, need_jser);
+    pend.status = st;
+    if (st != CLG_OK) pend.err = g_err;
+    pend.build = nullptr;
+    return CLG_OK;  // the decode's own status goes to clg_decode_wait
   }
 
   int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
@@ -1381,9 +1481,15 @@ struct clg_engine {
 // =======================================================================================
 extern "C" {
 
-#define ENGINE_GUARD(e)                                             \
+// Exclusive calls first complete a pending asynchronous decode (clg_decode_logs_async);
+// ENGINE_GUARD_KEEP leaves it pending (calls that only read log segments on the gather
+// stream or move consumer offsets).
+#define ENGINE_GUARD_KEEP(e)                                        \
   if (!(e)) return fail(CLG_E_INVALID_ARG, "null engine");          \
   XGuard guard_((e)->mu)
+#define ENGINE_GUARD(e) \
+  ENGINE_GUARD_KEEP(e); \
+  (e)->settle()
 
 // A per-log call: only the log's stripe (see EngineLock).
 struct LogGuard {
@@ -1430,7 +1536,17 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->three_pass = !(dm && !strcmp(dm, "onepass"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+  {
+    // The device-output slice gather (HBM-bound) runs beside the next decode (VALU-bound):
+    // its queue gets the higher priority so its workgroups are dispatched first
+    // (CLONOS_GATHER_PRIO=0: same priority as the decode stream).
+    const char* gp = getenv("CLONOS_GATHER_PRIO");
+    int lo = 0, hi = 0;
+    if (!(gp && !strcmp(gp, "0")) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+      HIPCHK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, hi));
+    else
+      HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+  }
   HIPCHK(hipEventCreateWithFlags(&e->gready, hipEventDisableTiming));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
   void* p = nullptr;
@@ -1727,7 +1843,8 @@ int clg_log_read_phys(clg_engine* e, uint32_t h, int32_t phys, uint32_t n, uint8
 
 int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res, void* out, uint64_t cap,
                     uint32_t out_kind, uint64_t* total) {
-  ENGINE_GUARD(e);
+  ENGINE_GUARD_KEEP(e);
+  if (!(out_kind == CLG_MEM_DEVICE && (e->cfg.flags & CLG_F_ASYNC_SLICE))) e->settle();
   if (n && (!reqs || !res)) return fail(CLG_E_INVALID_ARG, "null argument");
   CHK(e->flush());
   std::vector<clg::SegSpan> runs;
@@ -1784,7 +1901,7 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
 }
 
 int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch, int32_t offset) {
-  ENGINE_GUARD(e);
+  ENGINE_GUARD_KEEP(e);
   Log* l;
   CHK(e->get_log(h, &l));
   auto it = l->epochs.find(epoch);
@@ -1800,7 +1917,7 @@ int clg_upstream_delta_batch(clg_engine* e, clg_delta_req* reqs, uint32_t n, con
 }
 
 int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int32_t* offsets, uint32_t n) {
-  ENGINE_GUARD(e);
+  ENGINE_GUARD_KEEP(e);
   if (n && (!reqs || !offsets)) return fail(CLG_E_INVALID_ARG, "null argument");
   for (uint32_t i = 0; i < n; ++i) {
     Log* l;
@@ -1868,6 +1985,36 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
     for (uint32_t i = 0; i < n; ++i) e->plan_log_span(p, *ls[i], st[i], nb[i], i, T);
   };
   return e->decode(build, total, out, span_rec_base);
+}
+
+int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
+                          clg_decoded* out, uint64_t* span_rec_base) {
+  ENGINE_GUARD(e);
+  if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
+  CHK(e->flush());
+  std::vector<uint32_t> hs(log, log + n);
+  std::vector<int32_t> st(n), nb(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    Log* l;
+    CHK(e->get_log(log[i], &l));
+    if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
+    total += uint64_t(nb[i]);
+  }
+  // by value: the robust fallback may re-plan when the decode is settled (the logs' ranges
+  // cannot change before that: every call that could change them settles first)
+  auto build = [e, hs = std::move(hs), st = std::move(st), nb = std::move(nb)](clg_engine::DecodePlan& p, uint32_t T) {
+    for (uint32_t i = 0; i < uint32_t(hs.size()); ++i) e->plan_log_span(p, e->logs[hs[i]], st[i], nb[i], i, T);
+  };
+  return e->decode_async(build, total, out, span_rec_base);
+}
+
+int clg_decode_wait(clg_engine* e) {
+  ENGINE_GUARD_KEEP(e);
+  e->settle();
+  const int st = e->pend.status;
+  e->pend.status = CLG_OK;
+  return st == CLG_OK ? CLG_OK : fail(st, "%s", e->pend.err.c_str());
 }
 
 int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off, const uint64_t* len,

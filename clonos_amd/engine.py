@@ -345,11 +345,36 @@ class Engine:
         sb = [np.frombuffer(l.getDeterminants(e), np.uint8) for l, e in zip(logs, start_epochs)] if keep_bytes else None
         return self._finish(st, d, arrs, base, len(logs), sb)
 
+    def decode_logs_async(self, logs: Sequence["ThreadCausalLog"], start_epochs: Sequence[int]) -> "PendingDecode":
+        """clg_decode_logs_async into host arrays: returns at once; .wait() gives the batch."""
+        h = np.array([l.handle for l in logs], np.uint32)
+        ep = np.array(start_epochs, np.int64)
+        total = sum(l.state()["writer"] for l in logs)
+        d, arrs = self._host_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
+        base = np.zeros(len(logs) + 1, np.uint64)
+        pd = PendingDecode(self, (h, ep, d, arrs, base), len(logs))
+        check(lib.clg_decode_logs_async(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base)))
+        return pd
+
     def decode_logs_device(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
                            base: np.ndarray) -> None:
         """Benchmark variant: outputs are caller-owned device arrays described by `dec`."""
         check(lib.clg_decode_logs(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles), C.byref(dec),
                                   _np_ptr(base)))
+
+    def decode_logs_device_async(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
+                                 base: np.ndarray) -> None:
+        """clg_decode_logs_async: queues the decode and returns; `dec`, `base` and the output
+        arrays stay untouched by the caller until decode_wait()."""
+        self._pending = (handles, start_epochs, dec, base)  # kept alive until the wait
+        check(lib.clg_decode_logs_async(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles),
+                                        C.byref(dec), _np_ptr(base)))
+
+    def decode_wait(self) -> None:
+        """clg_decode_wait: completes a pending asynchronous decode and raises its error."""
+        st = lib.clg_decode_wait(self._h)
+        self._pending = None
+        check(st)
 
     # ---- piggybacked deltas (AbstractDeltaSerializerDeserializer) ---------------------------
     def enrich_batch(self, strategy: int, reqs):
@@ -446,6 +471,18 @@ class Engine:
 
     def kernel_stats_reset(self):
         check(lib.clg_kernel_stats_reset(self._h))
+
+
+class PendingDecode:
+    """A queued clg_decode_logs_async; holds the output arrays until wait()."""
+
+    def __init__(self, engine: "Engine", keep, n_spans: int):
+        self._e, self._keep, self._n = engine, keep, n_spans
+
+    def wait(self) -> DecodedBatch:
+        st = lib.clg_decode_wait(self._e._h)
+        _, _, d, arrs, base = self._keep
+        return self._e._finish(st, d, arrs, base, self._n, None)
 
 
 class ThreadCausalLog:

@@ -270,6 +270,16 @@ int clg_decode_host(clg_engine* e, const uint8_t* bytes, const uint64_t* span_of
  * (no copy: kernels read the segments in place). */
 int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
                     clg_decoded* out, uint64_t* span_rec_base);
+/* Asynchronous clg_decode_logs: returns once the decode is queued on the engine stream, so
+ * the caller can plan and queue other work (e.g. the slices of the same step) while it
+ * runs.  `out`, its arrays and span_rec_base must stay valid, and are not to be read, until
+ * clg_decode_wait returns, which completes the decode (fallback paths included) and
+ * returns its status.  Every other call that needs the engine exclusively completes a
+ * pending decode first (its status is then kept for clg_decode_wait); clg_slice_batch into
+ * device memory with CLG_F_ASYNC_SLICE and the consumer seeks leave it pending. */
+int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
+                          clg_decoded* out, uint64_t* span_rec_base);
+int clg_decode_wait(clg_engine* e);
 
 /* ---- replay-prep (DeterminantResponseEvent.merge + LogReplayer decode) ----------------
  * `n` candidate copies of logs (e.g. one per responding GPU / downstream):

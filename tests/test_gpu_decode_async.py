@@ -1,0 +1,128 @@
+"""GPU: the asynchronous batched decode (clg_decode_logs_async + clg_decode_wait) gives the
+synchronous decode's results bit for bit -- and so the oracle's -- whether it is waited for
+directly, left pending across device slices on the gather stream and consumer seeks, or
+completed implicitly by a call that needs the engine exclusively; errors and the fallback
+paths (Serializable tables, robust pipeline) surface at the wait."""
+import numpy as np
+import pytest
+import torch
+
+import _oracle as O
+from clonos_amd import ClonosError, CausalLogID, Engine, _lib
+from clonos_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def logs_of(eng, blobs):
+    logs = []
+    for v, b in enumerate(blobs):
+        lg = eng.open_log(CausalLogID.main(v))
+        lg.processUpstreamDelta(bytes(b), 0, 1)
+        logs.append(lg)
+    return logs
+
+
+def same(a, b):
+    for f in ("off", "tag", "v0", "w_idx", "w_rc", "w_v1", "w_var_off", "w_var_len", "w_sub", "span_rec_base"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+
+
+def check_oracle(dec, blobs):
+    for s, b in enumerate(blobs):
+        st, r, _, _ = O.decode(bytes(b))
+        assert st == 0
+        sl = dec.span_slice(s)
+        np.testing.assert_array_equal(dec.tag[sl], r["tag"])
+        np.testing.assert_array_equal(dec.v0[sl], r["v0"])
+        np.testing.assert_array_equal(dec.off[sl], r["off"])
+
+
+@pytest.mark.parametrize("decode", ["auto", "robust"])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_async_equals_sync(decode, seed):
+    rng = np.random.default_rng(seed)
+    blobs = [synth.random_log(int(rng.integers(0, 3000)), rng) for _ in range(12)]
+    with Engine(segment_bytes=1024, pool_segments=1 << 14, decode=decode) as eng:
+        logs = logs_of(eng, blobs)
+        ref = eng.decode_logs(logs, [1] * len(logs))
+        got = eng.decode_logs_async(logs, [1] * len(logs)).wait()
+        same(got, ref)
+        check_oracle(got, blobs)
+
+
+def test_async_pending_across_device_slices_and_seeks():
+    """The bench's step: decode queued, consumers rewound, slices gathered into device
+    memory on the second stream while the decode runs, then the wait."""
+    rng = np.random.default_rng(5)
+    blobs = [synth.config2_log(20000, rng)[0] for _ in range(6)]
+    with Engine(segment_bytes=16384, pool_segments=1 << 12, async_slice=True) as eng:
+        logs = logs_of(eng, blobs)
+        n_req = len(logs)
+        creq = (_lib.SliceReq * n_req)()
+        cres = (_lib.SliceRes * n_req)()
+        for i, lg in enumerate(logs):
+            creq[i].log, creq[i].consumer, creq[i].epoch = lg.handle, _lib.ChannelId(3, i), 1
+        total = sum(int(b.size) for b in blobs)
+        out = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        ref = eng.decode_logs(logs, [1] * n_req)
+        for _ in range(3):
+            pd = eng.decode_logs_async(logs, [1] * n_req)
+            eng.seek_consumers_raw(creq, np.zeros(n_req, np.int32), n_req)
+            got_bytes = eng.slice_batch_raw(creq, cres, n_req, out.data_ptr(), out.numel(), device=True)
+            got = pd.wait()
+            assert got_bytes == total
+            same(got, ref)
+            eng.sync()
+            assert out[:total].cpu().numpy().tobytes() == b"".join(bytes(b) for b in blobs)
+
+
+def test_async_settled_by_exclusive_call():
+    """An append flush / log open in between completes the pending decode first; the wait
+    then returns its result, and the decode saw the logs as they were when it was queued."""
+    rng = np.random.default_rng(9)
+    blobs = [synth.random_log(2000, rng) for _ in range(4)]
+    with Engine(segment_bytes=512, pool_segments=1 << 13) as eng:
+        logs = logs_of(eng, blobs)
+        ref = eng.decode_logs(logs, [1] * len(logs))
+        pd = eng.decode_logs_async(logs, [1] * len(logs))
+        eng.open_log(CausalLogID.main(99))           # exclusive: settles the decode
+        logs[0].appendDeterminant(bytes([0, 1]), 2)  # staged; flushed by the next exclusive call
+        eng.sync()
+        same(pd.wait(), ref)
+        assert logs[0].getDeterminants(1)[-2:] == bytes([0, 1])
+
+
+def test_async_error_at_wait():
+    rng = np.random.default_rng(3)
+    good = synth.random_log(500, rng, allow_serializable=False)
+    bad = bytes(good) + bytes([0x7F, 1, 2, 3])  # corrupt tag after the good records
+    with Engine(segment_bytes=256, pool_segments=1 << 12) as eng:
+        logs = logs_of(eng, [good, bad])
+        with pytest.raises(ClonosError) as sync_err:
+            eng.decode_logs(logs, [1, 1])
+        pd = eng.decode_logs_async(logs, [1, 1])
+        eng.sync()  # settles: the error is kept for the wait
+        with pytest.raises(ClonosError) as async_err:
+            pd.wait()
+        a, b = sync_err.value, async_err.value
+        assert (a.status, a.err_span, a.err_off, a.err_tag) == (b.status, b.err_span, b.err_off, b.err_tag)
+        assert b.status == _lib.CLG_E_CORRUPT_TAG and b.err_span == 1 and b.err_off == len(good)
+        # the next wait has nothing pending
+        eng.decode_wait()
+
+
+def test_async_serializable_retry_and_hint():
+    """A batch with Serializable records on a fresh engine (no table hint yet): the async
+    decode aborts, and the wait re-runs it with the tables."""
+    rng = np.random.default_rng(11)
+    e3, offs = synth.config3_epoch(4000, rng, 0)
+    blobs = [e3, e3[:int(offs[len(offs) // 2])]]  # the second cut at a record boundary
+    with Engine(segment_bytes=16384, pool_segments=1 << 10, timing=True) as eng:
+        logs = logs_of(eng, blobs)
+        got = eng.decode_logs_async(logs, [1, 1]).wait()
+        ref = eng.decode_logs(logs, [1, 1])
+        same(got, ref)
+        st, r, _, _ = O.decode(bytes(e3))
+        assert st == 0 and got.span_rec_base[1] == len(r["tag"])
+        assert eng.kernel_stats().get("decode_jser_retry", {}).get("launches", 0) >= 1

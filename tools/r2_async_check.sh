@@ -1,0 +1,9 @@
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/async2
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/async2/all.log 2>&1 &&
+timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-config3 --no-inflight --no-config4 > gpurun_out/async2/b.json 2>gpurun_out/async2/b.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/async2/trace -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-inflight --no-isolated --no-config4 > gpurun_out/async2/trace.log 2>&1 &&
+echo ok
