@@ -143,14 +143,23 @@ def main():
 
     seek_offs = np.array([off for _, _, off in cons], np.int32)
 
+    probe = [0.0] * 4 if os.environ.get("CLONOS_STEP_PROBE") else None  # developer: host time per call
+
     def step():
         # the decode is queued asynchronously, so planning the slices overlaps it on the GPU;
         # the slice gather runs on the engine's second stream beside the decode and the next
         # step's (it only reads log segments); the timed region ends with a device-wide sync
+        c0 = time.perf_counter()
         eng.decode_logs_device_async(handles, starts, dec, base)
+        c1 = time.perf_counter()
         eng.seek_consumers_raw(creq, seek_offs, n_req)  # rewind the consumers to their start offsets
         got = eng.slice_batch_raw(creq, cres, n_req, o_slice.data_ptr(), o_slice.numel(), device=True)
+        c2 = time.perf_counter()
         eng.decode_wait()
+        c3 = time.perf_counter()
+        if probe is not None:
+            for k, v in enumerate((c1 - c0, c2 - c1, c3 - c2, c3 - c0)):
+                probe[k] += v
         assert got == slice_total, (got, slice_total)
 
     # correctness guard on the first step: record count and spot values
@@ -185,6 +194,9 @@ def main():
     torch.cuda.synchronize()
     iso_stats = eng.kernel_stats()
 
+    if probe is not None:
+        print("step probe ms (decode queue, seek+slice, wait, step):",
+              [round(v * 1e3 / (args.steps + 5 + max(0, args.warmup - 1) + 1), 4) for v in probe], file=sys.stderr)
     ms_per_step = elapsed * 1e3 / args.steps
     value = n_det * world / (elapsed / args.steps)
 

@@ -749,7 +749,7 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
 // ---------------------------------------------------------------------------------
 // Launchers.
 // ---------------------------------------------------------------------------------
-static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
+static int ok(hipError_t e) { return launch_status(e); }
 
 int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
                      uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, uint64_t* d_prof, void* stream) {

@@ -1541,7 +1541,7 @@ int launch_decode_one(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc*
   } else {
     hipLaunchKernelGGL(k_decode_spans1, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
   }
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
@@ -1591,7 +1591,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
                        d_tiles, d_spans, ctl);
     hipLaunchKernelGGL(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 }  // namespace clg

@@ -284,7 +284,7 @@ int launch_encode(const EncodeIn& in, uint32_t* d_wsum, uint64_t* d_wbase, uint6
   } else {
     hipLaunchKernelGGL(k_enc_write, dim3(nb), dim3(kEncThreads), 0, st, in, d_wbase, d_bbase, d_out);
   }
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 }  // namespace clg

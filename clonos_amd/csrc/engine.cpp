@@ -50,10 +50,17 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(CLG_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(e_)); \
   } while (0)
 
-#define CHK(x)                     \
-  do {                             \
-    int r_ = (x);                  \
-    if (r_ != CLG_OK) return r_;   \
+// A launch helper's CLG_E_DEVICE carries the HIP error into the error text.
+void note_launch_error(const char* what) {
+  if (const char* m = clg::take_launch_error()) fail(CLG_E_DEVICE, "%s: %s", what, m);
+}
+#define CHK(x)                                          \
+  do {                                                  \
+    int r_ = (x);                                       \
+    if (r_ != CLG_OK) {                                 \
+      if (r_ == CLG_E_DEVICE) note_launch_error(#x);    \
+      return r_;                                        \
+    }                                                   \
   } while (0)
 
 struct EpochStart {
@@ -893,31 +900,49 @@ struct clg_engine {
   // Uploads the plan's descriptors (spans into d_spans) and materialises its tiles in
   // `dtiles` (device planning from the segment table, or the host-built list).
   int upload_plan(DecodePlan& p, DevBuf& dtiles) {
+    PlanLayout L;
+    CHK(stage_plan(p, dtiles, &L));
+    return enqueue_plan(p, L, dtiles);
+  }
+  // Where a staged plan lies in h_plan / d_plan (byte offsets).
+  struct PlanLayout {
+    size_t tb = 0, sb = 0, o_runs = 0, o_seg = 0, o_spans = 0, hb = 0;
+  };
+  // Host half: the plan's descriptors into the pinned plan buffer (its own: an
+  // asynchronous decode may still be uploading it while later calls -- flush, slices --
+  // stage theirs).
+  int stage_plan(const DecodePlan& p, DevBuf& dtiles, PlanLayout* L) {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     CHK(dtiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
     CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
     const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
                  gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
-    const size_t o_runs = (tb + 15) & ~size_t(15), o_seg = (o_runs + rb + 15) & ~size_t(15),
-                 o_spans = (o_seg + gb + 15) & ~size_t(15), hb = o_spans + sb;
-    // the plan has buffers of its own: an asynchronous decode may still be uploading it
-    // while later calls (flush, slices) stage their descriptors
-    CHK(h_plan.ensure(hb + 64));
-    CHK(d_plan.ensure(hb));
+    L->tb = tb;
+    L->sb = sb;
+    L->o_runs = (tb + 15) & ~size_t(15);
+    L->o_seg = (L->o_runs + rb + 15) & ~size_t(15);
+    L->o_spans = (L->o_seg + gb + 15) & ~size_t(15);
+    L->hb = L->o_spans + sb;
+    CHK(h_plan.ensure(L->hb + 64));
+    CHK(d_plan.ensure(L->hb));
     uint8_t* hd = h_plan.as<uint8_t>();
     memcpy(hd, p.tiles.data(), tb);
-    memcpy(hd + o_runs, p.runs.data(), rb);
-    memcpy(hd + o_seg, p.segtab.data(), gb);
-    memcpy(hd + o_spans, p.spans.data(), sb);
-    HIPCHK(hipMemcpyAsync(d_plan.p, hd, hb, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemcpyAsync(d_spans.p, d_plan.as<uint8_t>() + o_spans, sb, hipMemcpyDeviceToDevice, stream));
+    memcpy(hd + L->o_runs, p.runs.data(), rb);
+    memcpy(hd + L->o_seg, p.segtab.data(), gb);
+    memcpy(hd + L->o_spans, p.spans.data(), sb);
+    return CLG_OK;
+  }
+  // Device half: upload, span table, tiles (expanded on the device from the runs).
+  int enqueue_plan(const DecodePlan& p, const PlanLayout& L, DevBuf& dtiles) {
+    HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_spans.p, d_plan.as<uint8_t>() + L.o_spans, L.sb, hipMemcpyDeviceToDevice, stream));
     if (!p.runs.empty()) {
-      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + o_runs),
-                                   uint32_t(p.runs.size()), nt,
-                                   reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + o_seg), pool, C(),
+      CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + L.o_runs),
+                                   uint32_t(p.runs.size()), p.n_tiles,
+                                   reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_seg), pool, C(),
                                    p.unit, dtiles.as<clg::TileDesc>(), stream));
-    } else if (tb) {
-      HIPCHK(hipMemcpyAsync(dtiles.p, d_plan.p, tb, hipMemcpyDeviceToDevice, stream));
+    } else if (L.tb) {
+      HIPCHK(hipMemcpyAsync(dtiles.p, d_plan.p, L.tb, hipMemcpyDeviceToDevice, stream));
     }
     return CLG_OK;
   }
@@ -1009,13 +1034,34 @@ struct clg_engine {
   struct FusedRun {
     uint64_t log_bytes = 0;
     bool jser = false;
-    hipEvent_t ea = nullptr, eb = nullptr;
+    hipEvent_t ea = nullptr, eb = nullptr;  // emit (direct launches; events from ev_pool)
+    bool graph = false;                     // replayed a captured graph
+    hipEvent_t gev[8] = {};                 // the graph's own events: jser, count, offsets, emit
   };
+  // One captured decode per table mode (without / with Serializable tables).
+  struct FusedGraph {
+    std::vector<uint64_t> key;
+    hipGraphExec_t exec = nullptr;
+    hipEvent_t ev[8] = {};
+    void reset() {
+      if (exec) hipGraphExecDestroy(exec);
+      exec = nullptr;
+      for (auto& e : ev) {
+        if (e) hipEventDestroy(e);
+        e = nullptr;
+      }
+      key.clear();
+    }
+  };
+  FusedGraph fgraph[2];
+  bool use_graphs = true;  // CLONOS_GRAPHS=0: always launch directly (timing engines always do)
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
     r->jser = jser;
-    CHK(upload_plan(p, d_ztiles));
+    r->graph = false;
+    PlanLayout L;
+    CHK(stage_plan(p, d_ztiles, &L));
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
     // words: st_x[nt] cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
@@ -1027,21 +1073,14 @@ struct clg_engine {
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
-    if (zdbg) {
-      CHK(d_dbg.ensure(16 * 4 + 64 * 32));
-      HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
-    }
     const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
-    if (prof_path) {
-      CHK(d_prof.ensure(size_t(nt) * 64));
-      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
-    }
+    if (zdbg) CHK(d_dbg.ensure(16 * 4 + 64 * 32));
+    if (prof_path) CHK(d_prof.ensure(size_t(nt) * 64));
     if (jser) {
       CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
       CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
       CHK(d_zjn.ensure(size_t(nt) * 4));
       CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
-      HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
     }
     clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), w + 3 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
@@ -1050,30 +1089,82 @@ struct clg_engine {
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
                       jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr, spec_warm()};
-    HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
-    HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
-    if (jser)
-      CHK(timed("decode_jser", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 3); }));
-    CHK(timed("decode_count", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 0); }));
-    CHK(timed("decode_offsets", 24 * uint64_t(nt), [&] {
-      return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 1);
-    }));
-    // emit right behind the scan (it returns at once when the batch aborted; its stores are
-    // bounded by the output capacity), then read the span ranges and abort words
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (cfg.flags & CLG_F_TIMING) {
-      ea = get_event();
-      eb = get_event();
-      hipEventRecord(ea, stream);
+    const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
+    // The whole sequence, enqueued on `stream`; `ev` (timing) brackets jser, count, offsets
+    // and emit.
+    auto enqueue = [&](hipEvent_t* ev) -> int {
+      CHK(enqueue_plan(p, L, d_ztiles));
+      if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
+      if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
+      if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
+      HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
+      HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
+      for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
+        if (ph == 3 && !jser) continue;
+        const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
+        if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
+        CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
+        if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
+      }
+      // read the span ranges and abort words (emit ran right behind the scan: it returns at
+      // once when the batch aborted, and its stores are bounded by the output capacity)
+      HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+      return CLG_OK;
+    };
+    // Launch-bound: ~15 queue operations per decode.  A batch of the same shape (same tile
+    // and span counts, buffers, outputs) replays one captured hipGraph instead.
+    // (HIP cannot time events a graph records, so a timing engine launches directly.)
+    if (use_graphs && !timing && !zdbg && !prof_path) {
+      std::vector<uint64_t> key = {nt, ns, jser, timing, L.tb, L.sb, L.o_runs, L.o_seg, L.o_spans, L.hb,
+                                   p.runs.size(), p.unit, uint64_t(uintptr_t(d_plan.p)), uint64_t(uintptr_t(h_plan.p)),
+                                   uint64_t(uintptr_t(d_spans.p)), uint64_t(uintptr_t(zt)), uint64_t(uintptr_t(w)),
+                                   uint64_t(uintptr_t(d_zbits.p)), uint64_t(uintptr_t(h_zres.p)),
+                                   uint64_t(uintptr_t(o.off)), uint64_t(uintptr_t(o.tag)), uint64_t(uintptr_t(o.v0)),
+                                   uint64_t(uintptr_t(o.w_idx)), uint64_t(uintptr_t(o.w_rc)), uint64_t(uintptr_t(o.w_v1)),
+                                   uint64_t(uintptr_t(o.w_var_off)), uint64_t(uintptr_t(o.w_var_len)),
+                                   uint64_t(uintptr_t(o.w_sub)), o.cap, o.wcap, uint64_t(uintptr_t(ctl.jpos)),
+                                   uint64_t(uintptr_t(ctl.jlen)), uint64_t(uintptr_t(ctl.jn)),
+                                   uint64_t(uintptr_t(ctl.jwork)), ctl.warm, ctl.nodep};
+      FusedGraph& g = fgraph[jser ? 1 : 0];
+      if (!g.exec || g.key != key) {
+        g.reset();
+        if (timing)
+          for (auto& e : g.ev) HIPCHK(hipEventCreate(&e));
+        hipGraph_t graph = nullptr;
+        bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed) == hipSuccess;
+        const int est = ok ? enqueue(timing ? g.ev : nullptr) : CLG_OK;
+        ok = hipStreamEndCapture(stream, &graph) == hipSuccess && ok && est == CLG_OK;
+        ok = ok && hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0) == hipSuccess;
+        if (graph) hipGraphDestroy(graph);
+        if (!ok) {  // capture unsupported here: launch directly from now on
+          g.reset();
+          use_graphs = false;
+          (void)hipGetLastError();
+        } else {
+          g.key = std::move(key);
+        }
+      }
+      if (use_graphs) {
+        HIPCHK(hipGraphLaunch(g.exec, stream));
+        r->graph = true;
+        if (timing) std::copy(std::begin(g.ev), std::end(g.ev), std::begin(r->gev));
+        return CLG_OK;
+      }
     }
-    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 2));
-    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
-    uint64_t* hz = h_zres.as<uint64_t>();
-    HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
-    r->ea = ea;
-    r->eb = eb;
+    hipEvent_t ev[8] = {};
+    if (timing)
+      for (auto& e : ev) e = get_event();
+    CHK(enqueue(timing ? ev : nullptr));
+    if (timing) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
+      if (jser) timings.push_back(PendingTiming{"decode_jser", ev[0], ev[1], log_bytes});
+      else ev_pool.insert(ev_pool.end(), {ev[0], ev[1]});
+      timings.push_back(PendingTiming{"decode_count", ev[2], ev[3], log_bytes});
+      timings.push_back(PendingTiming{"decode_offsets", ev[4], ev[5], 24 * uint64_t(nt)});
+      r->ea = ev[6];
+      r->eb = ev[7];
+    }
     return CLG_OK;
   }
 
@@ -1096,6 +1187,11 @@ struct clg_engine {
       }
     }
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
+    if (r.graph && (cfg.flags & CLG_F_TIMING)) {  // the graph's events: complete after the sync
+      if (jser) add_stat("decode_jser", r.gev[0], r.gev[1], log_bytes);
+      add_stat("decode_count", r.gev[2], r.gev[3], log_bytes);
+      add_stat("decode_offsets", r.gev[4], r.gev[5], 24 * uint64_t(nt));
+    }
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[0]) {
       if (ea) {
@@ -1135,7 +1231,21 @@ struct clg_engine {
     }
     if (span_rec_base) span_rec_base[ns] = nrec;
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    if (r.graph && (cfg.flags & CLG_F_TIMING)) add_stat("decode_emit", r.gev[6], r.gev[7], log_bytes + 13 * nrec + 25 * nwide);
     return finish_out(out, nrec, nwide);
+  }
+  void add_stat(const char* name, hipEvent_t a, hipEvent_t b, uint64_t bytes) {
+    float ms = 0;
+    const hipError_t e = hipEventElapsedTime(&ms, a, b);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // not sticky: the next launch check must not see it
+      if (getenv("CLONOS_DEBUG_TIMING")) fprintf(stderr, "[clonos] %s: hipEventElapsedTime: %s\n", name, hipGetErrorString(e));
+      return;
+    }
+    Stat& st = stats[name];
+    st.launches++;
+    st.ms += ms;
+    st.bytes += bytes;
   }
 
   // One-pass decode (k_decode_one): stage, chain, look-back and emit per tile in one
@@ -1534,6 +1644,8 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   const char* dm = getenv("CLONOS_DECODE");
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
   e->three_pass = !(dm && !strcmp(dm, "onepass"));
+  const char* gr = getenv("CLONOS_GRAPHS");
+  e->use_graphs = !(gr && !strcmp(gr, "0"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   {
@@ -1582,6 +1694,7 @@ void clg_engine_destroy(clg_engine* e) {
     hipEventDestroy(t.b);
   }
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  for (auto& g : e->fgraph) g.reset();
   if (e->pool_alloc) hipFree(e->pool_alloc);
   if (e->ifl_alloc) hipFree(e->ifl_alloc);
   hipStreamDestroy(e->stream);

@@ -237,6 +237,10 @@ struct SegSpan {
   uint32_t first;       // first piece / tile generated for the run
   uint32_t pad;
 };
+// Launch helpers' status: CLG_OK, or CLG_E_DEVICE with the HIP error kept (thread-local)
+// for the engine's error text (take_launch_error, nullptr when none).
+int launch_status(hipError_t e);
+const char* take_launch_error();
 int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pieces, const uint32_t* d_segtab,
                          const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream);
 int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,

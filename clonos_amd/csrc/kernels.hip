@@ -670,7 +670,21 @@ __global__ __launch_bounds__(64) void k_dec_emit(const TileDesc* __restrict__ ti
 // ==================================================================================
 // Launchers.
 // ==================================================================================
-static int ok(hipError_t e) { return e == hipSuccess ? CLG_OK : CLG_E_DEVICE; }
+namespace {
+thread_local hipError_t g_launch_err = hipSuccess;
+}
+int launch_status(hipError_t e) {
+  if (e == hipSuccess) return CLG_OK;
+  g_launch_err = e;
+  return CLG_E_DEVICE;
+}
+const char* take_launch_error() {
+  const hipError_t e = g_launch_err;
+  g_launch_err = hipSuccess;
+  return e == hipSuccess ? nullptr : hipGetErrorString(e);
+}
+
+static int ok(hipError_t e) { return launch_status(e); }
 
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream) {
   if (!n) return CLG_OK;
@@ -684,7 +698,7 @@ int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pi
   if (!n_pieces) return CLG_OK;
   hipLaunchKernelGGL(k_expand_pieces, dim3((n_pieces + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
                      n_pieces, d_segtab, pool, seg_bytes, d_out);
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
@@ -692,7 +706,7 @@ int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_til
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_expand_tiles, dim3((n_tiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
                      n_tiles, d_segtab, pool, seg_bytes, unit, d_out);
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream) {

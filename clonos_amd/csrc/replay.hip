@@ -76,7 +76,7 @@ int launch_bufsizes(const BufChunk* d_chunks, uint32_t n_chunks, const BufSpan* 
   if (!n_chunks) return CLG_OK;
   hipLaunchKernelGGL(k_bufsizes, dim3(n_chunks), dim3(kBufThreads), 0, (hipStream_t)stream, d_chunks, d_spans,
                      d_sizes, reinterpret_cast<unsigned long long*>(d_first_bad));
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 int launch_bufsizes_classify(const BufSpan* d_spans, uint32_t n_spans, const uint64_t* d_first_bad,
@@ -85,7 +85,7 @@ int launch_bufsizes_classify(const BufSpan* d_spans, uint32_t n_spans, const uin
   if (!n_spans) return CLG_OK;
   hipLaunchKernelGGL(k_bufsizes_classify, dim3((n_spans + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_spans,
                      n_spans, d_first_bad, d_count, d_status, d_err_off, d_err_tag);
-  return hipGetLastError() == hipSuccess ? CLG_OK : CLG_E_DEVICE;
+  return launch_status(hipGetLastError());
 }
 
 }  // namespace clg
