@@ -1034,32 +1034,12 @@ struct clg_engine {
   struct FusedRun {
     uint64_t log_bytes = 0;
     bool jser = false;
-    hipEvent_t ea = nullptr, eb = nullptr;  // emit (direct launches; events from ev_pool)
-    bool graph = false;                     // replayed a captured graph
-    hipEvent_t gev[8] = {};                 // the graph's own events: jser, count, offsets, emit
+    hipEvent_t ea = nullptr, eb = nullptr;  // emit's timing events
   };
-  // One captured decode per table mode (without / with Serializable tables).
-  struct FusedGraph {
-    std::vector<uint64_t> key;
-    hipGraphExec_t exec = nullptr;
-    hipEvent_t ev[8] = {};
-    void reset() {
-      if (exec) hipGraphExecDestroy(exec);
-      exec = nullptr;
-      for (auto& e : ev) {
-        if (e) hipEventDestroy(e);
-        e = nullptr;
-      }
-      key.clear();
-    }
-  };
-  FusedGraph fgraph[2];
-  bool use_graphs = true;  // CLONOS_GRAPHS=0: always launch directly (timing engines always do)
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
     r->jser = jser;
-    r->graph = false;
     PlanLayout L;
     CHK(stage_plan(p, d_ztiles, &L));
     clg::DecodeOut o{};
@@ -1093,7 +1073,8 @@ struct clg_engine {
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     // The whole sequence, enqueued on `stream`; `ev` (timing) brackets jser, count, offsets
-    // and emit.
+    // and emit.  (Captured as a hipGraph and replayed per batch shape it was no faster:
+    // 197 us for a 16-log decode either way, and the bench step unchanged.)
     auto enqueue = [&](hipEvent_t* ev) -> int {
       CHK(enqueue_plan(p, L, d_ztiles));
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
@@ -1113,46 +1094,6 @@ struct clg_engine {
       HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
       return CLG_OK;
     };
-    // Launch-bound: ~15 queue operations per decode.  A batch of the same shape (same tile
-    // and span counts, buffers, outputs) replays one captured hipGraph instead.
-    // (HIP cannot time events a graph records, so a timing engine launches directly.)
-    if (use_graphs && !timing && !zdbg && !prof_path) {
-      std::vector<uint64_t> key = {nt, ns, jser, timing, L.tb, L.sb, L.o_runs, L.o_seg, L.o_spans, L.hb,
-                                   p.runs.size(), p.unit, uint64_t(uintptr_t(d_plan.p)), uint64_t(uintptr_t(h_plan.p)),
-                                   uint64_t(uintptr_t(d_spans.p)), uint64_t(uintptr_t(zt)), uint64_t(uintptr_t(w)),
-                                   uint64_t(uintptr_t(d_zbits.p)), uint64_t(uintptr_t(h_zres.p)),
-                                   uint64_t(uintptr_t(o.off)), uint64_t(uintptr_t(o.tag)), uint64_t(uintptr_t(o.v0)),
-                                   uint64_t(uintptr_t(o.w_idx)), uint64_t(uintptr_t(o.w_rc)), uint64_t(uintptr_t(o.w_v1)),
-                                   uint64_t(uintptr_t(o.w_var_off)), uint64_t(uintptr_t(o.w_var_len)),
-                                   uint64_t(uintptr_t(o.w_sub)), o.cap, o.wcap, uint64_t(uintptr_t(ctl.jpos)),
-                                   uint64_t(uintptr_t(ctl.jlen)), uint64_t(uintptr_t(ctl.jn)),
-                                   uint64_t(uintptr_t(ctl.jwork)), ctl.warm, ctl.nodep};
-      FusedGraph& g = fgraph[jser ? 1 : 0];
-      if (!g.exec || g.key != key) {
-        g.reset();
-        if (timing)
-          for (auto& e : g.ev) HIPCHK(hipEventCreate(&e));
-        hipGraph_t graph = nullptr;
-        bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed) == hipSuccess;
-        const int est = ok ? enqueue(timing ? g.ev : nullptr) : CLG_OK;
-        ok = hipStreamEndCapture(stream, &graph) == hipSuccess && ok && est == CLG_OK;
-        ok = ok && hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0) == hipSuccess;
-        if (graph) hipGraphDestroy(graph);
-        if (!ok) {  // capture unsupported here: launch directly from now on
-          g.reset();
-          use_graphs = false;
-          (void)hipGetLastError();
-        } else {
-          g.key = std::move(key);
-        }
-      }
-      if (use_graphs) {
-        HIPCHK(hipGraphLaunch(g.exec, stream));
-        r->graph = true;
-        if (timing) std::copy(std::begin(g.ev), std::end(g.ev), std::begin(r->gev));
-        return CLG_OK;
-      }
-    }
     hipEvent_t ev[8] = {};
     if (timing)
       for (auto& e : ev) e = get_event();
@@ -1187,11 +1128,6 @@ struct clg_engine {
       }
     }
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
-    if (r.graph && (cfg.flags & CLG_F_TIMING)) {  // the graph's events: complete after the sync
-      if (jser) add_stat("decode_jser", r.gev[0], r.gev[1], log_bytes);
-      add_stat("decode_count", r.gev[2], r.gev[3], log_bytes);
-      add_stat("decode_offsets", r.gev[4], r.gev[5], 24 * uint64_t(nt));
-    }
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[0]) {
       if (ea) {
@@ -1231,23 +1167,8 @@ struct clg_engine {
     }
     if (span_rec_base) span_rec_base[ns] = nrec;
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
-    if (r.graph && (cfg.flags & CLG_F_TIMING)) add_stat("decode_emit", r.gev[6], r.gev[7], log_bytes + 13 * nrec + 25 * nwide);
     return finish_out(out, nrec, nwide);
   }
-  void add_stat(const char* name, hipEvent_t a, hipEvent_t b, uint64_t bytes) {
-    float ms = 0;
-    const hipError_t e = hipEventElapsedTime(&ms, a, b);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();  // not sticky: the next launch check must not see it
-      if (getenv("CLONOS_DEBUG_TIMING")) fprintf(stderr, "[clonos] %s: hipEventElapsedTime: %s\n", name, hipGetErrorString(e));
-      return;
-    }
-    Stat& st = stats[name];
-    st.launches++;
-    st.ms += ms;
-    st.bytes += bytes;
-  }
-
   // One-pass decode (k_decode_one): stage, chain, look-back and emit per tile in one
   // kernel; then the span ranges.  *aborted / *need_jser as in run_fused.
   int run_one(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted, bool jser,
@@ -1644,8 +1565,6 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   const char* dm = getenv("CLONOS_DECODE");
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
   e->three_pass = !(dm && !strcmp(dm, "onepass"));
-  const char* gr = getenv("CLONOS_GRAPHS");
-  e->use_graphs = !(gr && !strcmp(gr, "0"));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   {
@@ -1694,7 +1613,6 @@ void clg_engine_destroy(clg_engine* e) {
     hipEventDestroy(t.b);
   }
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
-  for (auto& g : e->fgraph) g.reset();
   if (e->pool_alloc) hipFree(e->pool_alloc);
   if (e->ifl_alloc) hipFree(e->ifl_alloc);
   hipStreamDestroy(e->stream);

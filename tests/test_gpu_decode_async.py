@@ -128,10 +128,11 @@ def test_async_serializable_retry_and_hint():
         assert eng.kernel_stats().get("decode_jser_retry", {}).get("launches", 0) >= 1
 
 
-def test_graph_replay_same_shape_new_bytes():
-    """Without timing the three-pass decode is captured once per batch shape and replayed:
-    the same shape with other bytes (timestamps rewritten in place), a new shape, then the
-    first shape again -- every result equals the oracle's."""
+def test_repeated_shapes_new_bytes_no_timing():
+    """A non-timing engine decoding the same batch shape again with other bytes (timestamps
+    rewritten in place), a new shape, then the first shape again, sync and async: every
+    result equals the oracle's (the reused plan, control and output buffers carry nothing
+    over)."""
     rng = np.random.default_rng(21)
     shapes = {k: [synth.config2_log(n, rng) for _ in range(m)] for k, (m, n) in {"a": (4, 3000), "b": (7, 1000)}.items()}
 

@@ -1,6 +1,5 @@
 """Latency of small batched decodes (a launch-bound case): 16 logs x ~4 KiB decoded into
-host arrays, repeated; with the captured-graph replay (default, timing off) and without
-(CLONOS_GRAPHS=0 in the environment).  Prints one JSON line."""
+host arrays, repeated, timing off.  Prints one JSON line."""
 import json
 import os
 import sys
@@ -28,5 +27,5 @@ with Engine(segment_bytes=16384, pool_segments=256, timing=False) as eng:
         ts.append((time.perf_counter() - t) * 1e6)
 ts.sort()
 print(json.dumps({"metric": "small batched decode latency (us)", "logs": 16, "bytes": int(sum(b.size for b in blobs)),
-                  "graphs": os.environ.get("CLONOS_GRAPHS", "1") != "0", "p50": round(ts[len(ts) // 2], 1),
+                  "p50": round(ts[len(ts) // 2], 1),
                   "p99": round(ts[int(len(ts) * 0.99)], 1)}))
