@@ -185,11 +185,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = eng.kernel_stats()
-    # isolated pass (after the timed region): the same steps with the slice gather waited
-    # for before the next decode, so every kernel's duration is its own (no overlap)
+    # isolated pass (after the timed region): decode, then the slices, each waited for, so
+    # every kernel's duration is its own (no overlap)
     eng.kernel_stats_reset()
     for _ in range(0 if args.no_isolated else min(args.steps, 5)):
-        step()
+        eng.decode_logs_device(handles, starts, dec, base)
+        eng.seek_consumers_raw(creq, seek_offs, n_req)
+        eng.slice_batch_raw(creq, cres, n_req, o_slice.data_ptr(), o_slice.numel(), device=True)
         eng.sync()
     torch.cuda.synchronize()
     iso_stats = eng.kernel_stats()

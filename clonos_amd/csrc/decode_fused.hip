@@ -931,6 +931,14 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   }
   const uint32_t total = __shfl(incl, 63);
   const uint64_t rec0 = base & ((1ull << 31) - 1), wide0 = base >> 31;
+  // wave-uniform output bases (scalar registers; per-lane 32-bit offsets) and one capacity
+  // test per tile instead of one per record
+  const uint64_t rec0u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)rec0) |
+                         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rec0 >> 32)) << 32;
+  auto* const o_off = gp(out.off) + rec0u;
+  auto* const o_tag = gp(out.tag) + rec0u;
+  auto* const o_v0 = gp(out.v0) + rec0u;
+  const bool fits = rec0u + total <= out.cap;
   Bits cur{bits.x, bits.y};
   uint32_t idx = incl - cnt;
   uint64_t wide = wide0;
@@ -955,9 +963,14 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
       const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
       uint32_t tg = x0 & 0xFFu;
       const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
-      int64_t v0 = tg == CLG_TAG_ORDER       ? (int64_t)(int8_t)(blo & 0xFFu)
-                   : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)bhi << 32 | blo)
-                                             : (int64_t)(int32_t)__builtin_bswap32(blo);
+      // v0 without branches: Order's channel byte, Timestamp's big-endian i64, else (RNG,
+      // BufferBuilt) a big-endian i32; wide records overwrite it below
+      const bool is_ts = tg == CLG_TAG_TIMESTAMP;
+      const uint32_t be32 = __builtin_bswap32(blo);
+      const uint32_t v_lo = is_ts ? __builtin_bswap32(bhi)
+                                  : (tg == CLG_TAG_ORDER ? (uint32_t)(int32_t)(int8_t)(blo & 0xFFu) : be32);
+      const uint32_t v_hi = is_ts ? be32 : (uint32_t)((int32_t)v_lo >> 31);
+      int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
       const bool wide_rec = act && is_wide((int)tg);
       Rec rr{};
       if (wide_rec) {
@@ -973,10 +986,11 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
       const uint64_t g = rec0 + w0 + i;
       if (act) {
         const uint32_t so = (uint32_t)(td.span_off + (a - lo));
-        if (g < out.cap) {
-          gp(out.off)[g] = so;
-          gp(out.tag)[g] = (uint8_t)tg;
-          gp(out.v0)[g] = v0;
+        if (fits || g < out.cap) {
+          const uint32_t j = w0 + i;
+          o_off[j] = so;
+          o_tag[j] = (uint8_t)tg;
+          o_v0[j] = v0;
         }
         if (wide_rec) {
           const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));

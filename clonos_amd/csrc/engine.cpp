@@ -71,6 +71,75 @@ struct Consumer {
   std::shared_ptr<EpochStart> es;  // ConsumerOffset.epochStart (a reference, may go stale)
   int32_t offset;
 };
+
+// EpochStart objects (with their shared_ptr control blocks) come from a per-thread free
+// list: a config-4 step opens an epoch in, and truncates one out of, each of 66 k logs.
+template <class T>
+struct EpochAlloc {
+  using value_type = T;
+  EpochAlloc() = default;
+  template <class U>
+  EpochAlloc(const EpochAlloc<U>&) {}
+  static std::vector<void*>& free_list() {
+    static thread_local std::vector<void*> f;
+    return f;
+  }
+  T* allocate(size_t n) {
+    auto& f = free_list();
+    if (n == 1 && !f.empty()) {
+      void* p = f.back();
+      f.pop_back();
+      return static_cast<T*>(p);
+    }
+    return static_cast<T*>(::operator new(n * sizeof(T)));
+  }
+  void deallocate(T* p, size_t n) {
+    auto& f = free_list();
+    if (n == 1 && f.size() < (1u << 20)) f.push_back(p);
+    else ::operator delete(p);
+  }
+  template <class U>
+  bool operator==(const EpochAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const EpochAlloc<U>&) const { return false; }
+};
+
+// A log's epochs: epoch id -> its start offset, in id order.  A log holds few epochs
+// between checkpoints, appended in increasing order, so a sorted vector (the interface
+// of the std::map it replaces) avoids a node allocation per epoch.
+class EpochMap {
+ public:
+  using value_type = std::pair<int64_t, std::shared_ptr<EpochStart>>;
+  using iterator = std::vector<value_type>::iterator;
+  using const_iterator = std::vector<value_type>::const_iterator;
+  iterator begin() { return v_.begin(); }
+  iterator end() { return v_.end(); }
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  iterator find(int64_t k) {
+    auto it = lower(k);
+    return it != v_.end() && it->first == k ? it : v_.end();
+  }
+  const_iterator find(int64_t k) const { return const_cast<EpochMap*>(this)->find(k); }
+  void emplace(int64_t k, std::shared_ptr<EpochStart> e) {
+    auto it = lower(k);
+    if (it != v_.end() && it->first == k) return;
+    v_.insert(it, value_type(k, std::move(e)));
+  }
+  iterator erase(iterator it) { return v_.erase(it); }
+  // drop every epoch with id < k (checkpoint completion)
+  void erase_below(int64_t k) { v_.erase(v_.begin(), lower(k)); }
+
+ private:
+  iterator lower(int64_t k) {
+    if (v_.empty() || v_.back().first < k) return v_.end();  // the common case: a new epoch
+    return std::lower_bound(v_.begin(), v_.end(), k,
+                            [](const value_type& a, int64_t b) { return a.first < b; });
+  }
+  std::vector<value_type> v_;
+};
 struct ChKey {
   uint64_t lo, hi;
   bool operator==(const ChKey& o) const { return lo == o.lo && hi == o.hi; }
@@ -105,7 +174,7 @@ struct Log {
   int32_t tail_start = 0;
   uint32_t pending_bytes() const { return uint32_t(writer - flushed); }
   const uint8_t* pending_data() const { return tail.data() + (flushed - tail_start); }
-  std::map<int64_t, std::shared_ptr<EpochStart>> epochs;
+  EpochMap epochs;
   std::unordered_map<ChKey, Consumer, ChKeyHash> consumers;
 };
 
@@ -387,7 +456,7 @@ struct clg_engine {
   std::shared_ptr<EpochStart> compute_if_absent(Log& l, int64_t e) {
     auto it = l.epochs.find(e);
     if (it != l.epochs.end()) return it->second;
-    auto es = std::make_shared<EpochStart>(EpochStart{e, l.writer});
+    auto es = std::allocate_shared<EpochStart>(EpochAlloc<EpochStart>(), EpochStart{e, l.writer});
     l.epochs.emplace(e, es);
     return es;
   }
@@ -790,12 +859,7 @@ struct clg_engine {
   // component).
   int checkpoint_complete(Log& l, int64_t cp) {
     auto following = compute_if_absent(l, cp);
-    for (auto it = l.epochs.begin(); it != l.epochs.end();) {
-      if (it->first < cp)
-        it = l.epochs.erase(it);
-      else
-        ++it;
-    }
+    l.epochs.erase_below(cp);
     const int32_t R = following->offset;
     if (R < 0 || R > l.writer) return fail(CLG_E_STATE, "readerIndex %d outside [0, %d]", R, l.writer);
     int32_t move = 0;
