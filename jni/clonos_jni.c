@@ -211,6 +211,66 @@ JNIEXPORT jint JNICALL FN(nDecodeLogs)(JNIEnv* env, jclass cls, jlong e, jintArr
   return s;
 }
 
+/* clg_decode_logs_async: the decode is queued; ctx[0] receives a handle that nDecodeWait
+ * completes and frees (the output ByteBuffers must stay reachable until then). */
+typedef struct {
+  clg_decoded d;
+  uint64_t* base;
+  jsize n;
+} async_decode;
+
+JNIEXPORT jint JNICALL FN(nDecodeLogsAsync)(JNIEnv* env, jclass cls, jlong e, jintArray logs, jlongArray starts,
+                                            jobject off, jobject tag, jobject v0, jobject w_idx, jobject w_rc,
+                                            jobject w_v1, jobject w_var_off, jobject w_var_len, jobject w_sub,
+                                            jlongArray ctx) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, logs);
+  async_decode* a = (async_decode*)calloc(1, sizeof(async_decode));
+  if (!a) return CLG_E_INVALID_ARG;
+  a->base = (uint64_t*)calloc((size_t)n + 1, sizeof(uint64_t));
+  a->n = n;
+  a->d.off = (uint32_t*)addr(env, off, 0);
+  a->d.tag = addr(env, tag, 0);
+  a->d.v0 = (int64_t*)addr(env, v0, 0);
+  a->d.w_idx = (uint32_t*)addr(env, w_idx, 0);
+  a->d.w_rc = (int32_t*)addr(env, w_rc, 0);
+  a->d.w_v1 = (int64_t*)addr(env, w_v1, 0);
+  a->d.w_var_off = (uint32_t*)addr(env, w_var_off, 0);
+  a->d.w_var_len = (uint32_t*)addr(env, w_var_len, 0);
+  a->d.w_sub = addr(env, w_sub, 0);
+  a->d.cap = cap(env, tag);
+  a->d.wcap = cap(env, w_sub);
+  a->d.out_kind = CLG_MEM_HOST;
+  jint* lg = (*env)->GetIntArrayElements(env, logs, NULL);
+  jlong* st = (*env)->GetLongArrayElements(env, starts, NULL);
+  int s = clg_decode_logs_async(ENG(e), (const uint32_t*)lg, (const int64_t*)st, (uint32_t)n, &a->d, a->base);
+  (*env)->ReleaseLongArrayElements(env, starts, st, JNI_ABORT);
+  (*env)->ReleaseIntArrayElements(env, logs, lg, JNI_ABORT);
+  if (s != CLG_OK) {
+    free(a->base);
+    free(a);
+    return s;
+  }
+  jlong h = (jlong)(intptr_t)a;
+  (*env)->SetLongArrayRegion(env, ctx, 0, 1, &h);
+  return s;
+}
+
+/* clg_decode_wait for the decode nDecodeLogsAsync queued: results as nDecodeLogs. */
+JNIEXPORT jint JNICALL FN(nDecodeWait)(JNIEnv* env, jclass cls, jlong e, jlong ctx, jlongArray res,
+                                       jlongArray span_rec_base) {
+  (void)cls;
+  async_decode* a = (async_decode*)(intptr_t)ctx;
+  int s = clg_decode_wait(ENG(e));
+  if (!a) return s;
+  jlong r[6] = {(jlong)a->d.n_rec, (jlong)a->d.n_wide, a->d.err_status, a->d.err_span, a->d.err_off, a->d.err_tag};
+  (*env)->SetLongArrayRegion(env, res, 0, 6, r);
+  (*env)->SetLongArrayRegion(env, span_rec_base, 0, a->n + 1, (const jlong*)a->base);
+  free(a->base);
+  free(a);
+  return s;
+}
+
 /* clg_decode_host over bytes[off, off + len): one span; results as nDecodeLogs. */
 JNIEXPORT jint JNICALL FN(nDecodeHost)(JNIEnv* env, jclass cls, jlong e, jobject bytes, jint off, jint len, jobject o_off,
                                        jobject tag, jobject v0, jobject w_idx, jobject w_rc, jobject w_v1,

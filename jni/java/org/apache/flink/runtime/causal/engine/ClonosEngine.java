@@ -197,6 +197,12 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nDecodeLogs(long engine, int[] logs, long[] startEpochs, ByteBuffer off, ByteBuffer tag,
 								  ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
 								  ByteBuffer wVarLen, ByteBuffer wSub, long[] result, long[] spanRecBase);
+	/** clg_decode_logs_async: ctx[0] = a handle for nDecodeWait (the buffers stay reachable until then). */
+	static native int nDecodeLogsAsync(long engine, int[] logs, long[] startEpochs, ByteBuffer off, ByteBuffer tag,
+									   ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
+									   ByteBuffer wVarLen, ByteBuffer wSub, long[] ctx);
+	/** clg_decode_wait: completes the decode nDecodeLogsAsync queued; result as nDecodeLogs. */
+	static native int nDecodeWait(long engine, long ctx, long[] result, long[] spanRecBase);
 	/** One span of host bytes decoded on the GPU (clg_decode_host); result as nDecodeLogs. */
 	static native int nDecodeHost(long engine, ByteBuffer bytes, int off, int len, ByteBuffer recOff, ByteBuffer tag,
 								  ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc, ByteBuffer wV1, ByteBuffer wVarOff,
