@@ -403,37 +403,61 @@ __device__ __forceinline__ uint32_t spec_len_fast(const uint32_t* T, uint32_t q,
   return L;
 }
 
-template <bool J>
-__device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
-                                                uint32_t r0, const JL& jl) {
+// One speculative step in the region: the start bit of a followed record goes into sbw and,
+// for a wide record, into wbw -- inside the rare branch, so the common path (fixed-length
+// tags) pays nothing for the wide bitmap.  SAFE: the record's bytes cannot pass end_a.
+template <bool J, bool SAFE>
+__device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uint32_t end_a, const JL& jl,
+                                              uint64_t& sbw, uint64_t& wbw, uint32_t& bad) {
+  constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16 | (J ? 0x40u : 0u) << 24;  // tags 0..3
+  constexpr uint32_t kHi = 0x40u | 0x40u << 8 | 0x40u << 16 | 5u << 24;       // tags 4..7
+  const uint32_t tg = zb8(T, q);
+  const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
+  uint32_t L = c;
+  const uint64_t m = 1ull << (q & 63u);
+  if (c & 0x40u) {  // rare: the length needs fields of the record
+    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
+      L = 13;
+    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
+      L = jl_len(jl, q);
+      L = L <= (uint32_t)kZSpecMax ? L : 0u;
+    } else {
+      L = zspec_var(T, q, end_a, tg);
+    }
+    if (!SAFE) L = q + L <= end_a ? L : 0u;
+    if (L) wbw |= m;
+  } else if (!SAFE) {
+    L = q + L <= end_a ? L : 0u;
+  }
+  sbw |= L ? m : 0ull;
+  bad = L ? bad : q + 1u;
+  return q + (L > 1u ? L : 1u);
+}
+
+template <bool J, bool SAFE>
+__device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
+                                             uint32_t r0, const JL& jl) {
   SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
-  const bool safe = re + 16u <= end_a;
   uint32_t q = ws;
   bool w;
   while (q < rs) {
-    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
+    const uint32_t L = spec_len_fast<J>(T, q, end_a, SAFE, jl, &w);
     q += L > 1u ? L : 1u;
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
-  while (q < mid) {
-    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
-    const uint64_t m = (uint64_t)(L ? 1u : 0u) << (q & 63u);
-    s.sb.lo |= m;
-    if (w) s.wb.lo |= m;
-    s.bad = L ? s.bad : q + 1u;
-    q += L > 1u ? L : 1u;
-  }
-  while (q < re) {
-    const uint32_t L = spec_len_fast<J>(T, q, end_a, safe, jl, &w);
-    const uint64_t m = (uint64_t)(L ? 1u : 0u) << (q & 63u);
-    s.sb.hi |= m;
-    if (w) s.wb.hi |= m;
-    s.bad = L ? s.bad : q + 1u;
-    q += L > 1u ? L : 1u;
-  }
+  while (q < mid) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.lo, s.wb.lo, s.bad);
+  while (q < re) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.hi, s.wb.hi, s.bad);
   s.exit = q;
   return s;
+}
+
+template <bool J>
+__device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
+                                                uint32_t r0, const JL& jl) {
+  // lanes whose records cannot run past the span end (all but the last tile's) skip the test
+  return re + 16u <= end_a ? spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl)
+                           : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
 }
 
 // Canonical chain through region: the speculative rule from entry e merged with the
