@@ -80,8 +80,13 @@ struct EpochAlloc {
   EpochAlloc() = default;
   template <class U>
   EpochAlloc(const EpochAlloc<U>&) {}
-  static std::vector<void*>& free_list() {
-    static thread_local std::vector<void*> f;
+  struct FreeList : std::vector<void*> {  // a thread's pooled blocks go back at its exit
+    ~FreeList() {
+      for (void* p : *this) ::operator delete(p);
+    }
+  };
+  static FreeList& free_list() {
+    static thread_local FreeList f;
     return f;
   }
   T* allocate(size_t n) {

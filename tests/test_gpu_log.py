@@ -445,3 +445,40 @@ def test_many_threads_many_logs(tail):
             for i, r in enumerate(recs[t]):
                 ol.append(i // 500, r)
             assert logs[t].getDeterminants(0) == ol.get_determinants(0)[1]
+
+
+def test_many_logs_batched_upstream_and_truncation():
+    """A device-input upstream batch over 6000 logs, each receiving its epoch as two
+    overlapping deltas in ONE batch (the second re-delivers part of the first: dedup), three
+    epochs, then the job's truncation.  Every log's state and bytes == the oracle's
+    ThreadCausalLogImpl fed the same calls (pooled epoch objects, flat epoch maps)."""
+    import torch
+    from clonos_amd import _lib
+    from clonos_amd import dist as X
+    n_logs, seg = 6000, 256
+    rng = np.random.default_rng(77)
+    with Engine(segment_bytes=seg, pool_segments=n_logs * 8, ifl_pool_segments=16) as eng:
+        logs = [eng.open_log(CausalLogID.main(v)) for v in range(n_logs)]
+        oracle = [O.OracleLog(seg) for _ in range(n_logs)]
+        for ep in range(3):
+            blobs = [synth.random_log(int(rng.integers(0, 40)), rng, allow_serializable=False) for _ in range(n_logs)]
+            host = bytearray()
+            reqs = np.zeros(2 * n_logs, X.DELTA_REQ)
+            k = 0
+            for i, b in enumerate(blobs):
+                cut = int(rng.integers(0, len(b) + 1))
+                for off, part in ((0, b[:max(cut, len(b) // 2)]), (cut // 2, b[cut // 2:])):
+                    reqs[k] = (logs[i].handle, off, ep, len(host), len(part), 0)
+                    host += part
+                    k += 1
+                    assert oracle[i].upstream(part, off, ep) == 0
+            d = torch.frombuffer(bytearray(host or b"\0"), dtype=torch.uint8).to("cuda")
+            _lib.check(_lib.lib.clg_upstream_delta_batch(eng.handle, reqs.ctypes.data, len(reqs), d.data_ptr(),
+                                                         _lib.CLG_MEM_DEVICE))
+            assert (reqs["status"] == 0).all()
+        assert eng.truncate_all(2)
+        for i in range(n_logs):
+            assert oracle[i].checkpoint_complete(2) == 0
+        for i in rng.choice(n_logs, 400, replace=False):
+            assert logs[i].state() == oracle[i].state(), i
+            assert logs[i].getDeterminants(2) == oracle[i].get_determinants(2)[1], i
