@@ -968,10 +968,16 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   uint64_t wide = wide0;
   for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
     const uint32_t wend = w0 + kZWin;
-    while ((cur.lo | cur.hi) && idx < wend) {
-      const uint32_t i = cur.lo ? (uint32_t)__builtin_ctzll(cur.lo) : 64u + (uint32_t)__builtin_ctzll(cur.hi);
-      if (cur.lo) cur.lo &= cur.lo - 1; else cur.hi &= cur.hi - 1;
-      s_pos[idx - w0] = (uint16_t)(r0 + i);
+    // the lane's record starts into s_pos in order: the low 64 region bytes, then the high
+    // 64 (one 64-bit word per loop: no per-start choice between the halves)
+    while (cur.lo && idx < wend) {
+      s_pos[idx - w0] = (uint16_t)(r0 + (uint32_t)__builtin_ctzll(cur.lo));
+      cur.lo &= cur.lo - 1;
+      ++idx;
+    }
+    while (!cur.lo && cur.hi && idx < wend) {
+      s_pos[idx - w0] = (uint16_t)(r0 + 64u + (uint32_t)__builtin_ctzll(cur.hi));
+      cur.hi &= cur.hi - 1;
       ++idx;
     }
     __syncthreads();
@@ -1494,10 +1500,16 @@ __global__ __launch_bounds__(64) void k_decode_one(const TileDesc* __restrict__ 
   uint32_t idx = incl - cnt;
   for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
     const uint32_t wend = w0 + kZWin;
-    while ((cur.lo | cur.hi) && idx < wend) {
-      const uint32_t i = cur.lo ? (uint32_t)__builtin_ctzll(cur.lo) : 64u + (uint32_t)__builtin_ctzll(cur.hi);
-      if (cur.lo) cur.lo &= cur.lo - 1; else cur.hi &= cur.hi - 1;
-      s_pos[idx - w0] = (uint16_t)(r0 + i);
+    // the lane's record starts into s_pos in order: the low 64 region bytes, then the high
+    // 64 (one 64-bit word per loop: no per-start choice between the halves)
+    while (cur.lo && idx < wend) {
+      s_pos[idx - w0] = (uint16_t)(r0 + (uint32_t)__builtin_ctzll(cur.lo));
+      cur.lo &= cur.lo - 1;
+      ++idx;
+    }
+    while (!cur.lo && cur.hi && idx < wend) {
+      s_pos[idx - w0] = (uint16_t)(r0 + 64u + (uint32_t)__builtin_ctzll(cur.hi));
+      cur.hi &= cur.hi - 1;
       ++idx;
     }
     __syncthreads();
