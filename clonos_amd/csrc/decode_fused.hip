@@ -429,7 +429,9 @@ __device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uin
   } else if (!SAFE) {
     L = q + L <= end_a ? L : 0u;
   }
-  sbw |= L ? m : 0ull;
+  // a skipped byte's bit is set too: every skip lies below `bad`, and the merge walk only
+  // uses starts at or past `bad`, so such bits are never read
+  sbw |= m;
   bad = L ? bad : q + 1u;
   return q + (L > 1u ? L : 1u);
 }
