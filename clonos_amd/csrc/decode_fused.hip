@@ -54,7 +54,8 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_FUSED_PIPELINE
 #define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
 #endif
-constexpr uint32_t kZWin = 1024;                       // record starts staged per emit window
+constexpr uint32_t kZWin = 1024;                       // record starts staged per window (one-pass kernel)
+constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
@@ -932,7 +933,13 @@ template <bool J>
 __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                     FusedCtl ctl, DecodeOut out) {
   __shared__ uint32_t s_img[kZImgDw];
-  __shared__ uint16_t s_pos[kZWin];
+  // record starts of the window by output position.  With Serializable tables (J: the
+  // batches with many wide records) the entries are 32-bit and, reused in place, also hold
+  // the window's wide records (position | window index << 16) for a compacted wide pass;
+  // without, 16-bit entries and wide records decoded inline (same 2 KiB of LDS either way).
+  using PosT = typename std::conditional<J, uint32_t, uint16_t>::type;
+  constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
+  __shared__ PosT s_pos[kWin];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
@@ -968,26 +975,27 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   Bits cur{bits.x, bits.y};
   uint32_t idx = incl - cnt;
   uint64_t wide = wide0;
-  for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
-    const uint32_t wend = w0 + kZWin;
+  for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
+    const uint32_t wend = w0 + kWin;
     // the lane's record starts into s_pos in order: the low 64 region bytes, then the high
     // 64 (one 64-bit word per loop: no per-start choice between the halves)
     while (cur.lo && idx < wend) {
-      s_pos[idx - w0] = (uint16_t)(r0 + (uint32_t)__builtin_ctzll(cur.lo));
+      s_pos[idx - w0] = (PosT)(r0 + (uint32_t)__builtin_ctzll(cur.lo));
       cur.lo &= cur.lo - 1;
       ++idx;
     }
     while (!cur.lo && cur.hi && idx < wend) {
-      s_pos[idx - w0] = (uint16_t)(r0 + 64u + (uint32_t)__builtin_ctzll(cur.hi));
+      s_pos[idx - w0] = (PosT)(r0 + 64u + (uint32_t)__builtin_ctzll(cur.hi));
       cur.hi &= cur.hi - 1;
       ++idx;
     }
     __syncthreads();
-    const uint32_t nw = total - w0 < kZWin ? total - w0 : kZWin;
+    const uint32_t nw = total - w0 < kWin ? total - w0 : kWin;
+    uint32_t nwide = 0;  // wide records of the window so far (wave-uniform)
     for (uint32_t i0 = 0; i0 < nw; i0 += 64) {
       const uint32_t i = i0 + lane;
       const bool act = i < nw;
-      const uint32_t a = act ? (uint32_t)s_pos[i] : lo;
+      const uint32_t a = act ? s_pos[i] : lo;
       const uint32_t kk = rk(a >> 2), sh = 8u * (a & 3u);
       const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
       const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
@@ -996,48 +1004,88 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
       uint32_t tg = x0 & 0xFFu;
       const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
       // v0 without branches: Order's channel byte, Timestamp's big-endian i64, else (RNG,
-      // BufferBuilt) a big-endian i32; wide records overwrite it below
+      // BufferBuilt) a big-endian i32; wide records get theirs in the wide pass
       const bool is_ts = tg == CLG_TAG_TIMESTAMP;
       const uint32_t be32 = __builtin_bswap32(blo);
       const uint32_t v_lo = is_ts ? __builtin_bswap32(bhi)
                                   : (tg == CLG_TAG_ORDER ? (uint32_t)(int32_t)(int8_t)(blo & 0xFFu) : be32);
       const uint32_t v_hi = is_ts ? be32 : (uint32_t)((int32_t)v_lo >> 31);
-      int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
+      const int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
       const bool wide_rec = act && is_wide((int)tg);
-      Rec rr{};
-      if (wide_rec) {
-        const ZBytes b{s_img, a};
-        int tagd;
-        uint32_t tgu;
-        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
-        tagd = (int)tg;
-        decode_fields(b, tagd, (int64_t)L, rr);
-        v0 = rr.v0;
-      }
       const uint64_t wm = __ballot(wide_rec);
-      const uint64_t g = rec0 + w0 + i;
-      if (act) {
-        const uint32_t so = (uint32_t)(td.span_off + (a - lo));
-        if (fits || g < out.cap) {
-          const uint32_t j = w0 + i;
-          o_off[j] = so;
-          o_tag[j] = (uint8_t)tg;
-          o_v0[j] = v0;
+      if constexpr (J) {
+        if (act) {
+          const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+          if (fits || rec0 + w0 + i < out.cap) {
+            const uint32_t j = w0 + i;
+            o_off[j] = so;
+            o_tag[j] = (uint8_t)tg;
+            if (!wide_rec) o_v0[j] = v0;
+          }
+          // compaction in place: every entry below i0 + 64 has been read already
+          if (wide_rec) s_pos[nwide + (uint32_t)__popcll(wm & ((1ull << lane) - 1ull))] = a | i << 16;
         }
+        nwide += (uint32_t)__popcll(wm);
+      } else {
+        Rec rr{};
+        int64_t v = v0;
         if (wide_rec) {
-          const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
-          if (wi < out.wcap) {
-            gp(out.w_idx)[wi] = (uint32_t)g;
-            gp(out.w_rc)[wi] = rr.rc;
-            gp(out.w_v1)[wi] = rr.v1;
-            gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
-            gp(out.w_var_len)[wi] = rr.var_len;
-            gp(out.w_sub)[wi] = rr.sub;
+          uint32_t tgu;
+          const int L = zlen(s_img, a, end_a, &tgu);
+          decode_fields(ZBytes{s_img, a}, (int)tg, (int64_t)L, rr);
+          v = rr.v0;
+        }
+        if (act) {
+          const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+          const uint64_t g = rec0 + w0 + i;
+          if (fits || g < out.cap) {
+            const uint32_t j = w0 + i;
+            o_off[j] = so;
+            o_tag[j] = (uint8_t)tg;
+            o_v0[j] = v;
+          }
+          if (wide_rec) {
+            const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+            if (wi < out.wcap) {
+              gp(out.w_idx)[wi] = (uint32_t)g;
+              gp(out.w_rc)[wi] = rr.rc;
+              gp(out.w_v1)[wi] = rr.v1;
+              gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
+              gp(out.w_var_len)[wi] = rr.var_len;
+              gp(out.w_sub)[wi] = rr.sub;
+            }
           }
         }
+        wide += (uint64_t)__popcll(wm);
       }
-      wide += (uint64_t)__popcll(wm);
     }
+    __syncthreads();
+    // the window's wide records, 64 at a time: field decoding and side-table rows run with
+    // every lane busy instead of inside the record loop's divergent branch
+    for (uint32_t k0 = 0; J && k0 < nwide; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      if (k < nwide) {
+        const uint32_t e = s_pos[k], a = e & 0xFFFFu, i = e >> 16;
+        const uint64_t g = rec0 + w0 + i;
+        const uint32_t tg = zb(s_img, a);
+        uint32_t tgu;
+        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
+        Rec rr{};
+        decode_fields(ZBytes{s_img, a}, (int)tg, (int64_t)L, rr);
+        if (fits || g < out.cap) o_v0[w0 + i] = rr.v0;
+        const uint64_t wi = wide + k;
+        if (wi < out.wcap) {
+          const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+          gp(out.w_idx)[wi] = (uint32_t)g;
+          gp(out.w_rc)[wi] = rr.rc;
+          gp(out.w_v1)[wi] = rr.v1;
+          gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
+          gp(out.w_var_len)[wi] = rr.var_len;
+          gp(out.w_sub)[wi] = rr.sub;
+        }
+      }
+    }
+    wide += nwide;
     __syncthreads();
   }
 }
