@@ -1247,8 +1247,8 @@ constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
 __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                          const FusedCtl& ctl, uint32_t* s_img, const uint32_t t, const uint32_t lane,
-                                          bool* flagged) {
+                                          const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_cand, const uint32_t t,
+                                          const uint32_t lane, bool* flagged) {
   const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const ZTile z = ztile(tiles, spans, t, lane);
   stage_image<kZJHalo, kZJRows>(z.td, z.sd, t, tiles, s_img, lane, z.hi);
@@ -1300,34 +1300,41 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   const uint32_t t1 = z.sd.first_tile + z.sd.n_tiles;
   uint32_t idx = ex - nm;
   (void)t1;
-  auto emit = [&](uint32_t a) {
-    const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
-    bool general;
-    const uint64_t L = jser_inline_len(s_img, a, img_end, avail, &general);
-    if (idx < kZJCap) {
-      gp(ctl.jpos)[(uint64_t)t * kZJCap + idx] = a;
-      gp(ctl.jlen)[(uint64_t)t * kZJCap + idx] = general ? kZJGeneral : (L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u);
-      if (general) {  // nested objects, arrays, ...: k_decode_jser_general walks the grammar
-        const uint32_t w = atomicAdd(ctl.jwork, 1u);
-        if (w < ctl.jwork_cap) ctl.jwork[1 + w] = t * kZJCap + idx;
-        else raise_abort(ctl, 6, t);
-      }
-    }
+  // the tile's candidates in order into LDS, then their lengths 64 at a time (a lane holds
+  // ~1 candidate on average: computed in place, the inline parser ran once per register
+  // slot with few lanes active)
+  auto put = [&](uint32_t a) {
+    if (idx < kZJCap) s_cand[idx] = a;
     ++idx;
   };
   if (!nm) {
   } else if (nm <= (uint32_t)kZJReg) {
 #pragma unroll
     for (int r = 0; r < kZJReg; ++r)
-      if ((uint32_t)r < nm) emit(cand[r]);
+      if ((uint32_t)r < nm) put(cand[r]);
   } else {  // rare: rescan the region
     for (uint32_t k = z.rs >> 2; 4 * k < z.re; ++k) {
       const uint32_t w = s_img[rk(k)] ^ 0x03030303u;
       if (!((w - 0x01010101u) & ~w & 0x80808080u)) continue;
       for (uint32_t i = 0; i < 4; ++i) {
         const uint32_t a = 4 * k + i;
-        if (a >= z.rs && a < z.re && zmagic(s_img, a)) emit(a);
+        if (a >= z.rs && a < z.re && zmagic(s_img, a)) put(a);
       }
+    }
+  }
+  __syncthreads();
+  const uint32_t nc = total < kZJCap ? total : kZJCap;
+  for (uint32_t k = lane; k < nc; k += 64) {
+    const uint32_t a = s_cand[k];
+    const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
+    bool general;
+    const uint64_t L = jser_inline_len(s_img, a, img_end, avail, &general);
+    gp(ctl.jpos)[(uint64_t)t * kZJCap + k] = a;
+    gp(ctl.jlen)[(uint64_t)t * kZJCap + k] = general ? kZJGeneral : (L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u);
+    if (general) {  // nested objects, arrays, ...: k_decode_jser_general walks the grammar
+      const uint32_t w = atomicAdd(ctl.jwork, 1u);
+      if (w < ctl.jwork_cap) ctl.jwork[1 + w] = t * kZJCap + k;
+      else raise_abort(ctl, 6, t);
     }
   }
   if (ctl.prof && lane == 0) {  // developer diagnostics: stage / scan+lengths cycles
@@ -1340,9 +1347,10 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
 __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                     FusedCtl ctl) {
   __shared__ uint32_t s_img[kZJRows * kZPitch];
+  __shared__ uint32_t s_cand[kZJCap];
   bool flagged = false;
   for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
-    jser_tile(tiles, spans, ctl, s_img, t, threadIdx.x, &flagged);
+    jser_tile(tiles, spans, ctl, s_img, s_cand, t, threadIdx.x, &flagged);
     __syncthreads();  // the image is reused by the next tile
   }
 }
