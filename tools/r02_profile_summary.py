@@ -110,7 +110,11 @@ for k, v in durations("trace").items():
     timed[k] = {"dispatches": len(v), "timed_avg_ms": round(sum(last) / len(last), 5), "all_avg_ms": round(sum(v) / len(v), 5)}
 timed["note"] = ("timed_avg_ms: mean of the last %d dispatches of each kernel in the rocprofv3 kernel trace of "
                  "`bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-inflight --no-isolated "
-                 "--no-config4` (the timed region); all_avg_ms includes the warm-up dispatches" % STEPS)
+                 "--no-config4` (the timed region); all_avg_ms includes the warm-up dispatches.  Under "
+                 "rocprofv3 --kernel-trace the two streams do not overlap (the trace shows the slice gather "
+                 "starting after the decode's emit), so these are isolated durations: compare them with the "
+                 "bench's kernels_isolated / roofline_isolated; the bench's timed-region figure (gather beside "
+                 "the decode) has no counterpart under the profiler" % STEPS)
 json.dump(timed, open(os.path.join(prof, f"{tag}_kernel_timed.json"), "w"), indent=1)
 c3_bytes = b["config3"]["log_bytes"]
 pmc = {"config2": decode_table("c2", b["config"]["log_bytes_per_gpu"]),
