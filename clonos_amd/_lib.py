@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libclonos_engine.so")
+LIB_PATH = os.environ.get("CLONOS_LIB") or os.path.join(HERE, "libclonos_engine.so")  # CLONOS_LIB: A/B builds
 
 # ---- status codes (clonos_engine.h) ------------------------------------------------
 CLG_OK = 0

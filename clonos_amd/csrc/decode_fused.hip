@@ -169,25 +169,10 @@ __device__ __forceinline__ int zlen(const uint32_t* T, uint32_t a, uint32_t end_
 //   spec step  -- follow records of at most kZSpecMax bytes, step one byte past anything
 //                 else.  Speculative chains start at arbitrary bytes, and a garbage
 //                 TimerTrigger / SourceCheckpoint can claim a length of megabytes; the cap
-//                 keeps such a chain local.  A skip is recorded (Spec::bad) because from
+//                 keeps such a chain local.  A skip is recorded (SpecR::bad) because from
 //                 a skipped byte on the speculative chain no longer follows the true one.
 // ---------------------------------------------------------------------------------
 constexpr int kZSpecMax = 256;
-constexpr uint32_t kZBitsPitch = 5;  // dwords per lane of the LDS spec bitmaps (4 + 1: banks)
-
-struct Spec {
-  Bits wb;         // followed wide starts in the region (the starts themselves: LDS bitmap)
-  uint32_t first;  // first position >= rs
-  uint32_t exit;   // first position >= re
-  uint32_t bad;    // 1 + last position skipped inside the region, 0 if none
-};
-
-// Speculative step length at a (< tile end): L in [1, kZSpecMax] to follow the record,
-// 0 to step one byte.  Fixed-length tags cost a nibble table (kZLut; 0: not followed,
-// 15: TimerTrigger / SourceCheckpoint / IgnoreCheckpoint, the out-of-line case);
-// Serializable and invalid tags are never followed.  *wide: the record is a wide one.
-constexpr uint32_t kZLut = 2u | 9u << 4 | 5u << 8 | 0u << 12 | 15u << 16 | 15u << 20 | 15u << 24 | 5u << 28;
-constexpr uint32_t kZLutJ = kZLut | 15u << 12;  // with tables: Serializable is a wide case too
 
 // Serializable record lengths of the tile (phase 3 tables), staged in LDS: a candidate
 // bitmap over aligned coordinates, the number of candidates before each bitmap dword, and
@@ -204,75 +189,6 @@ __device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
   return j.len[j.rank[a >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))];
 }
 
-template <bool J>
-__device__ __forceinline__ uint32_t zspec_len(const uint32_t* T, uint32_t a, uint32_t end_a, bool* wide, const JL& jl) {
-  const uint32_t tg = zb8(T, a);
-  uint32_t L = __builtin_amdgcn_ubfe(J ? kZLutJ : kZLut, tg << 2, 4);
-  *wide = false;
-  if (L == 15u && tg < 8u) {
-    *wide = true;
-    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
-      L = 13;
-    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
-      L = jl_len(jl, a);
-      L = L <= (uint32_t)kZSpecMax ? L : 0u;
-    } else {
-      const int v = zlen_var(T, a, end_a, tg, 0);
-      L = (v > 0 && v <= kZSpecMax) ? (uint32_t)v : 0u;
-    }
-  }
-  return (tg < 8u && a + L <= end_a) ? L : 0u;
-}
-
-// The walk starts kZWarm bytes before the region (inside the previous one), so that by
-// the region start the chain has almost always re-synchronised with the true one; then
-// true chains meet it at their first step and entries rarely cascade across lanes.  Skips
-// in the warm-up never matter (true chains meet it at or after rs).  The region's
-// followed starts are or-ed into the lane's LDS bitmap `bits` (bit i <-> byte r0 + i,
-// r0 = rs & ~127; zeroed by the caller).
-constexpr uint32_t kZWarm = 96;
-template <bool J>
-__device__ __forceinline__ Spec spec_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
-                                          uint32_t* bits, const JL& jl) {
-  Spec s{{0, 0}, rs, rs, 0};
-  uint32_t q = ws;
-  while (q < rs) {
-    bool w;
-    const uint32_t L = zspec_len<J>(T, q, end_a, &w, jl);
-    q += L > 1u ? L : 1u;
-  }
-  s.first = q;
-  while (q < re) {
-    bool w;
-    const uint32_t L = zspec_len<J>(T, q, end_a, &w, jl);
-    const uint32_t nq = q + (L > 1u ? L : 1u);
-    atomicOr(&bits[(q >> 5) & 3u], L ? 1u << (q & 31u) : 0u);
-    if (w && L) bset(s.wb, q & 127u);
-    s.bad = L ? s.bad : nq;
-    q = nq;
-  }
-  s.exit = q;
-  return s;
-}
-
-// Canonical chain: the speculative rule from entry e, merged with the region's
-// speculative chain (both follow the same rule, so meeting means identical from there).
-template <bool J>
-__device__ __forceinline__ uint32_t canon_walk(const uint32_t* T, uint32_t rs, uint32_t re, uint32_t end_a, uint32_t e,
-                                               const Spec& s, const JL& jl) {
-  if (e >= re) return e;
-  uint32_t p = e, q = s.first;
-  for (;;) {
-    if (p == q) return s.exit;
-    if (p >= re) return p;
-    bool w;
-    const uint32_t x = p < q ? p : q;
-    const uint32_t L = zspec_len<J>(T, x, end_a, &w, jl);
-    const uint32_t nx = x + (L > 1u ? L : 1u);
-    if (p < q) p = nx; else q = nx;
-  }
-}
-
 struct Res {
   Bits bm, wb;     // true record starts in the region / wide ones
   uint32_t exit;   // first true start >= re (bad: the speculative exit)
@@ -283,68 +199,6 @@ struct Res {
 // True step lengths of the fixed-length tags (nibble per tag; 15: Serializable,
 // TimerTrigger, SourceCheckpoint, IgnoreCheckpoint, the out-of-line case).
 constexpr uint32_t kZLutTrue = 2u | 9u << 4 | 5u << 8 | 15u << 12 | 15u << 16 | 15u << 20 | 15u << 24 | 5u << 28;
-
-// True chain from entry e (e >= rs) merged with the speculative chain (its starts are the
-// lane's LDS bitmap `bits`): walk the true chain until it lands on a speculative start
-// past the speculative chain's last skip; from there on the two chains are the same.
-template <bool J>
-__device__ __forceinline__ Res merge_walk(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e, const Spec& s,
-                                          const uint32_t* bits, const JL& jl) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0};
-  if (e >= re) return r;  // no record starts in this region
-  const uint32_t b0 = bits[0], b1 = bits[1], b2 = bits[2], b3 = bits[3];
-  uint32_t p = e;
-  Bits pb{0, 0}, pw{0, 0};
-  for (;; ++r.steps) {
-    if (p >= re) break;
-    const uint32_t i = p & 127u;
-    const uint32_t w = (i & 64u) ? ((i & 32u) ? b3 : b2) : ((i & 32u) ? b1 : b0);
-    if (__builtin_amdgcn_ubfe(w, i, 1) && p >= s.bad) {  // met the speculative chain
-      const Bits sb{(uint64_t)b1 << 32 | b0, (uint64_t)b3 << 32 | b2};
-      r.bm = bor(pb, bge(sb, i));
-      r.wb = bor(pw, bge(s.wb, i));
-      r.exit = s.exit;
-      return r;
-    }
-    const uint32_t tg = zb8(T, p);
-    uint32_t L = __builtin_amdgcn_ubfe(kZLutTrue, tg << 2, 4);
-    if (L == 15u || tg >= 8u) {  // rare: wide, Serializable or invalid
-      int v;
-      uint32_t why = 1u;
-      if (tg >= 8u) {
-        v = (int)kLenErr;
-      } else if (tg == CLG_TAG_SERIALIZABLE) {
-        if (J) {
-          const uint32_t jv = jl_len(jl, p);
-          v = jv ? (int)jv : (int)kLenErr;
-        } else {  // a stream with the magic needs the tables (abort reason 5)
-          v = (int)kLenErr;
-          why = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
-        }
-      } else {
-        v = tg == CLG_TAG_IGNORE_CHECKPOINT ? 13 : zlen_var(T, p, end_a, tg, 0);
-      }
-      if (v <= 0) {
-        r.bad = why;
-        r.exit = s.exit;
-        return r;
-      }
-      L = (uint32_t)v;
-      bset(pw, i);
-    }
-    if (p + L > end_a || p + L < p) {
-      r.bad = 1;
-      r.exit = s.exit;
-      return r;
-    }
-    bset(pb, i);
-    p += L;
-  }
-  r.bm = pb;
-  r.wb = pw;
-  r.exit = p;
-  return r;
-}
 
 struct SpecR {
   Bits sb, wb;     // followed starts in the region / wide ones (registers)
@@ -575,15 +429,26 @@ __device__ __forceinline__ uint64_t pack_cnt(uint32_t rec, uint32_t wide) { retu
 // Stage tile t into the padded row layout: the tile (16-byte loads, all in flight before
 // any LDS store), a halo of the span's next bytes, a zero pad, then every row's pad dwords.
 // kHaloMax bytes of halo (kZHalo for count / emit; phase 3 stages more so that whole
-// Serializable streams near the tile end are in LDS); kRows rows of image.
+// Serializable streams near the tile end are in LDS); kRows rows of image.  n1: the next
+// tile's descriptor when the caller has it.  If that tile continues the span and holds the
+// whole halo (every tile but a span's last two, normally), the halo bytes are loaded
+// together with the tile, so staging costs one memory latency; otherwise the halo is found
+// by walking the span's tiles.
 template <uint32_t kHaloMax = kZHalo, uint32_t kRows = kZRows>
 __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
                                             const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
-                                            const uint32_t hi) {
+                                            const uint32_t hi, const TileDesc* n1 = nullptr) {
   static_assert((kZTile + 15 + kHaloMax + 64 + 127) / 128 <= kRows, "image rows: tile + halo + zero pad");
   const uint32_t t1 = sd.first_tile + sd.n_tiles;
+  const uint64_t after = td.span_off + td.len;
+  const uint64_t rem = sd.len > after ? sd.len - after : 0;
+  const uint32_t halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
+  const uint32_t img_end = hi + halo;
+  const bool near = kHaloMax <= 64u && n1 && halo && t + 1 < t1 && n1->span_off == after && n1->len >= halo;
+  uint32_t hb = 0;
   {
-    // every lane issues its 8 loads before any LDS store (the tile is at most 512 x 16 B)
+    // every lane issues its 8 loads (and its halo byte) before any LDS store (the tile is at
+    // most 512 x 16 B)
     const uint32_t words = (hi + 15) >> 4;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
@@ -594,6 +459,7 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
       const uint32_t w = lane + 64u * (uint32_t)i;
       v[i] = src[w < words ? w : words - 1u];
     }
+    if (near && lane < halo) hb = gp(n1->abase)[n1->delta + lane];
 #pragma unroll
     for (int i = 0; i < kLoads; ++i) {
       const uint32_t w = lane + 64u * (uint32_t)i;
@@ -606,33 +472,33 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
       }
     }
   }
-  const uint64_t after = td.span_off + td.len;
-  const uint64_t rem = sd.len > after ? sd.len - after : 0;
-  const uint32_t halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
-  const uint32_t img_end = hi + halo;
-  __syncthreads();
+  __syncthreads();  // the tile's last word may run past hi: the halo overwrites it
   {
     uint8_t* bb = reinterpret_cast<uint8_t*>(s_img);
-    const TileDesc n1 = halo ? tiles[t + 1] : td;
-    if (kHaloMax > 64u && halo > 64u && n1.span_off == after && n1.len >= halo) {
-      // the next tile holds the whole halo: 16-byte loads, byte stores
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      for (uint32_t c = lane; 16u * c < n1.delta + halo; c += 64) {
-        const u32x4 v = gp(reinterpret_cast<const u32x4*>(n1.abase))[c];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (uint32_t b = 0; b < 16; ++b) {
-          const uint32_t x = 16u * c + b;  // byte of the next tile's aligned coordinates
-          if (x >= n1.delta && x < n1.delta + halo) bb[rb(hi + x - n1.delta)] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
-        }
-      }
+    if (near) {
+      if (lane < halo) bb[rb(hi + lane)] = (uint8_t)hb;
     } else {
-      uint32_t k = t + 1;
-      for (uint32_t i = lane; i < halo; i += 64) {
-        const uint64_t o = after + i;  // span offset of the halo byte
-        while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
-        const TileDesc nt = tiles[k];
-        bb[rb(hi + i)] = gp(nt.abase)[nt.delta + (uint32_t)(o - nt.span_off)];
+      const TileDesc nn = halo ? tiles[t + 1] : td;
+      if (kHaloMax > 64u && halo > 64u && nn.span_off == after && nn.len >= halo) {
+        // the next tile holds the whole halo: 16-byte loads, byte stores
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        for (uint32_t c = lane; 16u * c < nn.delta + halo; c += 64) {
+          const u32x4 v = gp(reinterpret_cast<const u32x4*>(nn.abase))[c];
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t b = 0; b < 16; ++b) {
+            const uint32_t x = 16u * c + b;  // byte of the next tile's aligned coordinates
+            if (x >= nn.delta && x < nn.delta + halo) bb[rb(hi + x - nn.delta)] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
+          }
+        }
+      } else {
+        uint32_t k = t + 1;
+        for (uint32_t i = lane; i < halo; i += 64) {
+          const uint64_t o = after + i;  // span offset of the halo byte
+          while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+          const TileDesc nt = tiles[k];
+          bb[rb(hi + i)] = gp(nt.abase)[nt.delta + (uint32_t)(o - nt.span_off)];
+        }
       }
     }
     bb[rb(img_end + lane)] = 0;  // zero pad (64 bytes) so 16-byte reads near the end are defined
@@ -643,7 +509,6 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
     s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
   }
   __syncthreads();
-
 }
 
 // ---------------------------------------------------------------------------------
@@ -696,35 +561,6 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
   return __shfl(cx, 63);
 }
 
-// Canonical exit of tile t: the speculative rule's chain from region c0 = (last region -
-// kZCanonLanes + 1) to the tile end (entries = previous lane's exit; lanes whose entry
-// changed re-merge).  It depends only on the tile's last ~2 KiB and not on where the
-// true chain enters the tile, so a block publishes it for its chunk's last tile before
-// decoding anything; the true chain meets it inside those 2 KiB unless the data never
-// re-synchronises, and then the exit check in count_tile aborts the batch.
-template <bool J>
-__device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s_img, uint32_t* s_bits, uint32_t lane,
-                                               const JL& jl) {
-  const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
-  const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
-  const bool on = lane >= c0 && z.rs < z.re;
-  const uint32_t ws = z.rs >= z.lo + kZWarm ? z.rs - kZWarm : z.lo;
-  uint32_t* bits = s_bits + lane * kZBitsPitch;
-  const Spec sp = on ? spec_walk<J>(s_img, ws, z.rs, z.re, z.end_a, bits, jl) : Spec{{0, 0}, z.rs, z.rs, 0};
-  uint32_t cx = sp.exit, entry = kZCanon;
-  for (int it = 0; it <= 64; ++it) {
-    const uint32_t prev = __shfl_up(cx, 1);
-    const uint32_t want = lane <= c0 ? kZCanon : prev;
-    const bool ch = want != entry;
-    if (!__any(ch)) break;
-    if (ch) {
-      entry = want;
-      cx = on ? canon_walk<J>(s_img, z.rs, z.re, z.end_a, want, sp, jl) : want;
-    }
-  }
-  return __shfl(cx, 63);
-}
-
 // Pass 1 for one tile, given its true entry e_true (aligned coordinate): spec walks,
 // true chain, exit checks, then the tile's record / wide-record counts and its
 // record-start bitmap (1 KiB) for the emit pass.  *x_true = the tile's exit.  must_exit:
@@ -732,11 +568,10 @@ __device__ __forceinline__ uint32_t canon_exit(const ZTile& z, const uint32_t* s
 template <bool J>
 __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
-                                           uint32_t* s_bits, const uint32_t lane, uint32_t* x_out, const JL& jl) {
+                                           const uint32_t lane, uint32_t* x_out, const JL& jl) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
-  (void)s_bits;
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
   // ---- speculative walk of the lane's region (with warm-up), starts in registers
   const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
@@ -944,6 +779,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   const TileDesc td = tiles[t];
+  const TileDesc n1 = tiles[t + 1 < ctl.n_tiles ? t + 1 : t];  // halo source, loaded beside td
   const SpanDesc sd = spans[td.span];
   const uint32_t lo = td.delta, hi = td.delta + td.len;
   const uint64_t ea = sd.len - td.span_off + td.delta;
@@ -951,7 +787,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
-  stage_image(td, sd, t, tiles, s_img, lane, hi);
+  stage_image(td, sd, t, tiles, s_img, lane, hi, &n1);
   JL jl{nullptr, nullptr, nullptr};
   if (J) jl = load_jl(ctl, t, s_j, lane);
   const uint32_t r0 = lane * kZRegion;
@@ -1101,7 +937,6 @@ template <bool J>
 __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
-  __shared__ uint32_t s_bits[64 * kZBitsPitch];  // speculative-start bitmaps, one row per lane
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
@@ -1126,6 +961,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
   uint64_t x_prev = 0;  // previous tile's exit, span offset
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
+    const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
     if (z.first || ctl.nodep) {
@@ -1149,10 +985,10 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     }
     const uint64_t ee = xs - z.td.span_off + z.lo;
     const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
-    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
     if (J) jl = load_jl(ctl, t, s_j, lane);
     uint32_t x_true;
-    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, s_bits, lane, &x_true, jl)) return;
+    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl)) return;
     x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
   }

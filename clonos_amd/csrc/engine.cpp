@@ -1069,12 +1069,16 @@ struct clg_engine {
   }
 
   // Speculative warm-up bytes before each lane's region (CLONOS_WARM overrides; tuning aid).
-  static uint32_t spec_warm() {
-    static const uint32_t w = [] {
+  // Measured on MI355X (tools/warm_sweep.sh): 96 B is best for short fixed-length records
+  // (config 2: count 0.213 ms at 96 B, 0.270 ms at 0 B); with Serializable tables the batch
+  // is dominated by wide records, whose warm-up steps diverge, and 16 B is best (config 3
+  // subset: 0.676 ms at 16 B, 0.773 ms at 96 B).
+  static uint32_t spec_warm(bool jser) {
+    static const int w = [] {
       const char* v = getenv("CLONOS_WARM");
-      return v ? uint32_t(atoi(v)) : 96u;
+      return v ? atoi(v) : -1;
     }();
-    return w;
+    return w >= 0 ? uint32_t(w) : (jser ? 16u : 96u);
   }
 
   // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
@@ -1137,7 +1141,7 @@ struct clg_engine {
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
-                      jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr, spec_warm()};
+                      jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr, spec_warm(jser)};
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
@@ -1285,7 +1289,7 @@ struct clg_engine {
     ctl.jwork_cap = uint32_t(nt) * 16 + 1024;
     ctl.jwork = jser ? d_zjwork.as<uint32_t>() : nullptr;
     ctl.ticket = reinterpret_cast<uint32_t*>(w + o_ab + 4);
-    ctl.warm = spec_warm();
+    ctl.warm = spec_warm(jser);
     // developer timing probe (CLONOS_ONE_PROBE bits: 1 no entry wait, 2 no look-back, 4 no
     // emit); output invalid
     static const uint32_t probe = [] {
