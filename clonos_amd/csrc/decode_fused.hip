@@ -444,13 +444,17 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
   const uint64_t rem = sd.len > after ? sd.len - after : 0;
   const uint32_t halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
   const uint32_t img_end = hi + halo;
-  const bool near = kHaloMax <= 64u && n1 && halo && t + 1 < t1 && n1->span_off == after && n1->len >= halo;
+  const bool next_ok = n1 && halo && t + 1 < t1 && n1->span_off == after && n1->len >= halo;
+  const bool near = kHaloMax <= 64u && next_ok;  // one byte per lane
+  const bool far = kHaloMax > 64u && next_ok;    // phase 3: up to 1 KiB, 16-byte words
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   uint32_t hb = 0;
+  u32x4 hv[2] = {};
+  static_assert(kHaloMax <= 64u * 16u * 2u - 32u, "halo words: two per lane");
   {
     // every lane issues its 8 loads (and its halo byte) before any LDS store (the tile is at
     // most 512 x 16 B)
     const uint32_t words = (hi + 15) >> 4;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
     constexpr int kLoads = (int)(kZTile / 16 / 64);
     u32x4 v[kLoads];
@@ -460,6 +464,12 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
       v[i] = src[w < words ? w : words - 1u];
     }
     if (near && lane < halo) hb = gp(n1->abase)[n1->delta + lane];
+    if (far) {
+      const uint32_t nw = (n1->delta + halo + 15u) >> 4;
+      const CLG_GLOBAL u32x4* src1 = gp(reinterpret_cast<const u32x4*>(n1->abase));
+      if (lane < nw) hv[0] = src1[lane];
+      if (lane + 64u < nw) hv[1] = src1[lane + 64u];
+    }
 #pragma unroll
     for (int i = 0; i < kLoads; ++i) {
       const uint32_t w = lane + 64u * (uint32_t)i;
@@ -477,6 +487,17 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
     uint8_t* bb = reinterpret_cast<uint8_t*>(s_img);
     if (near) {
       if (lane < halo) bb[rb(hi + lane)] = (uint8_t)hb;
+    } else if (far) {
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t c = lane + 64u * k;
+        const uint32_t w[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b) {
+          const uint32_t x = 16u * c + b;  // byte of the next tile's aligned coordinates
+          if (x >= n1->delta && x < n1->delta + halo) bb[rb(hi + x - n1->delta)] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
+        }
+      }
     } else {
       const TileDesc nn = halo ? tiles[t + 1] : td;
       if (kHaloMax > 64u && halo > 64u && nn.span_off == after && nn.len >= halo) {
@@ -1087,35 +1108,40 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
                                           const uint32_t lane, bool* flagged) {
   const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const ZTile z = ztile(tiles, spans, t, lane);
-  stage_image<kZJHalo, kZJRows>(z.td, z.sd, t, tiles, s_img, lane, z.hi);
+  const TileDesc n1 = tiles[t + 1 < ctl.n_tiles ? t + 1 : t];  // halo source, loaded beside t's
+  stage_image<kZJHalo, kZJRows>(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
   const uint64_t c1 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t after = z.td.span_off + z.td.len;
   const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
   const uint32_t img_end = z.hi + (rem < (uint64_t)kZJHalo ? (uint32_t)rem : kZJHalo);
   // candidates in the lane's region (row `lane` of the image, dwords 35 lane + j; j = 32..34
-  // are the row's pad = the next row's head): all 35 dwords loaded up front (independent
-  // LDS reads, no dependent round trips), then "03 AC ED 00 05" tested in registers where a
-  // dword pair holds an ED byte (rare outside the magic)
-  uint32_t D[kZRowDw + kZPad];
-#pragma unroll
-  for (uint32_t j = 0; j < kZRowDw + kZPad; ++j) D[j] = s_img[lane * kZPitch + j];
+  // are the row's pad = the next row's head): a slice's dwords are loaded together
+  // (independent LDS reads), then "03 AC ED 00 05" is tested in registers where a dword
+  // pair holds an ED byte (rare outside the magic)
   uint32_t nm = 0, cand[kZJReg];
   const uint32_t r0 = lane * kZRegion;
+  // the row in 4 slices of 8 dwords (+2 of lookahead): holding the whole row took the
+  // kernel to 220 VGPRs (2 waves per SIMD), a slice keeps it at 91
+  for (uint32_t j0 = 0; j0 < kZRowDw; j0 += 8) {
+    uint32_t D[10];
 #pragma unroll
-  for (uint32_t j = 0; j < kZRowDw; ++j) {
-    const uint32_t x = D[j], y = D[j + 1], z2 = D[j + 2];
-    const uint32_t ex_ = x ^ 0xEDEDEDEDu, ey = y ^ 0xEDEDEDEDu;
-    if (!(((ex_ - 0x01010101u) & ~ex_ & 0x80808080u) | ((ey - 0x01010101u) & ~ey & 0x80808080u))) continue;
+    for (uint32_t j = 0; j < 10; ++j) D[j] = s_img[lane * kZPitch + j0 + j];
 #pragma unroll
-    for (uint32_t sh = 0; sh < 4; ++sh) {
-      const uint32_t w0 = __builtin_amdgcn_alignbyte(y, x, sh);     // bytes a .. a+3 (LE)
-      const uint32_t w1 = __builtin_amdgcn_alignbyte(z2, y, sh);    // bytes a+4 .. a+7
-      const uint32_t a = r0 + 4u * j + sh;
-      if (w0 == 0x00EDAC03u && (w1 & 0xFFu) == 0x05u && a >= z.rs && a < z.re) {
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t x = D[j], y = D[j + 1], z2 = D[j + 2];
+      const uint32_t ex_ = x ^ 0xEDEDEDEDu, ey = y ^ 0xEDEDEDEDu;
+      if (!(((ex_ - 0x01010101u) & ~ex_ & 0x80808080u) | ((ey - 0x01010101u) & ~ey & 0x80808080u))) continue;
 #pragma unroll
-        for (int r = 0; r < kZJReg; ++r)
-          if ((uint32_t)r == nm) cand[r] = a;
-        ++nm;
+      for (uint32_t sh = 0; sh < 4; ++sh) {
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(y, x, sh);   // bytes a .. a+3 (LE)
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(z2, y, sh);  // bytes a+4 .. a+7
+        const uint32_t a = r0 + 4u * (j0 + j) + sh;
+        if (w0 == 0x00EDAC03u && (w1 & 0xFFu) == 0x05u && a >= z.rs && a < z.re) {
+#pragma unroll
+          for (int r = 0; r < kZJReg; ++r)
+            if ((uint32_t)r == nm) cand[r] = a;
+          ++nm;
+        }
       }
     }
   }
