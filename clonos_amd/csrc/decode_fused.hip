@@ -51,6 +51,9 @@ constexpr uint32_t kZPad = 3;
 constexpr uint32_t kZPitch = kZRowDw + kZPad;
 constexpr uint32_t kZRows = kZTile / kZRegion + 2;
 constexpr uint32_t kZImgDw = kZRows * kZPitch;
+#ifndef CLG_COUNT_LM
+#define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
+#endif
 #ifndef CLG_FUSED_PIPELINE
 #define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
 #endif
@@ -182,6 +185,7 @@ struct JL {
   const uint32_t* bits;
   const uint32_t* rank;
   const uint32_t* len;
+  const uint32_t* lm = nullptr;  // count pass: the tile's step-code map (below), else null
 };
 __device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
   const uint32_t w = j.bits[a >> 5], b = a & 31u;
@@ -309,9 +313,63 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
   return s;
 }
 
+// ---------------------------------------------------------------------------------
+// Step-code map (count pass with Serializable tables).  Batches that hold Serializable
+// records are dominated by wide records (config 3: 20 %), and a speculative walk that meets
+// one takes a divergent branch with two or three dependent LDS reads; with 64 lanes some lane
+// is in that branch at almost every step.  So before walking, the wave turns every byte of
+// the tile into a step code, data-parallel, in an LDS map with the image's row layout:
+//   0      no record the speculative walk follows (invalid, or longer than kZLmMax): step 1
+//   else   bits 0-6 the record length, bit 7 set for a wide record
+// Fixed-length tags come from a byte-permute table over four tags at a time; TimerTrigger
+// and SourceCheckpoint bytes (a few per region) get their length from their fields by the
+// decodeNext rules (zlen_var); Serializable records get theirs from the phase-3 table
+// (load_jl).  The speculative walk then costs one LDS read and no branch per step.  The true
+// chain (merge_walk_r) still reads the image, so every record it accepts is checked by the
+// full rules; the map only decides the speculative (and canonical) chains.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kZLmMax = 126;
+// codes of tags 0..7: Order 2, Timestamp 9, RNG 5, Serializable 0 (table), TimerTrigger and
+// SourceCheckpoint 0 (fields), IgnoreCheckpoint 13 (wide), BufferBuilt 5
+constexpr uint32_t kLmLo = 2u | 9u << 8 | 5u << 16;
+constexpr uint32_t kLmHi = (0x80u | 13u) << 16 | 5u << 24;
+constexpr uint32_t kLmCand = 0x80u | 0x80u << 8;  // tags 4, 5 (the high table word)
+
+__device__ __forceinline__ uint32_t lm8(const uint32_t* M, uint32_t a) { return ((lds_u8*)(M))[zoff(a)]; }
+__device__ __forceinline__ void lm8_set(uint32_t* M, uint32_t a, uint32_t c) { ((uint8_t*)(M))[zoff(a)] = (uint8_t)c; }
+__device__ __forceinline__ uint32_t lm_code(int L, bool wide) {
+  return (L > 0 && L <= (int)kZLmMax) ? (uint32_t)L | (wide ? 0x80u : 0u) : 0u;
+}
+
+// One speculative step over the map (bits as spec_step; skipped bytes' bits are never read).
+__device__ __forceinline__ uint32_t lm_step(const uint32_t* M, uint32_t q, uint64_t& sbw, uint64_t& wbw, uint32_t& bad) {
+  const uint32_t c = lm8(M, q);
+  const uint64_t m = 1ull << (q & 63u);
+  sbw |= m;
+  wbw |= m & (0ull - (uint64_t)(c >> 7));
+  bad = c ? bad : q + 1u;
+  const uint32_t L = c & 0x7Fu;
+  return q + (L > 1u ? L : 1u);
+}
+__device__ __forceinline__ SpecR lm_spec_walk(const uint32_t* M, uint32_t ws, uint32_t rs, uint32_t re, uint32_t r0) {
+  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
+  uint32_t q = ws;
+  while (q < rs) {
+    const uint32_t L = lm8(M, q) & 0x7Fu;
+    q += L > 1u ? L : 1u;
+  }
+  s.first = q;
+  const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
+  while (q < mid) q = lm_step(M, q, s.sb.lo, s.wb.lo, s.bad);
+  while (q < re) q = lm_step(M, q, s.sb.hi, s.wb.hi, s.bad);
+  s.exit = q;
+  return s;
+}
+
 template <bool J>
 __device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
                                                 uint32_t r0, const JL& jl) {
+  if (J && jl.lm) return lm_spec_walk(jl.lm, ws, rs, re, r0);
   // lanes whose records cannot run past the span end (all but the last tile's) skip the test
   return re + 16u <= end_a ? spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl)
                            : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
@@ -323,6 +381,17 @@ template <bool J>
 __device__ __forceinline__ uint32_t canon_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
                                                  const SpecR& s, const JL& jl) {
   if (e >= re) return e;
+  if (J && jl.lm) {
+    uint32_t p = e, q = s.first;
+    for (;;) {
+      if (p == q) return s.exit;
+      if (p >= re) return p;
+      const uint32_t x = p < q ? p : q;
+      const uint32_t L = lm8(jl.lm, x) & 0x7Fu;
+      const uint32_t nx = x + (L > 1u ? L : 1u);
+      if (p < q) p = nx; else q = nx;
+    }
+  }
   uint32_t p = e, q = s.first;
   for (;;) {
     if (p == q) return s.exit;
@@ -559,6 +628,140 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
   return z;
 }
 
+// Build the map in place over the tile's rows of the image (every lane of the wave calls it:
+// it holds a barrier).  The codes stay in registers until every lane has read the fields it
+// needs (a record's fields reach into the next row); TimerTrigger / SourceCheckpoint codes go
+// through `patch` (kZLmPatch per lane; a lane with more leaves the rest at 0, a deterministic
+// function of the tile like the rest of the map).  The span's end is applied last.
+constexpr uint32_t kZLmPatch = 8;
+__device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* patch, const uint32_t lane) {
+  const bool on = z.rs < z.re;
+  const uint32_t r0 = lane * kZRegion;
+  uint32_t c[kZRowDw];
+  // TimerTrigger / SourceCheckpoint bytes: word h, bit 32 s + 8 b + k <-> byte 64 h + 32 s + 4 k + b
+  uint64_t cw0 = 0, cw1 = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kZRowDw; ++j) {
+    const uint32_t x = T[lane * kZPitch + j];
+    // 0xFF in every byte holding a tag (< 8): bytes with none of bits 3-7 set
+    const uint32_t h = x & 0xF8F8F8F8u;
+    const uint32_t zz = (h - 0x01010101u) & ~h & 0x80808080u;
+    const uint32_t vm = __builtin_amdgcn_perm(zz << 8, zz, 0x090B080Au);  // sign of each byte
+    c[j] = __builtin_amdgcn_perm(kLmHi, kLmLo, x) & vm;
+    const uint64_t f = (uint64_t)((__builtin_amdgcn_perm(kLmCand, 0u, x) & vm) >> (7u - (j & 7u))) << (32u * ((j >> 3) & 1u));
+    if (j < 16u) cw0 |= f; else cw1 |= f;
+  }
+  uint32_t np = 0;
+  if (on) {  // TimerTrigger / SourceCheckpoint bytes: length from the fields (the rules of decodeNext)
+#pragma unroll 1
+    for (uint32_t hh = 0; hh < 2; ++hh) {
+      uint64_t m = hh ? cw1 : cw0;
+      while (m) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1u;
+        const uint32_t a = r0 + 64u * hh + 32u * (i >> 5) + 4u * (i & 7u) + ((i >> 3) & 3u);
+        if (a < z.rs || a >= z.re) continue;
+        const uint32_t code = lm_code(zlen_var(T, a, z.end_a, zb(T, a), 0u), true);
+        if (code && np < kZLmPatch) patch[lane * kZLmPatch + np++] = a | code << 16;
+      }
+    }
+  }
+  __syncthreads();  // every lane has read the image
+  if (on) {
+#pragma unroll
+    for (uint32_t j = 0; j < kZRowDw; ++j) T[lane * kZPitch + j] = c[j];
+    for (uint32_t k = 0; k < np; ++k) {
+      const uint32_t e = patch[lane * kZLmPatch + k];
+      lm8_set(T, e & 0xFFFFu, e >> 16);
+    }
+    // the span's end: a fixed-length record must end by end_a (the wide ones were checked)
+    if (z.end_a < r0 + kZRegion + 13u) {
+      for (uint32_t a = z.end_a > r0 + 13u ? z.end_a - 13u : r0; a < r0 + kZRegion; ++a) {
+        const uint32_t cc = lm8(T, a);
+        if (a + (cc & 0x7Fu) > z.end_a) lm8_set(T, a, 0u);
+      }
+    }
+  }
+}
+
+// Span bytes from HBM by aligned coordinate (the map's true walk, for a code of 0: an
+// invalid record, or one the map does not hold).
+struct GSpan {
+  const TileDesc* tiles;
+  uint32_t t, t1, lo;
+  uint64_t so;  // span offset of aligned coordinate lo
+  __device__ uint32_t at(uint32_t a) const {
+    const uint64_t o = so + (a - lo);
+    uint32_t k = t;
+    while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+    const TileDesc d = tiles[k];
+    return gp(d.abase)[d.delta + (uint32_t)(o - d.span_off)];
+  }
+};
+struct GRec {
+  const GSpan* g;
+  uint32_t base;
+  __device__ int operator()(uint64_t k) const { return (int)g->at(base + (uint32_t)k); }
+};
+__device__ __forceinline__ uint32_t fld_be32(const GRec& b, uint32_t k) {
+  return (uint32_t)b(k) << 24 | (uint32_t)b(k + 1) << 16 | (uint32_t)b(k + 2) << 8 | (uint32_t)b(k + 3);
+}
+// True length of the record at p by the full rules (-1: decodeNext rejects it); *wide.
+__device__ __forceinline__ int lm_true_slow(const GSpan& g, uint32_t p, uint32_t end_a, const JL& jl, uint32_t* wide) {
+  const uint32_t tg = g.at(p);
+  *wide = is_wide((int)tg);
+  if (tg == CLG_TAG_SERIALIZABLE) {
+    const uint32_t v = jl_len(jl, p);
+    return v ? (int)v : -1;
+  }
+  const int64_t L = len_fields(GRec{&g, p}, (int)tg, (uint64_t)(end_a - p));
+  return (L > 0 && L <= 0x7FFFFFF0ll) ? (int)L : -1;
+}
+
+// merge_walk_r over the map: the true chain takes a code's length (the full rules made it)
+// and asks HBM only where the code is 0.
+__device__ __forceinline__ Res merge_walk_lm(const uint32_t* M, uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s,
+                                             const JL& jl, const GSpan& g) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  if (e >= re) return r;
+  uint32_t p = e;
+  Bits pb{0, 0}, pw{0, 0};
+  for (;; ++r.steps) {
+    if (p >= re) break;
+    const uint32_t i = p & 127u;
+    const uint64_t word = i < 64u ? s.sb.lo : s.sb.hi;
+    if (((word >> (i & 63u)) & 1ull) && p >= s.bad) {
+      r.bm = bor(pb, bge(s.sb, i));
+      r.wb = bor(pw, bge(s.wb, i));
+      r.exit = s.exit;
+      return r;
+    }
+    const uint32_t cc = lm8(M, p);
+    uint32_t L = cc & 0x7Fu, w = cc >> 7;
+    if (!cc) {
+      const int v = lm_true_slow(g, p, end_a, jl, &w);
+      if (v <= 0) {
+        r.bad = 1;
+        r.exit = s.exit;
+        return r;
+      }
+      L = (uint32_t)v;
+    }
+    if (p + L > end_a || p + L < p) {
+      r.bad = 1;
+      r.exit = s.exit;
+      return r;
+    }
+    bset(pb, i);
+    if (w) bset(pw, i);
+    p += L;
+  }
+  r.bm = pb;
+  r.wb = pw;
+  r.exit = p;
+  return r;
+}
+
 // Canonical exit of the tile from the lanes' speculative walks: lanes >= c0 (the last
 // kZCanonLanes regions) chain their speculative exits, lane c0 starting from its own
 // speculative chain; lanes whose entry changed merge again.
@@ -589,7 +792,8 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
 template <bool J>
 __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
-                                           const uint32_t lane, uint32_t* x_out, const JL& jl) {
+                                           const uint32_t lane, uint32_t* x_out, const JL& jl,
+                                           const TileDesc* __restrict__ tiles = nullptr) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
@@ -605,7 +809,13 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   // is consistent (each pass fixes at least the lowest changed lane)
   const uint32_t guess = __shfl_up(sp.exit, 1);
   uint32_t entry = lane == 0 ? e_true : guess;
-  Res r = rs < re ? merge_walk_r<J>(s_img, re, end_a, entry, sp, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
+  const GSpan g{tiles, t, z.sd.first_tile + z.sd.n_tiles, lo, z.td.span_off};
+  auto merge = [&](uint32_t from) -> Res {
+    if (rs >= re) return Res{{0, 0}, {0, 0}, from, 0, 0};
+    if (J && jl.lm) return merge_walk_lm(s_img, re, end_a, from, sp, jl, g);
+    return merge_walk_r<J>(s_img, re, end_a, from, sp, jl);
+  };
+  Res r = merge(entry);
   uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
@@ -615,7 +825,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     ++iters;
     if (ch) {
       entry = want;
-      r = rs < re ? merge_walk_r<J>(s_img, re, end_a, want, sp, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
+      r = merge(want);
       steps_more += r.steps;
     }
   }
@@ -747,7 +957,9 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
 // contiguous run.
 // ---------------------------------------------------------------------------------
 // Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
-__device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane) {
+// lm: the count pass's step-code map (built, barrier passed): Serializable codes go into it.
+__device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane,
+                                     uint32_t* lm = nullptr) {
   uint32_t* bits = s_j;
   uint32_t* rank = s_j + kZJBitsDw;
   uint32_t* len = s_j + 2 * kZJBitsDw;
@@ -756,8 +968,10 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
   const uint32_t n = min(gp(ctl.jn)[t], kZJCap);
   for (uint32_t i = lane; i < n; i += 64) {
     const uint32_t a = gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
-    len[i] = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    const uint32_t L = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    len[i] = L;
     atomicOr(&bits[a >> 5], 1u << (a & 31u));
+    if (lm) lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
   }
   __syncthreads();
   // ranks: lane l takes dwords [5 l, 5 l + 5) (64 x 5 >= 260)
@@ -782,7 +996,7 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
     run += c[k];
   }
   __syncthreads();
-  return JL{bits, rank, len};
+  return JL{bits, rank, len, lm};
 }
 
 template <bool J>
@@ -959,6 +1173,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
+  constexpr bool kLm = CLG_COUNT_LM != 0;  // J: the image becomes the step-code map (build_lm)
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
@@ -970,7 +1185,8 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
-      if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
+      if (J && kLm) build_lm(z, s_img, s_j, lane);
+      if (J) jl = load_jl(ctl, t1 - 1, s_j, lane, kLm ? s_img : nullptr);
       const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
       const SpecR sp = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
                                    : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
@@ -1007,9 +1223,10 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     const uint64_t ee = xs - z.td.span_off + z.lo;
     const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
     stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
-    if (J) jl = load_jl(ctl, t, s_j, lane);
+    if (J && kLm) build_lm(z, s_img, s_j, lane);  // load_jl's first barrier orders it before the table's codes
+    if (J) jl = load_jl(ctl, t, s_j, lane, kLm ? s_img : nullptr);
     uint32_t x_true;
-    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl)) return;
+    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles)) return;
     x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
   }
