@@ -956,19 +956,31 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
 // contiguous run.
 // ---------------------------------------------------------------------------------
+// Tile t's entry count and the first 64 entries of its table (one per lane), loaded before
+// the tile is staged so that their latency overlaps the staging's (config 3 holds ~50
+// entries per tile; load_jl loads any past 64 itself).
+struct JLPre {
+  uint32_t n, a, L;
+};
+__device__ __forceinline__ JLPre jl_prefetch(const FusedCtl& ctl, uint32_t t, uint32_t lane) {
+  const uint64_t b = (uint64_t)t * kZJCap + lane;  // inside the table even past its entries
+  return JLPre{gp(ctl.jn)[t], gp(ctl.jpos)[b], gp(ctl.jlen)[b]};
+}
+
 // Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
 // lm: the count pass's step-code map (built, barrier passed): Serializable codes go into it.
 __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane,
-                                     uint32_t* lm = nullptr) {
+                                     uint32_t* lm = nullptr, const JLPre* pre = nullptr) {
   uint32_t* bits = s_j;
   uint32_t* rank = s_j + kZJBitsDw;
   uint32_t* len = s_j + 2 * kZJBitsDw;
   for (uint32_t i = lane; i < kZJBitsDw; i += 64) bits[i] = 0;
   __syncthreads();
-  const uint32_t n = min(gp(ctl.jn)[t], kZJCap);
+  const uint32_t n = min(pre ? pre->n : gp(ctl.jn)[t], kZJCap);
   for (uint32_t i = lane; i < n; i += 64) {
-    const uint32_t a = gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
-    const uint32_t L = gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    const bool p0 = pre && i == lane;
+    const uint32_t a = p0 ? pre->a : gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
+    const uint32_t L = p0 ? pre->L : gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
     len[i] = L;
     atomicOr(&bits[a >> 5], 1u << (a & 31u));
     if (lm) lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
@@ -1022,9 +1034,11 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
+  JLPre pre{};
+  if (J) pre = jl_prefetch(ctl, t, lane);
   stage_image(td, sd, t, tiles, s_img, lane, hi, &n1);
   JL jl{nullptr, nullptr, nullptr};
-  if (J) jl = load_jl(ctl, t, s_j, lane);
+  if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
   const uint32_t r0 = lane * kZRegion;
   const uint32_t cnt = (uint32_t)(__popcll(bits.x) + __popcll(bits.y));
   uint32_t incl = cnt;
@@ -1222,9 +1236,11 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     }
     const uint64_t ee = xs - z.td.span_off + z.lo;
     const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+    JLPre pre{};
+    if (J) pre = jl_prefetch(ctl, t, lane);
     stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
     if (J && kLm) build_lm(z, s_img, s_j, lane);  // load_jl's first barrier orders it before the table's codes
-    if (J) jl = load_jl(ctl, t, s_j, lane, kLm ? s_img : nullptr);
+    if (J) jl = load_jl(ctl, t, s_j, lane, kLm ? s_img : nullptr, &pre);
     uint32_t x_true;
     if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles)) return;
     x_prev = z.td.span_off + (x_true - z.lo);

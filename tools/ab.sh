@@ -18,5 +18,6 @@ for v in sys.argv[1:]:
           "step", [b["ms_per_step"] for b in c2],
           "| c3 count", [round(b["kernels"]["decode_count"]["avg_ms"], 3) for b in c3],
           "emit", [round(b["kernels"]["decode_emit"]["avg_ms"], 3) for b in c3],
-          "jser", [round(b["kernels"]["decode_jser"]["avg_ms"], 3) for b in c3])
+          "jser", [round(b["kernels"].get("decode_jser", {"avg_ms": 0})["avg_ms"], 3) for b in c3],
+          "step", [round(b["ms_per_step"], 3) for b in c3], "fallback", [b["kernels"].get("decode_fallback", {}).get("launches", 0) for b in c3])
 PY
