@@ -247,7 +247,7 @@ __device__ __forceinline__ uint32_t spec_len_fast(const uint32_t* T, uint32_t q,
   const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
   uint32_t L = c;
   *wide = false;
-  if (c & 0x40u) {  // rare: the length needs fields of the record
+  if (c >= 0x40u) {  // rare: the length needs fields of the record
     *wide = true;
     if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
       L = 13;
@@ -264,17 +264,18 @@ __device__ __forceinline__ uint32_t spec_len_fast(const uint32_t* T, uint32_t q,
 
 // One speculative step in the region: the start bit of a followed record goes into sbw and,
 // for a wide record, into wbw -- inside the rare branch, so the common path (fixed-length
-// tags) pays nothing for the wide bitmap.  SAFE: the record's bytes cannot pass end_a.
+// tags) pays nothing for the wide bitmap.  SAFE: the record's bytes cannot pass end_a.  A
+// skipped byte's bit is set too; the skips are found from the bitmap afterwards (spec_bad).
 template <bool J, bool SAFE>
 __device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uint32_t end_a, const JL& jl,
-                                              uint64_t& sbw, uint64_t& wbw, uint32_t& bad) {
+                                              uint64_t& sbw, uint64_t& wbw) {
   constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16 | (J ? 0x40u : 0u) << 24;  // tags 0..3
   constexpr uint32_t kHi = 0x40u | 0x40u << 8 | 0x40u << 16 | 5u << 24;       // tags 4..7
   const uint32_t tg = zb8(T, q);
   const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
   uint32_t L = c;
   const uint64_t m = 1ull << (q & 63u);
-  if (c & 0x40u) {  // rare: the length needs fields of the record
+  if (c >= 0x40u) {  // rare: the length needs fields of the record
     if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
       L = 13;
     } else if (J && tg == CLG_TAG_SERIALIZABLE) {
@@ -288,11 +289,21 @@ __device__ __forceinline__ uint32_t spec_step(const uint32_t* T, uint32_t q, uin
   } else if (!SAFE) {
     L = q + L <= end_a ? L : 0u;
   }
-  // a skipped byte's bit is set too: every skip lies below `bad`, and the merge walk only
-  // uses starts at or past `bad`, so such bits are never read
   sbw |= m;
-  bad = L ? bad : q + 1u;
   return q + (L > 1u ? L : 1u);
+}
+
+// 1 + the last position a speculative walk skipped in its region (0: none), from its start
+// bitmap: every record is at least 2 bytes, so a start followed by a start one byte later
+// was a skip, and so was the region's last start if the exit lies one byte past it.  (The
+// merge walk uses only starts at or past it; the skipped bytes' own bits are never read.)
+__device__ __forceinline__ uint32_t spec_bad(const SpecR& s, uint32_t r0) {
+  const uint64_t klo = s.sb.lo & ((s.sb.lo >> 1) | (s.sb.hi << 63));
+  const uint64_t khi = s.sb.hi & (s.sb.hi >> 1);
+  uint32_t bad = khi ? r0 + 128u - (uint32_t)__clzll(khi) : (klo ? r0 + 64u - (uint32_t)__clzll(klo) : 0u);
+  const uint32_t last1 = s.sb.hi ? r0 + 128u - (uint32_t)__clzll(s.sb.hi)
+                                 : (s.sb.lo ? r0 + 64u - (uint32_t)__clzll(s.sb.lo) : 0u);  // 1 + last start
+  return (last1 && s.exit == last1) ? last1 : bad;
 }
 
 template <bool J, bool SAFE>
@@ -307,9 +318,10 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
-  while (q < mid) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.lo, s.wb.lo, s.bad);
-  while (q < re) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.hi, s.wb.hi, s.bad);
+  while (q < mid) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.lo, s.wb.lo);
+  while (q < re) q = spec_step<J, SAFE>(T, q, end_a, jl, s.sb.hi, s.wb.hi);
   s.exit = q;
+  s.bad = spec_bad(s, r0);
   return s;
 }
 
@@ -341,13 +353,12 @@ __device__ __forceinline__ uint32_t lm_code(int L, bool wide) {
   return (L > 0 && L <= (int)kZLmMax) ? (uint32_t)L | (wide ? 0x80u : 0u) : 0u;
 }
 
-// One speculative step over the map (bits as spec_step; skipped bytes' bits are never read).
-__device__ __forceinline__ uint32_t lm_step(const uint32_t* M, uint32_t q, uint64_t& sbw, uint64_t& wbw, uint32_t& bad) {
+// One speculative step over the map (bits as spec_step; skips found by spec_bad).
+__device__ __forceinline__ uint32_t lm_step(const uint32_t* M, uint32_t q, uint64_t& sbw, uint64_t& wbw) {
   const uint32_t c = lm8(M, q);
   const uint64_t m = 1ull << (q & 63u);
   sbw |= m;
   wbw |= m & (0ull - (uint64_t)(c >> 7));
-  bad = c ? bad : q + 1u;
   const uint32_t L = c & 0x7Fu;
   return q + (L > 1u ? L : 1u);
 }
@@ -360,9 +371,10 @@ __device__ __forceinline__ SpecR lm_spec_walk(const uint32_t* M, uint32_t ws, ui
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
-  while (q < mid) q = lm_step(M, q, s.sb.lo, s.wb.lo, s.bad);
-  while (q < re) q = lm_step(M, q, s.sb.hi, s.wb.hi, s.bad);
+  while (q < mid) q = lm_step(M, q, s.sb.lo, s.wb.lo);
+  while (q < re) q = lm_step(M, q, s.sb.hi, s.wb.hi);
   s.exit = q;
+  s.bad = spec_bad(s, r0);
   return s;
 }
 
