@@ -417,29 +417,65 @@ __device__ __forceinline__ uint32_t canon_walk_r(const uint32_t* T, uint32_t re,
 }
 
 // True chain from entry e (e >= rs) merged with the speculative chain: walk until the true
-// chain lands on a speculative start past the speculative chain's last skip.
+// chain lands on a speculative start past the speculative chain's last skip.  The walk runs
+// over the region's two 64-bit bitmap halves in turn (as spec_walk_t), so a start costs one
+// 64-bit shift and OR; `step(p, &L, &wide)` is the true length rule (false: decodeNext
+// rejects the record, *why set).
+template <class Step>
+__device__ __forceinline__ Res merge_walk_h(uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s, Step&& step) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  if (e >= re) return r;
+  const uint32_t r0 = (re - 1u) & ~(kZRegion - 1u);
+  uint32_t p = e, why = 0;
+  Bits pb{0, 0}, pw{0, 0};
+  // 0: reached lim, 1: met the speculative chain, 2: an invalid record
+  auto run = [&](uint64_t sbw, uint64_t& pbw, uint64_t& pww, uint32_t lim) -> uint32_t {
+    for (; p < lim; ++r.steps) {
+      const uint32_t b = p & 63u;
+      if (((sbw >> b) & 1ull) && p >= s.bad) return 1u;
+      uint32_t L;
+      bool w;
+      if (!step(p, &L, &w, &why)) return 2u;
+      if (p + L > end_a || p + L < p) {
+        why = 1;
+        return 2u;
+      }
+      const uint64_t m = 1ull << b;
+      pbw |= m;
+      if (w) pww |= m;
+      p += L;
+    }
+    return 0u;
+  };
+  const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
+  uint32_t st = run(s.sb.lo, pb.lo, pw.lo, mid);
+  if (st == 0u) st = run(s.sb.hi, pb.hi, pw.hi, re);
+  if (st == 1u) {
+    const uint32_t i = p & 127u;
+    r.bm = bor(pb, bge(s.sb, i));
+    r.wb = bor(pw, bge(s.wb, i));
+    r.exit = s.exit;
+  } else if (st == 2u) {
+    r.bad = why;
+    r.exit = s.exit;
+  } else {
+    r.bm = pb;
+    r.wb = pw;
+    r.exit = p;
+  }
+  return r;
+}
+
 template <bool J>
 __device__ __forceinline__ Res merge_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s,
                                             const JL& jl) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0};
-  if (e >= re) return r;
-  uint32_t p = e;
-  Bits pb{0, 0}, pw{0, 0};
-  for (;; ++r.steps) {
-    if (p >= re) break;
-    const uint32_t i = p & 127u;
-    const uint64_t word = i < 64u ? s.sb.lo : s.sb.hi;
-    if (((word >> (i & 63u)) & 1ull) && p >= s.bad) {
-      r.bm = bor(pb, bge(s.sb, i));
-      r.wb = bor(pw, bge(s.wb, i));
-      r.exit = s.exit;
-      return r;
-    }
+  return merge_walk_h(re, end_a, e, s, [&](uint32_t p, uint32_t* Lp, bool* w, uint32_t* why) -> bool {
     const uint32_t tg = zb8(T, p);
     uint32_t L = __builtin_amdgcn_ubfe(kZLutTrue, tg << 2, 4);
+    *w = false;
     if (L == 15u || tg >= 8u) {
       int v;
-      uint32_t why = 1u;
+      uint32_t y = 1u;
       if (tg >= 8u) {
         v = (int)kLenErr;
       } else if (tg == CLG_TAG_SERIALIZABLE) {
@@ -448,31 +484,21 @@ __device__ __forceinline__ Res merge_walk_r(const uint32_t* T, uint32_t re, uint
           v = jv ? (int)jv : (int)kLenErr;
         } else {
           v = (int)kLenErr;
-          why = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
+          y = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
         }
       } else {
         v = tg == CLG_TAG_IGNORE_CHECKPOINT ? 13 : zlen_var(T, p, end_a, tg, 0);
       }
       if (v <= 0) {
-        r.bad = why;
-        r.exit = s.exit;
-        return r;
+        *why = y;
+        return false;
       }
       L = (uint32_t)v;
-      bset(pw, i);
+      *w = true;
     }
-    if (p + L > end_a || p + L < p) {
-      r.bad = 1;
-      r.exit = s.exit;
-      return r;
-    }
-    bset(pb, i);
-    p += L;
-  }
-  r.bm = pb;
-  r.wb = pw;
-  r.exit = p;
-  return r;
+    *Lp = L;
+    return true;
+  });
 }
 
 // ---------------------------------------------------------------------------------
@@ -734,44 +760,21 @@ __device__ __forceinline__ int lm_true_slow(const GSpan& g, uint32_t p, uint32_t
 // and asks HBM only where the code is 0.
 __device__ __forceinline__ Res merge_walk_lm(const uint32_t* M, uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s,
                                              const JL& jl, const GSpan& g) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0};
-  if (e >= re) return r;
-  uint32_t p = e;
-  Bits pb{0, 0}, pw{0, 0};
-  for (;; ++r.steps) {
-    if (p >= re) break;
-    const uint32_t i = p & 127u;
-    const uint64_t word = i < 64u ? s.sb.lo : s.sb.hi;
-    if (((word >> (i & 63u)) & 1ull) && p >= s.bad) {
-      r.bm = bor(pb, bge(s.sb, i));
-      r.wb = bor(pw, bge(s.wb, i));
-      r.exit = s.exit;
-      return r;
-    }
+  return merge_walk_h(re, end_a, e, s, [&](uint32_t p, uint32_t* Lp, bool* w, uint32_t* why) -> bool {
     const uint32_t cc = lm8(M, p);
-    uint32_t L = cc & 0x7Fu, w = cc >> 7;
+    uint32_t L = cc & 0x7Fu, wu = cc >> 7;
     if (!cc) {
-      const int v = lm_true_slow(g, p, end_a, jl, &w);
+      const int v = lm_true_slow(g, p, end_a, jl, &wu);
       if (v <= 0) {
-        r.bad = 1;
-        r.exit = s.exit;
-        return r;
+        *why = 1;
+        return false;
       }
       L = (uint32_t)v;
     }
-    if (p + L > end_a || p + L < p) {
-      r.bad = 1;
-      r.exit = s.exit;
-      return r;
-    }
-    bset(pb, i);
-    if (w) bset(pw, i);
-    p += L;
-  }
-  r.bm = pb;
-  r.wb = pw;
-  r.exit = p;
-  return r;
+    *Lp = L;
+    *w = wu != 0;
+    return true;
+  });
 }
 
 // Canonical exit of the tile from the lanes' speculative walks: lanes >= c0 (the last
