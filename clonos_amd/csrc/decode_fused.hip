@@ -808,15 +808,18 @@ template <bool J>
 __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
                                            const uint32_t lane, uint32_t* x_out, const JL& jl,
-                                           const TileDesc* __restrict__ tiles = nullptr) {
+                                           const TileDesc* __restrict__ tiles = nullptr,
+                                           const SpecR* walked = nullptr) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
-  // ---- speculative walk of the lane's region (with warm-up), starts in registers
+  // ---- speculative walk of the lane's region (with warm-up), starts in registers (walked:
+  // the chunk prologue's walk of this same tile, a function of the tile's bytes only)
   const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
-  const SpecR sp = rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
-                           : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
+  const SpecR sp = walked ? *walked
+                          : rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
+                                    : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
 
   ZPHASE(2);
   // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
@@ -1210,6 +1213,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
   if (t0 >= t1) return;
   // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
   uint32_t x_pub = kZCanon;
+  SpecR sp_last{{0, 0}, {0, 0}, 0, 0, 0};  // its speculative walk, reused when the loop reaches it
   {
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
@@ -1217,9 +1221,9 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
       if (J && kLm) build_lm(z, s_img, s_j, lane);
       if (J) jl = load_jl(ctl, t1 - 1, s_j, lane, kLm ? s_img : nullptr);
       const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
-      const SpecR sp = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
-                                   : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
-      x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl);
+      sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
+                            : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+      x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
@@ -1257,7 +1261,10 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     if (J && kLm) build_lm(z, s_img, s_j, lane);  // load_jl's first barrier orders it before the table's codes
     if (J) jl = load_jl(ctl, t, s_j, lane, kLm ? s_img : nullptr, &pre);
     uint32_t x_true;
-    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles)) return;
+    const bool reuse = t + 1 == t1 && x_pub != kZCanon;
+    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles,
+                       reuse ? &sp_last : nullptr))
+      return;
     x_prev = z.td.span_off + (x_true - z.lo);
     __syncthreads();  // the image is reused by the next tile
   }
