@@ -152,6 +152,31 @@ def test_fused_serializable_long_streams(feng):
     assert_span_equal(dec, 0, buf)
 
 
+def test_fused_tables_long_wide_records(feng):
+    """With Serializable tables the count pass walks a step-code map whose codes hold
+    lengths up to 126 bytes: longer TimerTrigger names, SourceCheckpoint references and
+    Serializable streams get code 0, and the true walk measures them from HBM (TimerTrigger /
+    SourceCheckpoint by the decodeNext rules, Serializable from the table).  Bit-exact
+    against the oracle, on the batch that builds the tables and on the next one."""
+    rng = np.random.default_rng(21)
+    for _ in range(2):
+        parts = []
+        for i in range(400):
+            parts.append(synth.config3_epoch(int(rng.integers(5, 60)), rng)[0].tobytes())
+            k = i % 4
+            n = int(rng.integers(100, 320))
+            if k == 0:
+                parts.append(D.encode(D.TimerTriggerDeterminant(i, 7 * i, D.INTERNAL, b"A" * n)))
+            elif k == 1:
+                parts.append(D.encode(D.SourceCheckpointDeterminant(i, i, 3 * i, D.CHECKPOINT, b"r" * n)))
+            elif k == 2:
+                parts.append(D.encode(D.SerializableDeterminant(D.jser_string("s" * n))))
+        buf = b"".join(parts)
+        dec = feng.decode_host(buf)
+        assert_span_equal(dec, 0, buf)
+    assert "decode_jser" in feng.kernel_stats()
+
+
 @pytest.mark.parametrize("bad", ["magic_no_object", "truncated_stream", "bad_magic"])
 def test_fused_serializable_errors(feng, bad):
     """Invalid Serializable records after valid ones: same status / offset / tag as the
