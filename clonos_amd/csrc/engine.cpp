@@ -1069,16 +1069,16 @@ struct clg_engine {
   }
 
   // Speculative warm-up bytes before each lane's region (CLONOS_WARM overrides; tuning aid).
-  // Measured on MI355X (tools/warm_sweep.sh): 96 B is best for short fixed-length records
-  // (config 2: count 0.213 ms at 96 B, 0.270 ms at 0 B); with Serializable tables the batch
-  // is dominated by wide records, whose warm-up steps diverge, and 16 B is best (config 3
-  // subset: 0.676 ms at 16 B, 0.773 ms at 96 B).
-  static uint32_t spec_warm(bool jser) {
+  // Measured on MI355X (tools/r3_warm.sh): 96 B is best for short fixed-length records
+  // (config 2: count 0.176 ms at 96 B, 0.194 at 64, 0.182 at 128).  With Serializable
+  // tables the count pass walks the step-code map, whose steps no longer diverge on wide
+  // records, and 48-128 B are best too (config-3 subset: 0.43-0.44 ms, 0.451 at 16 B).
+  static uint32_t spec_warm(bool /*jser*/) {
     static const int w = [] {
       const char* v = getenv("CLONOS_WARM");
       return v ? atoi(v) : -1;
     }();
-    return w >= 0 ? uint32_t(w) : (jser ? 16u : 96u);
+    return w >= 0 ? uint32_t(w) : 96u;
   }
 
   // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
