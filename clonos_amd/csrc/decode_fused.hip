@@ -1170,21 +1170,38 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
       if (k < nwide) {
         const uint32_t e = s_pos[k], a = e & 0xFFFFu, i = e >> 16;
         const uint64_t g = rec0 + w0 + i;
-        const uint32_t tg = zb(s_img, a);
-        uint32_t tgu;
-        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
-        Rec rr{};
-        decode_fields(ZBytes{s_img, a}, (int)tg, (int64_t)L, rr);
-        if (fits || g < out.cap) o_v0[w0 + i] = rr.v0;
+        // Branch-free over the four wide tags (the count pass validated every record, so
+        // the lengths need no checks): the record's bytes a .. a+31 as eight little-endian
+        // dwords x[j] = bytes a+4j .. a+4j+3 from nine LDS reads, every field taken from
+        // them, the values selected by tag -- decode_fields' rules (dev_common.h;
+        // SimpleDeterminantEncoder.java:202-341).
+        const uint32_t k0 = a >> 2, sh = 8u * (a & 3u);
+        uint32_t d[9], x[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 9; ++j) d[j] = s_img[rk(k0 + j)];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) x[j] = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
+        auto be32 = [&](uint32_t off) {  // bytes a+off .. a+off+3, big-endian (off constant)
+          return __builtin_bswap32(__builtin_amdgcn_alignbyte(x[(off >> 2) + 1], x[off >> 2], off & 3u));
+        };
+        const uint32_t tg = x[0] & 0xFFu;
+        const bool ser = tg == CLG_TAG_SERIALIZABLE, tt = tg == CLG_TAG_TIMER_TRIGGER, sc = tg == CLG_TAG_SOURCE_CHECKPOINT;
+        const uint32_t b13 = (x[3] >> 8) & 0xFFu, b21 = (x[5] >> 8) & 0xFFu, b22 = (x[5] >> 16) & 0xFFu;
+        const bool tt_name = tt && b13 == 6u, sc_ref = sc && b22 != 0u;
+        const uint32_t jlen = ser ? jl_len(jl, a) : 0u;
+        const uint32_t L = ser ? jlen : tt_name ? 18u + be32(14) : tt ? 14u : sc_ref ? 27u + be32(23) : sc ? 23u : 13u;
+        const uint32_t var_off = ser ? 1u : tt_name ? 18u : sc_ref ? 27u : 0u;
+        const int64_t v0 = ser ? (int64_t)L - 1 : (int64_t)((uint64_t)be32(5) << 32 | be32(9));
+        if (fits || g < out.cap) o_v0[w0 + i] = v0;
         const uint64_t wi = wide + k;
         if (wi < out.wcap) {
           const uint32_t so = (uint32_t)(td.span_off + (a - lo));
           gp(out.w_idx)[wi] = (uint32_t)g;
-          gp(out.w_rc)[wi] = rr.rc;
-          gp(out.w_v1)[wi] = rr.v1;
-          gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
-          gp(out.w_var_len)[wi] = rr.var_len;
-          gp(out.w_sub)[wi] = rr.sub;
+          gp(out.w_rc)[wi] = ser ? 0 : (int32_t)be32(1);
+          gp(out.w_v1)[wi] = sc ? (int64_t)((uint64_t)be32(13) << 32 | be32(17)) : 0;
+          gp(out.w_var_off)[wi] = var_off ? so + var_off : 0u;
+          gp(out.w_var_len)[wi] = var_off ? L - var_off : 0u;
+          gp(out.w_sub)[wi] = (uint8_t)(tt ? b13 : sc ? (b21 | (sc_ref ? 0x80u : 0u)) : 0u);
         }
       }
     }
