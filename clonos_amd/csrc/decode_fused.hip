@@ -594,6 +594,30 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
     uint8_t* bb = reinterpret_cast<uint8_t*>(s_img);
     if (near) {
       if (lane < halo) bb[rb(hi + lane)] = (uint8_t)hb;
+    } else if (far && ((hi - n1->delta) & 15u) == 0u) {
+      // the usual case: tiles split at 8 KiB inside a segment or at a segment's end, so the
+      // next tile starts at this one's end in the same 16-byte alignment and its words land
+      // on 16-byte image boundaries whole (bytes past the halo fall under the zero pad or
+      // past the image's end; only the first word's bytes before the next tile are skipped)
+      const uint32_t nw = (n1->delta + halo + 15u) >> 4;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t c = lane + 64u * k;
+        if (c >= nw) continue;
+        const uint32_t at = hi - n1->delta + 16u * c;  // image position of the word's byte 0
+        if (16u * c >= n1->delta) {
+          uint32_t* d = s_img + rk(at >> 2);
+          d[0] = hv[k].x;
+          d[1] = hv[k].y;
+          d[2] = hv[k].z;
+          d[3] = hv[k].w;
+        } else {
+          const uint32_t w[4] = {hv[k].x, hv[k].y, hv[k].z, hv[k].w};
+#pragma unroll
+          for (uint32_t b = 0; b < 16; ++b)
+            if (16u * c + b >= n1->delta) bb[rb(at + b)] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
+        }
+      }
     } else if (far) {
 #pragma unroll
       for (uint32_t k = 0; k < 2; ++k) {
