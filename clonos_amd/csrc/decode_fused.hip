@@ -1411,33 +1411,40 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
   const uint32_t img_end = z.hi + (rem < (uint64_t)kZJHalo ? (uint32_t)rem : kZJHalo);
   // candidates in the lane's region (row `lane` of the image, dwords 35 lane + j; j = 32..34
-  // are the row's pad = the next row's head): a slice's dwords are loaded together
-  // (independent LDS reads), then "03 AC ED 00 05" is tested in registers where a dword
-  // pair holds an ED byte (rare outside the magic)
+  // are the row's pad = the next row's head).  First a mask of the row's dwords holding an
+  // ED byte (rare outside the magic), branch-free; then only the dwords where a magic could
+  // start (its ED byte, at +2, lies in that dword or the next) are tested at their four
+  // byte offsets for "03 AC ED 00 05" -- a loop over a few set bits per lane, where testing
+  // every dword under a per-dword branch ran the test for nearly every dword of the wave
   uint32_t nm = 0, cand[kZJReg];
   const uint32_t r0 = lane * kZRegion;
-  // the row in 4 slices of 8 dwords (+2 of lookahead): holding the whole row took the
-  // kernel to 220 VGPRs (2 waves per SIMD), a slice keeps it at 91
-  for (uint32_t j0 = 0; j0 < kZRowDw; j0 += 8) {
-    uint32_t D[10];
+  const uint32_t* row = s_img + lane * kZPitch;
+  uint64_t edm = 0;  // bit j: dword j (0..33) holds an ED byte
+  for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
+    uint32_t D[17];
 #pragma unroll
-    for (uint32_t j = 0; j < 10; ++j) D[j] = s_img[lane * kZPitch + j0 + j];
+    for (uint32_t j = 0; j < 17; ++j) D[j] = row[j0 + j];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-      const uint32_t x = D[j], y = D[j + 1], z2 = D[j + 2];
-      const uint32_t ex_ = x ^ 0xEDEDEDEDu, ey = y ^ 0xEDEDEDEDu;
-      if (!(((ex_ - 0x01010101u) & ~ex_ & 0x80808080u) | ((ey - 0x01010101u) & ~ey & 0x80808080u))) continue;
+    for (uint32_t j = 0; j < 17; ++j) {
+      const uint32_t e = D[j] ^ 0xEDEDEDEDu;
+      edm |= (((e - 0x01010101u) & ~e & 0x80808080u) ? 1ull : 0ull) << (j0 + j);
+    }
+  }
+  uint64_t sm = (edm | (edm >> 1)) & 0xFFFFFFFFull;  // dwords where a magic may start
+  while (sm) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(sm);
+    sm &= sm - 1u;
+    const uint32_t x = row[j], y = row[j + 1], z2 = row[j + 2];
 #pragma unroll
-      for (uint32_t sh = 0; sh < 4; ++sh) {
-        const uint32_t w0 = __builtin_amdgcn_alignbyte(y, x, sh);   // bytes a .. a+3 (LE)
-        const uint32_t w1 = __builtin_amdgcn_alignbyte(z2, y, sh);  // bytes a+4 .. a+7
-        const uint32_t a = r0 + 4u * (j0 + j) + sh;
-        if (w0 == 0x00EDAC03u && (w1 & 0xFFu) == 0x05u && a >= z.rs && a < z.re) {
+    for (uint32_t sh = 0; sh < 4; ++sh) {
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(y, x, sh);   // bytes a .. a+3 (LE)
+      const uint32_t w1 = __builtin_amdgcn_alignbyte(z2, y, sh);  // bytes a+4 .. a+7
+      const uint32_t a = r0 + 4u * j + sh;
+      if (w0 == 0x00EDAC03u && (w1 & 0xFFu) == 0x05u && a >= z.rs && a < z.re) {
 #pragma unroll
-          for (int r = 0; r < kZJReg; ++r)
-            if ((uint32_t)r == nm) cand[r] = a;
-          ++nm;
-        }
+        for (int r = 0; r < kZJReg; ++r)
+          if ((uint32_t)r == nm) cand[r] = a;
+        ++nm;
       }
     }
   }
