@@ -1334,6 +1334,14 @@ struct ZStreamBytes {  // stream byte k = span byte at aligned coordinate base +
   }
 };
 
+// Bytes q .. q+3 of the image, little-endian: two independent LDS reads, so a parser step
+// that needs a tag and a big-endian u16 after it waits for one LDS latency, not three.
+__device__ __forceinline__ uint32_t z4(const uint32_t* T, uint32_t q) {
+  const uint32_t k = q >> 2;
+  return __builtin_amdgcn_alignbit(T[rk(k + 1)], T[rk(k)], (q & 3u) << 3);
+}
+__device__ __forceinline__ uint32_t be16_12(uint32_t v) { return ((v >> 8) & 0xFFu) << 8 | ((v >> 16) & 0xFFu); }
+
 // Record length of the common stream shape, inline and call-free: one TC_OBJECT whose
 // class and superclasses are fresh TC_CLASSDESCs with flags SC_SERIALIZABLE only, primitive
 // fields only and an empty annotation (java.lang.Boolean, Integer, Long, ...); its class
@@ -1342,33 +1350,37 @@ struct ZStreamBytes {  // stream byte k = span byte at aligned coordinate base +
 // Specification 6.4 (newObject, newClassDesc, classDescInfo, fieldDesc, nowrclass).
 __device__ __forceinline__ uint32_t jser_flat_len(const uint32_t* T, uint32_t a, uint32_t img_end) {
   uint32_t p = a + 5;  // after the tag and AC ED 00 05
-  if (p + 1 > img_end || zb(T, p) != jser::TC_OBJECT) return 0u;
+  if (p + 1 > img_end || (z4(T, p) & 0xFFu) != jser::TC_OBJECT) return 0u;
   ++p;
   uint32_t data = 0;
   for (int depth = 0;; ++depth) {
     if (p + 1 > img_end || depth > 8) return 0u;
-    const uint32_t b = zb(T, p);
+    const uint32_t v = z4(T, p);  // [TC_CLASSDESC][className length u16] or [TC_NULL]
+    const uint32_t b = v & 0xFFu;
     if (b == jser::TC_NULL) {  // no (further) superclass
       ++p;
       break;
     }
     if (b != jser::TC_CLASSDESC || p + 3 > img_end) return 0u;
-    p += 3 + (zb(T, p + 1) << 8 | zb(T, p + 2)) + 8;  // className, serialVersionUID
-    if (p + 3 > img_end || zb(T, p) != jser::SC_SERIALIZABLE) return 0u;
-    const uint32_t nf = zb(T, p + 1) << 8 | zb(T, p + 2);
+    p += 3 + be16_12(v) + 8;  // className, serialVersionUID
+    if (p + 3 > img_end) return 0u;
+    const uint32_t f = z4(T, p);  // [flags][field count u16]
+    if ((f & 0xFFu) != jser::SC_SERIALIZABLE) return 0u;
+    const uint32_t nf = be16_12(f);
     if (nf & 0x8000u) return 0u;
     p += 3;
     for (uint32_t i = 0; i < nf; ++i) {
       if (p + 3 > img_end) return 0u;
-      const uint32_t tc = zb(T, p);
+      const uint32_t fv = z4(T, p);  // [typecode][fieldName length u16]
+      const uint32_t tc = fv & 0xFFu;
       // primitive sizes: B 1, C 2, D 8, F 4, I 4, J 8, S 2, Z 1
       const uint32_t sz = tc == 'B' || tc == 'Z' ? 1u : tc == 'C' || tc == 'S' ? 2u : tc == 'I' || tc == 'F' ? 4u
                           : tc == 'J' || tc == 'D' ? 8u : 0u;
       if (!sz) return 0u;
       data += sz;
-      p += 3 + (zb(T, p + 1) << 8 | zb(T, p + 2));
+      p += 3 + be16_12(fv);
     }
-    if (p + 1 > img_end || zb(T, p) != jser::TC_ENDBLOCKDATA) return 0u;
+    if (p + 1 > img_end || (z4(T, p) & 0xFFu) != jser::TC_ENDBLOCKDATA) return 0u;
     ++p;
   }
   p += data;
@@ -1383,10 +1395,11 @@ __device__ __forceinline__ bool zmagic(const uint32_t* T, uint32_t a) {
 // the general walker (*general set), or an invalid stream (0, *general clear).
 __device__ __forceinline__ uint32_t jser_inline_len(const uint32_t* T, uint32_t a, uint32_t img_end, uint64_t avail,
                                                     bool* general) {
-  const uint32_t tc = zb(T, a + 5);
+  const uint32_t v = z4(T, a + 5);
+  const uint32_t tc = v & 0xFFu;
   *general = false;
   if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
-    const uint64_t L = 8ull + (zb(T, a + 6) << 8 | zb(T, a + 7));
+    const uint64_t L = 8ull + be16_12(v);
     return L <= avail ? (uint32_t)L : 0u;
   }
   const uint32_t fl = tc == jser::TC_OBJECT ? jser_flat_len(T, a, img_end) : 0u;
