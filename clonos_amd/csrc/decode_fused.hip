@@ -186,8 +186,19 @@ struct JL {
   const uint32_t* rank;
   const uint32_t* len;
   const uint32_t* lm = nullptr;  // count pass: the tile's step-code map (below), else null
+  // count pass (load_jl_map): no bitmap or ranks, the entries' positions (sorted) instead
+  const uint32_t* pos = nullptr;
+  uint32_t n = 0;
 };
 __device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
+  if (!j.bits) {  // sorted positions: binary search (the count pass's rare slow path)
+    uint32_t lo = 0, hi = j.n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (j.pos[mid] < a) lo = mid + 1; else hi = mid;
+    }
+    return lo < j.n && j.pos[lo] == a ? j.len[lo] : 0u;
+  }
   const uint32_t w = j.bits[a >> 5], b = a & 31u;
   if (!((w >> b) & 1u)) return 0u;
   return j.len[j.rank[a >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))];
@@ -998,6 +1009,14 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
 // contiguous run.
 // ---------------------------------------------------------------------------------
+// The count pass's table (step-code map built): the Serializable codes go into the map, and
+// the entries stay in LDS as sorted positions and lengths for the true walk's rare lookups
+// (a code of 0: a stream longer than the map holds, or an invalid one) -- no bitmap or
+// ranks to build.
+struct JLPre;
+__device__ __forceinline__ JL load_jl_map(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane, uint32_t* lm,
+                                         const JLPre& pre);
+
 // Tile t's entry count and the first 64 entries of its table (one per lane), loaded before
 // the tile is staged so that their latency overlaps the staging's (config 3 holds ~50
 // entries per tile; load_jl loads any past 64 itself).
@@ -1007,6 +1026,26 @@ struct JLPre {
 __device__ __forceinline__ JLPre jl_prefetch(const FusedCtl& ctl, uint32_t t, uint32_t lane) {
   const uint64_t b = (uint64_t)t * kZJCap + lane;  // inside the table even past its entries
   return JLPre{gp(ctl.jn)[t], gp(ctl.jpos)[b], gp(ctl.jlen)[b]};
+}
+__device__ __forceinline__ JL load_jl_map(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane, uint32_t* lm,
+                                         const JLPre& pre) {
+  uint32_t* pos = s_j;
+  uint32_t* len = s_j + kZJCap;
+  const uint32_t n = min(pre.n, kZJCap);
+  __syncthreads();  // every row of the map is written (build_lm) before codes go over them
+  for (uint32_t i = lane; i < n; i += 64) {
+    const bool p0 = i == lane;
+    const uint32_t a = p0 ? pre.a : gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
+    const uint32_t L = p0 ? pre.L : gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
+    pos[i] = a;
+    len[i] = L;
+    lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
+  }
+  __syncthreads();  // the map's rows (written before the call) and the codes above
+  JL j{nullptr, nullptr, len, lm};
+  j.pos = pos;
+  j.n = n;
+  return j;
 }
 
 // Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
@@ -1260,7 +1299,8 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
       if (J && kLm) build_lm(z, s_img, s_j, lane);
-      if (J) jl = load_jl(ctl, t1 - 1, s_j, lane, kLm ? s_img : nullptr);
+      if (J && kLm) jl = load_jl_map(ctl, t1 - 1, s_j, lane, s_img, jl_prefetch(ctl, t1 - 1, lane));
+      else if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
       const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
       sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
@@ -1299,8 +1339,9 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
     JLPre pre{};
     if (J) pre = jl_prefetch(ctl, t, lane);
     stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
-    if (J && kLm) build_lm(z, s_img, s_j, lane);  // load_jl's first barrier orders it before the table's codes
-    if (J) jl = load_jl(ctl, t, s_j, lane, kLm ? s_img : nullptr, &pre);
+    if (J && kLm) build_lm(z, s_img, s_j, lane);
+    if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
+    else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
     uint32_t x_true;
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
     if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles,
