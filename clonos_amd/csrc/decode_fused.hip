@@ -322,10 +322,16 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
                                              uint32_t r0, const JL& jl) {
   SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
   uint32_t q = ws;
-  bool w;
-  while (q < rs) {
-    const uint32_t L = spec_len_fast<J>(T, q, end_a, SAFE, jl, &w);
-    q += L > 1u ? L : 1u;
+  // warm-up: only where the chain enters the region matters, so any fixed rule will do;
+  // this one steps one byte past wide tags (no branch, no field reads) and follows the
+  // fixed-length ones
+  {
+    constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
+    constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
+    while (q < rs) {
+      const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
+      q += L > 1u ? L : 1u;
+    }
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
