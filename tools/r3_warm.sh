@@ -1,9 +1,9 @@
 # Warm-up sweep (CLONOS_WARM) on one MI355X: config-2 count and config-3 (128-log subset) count.
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"; out=gpurun_out/warm; rm -rf $out; mkdir -p $out
-for w in; do
+for w in 96 128 160 192; do
   CLONOS_WARM=$w timeout -k 10 150 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-config3 --no-inflight --no-config4 > $out/c2_$w.json 2>/dev/null || exit 1
 done
-for w in 48 64 96 128; do
+for w in; do
   CLONOS_WARM=$w timeout -k 10 200 python3 tools/bench_config3.py --logs 128 --steps 3 > $out/c3_$w.json 2>/dev/null || exit 1
 done
 python3 - <<'PY'
