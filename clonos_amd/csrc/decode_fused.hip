@@ -708,12 +708,15 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
 }
 
 // Build the map in place over the tile's rows of the image (every lane of the wave calls it:
-// it holds a barrier).  The codes stay in registers until every lane has read the fields it
-// needs (a record's fields reach into the next row); TimerTrigger / SourceCheckpoint codes go
-// through `patch` (kZLmPatch per lane; a lane with more leaves the rest at 0, a deterministic
-// function of the tile like the rest of the map).  The span's end is applied last.
-constexpr uint32_t kZLmPatch = 8;
-__device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* patch, const uint32_t lane) {
+// it holds barriers).  The codes stay in registers until every lane has read the fields it
+// needs (a record's fields reach into the next row).  The span's end is applied last.
+// The tile's TimerTrigger / SourceCheckpoint bytes are compacted into `list` (the table's
+// LDS, free until load_jl_map) and measured 64 at a time, every lane busy: measured per
+// lane, a wave ran as many field decodes as its busiest lane's count, at about half lane use.
+// A tile with more than kZLmList such bytes leaves the rest at code 0 (a deterministic
+// function of the tile, like the rest of the map).
+constexpr uint32_t kZLmList = 2 * kZJBitsDw + kZJCap;
+__device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* list, const uint32_t lane) {
   const bool on = z.rs < z.re;
   const uint32_t r0 = lane * kZRegion;
   uint32_t c[kZRowDw];
@@ -730,35 +733,51 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
     const uint64_t f = (uint64_t)((__builtin_amdgcn_perm(kLmCand, 0u, x) & vm) >> (7u - (j & 7u))) << (32u * ((j >> 3) & 1u));
     if (j < 16u) cw0 |= f; else cw1 |= f;
   }
-  uint32_t np = 0;
-  if (on) {  // TimerTrigger / SourceCheckpoint bytes: length from the fields (the rules of decodeNext)
+  if (!on) cw0 = cw1 = 0;
+  // the lanes' candidates into the list, in lane order
+  const uint32_t nc = (uint32_t)(__popcll(cw0) + __popcll(cw1));
+  uint32_t incl = nc;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off);
+    if ((int)lane >= off) incl += y;
+  }
+  const uint32_t n = min((uint32_t)__shfl(incl, 63), kZLmList);
+  uint32_t idx = incl - nc;
 #pragma unroll 1
-    for (uint32_t hh = 0; hh < 2; ++hh) {
-      uint64_t m = hh ? cw1 : cw0;
-      while (m) {
-        const uint32_t i = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1u;
-        const uint32_t a = r0 + 64u * hh + 32u * (i >> 5) + 4u * (i & 7u) + ((i >> 3) & 3u);
-        if (a < z.rs || a >= z.re) continue;
-        const uint32_t code = lm_code(zlen_var(T, a, z.end_a, zb(T, a), 0u), true);
-        if (code && np < kZLmPatch) patch[lane * kZLmPatch + np++] = a | code << 16;
-      }
+  for (uint32_t hh = 0; hh < 2; ++hh) {
+    uint64_t m = hh ? cw1 : cw0;
+    while (m) {
+      const uint32_t i = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1u;
+      const uint32_t a = r0 + 64u * hh + 32u * (i >> 5) + 4u * (i & 7u) + ((i >> 3) & 3u);
+      // (a row may run past the tile: those bytes are no candidates)
+      if (idx < kZLmList) list[idx] = a >= z.rs && a < z.re ? a : 0xFFFFu;
+      ++idx;
     }
+  }
+  __syncthreads();
+  // their codes, 64 at a time: the length from the fields (the rules of decodeNext)
+  for (uint32_t k = lane; k < n; k += 64) {
+    const uint32_t a = list[k];
+    const uint32_t code = a != 0xFFFFu ? lm_code(zlen_var(T, a, z.end_a, zb(T, a), 0u), true) : 0u;
+    list[k] = a | code << 16;
   }
   __syncthreads();  // every lane has read the image
   if (on) {
 #pragma unroll
     for (uint32_t j = 0; j < kZRowDw; ++j) T[lane * kZPitch + j] = c[j];
-    for (uint32_t k = 0; k < np; ++k) {
-      const uint32_t e = patch[lane * kZLmPatch + k];
-      lm8_set(T, e & 0xFFFFu, e >> 16);
-    }
-    // the span's end: a fixed-length record must end by end_a (the wide ones were checked)
-    if (z.end_a < r0 + kZRegion + 13u) {
-      for (uint32_t a = z.end_a > r0 + 13u ? z.end_a - 13u : r0; a < r0 + kZRegion; ++a) {
-        const uint32_t cc = lm8(T, a);
-        if (a + (cc & 0x7Fu) > z.end_a) lm8_set(T, a, 0u);
-      }
+  }
+  __syncthreads();  // the rows hold codes: the candidates' go over them
+  for (uint32_t k = lane; k < n; k += 64) {
+    const uint32_t e = list[k];
+    if (e >> 16) lm8_set(T, e & 0xFFFFu, e >> 16);
+  }
+  // the span's end: a fixed-length record must end by end_a (the wide ones were checked)
+  if (on && z.end_a < r0 + kZRegion + 13u) {
+    for (uint32_t a = z.end_a > r0 + 13u ? z.end_a - 13u : r0; a < r0 + kZRegion; ++a) {
+      const uint32_t cc = lm8(T, a);
+      if (a + (cc & 0x7Fu) > z.end_a) lm8_set(T, a, 0u);
     }
   }
 }
