@@ -366,8 +366,10 @@ constexpr uint32_t kLmCand = 0x80u | 0x80u << 8;  // tags 4, 5 (the high table w
 
 __device__ __forceinline__ uint32_t lm8(const uint32_t* M, uint32_t a) { return ((lds_u8*)(M))[zoff(a)]; }
 __device__ __forceinline__ void lm8_set(uint32_t* M, uint32_t a, uint32_t c) { ((uint8_t*)(M))[zoff(a)] = (uint8_t)c; }
+// code 0x80 (wide, no length): a valid wide record longer than kZLmMax -- the speculative
+// chains step one byte, the true and canonical chains measure it by the full rules
 __device__ __forceinline__ uint32_t lm_code(int L, bool wide) {
-  return (L > 0 && L <= (int)kZLmMax) ? (uint32_t)L | (wide ? 0x80u : 0u) : 0u;
+  return (L > 0 && L <= (int)kZLmMax) ? (uint32_t)L | (wide ? 0x80u : 0u) : (L > 0 && wide ? 0x80u : 0u);
 }
 
 // One speculative step over the map (bits as spec_step; skips found by spec_bad).
@@ -402,35 +404,6 @@ __device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, 
   // lanes whose records cannot run past the span end (all but the last tile's) skip the test
   return re + 16u <= end_a ? spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl)
                            : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
-}
-
-// Canonical chain through region: the speculative rule from entry e merged with the
-// region's speculative chain (same rule, so meeting means identical from there on).
-template <bool J>
-__device__ __forceinline__ uint32_t canon_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
-                                                 const SpecR& s, const JL& jl) {
-  if (e >= re) return e;
-  if (J && jl.lm) {
-    uint32_t p = e, q = s.first;
-    for (;;) {
-      if (p == q) return s.exit;
-      if (p >= re) return p;
-      const uint32_t x = p < q ? p : q;
-      const uint32_t L = lm8(jl.lm, x) & 0x7Fu;
-      const uint32_t nx = x + (L > 1u ? L : 1u);
-      if (p < q) p = nx; else q = nx;
-    }
-  }
-  uint32_t p = e, q = s.first;
-  for (;;) {
-    if (p == q) return s.exit;
-    if (p >= re) return p;
-    bool w;
-    const uint32_t x = p < q ? p : q;
-    const uint32_t L = spec_len_fast<J>(T, x, end_a, false, jl, &w);
-    const uint32_t nx = x + (L > 1u ? L : 1u);
-    if (p < q) p = nx; else q = nx;
-  }
 }
 
 // True chain from entry e (e >= rs) merged with the speculative chain: walk until the true
@@ -797,9 +770,9 @@ struct GSpan {
   }
 };
 struct GRec {
-  const GSpan* g;
+  GSpan g;  // by value: no address taken, the span stays in registers
   uint32_t base;
-  __device__ int operator()(uint64_t k) const { return (int)g->at(base + (uint32_t)k); }
+  __device__ int operator()(uint64_t k) const { return (int)g.at(base + (uint32_t)k); }
 };
 __device__ __forceinline__ uint32_t fld_be32(const GRec& b, uint32_t k) {
   return (uint32_t)b(k) << 24 | (uint32_t)b(k + 1) << 16 | (uint32_t)b(k + 2) << 8 | (uint32_t)b(k + 3);
@@ -812,7 +785,7 @@ __device__ __forceinline__ int lm_true_slow(const GSpan& g, uint32_t p, uint32_t
     const uint32_t v = jl_len(jl, p);
     return v ? (int)v : -1;
   }
-  const int64_t L = len_fields(GRec{&g, p}, (int)tg, (uint64_t)(end_a - p));
+  const int64_t L = len_fields(GRec{g, p}, (int)tg, (uint64_t)(end_a - p));
   return (L > 0 && L <= 0x7FFFFFF0ll) ? (int)L : -1;
 }
 
@@ -823,7 +796,7 @@ __device__ __forceinline__ Res merge_walk_lm(const uint32_t* M, uint32_t re, uin
   return merge_walk_h(re, end_a, e, s, [&](uint32_t p, uint32_t* Lp, bool* w, uint32_t* why) -> bool {
     const uint32_t cc = lm8(M, p);
     uint32_t L = cc & 0x7Fu, wu = cc >> 7;
-    if (!cc) {
+    if (!L) {
       const int v = lm_true_slow(g, p, end_a, jl, &wu);
       if (v <= 0) {
         *why = 1;
@@ -837,12 +810,53 @@ __device__ __forceinline__ Res merge_walk_lm(const uint32_t* M, uint32_t re, uin
   });
 }
 
+// Canonical chain through the region from entry e: the speculative rule, except at a byte
+// it skips that holds a valid Serializable / TimerTrigger / SourceCheckpoint record too long
+// for it (map code 0x80; without the map: a zero speculative length) -- that record is
+// measured by the full rules (up to a tile), so a long record across the tile end leaves
+// the canonical exit at its end, where the true chain exits, not inside it.  The chain
+// meets the region's speculative chain at a start at or past its last skip (from there on
+// the two rules agree, so its exit is the region's).
+template <bool J>
+__device__ __forceinline__ uint32_t canon_walk_r(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
+                                                 const SpecR& s, const JL& jl, const GSpan& g) {
+  if (e >= re) return e;
+  const uint32_t r0 = (re - 1u) & ~(kZRegion - 1u);
+  uint32_t p = e;
+  while (p < re) {
+    const uint32_t i = p - r0;
+    if ((((i < 64u ? s.sb.lo : s.sb.hi) >> (i & 63u)) & 1ull) && p >= s.bad) return s.exit;
+    uint32_t L;
+    int v = 0;
+    if (J && jl.lm) {
+      const uint32_t c = lm8(jl.lm, p);
+      L = c & 0x7Fu;
+      if (c == 0x80u) {
+        uint32_t w;
+        v = lm_true_slow(g, p, end_a, jl, &w);
+      }
+    } else {
+      bool w;
+      L = spec_len_fast<J>(T, p, end_a, false, jl, &w);
+      if (!L) {
+        const uint32_t tg = zb8(T, p);
+        if (tg == CLG_TAG_TIMER_TRIGGER || tg == CLG_TAG_SOURCE_CHECKPOINT) v = zlen_var(T, p, end_a, tg, 0u);
+        else if (J && tg == CLG_TAG_SERIALIZABLE) v = (int)min(jl_len(jl, p), 0x7FFFFFFFu);
+      }
+    }
+    if (!L) L = (v > 0 && v <= (int)kZTile) ? (uint32_t)v : 1u;
+    p += L;
+  }
+  return p;
+}
+
 // Canonical exit of the tile from the lanes' speculative walks: lanes >= c0 (the last
 // kZCanonLanes regions) chain their speculative exits, lane c0 starting from its own
 // speculative chain; lanes whose entry changed merge again.
 template <bool J>
 __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t* s_img, const SpecR& sp, uint32_t lane,
-                                                 const JL& jl) {
+                                                 const JL& jl, const TileDesc* __restrict__ tiles, uint32_t t) {
+  const GSpan g{tiles, t, z.sd.first_tile + z.sd.n_tiles, z.lo, z.td.span_off};
   const uint32_t last_l = z.hi > z.lo ? (z.hi - 1) >> 7 : 0;
   const uint32_t c0 = last_l >= kZCanonLanes - 1 ? last_l - (kZCanonLanes - 1) : 0;
   const bool on = lane >= c0 && z.rs < z.re;
@@ -854,7 +868,7 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
     if (!__any(ch)) break;
     if (ch) {
       entry = want;
-      cx = on ? canon_walk_r<J>(s_img, z.re, z.end_a, want, sp, jl) : want;
+      cx = on ? canon_walk_r<J>(s_img, z.re, z.end_a, want, sp, jl, g) : want;
     }
   }
   return __shfl(cx, 63);
@@ -1329,7 +1343,7 @@ __global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict_
       const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
       sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
-      x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl);
+      x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
@@ -1665,7 +1679,7 @@ __global__ __launch_bounds__(64) void k_decode_one(const TileDesc* __restrict__ 
   // ---- publish the canonical exit, then take the entry from the predecessor's
   uint32_t x_pub = kZCanon;
   if (!z.last) {
-    x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl);
+    x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl, tiles, t);
     if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (z.td.span_off + (x_pub - lo)));
   }
   OPHASE(3);

@@ -155,9 +155,11 @@ def test_fused_serializable_long_streams(feng):
 def test_fused_tables_long_wide_records(feng):
     """With Serializable tables the count pass walks a step-code map whose codes hold
     lengths up to 126 bytes: longer TimerTrigger names, SourceCheckpoint references and
-    Serializable streams get code 0, and the true walk measures them from HBM (TimerTrigger /
-    SourceCheckpoint by the decodeNext rules, Serializable from the table).  Bit-exact
-    against the oracle, on the batch that builds the tables and on the next one."""
+    Serializable streams get code 0x80, and the true walk measures them from HBM (TimerTrigger /
+    SourceCheckpoint by the decodeNext rules, Serializable from the table), as does the
+    canonical walk, so such a record across a chunk's last tile end leaves the published exit
+    where the true chain exits.  Bit-exact against the oracle, on the batch that builds the
+    tables and on the next one, and (16 KiB segments) without falling back."""
     rng = np.random.default_rng(21)
     for _ in range(2):
         parts = []
@@ -172,9 +174,12 @@ def test_fused_tables_long_wide_records(feng):
             elif k == 2:
                 parts.append(D.encode(D.SerializableDeterminant(D.jser_string("s" * n))))
         buf = b"".join(parts)
+        feng.kernel_stats_reset()
         dec = feng.decode_host(buf)
         assert_span_equal(dec, 0, buf)
-    assert "decode_jser" in feng.kernel_stats()
+        assert "decode_jser" in feng.kernel_stats()
+        if feng.segment_bytes == 16384:
+            assert not fell_back(feng)
 
 
 @pytest.mark.parametrize("bad", ["magic_no_object", "truncated_stream", "bad_magic"])
