@@ -182,6 +182,27 @@ def test_fused_tables_long_wide_records(feng):
             assert not fell_back(feng)
 
 
+def test_fused_long_names_no_tables(feng):
+    """No Serializable records (no tables): TimerTrigger names and SourceCheckpoint
+    references of 200-1500 bytes, past the 256 bytes the speculative rule follows.  The
+    canonical walk measures them by the full rules, so the batch stays on the fast path
+    (16 KiB segments) and matches the oracle bit for bit."""
+    rng = np.random.default_rng(23)
+    parts = []
+    for i in range(300):
+        parts.append(synth.random_log(int(rng.integers(5, 80)), rng, allow_serializable=False))
+        n = int(rng.integers(200, 1500))
+        if i % 2:
+            parts.append(D.encode(D.TimerTriggerDeterminant(i, 5 * i, D.INTERNAL, b"N" * n)))
+        else:
+            parts.append(D.encode(D.SourceCheckpointDeterminant(i, i, 2 * i, D.CHECKPOINT, b"R" * n)))
+    buf = b"".join(parts)
+    dec = feng.decode_host(buf)
+    assert_span_equal(dec, 0, buf)
+    if feng.segment_bytes == 16384:
+        assert not fell_back(feng)
+
+
 @pytest.mark.parametrize("bad", ["magic_no_object", "truncated_stream", "bad_magic"])
 def test_fused_serializable_errors(feng, bad):
     """Invalid Serializable records after valid ones: same status / offset / tag as the
