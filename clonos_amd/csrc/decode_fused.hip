@@ -347,15 +347,16 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
 // records are dominated by wide records (config 3: 20 %), and a speculative walk that meets
 // one takes a divergent branch with two or three dependent LDS reads; with 64 lanes some lane
 // is in that branch at almost every step.  So before walking, the wave turns every byte of
-// the tile into a step code, data-parallel, in an LDS map with the image's row layout:
-//   0      no record the speculative walk follows (invalid, or longer than kZLmMax): step 1
+// the tile into a step code, data-parallel, in place over the LDS image (same row layout):
+//   0      no valid record starts here: the speculative walk steps 1
+//   0x80   a valid wide record longer than kZLmMax: the speculative walk steps 1, the true
+//          and canonical walks measure it from HBM / the table (lm_true_slow)
 //   else   bits 0-6 the record length, bit 7 set for a wide record
 // Fixed-length tags come from a byte-permute table over four tags at a time; TimerTrigger
 // and SourceCheckpoint bytes (a few per region) get their length from their fields by the
 // decodeNext rules (zlen_var); Serializable records get theirs from the phase-3 table
-// (load_jl).  The speculative walk then costs one LDS read and no branch per step.  The true
-// chain (merge_walk_r) still reads the image, so every record it accepts is checked by the
-// full rules; the map only decides the speculative (and canonical) chains.
+// (load_jl_map).  Every walk then costs one LDS read and no branch per step.  Every code
+// was made by the full rules, so the true chain (merge_walk_lm) may follow codes too.
 // ---------------------------------------------------------------------------------
 constexpr uint32_t kZLmMax = 126;
 // codes of tags 0..7: Order 2, Timestamp 9, RNG 5, Serializable 0 (table), TimerTrigger and
