@@ -1320,8 +1320,11 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
 // and a chunk's first tile enters at the previous chunk's published exit, which that
 // chunk's last tile must then reproduce.  Blocks are all resident and publish first, so
 // the one wait always ends; a wait past kZSpinLimit cycles aborts the batch instead.
+// 128 VGPRs (4 waves per SIMD by registers, 3.25 by LDS with tables): count<J> 0.396 to
+// 0.376 ms on the config-3 subset, count<false> (88 VGPRs) unaffected.  The same bound on
+// k_decode_jser made it slower (0.26 to 0.28 ms), so that kernel keeps its 150.
 template <bool J>
-__global__ __launch_bounds__(64) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
