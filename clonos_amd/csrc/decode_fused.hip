@@ -378,7 +378,7 @@ __device__ __forceinline__ uint32_t lm_step(const uint32_t* M, uint32_t q, uint6
   const uint32_t c = lm8(M, q);
   const uint64_t m = 1ull << (q & 63u);
   sbw |= m;
-  wbw |= m & (0ull - (uint64_t)(c >> 7));
+  wbw |= (uint64_t)(c >> 7) << (q & 63u);  // bit 7: a wide record
   const uint32_t L = c & 0x7Fu;
   return q + (L > 1u ? L : 1u);
 }
