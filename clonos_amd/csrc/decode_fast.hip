@@ -488,7 +488,7 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   // deferred tiles, and the successor of a deferred tile (its segment crossing the tile
   // end, and its next-tile points, may land on Serializable records there)
   if (!J.defer[t] && !(t > sd.first_tile && J.defer[t - 1])) return;
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, J.ar};
   stage_tile(s_tile, td, sr, lane);
   const TileGeom g{td.delta, td.delta + td.len};
   const uint32_t rs = g.rs((int)lane), re = g.re((int)lane);

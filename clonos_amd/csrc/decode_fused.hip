@@ -21,8 +21,8 @@
 //   4. across tiles: every tile first computes its exit assuming the chain merges inside
 //      it ("canonical" exit, independent of its entry) and publishes it, then reads its
 //      predecessor's canonical exit as its entry, re-merges lane 0 and checks that its
-//      true exit is the one it published.  Record and wide-record bases come from a
-//      decoupled look-back over per-tile aggregates;
+//      true exit is the one it published.  Record and wide-record bases come from the
+//      scan pass over the per-tile counts;
 //   5. emit: record starts are dropped into LDS by output index and decoded by
 //      consecutive lanes, so every SoA store of the wave is one contiguous run.
 //
@@ -57,7 +57,7 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_FUSED_PIPELINE
 #define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
 #endif
-constexpr uint32_t kZWin = 1024;                       // record starts staged per window (one-pass kernel)
+constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
@@ -1630,288 +1630,11 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
     const uint32_t a = ctl.jpos[item];
     const uint64_t so = td.span_off + (a - td.delta);  // span offset of the record
     ZStreamBytes acc{nullptr, a + 1, 0u, td.delta, td.span_off, tiles, t, sd.first_tile + sd.n_tiles};
-    const int64_t sl = jser::stream_len(acc, sd.len - so - 1);
+    const jser::DevArena ar{ctl.jar};
+    const int64_t sl = jser::stream_len(acc, sd.len - so - 1, ar);  // kJsSpill: 0, the robust pipeline retries
     const uint64_t L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
     ctl.jlen[item] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
   }
-}
-
-// =================================================================================
-// One-pass decode (k_decode_one): every tile is staged once, its record chain found and
-// its records emitted by the same wave.  Tiles are taken in order from a ticket, so every
-// tile a wave waits for is held by a wave that already runs:
-//   * a tile publishes its canonical exit (entry-independent, canon_exit_r) before it
-//     waits for anything; its successor enters there and the tile later checks that its
-//     true exit is that value (else the batch aborts to the robust pipeline);
-//   * record / wide-record bases come from a decoupled look-back over per-tile words
-//     (flag 1: the tile's own counts, flag 2: the inclusive prefix), 64 predecessors per
-//     wave step.
-// Input bytes are read once; the only other traffic is the SoA output.
-// =================================================================================
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
-template <bool J>
-__global__ __launch_bounds__(64) void k_decode_one(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                   FusedCtl ctl, DecodeOut out) {
-  __shared__ uint32_t s_img[kZImgDw];
-  __shared__ uint16_t s_pos[kZWin];
-  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  __shared__ uint32_t s_tk;
-  const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
-  if (lane == 0) s_tk = (ctl.nodep & 8u) ? atomicAdd(ctl.ticket, 1u) : blockIdx.x;
-  __syncthreads();
-  const uint32_t t = s_tk;
-  if (t >= nt || ld_agent32(ctl.abort)) return;
-#define OPHASE(i) \
-  if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
-  OPHASE(0);
-  const ZTile z = ztile(tiles, spans, t, lane);
-  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi);
-  OPHASE(1);
-  JL jl{nullptr, nullptr, nullptr};
-  if (J) jl = load_jl(ctl, t, s_j, lane);
-  const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
-  const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
-  const SpecR sp = rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
-                           : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
-  OPHASE(2);
-
-  // ---- publish the canonical exit, then take the entry from the predecessor's
-  uint32_t x_pub = kZCanon;
-  if (!z.last) {
-    x_pub = canon_exit_r<J>(z, s_img, sp, lane, jl, tiles, t);
-    if (lane == 0) st_agent(&ctl.st_x[t], (1ull << 63) | (z.td.span_off + (x_pub - lo)));
-  }
-  OPHASE(3);
-  uint64_t xs;
-  if (z.first || (ctl.nodep & 1u)) {
-    xs = z.td.span_off;  // a span starts on a record boundary
-  } else {
-    uint64_t v;
-    const uint64_t w0 = __builtin_amdgcn_s_memtime();
-    for (;;) {
-      v = ld_agent(&ctl.st_x[t - 1]);
-      if (v) break;
-      if (ld_agent32(ctl.abort)) return;
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
-        if (lane == 0) raise_abort(ctl, 4, t);
-        return;
-      }
-    }
-    xs = v & ~(1ull << 63);
-  }
-  const uint64_t ee = xs - z.td.span_off + lo;
-  const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
-  OPHASE(4);
-
-  // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
-  // exit; lane 0 the true entry); lanes whose entry changed re-merge until consistent
-  uint32_t entry = lane == 0 ? e_true : __shfl_up(sp.exit, 1);
-  Res r = rs < re ? merge_walk_r<J>(s_img, re, end_a, entry, sp, jl) : Res{{0, 0}, {0, 0}, entry, 0, 0};
-  for (int it = 0; it <= 64; ++it) {
-    const uint32_t prev = __shfl_up(r.exit, 1);
-    const uint32_t want = lane == 0 ? e_true : prev;
-    const bool ch = want != entry;
-    if (!__any(ch)) break;
-    if (ch) {
-      entry = want;
-      r = rs < re ? merge_walk_r<J>(s_img, re, end_a, want, sp, jl) : Res{{0, 0}, {0, 0}, want, 0, 0};
-    }
-  }
-  const uint32_t x_true = __shfl(r.exit, 63);
-  const uint64_t badm = __ballot(r.bad != 0u);
-  uint32_t reason = badm ? (__shfl(r.bad, (int)__builtin_ctzll(badm)) == 2u ? 5u : 1u) : 0u;
-  if (z.last) {
-    if (x_true != end_a) reason = reason ? reason : 2u;
-  } else if (x_true != x_pub) {
-    reason = reason ? reason : 3u;  // the successor already entered at the published exit
-  }
-  if (reason && !ctl.nodep) {
-    if (lane == 0) raise_abort(ctl, reason, t);
-    return;
-  }
-
-  // ---- counts, then the exclusive prefix by decoupled look-back
-  uint32_t rec = bcount(r.bm), wide = bcount(r.wb);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    rec += __shfl_xor(rec, off);
-    wide += __shfl_xor(wide, off);
-  }
-  const uint64_t agg = (uint64_t)wide << 32 | rec;
-  if (lane == 0) {
-    gp(ctl.cnt)[t] = agg;
-    st_agent(&ctl.look[t], kZLookAgg | agg);
-  }
-  OPHASE(5);
-  // two-level look-back: the tile's offset inside its group of kZGroup tiles (one read of
-  // the group mates' words), then the group's offset from the group words (64 groups per
-  // read; the last tile of a group publishes the group's counts, then its inclusive prefix)
-  const uint32_t g = t / kZGroup, g0 = g * kZGroup;
-  const uint32_t g1 = min(g0 + kZGroup, nt) - 1;
-  uint64_t ingrp = 0, excl = 0;
-  if (!(ctl.nodep & 2u)) {
-    const uint64_t w0 = __builtin_amdgcn_s_memtime();
-    for (;;) {
-      const uint32_t k = g0 + lane;
-      const uint64_t v = k < t ? ld_agent(&ctl.look[k]) : kZLookAgg;
-      if (!__any((v >> 62) == 0u)) {
-        ingrp = wave_sum64(k < t ? (v & kZLookVal) : 0ull);
-        break;
-      }
-      if (ld_agent32(ctl.abort)) return;
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
-        if (lane == 0) raise_abort(ctl, 4, t);
-        return;
-      }
-    }
-  }
-  if (t == g1 && lane == 0) st_agent(&ctl.glook[g], kZLookAgg | (ingrp + agg));
-  if (!(ctl.nodep & 2u)) {
-    int64_t j = (int64_t)g - 1;
-    const uint64_t w0 = __builtin_amdgcn_s_memtime();
-    while (j >= 0) {
-      const int64_t k = j - (int64_t)lane;
-      const uint64_t v = k >= 0 ? ld_agent(&ctl.glook[k]) : kZLookInc;  // before group 0: an inclusive 0
-      const uint64_t f = v >> 62;
-      const uint64_t incm = __ballot(f == 2u);
-      const uint64_t zm = __ballot(f == 0u);
-      const uint32_t stop = incm ? (uint32_t)__builtin_ctzll(incm) : 64u;
-      const uint64_t upto = stop >= 63u ? ~0ull : ((2ull << stop) - 1ull);  // lanes 0 .. stop
-      if (zm & upto) {  // an earlier group is not complete yet
-        if (ld_agent32(ctl.abort)) return;
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memtime() - w0 > kZSpinLimit) {
-          if (lane == 0) raise_abort(ctl, 4, t);
-          return;
-        }
-        continue;
-      }
-      excl += wave_sum64(lane <= stop ? (v & kZLookVal) : 0ull);
-      if (incm) break;
-      j -= 64;
-    }
-  }
-  if (t == g1 && lane == 0) st_agent(&ctl.glook[g], kZLookInc | (excl + ingrp + agg));
-  excl += ingrp;
-  if (lane == 0) gp(ctl.base)[t] = excl;  // look[] keeps the tile's own counts for its group mates
-  OPHASE(6);
-
-  // ---- emit: record starts into LDS by output index, consecutive lanes decode
-  // consecutive records (each SoA store of the wave is one contiguous run)
-  const uint32_t r0 = lane * kZRegion;
-  const uint32_t cnt = bcount(r.bm);
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += y;
-  }
-  const uint32_t total = (ctl.nodep & 4u) ? 0u : __shfl(incl, 63);
-  const uint64_t rec0 = excl & 0xFFFFFFFFull;
-  uint64_t wbase = (excl >> 32) & ((1ull << 30) - 1);
-  Bits cur = r.bm;
-  uint32_t idx = incl - cnt;
-  for (uint32_t w0 = 0; w0 < total; w0 += kZWin) {
-    const uint32_t wend = w0 + kZWin;
-    // the lane's record starts into s_pos in order: the low 64 region bytes, then the high
-    // 64 (one 64-bit word per loop: no per-start choice between the halves)
-    while (cur.lo && idx < wend) {
-      s_pos[idx - w0] = (uint16_t)(r0 + (uint32_t)__builtin_ctzll(cur.lo));
-      cur.lo &= cur.lo - 1;
-      ++idx;
-    }
-    while (!cur.lo && cur.hi && idx < wend) {
-      s_pos[idx - w0] = (uint16_t)(r0 + 64u + (uint32_t)__builtin_ctzll(cur.hi));
-      cur.hi &= cur.hi - 1;
-      ++idx;
-    }
-    __syncthreads();
-    const uint32_t nw = total - w0 < kZWin ? total - w0 : kZWin;
-    for (uint32_t i0 = 0; i0 < nw; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const bool act = i < nw;
-      const uint32_t a = act ? (uint32_t)s_pos[i] : lo;
-      const uint32_t kk = rk(a >> 2), sh = 8u * (a & 3u);
-      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
-      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
-      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
-      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-      const uint32_t tg = x0 & 0xFFu;
-      const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
-      int64_t v0 = tg == CLG_TAG_ORDER       ? (int64_t)(int8_t)(blo & 0xFFu)
-                   : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)bhi << 32 | blo)
-                                             : (int64_t)(int32_t)__builtin_bswap32(blo);
-      const bool wide_rec = act && is_wide((int)tg);
-      Rec rr{};
-      if (wide_rec) {
-        const ZBytes b{s_img, a};
-        uint32_t tgu;
-        const int L = (J && tg == CLG_TAG_SERIALIZABLE) ? (int)jl_len(jl, a) : zlen(s_img, a, end_a, &tgu);
-        decode_fields(b, (int)tg, (int64_t)L, rr);
-        v0 = rr.v0;
-      }
-      const uint64_t wm = __ballot(wide_rec);
-      const uint64_t g = rec0 + w0 + i;
-      if (act) {
-        const uint32_t so = (uint32_t)(z.td.span_off + (a - lo));
-        if (g < out.cap) {
-          gp(out.off)[g] = so;
-          gp(out.tag)[g] = (uint8_t)tg;
-          gp(out.v0)[g] = v0;
-        }
-        if (wide_rec) {
-          const uint64_t wi = wbase + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
-          if (wi < out.wcap) {
-            gp(out.w_idx)[wi] = (uint32_t)g;
-            gp(out.w_rc)[wi] = rr.rc;
-            gp(out.w_v1)[wi] = rr.v1;
-            gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
-            gp(out.w_var_len)[wi] = rr.var_len;
-            gp(out.w_sub)[wi] = rr.sub;
-          }
-        }
-      }
-      wbase += (uint64_t)__popcll(wm);
-    }
-    __syncthreads();
-  }
-  OPHASE(7);
-#undef OPHASE
-}
-
-// Each span's record / wide-record range from the one-pass look-back words.
-__global__ __launch_bounds__(256) void k_decode_spans1(const SpanDesc* __restrict__ spans, uint32_t n_spans,
-                                                       FusedCtl ctl) {
-  const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-  if (s >= n_spans || ld_agent32(ctl.abort)) return;
-  const SpanDesc sd = spans[s];
-  if (!sd.n_tiles) return;
-  const uint32_t t0 = sd.first_tile, t1 = sd.first_tile + sd.n_tiles - 1;
-  gp(ctl.span_lo)[s] = gp(ctl.base)[t0];
-  gp(ctl.span_hi)[s] = gp(ctl.base)[t1] + gp(ctl.cnt)[t1];
-}
-
-int launch_decode_one(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                      FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase) {
-  if (!n_tiles) return CLG_OK;
-  ctl.n_tiles = n_tiles;
-  hipStream_t st = (hipStream_t)stream;
-  if (phase == 0) {
-    if (ctl.jser)
-      hipLaunchKernelGGL(k_decode_one<true>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
-    else
-      hipLaunchKernelGGL(k_decode_one<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
-  } else {
-    hipLaunchKernelGGL(k_decode_spans1, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
-  }
-  return launch_status(hipGetLastError());
 }
 
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,

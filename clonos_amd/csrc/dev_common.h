@@ -39,6 +39,7 @@ struct SpanReader {
   const TileDesc* tiles;
   uint32_t t0, t1, cur;
   uint64_t len;
+  JArena ar;  // the stream walker's spill arena
   __device__ int at(uint64_t o) {
     if (o >= len) return -1;
     while (cur > t0 && o < tiles[cur].span_off) --cur;
@@ -73,6 +74,7 @@ struct AtSpan {
   SpanReader* r;
   uint64_t base;
   __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + k); }
+  __device__ __forceinline__ JArena arena() const { return r->ar; }
 };
 
 template <class F>

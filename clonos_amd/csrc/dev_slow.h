@@ -9,7 +9,8 @@ namespace clg {
 
 // Exact record length at a record start (decodeNext read order and error precedence).
 // `avail` = bytes from the record start to the span end (>= 1).  Returns L > 0 or a
-// negative CLG_E_* status.
+// negative CLG_E_* status; CLG_E_NOSPACE: the stream walker's spill arena (b.arena())
+// is full -- not a decode result, the engine grows the arena and decodes again.
 template <class F>
 __device__ __noinline__ int64_t rec_len_slow(F& b, uint64_t avail) {
   const int tag = (int8_t)b(0);
@@ -54,7 +55,9 @@ __device__ __noinline__ int64_t rec_len_slow(F& b, uint64_t avail) {
         F* f;
         __device__ int operator()(uint64_t k) { return (*f)(k + 1); }
       } sh{&b};
-      const int64_t j = jser::stream_len(sh, avail - 1);
+      const jser::DevArena ar{b.arena()};
+      const int64_t j = jser::stream_len(sh, avail - 1, ar);
+      if (j == jser::kJsSpill) return CLG_E_NOSPACE;
       if (j < 0) return CLG_E_BAD_SERIAL;
       L = 1 + j;
       break;

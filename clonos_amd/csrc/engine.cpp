@@ -359,6 +359,10 @@ struct clg_engine {
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
   DevBuf d_hdr;                      // piggyback: delta headers staged for the gather
+  // The Serializable walker's spill arena (kernels.h JArena): [used u64 | pad to 256 | bytes].
+  // Grown (doubled) whenever a decode reports CLG_E_NOSPACE, i.e. a walk found it full.
+  DevBuf d_jarena;
+  size_t jarena_bytes = size_t(16) << 20;
   // Slices into device memory run on their own stream, overlapping the next decode: the
   // gather only reads log segments, so every pool write (flush / upstream scatter) and
   // every full sync first waits for it (gwait).
@@ -375,7 +379,6 @@ struct clg_engine {
   PinBuf h_plan;  // decode plans (upload_plan)
   DevBuf d_plan;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
-  bool three_pass = true;    // CLONOS_DECODE=onepass: the experimental one-pass kernel instead of count/scan/emit
 
   // timing
   std::map<std::string, Stat> stats;
@@ -427,6 +430,22 @@ struct clg_engine {
     }
     return CLG_OK;
   }
+  // The arena for kernels queued next on `stream`, its bump counter reset first.
+  int jarena_reset(clg::JArena* a) {
+    CHK(d_jarena.ensure(jarena_bytes + 256));
+    HIPCHK(hipMemsetAsync(d_jarena.p, 0, 8, stream));
+    *a = clg::JArena{d_jarena.as<uint8_t>() + 256, jarena_bytes, d_jarena.as<unsigned long long>()};
+    return CLG_OK;
+  }
+  int jarena_grow() {
+    CHK(sync());  // kernels still using the old arena
+    if (jarena_bytes >= (size_t(1) << 36))
+      return fail(CLG_E_DEVICE, "Serializable walker spill arena would exceed 64 GiB");
+    jarena_bytes *= 2;
+    stats["jser_arena_grow"].launches++;
+    return CLG_OK;
+  }
+
   int sync() {
     CHK(gwait());
     HIPCHK(hipStreamSynchronize(stream));
@@ -1081,7 +1100,7 @@ struct clg_engine {
     return w >= 0 ? uint32_t(w) : 96u;
   }
 
-  // Single-pass fused decode (decode_fused.hip).  *aborted = true when the kernel met
+  // Fast three-pass decode (decode_fused.hip).  *aborted = true when the kernels met
   // anything outside its fast path; the caller then runs the robust pipeline.
   // jser: build the Serializable tables first (phase 3).  *need_jser: the batch aborted
   // only because it met Serializable records without tables.
@@ -1141,7 +1160,8 @@ struct clg_engine {
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
-                      jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr, spec_warm(jser)};
+                      jser ? d_zjwork.as<uint32_t>() : nullptr, spec_warm(jser), clg::JArena{}};
+    if (jser) CHK(jarena_reset(&ctl.jar));
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
@@ -1242,122 +1262,6 @@ struct clg_engine {
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     return finish_out(out, nrec, nwide);
   }
-  // One-pass decode (k_decode_one): stage, chain, look-back and emit per tile in one
-  // kernel; then the span ranges.  *aborted / *need_jser as in run_fused.
-  int run_one(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted, bool jser,
-              bool* need_jser) {
-    *aborted = false;
-    *need_jser = false;
-    reset_result(out);
-    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
-    if (ns == 0) return CLG_OK;
-    if (nt > (1u << 19)) {  // > 4 GiB in one batch: the look-back words hold 32-bit record prefixes
-      *aborted = true;
-      return CLG_OK;
-    }
-    CHK(upload_plan(p, d_ztiles));
-    clg::DecodeOut o{};
-    CHK(prep_out(out, &o));
-    // words: st_x[nt] cnt[nt] look[nt] glook[ng] base[nt] | span_lo[ns] span_hi[ns] | abort[8] (u32) | ticket
-    const size_t ng = (size_t(nt) + clg::kZGroup - 1) / clg::kZGroup;
-    const size_t o_span = 4 * size_t(nt) + ng, o_ab = o_span + 2 * size_t(ns), words = o_ab + 5;
-    CHK(d_zctl.ensure(words * 8));
-    CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
-    uint64_t* w = d_zctl.as<uint64_t>();
-    uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
-    if (jser) {
-      CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
-      CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
-      CHK(d_zjn.ensure(size_t(nt) * 4));
-      CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
-      HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
-    }
-    clg::FusedCtl ctl{};
-    ctl.st_x = w;
-    ctl.cnt = w + nt;
-    ctl.look = w + 2 * size_t(nt);
-    ctl.glook = w + 3 * size_t(nt);
-    ctl.base = w + 3 * size_t(nt) + ng;  // per tile: exclusive record / wide prefix
-    ctl.span_lo = w + o_span;
-    ctl.span_hi = w + o_span + ns;
-    ctl.abort = ab;
-    ctl.n_tiles = nt;
-    ctl.jpos = jser ? d_zjpos.as<uint32_t>() : nullptr;
-    ctl.jlen = jser ? d_zjlen.as<uint32_t>() : nullptr;
-    ctl.jn = jser ? d_zjn.as<uint32_t>() : nullptr;
-    ctl.jser = jser ? 1u : 0u;
-    ctl.jwork_cap = uint32_t(nt) * 16 + 1024;
-    ctl.jwork = jser ? d_zjwork.as<uint32_t>() : nullptr;
-    ctl.ticket = reinterpret_cast<uint32_t*>(w + o_ab + 4);
-    ctl.warm = spec_warm(jser);
-    // developer timing probe (CLONOS_ONE_PROBE bits: 1 no entry wait, 2 no look-back, 4 no
-    // emit); output invalid
-    static const uint32_t probe = [] {
-      const char* v = getenv("CLONOS_ONE_PROBE");
-      return v ? uint32_t(atoi(v)) : 0u;
-    }();
-    ctl.nodep = probe;
-    const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
-    if (prof_path) {
-      CHK(d_prof.ensure(size_t(nt) * 64));
-      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
-      ctl.prof = d_prof.as<uint64_t>();
-    }
-    HIPCHK(hipMemsetAsync(w, 0, (4 * size_t(nt) + ng) * 8, stream));
-    HIPCHK(hipMemsetAsync(ab, 0, 40, stream));
-    auto* zt = d_ztiles.as<clg::TileDesc>();
-    auto* zs = d_spans.as<clg::SpanDesc>();
-    if (jser)
-      CHK(timed("decode_jser", log_bytes, [&] { return clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 3); }));
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (cfg.flags & CLG_F_TIMING) {
-      ea = get_event();
-      eb = get_event();
-      hipEventRecord(ea, stream);
-    }
-    CHK(clg::launch_decode_one(zt, nt, zs, ns, ctl, o, stream, 0));
-    if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
-    CHK(clg::launch_decode_one(zt, nt, zs, ns, ctl, o, stream, 1));
-    uint64_t* hz = h_zres.as<uint64_t>();
-    HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipStreamSynchronize(stream));
-    if (prof_path) {
-      std::vector<uint64_t> hp(size_t(nt) * 8);
-      hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
-      if (FILE* fp = fopen(prof_path, "wb")) {
-        fwrite(hp.data(), 8, hp.size(), fp);
-        fclose(fp);
-      }
-    }
-    const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
-    if (jser) jser_hint = hab[7] != 0;
-    if (hab[0]) {
-      if (ea) {
-        ev_pool.push_back(ea);
-        ev_pool.push_back(eb);
-      }
-      *aborted = true;
-      *need_jser = !jser && hab[5];
-      if (getenv("CLONOS_FUSED_DEBUG"))
-        fprintf(stderr, "[clonos] one-pass decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d "
-                "exit=%d timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]),
-                int(~hab[3]), int(~hab[4]), int(~hab[5]), int(~hab[6]));
-      return CLG_OK;
-    }
-    constexpr uint64_t kRecMask = 0xFFFFFFFFull;
-    uint64_t nrec = 0, nwide = 0;
-    for (uint32_t s = 0; s < ns; ++s) {
-      if (span_rec_base) span_rec_base[s] = nrec;
-      if (p.spans[s].n_tiles == 0) continue;
-      const uint64_t a = hz[s], b = hz[ns + s];
-      nrec += (b & kRecMask) - (a & kRecMask);
-      nwide += (b >> 32) - (a >> 32);
-    }
-    if (span_rec_base) span_rec_base[ns] = nrec;
-    if (ea) timings.push_back(PendingTiming{"decode_one", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
-    return finish_out(out, nrec, nwide);
-  }
-
   // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
   // tile_bytes)` fills a plan for the given tile geometry.
   template <class Build>
@@ -1367,11 +1271,7 @@ struct clg_engine {
       DecodePlan pf;
       build(pf, clg::kZTile);
       bool aborted = false, need_jser = false;
-      auto run = [&](bool j) {
-        return three_pass ? run_fused(pf, log_bytes, out, span_rec_base, &aborted, j, &need_jser)
-                          : run_one(pf, log_bytes, out, span_rec_base, &aborted, j, &need_jser);
-      };
-      CHK(run(jser_hint));
+      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, jser_hint, &need_jser));
       if (!aborted) return CLG_OK;
       return after_abort(pf, build, log_bytes, out, span_rec_base, need_jser);
     }
@@ -1388,8 +1288,7 @@ struct clg_engine {
     bool aborted = true, nj = false;
     if (need_jser) {
       stats["decode_jser_retry"].launches++;
-      CHK(three_pass ? run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &nj)
-                     : run_one(pf, log_bytes, out, span_rec_base, &aborted, true, &nj));
+      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &nj));
       if (!aborted) return CLG_OK;
     }
     stats["decode_fallback"].launches++;
@@ -1418,7 +1317,7 @@ struct clg_engine {
   int decode_async(std::function<void(DecodePlan&, uint32_t)> build, uint64_t log_bytes, clg_decoded* out,
                    uint64_t* span_rec_base) {
     pend.status = CLG_OK;
-    if (!(fused_decode && three_pass && log_bytes / 2 < (1ull << 31))) return decode(build, log_bytes, out, span_rec_base);
+    if (!(fused_decode && log_bytes / 2 < (1ull << 31))) return decode(build, log_bytes, out, span_rec_base);
     DecodePlan pf;
     build(pf, clg::kZTile);
     reset_result(out);
@@ -1448,7 +1347,16 @@ struct clg_engine {
     return CLG_OK;  // the decode's own status goes to clg_decode_wait
   }
 
+  // The robust pipeline; again with a grown spill arena while a Serializable stream walk
+  // found the arena full (CLG_E_NOSPACE is never a decode result).
   int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+    for (;;) {
+      CHK(run_decode_once(p, log_bytes, out, span_rec_base));
+      if (out->err_status != CLG_E_NOSPACE) return CLG_OK;
+      CHK(jarena_grow());
+    }
+  }
+  int run_decode_once(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
     reset_result(out);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     if (ns == 0) return CLG_OK;
@@ -1474,7 +1382,9 @@ struct clg_engine {
     auto* ds = d_spans.as<clg::SpanDesc>();
     auto* flags = d_flags.as<uint32_t>();
     // fast path: fused scan (points + segments) -> per-span resolution -> emit
-    const clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>()};
+    clg::JArena jar;
+    CHK(jarena_reset(&jar));
+    const clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>(), jar};
     uint32_t* dbg = nullptr;
     if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kFPoints * 4) == CLG_OK)
       dbg = d_dbg.as<uint32_t>();
@@ -1509,11 +1419,11 @@ struct clg_engine {
     }));
     // robust DP pipeline for flagged spans only (early exit elsewhere)
     CHK(timed("robust_dp_tables", 0, [&] {
-      return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), flags, stream);
+      return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), flags, jar, stream);
     }));
     CHK(timed("robust_dp_resolve", 0, [&] {
       return clg::launch_decode_resolve(dt, ds, ns, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(),
-                                        d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), flags, stream);
+                                        d_tres.as<clg::TileRes>(), d_sres.as<clg::SpanRes>(), flags, jar, stream);
     }));
     CHK(timed("robust_spanscan", uint64_t(ns) * 48, [&] {
       return clg::launch_decode_spanscan(d_sres.as<clg::SpanRes>(), ns, d_totals.as<uint64_t>(), stream);
@@ -1530,7 +1440,7 @@ struct clg_engine {
     if (cfg.flags & CLG_F_TIMING) hipEventRecord(eb, stream);
     CHK(timed("robust_dp_emit", 0, [&] {
       return clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
-                                     d_sres.as<clg::SpanRes>(), flags, o, stream);
+                                     d_sres.as<clg::SpanRes>(), flags, o, jar, stream);
     }));
     if (const char* dump = getenv("CLONOS_DEBUG_DUMP")) {  // developer diagnostics only
       std::vector<uint32_t> hc(size_t(nt) * clg::kFPoints), hf(ns);
@@ -1637,7 +1547,8 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->cfg = *cfg;
   const char* dm = getenv("CLONOS_DECODE");
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
-  e->three_pass = !(dm && !strcmp(dm, "onepass"));
+  if (const char* ja = getenv("CLONOS_JSER_ARENA"))  // initial spill arena bytes (tests: force its growth)
+    e->jarena_bytes = std::max<size_t>(256, size_t(strtoull(ja, nullptr, 0)));
   HIPCHK(hipSetDevice(cfg->device));
   HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   {
@@ -2215,6 +2126,8 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
   if (total) HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
   const uint8_t* dst = e->d_stage.as<uint8_t>();
   // subpartition buffers first (their kernels only read the staged bytes)
+  std::function<int(clg::JArena)> classify;
+  const int32_t* d_sub_status = nullptr;
   if (ns) {
     std::vector<clg::BufSpan> bs(ns);
     std::vector<clg::BufChunk> bc;
@@ -2247,7 +2160,13 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
       return clg::launch_bufsizes(reinterpret_cast<const clg::BufChunk*>(dm + o_chunks), uint32_t(bc.size()), d_spans,
                                   e->d_rsizes.as<int32_t>(), d_first, e->stream);
     }));
-    CHK(clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, e->stream));
+    clg::JArena jar;
+    CHK(e->jarena_reset(&jar));
+    CHK(clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, jar, e->stream));
+    classify = [=](clg::JArena a) {
+      return clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, a, e->stream);
+    };
+    d_sub_status = d_status;
     if (n_sizes)
       HIPCHK(hipMemcpyAsync(out->buffer_sizes, e->d_rsizes.p, n_sizes * 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(out->sub_count, d_count, ns * 8, hipMemcpyDeviceToHost, e->stream));
@@ -2260,7 +2179,17 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
     for (uint32_t i = 0; i < n; ++i) e->plan_host_span(p, dst + at[i], mains[i].len, i, T);
   };
   CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
-  return e->sync();
+  CHK(e->sync());
+  // a Serializable walk in a subpartition buffer found the spill arena full: again, larger
+  while (ns && std::find(out->sub_status, out->sub_status + ns, int32_t(CLG_E_NOSPACE)) != out->sub_status + ns) {
+    CHK(e->jarena_grow());
+    clg::JArena jar;
+    CHK(e->jarena_reset(&jar));
+    CHK(classify(jar));
+    HIPCHK(hipMemcpyAsync(out->sub_status, d_sub_status, ns * 4, hipMemcpyDeviceToHost, e->stream));
+    CHK(e->sync());
+  }
+  return CLG_OK;
 }
 
 // SimpleDeterminantEncoder.encodeTo over a batch (encode.hip): sizes pass, one host read

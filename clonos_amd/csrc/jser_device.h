@@ -1,15 +1,33 @@
-// jser_device.h -- device-side length of one Java Object Serialization stream.
+// jser_device.h -- the length of one Java Object Serialization stream, on the device.
 //
 // SERIALIZABLE determinants carry `ObjectOutputStream(...).writeObject(o)` bytes with no
 // length prefix (reference: causal/determinant/SimpleDeterminantEncoder.java:316-341);
 // decodeNext relies on ObjectInputStream consuming exactly one object.  To find the
 // record end on the GPU we walk the stream grammar (Java Object Serialization
-// Specification section 6.4) with an explicit stack -- one lane per record, bounded
-// tables.  Streams that exceed the bounds are reported as malformed (CLG_E_BAD_SERIAL).
-// Independent of the CPU oracle's recursive walker (oracle/clonos_oracle.cpp).
+// Specification section 6.4) with an explicit frame stack, one lane per stream.
+//
+// Tables.  The walk keeps a handle table, class descriptors, their field typecodes and
+// the frame stack.  A first tier lives in the lane's private memory (enough for every
+// stream the reference's own test resources hold but a few); past it each table doubles
+// into the spill arena (kernels.h JArena: bump-allocated HBM scratch).  A walk that finds
+// the arena full returns kJsSpill -- never "invalid" -- and the engine grows the arena and
+// decodes again, so no table bound rejects a valid stream.
+//
+// Limits that are semantics, not capacity (identical in both CPU restatements under
+// oracle/): object nesting deeper than kMaxDepth stands for the JVM's
+// StackOverflowError (an Error the reference's `catch (Exception e)` does not catch), a
+// class hierarchy longer than kMaxChain for a cyclic superclass chain.  A class
+// descriptor is usable only once complete (its superclass read): JDK 8's
+// ObjectStreamClass is initialised at the end of readNonProxyDesc.
+//
+// The walk is __host__ __device__ so that tests compile this very code for the CPU and
+// compare it with the oracle (tests/jser_walker_host.cpp).  Independent of the oracle's
+// recursive walker.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "kernels.h"
 
 namespace clg {
 namespace jser {
@@ -21,51 +39,98 @@ constexpr uint8_t TC_NULL = 0x70, TC_REFERENCE = 0x71, TC_CLASSDESC = 0x72, TC_O
 constexpr uint8_t SC_WRITE_METHOD = 0x01, SC_SERIALIZABLE = 0x02, SC_EXTERNALIZABLE = 0x04,
                   SC_BLOCK_DATA = 0x08;
 
-constexpr int kMaxHandles = 64, kMaxDescs = 16, kMaxFields = 128, kMaxStack = 32;
-constexpr int kMaxSteps = 1 << 16;
+constexpr int kMaxDepth = 512;  // open object() activations (oracle JWalker::object)
+constexpr int kMaxChain = 256;  // classes in one object's hierarchy
+// private first tier (entries)
+constexpr uint32_t kPrivHandles = 64, kPrivDescs = 16, kPrivFields = 128, kPrivFrames = 32;
+
+constexpr int64_t kJsInvalid = -1;  // not a stream (the record is CLG_E_BAD_SERIAL)
+constexpr int64_t kJsSpill = -2;    // the spill arena is full: grow it and decode again
 
 enum : uint8_t { K_OBJ, K_STROBJ, K_DESC, K_NEWHANDLE, K_ANNOT, K_ODATA, K_ARR };
 
 struct Desc {
-  uint8_t flags;
-  uint8_t arr;  // component typecode for array classes ("[I" -> 'I'), 0 otherwise
-  uint8_t f0;   // first field in the field table
-  uint8_t nf;
-  int8_t super;
-  uint8_t pad[3];
+  uint32_t f0, nf;  // the class's field typecodes: ftab[f0, f0 + nf)
+  int32_t super;    // superclass descriptor, -1 none
+  uint8_t flags;    // 0 until the descriptor is complete (unusable before)
+  uint8_t arr;      // component typecode of an array class ("[I" -> 'I'), 0 otherwise
+  uint8_t pad[2];
 };
 struct Frame {
   uint8_t kind, st;
-  int16_t d;
-  int32_t i, n, j;
+  uint16_t act;  // object() activations that end when this frame pops
+  int32_t d, i, n, j;
 };
 
-// F: callable returning the byte at stream offset k (k < avail), as int.
-// Returns the stream length (magic through the end of the first object) or -1.
-template <class F>
-__device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
-  if (avail < 5) return -1;
-  if (at(0) != 0xAC || at(1) != 0xED || at(2) != 0x00 || at(3) != 0x05) return -1;
-  uint64_t pos = 4;
-  int16_t handles[kMaxHandles];
-  Desc descs[kMaxDescs];
-  uint8_t ftab[kMaxFields];
-  Frame st[kMaxStack];
-  int nh = 0, nd = 0, nf = 0, sp = 0, ret = -1;
+// Spill allocator over the device arena (one atomic per table growth; rare).
+struct DevArena {
+  JArena a;
+  __device__ void* take(uint64_t bytes) const {
+    if (!a.base) return nullptr;
+    bytes = (bytes + 15) & ~15ull;
+    const uint64_t o = atomicAdd(a.used, (unsigned long long)bytes);
+    return o + bytes <= a.cap ? a.base + o : nullptr;
+  }
+};
 
-#define JS_FAIL return -1
-#define JS_NEED(k) if ((uint64_t)(k) > avail - pos) JS_FAIL
-#define JS_PUSH(kd)                      \
-  do {                                   \
-    if (sp >= kMaxStack) JS_FAIL;        \
-    st[sp].kind = (kd); st[sp].st = 0;   \
-    st[sp].d = 0; st[sp].i = st[sp].n = st[sp].j = 0; \
-    ++sp;                                \
+// Doubles table p (n == cap entries in use) into the arena.
+template <class T, class A>
+__host__ __device__ inline bool grow(const A& ar, T*& p, uint32_t& cap, uint32_t n) {
+  const uint64_t nc = 2ull * cap;
+  if (nc > (1ull << 30)) return false;
+  T* q = static_cast<T*>(ar.take(nc * sizeof(T)));
+  if (!q) return false;
+  for (uint32_t k = 0; k < n; ++k) q[k] = p[k];
+  p = q;
+  cap = uint32_t(nc);
+  return true;
+}
+
+// F: callable returning the byte at stream offset k (k < avail), as int.  A: spill
+// allocator (take(bytes) -> pointer or null).  Returns the stream length (magic through
+// the end of the first object), kJsInvalid or kJsSpill.
+template <class F, class A>
+__host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const A& ar) {
+  if (avail < 5) return kJsInvalid;
+  if (at(0) != 0xAC || at(1) != 0xED || at(2) != 0x00 || at(3) != 0x05) return kJsInvalid;
+  uint64_t pos = 4;
+  int32_t h_priv[kPrivHandles];  // handle -> descriptor index; -1 other object, -2 string
+  Desc d_priv[kPrivDescs];
+  uint8_t f_priv[kPrivFields];
+  Frame s_priv[kPrivFrames];
+  int32_t* handles = h_priv;
+  Desc* descs = d_priv;
+  uint8_t* ftab = f_priv;
+  Frame* st = s_priv;
+  uint32_t ch = kPrivHandles, cd = kPrivDescs, cf = kPrivFields, cs = kPrivFrames;
+  uint32_t nh = 0, nd = 0, nf = 0, sp = 0;
+  int od = 0;       // open object() activations
+  int32_t ret = -1;  // descriptor the last completed classDesc resolved to (-1: null)
+
+#define JS_FAIL return kJsInvalid
+#define JS_NEED(k) \
+  if ((uint64_t)(k) > avail - pos) JS_FAIL
+#define JS_PUSH(kd)                                           \
+  do {                                                        \
+    if (sp == cs && !grow(ar, st, cs, sp)) return kJsSpill;   \
+    st[sp] = Frame{(uint8_t)(kd), 0, 0, 0, 0, 0, 0};          \
+    ++sp;                                                     \
   } while (0)
-#define JS_NEWHANDLE(v)                  \
-  do {                                   \
-    if (nh >= kMaxHandles) JS_FAIL;      \
-    handles[nh++] = (int16_t)(v);        \
+#define JS_POP()           \
+  do {                     \
+    od -= st[sp - 1].act;  \
+    --sp;                  \
+  } while (0)
+#define JS_NEWHANDLE(v)                                            \
+  do {                                                             \
+    if (nh == ch && !grow(ar, handles, ch, nh)) return kJsSpill;   \
+    handles[nh++] = (int32_t)(v);                                  \
+  } while (0)
+#define JS_NEWDESC(di)                                         \
+  do {                                                         \
+    if (nd == cd && !grow(ar, descs, cd, nd)) return kJsSpill; \
+    di = (int32_t)nd++;                                        \
+    descs[di] = Desc{nf, 0, -1, 0, 0, {0, 0}};                 \
   } while (0)
 
   auto u8 = [&]() -> int { return at(pos++); };
@@ -76,12 +141,17 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
     return (int32_t)v;
   };
 
+  // Termination: every step consumes bytes, pushes a frame that will, pops, or advances a
+  // frame's bounded state (class index < chain length <= kMaxChain); no step bound needed.
   JS_PUSH(K_OBJ);
-  for (int steps = 0; sp > 0; ++steps) {
-    if (steps > kMaxSteps) JS_FAIL;
-    Frame& f = st[sp - 1];
+  while (sp > 0) {
+    Frame& f = st[sp - 1];  // not used after a push (the stack may move)
     switch (f.kind) {
       case K_OBJ: {
+        const uint32_t inh = f.act;  // activations (an enum's) that end with this object
+        --sp;                        // replaced by whatever the object needs
+        const uint32_t base = sp;
+        if (++od > kMaxDepth) JS_FAIL;
         int tc;
         for (;;) {  // readObject0 consumes leading TC_RESETs
           JS_NEED(1);
@@ -89,19 +159,18 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           if (tc != TC_RESET) break;
           nh = 0;
         }
-        --sp;  // this frame is replaced by whatever the object needs
         switch (tc) {
           case TC_NULL: break;
           case TC_REFERENCE: {
             JS_NEED(4);
-            int64_t k = (int64_t)s32() - 0x7E0000;
-            if (k < 0 || k >= nh) JS_FAIL;
+            const int64_t k = (int64_t)s32() - 0x7E0000;
+            if (k < 0 || k >= (int64_t)nh) JS_FAIL;
             break;
           }
           case TC_STRING: {
             JS_NEWHANDLE(-2);
             JS_NEED(2);
-            uint32_t l = u16();
+            const uint32_t l = u16();
             JS_NEED(l);
             pos += l;
             break;
@@ -109,8 +178,8 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           case TC_LONGSTRING: {
             JS_NEWHANDLE(-2);
             JS_NEED(8);
-            uint64_t hi = (uint32_t)s32(), lo = (uint32_t)s32();
-            uint64_t l = hi << 32 | lo;
+            const uint64_t hi = (uint32_t)s32(), lo = (uint32_t)s32();
+            const uint64_t l = hi << 32 | lo;
             if (l > avail - pos) JS_FAIL;
             pos += l;
             break;
@@ -140,35 +209,37 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           default:
             JS_FAIL;
         }
+        if (sp > base) st[base].act = (uint16_t)(inh + 1);  // the object ends when its bottom frame pops
+        else od -= (int)(inh + 1);
         break;
       }
-      case K_STROBJ: {  // className1 / enum constant: must be a String object
+      case K_STROBJ: {  // className1 / enum constant name: must be a String object
         JS_NEED(1);
-        int tc = at(pos);
+        const int tc = at(pos);
         if (tc != TC_STRING && tc != TC_LONGSTRING && tc != TC_REFERENCE) JS_FAIL;
         f.kind = K_OBJ;
         break;
       }
       case K_NEWHANDLE:
         JS_NEWHANDLE(-1);
-        --sp;
+        JS_POP();
         break;
       case K_ANNOT: {  // contents up to TC_ENDBLOCKDATA
         JS_NEED(1);
-        int tc = at(pos);
+        const int tc = at(pos);
         if (tc == TC_ENDBLOCKDATA) {
           ++pos;
-          --sp;
+          JS_POP();
         } else if (tc == TC_BLOCKDATA) {
           ++pos;
           JS_NEED(1);
-          uint32_t l = (uint32_t)u8();
+          const uint32_t l = (uint32_t)u8();
           JS_NEED(l);
           pos += l;
         } else if (tc == TC_BLOCKDATALONG) {
           ++pos;
           JS_NEED(4);
-          int32_t l = s32();
+          const int32_t l = s32();
           if (l < 0) JS_FAIL;
           JS_NEED(l);
           pos += (uint32_t)l;
@@ -177,60 +248,55 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
         }
         break;
       }
-      case K_DESC: {
+      case K_DESC: {  // d: descriptor, i/n: fields read/declared, j: flags | arr << 8
         if (f.st == 0) {
           JS_NEED(1);
-          int tc = u8();
+          const int tc = u8();
           if (tc == TC_NULL) {
             ret = -1;
-            --sp;
+            JS_POP();
           } else if (tc == TC_REFERENCE) {
             JS_NEED(4);
-            int64_t k = (int64_t)s32() - 0x7E0000;
-            if (k < 0 || k >= nh || handles[k] < 0) JS_FAIL;
+            const int64_t k = (int64_t)s32() - 0x7E0000;
+            if (k < 0 || k >= (int64_t)nh || handles[k] < 0) JS_FAIL;
             ret = handles[k];
-            --sp;
+            JS_POP();
           } else if (tc == TC_CLASSDESC) {
             JS_NEED(2);
-            uint32_t l = u16();
+            const uint32_t l = u16();
             JS_NEED(l);
-            uint8_t c0 = l > 0 ? (uint8_t)at(pos) : 0, c1 = l > 1 ? (uint8_t)at(pos + 1) : 0;
+            const uint8_t c0 = l > 0 ? (uint8_t)at(pos) : 0, c1 = l > 1 ? (uint8_t)at(pos + 1) : 0;
             pos += l;
-            JS_NEED(8 + 1 + 2);
+            JS_NEED(8);
             pos += 8;  // serialVersionUID
-            if (nd >= kMaxDescs) JS_FAIL;
-            int di = nd++;
-            JS_NEWHANDLE(di);
-            descs[di].flags = (uint8_t)u8();
-            descs[di].arr = (c0 == '[') ? c1 : 0;
-            uint32_t cnt = u16();
-            if (nf + cnt > (uint32_t)kMaxFields) JS_FAIL;
-            descs[di].f0 = (uint8_t)nf;
-            descs[di].nf = (uint8_t)cnt;
-            descs[di].super = -1;
-            f.d = (int16_t)di;
+            int32_t di;
+            JS_NEWDESC(di);
+            JS_NEWHANDLE(di);  // assigned before classDescInfo (ObjectInputStream.readNonProxyDesc)
+            JS_NEED(1);
+            const uint32_t flags = (uint32_t)u8();
+            JS_NEED(2);
+            const uint32_t cnt = u16();
+            f.d = di;
             f.i = 0;
             f.n = (int32_t)cnt;
+            f.j = (int32_t)(flags | (c0 == '[' ? (uint32_t)c1 : 0u) << 8);
             f.st = 1;
           } else if (tc == TC_PROXYCLASSDESC) {
-            if (nd >= kMaxDescs) JS_FAIL;
-            int di = nd++;
+            int32_t di;
+            JS_NEWDESC(di);
             JS_NEWHANDLE(di);
-            descs[di].flags = SC_SERIALIZABLE;
-            descs[di].arr = 0;
-            descs[di].f0 = (uint8_t)nf;
-            descs[di].nf = 0;
-            descs[di].super = -1;
             JS_NEED(4);
-            int32_t cnt = s32();
+            const int32_t cnt = s32();
             if (cnt < 0) JS_FAIL;
             for (int32_t k = 0; k < cnt; ++k) {
               JS_NEED(2);
-              uint32_t l = u16();
+              const uint32_t l = u16();
               JS_NEED(l);
               pos += l;
             }
-            f.d = (int16_t)di;
+            f.d = di;
+            f.n = 0;
+            f.j = SC_SERIALIZABLE;
             f.st = 2;
             JS_PUSH(K_ANNOT);
           } else {
@@ -238,45 +304,52 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           }
         } else if (f.st == 1) {  // field descriptors
           if (f.i < f.n) {
-            JS_NEED(3);
-            int t = u8();
-            uint32_t l = u16();
+            JS_NEED(1);
+            const int t = u8();
+            JS_NEED(2);
+            const uint32_t l = u16();
             JS_NEED(l);
             pos += l;  // field name
+            const bool obj = t == 'L' || t == '[';
+            if (!obj && !(t == 'B' || t == 'C' || t == 'D' || t == 'F' || t == 'I' || t == 'J' || t == 'S' || t == 'Z'))
+              JS_FAIL;
+            if (nf == cf && !grow(ar, ftab, cf, nf)) return kJsSpill;
             ftab[nf++] = (uint8_t)t;
             f.i++;
-            if (t == 'L' || t == '[') {
-              JS_PUSH(K_STROBJ);
-            } else if (!(t == 'B' || t == 'C' || t == 'D' || t == 'F' || t == 'I' || t == 'J' || t == 'S' || t == 'Z')) {
-              JS_FAIL;
-            }
+            if (obj) JS_PUSH(K_STROBJ);
           } else {
+            descs[f.d].f0 = nf - (uint32_t)f.n;  // className1 strings add no fields: contiguous
+            descs[f.d].nf = (uint32_t)f.n;
             f.st = 2;
             JS_PUSH(K_ANNOT);  // classAnnotation
           }
         } else if (f.st == 2) {
           f.st = 3;
           JS_PUSH(K_DESC);  // superClassDesc
-        } else {
-          descs[f.d].super = (int8_t)ret;
+        } else {  // complete: usable from now on
+          Desc& dd = descs[f.d];
+          dd.super = ret;
+          dd.flags = (uint8_t)(f.j & 0xFF);
+          dd.arr = (uint8_t)((uint32_t)f.j >> 8);
           ret = f.d;
-          --sp;
+          JS_POP();
         }
         break;
       }
-      case K_ODATA: {
+      case K_ODATA: {  // d: class, n: hierarchy length, i: class (top-most first), j: field
         if (f.st == 0) {
           if (ret < 0) JS_FAIL;
           JS_NEWHANDLE(-1);
-          f.d = (int16_t)ret;
+          f.d = ret;
           int n = 0;
-          for (int c = ret; c >= 0; c = descs[c].super)
-            if (++n > kMaxDescs) JS_FAIL;
-          f.n = n;  // chain length
-          f.i = 0;  // class index counted from the top-most superclass
-          f.j = 0;  // field index within the class
-          if (descs[f.d].flags & SC_EXTERNALIZABLE) {
-            if (!(descs[f.d].flags & SC_BLOCK_DATA)) JS_FAIL;  // protocol-1 externalizable
+          for (int32_t c = ret; c >= 0; c = descs[c].super)
+            if (++n > kMaxChain) JS_FAIL;
+          f.n = n;
+          f.i = 0;
+          f.j = 0;
+          const uint8_t fl = descs[f.d].flags;
+          if (fl & SC_EXTERNALIZABLE) {
+            if (!(fl & SC_BLOCK_DATA)) JS_FAIL;  // protocol-1 externalizable: length unknowable
             f.st = 2;
             JS_PUSH(K_ANNOT);
           } else {
@@ -284,27 +357,21 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           }
         } else if (f.st == 1) {
           if (f.i >= f.n) {
-            --sp;
+            JS_POP();
             break;
           }
-          int c = f.d;
+          int32_t c = f.d;
           for (int k = 0; k < f.n - 1 - f.i; ++k) c = descs[c].super;
-          const Desc& dc = descs[c];
+          const Desc dc = descs[c];
           if (!(dc.flags & SC_SERIALIZABLE)) JS_FAIL;
-          if (f.j < dc.nf) {
-            int t = ftab[dc.f0 + f.j];
+          if ((uint32_t)f.j < dc.nf) {
+            const int t = ftab[dc.f0 + (uint32_t)f.j];
             f.j++;
-            int sz = 0;
-            switch (t) {
-              case 'B': case 'Z': sz = 1; break;
-              case 'C': case 'S': sz = 2; break;
-              case 'I': case 'F': sz = 4; break;
-              case 'J': case 'D': sz = 8; break;
-              default: sz = -1; break;
-            }
-            if (sz > 0) {
+            const int sz = (t == 'B' || t == 'Z') ? 1 : (t == 'C' || t == 'S') ? 2 : (t == 'I' || t == 'F') ? 4
+                           : (t == 'J' || t == 'D') ? 8 : 0;
+            if (sz) {
               JS_NEED(sz);
-              pos += sz;
+              pos += (uint64_t)sz;
             } else {
               JS_PUSH(K_OBJ);
             }
@@ -314,7 +381,7 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
             if (dc.flags & SC_WRITE_METHOD) JS_PUSH(K_ANNOT);  // custom data up to TC_ENDBLOCKDATA
           }
         } else {
-          --sp;
+          JS_POP();
         }
         break;
       }
@@ -323,7 +390,7 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
           if (ret < 0) JS_FAIL;
           JS_NEWHANDLE(-1);
           JS_NEED(4);
-          int32_t size = s32();
+          const int32_t size = s32();
           if (size < 0) JS_FAIL;
           int es;
           switch (descs[ret].arr) {
@@ -335,10 +402,10 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
             default: JS_FAIL;
           }
           if (es) {
-            uint64_t b = (uint64_t)(uint32_t)size * (uint64_t)es;
+            const uint64_t b = (uint64_t)(uint32_t)size * (uint64_t)es;
             if (b > avail - pos) JS_FAIL;
             pos += b;
-            --sp;
+            JS_POP();
           } else {
             f.i = 0;
             f.n = size;
@@ -349,7 +416,7 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
             f.i++;
             JS_PUSH(K_OBJ);
           } else {
-            --sp;
+            JS_POP();
           }
         }
         break;
@@ -361,7 +428,9 @@ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail) {
 #undef JS_FAIL
 #undef JS_NEED
 #undef JS_PUSH
+#undef JS_POP
 #undef JS_NEWHANDLE
+#undef JS_NEWDESC
   return (int64_t)pos;
 }
 

@@ -130,6 +130,17 @@ struct FastRes {
   uint64_t wide_base;
 };
 
+// Device scratch the Serializable stream walker (jser_device.h) spills its handle, class
+// descriptor, field and frame tables to once a stream outgrows the walker's private
+// first tier.  Bump-allocated (*used reset before each decode); a walk that finds it
+// full reports kJsSpill and the engine grows the arena and decodes again, so no table
+// bound ever rejects a valid stream.
+struct JArena {
+  uint8_t* base;
+  uint64_t cap;
+  unsigned long long* used;
+};
+
 constexpr int kCands = 32;     // candidate entries per region (covers every fixed-layout record)
 constexpr int kJserCap = 256;  // Serializable stream-length table entries per tile
 
@@ -141,6 +152,7 @@ struct JserTabs {
   uint32_t* len;
   uint32_t* n;
   uint32_t* defer;
+  JArena ar;
 };
 
 // Fused convergence + segment pass.  mode 0: every tile (tiles meeting a Serializable
@@ -185,19 +197,9 @@ struct FusedCtl {
   uint32_t jser;
   uint32_t jwork_cap;  // capacity of the general-walker work list
   uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
-  // one-pass kernel (k_decode_one): tiles taken in order from a ticket; per tile a
-  // look-back word flag<<62 | wide<<32 | records (flag 1: the tile's own counts, 2: the
-  // inclusive prefix); cnt[t] = the tile's own counts in the same packing
-  uint32_t* ticket;
-  uint64_t* look;   // per tile
-  uint64_t* glook;  // per group of kZGroup tiles: flag<<62 | the group's counts / inclusive prefix
   uint32_t warm;    // speculative warm-up bytes before each region
+  JArena jar;       // the stream walker's spill arena (k_decode_jser_general)
 };
-constexpr uint32_t kZGroup = 64;
-constexpr uint64_t kZLookAgg = 1ull << 62, kZLookInc = 2ull << 62, kZLookVal = (1ull << 62) - 1;
-// one-pass decode: kernel (phase 0) then span ranges (phase 1) from the look-back words
-int launch_decode_one(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                      FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
 // 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
@@ -252,14 +254,14 @@ int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void*
 // Robust pipeline (per-byte DP transfer tables); runs only on spans whose flag is set
 // (d_span_flags == nullptr: all spans).
 int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
-                         uint64_t* d_agg, TileConv* d_conv, const uint32_t* d_span_flags, void* stream);
+                         uint64_t* d_agg, TileConv* d_conv, const uint32_t* d_span_flags, JArena ar, void* stream);
 int launch_decode_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                           const uint64_t* d_agg, const TileConv* d_conv, TileRes* d_tres,
-                          SpanRes* d_sres, const uint32_t* d_span_flags, void* stream);
+                          SpanRes* d_sres, const uint32_t* d_span_flags, JArena ar, void* stream);
 int launch_decode_spanscan(SpanRes* d_sres, uint32_t n_spans, uint64_t* d_totals, void* stream);
 int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,
                        const TileConv* d_conv, const TileRes* d_tres, const SpanRes* d_sres,
-                       const uint32_t* d_span_flags, DecodeOut out, void* stream);
+                       const uint32_t* d_span_flags, DecodeOut out, JArena ar, void* stream);
 
 
 // ---- batched encode (encode.hip) -------------------------------------------------
@@ -300,6 +302,6 @@ int launch_bufsizes(const BufChunk* d_chunks, uint32_t n_chunks, const BufSpan* 
 // record first_bad (decodeNext's error, or CLG_E_NOT_BUFFER_BUILT for a valid other record).
 int launch_bufsizes_classify(const BufSpan* d_spans, uint32_t n_spans, const uint64_t* d_first_bad,
                              uint64_t* d_count, int32_t* d_status, int64_t* d_err_off, int32_t* d_err_tag,
-                             void* stream);
+                             JArena ar, void* stream);
 
 }  // namespace clg

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict_
 // ==================================================================================
 __global__ __launch_bounds__(64) void k_dec_tables(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                    uint64_t* __restrict__ agg, TileConv* __restrict__ conv,
-                                                   const uint32_t* __restrict__ span_flags) {
+                                                   const uint32_t* __restrict__ span_flags, JArena ar) {
   __shared__ uint32_t s_tile[kImageDwords];
   __shared__ uint32_t s_ring[kEntries * 64];  // [position mod 64][lane]
   __shared__ uint32_t s_conv_lane[kRegions];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(64) void k_dec_tables(const TileDesc* __restrict__ 
   const TileDesc td = tiles[t];
   if (span_flags && !span_flags[td.span]) return;
   const SpanDesc sd = spans[td.span];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, ar};
   stage_tile(s_tile, td, sr, lane);
 
   const TileGeom g{td.delta, td.delta + td.len};
@@ -312,9 +312,9 @@ constexpr int kResolveChunk = 96;  // tiles cached in LDS per step (96*64*8 = 48
 // Uses convergence info to short-cut once the path meets the shared path.
 __device__ int tile_eval_concrete(const TileDesc* tiles, const SpanDesc& sd, uint32_t t, const TileConv& cv,
                                   uint32_t e, uint32_t* exit_rel, uint32_t* cnt, uint32_t* wcnt, int64_t* err_off,
-                                  int* err_tag, uint32_t* limit) {
+                                  int* err_tag, uint32_t* limit, JArena ar) {
   const TileDesc td = tiles[t];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, ar};
   const uint32_t lo = td.delta, hi = td.delta + td.len;
   uint32_t a = lo + e;
   uint32_t c = 0, w = 0;
@@ -359,7 +359,7 @@ __device__ int tile_eval_concrete(const TileDesc* tiles, const SpanDesc& sd, uin
 __global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      const uint64_t* __restrict__ agg, const TileConv* __restrict__ conv,
                                                      TileRes* __restrict__ tres, SpanRes* __restrict__ sres,
-                                                     const uint32_t* __restrict__ span_flags) {
+                                                     const uint32_t* __restrict__ span_flags, JArena ar) {
   __shared__ uint64_t s_agg[kResolveChunk * kEntries];
   __shared__ uint32_t s_len[kResolveChunk];
   __shared__ uint64_t s_state[4];  // entry, rec, wide, done
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict_
         uint32_t c, w;
         if (xr == kExitErr || xr == kExitFar) {
           uint32_t lim;
-          const int st = tile_eval_concrete(tiles, sd, t, conv[t], (uint32_t)e, &xr, &c, &w, &err_off, &err_tag, &lim);
+          const int st = tile_eval_concrete(tiles, sd, t, conv[t], (uint32_t)e, &xr, &c, &w, &err_off, &err_tag, &lim, ar);
           r.limit = lim;
           if (st != CLG_OK) {
             status = st;
@@ -556,7 +556,7 @@ __device__ __forceinline__ int decode_at(const uint32_t* T, SpanReader* sr, uint
 __global__ __launch_bounds__(64) void k_dec_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                  const TileConv* __restrict__ conv, const TileRes* __restrict__ tres,
                                                  const SpanRes* __restrict__ sres, const uint32_t* __restrict__ span_flags,
-                                                 DecodeOut out) {
+                                                 DecodeOut out, JArena ar) {
   __shared__ uint32_t s_tile[kImageDwords];
   __shared__ uint32_t s_entry[kRegions];
   __shared__ uint16_t s_ce[kRegions];
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(64) void k_dec_emit(const TileDesc* __restrict__ ti
   if (tr.entry >= td.len) return;  // no record starts in this tile (uniform)
   const SpanDesc sd = spans[td.span];
   const SpanRes sp = sres[td.span];
-  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len};
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, ar};
   stage_tile(s_tile, td, sr, lane);
 
   const TileGeom g{td.delta, td.delta + td.len};
@@ -716,19 +716,19 @@ int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void*
 }
 
 int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint64_t* d_agg,
-                         TileConv* d_conv, const uint32_t* d_span_flags, void* stream) {
+                         TileConv* d_conv, const uint32_t* d_span_flags, JArena ar, void* stream) {
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_dec_tables, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_agg, d_conv,
-                     d_span_flags);
+                     d_span_flags, ar);
   return ok(hipGetLastError());
 }
 
 int launch_decode_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, const uint64_t* d_agg,
                           const TileConv* d_conv, TileRes* d_tres, SpanRes* d_sres, const uint32_t* d_span_flags,
-                          void* stream) {
+                          JArena ar, void* stream) {
   if (!n_spans) return CLG_OK;
   hipLaunchKernelGGL(k_dec_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_agg, d_conv,
-                     d_tres, d_sres, d_span_flags);
+                     d_tres, d_sres, d_span_flags, ar);
   return ok(hipGetLastError());
 }
 
@@ -739,10 +739,10 @@ int launch_decode_spanscan(SpanRes* d_sres, uint32_t n_spans, uint64_t* d_totals
 
 int launch_decode_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const TileConv* d_conv,
                        const TileRes* d_tres, const SpanRes* d_sres, const uint32_t* d_span_flags, DecodeOut out,
-                       void* stream) {
+                       JArena ar, void* stream) {
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_dec_emit, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_tres,
-                     d_sres, d_span_flags, out);
+                     d_sres, d_span_flags, out, ar);
   return ok(hipGetLastError());
 }
 

@@ -41,13 +41,15 @@ __global__ __launch_bounds__(kBufThreads) void k_bufsizes(const BufChunk* __rest
 struct GBytes {  // bytes of a record start through the span end
   const uint8_t* p;
   uint64_t n;
+  JArena ar;
   __device__ __forceinline__ int operator()(uint64_t k) const { return k < n ? (int)p[k] : 0; }
+  __device__ __forceinline__ JArena arena() const { return ar; }
 };
 
 __global__ void k_bufsizes_classify(const BufSpan* __restrict__ spans, uint32_t n_spans,
                                     const uint64_t* __restrict__ first_bad, uint64_t* __restrict__ count,
                                     int32_t* __restrict__ status, int64_t* __restrict__ err_off,
-                                    int32_t* __restrict__ err_tag) {
+                                    int32_t* __restrict__ err_tag, JArena ar) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_spans) return;
   const BufSpan s = spans[i];
@@ -62,7 +64,7 @@ __global__ void k_bufsizes_classify(const BufSpan* __restrict__ spans, uint32_t 
   }
   const uint64_t p = 5 * k;
   count[i] = k;
-  GBytes b{s.src + p, s.len - p};
+  GBytes b{s.src + p, s.len - p, ar};
   const int tag = (int8_t)s.src[p];
   err_off[i] = (int64_t)p;
   err_tag[i] = tag;
@@ -81,10 +83,10 @@ int launch_bufsizes(const BufChunk* d_chunks, uint32_t n_chunks, const BufSpan* 
 
 int launch_bufsizes_classify(const BufSpan* d_spans, uint32_t n_spans, const uint64_t* d_first_bad,
                              uint64_t* d_count, int32_t* d_status, int64_t* d_err_off, int32_t* d_err_tag,
-                             void* stream) {
+                             JArena ar, void* stream) {
   if (!n_spans) return CLG_OK;
   hipLaunchKernelGGL(k_bufsizes_classify, dim3((n_spans + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_spans,
-                     n_spans, d_first_bad, d_count, d_status, d_err_off, d_err_tag);
+                     n_spans, d_first_bad, d_count, d_status, d_err_off, d_err_tag, ar);
   return launch_status(hipGetLastError());
 }
 

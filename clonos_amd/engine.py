@@ -120,7 +120,7 @@ class Engine:
                  sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto",
                  async_slice: bool = False, ifl_segment_bytes: Optional[int] = None,
                  ifl_pool_segments: Optional[int] = None, host_tail_bytes: Optional[int] = None):
-        """decode: "auto" = single-pass fused kernel, robust multi-pass pipeline on abort;
+        """decode: "auto" = fast three-pass decode, robust multi-pass pipeline on abort;
         "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
         slices return once queued on the gather stream (CLG_F_ASYNC_SLICE); sync() before
         reading them.  ifl_*: the in-flight log's own pool (default: the same geometry as the

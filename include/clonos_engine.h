@@ -18,8 +18,11 @@
  * offsets, consumer offsets, visible writer index) lives in the host engine and is
  * updated with exactly the reference's semantics.  Outputs go to caller-allocated
  * buffers, either host (CLG_MEM_HOST) or device (CLG_MEM_DEVICE, a hipMalloc'd pointer
- * on the engine's device).  Entry points are safe to call from any thread: the engine
- * serialises on one mutex and issues all GPU work on one HIP stream.
+ * on the engine's device).  Entry points are safe to call from any thread.  Per-log calls
+ * (append, hasDelta, offset, a slice served from the host tail, logLength, a host-input
+ * upstream delta) take only their log's lock stripe; GPU and multi-log calls take the
+ * engine lock and every stripe.  GPU work runs on the engine stream, apart from device
+ * slices with CLG_F_ASYNC_SLICE, which run on a second (gather) stream.
  */
 #ifndef CLONOS_ENGINE_H
 #define CLONOS_ENGINE_H
@@ -100,7 +103,7 @@ typedef struct clg_config {
 } clg_config;
 
 #define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
-#define CLG_F_ROBUST_DECODE 2u /* skip the single-pass decode kernel; always use the robust
+#define CLG_F_ROBUST_DECODE 2u /* skip the fast three-pass decode; always use the robust
                                   multi-pass pipeline (the fallback the fused kernel aborts to) */
 #define CLG_F_ASYNC_SLICE 4u   /* slices into device memory (clg_slice_batch, CLG_MEM_DEVICE)
                                   return once queued on the engine's gather stream and overlap

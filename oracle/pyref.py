@@ -13,6 +13,7 @@ Restates (R/ = /root/reference/flink-runtime/src/main/java/org/apache/flink/runt
 from __future__ import annotations
 
 import struct
+import sys
 from typing import Dict, List, Optional, Tuple
 
 OK, E_CORRUPT_TAG, E_TRUNCATED, E_BAD_ENUM, E_NEG_LEN, E_BAD_SERIAL = 0, -2, -3, -4, -5, -6
@@ -28,10 +29,15 @@ class DecodeError(Exception):
 # --------------------------------------------------------------------------------------
 # Java serialization stream length (recursive descent; independent of the C++ walker)
 # --------------------------------------------------------------------------------------
+MAX_DEPTH = 512  # open obj() calls: the JVM's StackOverflowError, which the reference does not catch
+MAX_CHAIN = 256  # classes in one object's hierarchy (longer: a cyclic superclass chain)
+
+
 class _J:
     def __init__(self, b: bytes):
         self.b, self.p = b, 0
         self.handles: List[object] = []
+        self.depth = 0
 
     def take(self, n):
         if self.p + n > len(self.b):
@@ -70,8 +76,11 @@ class _J:
         if tc == 0x72:
             name = self.utf()
             self.take(8)
+            # the handle is assigned before classDescInfo, but the descriptor is usable only
+            # once complete (JDK 8 initialises ObjectStreamClass at the end of readNonProxyDesc)
+            slot = {"name": b"", "flags": 0, "fields": [], "super": None}
+            self.handles.append(slot)
             d = {"name": name, "flags": 0, "fields": [], "super": None}
-            self.handles.append(d)
             d["flags"] = self.u8()
             for _ in range(self.u16()):
                 t = chr(self.u8())
@@ -85,10 +94,12 @@ class _J:
                 d["fields"].append(t)
             self.annotation()
             d["super"] = self.class_desc()
-            return d
+            slot.update(d)
+            return slot
         if tc == 0x7D:
+            slot = {"name": b"", "flags": 0, "fields": [], "super": None}
+            self.handles.append(slot)
             d = {"name": b"<proxy>", "flags": 2, "fields": [], "super": None}
-            self.handles.append(d)
             n = self.s32()
             if n < 0:
                 raise ValueError("proxy")
@@ -96,7 +107,8 @@ class _J:
                 self.utf()
             self.annotation()
             d["super"] = self.class_desc()
-            return d
+            slot.update(d)
+            return slot
         raise ValueError("classDesc tc")
 
     def annotation(self):
@@ -126,6 +138,15 @@ class _J:
                 self.obj()
 
     def obj(self):
+        self.depth += 1
+        try:
+            if self.depth > MAX_DEPTH:
+                raise ValueError("depth")
+            self._obj()
+        finally:
+            self.depth -= 1
+
+    def _obj(self):
         tc = self.u8()
         while tc == 0x79:
             self.handles = []
@@ -189,6 +210,8 @@ class _J:
             c = d
             while c is not None:
                 chain.append(c)
+                if len(chain) > MAX_CHAIN:
+                    raise ValueError("hierarchy")
                 c = c["super"]
             if d["flags"] & 0x04:
                 if not d["flags"] & 0x08:
@@ -210,10 +233,14 @@ def jser_len(b: bytes) -> Optional[int]:
         return None
     j = _J(b)
     j.p = 4
+    lim = sys.getrecursionlimit()
+    sys.setrecursionlimit(max(lim, 8 * MAX_DEPTH + 1000))  # a few Python frames per obj()
     try:
         j.obj()
-    except (ValueError, IndexError, struct.error, RecursionError):
+    except (ValueError, IndexError, struct.error):
         return None
+    finally:
+        sys.setrecursionlimit(lim)
     return j.p
 
 

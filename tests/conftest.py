@@ -28,7 +28,7 @@ def have_gpu():
 @pytest.fixture(params=["auto", "robust"])
 def engine(request):
     """A fresh engine on cuda:0 with small segments (exercise segment boundaries), once
-    with the single-pass fused decode (robust pipeline on abort) and once robust-only."""
+    with the fast three-pass decode (robust pipeline on abort) and once robust-only."""
     from clonos_amd import Engine
     e = Engine(segment_bytes=256, pool_segments=1 << 16, timing=True, decode=request.param)
     yield e
