@@ -363,6 +363,7 @@ struct clg_engine {
   // Grown (doubled) whenever a decode reports CLG_E_NOSPACE, i.e. a walk found it full.
   DevBuf d_jarena;
   size_t jarena_bytes = size_t(16) << 20;
+  PinBuf h_jused;  // read-backs of the arena's bump counter: [0] decode, [1] replay classification
   // Slices into device memory run on their own stream, overlapping the next decode: the
   // gather only reads log segments, so every pool write (flush / upstream scatter) and
   // every full sync first waits for it (gwait).
@@ -437,6 +438,20 @@ struct clg_engine {
     *a = clg::JArena{d_jarena.as<uint8_t>() + 256, jarena_bytes, d_jarena.as<unsigned long long>()};
     return CLG_OK;
   }
+  // Queues a read-back of the arena's bump counter into slot k, after the walks queued so
+  // far; jarena_spilled(k) (after a sync) says whether any of them found the arena full --
+  // then some walk returned kJsSpill and whatever the kernels derived from it is void.
+  int jarena_note(int k) {
+    CHK(h_jused.ensure(64));
+    HIPCHK(hipMemcpyAsync(h_jused.as<uint64_t>() + k, d_jarena.p, 8, hipMemcpyDeviceToHost, stream));
+    return CLG_OK;
+  }
+  int jarena_clear_note(int k) {
+    CHK(h_jused.ensure(64));
+    h_jused.as<uint64_t>()[k] = 0;
+    return CLG_OK;
+  }
+  bool jarena_spilled(int k) const { return h_jused.p && h_jused.as<uint64_t>()[k] > jarena_bytes; }
   int jarena_grow() {
     CHK(sync());  // kernels still using the old arena
     if (jarena_bytes >= (size_t(1) << 36))
@@ -1185,6 +1200,7 @@ struct clg_engine {
       // read the span ranges and abort words (emit ran right behind the scan: it returns at
       // once when the batch aborted, and its stores are bounded by the output capacity)
       HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+      if (jser) CHK(jarena_note(0));
       return CLG_OK;
     };
     hipEvent_t ev[8] = {};
@@ -1222,7 +1238,9 @@ struct clg_engine {
     }
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
-    if (hab[0]) {
+    const bool spilled = jser && jarena_spilled(0);  // a stream walk found the spill arena full
+    if (spilled) CHK(jarena_grow());
+    if (hab[0] || spilled) {
       if (ea) {
         ev_pool.push_back(ea);
         ev_pool.push_back(eb);
@@ -1230,7 +1248,7 @@ struct clg_engine {
       *aborted = true;
       // Serializable records were met without tables: other aborts may be consequences
       // (entries guessed across them), so the tables decide; a second abort goes robust
-      *need_jser = !jser && hab[5];
+      *need_jser = !jser && hab[5] && !spilled;
       if (getenv("CLONOS_FUSED_DEBUG"))
         fprintf(stderr, "[clonos] fused decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d exit=%d "
                 "timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]), int(~hab[3]),
@@ -1351,8 +1369,9 @@ struct clg_engine {
   // found the arena full (CLG_E_NOSPACE is never a decode result).
   int run_decode(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
     for (;;) {
-      CHK(run_decode_once(p, log_bytes, out, span_rec_base));
-      if (out->err_status != CLG_E_NOSPACE) return CLG_OK;
+      CHK(jarena_clear_note(0));
+      const int st = run_decode_once(p, log_bytes, out, span_rec_base);
+      if (!jarena_spilled(0)) return st;
       CHK(jarena_grow());
     }
   }
@@ -1466,6 +1485,7 @@ struct clg_engine {
     }
     clg::SpanRes* hres = h_sres.as<clg::SpanRes>();
     HIPCHK(hipMemcpyAsync(hres, d_sres.p, ns * sizeof(clg::SpanRes), hipMemcpyDeviceToHost, stream));
+    CHK(jarena_note(0));
     HIPCHK(hipStreamSynchronize(stream));
     uint64_t nrec = 0, nwide = 0;
     for (uint32_t s = 0; s < ns; ++s) {
@@ -2163,6 +2183,8 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
     clg::JArena jar;
     CHK(e->jarena_reset(&jar));
     CHK(clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, jar, e->stream));
+    CHK(e->jarena_clear_note(1));
+    CHK(e->jarena_note(1));
     classify = [=](clg::JArena a) {
       return clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, a, e->stream);
     };
@@ -2181,11 +2203,12 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
   CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
   CHK(e->sync());
   // a Serializable walk in a subpartition buffer found the spill arena full: again, larger
-  while (ns && std::find(out->sub_status, out->sub_status + ns, int32_t(CLG_E_NOSPACE)) != out->sub_status + ns) {
+  while (ns && e->jarena_spilled(1)) {
     CHK(e->jarena_grow());
     clg::JArena jar;
     CHK(e->jarena_reset(&jar));
     CHK(classify(jar));
+    CHK(e->jarena_note(1));
     HIPCHK(hipMemcpyAsync(out->sub_status, d_sub_status, ns * 4, hipMemcpyDeviceToHost, e->stream));
     CHK(e->sync());
   }

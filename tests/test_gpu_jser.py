@@ -4,7 +4,7 @@ Every stream of tests/golden/jser_reference.json (199 distinct ObjectOutputStrea
 the reference's test resources hold behind a TypeSerializerSerializationUtil length
 prefix; tests/test_jser_reference.py pins the oracle and the walker source to those
 lengths on the CPU) becomes a `03`-tagged record (SimpleDeterminantEncoder.java:316-323)
-inside config-3-style logs: inline between other records, crossing the fast decode's
+inside logs of every other tag: inline between other records, crossing the fast decode's
 8 KiB tiles, the robust pipeline's 16 KiB tiles and 256-byte HBM segments.  Each log is
 decoded through the fast three-pass path and the robust pipeline and compared with the
 CPU oracle word for word; with a tiny initial spill arena the engine must grow it
@@ -32,16 +32,14 @@ RECS = [b"\x03" + bytes.fromhex(x["hex"]) for x in FIX]
 
 
 def _log_with_streams(rng, recs, filler_per_gap=(0, 400)):
-    """Config-3 records with the given Serializable records spliced in between them."""
+    """Records of every other tag with the given Serializable records spliced in between."""
     parts = []
     for r in recs:
         n = int(rng.integers(*filler_per_gap))
         if n:
-            b, _ = synth.config3_epoch(n, rng)
-            parts.append(b.tobytes())
+            parts.append(synth.random_log(n, rng, allow_serializable=False))
         parts.append(r)
-    b, _ = synth.config3_epoch(int(rng.integers(1, 300)), rng)
-    parts.append(b.tobytes())
+    parts.append(synth.random_log(int(rng.integers(1, 300)), rng, allow_serializable=False))
     return b"".join(parts)
 
 
