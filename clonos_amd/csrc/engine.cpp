@@ -1328,6 +1328,7 @@ struct clg_engine {
     clg_decoded* out = nullptr;
     uint64_t* span_rec_base = nullptr;
     std::function<void(DecodePlan&, uint32_t)> build;
+    bool unwaited = false;  // queued by clg_decode_logs_async, status not yet taken by clg_decode_wait
     int status = CLG_OK;  // result of the last settled decode, for clg_decode_wait
     std::string err;      // and its error text
   } pend;
@@ -1344,6 +1345,7 @@ struct clg_engine {
     FusedRun r;
     CHK(launch_fused(pf, log_bytes, out, jser_hint, &r));
     pend.active = true;
+    pend.unwaited = true;
     pend.plan = std::move(pf);
     pend.run = r;
     pend.out = out;
@@ -1610,6 +1612,7 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
 void clg_engine_destroy(clg_engine* e) {
   if (!e) return;
   hipSetDevice(e->cfg.device);
+  e->settle();  // a pending asynchronous decode: its events go back to the pool
   hipStreamSynchronize(e->stream);
   e->gwait();
   for (auto& t : e->timings) {
@@ -2026,6 +2029,9 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
                           clg_decoded* out, uint64_t* span_rec_base) {
   ENGINE_GUARD(e);
   if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
+  // one decode per wait: a second one would overwrite the first one's status
+  if (e->pend.unwaited)
+    return fail(CLG_E_STATE, "the previous asynchronous decode was not waited for (clg_decode_wait)");
   CHK(e->flush());
   std::vector<uint32_t> hs(log, log + n);
   std::vector<int32_t> st(n), nb(n);
@@ -2049,6 +2055,7 @@ int clg_decode_wait(clg_engine* e) {
   e->settle();
   const int st = e->pend.status;
   e->pend.status = CLG_OK;
+  e->pend.unwaited = false;
   return st == CLG_OK ? CLG_OK : fail(st, "%s", e->pend.err.c_str());
 }
 

@@ -149,7 +149,9 @@ int clg_log_find(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint3
 /* The CausalLogID and job of an open log (e.g. one clg_process_delta opened). */
 int clg_log_get_id(clg_engine* e, uint32_t log, clg_causal_log_id* id, uint32_t* job);
 /* appendDeterminant :158-177.  `rec` holds ONE encoded determinant (encodeTo bytes;
- * n == getEncodedSizeInBytes).  Staged on the host, flushed to HBM in batches. */
+ * n == getEncodedSizeInBytes).  Staged on the host, flushed to HBM in batches.  When the
+ * append crosses the log's staging bound it also flushes; CLG_E_DEVICE from that flush
+ * means the record WAS logged (staged) and only the write-behind failed. */
 int clg_append(clg_engine* e, uint32_t log, int64_t epoch, const uint8_t* rec, uint32_t n);
 /* Many appends at once: rec i = bytes[off[i], off[i]+len[i]) for log[i] in epoch[i]. */
 int clg_append_batch(clg_engine* e, const uint32_t* log, const int64_t* epoch, const uint64_t* off,
@@ -282,6 +284,9 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
  * device memory with CLG_F_ASYNC_SLICE and the consumer seeks leave it pending. */
 int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
                           clg_decoded* out, uint64_t* span_rec_base);
+/* Completes the pending decode and returns ITS status.  One asynchronous decode at a time:
+ * clg_decode_logs_async before the previous one was waited for is CLG_E_STATE (so no
+ * decode's error is ever overwritten by the next one's). */
 int clg_decode_wait(clg_engine* e);
 
 /* ---- replay-prep (DeterminantResponseEvent.merge + LogReplayer decode) ----------------

@@ -33,6 +33,11 @@ public class EngineInFlightLog implements InFlightLog {
 	private final long[] stagedEpochs = new long[STAGE_BUFFERS];
 	private final int[] stagedLens = new int[STAGE_BUFFERS];
 	private int staged;
+	// a batch is being handed to the engine (the staged arrays, or one large buffer): it may
+	// wait for pool space (backpressure, wait() releases the monitor), and meanwhile no other
+	// thread touches the stage or submits, so buffers reach the engine once and in log() order
+	private boolean submitting;
+	private boolean closed;
 
 	public EngineInFlightLog(ClonosEngine engine) {
 		this.engine = engine;
@@ -48,6 +53,7 @@ public class EngineInFlightLog implements InFlightLog {
 
 	@Override
 	public synchronized void log(Buffer buffer, long epochID, boolean isFinished) { // :44-48
+		awaitNoSubmit();
 		ByteBuffer nio = buffer.getNioBufferReadable();
 		int n = nio.remaining();
 		if (n > stage.remaining() || staged == STAGE_BUFFERS) {
@@ -55,7 +61,7 @@ public class EngineInFlightLog implements InFlightLog {
 		}
 		if (n > STAGE_BYTES) { // larger than the stage: a batch of its own
 			ByteBuffer direct = nio.isDirect() ? nio.slice() : ByteBuffer.allocateDirect(n).put(nio.duplicate());
-			logBatch(new long[]{epochID}, new int[]{n}, direct, 1);
+			submit(new long[]{epochID}, new int[]{n}, direct, 1);
 			return;
 		}
 		stage.put(nio.duplicate());
@@ -65,34 +71,85 @@ public class EngineInFlightLog implements InFlightLog {
 	}
 
 	private void flush() {
+		awaitNoSubmit();
 		if (staged == 0) {
 			return;
 		}
-		logBatch(stagedEpochs, stagedLens, stage, staged);
+		submit(stagedEpochs, stagedLens, stage, staged);
 		stage.clear();
 		staged = 0;
 	}
 
+	private void awaitNoSubmit() {
+		while (submitting) {
+			waitQuietly();
+		}
+	}
+
+	private void waitQuietly() {
+		try {
+			wait(10);
+		} catch (InterruptedException e) {
+			Thread.currentThread().interrupt();
+			throw new RuntimeException(e);
+		}
+	}
+
 	// Backpressure: a full in-flight pool (CLG_E_NOSPACE, nothing logged) waits until a
 	// checkpoint completes and frees epochs (notifyCheckpointComplete wakes us), then retries.
-	private void logBatch(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
-		int st;
-		while ((st = nIflLogBatch(engine.handle(), ifl, epochs, lens, bytes, n)) == CLG_E_NOSPACE) {
-			try {
-				wait(10);
-			} catch (InterruptedException e) {
-				Thread.currentThread().interrupt();
-				throw new RuntimeException(e);
+	private void submit(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
+		submitting = true;
+		try {
+			int st;
+			while ((st = nIflLogBatch(engine.handle(), ifl, epochs, lens, bytes, n)) == CLG_E_NOSPACE) {
+				if (closed) {
+					throw new IllegalStateException("in-flight log closed while waiting for pool space");
+				}
+				waitQuietly();
 			}
+			check(st);
+		} finally {
+			submitting = false;
+			notifyAll();
 		}
-		check(st);
 	}
 
 	@Override
 	public synchronized void notifyCheckpointComplete(long checkpointId) { // :51-70
-		flush();
+		// free the pool first: a log() waiting for space (backpressure) can then finish
 		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
 		notifyAll();
+		awaitNoSubmit();
+		// staged buffers of truncated epochs never reach HBM, and a batch that was waiting
+		// for space when this call began is truncated too: the reference truncates every
+		// buffer logged before the notification
+		dropStagedBelow(checkpointId);
+		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
+	}
+
+	private void dropStagedBelow(long checkpointId) {
+		int keep = 0, rd = 0, wr = 0;
+		for (int i = 0; i < staged; i++) {
+			int n = stagedLens[i];
+			if (stagedEpochs[i] >= checkpointId) {
+				if (rd != wr) {
+					byte[] tmp = new byte[n];
+					ByteBuffer src = stage.duplicate();
+					src.position(rd).limit(rd + n);
+					src.get(tmp);
+					ByteBuffer dst = stage.duplicate();
+					dst.position(wr);
+					dst.put(tmp);
+				}
+				stagedEpochs[keep] = stagedEpochs[i];
+				stagedLens[keep] = n;
+				keep++;
+				wr += n;
+			}
+			rd += n;
+		}
+		staged = keep;
+		stage.position(wr);
 	}
 
 	@Override
@@ -120,6 +177,9 @@ public class EngineInFlightLog implements InFlightLog {
 
 	@Override
 	public synchronized void close() { // :90-94
+		closed = true;
+		notifyAll();
+		awaitNoSubmit();
 		staged = 0;
 		stage.clear();
 		check(nIflClose(engine.handle(), ifl));

@@ -155,3 +155,22 @@ def test_repeated_shapes_new_bytes_no_timing():
                 check_oracle(dec, [b for b, _ in blobs])
             for lg in logs:
                 lg.close()
+
+
+def test_second_async_before_wait_is_refused():
+    """Two asynchronous decodes back to back, the first failing: the second is refused
+    (CLG_E_STATE) instead of overwriting the first one's status, which the wait returns."""
+    rng = np.random.default_rng(4)
+    good = synth.random_log(500, rng, allow_serializable=False)
+    bad = bytes(good) + bytes([0x7F, 1, 2, 3])
+    with Engine(segment_bytes=256, pool_segments=1 << 12) as eng:
+        logs = logs_of(eng, [good, bad])
+        pd = eng.decode_logs_async(logs, [1, 1])
+        with pytest.raises(ClonosError) as second:
+            eng.decode_logs_async(logs[:1], [1])
+        assert second.value.status == _lib.CLG_E_STATE
+        with pytest.raises(ClonosError) as first:
+            pd.wait()
+        assert first.value.status == _lib.CLG_E_CORRUPT_TAG and first.value.err_span == 1
+        got = eng.decode_logs_async(logs[:1], [1]).wait()  # waited for: the next one is accepted
+        assert got.n_rec == len(O.decode(good)[1]["tag"])
