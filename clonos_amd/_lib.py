@@ -52,7 +52,7 @@ EXPORTED = [
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
     "clg_ifl_open", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
-    "clg_ifl_replay_batch",
+    "clg_ifl_replay_batch", "clg_replay_prepare_device", "clg_get_determinants_batch",
 ]
 
 
@@ -289,6 +289,8 @@ def _load() -> C.CDLL:
         "clg_response_merge": (C.c_int, [C.POINTER(Response), C.POINTER(Response)]),
         "clg_causal_log_id_hash": (C.c_int32, [C.POINTER(CausalLogIdC)]),
         "clg_replay_prepare": (C.c_int, [P, C.POINTER(ReplayVertex), C.c_uint32, C.POINTER(ReplayOut)]),
+        "clg_replay_prepare_device": (C.c_int, [P, C.POINTER(ReplayVertex), C.c_uint32, C.POINTER(ReplayOut)]),
+        "clg_get_determinants_batch": (C.c_int, [P, P, P, C.c_uint32, P, C.c_uint64, C.c_uint32, P, P, u64p]),
         "clg_encode_batch": (C.c_int, [P, C.POINTER(EncodeIn), P, C.c_uint64, C.c_uint32, u64p, u64p]),
         "clg_enrich_batch": (C.c_int, [P, C.c_uint32, C.POINTER(EnrichReq), C.c_uint32, P, P, P, C.c_uint64,
                                        C.c_uint32, u64p]),

@@ -1879,6 +1879,44 @@ int clg_log_read_phys(clg_engine* e, uint32_t h, int32_t phys, uint32_t n, uint8
   return e->run_gather(pieces, n, host_out, CLG_MEM_HOST);
 }
 
+// getDeterminants(startEpoch) of many logs (respondToDeterminantRequest's copies for a
+// replay-prep merge, JobCausalLogImpl.java:188-204): the ranges on the host, the bytes by
+// one device gather, back to back in request order.
+int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n, void* out,
+                               uint64_t cap, uint32_t out_kind, uint64_t* out_off, uint32_t* len, uint64_t* total) {
+  ENGINE_GUARD(e);
+  if (n && (!log || !start_epoch || !len)) return fail(CLG_E_INVALID_ARG, "null argument");
+  std::vector<clg::SegSpan> runs;
+  std::vector<uint32_t> segtab;
+  std::unordered_map<uint32_t, uint64_t> tab_of;
+  uint32_t n_pieces = 0;
+  const uint32_t C = e->C();
+  uint64_t dst = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    Log* l;
+    CHK(e->get_log(log[i], &l));
+    int32_t s = 0, nb = 0;
+    if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &s, &nb));
+    len[i] = uint32_t(nb);
+    if (out_off) out_off[i] = dst;
+    if (nb > 0) {
+      auto ti = tab_of.find(log[i]);
+      if (ti == tab_of.end()) {
+        ti = tab_of.emplace(log[i], segtab.size()).first;
+        segtab.insert(segtab.end(), l->segs.begin(), l->segs.end());
+      }
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, n_pieces, 0});
+      n_pieces += uint32_t(s + nb - 1) / C - uint32_t(s) / C + 1;
+    }
+    dst += uint64_t(nb);
+  }
+  if (total) *total = dst;
+  if (!out) return CLG_OK;  // sizes only
+  if (dst > cap) return fail(CLG_E_CAPACITY, "getDeterminants batch needs %llu bytes", (unsigned long long)dst);
+  CHK(e->flush());
+  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
+}
+
 int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res, void* out, uint64_t cap,
                     uint32_t out_kind, uint64_t* total) {
   ENGINE_GUARD_KEEP(e);
@@ -2091,7 +2129,14 @@ int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, co
 // LogReplayerImpl (:51-158), batched over failed vertices.  Main logs go through the
 // batched decode; subpartition recovery buffers through k_bufsizes (5-byte BufferBuilt
 // records, no chain walk).  All inputs are staged to HBM in one copy.
+static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out, bool dev_in);
 int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out) {
+  return replay_prepare(e, v, n, out, false);
+}
+int clg_replay_prepare_device(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out) {
+  return replay_prepare(e, v, n, out, true);
+}
+static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out, bool dev_in) {
   ENGINE_GUARD(e);
   if (!out || !out->main || !out->main_rec_base || (n && !v)) return fail(CLG_E_INVALID_ARG, "null argument");
   struct Piece {
@@ -2145,12 +2190,22 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
     (i < n ? main_bytes : sub_bytes) += pc.len;
   }
   CHK(e->d_stage.ensure(total + 16));
-  CHK(e->h_stage.ensure(total + 16));
-  for (uint32_t i = 0; i < n + ns; ++i) {
-    const Piece& pc = i < n ? mains[i] : subs[i - n];
-    if (pc.len) memcpy(e->h_stage.as<uint8_t>() + at[i], pc.p, pc.len);
+  if (dev_in) {  // the winners already in HBM (e.g. an RCCL receive buffer): one device gather
+    std::vector<clg::GatherPiece> pieces;
+    for (uint32_t i = 0; i < n + ns; ++i) {
+      const Piece& pc = i < n ? mains[i] : subs[i - n];
+      for (uint64_t o = 0; o < pc.len; o += 1u << 30)  // a piece's length is 32-bit
+        pieces.push_back(clg::GatherPiece{pc.p + o, at[i] + o, uint32_t(std::min<uint64_t>(pc.len - o, 1u << 30)), 0});
+    }
+    CHK(e->run_gather(pieces, total, e->d_stage.p, CLG_MEM_DEVICE, "replay_stage"));
+  } else {
+    CHK(e->h_stage.ensure(total + 16));
+    for (uint32_t i = 0; i < n + ns; ++i) {
+      const Piece& pc = i < n ? mains[i] : subs[i - n];
+      if (pc.len) memcpy(e->h_stage.as<uint8_t>() + at[i], pc.p, pc.len);
+    }
+    if (total) HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
   }
-  if (total) HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
   const uint8_t* dst = e->d_stage.as<uint8_t>();
   // subpartition buffers first (their kernels only read the staged bytes)
   std::function<int(clg::JArena)> classify;

@@ -157,14 +157,28 @@ class EngineIO:
         kind = _lib.CLG_MEM_DEVICE if recv.is_cuda else _lib.CLG_MEM_HOST
         check(lib.clg_upstream_delta_batch(self.engine.handle, req.ctypes.data, len(req), recv.data_ptr(), kind))
 
-    # replay-prep merge: a copy is getDeterminants(startEpoch) of a log (owned or replica)
-    def copy_length(self, handle: int, cid: CausalLogID, start_epoch: int) -> int:
-        return ThreadCausalLog(self.engine, handle, cid).determinants_length(start_epoch)
+    # replay-prep merge: a copy is getDeterminants(startEpoch) of a log (owned or replica);
+    # both calls are one native call for all the copies (clg_get_determinants_batch)
+    def copy_lengths(self, handles: np.ndarray, start_epochs: np.ndarray) -> np.ndarray:
+        h = np.ascontiguousarray(handles, np.uint32)
+        ep = np.ascontiguousarray(start_epochs, np.int64)
+        ln = np.zeros(max(1, len(h)), np.uint32)
+        total = C.c_uint64()
+        check(lib.clg_get_determinants_batch(self.engine.handle, h.ctypes.data, ep.ctypes.data, len(h), None, 0,
+                                             _lib.CLG_MEM_DEVICE, None, ln.ctypes.data, C.byref(total)))
+        return ln[:len(h)].astype(np.int64)
 
-    def copy_into(self, handle: int, cid: CausalLogID, start_epoch: int, tensor, off: int, n: int) -> None:
-        got = ThreadCausalLog(self.engine, handle, cid).determinants_into(start_epoch, tensor.data_ptr() + off, n)
-        if got != n:
-            raise RuntimeError(f"log {cid} changed during the merge ({got} != {n} bytes)")
+    def copy_batch(self, handles: np.ndarray, start_epochs: np.ndarray, tensor, off: int) -> int:
+        """The copies back to back in the given order into tensor[off:] (one gather)."""
+        h = np.ascontiguousarray(handles, np.uint32)
+        ep = np.ascontiguousarray(start_epochs, np.int64)
+        ln = np.zeros(max(1, len(h)), np.uint32)
+        total = C.c_uint64()
+        kind = _lib.CLG_MEM_DEVICE if tensor.is_cuda else _lib.CLG_MEM_HOST
+        check(lib.clg_get_determinants_batch(self.engine.handle, h.ctypes.data, ep.ctypes.data, len(h),
+                                             tensor.data_ptr() + off, tensor.numel() - off, kind, None,
+                                             ln.ctypes.data, C.byref(total)))
+        return int(total.value)
 
 
 class Replicator:
@@ -268,8 +282,27 @@ class Replicator:
 
 
 # ---- replay-prep merge across GPUs ---------------------------------------------------------
+MERGE_GUARD = 64  # bytes before and after the received winners (device gathers read aligned 16-byte words)
+
+
+@dataclass
+class MergedCopies:
+    """The winners delivered to one rank: every log's winning copy inside one buffer (an RCCL
+    receive buffer in HBM, or host memory over gloo) at place[gid] = (offset, length), with
+    MERGE_GUARD bytes around them, ready for clg_replay_prepare_device as they lie."""
+    buf: object
+    place: Dict[int, Tuple[int, int]]
+
+    def bytes_of(self, gid: int) -> bytes:
+        o, n = self.place[gid]
+        return self.buf[o:o + n].cpu().numpy().tobytes() if n else b""
+
+    def as_dict(self) -> Dict[int, bytes]:
+        return {g: self.bytes_of(g) for g in self.place}
+
+
 def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int, int],
-                    start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None) -> Dict[int, bytes]:
+                    start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None) -> MergedCopies:
     """Cross-GPU DeterminantResponseEvent.merge for the logs of the failed vertices.
 
     copies: gid -> io handle of this rank's copy (owned log or replica) of a log of a failed
@@ -277,12 +310,13 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     (respondToDeterminantRequest -> getDeterminants(startEpoch), JobCausalLogImpl.java:
     188-204); dest_of: failed VertexID -> rank hosting its replacement.
 
-    Step 1: every rank reports len(getDeterminants) of each copy as (len << 8 | rank) and an
-    all-reduce(MAX) picks, per log, the longest copy (DeterminantResponseEvent.java:137-146;
-    equal lengths are equal bytes -- every copy is a prefix of the same log -- so the rank
-    tie-break picks identical content).  Step 2: one all-to-all carries each winner's bytes
-    from its rank to the destination.  Returns, on every rank, {gid: bytes} of the winners
-    whose destination is this rank (a log no rank holds is absent, as in the merged map)."""
+    Step 1: every rank measures all its copies in one call and reports (len << 8 | rank);
+    an all-reduce(MAX) picks, per log, the longest copy (DeterminantResponseEvent.java:
+    137-146; equal lengths are equal bytes -- every copy is a prefix of the same log -- so the
+    rank tie-break picks identical content).  Step 2: the winners this rank holds are
+    gathered in one call, grouped by destination, and one all-to-all carries them to the
+    ranks hosting the replacements.  Returns this rank's MergedCopies (a log no rank holds
+    is absent, as in the merged map)."""
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -293,11 +327,11 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     gids = np.nonzero(np.isin(table.vertex, failed))[0]
     n = len(gids)
     key = np.full(max(n, 1), -1, np.int64)
-    for k, g in enumerate(gids):
-        h = copies.get(int(g))
-        if h is not None:
-            ln = io.copy_length(h, table.ids[g], start_epochs[int(table.vertex[g])])
-            key[k] = (int(ln) << 8) | rank
+    held = np.array([k for k, g in enumerate(gids) if int(g) in copies], np.int64)
+    handles = np.array([copies[int(gids[k])] for k in held], np.int64)
+    epochs = np.array([start_epochs[int(table.vertex[gids[k]])] for k in held], np.int64)
+    if len(held):
+        key[held] = (io.copy_lengths(handles, epochs) << 8) | rank
     dev = device if backend == "nccl" else "cpu"
     kt = torch.from_numpy(key).to(dev)
     dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=group)
@@ -306,28 +340,27 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     win_len = np.where(win >= 0, win >> 8, 0)
     dest = np.array([dest_of[int(table.vertex[g])] for g in gids], np.int64)
     mine = np.nonzero(win_rank == rank)[0]
+    order = np.concatenate([mine[dest[mine] == d] for d in range(world)]) if len(mine) else mine
     send_split = np.array([int(win_len[mine[dest[mine] == d]].sum()) for d in range(world)], np.int64)
     recv_split = np.array([int(win_len[(win_rank == s) & (dest == rank)].sum()) for s in range(world)], np.int64)
     send = torch.empty(max(int(send_split.sum()), 1), dtype=torch.uint8, device=device)
-    off = 0
-    for d in range(world):  # the winners this rank holds, grouped by destination, gid order
-        for k in mine[dest[mine] == d]:
-            nb = int(win_len[k])
-            if nb:
-                g = int(gids[k])
-                io.copy_into(copies[g], table.ids[g], start_epochs[int(table.vertex[g])], send, off, nb)
-            off += nb
-    recv = torch.empty(max(int(recv_split.sum()), 1), dtype=torch.uint8, device=dev)
+    if int(send_split.sum()):
+        pos = {int(gids[k]): i for i, k in enumerate(held)}
+        sel = np.array([pos[int(gids[k])] for k in order], np.int64)
+        got = io.copy_batch(handles[sel], epochs[sel], send, 0)
+        if got != int(send_split.sum()):
+            raise RuntimeError(f"logs changed during the merge ({got} != {int(send_split.sum())} bytes)")
+    nrecv = int(recv_split.sum())
+    buf = torch.empty(MERGE_GUARD + max(nrecv, 1) + MERGE_GUARD, dtype=torch.uint8, device=dev)
     s_in = _to_comm(send, backend)
-    dist.all_to_all_single(recv[:int(recv_split.sum())], s_in[:int(send_split.sum())],
+    dist.all_to_all_single(buf[MERGE_GUARD:MERGE_GUARD + nrecv], s_in[:int(send_split.sum())],
                            output_split_sizes=recv_split.tolist(), input_split_sizes=send_split.tolist(),
                            group=group)
-    host = recv.cpu().numpy()
-    out = {}
-    o = 0
-    for s in range(world):
-        for k in np.nonzero((win_rank == s) & (dest == rank))[0]:
+    place = {}
+    o = MERGE_GUARD
+    for s_ in range(world):
+        for k in np.nonzero((win_rank == s_) & (dest == rank))[0]:
             nb = int(win_len[k])
-            out[int(gids[k])] = host[o:o + nb].tobytes()
+            place[int(gids[k])] = (o, nb)
             o += nb
-    return out
+    return MergedCopies(buf, place)

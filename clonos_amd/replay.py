@@ -87,6 +87,15 @@ class DeterminantResponseEvent:
         c = lid.to_c()
         check(lib.clg_response_put(C.byref(self._c), C.byref(c), _np_ptr(buf), len(data)))
 
+    def put_device(self, lid: CausalLogID, ptr: int, n: int, keep=None) -> None:
+        """An entry whose bytes live in device memory (replay-prep over a cross-GPU merge's
+        receive buffer, clg_replay_prepare_device); `keep` is held while the event lives."""
+        if keep is not None:
+            self._keep.append(keep)
+        self._grow(self._c.n + 1)
+        c = lid.to_c()
+        check(lib.clg_response_put(C.byref(self._c), C.byref(c), C.c_void_p(ptr), n))
+
     # ---- wire format
     def write(self) -> bytes:
         n = C.c_uint64()
@@ -139,10 +148,23 @@ class VertexReplay:
     subpartitions: List[SubpartitionReplay]
 
 
-def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, Sequence[CausalLogID]]]
-                   ) -> Tuple[DecodedBatch, List[VertexReplay]]:
+def merged_response(vertex_id: int, merged, table) -> DeterminantResponseEvent:
+    """The accumulated response of a failed vertex whose copies arrived by the cross-GPU merge
+    (dist.merge_responses): entries point into the merge's receive buffer, in HBM under RCCL
+    (prepare_replay(..., device_input=True))."""
+    ev = DeterminantResponseEvent(True, vertex_id, capacity=max(1, len(merged.place)))
+    base = merged.buf.data_ptr()
+    for gid, (o, n) in merged.place.items():
+        if int(table.vertex[gid]) == vertex_id:
+            ev.put_device(table.ids[gid], base + o, n, merged.buf)
+    return ev
+
+
+def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, Sequence[CausalLogID]]],
+                   device_input: bool = False) -> Tuple[DecodedBatch, List[VertexReplay]]:
     """ReplayingState construction for a batch of failed vertices: jobs are
-    (vertex_id, merged response, subpartition table in the task's order)."""
+    (vertex_id, merged response, subpartition table in the task's order).  device_input:
+    the responses' bytes are in device memory (clg_replay_prepare_device)."""
     n = len(jobs)
     vs = (_lib.ReplayVertex * max(1, n))()
     tables = []
@@ -151,9 +173,9 @@ def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponse
         t = (_lib.CausalLogIdC * max(1, len(subs)))(*[s.to_c() for s in subs])
         tables.append(t)
         vs[i] = _lib.ReplayVertex(C.pointer(acc._c), t, len(subs), vid, 0)
-        dets = acc.getDeterminants()
-        main_bytes += len(dets.get(CausalLogID.main(vid), b""))
-        sub_bytes += sum(len(dets.get(CausalLogID.sub(vid, s.irp_lower, s.irp_upper, s.subpartition), b""))
+        sizes_of = {_from_c(acc._entries[k].id): int(acc._entries[k].len) for k in range(acc._c.n)}
+        main_bytes += sizes_of.get(CausalLogID.main(vid), 0)
+        sub_bytes += sum(sizes_of.get(CausalLogID.sub(vid, s.irp_lower, s.irp_upper, s.subpartition), 0)
                          for s in subs)
     n_sub = sum(len(j[2]) for j in jobs)
     cap = main_bytes // 2 + n + 1
@@ -167,7 +189,8 @@ def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponse
     stag = np.zeros(max(1, n_sub), np.int32)
     out = _lib.ReplayOut(C.pointer(d), _np_ptr(base), _np_ptr(sizes), sizes.size, _np_ptr(sbase), _np_ptr(cnt),
                          _np_ptr(sst), _np_ptr(soff), _np_ptr(stag))
-    st = lib.clg_replay_prepare(engine.handle, vs, n, C.byref(out))
+    fn = lib.clg_replay_prepare_device if device_input else lib.clg_replay_prepare
+    st = fn(engine.handle, vs, n, C.byref(out))
     main = engine._finish(st, d, arrs, base, n, None)
     res, j = [], 0
     for i, (vid, acc, subs) in enumerate(jobs):

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 2
+#define CLG_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -436,6 +436,21 @@ typedef struct clg_replay_out {
 } clg_replay_out;
 
 int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out);
+/* The same with every response entry's bytes in device memory on the engine's device (e.g.
+ * the winners of a cross-GPU merge in an RCCL receive buffer): they are gathered into the
+ * engine's staging area on the GPU, never through the host.  The gather reads whole aligned
+ * 16-byte words, so each range needs 16 readable bytes before and after it inside its
+ * allocation. */
+int clg_replay_prepare_device(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out);
+
+/* getDeterminants(start_epoch[i]) of log[i] (:285-313) for n logs -- the copies
+ * respondToDeterminantRequest answers with (JobCausalLogImpl.java:188-204) -- gathered by ONE
+ * kernel back to back in request order into `out` (host or device); len[i] and out_off[i]
+ * (optional) give each copy's size and place.  out == NULL: sizes only (*total = bytes
+ * needed); cap < *total: CLG_E_CAPACITY. */
+int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
+                               void* out, uint64_t cap, uint32_t out_kind, uint64_t* out_off, uint32_t* len,
+                               uint64_t* total);
 
 /* ---- in-flight (data) log (RT/inflightlogging/, I/ below) -------------------------------------
  * InFlightLog I/InFlightLog.java:32-55, implementation InMemorySubpartitionInFlightLogger

@@ -686,21 +686,23 @@ int64_t orc_bench_decode(const uint8_t* buf, const uint64_t* span_off, const uin
   std::vector<std::thread> pool;
   for (uint32_t t = 0; t < threads; ++t) {
     pool.emplace_back([&, t]() {
-      // SoA outputs sized for the largest span this thread owns (allocated once).
+      // SoA outputs sized for the largest span this thread owns, allocated once per thread
+      // and not zero-filled (the decode writes every row it reports): the timed work is the
+      // decodeNext loop, not page-faulting output buffers in.
       size_t maxlen = 0;
       for (uint32_t s = t; s < n_spans; s += threads) maxlen = std::max<size_t>(maxlen, span_len[s]);
       size_t cap = maxlen / 2 + 1;
-      std::vector<uint32_t> off(cap), w_idx(cap), w_var_off(cap), w_var_len(cap);
-      std::vector<uint8_t> tag(cap), w_sub(cap);
-      std::vector<int64_t> v0(cap), w_v1(cap);
-      std::vector<int32_t> w_rc(cap);
+      std::unique_ptr<uint32_t[]> off(new uint32_t[cap]), w_idx(new uint32_t[cap]), w_var_off(new uint32_t[cap]),
+          w_var_len(new uint32_t[cap]);
+      std::unique_ptr<uint8_t[]> tag(new uint8_t[cap]), w_sub(new uint8_t[cap]);
+      std::unique_ptr<int64_t[]> v0(new int64_t[cap]), w_v1(new int64_t[cap]);
+      std::unique_ptr<int32_t[]> w_rc(new int32_t[cap]);
       for (uint32_t s = t; s < n_spans; s += threads) {
         size_t nr = 0, nw = 0;
         int64_t eo;
         int32_t et;
-        orc_decode_span(buf + span_off[s], span_len[s], off.data(), tag.data(), v0.data(), w_idx.data(),
-                        w_rc.data(), w_v1.data(), w_var_off.data(), w_var_len.data(), w_sub.data(), cap, cap,
-                        &nr, &nw, &eo, &et);
+        orc_decode_span(buf + span_off[s], span_len[s], off.get(), tag.get(), v0.get(), w_idx.get(), w_rc.get(),
+                        w_v1.get(), w_var_off.get(), w_var_len.get(), w_sub.get(), cap, cap, &nr, &nw, &eo, &et);
         counts[t] += int64_t(nr);
       }
     });

@@ -7,7 +7,9 @@ the ranks.  The launcher itself never touches the GPU; each rank is a fresh proc
 Checks, per rank: every replica holds exactly the owner's bytes (all ~33k replicas, read
 back in one batched slice), replica state == the oracle's ThreadCausalLogImpl fed the same
 epochs (a sample), the merge winners == DeterminantResponseEvent.merge of the ranks'
-responses (oracle/response_ref.py), and truncation afterwards (job CAS) matches the oracle.
+responses (oracle/response_ref.py), replay preparation on the destination ranks straight
+from the merge's receive buffer (clg_replay_prepare_device) == the oracle's decode and
+BufferBuilt sizes of the merged logs, and truncation afterwards (job CAS) matches the oracle.
 """
 import os
 import socket
@@ -116,7 +118,8 @@ def worker(rank, world, port, q):
         for gid in fg:
             if int(table.vertex[gid]) == 3:
                 extra[int(gid)] = content(int(gid), EPOCHS, table.ids[gid].is_main)
-        merged = X.merge_responses(X.EngineIO(eng), table, failed, copies, {3: 0, 131: 0}, dest_of, dev)
+        mc = X.merge_responses(X.EngineIO(eng), table, failed, copies, {3: 0, 131: 0}, dest_of, dev)
+        merged = mc.as_dict()
         for gid in fg:
             v = int(table.vertex[gid])
             if dest_of[v] != rank:
@@ -124,6 +127,30 @@ def worker(rank, world, port, q):
                 continue
             want = b"".join(content(int(gid), ep, table.ids[gid].is_main) for ep in range(EPOCHS))
             assert merged.get(int(gid)) == want + extra.get(int(gid), b""), (rank, int(gid))
+        # replay preparation on each failed vertex's destination rank, straight from the merge's
+        # receive buffer (device input: the winners never pass through the host)
+        from clonos_amd.replay import merged_response, prepare_replay
+        import response_ref as R
+        mine = [v for v in failed if dest_of[v] == rank]
+        if mine:
+            mcd = X.MergedCopies(mc.buf if mc.buf.is_cuda else mc.buf.to(dev), mc.place)  # gloo: lift to HBM
+            jobs, sub_gids = [], []
+            for v in mine:
+                sg = [int(g) for g in fg if int(table.vertex[g]) == v and not table.ids[g].is_main]
+                sub_gids.append(sg)
+                jobs.append((v, merged_response(v, mcd, table), [table.ids[g] for g in sg]))
+            main, res = prepare_replay(eng, jobs, device_input=True)
+            for i, v in enumerate(mine):
+                gm = [int(g) for g in fg if int(table.vertex[g]) == v and table.ids[g].is_main][0]
+                st_, r, _, _ = O.decode(merged[gm])
+                assert st_ == 0
+                sl = main.span_slice(i)
+                assert (main.tag[sl] == r["tag"]).all() and (main.v0[sl] == r["v0"]).all()
+                assert (main.off[sl] == r["off"]).all() and sl.stop - sl.start == len(r["tag"])
+                assert len(res[i].subpartitions) == PAR
+                for sp, g in zip(res[i].subpartitions, sub_gids[i]):
+                    assert sp.status == _lib.CLG_OK
+                    assert sp.buffer_sizes.tolist() == R.buffer_sizes(merged[g]), (rank, g)
         # checkpoint completion afterwards: the job's CAS + truncation of owned logs and replicas
         assert eng.truncate_all(2)
         for gid in rng.choice(wanted, 50, replace=False):

@@ -200,7 +200,10 @@ def merge_worker(rank, world, port, q):
         for gid in list(cut)[:3]:
             cut[gid] = [len(full[gid])] * world  # ties: every rank holds the whole log
         store = OracleStore(full, cut, rank)
-        got = X.merge_responses(store, table, failed, store.handles, {1: 0, 5: 0}, dest_of, "cpu")
+        merged = X.merge_responses(store, table, failed, store.handles, {1: 0, 5: 0}, dest_of, "cpu")
+        got = merged.as_dict()
+        for o, nb in merged.place.values():  # guard bytes around every winner
+            assert o >= X.MERGE_GUARD and o + nb + X.MERGE_GUARD <= merged.buf.numel()
 
         def lid(cid):
             return (R.LogId.main(cid.vertex_id) if cid.is_main else
@@ -230,12 +233,17 @@ class OracleStore:
         self.copies = {gid: b[:cut[gid][rank]] for gid, b in full.items()}
         self.handles = {gid: gid for gid in full}
 
-    def copy_length(self, handle, cid, start_epoch):
-        return len(self.copies[handle])
+    def copy_lengths(self, handles, start_epochs):
+        return np.array([len(self.copies[int(h)]) for h in handles], np.int64)
 
-    def copy_into(self, handle, cid, start_epoch, tensor, off, n):
+    def copy_batch(self, handles, start_epochs, tensor, off):
         import torch
-        tensor[off:off + n] = torch.frombuffer(bytearray(self.copies[handle]), dtype=torch.uint8)
+        for h in handles:
+            b = self.copies[int(h)]
+            if b:
+                tensor[off:off + len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            off += len(b)
+        return sum(len(self.copies[int(h)]) for h in handles)
 
 
 def test_merge_gloo_world2():
