@@ -365,31 +365,51 @@ JNIEXPORT jint JNICALL FN(nProcessDelta)(JNIEnv* env, jclass cls, jlong e, jint 
  * 3 longs per entry {irpLower, irpUpper, index}.  Main-log SoA as in nDecodeLogs (res:
  * 6 longs); per subpartition 4 longs {count, status, errOff, errTag} in subRes and the
  * BufferBuilt sizes back to back in `sizes` (int32, native order). */
-JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jshort vertex, jobject event, jint len,
-                                          jlongArray subparts, jobject off, jobject tag, jobject v0, jobject w_idx,
-                                          jobject w_rc, jobject w_v1, jobject w_var_off, jobject w_var_len,
-                                          jobject w_sub, jlongArray res, jobject sizes, jlongArray sub_res) {
+/* ReplayingState for one failed task (ReplayingState.java:67-70, :108-214) in one call:
+ * bufs[0] = its main log's bytes (null: absent), bufs[1 + j] = subpartition j's recovery
+ * buffer (null: absent, i.e. EMPTY_BUFFER), each a direct buffer holding lens[i] bytes;
+ * subparts = (irpLower, irpUpper, index) per subpartition in the task's table order.
+ * res = (n_rec, n_wide, err_status, err_span, err_off, err_tag) of the main-log decode;
+ * sub_res = (count, status, err_off, err_tag, sizes_base) per subpartition. */
+JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jshort vertex, jobjectArray bufs,
+                                          jintArray lens, jlongArray subparts, jobject off, jobject tag, jobject v0,
+                                          jobject w_idx, jobject w_rc, jobject w_v1, jobject w_var_off,
+                                          jobject w_var_len, jobject w_sub, jlongArray res, jobject sizes,
+                                          jlongArray sub_res) {
   (void)cls;
-  clg_response_entry* ents = (clg_response_entry*)calloc((size_t)len / 7u + 1u, sizeof(clg_response_entry));
-  clg_response acc;
-  memset(&acc, 0, sizeof acc);
-  acc.entries = ents;
-  acc.cap = (uint32_t)len / 7u + 1u;
-  uint64_t used = 0;
-  int s = clg_response_read(addr(env, event, 0), (uint64_t)len, &acc, &used);
   const jsize ns = (*env)->GetArrayLength(env, subparts) / 3;
   jlong* sp = (*env)->GetLongArrayElements(env, subparts, NULL);
-  clg_causal_log_id* ids = (clg_causal_log_id*)calloc(ns ? (size_t)ns : 1u, sizeof(clg_causal_log_id));
+  jint* ln = (*env)->GetIntArrayElements(env, lens, NULL);
+  clg_response_entry* ents = (clg_response_entry*)calloc((size_t)ns + 1u, sizeof(clg_response_entry));
+  clg_causal_log_id* ids = (clg_causal_log_id*)calloc((size_t)ns + 1u, sizeof(clg_causal_log_id));
   uint64_t* sbase = (uint64_t*)calloc((size_t)ns + 1u, 8);
   uint64_t* cnt = (uint64_t*)calloc((size_t)ns + 1u, 8);
   int32_t* sst = (int32_t*)calloc((size_t)ns + 1u, 4);
   int64_t* soff = (int64_t*)calloc((size_t)ns + 1u, 8);
   int32_t* stg = (int32_t*)calloc((size_t)ns + 1u, 4);
-  for (jsize i = 0; i < ns; ++i) {
-    ids[i].vertex_id = vertex;
-    ids[i].irp_lower = sp[3 * i];
-    ids[i].irp_upper = sp[3 * i + 1];
-    ids[i].subpartition = (int8_t)sp[3 * i + 2];
+  clg_response acc;
+  memset(&acc, 0, sizeof acc);
+  acc.found = 1;
+  acc.vertex_id = vertex;
+  acc.entries = ents;
+  acc.cap = (uint32_t)ns + 1u;
+  int s = CLG_OK;
+  for (jsize i = 0; i <= ns && s == CLG_OK; ++i) {
+    jobject b = (*env)->GetObjectArrayElement(env, bufs, i);
+    clg_causal_log_id id;
+    memset(&id, 0, sizeof id);
+    id.vertex_id = vertex;
+    id.is_main = i == 0;
+    if (i > 0) {
+      id.irp_lower = sp[3 * (i - 1)];
+      id.irp_upper = sp[3 * (i - 1) + 1];
+      id.subpartition = (int8_t)sp[3 * (i - 1) + 2];
+      ids[i - 1] = id;
+    }
+    if (b) {
+      s = clg_response_put(&acc, &id, addr(env, b, 0), (uint64_t)(uint32_t)ln[i]);
+      (*env)->DeleteLocalRef(env, b);
+    }
   }
   clg_decoded d;
   memset(&d, 0, sizeof d);
@@ -429,10 +449,11 @@ JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jsho
   jlong r[6] = {(jlong)d.n_rec, (jlong)d.n_wide, d.err_status, d.err_span, d.err_off, d.err_tag};
   (*env)->SetLongArrayRegion(env, res, 0, 6, r);
   for (jsize i = 0; i < ns; ++i) {
-    jlong w[4] = {(jlong)cnt[i], sst[i], soff[i], stg[i]};
-    (*env)->SetLongArrayRegion(env, sub_res, 4 * i, 4, w);
+    jlong w[5] = {(jlong)cnt[i], sst[i], soff[i], stg[i], (jlong)sbase[i]};
+    (*env)->SetLongArrayRegion(env, sub_res, 5 * i, 5, w);
   }
   (*env)->ReleaseLongArrayElements(env, subparts, sp, JNI_ABORT);
+  (*env)->ReleaseIntArrayElements(env, lens, ln, JNI_ABORT);
   free(ids), free(sbase), free(cnt), free(sst), free(soff), free(stg), free(ents);
   return s;
 }

@@ -213,7 +213,7 @@ public final class ClonosEngine implements AutoCloseable {
 								   ByteBuffer out, long[] results, long[] total);
 	static native int nProcessDelta(long engine, int job, int strategy, ByteBuffer msg, int off, int len,
 									int[] handles, long[] result);
-	static native int nReplayPrepare(long engine, short vertexId, ByteBuffer mergedEvent, int len, long[] subpartitions,
+	static native int nReplayPrepare(long engine, short vertexId, ByteBuffer[] buffers, int[] lens, long[] subpartitions,
 									 ByteBuffer off, ByteBuffer tag, ByteBuffer v0, ByteBuffer wIdx, ByteBuffer wRc,
 									 ByteBuffer wV1, ByteBuffer wVarOff, ByteBuffer wVarLen, ByteBuffer wSub,
 									 long[] result, ByteBuffer bufferSizes, long[] subpartitionResults);

@@ -90,6 +90,21 @@ public final class EngineDecodedLog {
 		this.errOff = (int) res[4];
 	}
 
+	/** Over a decode the engine already ran (replay-prep, EngineReplayPreparation): the
+	 *  record offsets and tags of log[readerIndex, writerIndex), the record count and the first
+	 *  error (status, offset; CLG_OK when none). */
+	public EngineDecodedLog(ByteBuf log, DeterminantEncoder encoder, ByteBuffer recOff, ByteBuffer tag, int nRec,
+							int errStatus, int errOff) {
+		this.log = log;
+		this.encoder = encoder;
+		this.base = log.readerIndex();
+		this.recOff = recOff;
+		this.tag = tag;
+		this.nRec = nRec;
+		this.errStatus = errStatus;
+		this.errOff = errOff;
+	}
+
 	/** decodeNext(ByteBuf, DeterminantPool) (:97-112): the next record, null at the end. */
 	public Determinant next(DeterminantPool pool) {
 		if (referencePath) {

@@ -17,6 +17,7 @@ typedef jobject jarray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
 typedef jarray jbyteArray;
+typedef jarray jobjectArray;
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
 #define JNI_ABORT 2
@@ -35,5 +36,7 @@ struct JNINativeInterface_ {
   void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
   void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
   jlong (*GetDirectBufferCapacity)(JNIEnv*, jobject);
+  jobject (*GetObjectArrayElement)(JNIEnv*, jobjectArray, jsize);
+  void (*DeleteLocalRef)(JNIEnv*, jobject);
 };
 #endif
