@@ -956,7 +956,10 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
     }
   }
   if (reason && !ctl.nodep) {
-    if (lane == 0) raise_abort(ctl, reason, t);
+    if (lane == 0) {
+      raise_abort(ctl, reason, t);
+      if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + z.td.span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return false;
   }
 
@@ -1147,6 +1150,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   const TileDesc td = tiles[t];
+  if (ctl.skip_bad && gp(ctl.span_bad)[td.span]) return;  // the robust output fills this span
   const TileDesc n1 = tiles[t + 1 < ctl.n_tiles ? t + 1 : t];  // halo source, loaded beside td
   const SpanDesc sd = spans[td.span];
   const uint32_t lo = td.delta, hi = td.delta + td.len;
@@ -1353,8 +1357,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
   }
   uint64_t x_prev = 0;  // previous tile's exit, span offset
+  uint32_t bad_span = 0xFFFFFFFFu;  // a span whose chain went wrong: its later tiles are skipped
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
+    if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
     const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
@@ -1388,9 +1394,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     uint32_t x_true;
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
     if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles,
-                       reuse ? &sp_last : nullptr))
-      return;
-    x_prev = z.td.span_off + (x_true - z.lo);
+                       reuse ? &sp_last : nullptr)) {
+      if (!ctl.span_bad) return;
+      bad_span = z.td.span;  // the next span starts on a record boundary: go on there
+    } else {
+      x_prev = z.td.span_off + (x_true - z.lo);
+    }
     __syncthreads();  // the image is reused by the next tile
   }
 }
@@ -1635,6 +1644,29 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
     const uint64_t L = sl > 0 ? 1ull + (uint64_t)sl : 0ull;
     ctl.jlen[item] = L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u;
   }
+}
+
+// Per-span fallback: one block per bad span sets its tiles' counts.
+__global__ __launch_bounds__(256) void k_decode_inject(const SpanDesc* __restrict__ spans, const uint32_t* __restrict__ bad,
+                                                       const uint64_t* __restrict__ packed, FusedCtl ctl) {
+  const SpanDesc sd = spans[bad[blockIdx.x]];
+  const uint64_t v = packed[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < sd.n_tiles; i += 256) gp(ctl.cnt)[sd.first_tile + i] = i == 0 ? v : 0ull;
+}
+int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const uint64_t* d_packed, uint32_t n_bad,
+                         FusedCtl ctl, void* stream) {
+  if (!n_bad) return CLG_OK;
+  hipLaunchKernelGGL(k_decode_inject, dim3(n_bad), dim3(256), 0, (hipStream_t)stream, d_spans, d_bad, d_packed, ctl);
+  return launch_status(hipGetLastError());
+}
+__global__ __launch_bounds__(256) void k_add_u32(uint32_t* __restrict__ x, uint64_t n, uint32_t delta) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) gp(x)[i] += delta;
+}
+int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
+  if (!n) return CLG_OK;
+  const uint64_t nb = (n + 255) / 256;
+  hipLaunchKernelGGL(k_add_u32, dim3(nb < 1024 ? (uint32_t)nb : 1024u), dim3(256), 0, (hipStream_t)stream, d_x, n, delta);
+  return launch_status(hipGetLastError());
 }
 
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,

@@ -355,6 +355,8 @@ struct clg_engine {
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
   DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
+  DevBuf d_zbad;                     // fast decode: per-span "chain went wrong" flags
+  DevBuf d_sf_meta, d_sf_rec, d_sf_wide;  // per-span fallback: bad-span list, robust outputs
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
@@ -934,7 +936,15 @@ struct clg_engine {
     std::vector<uint32_t> segtab;       // concatenated segment indices of the runs' logs
     uint32_t n_tiles = 0;
     uint32_t unit = 0;                  // device-planning tile window
+    int64_t only = -1;                  // >= 0: plan only this span of the batch (as span 0)
   };
+  // Span filter of a plan (the per-span fallback re-decodes single spans): false = skip.
+  static bool plan_keep(const DecodePlan& p, uint32_t* s) {
+    if (p.only < 0) return true;
+    if (*s != uint32_t(p.only)) return false;
+    *s = 0;
+    return true;
+  }
 
   // Tile window for device planning: min(segment, tile) when one divides the other.
   uint32_t tile_unit(uint32_t k) const {
@@ -944,6 +954,7 @@ struct clg_engine {
   }
 
   void plan_host_span(DecodePlan& p, const uint8_t* dbase, uint64_t len, uint32_t s, uint32_t T) {
+    if (!plan_keep(p, &s)) return;
     clg::SpanDesc sd{uint32_t(p.tiles.size()), 0, len};
     uint64_t o = 0;
     while (o < len) {
@@ -959,6 +970,7 @@ struct clg_engine {
   }
 
   void plan_log_span(DecodePlan& p, const Log& l, int32_t start, int32_t len, uint32_t s, uint32_t T) {
+    if (!plan_keep(p, &s)) return;
     p.unit = tile_unit(T);
     if (const uint32_t U = p.unit) {  // device planning
       const uint32_t cnt = len > 0 ? (uint32_t(start + len - 1) / U - uint32_t(start) / U + 1) : 0;
@@ -1142,7 +1154,13 @@ struct clg_engine {
     uint64_t log_bytes = 0;
     bool jser = false;
     hipEvent_t ea = nullptr, eb = nullptr;  // emit's timing events
+    // for the per-span fallback: the run's control words and outputs, and whether only
+    // span-local reasons aborted it (chains that went wrong, not a timeout / table overflow)
+    clg::FusedCtl ctl{};
+    clg::DecodeOut o{};
+    bool span_local = false;
   };
+  FusedRun zlast;  // the last finished fast run
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
@@ -1156,6 +1174,7 @@ struct clg_engine {
     const size_t o_span = 3 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), words = o_ab + 4;
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
+    CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
     CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
@@ -1177,6 +1196,10 @@ struct clg_engine {
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
                       jser ? d_zjwork.as<uint32_t>() : nullptr, spec_warm(jser), clg::JArena{}};
     if (jser) CHK(jarena_reset(&ctl.jar));
+    ctl.span_bad = d_zbad.as<uint32_t>();
+    ctl.skip_bad = 0;
+    r->ctl = ctl;
+    r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
@@ -1190,6 +1213,7 @@ struct clg_engine {
       if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
       HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
       HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
+      HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
       for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
         if (ph == 3 && !jser) continue;
         const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
@@ -1249,6 +1273,8 @@ struct clg_engine {
       // Serializable records were met without tables: other aborts may be consequences
       // (entries guessed across them), so the tables decide; a second abort goes robust
       *need_jser = !jser && hab[5] && !spilled;
+      r.span_local = !*need_jser && !spilled && !hab[4] && !hab[6];
+      zlast = r;
       if (getenv("CLONOS_FUSED_DEBUG"))
         fprintf(stderr, "[clonos] fused decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d exit=%d "
                 "timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]), int(~hab[3]),
@@ -1298,8 +1324,155 @@ struct clg_engine {
     return run_decode(p, log_bytes, out, span_rec_base);
   }
 
+  // Per-span fallback after a fast run whose chains went wrong in a few spans only (a
+  // decode error, a record the fast rules cannot place): those spans are decoded one by one
+  // by the robust pipeline into scratch, their counts injected into the fast run's per-tile
+  // counts, scan and emit re-run for the other spans (emit skips the bad ones), and the
+  // robust records copied into place (their wide rows' record indices moved by the span's
+  // record base).  *done = false: not applicable (too many or too large bad spans), the
+  // caller decodes the whole batch robustly.  The result equals the whole-batch robust
+  // decode's: every span's records, the first error of the lowest span.
+  template <class Build>
+  int span_fallback(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
+                    bool* done) {
+    *done = false;
+    const uint32_t ns = uint32_t(pf.spans.size()), nt = pf.n_tiles;
+    std::vector<uint32_t> flag(ns);
+    HIPCHK(hipMemcpy(flag.data(), d_zbad.p, size_t(ns) * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> bad;
+    uint64_t bad_bytes = 0;
+    for (uint32_t s = 0; s < ns; ++s)
+      if (flag[s]) {
+        bad.push_back(s);
+        bad_bytes += pf.spans[s].len;
+      }
+    if (bad.empty() || bad.size() > 64 || bad_bytes > log_bytes / 4) return CLG_OK;
+    stats["decode_span_fallback"].launches++;
+    const uint32_t nb = uint32_t(bad.size());
+    // scratch: per bad span the robust decode's records (13 B) and wide rows (25 B)
+    std::vector<uint64_t> rec_at(nb + 1, 0), wide_at(nb + 1, 0);
+    for (uint32_t i = 0; i < nb; ++i) {
+      rec_at[i + 1] = rec_at[i] + pf.spans[bad[i]].len / 2 + 1;
+      wide_at[i + 1] = wide_at[i] + pf.spans[bad[i]].len / 6 + 1;
+    }
+    const uint64_t RC = rec_at[nb], WC = wide_at[nb];
+    CHK(d_sf_rec.ensure(RC * 13 + 64));
+    CHK(d_sf_wide.ensure(WC * 25 + 64));
+    uint8_t* rb = d_sf_rec.as<uint8_t>();
+    uint8_t* wb = d_sf_wide.as<uint8_t>();
+    auto* s_off = reinterpret_cast<uint32_t*>(rb);
+    auto* s_v0 = reinterpret_cast<int64_t*>(rb + RC * 4 + 7 - (RC * 4 + 7) % 8);
+    auto* s_tag = reinterpret_cast<uint8_t*>(s_v0 + RC);
+    auto* s_widx = reinterpret_cast<uint32_t*>(wb);
+    auto* s_wrc = reinterpret_cast<int32_t*>(s_widx + WC);
+    auto* s_wvo = reinterpret_cast<uint32_t*>(s_wrc + WC);
+    auto* s_wvl = s_wvo + WC;
+    auto* s_wv1 = reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(s_wvl + WC) + 8 - (uintptr_t(s_wvl + WC) & 7));
+    auto* s_wsub = reinterpret_cast<uint8_t*>(s_wv1 + WC);
+    std::vector<uint64_t> packed(nb), nrec(nb), nwide(nb);
+    int e_status = CLG_OK, e_tag = 0;
+    uint32_t e_span = 0;
+    int64_t e_off = -1;
+    for (uint32_t i = 0; i < nb; ++i) {
+      DecodePlan sp;
+      sp.only = bad[i];
+      build(sp, uint32_t(clg::kTile));
+      clg_decoded so{};
+      so.off = s_off + rec_at[i];
+      so.tag = s_tag + rec_at[i];
+      so.v0 = s_v0 + rec_at[i];
+      so.w_idx = s_widx + wide_at[i];
+      so.w_rc = s_wrc + wide_at[i];
+      so.w_v1 = s_wv1 + wide_at[i];
+      so.w_var_off = s_wvo + wide_at[i];
+      so.w_var_len = s_wvl + wide_at[i];
+      so.w_sub = s_wsub + wide_at[i];
+      so.cap = rec_at[i + 1] - rec_at[i];
+      so.wcap = wide_at[i + 1] - wide_at[i];
+      so.out_kind = CLG_MEM_DEVICE;
+      uint64_t sbase[2];
+      const int st = run_decode(sp, pf.spans[bad[i]].len, &so, sbase);
+      if (st != CLG_OK && so.err_status == CLG_OK) return st;  // an engine failure, not a decode error
+      if (so.err_status != CLG_OK && e_status == CLG_OK) {     // bad[] ascends: the lowest span's error
+        e_status = so.err_status;
+        e_span = bad[i];
+        e_off = so.err_off;
+        e_tag = so.err_tag;
+      }
+      nrec[i] = so.n_rec;
+      nwide[i] = so.n_wide;
+      if (nrec[i] >= (1ull << 31) || nwide[i] >= (1ull << 32)) return CLG_OK;  // past the fast counts' packing
+      packed[i] = nwide[i] << 31 | nrec[i];
+    }
+    // the fast run again over the good spans: its plan back in place (the robust runs used
+    // the shared span table), the bad spans' counts injected, scan and emit
+    PlanLayout L;
+    CHK(stage_plan(pf, d_ztiles, &L));
+    CHK(enqueue_plan(pf, L, d_ztiles));
+    CHK(d_sf_meta.ensure(size_t(nb) * 12 + 64));
+    std::vector<uint8_t> meta(size_t(nb) * 12 + 8);
+    memcpy(meta.data(), packed.data(), size_t(nb) * 8);
+    memcpy(meta.data() + size_t(nb) * 8, bad.data(), size_t(nb) * 4);
+    HIPCHK(hipMemcpyAsync(d_sf_meta.p, meta.data(), size_t(nb) * 12, hipMemcpyHostToDevice, stream));
+    clg::FusedCtl ctl = zlast.ctl;
+    ctl.skip_bad = 1;
+    auto* zt = d_ztiles.as<clg::TileDesc>();
+    auto* zs = d_spans.as<clg::SpanDesc>();
+    CHK(clg::launch_decode_inject(zs, reinterpret_cast<const uint32_t*>(d_sf_meta.as<uint8_t>() + size_t(nb) * 8),
+                                  d_sf_meta.as<uint64_t>(), nb, ctl, stream));
+    HIPCHK(hipMemsetAsync(ctl.abort, 0, 32, stream));
+    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, zlast.o, stream, 1));
+    CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, zlast.o, stream, 2));
+    uint64_t* hz = h_zres.as<uint64_t>();
+    HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns))[0]) return CLG_OK;  // (cannot happen) whole batch
+    // the robust records into place
+    constexpr uint64_t kRecMask = (1ull << 31) - 1;
+    const clg::DecodeOut& o = zlast.o;
+    for (uint32_t i = 0; i < nb; ++i) {
+      const uint64_t R = hz[bad[i]] & kRecMask, W = hz[bad[i]] >> 31;
+      if (nrec[i] && R + nrec[i] <= o.cap) {
+        HIPCHK(hipMemcpyAsync(o.off + R, s_off + rec_at[i], nrec[i] * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.tag + R, s_tag + rec_at[i], nrec[i], hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.v0 + R, s_v0 + rec_at[i], nrec[i] * 8, hipMemcpyDeviceToDevice, stream));
+      }
+      if (nwide[i] && W + nwide[i] <= o.wcap) {
+        const uint64_t w = wide_at[i], n = nwide[i];
+        HIPCHK(hipMemcpyAsync(o.w_idx + W, s_widx + w, n * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.w_rc + W, s_wrc + w, n * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.w_v1 + W, s_wv1 + w, n * 8, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.w_var_off + W, s_wvo + w, n * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.w_var_len + W, s_wvl + w, n * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(o.w_sub + W, s_wsub + w, n, hipMemcpyDeviceToDevice, stream));
+        CHK(clg::launch_add_u32(o.w_idx + W, n, uint32_t(R), stream));  // span-local -> batch record index
+      }
+    }
+    uint64_t tr = 0, tw = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (span_rec_base) span_rec_base[s] = tr;
+      if (pf.spans[s].n_tiles == 0) continue;
+      const uint64_t a = hz[s], b = hz[ns + s];
+      tr += (b & kRecMask) - (a & kRecMask);
+      tw += (b >> 31) - (a >> 31);
+    }
+    if (span_rec_base) span_rec_base[ns] = tr;
+    *done = true;
+    CHK(finish_out(out, tr, tw));
+    if (e_status != CLG_OK) {
+      out->err_status = e_status;
+      out->err_span = e_span;
+      out->err_off = e_off;
+      out->err_tag = e_tag;
+      return fail(e_status, "decode error %d in span %u at offset %lld (tag %d)", e_status, e_span, (long long)e_off,
+                  e_tag);
+    }
+    return CLG_OK;
+  }
+
   // The fast path aborted: again with the Serializable length tables when that was the
-  // reason, then the robust pipeline.
+  // reason; then, when only some spans' chains went wrong, those spans alone through the
+  // robust pipeline (span_fallback); else the whole batch through it.
   template <class Build>
   int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                   bool need_jser) {
@@ -1308,6 +1481,11 @@ struct clg_engine {
       stats["decode_jser_retry"].launches++;
       CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &nj));
       if (!aborted) return CLG_OK;
+    }
+    if (zlast.span_local && !nj) {
+      bool done = false;
+      const int st = span_fallback(pf, build, log_bytes, out, span_rec_base, &done);
+      if (done) return st;
     }
     stats["decode_fallback"].launches++;
     DecodePlan p;

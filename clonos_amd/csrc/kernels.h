@@ -199,12 +199,24 @@ struct FusedCtl {
   uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
   uint32_t warm;    // speculative warm-up bytes before each region
   JArena jar;       // the stream walker's spill arena (k_decode_jser_general)
+  // Per-span fallback: a tile whose chain goes wrong (reasons 1-3, 5) sets span_bad[span]
+  // and the count pass goes on with the next span; the host decodes the bad spans with the
+  // robust pipeline, injects their counts (k_decode_inject) and re-runs scan + emit with
+  // skip_bad set, so emit leaves the bad spans' records to the robust output.
+  uint32_t* span_bad;
+  uint32_t skip_bad;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
 // 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
 // abort[7] != 0: phase 3 found Serializable candidates (any tile)
 // phase 0: count, 1: scan, 2: emit, 3: Serializable tables
+// Per-span fallback: cnt[t] of every tile of bad span bad[i] := t == its first tile ?
+// packed[i] (the robust decode's wide << 31 | records) : 0.
+int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const uint64_t* d_packed, uint32_t n_bad,
+                         FusedCtl ctl, void* stream);
+// x[i] += delta for i < n (the robust output's wide-row record indices moved into place).
+int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream);
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 

@@ -79,3 +79,61 @@ def test_config3_batch_with_long_records(leng):
         for s, b in enumerate(spans):
             assert_span_equal(dec, s, b)
     assert not fell_back(leng)
+
+
+def _odd_chain(n):
+    """A Timestamp then Order(0) runs: valid, but the true chain sits on odd offsets and every
+    speculative chain on even ones, so the fast count pass cannot settle it across tiles."""
+    return D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * n
+
+
+def test_span_fallback_only_the_bad_spans(leng):
+    """Two spans the fast path cannot settle among 20 ordinary ones: only those two go
+    through the robust pipeline (decode_span_fallback, not the whole-batch decode_fallback),
+    and every span is bit-exact."""
+    rng = np.random.default_rng(41)
+    spans = [synth.config3_epoch(int(rng.integers(2000, 9000)), rng)[0].tobytes() for _ in range(20)]
+    spans[7] = _odd_chain(30000)
+    spans[13] = _odd_chain(9000)
+    blob, sp = b"", []
+    for b in spans:
+        blob += bytes(int(rng.integers(0, 16)))
+        sp.append((len(blob), len(b)))
+        blob += b
+    for _ in range(2):
+        leng.kernel_stats_reset()
+        dec = leng.decode_host(blob, sp)
+        for s, b in enumerate(spans):
+            assert_span_equal(dec, s, b)
+        assert dec.span_rec_base[-1] == dec.n_rec
+        st = leng.kernel_stats()
+        assert "decode_span_fallback" in st and "decode_fallback" not in st
+
+
+def test_span_fallback_error_equals_robust():
+    """A decode error in one span and an unsettled span elsewhere: the error (status, span,
+    offset, tag) and the record count equal the robust pipeline's on the whole batch."""
+    from clonos_amd import ClonosError
+    rng = np.random.default_rng(43)
+    spans = [synth.config3_epoch(3000, rng)[0].tobytes() for _ in range(12)]
+    spans[4] = _odd_chain(20000)
+    b9, o9 = synth.config3_epoch(3000, rng)
+    k = int(o9[1500])  # a record boundary: the corrupt tag is where a record starts
+    spans[9] = b9.tobytes()[:k] + b"\x7f" + b9.tobytes()[k:]
+    blob, sp = b"", []
+    for b in spans:
+        sp.append((len(blob), len(b)))
+        blob += b
+    errs = []
+    for mode in ("auto", "robust"):
+        e = Engine(segment_bytes=16384, pool_segments=1 << 13, timing=True, decode=mode)
+        try:
+            with pytest.raises(ClonosError) as ei:
+                e.decode_host(blob, sp)
+            x = ei.value
+            errs.append((x.status, x.err_span, x.err_off, x.err_tag, x.n_rec))
+            if mode == "auto":
+                assert "decode_span_fallback" in e.kernel_stats()
+        finally:
+            e.close()
+    assert errs[0] == errs[1] and errs[0][1] == 9
