@@ -502,7 +502,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
     BufferBuilt sizes of the merged bytes."""
     import time as _t
     from clonos_amd import _lib, dist as X, job as J
-    from clonos_amd.replay import merged_response, prepare_replay
+    from clonos_amd.replay import merged_responses, prepare_replay_raw, table_ids
     g = table.graph
     failed = failed_vertices(g, np.random.default_rng(0xC1050005))
     dest_of = {v: J.owner_rank(v, world) for v in failed}
@@ -516,6 +516,8 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
             copies[int(gid)] = h
     mine = [v for v in failed if dest_of[v] == rank]
     subs_of = {v: [int(x) for x in fg if int(table.vertex[x]) == v and not table.ids[x].is_main] for v in mine}
+    ids = table_ids(table)
+    sub_tab = {v: ids[np.array(subs_of[v], np.int64)] for v in mine}  # the tasks' subpartition tables
     io = X.EngineIO(eng)
     ph = {"merge": 0.0, "replay_prep": 0.0, "truncate": 0.0}
     win_bytes, n_main_rec, n_sizes = 0, 0, 0
@@ -533,11 +535,11 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
         mc = X.merge_responses(io, table, failed, copies, {v: e - 1 for v in failed}, dest_of, dev)
         sync()
         t1 = _t.perf_counter()
-        main = res = None
+        ra = None
         if mine:
             mcd = mc if mc.buf.is_cuda else X.MergedCopies(mc.buf.to(dev), mc.place)
-            jobs = [(v, merged_response(v, mcd, table), [table.ids[x] for x in subs_of[v]]) for v in mine]
-            main, res = prepare_replay(eng, jobs, device_input=True)
+            accs = merged_responses(mcd, table, mine)
+            ra = prepare_replay_raw(eng, [(v, accs[v], sub_tab[v]) for v in mine], device_input=True)
         t2 = _t.perf_counter()
         rep.exchange(e)
         eng.sync()
@@ -551,21 +553,25 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
             import _oracle as O  # the checker
             import response_ref as R  # the checker
             merged = mc.as_dict()
+            j = 0
             for i, v in enumerate(mine):
                 gm = [int(x) for x in fg if int(table.vertex[x]) == v and table.ids[x].is_main][0]
                 st_, r, _, _ = O.decode(merged.get(gm, b""))
-                sl = main.span_slice(i)
-                assert st_ == 0 and sl.stop - sl.start == len(r["tag"]) and (main.v0[sl] == r["v0"]).all()
-                for sp, x in zip(res[i].subpartitions, subs_of[v]):
-                    assert sp.status == 0 and sp.buffer_sizes.tolist() == R.buffer_sizes(merged.get(x, b""))
+                sl = ra.main.span_slice(i)
+                assert st_ == 0 and sl.stop - sl.start == len(r["tag"]) and (ra.main.v0[sl] == r["v0"]).all()
+                for x in subs_of[v]:
+                    b0 = int(ra.base[j])
+                    got = ra.sizes[b0:b0 + int(ra.count[j])].tolist()
+                    assert ra.status[j] == 0 and got == R.buffer_sizes(merged.get(x, b""))
+                    j += 1
             continue
         ph["merge"] += t1 - t0
         ph["replay_prep"] += t2 - t1
         ph["truncate"] += t4 - t3
         win_bytes += sum(n for _, n in mc.place.values())
-        if main is not None:
-            n_main_rec += int(main.n_rec)
-            n_sizes += sum(len(sp.buffer_sizes) for r_ in res for sp in r_.subpartitions)
+        if ra is not None:
+            n_main_rec += int(ra.main.n_rec)
+            n_sizes += int(ra.count.sum())
     dev_t = "cpu" if rehearse else dev
     mx = torch.tensor([ph["merge"], ph["replay_prep"], ph["truncate"], ph["merge"] + ph["replay_prep"] + ph["truncate"]],
                       dtype=torch.float64, device=dev_t)

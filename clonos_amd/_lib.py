@@ -52,7 +52,7 @@ EXPORTED = [
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
     "clg_ifl_open", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
-    "clg_ifl_replay_batch", "clg_replay_prepare_device", "clg_get_determinants_batch",
+    "clg_ifl_replay_batch", "clg_replay_prepare_device", "clg_get_determinants_batch", "clg_response_put_batch",
 ]
 
 
@@ -284,6 +284,7 @@ def _load() -> C.CDLL:
         "clg_kernel_stats": (C.c_int, [P, C.POINTER(KernelStat), C.c_uint32, u32p]),
         "clg_kernel_stats_reset": (C.c_int, [P]),
         "clg_response_put": (C.c_int, [C.POINTER(Response), C.POINTER(CausalLogIdC), P, C.c_uint64]),
+        "clg_response_put_batch": (C.c_int, [C.POINTER(Response), P, P, P, C.c_uint32]),
         "clg_response_write": (C.c_int, [C.POINTER(Response), P, C.c_uint64, u64p]),
         "clg_response_read": (C.c_int, [P, C.c_uint64, C.POINTER(Response), u64p]),
         "clg_response_merge": (C.c_int, [C.POINTER(Response), C.POINTER(Response)]),

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -385,6 +386,23 @@ struct clg_engine {
 
   // timing
   std::map<std::string, Stat> stats;
+  // Developer host-phase timing (CLONOS_HOST_PROF set): the wall time of host-side work as
+  // pseudo-stats "host_*" beside the kernels' (launches = calls, ms = host wall time).
+  const bool host_prof = getenv("CLONOS_HOST_PROF") != nullptr;
+  struct HostTimer {
+    clg_engine* e;
+    const char* name;
+    std::chrono::steady_clock::time_point t0;
+    HostTimer(clg_engine* en, const char* n) : e(en && en->host_prof ? en : nullptr), name(n) {
+      if (e) t0 = std::chrono::steady_clock::now();
+    }
+    ~HostTimer() {
+      if (!e) return;
+      Stat& s = e->stats[name];
+      s.launches++;
+      s.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  };
   std::vector<PendingTiming> timings;
   std::vector<hipEvent_t> ev_pool;
 
@@ -622,6 +640,7 @@ struct clg_engine {
   // an RCCL receive buffer) is scattered straight into the log segments: pending host
   // bytes are flushed first, so the logs' byte order is preserved.
   int upstream_batch(clg_delta_req* r, uint32_t n, const uint8_t* bytes, uint32_t in_kind) {
+    HostTimer ht(this, "host_upstream_batch");
     if (in_kind != CLG_MEM_DEVICE) {
       for (uint32_t i = 0; i < n; ++i) {
         r[i].status = upstream(r[i].log, r[i].epoch, r[i].offset_from_epoch, bytes + r[i].src_off, r[i].len);
@@ -1162,6 +1181,7 @@ struct clg_engine {
   };
   FusedRun zlast;  // the last finished fast run
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
+    HostTimer ht(this, "host_decode_launch");
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
     r->jser = jser;
@@ -1251,7 +1271,11 @@ struct clg_engine {
     const uint64_t log_bytes = r.log_bytes;
     hipEvent_t ea = r.ea, eb = r.eb;
     uint64_t* hz = h_zres.as<uint64_t>();
-    HIPCHK(hipStreamSynchronize(stream));
+    {
+      HostTimer hw(this, "host_decode_wait");
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    HostTimer ht(this, "host_decode_finish");
     if (const char* prof_path = getenv("CLONOS_SCAN_PHASES")) {
       std::vector<uint64_t> hp(size_t(nt) * 8);
       hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
@@ -1313,7 +1337,10 @@ struct clg_engine {
     // fused counts are packed in 31-bit fields: at most log_bytes / 2 records
     if (fused_decode && log_bytes / 2 < (1ull << 31)) {
       DecodePlan pf;
-      build(pf, clg::kZTile);
+      {
+        HostTimer hp(this, "host_decode_plan");
+        build(pf, clg::kZTile);
+      }
       bool aborted = false, need_jser = false;
       CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, jser_hint, &need_jser));
       if (!aborted) return CLG_OK;
@@ -2191,6 +2218,7 @@ int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) 
   if (j.latest_cp >= cp) return CLG_OK;  // the CAS: only a newer checkpoint fans out
   j.latest_cp = cp;
   CHK(e->flush());
+  clg_engine::HostTimer ht(e, "host_truncate_all");
   for (auto& l : e->logs)
     if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
   if (applied) *applied = 1;
@@ -2230,12 +2258,17 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   std::vector<Log*> ls(n);
   std::vector<int32_t> st(n), nb(n);
   uint64_t total = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    CHK(e->get_log(log[i], &ls[i]));
-    if (ls[i]->depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
-    total += uint64_t(nb[i]);
+  {
+    clg_engine::HostTimer ht(e, "host_decode_ranges");
+    for (uint32_t i = 0; i < n; ++i) {
+      CHK(e->get_log(log[i], &ls[i]));
+      if (ls[i]->depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
+      total += uint64_t(nb[i]);
+    }
   }
   auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
+    p.spans.reserve(n);
+    p.runs.reserve(n);
     for (uint32_t i = 0; i < n; ++i) e->plan_log_span(p, *ls[i], st[i], nb[i], i, T);
   };
   return e->decode(build, total, out, span_rec_base);
@@ -2322,16 +2355,19 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
     uint64_t len;
   };
   std::vector<Piece> mains(n), subs;
-  auto lookup = [](const clg_response* r, const clg_causal_log_id& id) -> Piece {
+  // the accumulated map's entries by CausalLogID (equals :128-149), per vertex: O(entries +
+  // subpartitions) instead of a scan per subpartition
+  std::map<IdKey, uint32_t> index;
+  const clg_response* indexed = nullptr;
+  auto lookup = [&](const clg_response* r, const clg_causal_log_id& id) -> Piece {
     if (!r) return Piece{nullptr, 0};
-    for (uint32_t i = 0; i < r->n; ++i) {
-      const clg_causal_log_id& k = r->entries[i].id;
-      const bool eq = k.vertex_id == id.vertex_id && (k.is_main != 0) == (id.is_main != 0) &&
-                      (id.is_main || (k.irp_lower == id.irp_lower && k.irp_upper == id.irp_upper &&
-                                      k.subpartition == id.subpartition));
-      if (eq) return Piece{r->entries[i].bytes, r->entries[i].len};
+    if (r != indexed) {
+      index.clear();
+      for (uint32_t i = 0; i < r->n; ++i) index.emplace(key_of(0, r->entries[i].id), i);  // first of equal keys
+      indexed = r;
     }
-    return Piece{nullptr, 0};
+    const auto it = index.find(key_of(0, id));
+    return it == index.end() ? Piece{nullptr, 0} : Piece{r->entries[it->second].bytes, r->entries[it->second].len};
   };
   for (uint32_t i = 0; i < n; ++i) {
     if (v[i].n_subpartitions && !v[i].subpartitions) return fail(CLG_E_INVALID_ARG, "null subpartition table");

@@ -132,6 +132,16 @@ int clg_response_put(clg_response* r, const clg_causal_log_id* id, const uint8_t
   return CLG_OK;
 }
 
+int clg_response_put_batch(clg_response* r, const clg_causal_log_id* ids, const uint8_t* const* bytes,
+                           const uint64_t* lens, uint32_t n) {
+  if (n && (!ids || !bytes || !lens)) return set_error(CLG_E_INVALID_ARG, "null argument");
+  for (uint32_t i = 0; i < n; ++i) {
+    const int st = clg_response_put(r, &ids[i], bytes[i], lens[i]);
+    if (st != CLG_OK) return st;
+  }
+  return CLG_OK;
+}
+
 int clg_response_write(const clg_response* r, uint8_t* out, uint64_t cap, uint64_t* n_out) {
   if (!r || !n_out || (r->n && !r->entries)) return set_error(CLG_E_INVALID_ARG, "null argument");
   uint64_t need = 12;  // found (1) | vertexID (2) | correlationID (8) | size (1)

@@ -27,6 +27,31 @@ from ._lib import check, lib
 from .engine import CausalLogID, DecodedBatch, Engine, _np_ptr
 
 
+# numpy views of the C structs (include/clonos_engine.h)
+LOG_ID = np.dtype([("vertex_id", "<i2"), ("is_main", "u1"), ("subpartition", "i1"), ("reserved", "<u4"),
+                   ("irp_lower", "<i8"), ("irp_upper", "<i8")])
+ENTRY = np.dtype([("id", LOG_ID), ("bytes", "<u8"), ("len", "<u8")])
+assert LOG_ID.itemsize == C.sizeof(_lib.CausalLogIdC) and ENTRY.itemsize == C.sizeof(_lib.ResponseEntry)
+
+
+def log_id_array(ids: Sequence[CausalLogID]) -> np.ndarray:
+    """CausalLogIDs as a packed clg_causal_log_id array."""
+    a = np.zeros(len(ids), LOG_ID)
+    for i, c in enumerate(ids):
+        a[i] = (c.vertex_id, 1 if c.is_main else 0, 0 if c.is_main else c.subpartition, 0,
+                0 if c.is_main else c.irp_lower, 0 if c.is_main else c.irp_upper)
+    return a
+
+
+def table_ids(table) -> np.ndarray:
+    """The job's log table (job.LogTable) as a clg_causal_log_id array, built once per table."""
+    arr = getattr(table, "_c_ids", None)
+    if arr is None:
+        arr = log_id_array(table.ids)
+        table._c_ids = arr
+    return arr
+
+
 def _from_c(c: _lib.CausalLogIdC) -> CausalLogID:
     if c.is_main:
         return CausalLogID.main(c.vertex_id)
@@ -96,6 +121,25 @@ class DeterminantResponseEvent:
         c = lid.to_c()
         check(lib.clg_response_put(C.byref(self._c), C.byref(c), C.c_void_p(ptr), n))
 
+    def put_device_batch(self, ids: np.ndarray, ptrs: np.ndarray, lens: np.ndarray, keep=None) -> None:
+        """Many device-memory entries in one call (clg_response_put_batch); ids: LOG_ID array."""
+        if keep is not None:
+            self._keep.append(keep)
+        n = len(ids)
+        self._grow(self._c.n + n)
+        ids = np.ascontiguousarray(ids, LOG_ID)
+        ptrs = np.ascontiguousarray(ptrs, np.uint64)
+        lens = np.ascontiguousarray(lens, np.uint64)
+        self._keep.extend((ids, ptrs, lens))
+        check(lib.clg_response_put_batch(C.byref(self._c), ids.ctypes.data, ptrs.ctypes.data, lens.ctypes.data, n))
+
+    def entries(self) -> np.ndarray:
+        """The map's entries as an ENTRY array view (iteration order)."""
+        if not self._c.n:
+            return np.zeros(0, ENTRY)
+        return np.frombuffer((C.c_char * (ENTRY.itemsize * self._c.n)).from_address(C.addressof(self._entries)),
+                             ENTRY, self._c.n)
+
     # ---- wire format
     def write(self) -> bytes:
         n = C.c_uint64()
@@ -148,16 +192,74 @@ class VertexReplay:
     subpartitions: List[SubpartitionReplay]
 
 
-def merged_response(vertex_id: int, merged, table) -> DeterminantResponseEvent:
-    """The accumulated response of a failed vertex whose copies arrived by the cross-GPU merge
+def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, DeterminantResponseEvent]:
+    """The accumulated responses of failed vertices whose copies arrived by the cross-GPU merge
     (dist.merge_responses): entries point into the merge's receive buffer, in HBM under RCCL
-    (prepare_replay(..., device_input=True))."""
-    ev = DeterminantResponseEvent(True, vertex_id, capacity=max(1, len(merged.place)))
-    base = merged.buf.data_ptr()
-    for gid, (o, n) in merged.place.items():
-        if int(table.vertex[gid]) == vertex_id:
-            ev.put_device(table.ids[gid], base + o, n, merged.buf)
-    return ev
+    (prepare_replay(..., device_input=True)).  One batched put per vertex."""
+    gids = np.fromiter(merged.place.keys(), np.int64, len(merged.place))
+    place = np.array(list(merged.place.values()), np.uint64).reshape(-1, 2)
+    ids = table_ids(table)
+    base = np.uint64(merged.buf.data_ptr())
+    vert = table.vertex[gids] if len(gids) else np.zeros(0, np.int64)
+    out = {}
+    for v in vertices:
+        sel = np.nonzero(vert == v)[0]
+        ev = DeterminantResponseEvent(True, v, capacity=max(1, len(sel)))
+        if len(sel):
+            ev.put_device_batch(ids[gids[sel]], place[sel, 0] + base, place[sel, 1], merged.buf)
+        out[v] = ev
+    return out
+
+
+def merged_response(vertex_id: int, merged, table) -> DeterminantResponseEvent:
+    """merged_responses for one vertex."""
+    return merged_responses(merged, table, [vertex_id])[vertex_id]
+
+
+@dataclass
+class ReplayArrays:
+    """clg_replay_prepare's outputs as arrays (prepare_replay_raw): per subpartition (global
+    order: vertex order, then table order) its size list is sizes[base[j] : base[j] + count[j]]."""
+    main: DecodedBatch
+    sizes: np.ndarray
+    base: np.ndarray
+    count: np.ndarray
+    status: np.ndarray
+    err_off: np.ndarray
+    err_tag: np.ndarray
+
+
+def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, np.ndarray]],
+                       device_input: bool = False) -> ReplayArrays:
+    """clg_replay_prepare over jobs (vertex_id, merged response, subpartition table as a
+    LOG_ID array in the task's order), without per-subpartition Python objects."""
+    n = len(jobs)
+    vs = (_lib.ReplayVertex * max(1, n))()
+    tables = []
+    main_bytes, sub_bytes, n_sub = 0, 0, 0
+    for i, (vid, acc, subs) in enumerate(jobs):
+        t = np.ascontiguousarray(subs, LOG_ID)
+        tables.append(t)
+        n_sub += len(t)
+        vs[i] = _lib.ReplayVertex(C.pointer(acc._c), C.cast(t.ctypes.data, C.POINTER(_lib.CausalLogIdC)), len(t), vid, 0)
+        e = acc.entries()
+        main_bytes += int(e["len"][e["id"]["is_main"] != 0].sum())
+        sub_bytes += int(e["len"][e["id"]["is_main"] == 0].sum())  # a bound: the table may name fewer
+    cap = main_bytes // 2 + n + 1
+    d, arrs = engine._host_outputs(cap, main_bytes // 6 + n + 1)
+    base = np.zeros(n + 1, np.uint64)
+    sizes = np.empty(max(1, sub_bytes // 5), np.int32)
+    sbase = np.zeros(n_sub + 1, np.uint64)
+    cnt = np.zeros(max(1, n_sub), np.uint64)
+    sst = np.zeros(max(1, n_sub), np.int32)
+    soff = np.zeros(max(1, n_sub), np.int64)
+    stag = np.zeros(max(1, n_sub), np.int32)
+    out = _lib.ReplayOut(C.pointer(d), _np_ptr(base), _np_ptr(sizes), sizes.size, _np_ptr(sbase), _np_ptr(cnt),
+                         _np_ptr(sst), _np_ptr(soff), _np_ptr(stag))
+    fn = lib.clg_replay_prepare_device if device_input else lib.clg_replay_prepare
+    st = fn(engine.handle, vs, n, C.byref(out))
+    main = engine._finish(st, d, arrs, base, n, None)
+    return ReplayArrays(main, sizes, sbase[:n_sub], cnt[:n_sub], sst[:n_sub], soff[:n_sub], stag[:n_sub])
 
 
 def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, Sequence[CausalLogID]]],

@@ -391,6 +391,9 @@ typedef struct clg_response {
 
 /* HashMap.put (:54-63 constructors, JobCausalLogImpl.java:197-199): insert or replace. */
 int clg_response_put(clg_response* r, const clg_causal_log_id* id, const uint8_t* bytes, uint64_t len);
+/* n puts in order (one call for a response of many logs, e.g. a cross-GPU merge's winners). */
+int clg_response_put_batch(clg_response* r, const clg_causal_log_id* ids, const uint8_t* const* bytes,
+                           const uint64_t* lens, uint32_t n);
 /* write (:93-107).  *n_out = wire size (also on CLG_E_CAPACITY). */
 int clg_response_write(const clg_response* r, uint8_t* out, uint64_t cap, uint64_t* n_out);
 /* read (:109-125).  The count byte is signed: 128..255 entries read back as none, like the

@@ -1,9 +1,10 @@
-"""GPU: records longer than a fast-decode tile (8 KiB) stay on the fast path.
+"""GPU: records longer than a fast-decode tile (8 KiB), and spans the fast path cannot
+settle, cost only their own span.
 
 A TimerTrigger name of 40 KB or a Serializable stream of 9 KB anywhere in a batch used to
-send the whole batch to the robust pipeline.  Each case is decoded bit-exact against the
-oracle and must not fall back (16 KiB segments; a record may cross segments, tiles and
-the count pass's chunk boundaries).  SimpleDeterminantEncoder.java:228-242 (TimerTrigger
+send the whole batch to the robust pipeline.  Now only the span holding it may leave the
+fast path (the per-span fallback); each case is bit-exact against the oracle (16 KiB
+segments; a record may cross segments, tiles and the count pass's chunk boundaries).  SimpleDeterminantEncoder.java:228-242 (TimerTrigger
 name), :273-287 (SourceCheckpoint reference), :333-341 (Serializable stream)."""
 import numpy as np
 import pytest
@@ -41,16 +42,23 @@ def _long(kind: str, n: int, i: int = 0) -> bytes:
 
 @pytest.mark.parametrize("kind,n", [("timer", 40000), ("checkpoint", 20000), ("string", 9000),
                                     ("intarray", 9000), ("timer", 9000), ("string", 30000)])
-def test_long_record_stays_fast(leng, kind, n):
+def test_long_record_span_alone(leng, kind, n):
+    """One long record in one span of a batch of eight: at most that span leaves the fast path
+    (decode_span_fallback), never the whole batch (decode_fallback); bit-exact."""
     rng = np.random.default_rng(n)
     for pos in range(3):  # the long record at different offsets (tile / chunk phases)
+        spans = [synth.config3_epoch(4000, rng)[0].tobytes() for _ in range(8)]
         head = synth.config3_epoch(3000 + 1777 * pos, rng)[0].tobytes()
-        tail = synth.config3_epoch(5000, rng)[0].tobytes()
-        buf = head + _long(kind, n, pos) + tail
+        spans[5] = head + _long(kind, n, pos) + spans[5]
+        blob, sp = b"", []
+        for b in spans:
+            sp.append((len(blob), len(b)))
+            blob += b
         for _ in range(2):  # the first batch may learn the Serializable table hint
             leng.kernel_stats_reset()
-            dec = leng.decode_host(buf)
-            assert_span_equal(dec, 0, buf)
+            dec = leng.decode_host(blob, sp)
+            for s_, b in enumerate(spans):
+                assert_span_equal(dec, s_, b)
         assert not fell_back(leng), (kind, n, pos)
 
 
@@ -91,8 +99,8 @@ def test_span_fallback_only_the_bad_spans(leng):
     """Two spans the fast path cannot settle among 20 ordinary ones: only those two go
     through the robust pipeline (decode_span_fallback, not the whole-batch decode_fallback),
     and every span is bit-exact."""
-    rng = np.random.default_rng(41)
-    spans = [synth.config3_epoch(int(rng.integers(2000, 9000)), rng)[0].tobytes() for _ in range(20)]
+    rng = np.random.default_rng(41)  # no Serializable records: the count pass runs without tables
+    spans = [synth.config2_log(int(rng.integers(2000, 9000)), rng)[0].tobytes() for _ in range(20)]
     spans[7] = _odd_chain(30000)
     spans[13] = _odd_chain(9000)
     blob, sp = b"", []
