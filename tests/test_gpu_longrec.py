@@ -43,11 +43,13 @@ def _long(kind: str, n: int, i: int = 0) -> bytes:
 @pytest.mark.parametrize("kind,n", [("timer", 40000), ("checkpoint", 20000), ("string", 9000),
                                     ("intarray", 9000), ("timer", 9000), ("string", 30000)])
 def test_long_record_span_alone(leng, kind, n):
-    """One long record in one span of a batch of eight: at most that span leaves the fast path
-    (decode_span_fallback), never the whole batch (decode_fallback); bit-exact."""
+    """One long record in one span of a batch of twelve: at most that span leaves the fast path
+    (decode_span_fallback), never the whole batch (decode_fallback); bit-exact.  The spans are
+    large enough that the long one holds under a quarter of the batch's bytes (past that the
+    engine decodes the whole batch robustly, engine.cpp decode_span_fallback)."""
     rng = np.random.default_rng(n)
     for pos in range(3):  # the long record at different offsets (tile / chunk phases)
-        spans = [synth.config3_epoch(4000, rng)[0].tobytes() for _ in range(8)]
+        spans = [synth.config3_epoch(8000, rng)[0].tobytes() for _ in range(12)]
         head = synth.config3_epoch(3000 + 1777 * pos, rng)[0].tobytes()
         spans[5] = head + _long(kind, n, pos) + spans[5]
         blob, sp = b"", []
@@ -90,8 +92,9 @@ def test_config3_batch_with_long_records(leng):
 
 
 def _odd_chain(n):
-    """A Timestamp then Order(0) runs: valid, but the true chain sits on odd offsets and every
-    speculative chain on even ones, so the fast count pass cannot settle it across tiles."""
+    """A Timestamp then Order(0) runs: valid, but the true chain sits on odd offsets of the span
+    and, for a span that starts 16-byte aligned, every speculative chain on even ones, so the
+    fast count pass cannot settle it across tiles."""
     return D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * n
 
 
@@ -104,8 +107,10 @@ def test_span_fallback_only_the_bad_spans(leng):
     spans[7] = _odd_chain(30000)
     spans[13] = _odd_chain(9000)
     blob, sp = b"", []
-    for b in spans:
+    for i, b in enumerate(spans):
         blob += bytes(int(rng.integers(0, 16)))
+        if i in (7, 13):  # 16-byte aligned: the true chain on odd tile coordinates
+            blob += bytes(-len(blob) % 16)
         sp.append((len(blob), len(b)))
         blob += b
     for _ in range(2):
@@ -129,7 +134,9 @@ def test_span_fallback_error_equals_robust():
     k = int(o9[1500])  # a record boundary: the corrupt tag is where a record starts
     spans[9] = b9.tobytes()[:k] + b"\x7f" + b9.tobytes()[k:]
     blob, sp = b"", []
-    for b in spans:
+    for i, b in enumerate(spans):
+        if i == 4:  # a gap: span 4 16-byte aligned (_odd_chain)
+            blob += bytes(-len(blob) % 16)
         sp.append((len(blob), len(b)))
         blob += b
     errs = []
