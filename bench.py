@@ -248,7 +248,8 @@ def main():
                                  gbs=round(per_launch / (avg_ms * 1e-3) / 1e9, 1) if avg_ms > 0 else None)
         return out
     kern, kern_iso = per_kernel(stats), per_kernel(iso_stats)
-    dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"]) if kern else None
+    dom = max((k for k in kern if k != "decode_pipeline" and not k.startswith("host_")),
+              key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"], default=None)
     roof = None
     if dom:
         ach = kern[dom]["gbs"]
@@ -261,10 +262,16 @@ def main():
                 traffic = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic}
-    # decode pipeline as a whole (4 kernels) against its algorithmic bytes
-    dec_ms = sum(kern_iso[k]["avg_ms"] for k in kern_iso if k.startswith("decode_"))
+    # decode pipeline as a whole (HIP events from its first kernel's start to emit's end, on
+    # the engine's stream) against its algorithmic bytes
+    dec_ms = kern_iso["decode_pipeline"]["avg_ms"] if "decode_pipeline" in kern_iso else None
     dec_bytes = total_bytes + 13 * n_det
-    slice_bytes = 2 * slice_total + 16 * n_req
+    # the slice's algorithmic bytes: every source byte some consumer reads, once (per log the
+    # union of its consumers' suffixes), every byte written, 16 B of metadata per request
+    first_off = {}
+    for i, _, off in cons:
+        first_off[i] = min(first_off.get(i, off), off)
+    slice_bytes = sum(log_bytes[i] - o for i, o in first_off.items()) + slice_total + 16 * n_req
     roof_iso = None
     if dom and dom in kern_iso and kern_iso[dom]["gbs"]:
         roof_iso = {"kernel": dom, "achieved": kern_iso[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -314,7 +321,7 @@ def main():
                        "log_bytes_per_gpu": total_bytes, "slice_bytes_per_gpu": slice_total,
                        "segment_bytes": seg, "parallelism": f"shard-by-vertex x{world}"},
             "log_gbs": round(total_bytes * world / (elapsed / args.steps) / 1e9, 2),
-            "decode_pipeline": {"avg_ms_isolated": round(dec_ms, 4), "algo_bytes": dec_bytes,
+            "decode_pipeline": {"avg_ms_isolated": round(dec_ms, 4) if dec_ms else None, "algo_bytes": dec_bytes,
                                 "gbs": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1) if dec_ms else None},
             "step_roofline": {"note": "decode + slice algorithmic bytes / step time (slice gather overlaps the "
                                       "next decode on a second stream)", "achieved": round(step_gbs, 1),
@@ -537,7 +544,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
         t1 = _t.perf_counter()
         ra = None
         if mine:
-            mcd = mc if mc.buf.is_cuda else X.MergedCopies(mc.buf.to(dev), mc.place)
+            mcd = mc if mc.buf.is_cuda else X.MergedCopies(mc.buf.to(dev), gids=mc.gids, offs=mc.offs, lens=mc.lens)
             accs = merged_responses(mcd, table, mine)
             ra = prepare_replay_raw(eng, [(v, accs[v], sub_tab[v]) for v in mine], device_input=True)
         t2 = _t.perf_counter()
@@ -568,7 +575,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
         ph["merge"] += t1 - t0
         ph["replay_prep"] += t2 - t1
         ph["truncate"] += t4 - t3
-        win_bytes += sum(n for _, n in mc.place.values())
+        win_bytes += int(mc.lens.sum())
         if ra is not None:
             n_main_rec += int(ra.main.n_rec)
             n_sizes += int(ra.count.sum())
@@ -734,30 +741,46 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     headline line (decode only; no consumers are defined for this config)."""
     import time as _t
     from clonos_amd import CausalLogID, Engine, _lib, synth
+    from clonos_amd import determinants as D
     rng = np.random.default_rng(synth.SEED_CONFIG3)
-    epochs = [synth.config3_epoch(per_epoch, rng, e)[0] for e in range(n_epochs)]
+    gen = [synth.config3_epoch(per_epoch, rng, e) for e in range(n_epochs)]
+    epochs = [g[0] for g in gen]
     per_log = sum(int(e.size) for e in epochs)
     seg = 16384
-    eng = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
-                 timing=True, ifl_pool_segments=16)
-    logs = []
-    for v in range(n_logs):  # every log: the epoch sequence rotated, so layouts differ per log
-        log = eng.open_log(CausalLogID.main(v))
-        for e in range(n_epochs):
-            log.processUpstreamDelta(epochs[(e + v) % n_epochs].tobytes(), 0, e)
-        logs.append(log)
-    eng.sync()
     total = per_log * n_logs
     n_det = n_logs * per_epoch * n_epochs
-    o = [torch.empty(n_det, dtype=torch.int32, device=dev), torch.empty(n_det, dtype=torch.uint8, device=dev),
-         torch.empty(n_det, dtype=torch.int64, device=dev)]
+    # the long-record variant (VERDICT r2 next-5): one log's epoch carries a 40 KB TimerTrigger
+    # name, another's a 9 KB Serializable stream (an int[] of 2250), each at a record boundary
+    long_tt = D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * 40000))
+    long_js = D.encode(D.SerializableDeterminant(D.jser_int_array(list(range(2250)))))
+    def with_long(e, rec):
+        k = int(gen[e][1][len(gen[e][1]) // 2])
+        return np.concatenate([epochs[e][:k], np.frombuffer(rec, np.uint8), epochs[e][k:]])
+    special = {(37, 4): with_long(4, long_tt), (181, 7): with_long(7, long_js)}  # (log, epoch) -> bytes
+
+    def build_engine(variant, decode="auto"):
+        e_ = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
+                    timing=True, ifl_pool_segments=16, decode=decode)
+        ls = []
+        for v in range(n_logs):  # every log: the epoch sequence rotated, so layouts differ per log
+            log = e_.open_log(CausalLogID.main(v))
+            for e in range(n_epochs):
+                b = special.get((v, (e + v) % n_epochs)) if variant == "long" else None
+                log.processUpstreamDelta((b if b is not None else epochs[(e + v) % n_epochs]).tobytes(), 0, e)
+            ls.append(log)
+        e_.sync()
+        return e_, ls
+    eng, logs = build_engine("clean")
+    cap = n_det + 16  # (the long-record variant holds two records more)
+    o = [torch.empty(cap, dtype=torch.int32, device=dev), torch.empty(cap, dtype=torch.uint8, device=dev),
+         torch.empty(cap, dtype=torch.int64, device=dev)]
     wcap = n_det // 2 + 16
     ow = [torch.empty(wcap, dtype=t, device=dev) for t in
           (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
     dec = _lib.Decoded()
     dec.off, dec.tag, dec.v0 = [t.data_ptr() for t in o]
     dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len, dec.w_sub = [t.data_ptr() for t in ow]
-    dec.cap, dec.wcap, dec.out_kind = n_det, wcap, _lib.CLG_MEM_DEVICE
+    dec.cap, dec.wcap, dec.out_kind = cap, wcap, _lib.CLG_MEM_DEVICE
     handles = np.array([l.handle for l in logs], np.uint32)
     starts = np.zeros(n_logs, np.int64)
     base = np.zeros(n_logs + 1, np.uint64)
@@ -783,12 +806,39 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     algo = total + 13 * n_det + 25 * n_wide
     kern = {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5))
             for k, v in st.items() if v["launches"]}
+
+    def timed_decode(variant, decode, n_expect):
+        e_, ls = build_engine(variant, decode)
+        try:
+            h = np.array([l.handle for l in ls], np.uint32)
+            e_.decode_logs_device(h, starts, dec, base)  # warm-up (table hint)
+            assert dec.n_rec == n_expect and dec.err_status == 0, (variant, decode, dec.n_rec, n_expect)
+            torch.cuda.synchronize()
+            e_.kernel_stats_reset()
+            t0 = _t.perf_counter()
+            for _ in range(steps):
+                e_.decode_logs_device(h, starts, dec, base)
+            torch.cuda.synchronize()
+            ms = (_t.perf_counter() - t0) / steps * 1e3
+            paths = sorted(k for k in e_.kernel_stats() if k in ("decode_fallback", "decode_span_fallback"))
+            return ms, paths
+        finally:
+            e_.close()
+    # the robust pipeline alone (the fallback's throughput) and the long-record batch
+    rob_ms, _ = timed_decode("clean", "robust", n_det)
+    long_ms, long_paths = timed_decode("long", "auto", n_det + 2)
     out = {"workload": f"config3: {n_logs} subtask logs x {n_epochs} epochs x {per_epoch} mixed determinants "
                        "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
            "log_gbs": round(total / el / 1e9, 2), "algo_gbs": round(algo / el / 1e9, 1),
            "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern,
-           "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)}}
+           "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)},
+           "robust_pipeline": {"ms_per_step": round(rob_ms, 4), "determinants_per_s": round(n_det / rob_ms * 1e3, 1),
+                               "log_gbs": round(total / rob_ms / 1e6, 2)},
+           "long_records": {"note": "the same batch with a 40 KB TimerTrigger name (log 37) and a 9 KB "
+                                    "Serializable int[] stream (log 181) inserted at record boundaries",
+                            "ms_per_step": round(long_ms, 4), "vs_clean": round(long_ms / (el * 1e3), 4),
+                            "fallbacks": long_paths}}
     if not args.no_cpu_baseline:  # the C++ oracle's decodeNext loop on host cores, whole workload once
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import _oracle as O  # the checker, timed here as the CPU baseline

@@ -987,7 +987,6 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
 // 1024 tiles (block-relative bases + the block's total); scan2: one workgroup scans the
 // block totals into block offsets.  The emit pass adds the two.
 // ---------------------------------------------------------------------------------
-constexpr uint32_t kZScanBlock = 1024;
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, uint32_t lane) {
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1001,7 +1000,8 @@ __global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
   __shared__ uint64_t s_w[4];
   if (ld_agent32(ctl.abort)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t i0 = blockIdx.x * kZScanBlock + tid * 4u, nt = ctl.n_tiles;
+  const uint32_t nt = min(ctl.t_hi, ctl.n_tiles);
+  const uint32_t blk = blockIdx.x + ctl.t_lo / kZScanBlock, i0 = blk * kZScanBlock + tid * 4u;
   uint64_t v[4], sum = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1018,20 +1018,26 @@ __global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
     if (i0 + j < nt) gp(ctl.base)[i0 + j] = run;
     run += v[j];
   }
-  if (tid == 255u) gp(ctl.boff)[blockIdx.x] = run;  // block total (scan2 turns it into an offset)
+  if (tid == 255u) gp(ctl.boff)[blk] = run;  // block total (scan2 turns it into an offset)
 }
 
-__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_blocks) {
+// Blocks [b_lo, b_hi): their totals become offsets.  A later part (b_lo > 0) starts from
+// the previous part's last block: its offset + its tiles' last base + that tile's count.
+__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t b_lo, uint32_t b_hi) {
   __shared__ uint64_t s_w[16];
   if (ld_agent32(ctl.abort)) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint64_t v = tid < n_blocks ? gp(ctl.boff)[tid] : 0ull;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, b = b_lo + tid;
+  const uint64_t v = b < b_hi ? gp(ctl.boff)[b] : 0ull;
   const uint64_t incl = wave_incl_scan(v, lane);
   if (lane == 63u) s_w[wv] = incl;
   __syncthreads();
   uint64_t run = incl - v;
   for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
-  if (tid < n_blocks) gp(ctl.boff)[tid] = run;
+  if (b_lo) {
+    const uint32_t tl = b_lo * kZScanBlock - 1;  // the previous part's last tile
+    run += gp(ctl.boff)[b_lo - 1] + gp(ctl.base)[tl] + gp(ctl.cnt)[tl];
+  }
+  if (b < b_hi) gp(ctl.boff)[b] = run;
 }
 
 // Each span's record / wide-record range from the scan (the host reads them before the
@@ -1147,7 +1153,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
   __shared__ PosT s_pos[kWin];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  const uint32_t t = blockIdx.x + ctl.t_lo, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   const TileDesc td = tiles[t];
   if (ctl.skip_bad && gp(ctl.span_bad)[td.span]) return;  // the robust output fills this span
@@ -1335,8 +1341,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   constexpr bool kLm = CLG_COUNT_LM != 0;  // J: the image becomes the step-code map (build_lm)
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
-  const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
-  const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
+  const uint32_t tl = ctl.t_lo, th = min(ctl.t_hi, nt);
+  const uint32_t K = (th - tl + gridDim.x - 1) / gridDim.x;
+  const uint32_t t0 = tl + blockIdx.x * K, t1 = min(th, t0 + K);
   if (t0 >= t1) return;
   // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
   uint32_t x_pub = kZCanon;
@@ -1620,7 +1627,8 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   __shared__ uint32_t s_img[kZJRows * kZPitch];
   __shared__ uint32_t s_cand[kZJCap];
   bool flagged = false;
-  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
+  const uint32_t th = min(ctl.t_hi, ctl.n_tiles);
+  for (uint32_t t = ctl.t_lo + blockIdx.x; t < th; t += gridDim.x) {
     jser_tile(tiles, spans, ctl, s_img, s_cand, t, threadIdx.x, &flagged);
     __syncthreads();  // the image is reused by the next tile
   }
@@ -1634,6 +1642,7 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
   const uint32_t n = min(ld_agent32(ctl.jwork), ctl.jwork_cap);
   for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
     const uint32_t item = ctl.jwork[1 + i], t = item / kZJCap;
+    if (t < ctl.t_lo || t >= ctl.t_hi) continue;  // another part's candidate
     const TileDesc td = tiles[t];
     const SpanDesc sd = spans[td.span];
     const uint32_t a = ctl.jpos[item];
@@ -1670,9 +1679,13 @@ int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
 }
 
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase) {
+                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase, uint32_t grid_pct) {
   if (!n_tiles) return CLG_OK;
   ctl.n_tiles = n_tiles;
+  ctl.t_hi = min(ctl.t_hi, n_tiles);
+  if (ctl.t_lo >= ctl.t_hi) return CLG_OK;
+  if (ctl.t_lo % kZScanBlock) return CLG_E_INVALID_ARG;  // parts start on a scan block
+  const uint32_t nt = ctl.t_hi - ctl.t_lo;  // tiles of this launch
   hipStream_t st = (hipStream_t)stream;
   if (phase == 0) {
     static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
@@ -1686,22 +1699,25 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
         return CLG_E_DEVICE;
       resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
     }
-    const uint32_t grid = n_tiles < (uint32_t)resident[j] ? n_tiles : (uint32_t)resident[j];
+    uint32_t cap = (uint32_t)resident[j];
+    if (grid_pct && grid_pct < 100) cap = max(1u, cap * grid_pct / 100u);  // a part beside another part's emit
+    const uint32_t grid = nt < cap ? nt : cap;
     if (j)
       hipLaunchKernelGGL(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
     else
       hipLaunchKernelGGL(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {
-    const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
-    if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
-    hipLaunchKernelGGL(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
-    hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
-    hipLaunchKernelGGL(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
+    const uint32_t b_lo = ctl.t_lo / kZScanBlock, b_hi = (ctl.t_hi + kZScanBlock - 1) / kZScanBlock;
+    if (b_hi - b_lo > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per part: the host splits
+    hipLaunchKernelGGL(k_decode_scan1, dim3(b_hi - b_lo), dim3(256), 0, st, ctl);
+    hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, b_lo, b_hi);
+    if (ctl.t_hi == n_tiles)  // the last part: every tile's base is known
+      hipLaunchKernelGGL(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
   } else if (phase == 2) {
     if (ctl.jser)
-      hipLaunchKernelGGL(k_decode_emit<true>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+      hipLaunchKernelGGL(k_decode_emit<true>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
     else
-      hipLaunchKernelGGL(k_decode_emit<false>, dim3(n_tiles), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+      hipLaunchKernelGGL(k_decode_emit<false>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else {
     static int jres = 0;  // blocks the device keeps resident for the table kernel
     if (!jres) {
@@ -1712,7 +1728,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
         return CLG_E_DEVICE;
       jres = per_cu * cus;
     }
-    hipLaunchKernelGGL(k_decode_jser, dim3(n_tiles < (uint32_t)jres ? n_tiles : (uint32_t)jres), dim3(64), 0, st,
+    hipLaunchKernelGGL(k_decode_jser, dim3(nt < (uint32_t)jres ? nt : (uint32_t)jres), dim3(64), 0, st,
                        d_tiles, d_spans, ctl);
     hipLaunchKernelGGL(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }

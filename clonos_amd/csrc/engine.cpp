@@ -110,41 +110,127 @@ struct EpochAlloc {
   bool operator!=(const EpochAlloc<U>&) const { return false; }
 };
 
-// A log's epochs: epoch id -> its start offset, in id order.  A log holds few epochs
-// between checkpoints, appended in increasing order, so a sorted vector (the interface
-// of the std::map it replaces) avoids a node allocation per epoch.
+// A log's epochs: epoch id -> its start offset, in id order (the reference's
+// epochStartOffsets map).  A log holds few epochs between checkpoints, appended in
+// increasing order, so they live in a small sorted array, the first kInline inside the Log
+// itself: a config-4 step opens an epoch in, and truncates one out of, each of 66 k logs,
+// and per-log work is bound by cache misses.  The offset is kept inline; the shared
+// EpochStart object (Java's EpochStartOffset, which a ConsumerOffset references) exists
+// only once a consumer refers to the epoch (ref()), and rebase() keeps both in step.
+struct EpochEnt {
+  int64_t id = 0;
+  int32_t offset = 0;
+  std::shared_ptr<EpochStart> shared;  // null until a ConsumerOffset refers to the epoch
+};
 class EpochMap {
  public:
-  using value_type = std::pair<int64_t, std::shared_ptr<EpochStart>>;
-  using iterator = std::vector<value_type>::iterator;
-  using const_iterator = std::vector<value_type>::const_iterator;
-  iterator begin() { return v_.begin(); }
-  iterator end() { return v_.end(); }
-  const_iterator begin() const { return v_.begin(); }
-  const_iterator end() const { return v_.end(); }
-  size_t size() const { return v_.size(); }
-  bool empty() const { return v_.empty(); }
-  iterator find(int64_t k) {
-    auto it = lower(k);
-    return it != v_.end() && it->first == k ? it : v_.end();
+  EpochEnt* begin() { return data(); }
+  EpochEnt* end() { return data() + n_; }
+  const EpochEnt* begin() const { return data(); }
+  const EpochEnt* end() const { return data() + n_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  EpochEnt* find(int64_t k) {
+    EpochEnt* it = lower(k);
+    return it != end() && it->id == k ? it : end();
   }
-  const_iterator find(int64_t k) const { return const_cast<EpochMap*>(this)->find(k); }
-  void emplace(int64_t k, std::shared_ptr<EpochStart> e) {
-    auto it = lower(k);
-    if (it != v_.end() && it->first == k) return;
-    v_.insert(it, value_type(k, std::move(e)));
+  const EpochEnt* find(int64_t k) const { return const_cast<EpochMap*>(this)->find(k); }
+  // computeIfAbsent(k -> offset); the entry stays valid until the next insert or erase
+  EpochEnt* emplace(int64_t k, int32_t offset) {
+    EpochEnt* it = lower(k);
+    if (it != end() && it->id == k) return it;
+    const size_t i = size_t(it - begin());
+    if (big_.empty() && n_ < kInline) {
+      for (size_t j = n_; j > i; --j) inl_[j] = std::move(inl_[j - 1]);
+      inl_[i] = EpochEnt{k, offset, nullptr};
+    } else {
+      if (big_.empty()) {  // spill the inline entries
+        big_.reserve(2 * kInline);
+        for (uint32_t j = 0; j < n_; ++j) big_.push_back(std::move(inl_[j]));
+        for (auto& x : inl_) x.shared.reset();
+      }
+      big_.insert(big_.begin() + long(i), EpochEnt{k, offset, nullptr});
+    }
+    ++n_;
+    return begin() + i;
   }
-  iterator erase(iterator it) { return v_.erase(it); }
   // drop every epoch with id < k (checkpoint completion)
-  void erase_below(int64_t k) { v_.erase(v_.begin(), lower(k)); }
+  void erase_below(int64_t k) {
+    const size_t d = size_t(lower(k) - begin());
+    if (!d) return;
+    if (big_.empty()) {
+      for (size_t j = d; j < n_; ++j) inl_[j - d] = std::move(inl_[j]);
+      for (size_t j = n_ - d; j < n_; ++j) inl_[j].shared.reset();
+    } else {
+      big_.erase(big_.begin(), big_.begin() + long(d));
+    }
+    n_ -= uint32_t(d);
+  }
+  // every offset -= move (the shared objects too: consumers see the rebased offset)
+  void rebase(int32_t move) {
+    for (EpochEnt& x : *this) {
+      x.offset -= move;
+      if (x.shared) x.shared->offset = x.offset;
+    }
+  }
+  // the EpochStart object a ConsumerOffset holds (created on first reference)
+  static std::shared_ptr<EpochStart> ref(EpochEnt& x) {
+    if (!x.shared) x.shared = std::allocate_shared<EpochStart>(EpochAlloc<EpochStart>(), EpochStart{x.id, x.offset});
+    return x.shared;
+  }
 
  private:
-  iterator lower(int64_t k) {
-    if (v_.empty() || v_.back().first < k) return v_.end();  // the common case: a new epoch
-    return std::lower_bound(v_.begin(), v_.end(), k,
-                            [](const value_type& a, int64_t b) { return a.first < b; });
+  static constexpr uint32_t kInline = 2;
+  EpochEnt* data() { return big_.empty() ? inl_ : big_.data(); }
+  const EpochEnt* data() const { return big_.empty() ? inl_ : big_.data(); }
+  EpochEnt* lower(int64_t k) {
+    if (n_ == 0 || end()[-1].id < k) return end();  // the common case: a new epoch
+    return std::lower_bound(begin(), end(), k, [](const EpochEnt& a, int64_t b) { return a.id < b; });
   }
-  std::vector<value_type> v_;
+  uint32_t n_ = 0;
+  EpochEnt inl_[kInline];
+  std::vector<EpochEnt> big_;  // all entries once more than kInline were held
+};
+
+// A log's segments (Netty components), the first kInline inside the Log itself.
+class SegList {
+ public:
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  uint32_t operator[](size_t i) const { return data()[i]; }
+  const uint32_t* begin() const { return data(); }
+  const uint32_t* end() const { return data() + n_; }
+  void push_back(uint32_t v) {
+    if (big_.empty() && n_ < kInline) {
+      inl_[n_++] = v;
+      return;
+    }
+    if (big_.empty()) big_.assign(inl_, inl_ + n_);
+    big_.push_back(v);
+    ++n_;
+  }
+  // drop the first k (discardReadComponents)
+  void erase_front(size_t k) {
+    if (!k) return;
+    if (big_.empty()) {
+      for (size_t j = k; j < n_; ++j) inl_[j - k] = inl_[j];
+    } else {
+      big_.erase(big_.begin(), big_.begin() + long(k));
+      if (big_.size() <= kInline) {  // back inline
+        std::copy(big_.begin(), big_.end(), inl_);
+        big_.clear();
+        big_.shrink_to_fit();
+      }
+    }
+    n_ -= uint32_t(k);
+  }
+
+ private:
+  static constexpr uint32_t kInline = 6;
+  const uint32_t* data() const { return big_.empty() ? inl_ : big_.data(); }
+  uint32_t n_ = 0;
+  uint32_t inl_[kInline] = {};
+  std::vector<uint32_t> big_;  // all segments once more than kInline were held
 };
 struct ChKey {
   uint64_t lo, hi;
@@ -169,7 +255,7 @@ struct Log {
   uint32_t job = 0;
   int32_t depth = CLG_FULL_SHARING;  // the owning job's sharing depth
   bool open = false;
-  std::vector<uint32_t> segs;  // composite components
+  SegList segs;                // composite components
   int32_t writer = 0;          // visibleWriterIndex (== composite writerIndex)
   int32_t flushed = 0;         // physical bytes [0, flushed) are resident in HBM
   // Host copy of physical bytes [tail_start, writer): the staged bytes [flushed, writer)
@@ -351,7 +437,7 @@ struct clg_engine {
 
   // staging / scratch
   PinBuf h_stage, h_desc, h_sres, h_zres;
-  DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
@@ -372,11 +458,15 @@ struct clg_engine {
   // every full sync first waits for it (gwait).
   hipStream_t gstream = nullptr;
   hipEvent_t gready = nullptr;
+  // A fast decode in parts: scan + emit of each part on estream after its count (part_ev).
+  static constexpr uint32_t kMaxParts = 8;
+  hipStream_t estream = nullptr;
+  hipEvent_t part_ev[kMaxParts + 1] = {};
   bool g_pending = false;
   // two descriptor sets, so a gather can be queued while the previous one still runs;
   // gdone[s] marks the end of the last gather that used set s
   PinBuf h_gdesc[2];
-  DevBuf d_gdesc[2], d_gpieces[2];
+  DevBuf d_gdesc[2];
   hipEvent_t gdone[2] = {nullptr, nullptr};
   uint32_t gseq = 0;
   PinBuf h_rmeta;
@@ -492,10 +582,14 @@ struct clg_engine {
   int32_t capacity(const Log& l) const { return int32_t(l.segs.size()) * int32_t(C()); }
   // notEnoughSpaceFor / addComponent (:351-353, :438-452): all-or-nothing.
   int ensure_space(Log& l, int32_t n) {
+    if (int64_t(l.writer) + n <= capacity(l)) return CLG_OK;
+    std::lock_guard<std::mutex> g(pool_mu);
+    return ensure_space_locked(l, n);
+  }
+  int ensure_space_locked(Log& l, int32_t n) {  // pool_mu held
     int64_t need_bytes = int64_t(l.writer) + n - capacity(l);
     if (need_bytes <= 0) return CLG_OK;
     size_t need = size_t((need_bytes + C() - 1) / C());
-    std::lock_guard<std::mutex> g(pool_mu);
     if (need > free_segs.size())
       return fail(CLG_E_NOSPACE, "segment pool exhausted (need %zu, free %zu)", need, free_segs.size());
     for (size_t i = 0; i < need; ++i) {
@@ -512,16 +606,11 @@ struct clg_engine {
     l.tail.insert(l.tail.end(), b, b + n);
     l.writer += int32_t(n);
   }
-  std::shared_ptr<EpochStart> compute_if_absent(Log& l, int64_t e) {
-    auto it = l.epochs.find(e);
-    if (it != l.epochs.end()) return it->second;
-    auto es = std::allocate_shared<EpochStart>(EpochAlloc<EpochStart>(), EpochStart{e, l.writer});
-    l.epochs.emplace(e, es);
-    return es;
-  }
+  // epochStartOffsets.computeIfAbsent(e -> visibleWriterIndex); valid until the next insert
+  static EpochEnt* compute_if_absent(Log& l, int64_t e) { return l.epochs.emplace(e, l.writer); }
   int32_t bytes_to_send(const Log& l, int64_t epoch, int32_t phys) const {  // :384-395
     auto it = l.epochs.find(epoch + 1);
-    return (it != l.epochs.end() ? it->second->offset : l.writer) - phys;
+    return (it != l.epochs.end() ? it->offset : l.writer) - phys;
   }
 
   int get_log(uint32_t h, Log** out) {
@@ -650,7 +739,9 @@ struct clg_engine {
     CHK(flush());
     CHK(gwait());  // the scatter below writes segments an in-flight gather may read
     std::vector<clg::ScatterChunk> ch;
+    ch.reserve(n);
     size_t total = 0;
+    std::unique_lock<std::mutex> pool_guard(pool_mu);  // once for the batch, not per log
     for (uint32_t i = 0; i < n; ++i) {
       r[i].status = CLG_OK;
       Log* l;
@@ -659,7 +750,7 @@ struct clg_engine {
       const int32_t cur = l->writer - es->offset;
       const int32_t num_new = (r[i].offset_from_epoch + int32_t(r[i].len)) - cur;
       if (num_new <= 0) continue;
-      if ((r[i].status = ensure_space(*l, num_new)) != CLG_OK) continue;  // before the gap check (:136-143)
+      if ((r[i].status = ensure_space_locked(*l, num_new)) != CLG_OK) continue;  // before the gap check (:136-143)
       if (num_new > int32_t(r[i].len)) {
         r[i].status = fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d",
                            r[i].offset_from_epoch, r[i].len, cur);
@@ -681,6 +772,7 @@ struct clg_engine {
       reset_tail(*l);  // these bytes go to HBM only
       total += size_t(num_new);
     }
+    pool_guard.unlock();
     if (ch.empty()) return CLG_OK;
     const size_t db = ch.size() * sizeof(clg::ScatterChunk);
     CHK(h_desc.ensure(db));
@@ -701,13 +793,13 @@ struct clg_engine {
     auto it = l->epochs.find(epoch);
     if (it == l->epochs.end()) return CLG_OK;
     auto ci = l->consumers.find(k);
-    if (ci == l->consumers.end()) ci = l->consumers.emplace(k, Consumer{it->second, 0}).first;
+    if (ci == l->consumers.end()) ci = l->consumers.emplace(k, Consumer{EpochMap::ref(*it), 0}).first;
     Consumer& c = ci->second;
     if (c.es->id != epoch) {
       if (c.es->id > epoch)
         return fail(CLG_E_CONSUMER_BACKWARDS, "Consumer went backwards, current epoch %lld requested %lld",
                     (long long)c.es->id, (long long)epoch);
-      c.es = it->second;
+      c.es = EpochMap::ref(*it);
       c.offset = 0;
     }
     *out = bytes_to_send(*l, epoch, c.es->offset + c.offset) != 0;
@@ -774,23 +866,53 @@ struct clg_engine {
     return sync();
   }
 
-  // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
-  int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
-                      uint64_t total, void* out, uint32_t out_kind) {
-    if (runs.empty() || !n_pieces) return CLG_OK;
-    if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
-      return gather_runs_async(runs, segtab, n_pieces, total, out);
-    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
-    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
-    CHK(h_desc.ensure(hb));
-    CHK(d_desc.ensure(hb));
-    CHK(d_pieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
-    memcpy(h_desc.p, runs.data(), rb);
-    memcpy(h_desc.as<uint8_t>() + o_seg, segtab.data(), gb);
-    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
-    CHK(clg::launch_expand_pieces(d_desc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
-                                  reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
-                                  d_pieces.as<clg::GatherPiece>(), stream));
+  // Batched gather of log ranges (`runs`: one per request, output offsets in dst) by
+  // k_gather_seg: the runs are grouped by log (segtab_off identifies it), and the pieces of
+  // one segment (one per run reading it) run side by side on one XCD, so a segment that 8
+  // consumers' slices share comes from HBM once.  Host output: staged in d_out, copied back, waited
+  // for.  Device output with CLG_F_ASYNC_SLICE: on gstream, not waited for.
+  int gather_runs(std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint64_t total, void* out,
+                  uint32_t out_kind) {
+    if (runs.empty()) return CLG_OK;
+    auto by_log = [](const clg::SegSpan& a, const clg::SegSpan& b) { return a.segtab_off < b.segtab_off; };
+    if (!std::is_sorted(runs.begin(), runs.end(), by_log)) std::stable_sort(runs.begin(), runs.end(), by_log);
+    std::vector<clg::SliceGroup> groups;
+    groups.reserve(runs.size());
+    uint32_t n_jobs = 0;
+    const uint32_t c = C();
+    for (uint32_t i = 0; i < uint32_t(runs.size());) {
+      uint32_t j = i, lo = UINT32_MAX, hi = 0;
+      for (; j < uint32_t(runs.size()) && runs[j].segtab_off == runs[i].segtab_off; ++j) {
+        lo = std::min(lo, runs[j].phys / c);
+        hi = std::max(hi, (runs[j].phys + runs[j].len - 1) / c + 1);
+      }
+      groups.push_back(clg::SliceGroup{runs[i].segtab_off, lo, hi, i, j, n_jobs, 0});
+      n_jobs += (hi - lo) * (j - i);  // (segment, run) slots
+      i = j;
+    }
+    const uint64_t algo = (cfg.flags & CLG_F_TIMING) ? slice_bytes(runs, groups, total) : 0;  // (stats only)
+    if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE)) {
+      // on gstream, after everything already queued on `stream` (appends); returns without
+      // waiting.  Its own descriptor buffers, so the next decode on `stream` does not touch
+      // them; the gather two calls ago released this set.
+      const uint32_t set = gseq++ & 1u;
+      if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));
+      else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
+      SliceLayout L;
+      CHK(stage_groups(runs, groups, segtab, h_gdesc[set], d_gdesc[set], &L));
+      // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
+      // its call returned, and decodes only read the pool
+      HIPCHK(hipMemcpyAsync(d_gdesc[set].p, h_gdesc[set].p, L.hb, hipMemcpyHostToDevice, gstream));
+      CHK(timed("slice_gather", algo, [&] {
+        return launch_groups(d_gdesc[set], L, n_jobs, static_cast<uint8_t*>(out), gstream);
+      }, gstream));
+      HIPCHK(hipEventRecord(gdone[set], gstream));
+      g_pending = true;
+      return CLG_OK;
+    }
+    SliceLayout L;
+    CHK(stage_groups(runs, groups, segtab, h_desc, d_desc, &L));
+    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, L.hb, hipMemcpyHostToDevice, stream));
     uint8_t* dout;
     if (out_kind == CLG_MEM_DEVICE) {
       dout = static_cast<uint8_t*>(out);
@@ -798,43 +920,59 @@ struct clg_engine {
       CHK(d_out.ensure(total));
       dout = d_out.as<uint8_t>();
     }
-    CHK(timed("slice_gather", 2 * total, [&] {
-      return clg::launch_gather(d_pieces.as<clg::GatherPiece>(), n_pieces, dout, stream);
-    }));
+    CHK(timed("slice_gather", algo, [&] { return launch_groups(d_desc, L, n_jobs, dout, stream); }));
     if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
     return sync();
   }
-
-  // Device-output slice gather on gstream, after everything already queued on `stream`
-  // (appends); returns without waiting.  Its own descriptor buffers, so the next decode
-  // on `stream` does not touch them; the next gather waits for this one first.
-  int gather_runs_async(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
-                        uint64_t total, void* out) {
-    const uint32_t set = gseq++ & 1u;
-    if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
-    else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
-    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
-    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
-    PinBuf& hd = h_gdesc[set];
-    DevBuf& dd = d_gdesc[set];
-    DevBuf& dp = d_gpieces[set];
-    CHK(hd.ensure(hb));
-    CHK(dd.ensure(hb));
-    CHK(dp.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
-    memcpy(hd.p, runs.data(), rb);
-    memcpy(hd.as<uint8_t>() + o_seg, segtab.data(), gb);
-    // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
-    // its call returned, and decodes only read the pool
-    HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
-    CHK(clg::launch_expand_pieces(dd.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
-                                  reinterpret_cast<const uint32_t*>(dd.as<uint8_t>() + o_seg), pool, C(),
-                                  dp.as<clg::GatherPiece>(), gstream));
-    CHK(timed("slice_gather", 2 * total, [&] {
-      return clg::launch_gather(dp.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
-    }, gstream));
-    HIPCHK(hipEventRecord(gdone[set], gstream));
-    g_pending = true;
+  // Where a batched gather's descriptors lie in its staged buffer (byte offsets).
+  struct SliceLayout {
+    size_t o_runs = 0, o_seg = 0, hb = 0;
+    uint32_t n_groups = 0;
+  };
+  int stage_groups(const std::vector<clg::SegSpan>& runs, const std::vector<clg::SliceGroup>& groups,
+                   const std::vector<uint32_t>& segtab, PinBuf& hd, DevBuf& dd, SliceLayout* L) {
+    const size_t gb = groups.size() * sizeof(clg::SliceGroup), rb = runs.size() * sizeof(clg::SegSpan),
+                 sb = segtab.size() * sizeof(uint32_t);
+    L->o_runs = (gb + 15) & ~size_t(15);
+    L->o_seg = (L->o_runs + rb + 15) & ~size_t(15);
+    L->hb = L->o_seg + sb;
+    L->n_groups = uint32_t(groups.size());
+    CHK(hd.ensure(L->hb));
+    CHK(dd.ensure(L->hb));
+    memcpy(hd.p, groups.data(), gb);
+    memcpy(hd.as<uint8_t>() + L->o_runs, runs.data(), rb);
+    memcpy(hd.as<uint8_t>() + L->o_seg, segtab.data(), sb);
     return CLG_OK;
+  }
+  int launch_groups(const DevBuf& dd, const SliceLayout& L, uint32_t n_jobs, uint8_t* dout, hipStream_t on) {
+    const uint8_t* d = dd.as<uint8_t>();
+    return clg::launch_gather_seg(reinterpret_cast<const clg::SliceGroup*>(d), L.n_groups, n_jobs,
+                                  reinterpret_cast<const clg::SegSpan*>(d + L.o_runs),
+                                  reinterpret_cast<const uint32_t*>(d + L.o_seg), pool, C(), dout, on);
+  }
+  // A batched gather's algorithmic bytes: every source byte some run
+  // reads, once (the union of the runs' ranges per log), every byte written, and 16 B of
+  // request / result metadata per run.
+  static uint64_t slice_bytes(const std::vector<clg::SegSpan>& runs, const std::vector<clg::SliceGroup>& groups,
+                              uint64_t total) {
+    uint64_t read = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> iv;
+    for (const auto& g : groups) {
+      if (g.run_hi - g.run_lo == 1) {
+        read += runs[g.run_lo].len;
+        continue;
+      }
+      iv.clear();
+      for (uint32_t i = g.run_lo; i < g.run_hi; ++i) iv.emplace_back(runs[i].phys, runs[i].phys + runs[i].len);
+      std::sort(iv.begin(), iv.end());
+      uint32_t end = 0;
+      for (const auto& x : iv) {
+        const uint32_t a = std::max(x.first, end);
+        if (x.second > a) read += x.second - a;
+        end = std::max(end, x.second);
+      }
+    }
+    return read + total + 16 * uint64_t(runs.size());
   }
 
   // host_only: serve the slice from the host tail or return kNeedGpu with nothing changed
@@ -879,9 +1017,9 @@ struct clg_engine {
     int32_t s = 0;
     auto it = l.epochs.find(start_epoch);
     if (it != l.epochs.end())
-      s = it->second->offset;
+      s = it->offset;
     else if (!l.epochs.empty())
-      s = l.epochs.begin()->second->offset;
+      s = l.epochs.begin()->offset;
     *start = s;
     *nb = l.writer - s;
     if (*nb < 0 || s < 0 || l.writer > capacity(l))  // makeDeltaUnsafe IndexOutOfBounds
@@ -918,9 +1056,8 @@ struct clg_engine {
   // notifyCheckpointComplete :398-435 (flushes first so no staged byte lives in a dropped
   // component).
   int checkpoint_complete(Log& l, int64_t cp) {
-    auto following = compute_if_absent(l, cp);
+    const int32_t R = compute_if_absent(l, cp)->offset;  // (read before the erase moves entries)
     l.epochs.erase_below(cp);
-    const int32_t R = following->offset;
     if (R < 0 || R > l.writer) return fail(CLG_E_STATE, "readerIndex %d outside [0, %d]", R, l.writer);
     int32_t move = 0;
     if (R != 0) {
@@ -933,9 +1070,9 @@ struct clg_engine {
         move = int32_t(drop * C());
       }
       for (size_t i = 0; i < drop; ++i) free_segs.push_back(l.segs[i]);
-      l.segs.erase(l.segs.begin(), l.segs.begin() + long(drop));
+      l.segs.erase_front(drop);
     }
-    for (auto& e : l.epochs) e.second->offset -= move;
+    l.epochs.rebase(move);
     l.writer -= move;
     l.flushed -= move;
     l.tail_start -= move;
@@ -994,9 +1131,10 @@ struct clg_engine {
     if (const uint32_t U = p.unit) {  // device planning
       const uint32_t cnt = len > 0 ? (uint32_t(start + len - 1) / U - uint32_t(start) / U + 1) : 0;
       p.spans.push_back(clg::SpanDesc{p.n_tiles, cnt, uint64_t(len)});
-      if (cnt) {
-        p.runs.push_back(clg::SegSpan{p.segtab.size(), uint32_t(start), uint32_t(len), s, p.n_tiles, 0});
-        p.segtab.insert(p.segtab.end(), l.segs.begin(), l.segs.end());
+      if (cnt) {  // only the segments the span covers go into the table (phys rebased on them)
+        const uint32_t s0 = uint32_t(start) / C(), s1 = uint32_t(start + len - 1) / C() + 1;
+        p.runs.push_back(clg::SegSpan{p.segtab.size(), uint32_t(start) - s0 * C(), uint32_t(len), s, p.n_tiles, 0});
+        p.segtab.insert(p.segtab.end(), l.segs.begin() + s0, l.segs.begin() + s1);
       }
       p.n_tiles += cnt;
       return;
@@ -1173,6 +1311,7 @@ struct clg_engine {
     uint64_t log_bytes = 0;
     bool jser = false;
     hipEvent_t ea = nullptr, eb = nullptr;  // emit's timing events
+    hipEvent_t pa = nullptr, pb = nullptr;  // the whole pipeline's (count start .. emit end)
     // for the per-span fallback: the run's control words and outputs, and whether only
     // span-local reasons aborted it (chains that went wrong, not a timeout / table overflow)
     clg::FusedCtl ctl{};
@@ -1223,10 +1362,15 @@ struct clg_engine {
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
-    // The whole sequence, enqueued on `stream`; `ev` (timing) brackets jser, count, offsets
-    // and emit.  (Captured as a hipGraph and replayed per batch shape it was no faster:
-    // 197 us for a 16-log decode either way, and the bench step unchanged.)
-    auto enqueue = [&](hipEvent_t* ev) -> int {
+    // The whole sequence; `ev` (timing) brackets jser, count, offsets and emit, `evp` the
+    // whole pipeline.  (Captured as a hipGraph and replayed per batch shape it was no
+    // faster: 197 us for a 16-log decode either way, and the bench step unchanged.)
+    // In parts (decode_parts): tiles split at scan-block multiples; jser + count of each
+    // part on `stream`, scan + emit of each part on `estream` once its count is done, so
+    // the instruction-bound count of part k + 1 runs beside the memory-bound emit of part k.
+    const uint32_t P = decode_parts(nt);
+    if (P > 1) stats["decode_parts"].launches += P;  // (the parts actually run; tests read it)
+    auto enqueue = [&](hipEvent_t* ev, hipEvent_t* evp) -> int {
       CHK(enqueue_plan(p, L, d_ztiles));
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
@@ -1234,24 +1378,48 @@ struct clg_engine {
       HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
       HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
-      for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
-        if (ph == 3 && !jser) continue;
-        const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
-        if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
-        CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
-        if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
+      if (evp) HIPCHK(hipEventRecord(evp[0], stream));
+      if (P <= 1) {
+        for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
+          if (ph == 3 && !jser) continue;
+          const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
+          if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
+          CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
+          if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
+        }
+      } else {
+        uint32_t lo = 0;
+        for (uint32_t k = 0; k < P; ++k) {
+          const uint32_t hi = k + 1 == P ? nt : (uint32_t(uint64_t(nt) * (k + 1) / P) / clg::kZScanBlock) * clg::kZScanBlock;
+          clg::FusedCtl c = ctl;
+          c.t_lo = lo;
+          c.t_hi = hi;
+          if (jser) CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, stream, 3));
+          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, stream, 0, k ? count_grid_pct() : 0));
+          HIPCHK(hipEventRecord(part_ev[k], stream));
+          HIPCHK(hipStreamWaitEvent(estream, part_ev[k], 0));
+          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, estream, 1));
+          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, estream, 2));
+          lo = hi;
+        }
+        HIPCHK(hipEventRecord(part_ev[P], estream));
+        HIPCHK(hipStreamWaitEvent(stream, part_ev[P], 0));
       }
+      if (evp) HIPCHK(hipEventRecord(evp[1], stream));
       // read the span ranges and abort words (emit ran right behind the scan: it returns at
       // once when the batch aborted, and its stores are bounded by the output capacity)
       HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
       if (jser) CHK(jarena_note(0));
       return CLG_OK;
     };
-    hipEvent_t ev[8] = {};
-    if (timing)
-      for (auto& e : ev) e = get_event();
-    CHK(enqueue(timing ? ev : nullptr));
-    if (timing) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
+    hipEvent_t ev[8] = {}, evp[2] = {};
+    if (timing) {
+      if (P <= 1)
+        for (auto& e : ev) e = get_event();
+      for (auto& e : evp) e = get_event();
+    }
+    CHK(enqueue(timing && P <= 1 ? ev : nullptr, timing ? evp : nullptr));
+    if (timing && P <= 1) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
       if (jser) timings.push_back(PendingTiming{"decode_jser", ev[0], ev[1], log_bytes});
       else ev_pool.insert(ev_pool.end(), {ev[0], ev[1]});
       timings.push_back(PendingTiming{"decode_count", ev[2], ev[3], log_bytes});
@@ -1259,7 +1427,31 @@ struct clg_engine {
       r->ea = ev[6];
       r->eb = ev[7];
     }
+    if (timing) {
+      r->pa = evp[0];
+      r->pb = evp[1];
+    }
     return CLG_OK;
+  }
+  // Parts a fast decode runs in: clg_config.decode_parts, else CLONOS_DECODE_PARTS (tuning
+  // aid), else the default; only batches of at least two scan blocks per part are split.
+  static constexpr int kDefaultParts = 1;
+  uint32_t decode_parts(uint32_t nt) const {
+    static const int env = [] {
+      const char* s = getenv("CLONOS_DECODE_PARTS");
+      return s ? atoi(s) : 0;
+    }();
+    const int v = cfg.decode_parts ? int(cfg.decode_parts) : env ? env : kDefaultParts;
+    uint32_t P = uint32_t(std::max(1, std::min(v, int(kMaxParts))));
+    while (P > 1 && nt / P < 2 * clg::kZScanBlock) --P;
+    return P;
+  }
+  static uint32_t count_grid_pct() {  // CLONOS_COUNT_GRID_PCT: the count grid of parts after the first
+    static const int v = [] {
+      const char* s = getenv("CLONOS_COUNT_GRID_PCT");
+      return s ? atoi(s) : 0;
+    }();
+    return uint32_t(std::max(0, std::min(v, 100)));
   }
 
   int finish_fused(const DecodePlan& p, FusedRun& r, clg_decoded* out, uint64_t* span_rec_base, bool* aborted,
@@ -1292,6 +1484,10 @@ struct clg_engine {
       if (ea) {
         ev_pool.push_back(ea);
         ev_pool.push_back(eb);
+      }
+      if (r.pa) {
+        ev_pool.push_back(r.pa);
+        ev_pool.push_back(r.pb);
       }
       *aborted = true;
       // Serializable records were met without tables: other aborts may be consequences
@@ -1328,6 +1524,8 @@ struct clg_engine {
     }
     if (span_rec_base) span_rec_base[ns] = nrec;
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    // the pipeline's algorithmic bytes: log bytes read + the SoA rows
+    if (r.pa) timings.push_back(PendingTiming{"decode_pipeline", r.pa, r.pb, log_bytes + 13 * nrec + 25 * nwide});
     return finish_out(out, nrec, nwide);
   }
   // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
@@ -1755,6 +1953,7 @@ void clg_config_default(clg_config* cfg) {
   cfg->host_tail_bytes = 16384;    // one component of each log's tail kept on the host
   cfg->ifl_segment_bytes = 32768;  // the in-flight log's pool: Flink's 32 KiB memory segments
   cfg->ifl_pool_segments = 4096;   // 128 MiB
+  cfg->decode_parts = 0;           // the engine's default (decode_parts())
 }
 
 int clg_abi_version(void) { return CLG_ABI_VERSION; }
@@ -1790,6 +1989,8 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
       HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
   }
   HIPCHK(hipEventCreateWithFlags(&e->gready, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&e->estream, hipStreamNonBlocking));
+  for (auto& ev : e->part_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, pool_bytes + 2 * kPoolGuard));  // guards: aligned over-reads either side
@@ -1830,6 +2031,9 @@ void clg_engine_destroy(clg_engine* e) {
   hipStreamDestroy(e->stream);
   if (e->gstream) hipStreamDestroy(e->gstream);
   if (e->gready) hipEventDestroy(e->gready);
+  if (e->estream) hipStreamDestroy(e->estream);
+  for (auto ev : e->part_ev)
+    if (ev) hipEventDestroy(ev);
   for (auto ev : e->gdone)
     if (ev) hipEventDestroy(ev);
   delete e;
@@ -1974,7 +2178,7 @@ int clg_log_length(clg_engine* e, uint32_t h, int32_t* out) {  // :180-192
   LOG_GUARD(e, h);
   Log* l;
   CHK(e->get_log(h, &l));
-  *out = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
+  *out = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->offset;
   return CLG_OK;
 }
 
@@ -1985,7 +2189,7 @@ int clg_log_length_batch(clg_engine* e, const uint32_t* log, uint32_t n, int32_t
   for (uint32_t i = 0; i < n; ++i) {
     Log* l;
     CHK(e->get_log(log[i], &l));
-    const int32_t v = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->second->offset;
+    const int32_t v = l->epochs.empty() ? l->writer : l->writer - l->epochs.begin()->offset;
     if (out) out[i] = v;
     t += uint64_t(v);
   }
@@ -2052,8 +2256,8 @@ int clg_log_get_state(clg_engine* e, uint32_t h, clg_log_state* st, int64_t* ids
   int32_t i = 0;
   for (auto& ep : l->epochs) {
     if (i < cap) {
-      if (ids) ids[i] = ep.first;
-      if (offs) offs[i] = ep.second->offset;
+      if (ids) ids[i] = ep.id;
+      if (offs) offs[i] = ep.offset;
     }
     ++i;
   }
@@ -2094,8 +2298,6 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   std::vector<clg::SegSpan> runs;
   std::vector<uint32_t> segtab;
   std::unordered_map<uint32_t, uint64_t> tab_of;
-  uint32_t n_pieces = 0;
-  const uint32_t C = e->C();
   uint64_t dst = 0;
   for (uint32_t i = 0; i < n; ++i) {
     Log* l;
@@ -2110,8 +2312,7 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
         ti = tab_of.emplace(log[i], segtab.size()).first;
         segtab.insert(segtab.end(), l->segs.begin(), l->segs.end());
       }
-      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, n_pieces, 0});
-      n_pieces += uint32_t(s + nb - 1) / C - uint32_t(s) / C + 1;
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, 0, 0});
     }
     dst += uint64_t(nb);
   }
@@ -2119,7 +2320,7 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   if (!out) return CLG_OK;  // sizes only
   if (dst > cap) return fail(CLG_E_CAPACITY, "getDeterminants batch needs %llu bytes", (unsigned long long)dst);
   CHK(e->flush());
-  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
+  return e->gather_runs(runs, segtab, dst, out, out_kind);
 }
 
 int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res, void* out, uint64_t cap,
@@ -2132,8 +2333,6 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
   std::vector<uint32_t> segtab;
   std::unordered_map<uint32_t, uint64_t> tab_of;  // log -> its segment indices in segtab
   runs.reserve(n);
-  uint32_t n_pieces = 0;
-  const uint32_t C = e->C();
   uint64_t dst = 0;
   for (uint32_t i = 0; i < n; ++i) {
     clg_slice_res& r = res[i];
@@ -2172,13 +2371,12 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
         ti = tab_of.emplace(reqs[i].log, segtab.size()).first;
         segtab.insert(segtab.end(), segs.begin(), segs.end());
       }
-      runs.push_back(clg::SegSpan{ti->second, uint32_t(phys), uint32_t(nb), dst, n_pieces, 0});
-      n_pieces += uint32_t(phys + nb - 1) / C - uint32_t(phys) / C + 1;
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(phys), uint32_t(nb), dst, 0, 0});
     }
     dst += uint64_t(nb);
   }
   if (total) *total = dst;
-  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
+  return e->gather_runs(runs, segtab, dst, out, out_kind);
 }
 
 int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch, int32_t offset) {
@@ -2187,7 +2385,7 @@ int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch
   CHK(e->get_log(h, &l));
   auto it = l->epochs.find(epoch);
   if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)epoch);
-  l->consumers[ChKey{c.lo, c.hi}] = Consumer{it->second, offset};
+  l->consumers[ChKey{c.lo, c.hi}] = Consumer{EpochMap::ref(*it), offset};
   return CLG_OK;
 }
 
@@ -2205,7 +2403,7 @@ int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int3
     CHK(e->get_log(reqs[i].log, &l));
     auto it = l->epochs.find(reqs[i].epoch);
     if (it == l->epochs.end()) return fail(CLG_E_STATE, "epoch %lld not in log", (long long)reqs[i].epoch);
-    l->consumers[ChKey{reqs[i].consumer.lo, reqs[i].consumer.hi}] = Consumer{it->second, offsets[i]};
+    l->consumers[ChKey{reqs[i].consumer.lo, reqs[i].consumer.hi}] = Consumer{EpochMap::ref(*it), offsets[i]};
   }
   return CLG_OK;
 }
@@ -2294,6 +2492,8 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
   // by value: the robust fallback may re-plan when the decode is settled (the logs' ranges
   // cannot change before that: every call that could change them settles first)
   auto build = [e, hs = std::move(hs), st = std::move(st), nb = std::move(nb)](clg_engine::DecodePlan& p, uint32_t T) {
+    p.spans.reserve(hs.size());
+    p.runs.reserve(hs.size());
     for (uint32_t i = 0; i < uint32_t(hs.size()); ++i) e->plan_log_span(p, e->logs[hs[i]], st[i], nb[i], i, T);
   };
   return e->decode_async(build, total, out, span_rec_base);

@@ -285,13 +285,28 @@ class Replicator:
 MERGE_GUARD = 64  # bytes before and after the received winners (device gathers read aligned 16-byte words)
 
 
-@dataclass
 class MergedCopies:
     """The winners delivered to one rank: every log's winning copy inside one buffer (an RCCL
     receive buffer in HBM, or host memory over gloo) at place[gid] = (offset, length), with
-    MERGE_GUARD bytes around them, ready for clg_replay_prepare_device as they lie."""
-    buf: object
-    place: Dict[int, Tuple[int, int]]
+    MERGE_GUARD bytes around them, ready for clg_replay_prepare_device as they lie.  Also as
+    arrays (gids, offsets, lengths), which the batched consumers read."""
+
+    def __init__(self, buf, place: Optional[Dict[int, Tuple[int, int]]] = None, gids=None, offs=None, lens=None):
+        self.buf = buf
+        if place is not None:
+            gids = np.fromiter(place.keys(), np.int64, len(place))
+            ol = np.array(list(place.values()), np.int64).reshape(-1, 2)
+            offs, lens = ol[:, 0], ol[:, 1]
+        self.gids = np.asarray(gids if gids is not None else [], np.int64)
+        self.offs = np.asarray(offs if offs is not None else [], np.int64)
+        self.lens = np.asarray(lens if lens is not None else [], np.int64)
+        self._place = place
+
+    @property
+    def place(self) -> Dict[int, Tuple[int, int]]:
+        if self._place is None:
+            self._place = dict(zip(self.gids.tolist(), zip(self.offs.tolist(), self.lens.tolist())))
+        return self._place
 
     def bytes_of(self, gid: int) -> bytes:
         o, n = self.place[gid]
@@ -323,13 +338,22 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     if world > 255:
         raise ValueError("rank must fit the packed key's low byte")
     backend = dist.get_backend(group)
-    failed = sorted(set(int(v) for v in failed))
-    gids = np.nonzero(np.isin(table.vertex, failed))[0]
+    # every per-log step below is an array operation: a failed task has 129 logs at p=128
+    fv = np.unique(np.fromiter((int(v) for v in failed), np.int64))
+    gids = np.nonzero(np.isin(table.vertex, fv))[0]
     n = len(gids)
+    vslot = np.searchsorted(fv, table.vertex[gids])  # each log's failed vertex, as an index into fv
+    ep_of = np.array([start_epochs[int(v)] for v in fv], np.int64)
+    dest = np.array([dest_of[int(v)] for v in fv], np.int64)[vslot]
+    ck = np.fromiter(copies.keys(), np.int64, len(copies))
+    cv = np.fromiter(copies.values(), np.int64, len(copies))
+    srt = np.argsort(ck)
+    ck, cv = ck[srt], cv[srt]
+    pos = np.minimum(np.searchsorted(ck, gids), max(len(ck) - 1, 0))
+    held = np.nonzero(ck[pos] == gids)[0] if len(ck) else np.zeros(0, np.int64)  # logs this rank holds
+    handles = cv[pos[held]]
+    epochs = ep_of[vslot[held]]
     key = np.full(max(n, 1), -1, np.int64)
-    held = np.array([k for k, g in enumerate(gids) if int(g) in copies], np.int64)
-    handles = np.array([copies[int(gids[k])] for k in held], np.int64)
-    epochs = np.array([start_epochs[int(table.vertex[gids[k]])] for k in held], np.int64)
     if len(held):
         key[held] = (io.copy_lengths(handles, epochs) << 8) | rank
     dev = device if backend == "nccl" else "cpu"
@@ -338,15 +362,14 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     win = kt.cpu().numpy()[:n]
     win_rank = np.where(win >= 0, win & 0xFF, -1)
     win_len = np.where(win >= 0, win >> 8, 0)
-    dest = np.array([dest_of[int(table.vertex[g])] for g in gids], np.int64)
     mine = np.nonzero(win_rank == rank)[0]
-    order = np.concatenate([mine[dest[mine] == d] for d in range(world)]) if len(mine) else mine
-    send_split = np.array([int(win_len[mine[dest[mine] == d]].sum()) for d in range(world)], np.int64)
-    recv_split = np.array([int(win_len[(win_rank == s) & (dest == rank)].sum()) for s in range(world)], np.int64)
+    order = mine[np.argsort(dest[mine], kind="stable")]  # by destination, then log order
+    send_split = np.bincount(dest[mine], weights=win_len[mine], minlength=world).astype(np.int64)
+    inbound = np.nonzero((win_rank >= 0) & (dest == rank))[0]
+    recv_split = np.bincount(win_rank[inbound], weights=win_len[inbound], minlength=world).astype(np.int64)
     send = torch.empty(max(int(send_split.sum()), 1), dtype=torch.uint8, device=device)
     if int(send_split.sum()):
-        pos = {int(gids[k]): i for i, k in enumerate(held)}
-        sel = np.array([pos[int(gids[k])] for k in order], np.int64)
+        sel = np.searchsorted(held, order)  # (every winner of this rank is a held log)
         got = io.copy_batch(handles[sel], epochs[sel], send, 0)
         if got != int(send_split.sum()):
             raise RuntimeError(f"logs changed during the merge ({got} != {int(send_split.sum())} bytes)")
@@ -356,11 +379,8 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     dist.all_to_all_single(buf[MERGE_GUARD:MERGE_GUARD + nrecv], s_in[:int(send_split.sum())],
                            output_split_sizes=recv_split.tolist(), input_split_sizes=send_split.tolist(),
                            group=group)
-    place = {}
-    o = MERGE_GUARD
-    for s_ in range(world):
-        for k in np.nonzero((win_rank == s_) & (dest == rank))[0]:
-            nb = int(win_len[k])
-            place[int(gids[k])] = (o, nb)
-            o += nb
-    return MergedCopies(buf, place)
+    # received in source-rank order, each source's winners in log order
+    recv = inbound[np.lexsort((inbound, win_rank[inbound]))]
+    lens = win_len[recv]
+    offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(recv) else lens
+    return MergedCopies(buf, gids=gids[recv], offs=offs, lens=lens)

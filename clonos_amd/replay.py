@@ -196,8 +196,8 @@ def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, Determ
     """The accumulated responses of failed vertices whose copies arrived by the cross-GPU merge
     (dist.merge_responses): entries point into the merge's receive buffer, in HBM under RCCL
     (prepare_replay(..., device_input=True)).  One batched put per vertex."""
-    gids = np.fromiter(merged.place.keys(), np.int64, len(merged.place))
-    place = np.array(list(merged.place.values()), np.uint64).reshape(-1, 2)
+    gids = merged.gids
+    place = np.stack([merged.offs, merged.lens], 1).astype(np.uint64) if len(gids) else np.zeros((0, 2), np.uint64)
     ids = table_ids(table)
     base = np.uint64(merged.buf.data_ptr())
     vert = table.vertex[gids] if len(gids) else np.zeros(0, np.int64)

@@ -133,7 +133,7 @@ def worker(rank, world, port, q):
         import response_ref as R
         mine = [v for v in failed if dest_of[v] == rank]
         if mine:
-            mcd = X.MergedCopies(mc.buf if mc.buf.is_cuda else mc.buf.to(dev), mc.place)  # gloo: lift to HBM
+            mcd = X.MergedCopies(mc.buf if mc.buf.is_cuda else mc.buf.to(dev), gids=mc.gids, offs=mc.offs, lens=mc.lens)  # gloo: lift to HBM
             jobs, sub_gids = [], []
             for v in mine:
                 sg = [int(g) for g in fg if int(table.vertex[g]) == v and not table.ids[g].is_main]

@@ -160,12 +160,15 @@ def test_truncate_all_cas_and_pool_reuse():
             assert log.getDeterminants(4) == D.encode(D.TimestampDeterminant(4)) * 40 + D.encode(D.TimestampDeterminant(5)) * 40
 
 
-@pytest.mark.parametrize("seg", [16, 512, 16384, 65536])
-def test_seek_batch_then_slice(seg):
+@pytest.mark.parametrize("seg,shuffle", [(16, False), (512, False), (16384, False), (65536, False), (512, True),
+                                         (16384, True)])
+def test_seek_batch_then_slice(seg, shuffle):
     """clg_consumer_seek_batch positions consumers exactly like clg_consumer_seek; the
-    batched slice (pieces planned on the device) returns each consumer's suffix."""
+    batched slice (one gather block per segment of a log, serving all of that log's
+    requests) returns each consumer's suffix, packed in request order also when the requests
+    of a log are scattered through the batch (shuffle)."""
     from clonos_amd import _lib
-    rng = np.random.default_rng(seg + 3)
+    rng = np.random.default_rng(seg + 3 + shuffle)
     with Engine(segment_bytes=seg, pool_segments=(1 << 21) // seg + 64) as eng:
         logs, bufs = [], []
         for v in range(6):
@@ -178,6 +181,8 @@ def test_seek_batch_then_slice(seg):
         for i in range(len(logs)):
             for c in range(5):
                 reqs.append((i, (c + 1, i), int(rng.integers(0, len(bufs[i]) + 1))))
+        if shuffle:
+            reqs = [reqs[j] for j in rng.permutation(len(reqs))]
         creq = (_lib.SliceReq * len(reqs))()
         cres = (_lib.SliceRes * len(reqs))()
         for k, (i, ch, _) in enumerate(reqs):

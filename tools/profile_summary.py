@@ -1,4 +1,4 @@
-"""Turn tools/profile_r02.sh output into the files committed under profiles/.
+"""Turn tools/profile.sh output into the files committed under profiles/.
 
   profiles/<tag>_bench.json                the bench line of the profile run
   profiles/<tag>_kernel_stats.csv          rocprofv3 --stats, config-2 bench (2 warm-up + 5 timed steps)
@@ -12,7 +12,7 @@
   profiles/pmc_traffic.json                HBM bytes per launch of the bench's kernels (bench.py reads it)
 
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB), FETCH doubled per the gfx950 calibration
-(MI355X_MICROARCH.md, HBM section).  usage: python tools/r02_profile_summary.py <dir> <tag>"""
+(MI355X_MICROARCH.md, HBM section).  usage: python tools/profile_summary.py <dir> <tag>"""
 import collections
 import csv
 import glob
@@ -68,7 +68,7 @@ def decode_table(prefix, log_bytes):
     dur = durations(f"{prefix}_sq1")
     out = {}
     for k, cs in sorted(merged.items()):
-        if not k.startswith("k_decode") and k != "k_gather":
+        if not k.startswith("k_decode") and not k.startswith("k_gather"):
             continue
         row = {"counters_per_dispatch": cs}
         d = {}
@@ -98,7 +98,7 @@ def decode_table(prefix, log_bytes):
 
 
 os.makedirs(prof, exist_ok=True)
-bench = open(f"{src}/bench.json").read().strip().splitlines()[-1]
+bench = [l for l in open(f"{src}/bench.json").read().strip().splitlines() if l.startswith("{")][-1]
 open(os.path.join(prof, f"{tag}_bench.json"), "w").write(bench + "\n")
 b = json.loads(bench)
 for d, name in (("trace", "kernel_stats"), ("c3_trace", "config3_kernel_stats"), ("ifl_trace", "inflight_kernel_stats")):
@@ -110,11 +110,9 @@ for k, v in durations("trace").items():
     timed[k] = {"dispatches": len(v), "timed_avg_ms": round(sum(last) / len(last), 5), "all_avg_ms": round(sum(v) / len(v), 5)}
 timed["note"] = ("timed_avg_ms: mean of the last %d dispatches of each kernel in the rocprofv3 kernel trace of "
                  "`bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config3 --no-inflight --no-isolated "
-                 "--no-config4` (the timed region); all_avg_ms includes the warm-up dispatches.  Under "
-                 "rocprofv3 --kernel-trace the two streams do not overlap (the trace shows the slice gather "
-                 "starting after the decode's emit), so these are isolated durations: compare them with the "
-                 "bench's kernels_isolated / roofline_isolated; the bench's timed-region figure (gather beside "
-                 "the decode) has no counterpart under the profiler" % STEPS)
+                 "--no-config4 --no-config1` (the timed region); all_avg_ms includes the warm-up dispatches.  "
+                 "Whether the two streams overlapped under the profiler shows in tools/timeline.py over the same "
+                 "trace: compare with the bench's kernels (timed region) if they did, kernels_isolated if not" % STEPS)
 json.dump(timed, open(os.path.join(prof, f"{tag}_kernel_timed.json"), "w"), indent=1)
 c3_bytes = b["config3"]["log_bytes"]
 pmc = {"config2": decode_table("c2", b["config"]["log_bytes_per_gpu"]),
@@ -123,7 +121,7 @@ pmc = {"config2": decode_table("c2", b["config"]["log_bytes_per_gpu"]),
                "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH correction)"}
 json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc_decode.json"), "w"), indent=1)
 traffic = {}
-NAMES = {"k_decode_count": "decode_count", "k_decode_emit": "decode_emit", "k_gather": "slice_gather"}
+NAMES = {"k_decode_count": "decode_count", "k_decode_emit": "decode_emit", "k_gather_seg": "slice_gather"}
 for k, name in NAMES.items():
     r = pmc["config2"].get(k, {}).get("derived", {})
     if "hbm_bytes" in r:
