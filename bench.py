@@ -266,12 +266,15 @@ def main():
     # the engine's stream) against its algorithmic bytes
     dec_ms = kern_iso["decode_pipeline"]["avg_ms"] if "decode_pipeline" in kern_iso else None
     dec_bytes = total_bytes + 13 * n_det
-    # the slice's algorithmic bytes: every source byte some consumer reads, once (per log the
-    # union of its consumers' suffixes), every byte written, 16 B of metadata per request
+    # the slice's algorithmic bytes: each slice read and written once, 16 B of
+    # metadata per request.  Beside it the minimum traffic: every source byte some consumer
+    # reads, once (per log the union of its consumers' suffixes), plus the writes -- the 8
+    # consumers of a log re-read its tail, which the caches (MALL) serve in part
+    slice_bytes = 2 * slice_total + 16 * n_req
     first_off = {}
     for i, _, off in cons:
         first_off[i] = min(first_off.get(i, off), off)
-    slice_bytes = sum(log_bytes[i] - o for i, o in first_off.items()) + slice_total + 16 * n_req
+    slice_min_bytes = sum(log_bytes[i] - o for i, o in first_off.items()) + slice_total + 16 * n_req
     roof_iso = None
     if dom and dom in kern_iso and kern_iso[dom]["gbs"]:
         roof_iso = {"kernel": dom, "achieved": kern_iso[dom]["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -326,7 +329,7 @@ def main():
             "step_roofline": {"note": "decode + slice algorithmic bytes / step time (slice gather overlaps the "
                                       "next decode on a second stream)", "achieved": round(step_gbs, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4)},
-            "slice": {"algo_bytes": slice_bytes},
+            "slice": {"algo_bytes": slice_bytes, "min_traffic_bytes": slice_min_bytes},
             "decode_path": ("robust (fast path aborted)" if "decode_fallback" in stats else
                             "three-pass (count -> scan -> emit)"),
             "kernels": kern,

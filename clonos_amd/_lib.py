@@ -87,7 +87,6 @@ class Config(C.Structure):
         ("host_tail_bytes", C.c_uint32),
         ("ifl_segment_bytes", C.c_uint32),
         ("ifl_pool_segments", C.c_uint32),
-        ("decode_parts", C.c_uint32),
     ]
 
 

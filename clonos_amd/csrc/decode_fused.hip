@@ -1000,8 +1000,7 @@ __global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
   __shared__ uint64_t s_w[4];
   if (ld_agent32(ctl.abort)) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint32_t nt = min(ctl.t_hi, ctl.n_tiles);
-  const uint32_t blk = blockIdx.x + ctl.t_lo / kZScanBlock, i0 = blk * kZScanBlock + tid * 4u;
+  const uint32_t nt = ctl.n_tiles, blk = blockIdx.x, i0 = blk * kZScanBlock + tid * 4u;
   uint64_t v[4], sum = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1021,23 +1020,17 @@ __global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
   if (tid == 255u) gp(ctl.boff)[blk] = run;  // block total (scan2 turns it into an offset)
 }
 
-// Blocks [b_lo, b_hi): their totals become offsets.  A later part (b_lo > 0) starts from
-// the previous part's last block: its offset + its tiles' last base + that tile's count.
-__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t b_lo, uint32_t b_hi) {
+__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_blocks) {
   __shared__ uint64_t s_w[16];
   if (ld_agent32(ctl.abort)) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, b = b_lo + tid;
-  const uint64_t v = b < b_hi ? gp(ctl.boff)[b] : 0ull;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint64_t v = tid < n_blocks ? gp(ctl.boff)[tid] : 0ull;
   const uint64_t incl = wave_incl_scan(v, lane);
   if (lane == 63u) s_w[wv] = incl;
   __syncthreads();
   uint64_t run = incl - v;
   for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
-  if (b_lo) {
-    const uint32_t tl = b_lo * kZScanBlock - 1;  // the previous part's last tile
-    run += gp(ctl.boff)[b_lo - 1] + gp(ctl.base)[tl] + gp(ctl.cnt)[tl];
-  }
-  if (b < b_hi) gp(ctl.boff)[b] = run;
+  if (tid < n_blocks) gp(ctl.boff)[tid] = run;
 }
 
 // Each span's record / wide-record range from the scan (the host reads them before the
@@ -1153,7 +1146,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
   __shared__ PosT s_pos[kWin];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  const uint32_t t = blockIdx.x + ctl.t_lo, lane = threadIdx.x;
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   const TileDesc td = tiles[t];
   if (ctl.skip_bad && gp(ctl.span_bad)[td.span]) return;  // the robust output fills this span
@@ -1163,7 +1156,8 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint64_t ea = sd.len - td.span_off + td.delta;
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  const u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
+  u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
+  if (lane * kZRegion >= hi) bits = u64x2{0, 0};  // past the tile (the lane path of small spans skips them)
   const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   JLPre pre{};
   if (J) pre = jl_prefetch(ctl, t, lane);
@@ -1323,6 +1317,96 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   }
 }
 
+// Small complete spans, one lane each.  A batch of many small logs (config 4: 65 536
+// subpartition logs of 320 bytes) gives one tile per span, and a wave spent on a 320-byte
+// tile costs as much as one on 8 KiB.  When tile t is a whole span of at most kZTiny bytes,
+// lane i takes tile t + i of the run of such tiles (at most 64, inside the chunk) and walks
+// its span alone from HBM through a 16-byte window: fixed-length records only (Order,
+// Timestamp, RNG, BufferBuilt, IgnoreCheckpoint -- their lengths need no field), with the
+// reference's bounds; it writes the tile's count and record-start bitmap words (emit reads
+// the words of the regions the tile reaches).  A record of another tag anywhere in the run
+// (TimerTrigger, SourceCheckpoint, Serializable: lengths from fields) sends the whole run to
+// the wave path; an invalid tag or a record past the span end marks the span bad (abort
+// reason 1), as count_tile does.  Returns the tiles handled (0: none; ~0: the batch aborts).
+constexpr uint32_t kZTiny = 1024;
+__device__ __forceinline__ uint32_t tiny_tiles(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                               const FusedCtl& ctl, const uint32_t t, const uint32_t t1,
+                                               const uint32_t lane) {
+  const uint32_t ti = t + lane;
+  TileDesc td{};
+  bool ok = false;
+  if (ti < t1) {
+    td = tiles[ti];
+    const SpanDesc sd = spans[td.span];
+    ok = sd.n_tiles == 1 && td.span_off == 0 && td.len > 0 && td.len <= kZTiny && td.len == sd.len &&
+         !(ctl.skip_bad && gp(ctl.span_bad)[td.span]);
+  }
+  const uint64_t okm = __ballot(ok);
+  const uint32_t m = (uint32_t)__builtin_ctzll(~okm);  // the run: leading lanes
+  if (m == 0) return 0;
+  // 0 ok, 1 invalid record (a bad tag or a record past the span end), 3 a tag this path does not take
+  uint32_t why = 0, rec = 0, wide = 0;
+  if (lane < m) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
+    const uint32_t end = td.delta + td.len;
+    uint32_t a = td.delta, wb = 0xFFFFFFFFu, cur = 0;
+    u32x4 w{};
+    uint64_t blo = 0, bhi = 0;
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    auto* bits = gp(reinterpret_cast<u64x2*>(ctl.bits)) + (uint64_t)ti * 64;
+    // fixed lengths by tag (0: takes fields or invalid)
+    constexpr uint32_t kLut = 2u | 9u << 4 | 5u << 8 | 13u << 24 | 5u << 28;
+    while (a < end) {
+      if ((a >> 4) != wb) {  // the 16-byte window holding the tag
+        wb = a >> 4;
+        w = src[wb];
+      }
+      const uint32_t q = a & 15u;
+      const uint32_t dw = q < 8u ? (q < 4u ? w.x : w.y) : (q < 12u ? w.z : w.w);
+      const uint32_t tg = (dw >> (8u * (q & 3u))) & 0xFFu;
+      const uint32_t L = tg < 8u ? (kLut >> (4u * tg)) & 0xFu : 0u;
+      if (!L) {
+        why = (tg == CLG_TAG_SERIALIZABLE || tg == CLG_TAG_TIMER_TRIGGER || tg == CLG_TAG_SOURCE_CHECKPOINT) ? 3u : 1u;
+        break;
+      }
+      if (a + L > end) {  // (the true chain's bound: an invalid record, count_tile's reason 1)
+        why = 1u;
+        break;
+      }
+      for (const uint32_t r = a >> 7; cur < r; ++cur) {  // the regions before this start are complete
+        u64x2 v;
+        v.x = blo;
+        v.y = bhi;
+        bits[cur] = v;
+        blo = bhi = 0;
+      }
+      const uint32_t i = a & 127u;
+      if (i < 64u) blo |= 1ull << i; else bhi |= 1ull << (i - 64u);
+      ++rec;
+      wide += tg == CLG_TAG_IGNORE_CHECKPOINT ? 1u : 0u;
+      a += L;
+    }
+    if (!why) {
+      for (const uint32_t r = (end - 1) >> 7; cur <= r; ++cur) {
+        u64x2 v;
+        v.x = blo;
+        v.y = bhi;
+        bits[cur] = v;
+        blo = bhi = 0;
+      }
+      gp(ctl.cnt)[ti] = pack_cnt(rec, wide);
+    }
+  }
+  if (__any(why == 3u)) return 0;  // the run takes the wave path (its words are rewritten there)
+  if (lane < m && why) {
+    raise_abort(ctl, why, ti);
+    if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + td.span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!ctl.span_bad && __any(why != 0u)) return 0xFFFFFFFFu;  // the batch aborts (no per-span fallback)
+  return m;
+}
+
 // Pass 1 kernel.  Persistent grid (at most what the device keeps resident, see
 // launch_decode_fused); block b decodes the contiguous chunk of tiles [b K, (b + 1) K).
 // Inside a chunk a tile's entry is its predecessor's true exit.  Across chunks: each block
@@ -1341,9 +1425,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   constexpr bool kLm = CLG_COUNT_LM != 0;  // J: the image becomes the step-code map (build_lm)
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
-  const uint32_t tl = ctl.t_lo, th = min(ctl.t_hi, nt);
-  const uint32_t K = (th - tl + gridDim.x - 1) / gridDim.x;
-  const uint32_t t0 = tl + blockIdx.x * K, t1 = min(th, t0 + K);
+  const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
+  const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
   if (t0 >= t1) return;
   // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
   uint32_t x_pub = kZCanon;
@@ -1368,6 +1451,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
+    if (!J && z.first && z.last && z.td.len <= kZTiny && !ctl.nodep && !ctl.prof) {
+      const uint32_t m = tiny_tiles(tiles, spans, ctl, t, t1, lane);  // small whole spans, a lane each
+      if (m == 0xFFFFFFFFu) return;
+      if (m) {
+        t += m - 1;
+        continue;
+      }
+    }
     const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
@@ -1627,8 +1718,7 @@ __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__
   __shared__ uint32_t s_img[kZJRows * kZPitch];
   __shared__ uint32_t s_cand[kZJCap];
   bool flagged = false;
-  const uint32_t th = min(ctl.t_hi, ctl.n_tiles);
-  for (uint32_t t = ctl.t_lo + blockIdx.x; t < th; t += gridDim.x) {
+  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
     jser_tile(tiles, spans, ctl, s_img, s_cand, t, threadIdx.x, &flagged);
     __syncthreads();  // the image is reused by the next tile
   }
@@ -1642,7 +1732,6 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
   const uint32_t n = min(ld_agent32(ctl.jwork), ctl.jwork_cap);
   for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
     const uint32_t item = ctl.jwork[1 + i], t = item / kZJCap;
-    if (t < ctl.t_lo || t >= ctl.t_hi) continue;  // another part's candidate
     const TileDesc td = tiles[t];
     const SpanDesc sd = spans[td.span];
     const uint32_t a = ctl.jpos[item];
@@ -1678,14 +1767,24 @@ int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
   return launch_status(hipGetLastError());
 }
 
+// Checked launch: a configuration error names its kernel and grid (stderr) and is returned.
+#define ZLAUNCH(k, grid, block, ...)                                                                     \
+  do {                                                                                                  \
+    hipLaunchKernelGGL(k, grid, block, __VA_ARGS__);                                                    \
+    const hipError_t le_ = hipGetLastError();                                                           \
+    if (le_ != hipSuccess) {                                                                            \
+      fprintf(stderr, "[clonos] launch of %s (grid %u, block %u) failed: %s\n", #k, (unsigned)dim3(grid).x, \
+              (unsigned)dim3(block).x, hipGetErrorString(le_));                                        \
+      return launch_status(le_);                                                                        \
+    }                                                                                                   \
+  } while (0)
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase, uint32_t grid_pct) {
+                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase) {
   if (!n_tiles) return CLG_OK;
+  if (const hipError_t pre = hipGetLastError(); pre != hipSuccess)  // a stale error is not this launch's
+    fprintf(stderr, "[clonos] HIP error pending before the decode launch: %s\n", hipGetErrorString(pre));
   ctl.n_tiles = n_tiles;
-  ctl.t_hi = min(ctl.t_hi, n_tiles);
-  if (ctl.t_lo >= ctl.t_hi) return CLG_OK;
-  if (ctl.t_lo % kZScanBlock) return CLG_E_INVALID_ARG;  // parts start on a scan block
-  const uint32_t nt = ctl.t_hi - ctl.t_lo;  // tiles of this launch
+  const uint32_t nt = n_tiles;
   hipStream_t st = (hipStream_t)stream;
   if (phase == 0) {
     static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
@@ -1699,25 +1798,22 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
         return CLG_E_DEVICE;
       resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
     }
-    uint32_t cap = (uint32_t)resident[j];
-    if (grid_pct && grid_pct < 100) cap = max(1u, cap * grid_pct / 100u);  // a part beside another part's emit
-    const uint32_t grid = nt < cap ? nt : cap;
+    const uint32_t grid = nt < (uint32_t)resident[j] ? nt : (uint32_t)resident[j];
     if (j)
-      hipLaunchKernelGGL(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+      ZLAUNCH(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
     else
-      hipLaunchKernelGGL(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+      ZLAUNCH(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {
-    const uint32_t b_lo = ctl.t_lo / kZScanBlock, b_hi = (ctl.t_hi + kZScanBlock - 1) / kZScanBlock;
-    if (b_hi - b_lo > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per part: the host splits
-    hipLaunchKernelGGL(k_decode_scan1, dim3(b_hi - b_lo), dim3(256), 0, st, ctl);
-    hipLaunchKernelGGL(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, b_lo, b_hi);
-    if (ctl.t_hi == n_tiles)  // the last part: every tile's base is known
-      hipLaunchKernelGGL(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
+    const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
+    if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
+    ZLAUNCH(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
+    ZLAUNCH(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
+    ZLAUNCH(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
   } else if (phase == 2) {
     if (ctl.jser)
-      hipLaunchKernelGGL(k_decode_emit<true>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+      ZLAUNCH(k_decode_emit<true>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
     else
-      hipLaunchKernelGGL(k_decode_emit<false>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+      ZLAUNCH(k_decode_emit<false>, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else {
     static int jres = 0;  // blocks the device keeps resident for the table kernel
     if (!jres) {
@@ -1728,9 +1824,9 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
         return CLG_E_DEVICE;
       jres = per_cu * cus;
     }
-    hipLaunchKernelGGL(k_decode_jser, dim3(nt < (uint32_t)jres ? nt : (uint32_t)jres), dim3(64), 0, st,
+    ZLAUNCH(k_decode_jser, dim3(nt < (uint32_t)jres ? nt : (uint32_t)jres), dim3(64), 0, st,
                        d_tiles, d_spans, ctl);
-    hipLaunchKernelGGL(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    ZLAUNCH(k_decode_jser_general, dim3(256), dim3(64), 0, st, d_tiles, d_spans, ctl);
   }
   return launch_status(hipGetLastError());
 }

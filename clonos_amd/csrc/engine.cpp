@@ -437,7 +437,7 @@ struct clg_engine {
 
   // staging / scratch
   PinBuf h_stage, h_desc, h_sres, h_zres;
-  DevBuf d_stage, d_desc, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
@@ -458,15 +458,11 @@ struct clg_engine {
   // every full sync first waits for it (gwait).
   hipStream_t gstream = nullptr;
   hipEvent_t gready = nullptr;
-  // A fast decode in parts: scan + emit of each part on estream after its count (part_ev).
-  static constexpr uint32_t kMaxParts = 8;
-  hipStream_t estream = nullptr;
-  hipEvent_t part_ev[kMaxParts + 1] = {};
   bool g_pending = false;
   // two descriptor sets, so a gather can be queued while the previous one still runs;
   // gdone[s] marks the end of the last gather that used set s
   PinBuf h_gdesc[2];
-  DevBuf d_gdesc[2];
+  DevBuf d_gdesc[2], d_gpieces[2];
   hipEvent_t gdone[2] = {nullptr, nullptr};
   uint32_t gseq = 0;
   PinBuf h_rmeta;
@@ -866,53 +862,23 @@ struct clg_engine {
     return sync();
   }
 
-  // Batched gather of log ranges (`runs`: one per request, output offsets in dst) by
-  // k_gather_seg: the runs are grouped by log (segtab_off identifies it), and the pieces of
-  // one segment (one per run reading it) run side by side on one XCD, so a segment that 8
-  // consumers' slices share comes from HBM once.  Host output: staged in d_out, copied back, waited
-  // for.  Device output with CLG_F_ASYNC_SLICE: on gstream, not waited for.
-  int gather_runs(std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint64_t total, void* out,
-                  uint32_t out_kind) {
-    if (runs.empty()) return CLG_OK;
-    auto by_log = [](const clg::SegSpan& a, const clg::SegSpan& b) { return a.segtab_off < b.segtab_off; };
-    if (!std::is_sorted(runs.begin(), runs.end(), by_log)) std::stable_sort(runs.begin(), runs.end(), by_log);
-    std::vector<clg::SliceGroup> groups;
-    groups.reserve(runs.size());
-    uint32_t n_jobs = 0;
-    const uint32_t c = C();
-    for (uint32_t i = 0; i < uint32_t(runs.size());) {
-      uint32_t j = i, lo = UINT32_MAX, hi = 0;
-      for (; j < uint32_t(runs.size()) && runs[j].segtab_off == runs[i].segtab_off; ++j) {
-        lo = std::min(lo, runs[j].phys / c);
-        hi = std::max(hi, (runs[j].phys + runs[j].len - 1) / c + 1);
-      }
-      groups.push_back(clg::SliceGroup{runs[i].segtab_off, lo, hi, i, j, n_jobs, 0});
-      n_jobs += (hi - lo) * (j - i);  // (segment, run) slots
-      i = j;
-    }
-    const uint64_t algo = (cfg.flags & CLG_F_TIMING) ? slice_bytes(runs, groups, total) : 0;  // (stats only)
-    if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE)) {
-      // on gstream, after everything already queued on `stream` (appends); returns without
-      // waiting.  Its own descriptor buffers, so the next decode on `stream` does not touch
-      // them; the gather two calls ago released this set.
-      const uint32_t set = gseq++ & 1u;
-      if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));
-      else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
-      SliceLayout L;
-      CHK(stage_groups(runs, groups, segtab, h_gdesc[set], d_gdesc[set], &L));
-      // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
-      // its call returned, and decodes only read the pool
-      HIPCHK(hipMemcpyAsync(d_gdesc[set].p, h_gdesc[set].p, L.hb, hipMemcpyHostToDevice, gstream));
-      CHK(timed("slice_gather", algo, [&] {
-        return launch_groups(d_gdesc[set], L, n_jobs, static_cast<uint8_t*>(out), gstream);
-      }, gstream));
-      HIPCHK(hipEventRecord(gdone[set], gstream));
-      g_pending = true;
-      return CLG_OK;
-    }
-    SliceLayout L;
-    CHK(stage_groups(runs, groups, segtab, h_desc, d_desc, &L));
-    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, L.hb, hipMemcpyHostToDevice, stream));
+  // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
+  int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
+                      uint64_t total, void* out, uint32_t out_kind) {
+    if (runs.empty() || !n_pieces) return CLG_OK;
+    if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
+      return gather_runs_async(runs, segtab, n_pieces, total, out);
+    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
+    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    CHK(h_desc.ensure(hb));
+    CHK(d_desc.ensure(hb));
+    CHK(d_pieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
+    memcpy(h_desc.p, runs.data(), rb);
+    memcpy(h_desc.as<uint8_t>() + o_seg, segtab.data(), gb);
+    HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
+    CHK(clg::launch_expand_pieces(d_desc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
+                                  reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
+                                  d_pieces.as<clg::GatherPiece>(), stream));
     uint8_t* dout;
     if (out_kind == CLG_MEM_DEVICE) {
       dout = static_cast<uint8_t*>(out);
@@ -920,59 +886,43 @@ struct clg_engine {
       CHK(d_out.ensure(total));
       dout = d_out.as<uint8_t>();
     }
-    CHK(timed("slice_gather", algo, [&] { return launch_groups(d_desc, L, n_jobs, dout, stream); }));
+    CHK(timed("slice_gather", 2 * total, [&] {
+      return clg::launch_gather(d_pieces.as<clg::GatherPiece>(), n_pieces, dout, stream);
+    }));
     if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
     return sync();
   }
-  // Where a batched gather's descriptors lie in its staged buffer (byte offsets).
-  struct SliceLayout {
-    size_t o_runs = 0, o_seg = 0, hb = 0;
-    uint32_t n_groups = 0;
-  };
-  int stage_groups(const std::vector<clg::SegSpan>& runs, const std::vector<clg::SliceGroup>& groups,
-                   const std::vector<uint32_t>& segtab, PinBuf& hd, DevBuf& dd, SliceLayout* L) {
-    const size_t gb = groups.size() * sizeof(clg::SliceGroup), rb = runs.size() * sizeof(clg::SegSpan),
-                 sb = segtab.size() * sizeof(uint32_t);
-    L->o_runs = (gb + 15) & ~size_t(15);
-    L->o_seg = (L->o_runs + rb + 15) & ~size_t(15);
-    L->hb = L->o_seg + sb;
-    L->n_groups = uint32_t(groups.size());
-    CHK(hd.ensure(L->hb));
-    CHK(dd.ensure(L->hb));
-    memcpy(hd.p, groups.data(), gb);
-    memcpy(hd.as<uint8_t>() + L->o_runs, runs.data(), rb);
-    memcpy(hd.as<uint8_t>() + L->o_seg, segtab.data(), sb);
+
+  // Device-output slice gather on gstream, after everything already queued on `stream`
+  // (appends); returns without waiting.  Its own descriptor buffers, so the next decode
+  // on `stream` does not touch them; the next gather waits for this one first.
+  int gather_runs_async(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
+                        uint64_t total, void* out) {
+    const uint32_t set = gseq++ & 1u;
+    if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
+    else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
+    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
+    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    PinBuf& hd = h_gdesc[set];
+    DevBuf& dd = d_gdesc[set];
+    DevBuf& dp = d_gpieces[set];
+    CHK(hd.ensure(hb));
+    CHK(dd.ensure(hb));
+    CHK(dp.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
+    memcpy(hd.p, runs.data(), rb);
+    memcpy(hd.as<uint8_t>() + o_seg, segtab.data(), gb);
+    // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
+    // its call returned, and decodes only read the pool
+    HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
+    CHK(clg::launch_expand_pieces(dd.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
+                                  reinterpret_cast<const uint32_t*>(dd.as<uint8_t>() + o_seg), pool, C(),
+                                  dp.as<clg::GatherPiece>(), gstream));
+    CHK(timed("slice_gather", 2 * total, [&] {
+      return clg::launch_gather(dp.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
+    }, gstream));
+    HIPCHK(hipEventRecord(gdone[set], gstream));
+    g_pending = true;
     return CLG_OK;
-  }
-  int launch_groups(const DevBuf& dd, const SliceLayout& L, uint32_t n_jobs, uint8_t* dout, hipStream_t on) {
-    const uint8_t* d = dd.as<uint8_t>();
-    return clg::launch_gather_seg(reinterpret_cast<const clg::SliceGroup*>(d), L.n_groups, n_jobs,
-                                  reinterpret_cast<const clg::SegSpan*>(d + L.o_runs),
-                                  reinterpret_cast<const uint32_t*>(d + L.o_seg), pool, C(), dout, on);
-  }
-  // A batched gather's algorithmic bytes: every source byte some run
-  // reads, once (the union of the runs' ranges per log), every byte written, and 16 B of
-  // request / result metadata per run.
-  static uint64_t slice_bytes(const std::vector<clg::SegSpan>& runs, const std::vector<clg::SliceGroup>& groups,
-                              uint64_t total) {
-    uint64_t read = 0;
-    std::vector<std::pair<uint32_t, uint32_t>> iv;
-    for (const auto& g : groups) {
-      if (g.run_hi - g.run_lo == 1) {
-        read += runs[g.run_lo].len;
-        continue;
-      }
-      iv.clear();
-      for (uint32_t i = g.run_lo; i < g.run_hi; ++i) iv.emplace_back(runs[i].phys, runs[i].phys + runs[i].len);
-      std::sort(iv.begin(), iv.end());
-      uint32_t end = 0;
-      for (const auto& x : iv) {
-        const uint32_t a = std::max(x.first, end);
-        if (x.second > a) read += x.second - a;
-        end = std::max(end, x.second);
-      }
-    }
-    return read + total + 16 * uint64_t(runs.size());
   }
 
   // host_only: serve the slice from the host tail or return kNeedGpu with nothing changed
@@ -1362,14 +1312,11 @@ struct clg_engine {
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
-    // The whole sequence; `ev` (timing) brackets jser, count, offsets and emit, `evp` the
-    // whole pipeline.  (Captured as a hipGraph and replayed per batch shape it was no
-    // faster: 197 us for a 16-log decode either way, and the bench step unchanged.)
-    // In parts (decode_parts): tiles split at scan-block multiples; jser + count of each
-    // part on `stream`, scan + emit of each part on `estream` once its count is done, so
-    // the instruction-bound count of part k + 1 runs beside the memory-bound emit of part k.
-    const uint32_t P = decode_parts(nt);
-    if (P > 1) stats["decode_parts"].launches += P;  // (the parts actually run; tests read it)
+    // The whole sequence, enqueued on `stream`; `ev` (timing) brackets jser, count, offsets
+    // and emit, `evp` the whole pipeline.  (Captured as a hipGraph and replayed per batch
+    // shape it was no faster: 197 us for a 16-log decode either way, and the bench step
+    // unchanged.  Split into parts whose count ran beside the previous part's emit on a second
+    // stream it was slower: config 2 0.44 -> 0.46 / 0.53 ms in 2 / 4 parts.)
     auto enqueue = [&](hipEvent_t* ev, hipEvent_t* evp) -> int {
       CHK(enqueue_plan(p, L, d_ztiles));
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
@@ -1379,31 +1326,12 @@ struct clg_engine {
       HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
-      if (P <= 1) {
-        for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
-          if (ph == 3 && !jser) continue;
-          const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
-          if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
-          CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
-          if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
-        }
-      } else {
-        uint32_t lo = 0;
-        for (uint32_t k = 0; k < P; ++k) {
-          const uint32_t hi = k + 1 == P ? nt : (uint32_t(uint64_t(nt) * (k + 1) / P) / clg::kZScanBlock) * clg::kZScanBlock;
-          clg::FusedCtl c = ctl;
-          c.t_lo = lo;
-          c.t_hi = hi;
-          if (jser) CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, stream, 3));
-          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, stream, 0, k ? count_grid_pct() : 0));
-          HIPCHK(hipEventRecord(part_ev[k], stream));
-          HIPCHK(hipStreamWaitEvent(estream, part_ev[k], 0));
-          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, estream, 1));
-          CHK(clg::launch_decode_fused(zt, nt, zs, ns, c, o, estream, 2));
-          lo = hi;
-        }
-        HIPCHK(hipEventRecord(part_ev[P], estream));
-        HIPCHK(hipStreamWaitEvent(stream, part_ev[P], 0));
+      for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
+        if (ph == 3 && !jser) continue;
+        const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
+        if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
+        CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
+        if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
       }
       if (evp) HIPCHK(hipEventRecord(evp[1], stream));
       // read the span ranges and abort words (emit ran right behind the scan: it returns at
@@ -1414,12 +1342,11 @@ struct clg_engine {
     };
     hipEvent_t ev[8] = {}, evp[2] = {};
     if (timing) {
-      if (P <= 1)
-        for (auto& e : ev) e = get_event();
+      for (auto& e : ev) e = get_event();
       for (auto& e : evp) e = get_event();
     }
-    CHK(enqueue(timing && P <= 1 ? ev : nullptr, timing ? evp : nullptr));
-    if (timing && P <= 1) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
+    CHK(enqueue(timing ? ev : nullptr, timing ? evp : nullptr));
+    if (timing) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
       if (jser) timings.push_back(PendingTiming{"decode_jser", ev[0], ev[1], log_bytes});
       else ev_pool.insert(ev_pool.end(), {ev[0], ev[1]});
       timings.push_back(PendingTiming{"decode_count", ev[2], ev[3], log_bytes});
@@ -1433,27 +1360,6 @@ struct clg_engine {
     }
     return CLG_OK;
   }
-  // Parts a fast decode runs in: clg_config.decode_parts, else CLONOS_DECODE_PARTS (tuning
-  // aid), else the default; only batches of at least two scan blocks per part are split.
-  static constexpr int kDefaultParts = 1;
-  uint32_t decode_parts(uint32_t nt) const {
-    static const int env = [] {
-      const char* s = getenv("CLONOS_DECODE_PARTS");
-      return s ? atoi(s) : 0;
-    }();
-    const int v = cfg.decode_parts ? int(cfg.decode_parts) : env ? env : kDefaultParts;
-    uint32_t P = uint32_t(std::max(1, std::min(v, int(kMaxParts))));
-    while (P > 1 && nt / P < 2 * clg::kZScanBlock) --P;
-    return P;
-  }
-  static uint32_t count_grid_pct() {  // CLONOS_COUNT_GRID_PCT: the count grid of parts after the first
-    static const int v = [] {
-      const char* s = getenv("CLONOS_COUNT_GRID_PCT");
-      return s ? atoi(s) : 0;
-    }();
-    return uint32_t(std::max(0, std::min(v, 100)));
-  }
-
   int finish_fused(const DecodePlan& p, FusedRun& r, clg_decoded* out, uint64_t* span_rec_base, bool* aborted,
                    bool* need_jser) {
     *aborted = false;
@@ -1953,7 +1859,6 @@ void clg_config_default(clg_config* cfg) {
   cfg->host_tail_bytes = 16384;    // one component of each log's tail kept on the host
   cfg->ifl_segment_bytes = 32768;  // the in-flight log's pool: Flink's 32 KiB memory segments
   cfg->ifl_pool_segments = 4096;   // 128 MiB
-  cfg->decode_parts = 0;           // the engine's default (decode_parts())
 }
 
 int clg_abi_version(void) { return CLG_ABI_VERSION; }
@@ -1989,8 +1894,6 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
       HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
   }
   HIPCHK(hipEventCreateWithFlags(&e->gready, hipEventDisableTiming));
-  HIPCHK(hipStreamCreateWithFlags(&e->estream, hipStreamNonBlocking));
-  for (auto& ev : e->part_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, pool_bytes + 2 * kPoolGuard));  // guards: aligned over-reads either side
@@ -2031,9 +1934,6 @@ void clg_engine_destroy(clg_engine* e) {
   hipStreamDestroy(e->stream);
   if (e->gstream) hipStreamDestroy(e->gstream);
   if (e->gready) hipEventDestroy(e->gready);
-  if (e->estream) hipStreamDestroy(e->estream);
-  for (auto ev : e->part_ev)
-    if (ev) hipEventDestroy(ev);
   for (auto ev : e->gdone)
     if (ev) hipEventDestroy(ev);
   delete e;
@@ -2298,6 +2198,8 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   std::vector<clg::SegSpan> runs;
   std::vector<uint32_t> segtab;
   std::unordered_map<uint32_t, uint64_t> tab_of;
+  uint32_t n_pieces = 0;
+  const uint32_t C = e->C();
   uint64_t dst = 0;
   for (uint32_t i = 0; i < n; ++i) {
     Log* l;
@@ -2312,7 +2214,8 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
         ti = tab_of.emplace(log[i], segtab.size()).first;
         segtab.insert(segtab.end(), l->segs.begin(), l->segs.end());
       }
-      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, 0, 0});
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, n_pieces, 0});
+      n_pieces += uint32_t(s + nb - 1) / C - uint32_t(s) / C + 1;
     }
     dst += uint64_t(nb);
   }
@@ -2320,7 +2223,7 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   if (!out) return CLG_OK;  // sizes only
   if (dst > cap) return fail(CLG_E_CAPACITY, "getDeterminants batch needs %llu bytes", (unsigned long long)dst);
   CHK(e->flush());
-  return e->gather_runs(runs, segtab, dst, out, out_kind);
+  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
 }
 
 int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_slice_res* res, void* out, uint64_t cap,
@@ -2333,6 +2236,8 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
   std::vector<uint32_t> segtab;
   std::unordered_map<uint32_t, uint64_t> tab_of;  // log -> its segment indices in segtab
   runs.reserve(n);
+  uint32_t n_pieces = 0;
+  const uint32_t C = e->C();
   uint64_t dst = 0;
   for (uint32_t i = 0; i < n; ++i) {
     clg_slice_res& r = res[i];
@@ -2371,12 +2276,13 @@ int clg_slice_batch(clg_engine* e, const clg_slice_req* reqs, uint32_t n, clg_sl
         ti = tab_of.emplace(reqs[i].log, segtab.size()).first;
         segtab.insert(segtab.end(), segs.begin(), segs.end());
       }
-      runs.push_back(clg::SegSpan{ti->second, uint32_t(phys), uint32_t(nb), dst, 0, 0});
+      runs.push_back(clg::SegSpan{ti->second, uint32_t(phys), uint32_t(nb), dst, n_pieces, 0});
+      n_pieces += uint32_t(phys + nb - 1) / C - uint32_t(phys) / C + 1;
     }
     dst += uint64_t(nb);
   }
   if (total) *total = dst;
-  return e->gather_runs(runs, segtab, dst, out, out_kind);
+  return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
 }
 
 int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch, int32_t offset) {

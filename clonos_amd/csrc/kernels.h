@@ -205,10 +205,6 @@ struct FusedCtl {
   // skip_bad set, so emit leaves the bad spans' records to the robust output.
   uint32_t* span_bad;
   uint32_t skip_bad;
-  // The tiles one launch of a pass covers, [t_lo, t_hi): a decode split into parts runs the
-  // count of part k + 1 beside the scan and emit of part k (t_lo a multiple of the scan
-  // block, kZScanBlock = 1024 tiles).  Defaults: the whole batch.
-  uint32_t t_lo = 0, t_hi = 0xFFFFFFFFu;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
@@ -222,11 +218,8 @@ int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const u
                          FusedCtl ctl, void* stream);
 // x[i] += delta for i < n (the robust output's wide-row record indices moved into place).
 int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream);
-// One pass over tiles [ctl.t_lo, ctl.t_hi) (scan: the part's blocks; the span ranges after the
-// last part).  grid_pct (count): percent of the resident-block grid (0: all), for a part
-// that runs beside another part's emit.
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase, uint32_t grid_pct = 0);
+                        FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
@@ -259,29 +252,18 @@ struct SegSpan {
   uint32_t first;       // first piece / tile generated for the run
   uint32_t pad;
 };
-// A batched slice's requests on one log (k_gather_seg): runs [run_lo, run_hi) of the call's
-// run table read segments [seg_lo, seg_hi) of the log (segment indices in segtab from
-// segtab_off); its (segment, run) slots are first_slot .. first_slot + (seg_hi - seg_lo) *
-// (run_hi - run_lo) - 1, segment-major.
-struct SliceGroup {
-  uint64_t segtab_off;
-  uint32_t seg_lo, seg_hi;
-  uint32_t run_lo, run_hi;
-  uint32_t first_slot, pad;
-};
 // Launch helpers' status: CLG_OK, or CLG_E_DEVICE with the HIP error kept (thread-local)
 // for the engine's error text (take_launch_error, nullptr when none).
 int launch_status(hipError_t e);
 const char* take_launch_error();
+int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pieces, const uint32_t* d_segtab,
+                         const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream);
 int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
                         const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream);
-// Batched slice (k_gather_seg): one block per (segment, run) slot of the groups.
-int launch_gather_seg(const SliceGroup* d_groups, uint32_t n_groups, uint32_t n_slots, const SegSpan* d_runs,
-                      const uint32_t* d_segtab, const uint8_t* pool, uint32_t seg_bytes, uint8_t* d_out, void* stream);
 // Robust pipeline (per-byte DP transfer tables); runs only on spans whose flag is set
 // (d_span_flags == nullptr: all spans).
 int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,

@@ -58,11 +58,12 @@ __device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32
 // 16 bytes either side of the piece's source range: the pool has guard bytes both ends.
 constexpr int kGatherK = 4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// One piece by the whole block: bytes [src, src + len) to [d0, d0 + len).
-__device__ __forceinline__ void copy_piece(const uint8_t* src, uintptr_t d0, uint32_t len) {
-  const uintptr_t d1 = d0 + len;
+__global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
+  const GatherPiece p = pieces[blockIdx.x];
+  if (p.len == 0) return;
+  const uintptr_t d0 = (uintptr_t)(out + p.dst), d1 = d0 + p.len;
   const uintptr_t a0 = d0 & ~(uintptr_t)15;
-  const uintptr_t sdelta = (uintptr_t)src - d0;  // src address = dst address + sdelta
+  const uintptr_t sdelta = (uintptr_t)p.src - d0;  // src address = dst address + sdelta
   const uint32_t m = (uint32_t)(sdelta & 15);
   const uint32_t nch = (uint32_t)((((d1 + 15) & ~(uintptr_t)15) - a0) >> 4);
   for (uint32_t j0 = 0; j0 < nch; j0 += kGatherK * 256) {
@@ -96,45 +97,6 @@ __device__ __forceinline__ void copy_piece(const uint8_t* src, uintptr_t d0, uin
   }
 }
 
-__global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
-  const GatherPiece p = pieces[blockIdx.x];
-  if (p.len == 0) return;
-  copy_piece(p.src, (uintptr_t)(out + p.dst), p.len);
-}
-
-// Batched slice, one block per (segment, request) slot of each log's group of requests.
-// Slots are numbered segment-major inside a group (the group's requests on segment 0, then
-// on segment 1, ...) and dealt to blocks so that each XCD takes one contiguous eighth of
-// them in order (blocks b and b + 8 share an XCD): the up to 8 consumers' pieces of one
-// segment run side by side on one XCD, and that L2 serves the segment to all but the first.
-// A plain grid of pieces put them on different XCDs and read each segment from HBM up to 8
-// times.  A slot whose request does not read its segment returns at once.
-__device__ __forceinline__ uint32_t find_group(const SliceGroup* g, uint32_t n, uint32_t j) {
-  uint32_t lo = 0, hi = n;  // last group with first_slot <= j
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (g[mid].first_slot <= j) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-__global__ __launch_bounds__(256) void k_gather_seg(const SliceGroup* __restrict__ groups, uint32_t n_groups,
-                                                    uint32_t n_slots, const SegSpan* __restrict__ runs,
-                                                    const uint32_t* __restrict__ segtab, const uint8_t* __restrict__ pool,
-                                                    uint32_t C, uint8_t* __restrict__ out) {
-  const uint32_t per_xcd = (n_slots + 7) / 8;
-  const uint32_t slot = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
-  if (slot >= n_slots) return;
-  const SliceGroup g = groups[find_group(groups, n_groups, slot)];
-  const uint32_t R = g.run_hi - g.run_lo, k = slot - g.first_slot;
-  const uint32_t w = g.seg_lo + k / R;  // segment index within the log
-  const SegSpan r = runs[g.run_lo + k % R];
-  const uint32_t s_lo = w * C, s_hi = s_lo + C;
-  const uint32_t a = r.phys > s_lo ? r.phys : s_lo;
-  const uint32_t b = r.phys + r.len < s_hi ? r.phys + r.len : s_hi;
-  if (a >= b) return;
-  copy_piece(pool + (size_t)segtab[g.segtab_off + w] * C + (a - s_lo), (uintptr_t)(out + r.dst + (a - r.phys)), b - a);
-}
-
 // ==================================================================================
 // Device-side planning: item g -> its run (binary search over first) -> window.
 // ==================================================================================
@@ -145,6 +107,19 @@ __device__ __forceinline__ uint32_t find_run(const SegSpan* spans, uint32_t n, u
     if (spans[mid].first <= g) lo = mid; else hi = mid;
   }
   return lo;
+}
+
+__global__ __launch_bounds__(256) void k_expand_pieces(const SegSpan* __restrict__ spans, uint32_t n_spans,
+                                                       uint32_t n_pieces, const uint32_t* __restrict__ segtab,
+                                                       const uint8_t* __restrict__ pool, uint32_t C,
+                                                       GatherPiece* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_pieces) return;
+  const SegSpan r = spans[find_run(spans, n_spans, g)];
+  const uint32_t w = r.phys / C + (g - r.first);
+  const uint32_t s0 = w * C > r.phys ? w * C : r.phys;
+  const uint32_t e1 = (w + 1) * C < r.phys + r.len ? (w + 1) * C : r.phys + r.len;
+  out[g] = GatherPiece{pool + (size_t)segtab[r.segtab_off + w] * C + (s0 - w * C), r.dst + (s0 - r.phys), e1 - s0, 0};
 }
 
 __global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict__ spans, uint32_t n_spans,
@@ -718,6 +693,14 @@ int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_sr
   return ok(hipGetLastError());
 }
 
+int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pieces, const uint32_t* d_segtab,
+                         const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream) {
+  if (!n_pieces) return CLG_OK;
+  hipLaunchKernelGGL(k_expand_pieces, dim3((n_pieces + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
+                     n_pieces, d_segtab, pool, seg_bytes, d_out);
+  return launch_status(hipGetLastError());
+}
+
 int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
                         const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream) {
   if (!n_tiles) return CLG_OK;
@@ -729,15 +712,6 @@ int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_til
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream) {
   if (!n) return CLG_OK;
   hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, (hipStream_t)stream, d_pieces, d_out);
-  return ok(hipGetLastError());
-}
-
-int launch_gather_seg(const SliceGroup* d_groups, uint32_t n_groups, uint32_t n_slots, const SegSpan* d_runs,
-                      const uint32_t* d_segtab, const uint8_t* pool, uint32_t seg_bytes, uint8_t* d_out, void* stream) {
-  if (!n_slots) return CLG_OK;
-  const uint32_t blocks = 8 * ((n_slots + 7) / 8);
-  hipLaunchKernelGGL(k_gather_seg, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_groups, n_groups, n_slots, d_runs,
-                     d_segtab, pool, seg_bytes, d_out);
   return ok(hipGetLastError());
 }
 

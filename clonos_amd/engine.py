@@ -119,8 +119,7 @@ class Engine:
     def __init__(self, segment_bytes: int = 16384, pool_segments: int = 16384, device: int = 0,
                  sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto",
                  async_slice: bool = False, ifl_segment_bytes: Optional[int] = None,
-                 ifl_pool_segments: Optional[int] = None, host_tail_bytes: Optional[int] = None,
-                 decode_parts: Optional[int] = None):
+                 ifl_pool_segments: Optional[int] = None, host_tail_bytes: Optional[int] = None):
         """decode: "auto" = fast three-pass decode, robust multi-pass pipeline on abort;
         "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
         slices return once queued on the gather stream (CLG_F_ASYNC_SLICE); sync() before
@@ -138,8 +137,6 @@ class Engine:
             cfg.host_tail_bytes = host_tail_bytes
         cfg.ifl_segment_bytes = ifl_segment_bytes if ifl_segment_bytes is not None else segment_bytes
         cfg.ifl_pool_segments = ifl_pool_segments if ifl_pool_segments is not None else pool_segments
-        if decode_parts is not None:
-            cfg.decode_parts = decode_parts
         cfg.flags = ((_lib.CLG_F_TIMING if timing else 0) | (_lib.CLG_F_ROBUST_DECODE if decode == "robust" else 0)
                      | (_lib.CLG_F_ASYNC_SLICE if async_slice else 0))
         h = C.c_void_p()

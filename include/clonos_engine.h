@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 4
+#define CLG_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -100,10 +100,6 @@ typedef struct clg_config {
    * defaults (32 KiB segments = Flink's memory segment size, 4096 of them). */
   uint32_t ifl_segment_bytes;
   uint32_t ifl_pool_segments;
-  /* The fast decode of a large batch runs in this many parts (at most 8, at least 2048 tiles
-   * each), the count pass of part k + 1 beside the scan and emit of part k on a second
-   * stream.  0: the engine's default. */
-  uint32_t decode_parts;
 } clg_config;
 
 #define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
