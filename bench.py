@@ -823,13 +823,15 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
                 e_.decode_logs_device(h, starts, dec, base)
             torch.cuda.synchronize()
             ms = (_t.perf_counter() - t0) / steps * 1e3
-            paths = sorted(k for k in e_.kernel_stats() if k in ("decode_fallback", "decode_span_fallback"))
-            return ms, paths
+            ks = e_.kernel_stats()
+            paths = sorted(k for k in ks if k in ("decode_fallback", "decode_span_fallback"))
+            kms = {k: round(v["ms"] / v["launches"], 4) for k, v in ks.items() if v["launches"] and v["ms"] > 0}
+            return ms, paths, kms
         finally:
             e_.close()
     # the robust pipeline alone (the fallback's throughput) and the long-record batch
-    rob_ms, _ = timed_decode("clean", "robust", n_det)
-    long_ms, long_paths = timed_decode("long", "auto", n_det + 2)
+    rob_ms, _, rob_k = timed_decode("clean", "robust", n_det)
+    long_ms, long_paths, _ = timed_decode("long", "auto", n_det + 2)
     out = {"workload": f"config3: {n_logs} subtask logs x {n_epochs} epochs x {per_epoch} mixed determinants "
                        "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
@@ -837,7 +839,7 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
            "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern,
            "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)},
            "robust_pipeline": {"ms_per_step": round(rob_ms, 4), "determinants_per_s": round(n_det / rob_ms * 1e3, 1),
-                               "log_gbs": round(total / rob_ms / 1e6, 2)},
+                               "log_gbs": round(total / rob_ms / 1e6, 2), "kernels_ms": rob_k},
            "long_records": {"note": "the same batch with a 40 KB TimerTrigger name (log 37) and a 9 KB "
                                     "Serializable int[] stream (log 181) inserted at record boundaries",
                             "ms_per_step": round(long_ms, 4), "vs_clean": round(long_ms / (el * 1e3), 4),

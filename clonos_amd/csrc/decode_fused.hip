@@ -54,14 +54,15 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_COUNT_LM
 #define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
 #endif
-#ifndef CLG_FUSED_PIPELINE
-#define CLG_FUSED_PIPELINE 1  // 1: two tiles in flight per wave (count one, emit the previous)
+#ifndef CLG_TINY
+#define CLG_TINY 1  // 1: small whole spans a lane each in the count pass (tiny_tiles)
 #endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
+constexpr uint32_t kZTiny = 1024;                      // small whole spans: a lane each in the count pass
 
 // ---------------------------------------------------------------------------------
 // 128-bit region bitmaps (bit i <-> byte r0 + i of the lane's aligned region r0).
@@ -1328,7 +1329,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
 // (TimerTrigger, SourceCheckpoint, Serializable: lengths from fields) sends the whole run to
 // the wave path; an invalid tag or a record past the span end marks the span bad (abort
 // reason 1), as count_tile does.  Returns the tiles handled (0: none; ~0: the batch aborts).
-constexpr uint32_t kZTiny = 1024;
 __device__ __forceinline__ uint32_t tiny_tiles(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                const FusedCtl& ctl, const uint32_t t, const uint32_t t1,
                                                const uint32_t lane) {
@@ -1426,7 +1426,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
-  const uint32_t t0 = blockIdx.x * K, t1 = min(nt, t0 + K);
+  const uint32_t t0 = ctl.chunk ? ctl.chunk[blockIdx.x] : blockIdx.x * K;
+  const uint32_t t1 = ctl.chunk ? ctl.chunk[blockIdx.x + 1] : min(nt, t0 + K);
   if (t0 >= t1) return;
   // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
   uint32_t x_pub = kZCanon;
@@ -1451,7 +1452,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
-    if (!J && z.first && z.last && z.td.len <= kZTiny && !ctl.nodep && !ctl.prof) {
+    if (CLG_TINY && !J && z.first && z.last && z.td.len <= kZTiny && !ctl.nodep && !ctl.prof) {
       const uint32_t m = tiny_tiles(tiles, spans, ctl, t, t1, lane);  // small whole spans, a lane each
       if (m == 0xFFFFFFFFu) return;
       if (m) {
@@ -1767,6 +1768,21 @@ int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
   return launch_status(hipGetLastError());
 }
 
+uint32_t decode_count_grid(bool jser, uint32_t n_tiles) {
+  static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
+  const int j = jser ? 1 : 0;
+  if (!resident[j]) {
+    int dev = 0, per_cu = 0, cus = 0;
+    const hipError_t oe = j ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<true>, 64, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<false>, 64, 0);
+    if (hipGetDevice(&dev) != hipSuccess || oe != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+      return 0;
+    resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
+  }
+  return n_tiles < (uint32_t)resident[j] ? n_tiles : (uint32_t)resident[j];
+}
+
 // Checked launch: a configuration error names its kernel and grid (stderr) and is returned.
 #define ZLAUNCH(k, grid, block, ...)                                                                     \
   do {                                                                                                  \
@@ -1787,18 +1803,9 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
   const uint32_t nt = n_tiles;
   hipStream_t st = (hipStream_t)stream;
   if (phase == 0) {
-    static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
+    const uint32_t grid = decode_count_grid(ctl.jser != 0, nt);
+    if (!grid) return CLG_E_DEVICE;
     const int j = ctl.jser ? 1 : 0;
-    if (!resident[j]) {
-      int dev = 0, per_cu = 0, cus = 0;
-      const hipError_t oe = j ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<true>, 64, 0)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<false>, 64, 0);
-      if (hipGetDevice(&dev) != hipSuccess || oe != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
-        return CLG_E_DEVICE;
-      resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
-    }
-    const uint32_t grid = nt < (uint32_t)resident[j] ? nt : (uint32_t)resident[j];
     if (j)
       ZLAUNCH(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
     else

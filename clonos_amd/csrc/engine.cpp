@@ -1128,23 +1128,25 @@ struct clg_engine {
   }
   // Where a staged plan lies in h_plan / d_plan (byte offsets).
   struct PlanLayout {
-    size_t tb = 0, sb = 0, o_runs = 0, o_seg = 0, o_spans = 0, hb = 0;
+    size_t tb = 0, sb = 0, o_runs = 0, o_seg = 0, o_spans = 0, o_chunk = 0, hb = 0;
   };
-  // Host half: the plan's descriptors into the pinned plan buffer (its own: an
-  // asynchronous decode may still be uploading it while later calls -- flush, slices --
-  // stage theirs).
-  int stage_plan(const DecodePlan& p, DevBuf& dtiles, PlanLayout* L) {
+  // Host half: the plan's descriptors (and the count pass's chunk table, if any) into the
+  // pinned plan buffer (its own: an asynchronous decode may still be uploading it while later
+  // calls -- flush, slices -- stage theirs).
+  int stage_plan(const DecodePlan& p, DevBuf& dtiles, PlanLayout* L, const std::vector<uint32_t>* chunk = nullptr) {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     CHK(dtiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
     CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
     const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
-                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc);
+                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc),
+                 cb = chunk ? chunk->size() * sizeof(uint32_t) : 0;
     L->tb = tb;
     L->sb = sb;
     L->o_runs = (tb + 15) & ~size_t(15);
     L->o_seg = (L->o_runs + rb + 15) & ~size_t(15);
     L->o_spans = (L->o_seg + gb + 15) & ~size_t(15);
-    L->hb = L->o_spans + sb;
+    L->o_chunk = (L->o_spans + sb + 15) & ~size_t(15);
+    L->hb = L->o_chunk + cb;
     CHK(h_plan.ensure(L->hb + 64));
     CHK(d_plan.ensure(L->hb));
     uint8_t* hd = h_plan.as<uint8_t>();
@@ -1152,8 +1154,33 @@ struct clg_engine {
     memcpy(hd + L->o_runs, p.runs.data(), rb);
     memcpy(hd + L->o_seg, p.segtab.data(), gb);
     memcpy(hd + L->o_spans, p.spans.data(), sb);
+    if (cb) memcpy(hd + L->o_chunk, chunk->data(), cb);
     return CLG_OK;
   }
+  // The count pass's chunks of about equal cost: a tile costs its bytes plus a fixed 1 KiB
+  // (tiles of one span are taken as equally long), and block b takes the tiles whose
+  // cumulative cost passes b / G of the total.  ch[0 .. G]: boundaries, ch[G] = n_tiles.
+  static void count_chunks(const DecodePlan& p, uint32_t G, std::vector<uint32_t>& ch) {
+    ch.assign(size_t(G) + 1, p.n_tiles);
+    ch[0] = 0;
+    constexpr double kTileCost = 1024.0;
+    double total = 0;
+    for (const auto& s : p.spans) total += double(s.len) + kTileCost * s.n_tiles;
+    const double target = total / G;
+    double acc = 0, next = target;
+    uint32_t b = 1;
+    for (const auto& s : p.spans) {
+      if (!s.n_tiles) continue;
+      const double c = double(s.len) / s.n_tiles + kTileCost, end = acc + c * s.n_tiles;
+      while (b < G && next <= end) {  // boundary inside this span: the first tile past it
+        const double k = (next - acc) / c;
+        ch[b++] = s.first_tile + std::min<uint32_t>(s.n_tiles, uint32_t(k) + (k > double(uint32_t(k)) ? 1u : 0u));
+        next = target * b;
+      }
+      acc = end;
+    }
+  }
+  std::vector<uint32_t> chunk_buf;
   // Device half: upload, span table, tiles (expanded on the device from the runs).
   int enqueue_plan(const DecodePlan& p, const PlanLayout& L, DevBuf& dtiles) {
     HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
@@ -1274,8 +1301,12 @@ struct clg_engine {
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
     r->jser = jser;
+    // chunks of equal cost when blocks take several tiles of spans of different sizes
+    const uint32_t G = clg::decode_count_grid(jser, nt);
+    const bool chunked = G && nt > G && ns > 1;
+    if (chunked) count_chunks(p, G, chunk_buf);
     PlanLayout L;
-    CHK(stage_plan(p, d_ztiles, &L));
+    CHK(stage_plan(p, d_ztiles, &L, chunked ? &chunk_buf : nullptr));
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
     // words: st_x[nt] cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
@@ -1307,6 +1338,7 @@ struct clg_engine {
     if (jser) CHK(jarena_reset(&ctl.jar));
     ctl.span_bad = d_zbad.as<uint32_t>();
     ctl.skip_bad = 0;
+    ctl.chunk = chunked ? reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_chunk) : nullptr;
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -1437,11 +1469,13 @@ struct clg_engine {
   // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
   // tile_bytes)` fills a plan for the given tile geometry.
   template <class Build>
-  int decode(Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base) {
+  int decode(Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
+             DecodePlan* prebuilt = nullptr) {
     // fused counts are packed in 31-bit fields: at most log_bytes / 2 records
     if (fused_decode && log_bytes / 2 < (1ull << 31)) {
-      DecodePlan pf;
-      {
+      DecodePlan own;
+      DecodePlan& pf = prebuilt ? *prebuilt : own;  // (prebuilt: the fast plan, kZTile tiles)
+      if (!prebuilt) {
         HostTimer hp(this, "host_decode_plan");
         build(pf, clg::kZTile);
       }
@@ -2359,23 +2393,31 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   ENGINE_GUARD(e);
   if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
   CHK(e->flush());
-  std::vector<Log*> ls(n);
   std::vector<int32_t> st(n), nb(n);
   uint64_t total = 0;
+  // the ranges and the fast decode's plan in one pass over the logs (per-log work of a
+  // 66 k-log batch is bound by the cache misses on the log records)
+  clg_engine::DecodePlan pf;
+  if (e->fused_decode) {
+    pf.spans.reserve(n);
+    pf.runs.reserve(n);
+  }
   {
-    clg_engine::HostTimer ht(e, "host_decode_ranges");
+    clg_engine::HostTimer ht(e, "host_decode_plan");
     for (uint32_t i = 0; i < n; ++i) {
-      CHK(e->get_log(log[i], &ls[i]));
-      if (ls[i]->depth != 0) CHK(e->determinants_range(*ls[i], start_epoch[i], &st[i], &nb[i]));
+      Log* l;
+      CHK(e->get_log(log[i], &l));
+      if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
       total += uint64_t(nb[i]);
+      if (e->fused_decode) e->plan_log_span(pf, *l, st[i], nb[i], i, clg::kZTile);
     }
   }
-  auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
+  auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {  // re-plans (fallbacks)
     p.spans.reserve(n);
     p.runs.reserve(n);
-    for (uint32_t i = 0; i < n; ++i) e->plan_log_span(p, *ls[i], st[i], nb[i], i, T);
+    for (uint32_t i = 0; i < n; ++i) e->plan_log_span(p, e->logs[log[i]], st[i], nb[i], i, T);
   };
-  return e->decode(build, total, out, span_rec_base);
+  return e->decode(build, total, out, span_rec_base, e->fused_decode ? &pf : nullptr);
 }
 
 int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,

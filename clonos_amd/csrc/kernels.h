@@ -205,6 +205,11 @@ struct FusedCtl {
   // skip_bad set, so emit leaves the bad spans' records to the robust output.
   uint32_t* span_bad;
   uint32_t skip_bad;
+  // Count pass: block b's chunk is tiles [chunk[b], chunk[b + 1]) (chunks of about equal
+  // bytes, decode_count_chunks), or null: equal tile counts.  A batch of many small spans
+  // beside a few large ones (config 4: 320-byte subpartition logs, 22 KB main logs) would
+  // otherwise give a few blocks chunks of only large tiles and make them the critical path.
+  const uint32_t* chunk;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
@@ -220,6 +225,9 @@ int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const u
 int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream);
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
+// The count pass's grid for n_tiles tiles (the blocks the device keeps resident, at most one
+// per tile); CLG_E_DEVICE as 0.
+uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
