@@ -503,9 +503,13 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   uint32_t idx = ex - nm;
   if (lane == 0) J.n[t] = total;
   if (!nm) return;
+  // the walker reads the stream from the tile's LDS image (HBM only past the tile): byte by
+  // byte from HBM it took config 3's 5 M streams 285 ms
+  TileReader tr{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
   for (uint32_t a = rs; a < re; ++a) {
     if (t_u8(s_tile, a) != CLG_TAG_SERIALIZABLE || t_be32(s_tile, a + 1) != kSerMagic) continue;
-    const int64_t L = len_slow_span(&sr, td.span_off + (a - td.delta));  // walker: 1 + stream length
+    AtTileSpan b{&tr, a};
+    const int64_t L = rec_len_slow(b, sd.len - (td.span_off + (a - td.delta)));  // walker: 1 + stream length
     if (idx < (uint32_t)kJserCap) {
       J.pos[(uint64_t)t * kJserCap + idx] = a;
       J.len[(uint64_t)t * kJserCap + idx] = L > 1 ? (uint32_t)(L - 1) : 0u;

@@ -1021,17 +1021,28 @@ __global__ __launch_bounds__(256) void k_decode_scan1(FusedCtl ctl) {
   if (tid == 255u) gp(ctl.boff)[blk] = run;  // block total (scan2 turns it into an offset)
 }
 
-__global__ __launch_bounds__(1024) void k_decode_scan2(FusedCtl ctl, uint32_t n_blocks) {
-  __shared__ uint64_t s_w[16];
+// 256 threads, 4 block totals each: a 1024-thread workgroup waited up to 60 us for a CU with
+// 16 free wave slots while the slice gather (beside the decode) held them.
+__global__ __launch_bounds__(256) void k_decode_scan2(FusedCtl ctl, uint32_t n_blocks) {
+  __shared__ uint64_t s_w[4];
   if (ld_agent32(ctl.abort)) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-  const uint64_t v = tid < n_blocks ? gp(ctl.boff)[tid] : 0ull;
-  const uint64_t incl = wave_incl_scan(v, lane);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, i0 = 4u * tid;
+  uint64_t v[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = i0 + j < n_blocks ? gp(ctl.boff)[i0 + j] : 0ull;
+    sum += v[j];
+  }
+  const uint64_t incl = wave_incl_scan(sum, lane);
   if (lane == 63u) s_w[wv] = incl;
   __syncthreads();
-  uint64_t run = incl - v;
+  uint64_t run = incl - sum;
   for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
-  if (tid < n_blocks) gp(ctl.boff)[tid] = run;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (i0 + j < n_blocks) gp(ctl.boff)[i0 + j] = run;
+    run += v[j];
+  }
 }
 
 // Each span's record / wide-record range from the scan (the host reads them before the
@@ -1814,7 +1825,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits
     ZLAUNCH(k_decode_scan1, dim3(nb), dim3(256), 0, st, ctl);
-    ZLAUNCH(k_decode_scan2, dim3(1), dim3(1024), 0, st, ctl, nb);
+    ZLAUNCH(k_decode_scan2, dim3(1), dim3(256), 0, st, ctl, nb);
     ZLAUNCH(k_decode_spans, dim3((n_spans + 255) / 256), dim3(256), 0, st, d_spans, n_spans, ctl);
   } else if (phase == 2) {
     if (ctl.jser)

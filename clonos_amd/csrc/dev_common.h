@@ -70,6 +70,14 @@ struct At {
   uint32_t base;
   __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + (uint32_t)k); }
 };
+// A record through a tile reader (the LDS image inside the tile, HBM past it), with the
+// span's spill arena: the stream walker reads a Serializable record from LDS.
+struct AtTileSpan {
+  TileReader* r;
+  uint32_t base;
+  __device__ __forceinline__ int operator()(uint64_t k) { return r->at(base + (uint32_t)k); }
+  __device__ __forceinline__ JArena arena() const { return r->sr->ar; }
+};
 struct AtSpan {
   SpanReader* r;
   uint64_t base;

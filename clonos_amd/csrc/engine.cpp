@@ -516,7 +516,22 @@ struct clg_engine {
     timings.push_back(PendingTiming{name, a, b, bytes});
     return r;
   }
-  void collect_timings() {
+  // ready_only: only the timings whose end event has completed (the rest stay pending)
+  void collect_timings(bool ready_only = false) {
+    if (ready_only) {
+      std::vector<PendingTiming> later;
+      for (auto& t : timings)
+        if (hipEventQuery(t.b) == hipErrorNotReady) later.push_back(t);
+      if (!later.empty()) {
+        std::vector<PendingTiming> done;
+        for (auto& t : timings)
+          if (hipEventQuery(t.b) != hipErrorNotReady) done.push_back(t);
+        timings.swap(done);
+        collect_timings();
+        timings.swap(later);
+        return;
+      }
+    }
     for (auto& t : timings) {
       float ms = 0;
       hipEventSynchronize(t.b);
@@ -1221,6 +1236,13 @@ struct clg_engine {
     return CLG_OK;
   }
 
+  // Developer switch (CLONOS_DECODE_OWN_WAIT=1): an asynchronous decode into device memory
+  // completes on its own stream only, without waiting for slices still running on gstream.
+  static bool own_wait() {
+    static const bool v = getenv("CLONOS_DECODE_OWN_WAIT") && atoi(getenv("CLONOS_DECODE_OWN_WAIT")) == 1;
+    return v;
+  }
+  bool settling = false;  // settle() is completing an asynchronous decode
   int finish_out(clg_decoded* out, uint64_t nrec, uint64_t nwide) {
     out->n_rec = nrec;
     out->n_wide = nwide;
@@ -1240,7 +1262,12 @@ struct clg_engine {
         HIPCHK(hipMemcpyAsync(out->w_sub, d_o_wsub.p, w, hipMemcpyDeviceToHost, stream));
       }
     }
-    CHK(sync());
+    if (settling && own_wait() && out->out_kind == CLG_MEM_DEVICE) {
+      HIPCHK(hipStreamSynchronize(stream));
+      collect_timings(true);
+    } else {
+      CHK(sync());
+    }
     if (nrec > out->cap || nwide > out->wcap)
       return fail(CLG_E_CAPACITY, "decode produced %llu records / %llu wide rows, capacity %llu / %llu",
                   (unsigned long long)nrec, (unsigned long long)nwide, (unsigned long long)out->cap,
@@ -1701,7 +1728,9 @@ struct clg_engine {
     if (!pend.active) return CLG_OK;
     pend.active = false;
     bool aborted = false, need_jser = false;
+    settling = true;
     int st = finish_fused(pend.plan, pend.run, pend.out, pend.span_rec_base, &aborted, &need_jser);
+    settling = false;
     if (st == CLG_OK && aborted)
       st = after_abort(pend.plan, pend.build, pend.run.log_bytes, pend.out, pend.span_rec_base, need_jser);
     pend.status = st;

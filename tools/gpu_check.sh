@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-3 GPU check: the -m gpu suite (all failures listed), smoke, the default bench line.
+# GPU check: the -m gpu suite (all failures listed), smoke, the default bench line.
 # A test failure (pytest rc 1) still runs smoke and bench; a crash, abort or timeout stops.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-OUT=${1:-gpurun_out/r3a}
+OUT=${1:-gpurun_out/check}
 mkdir -p "$OUT"
 echo tests
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > "$OUT/gputest.log" 2>&1

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-3 host-side probe of the config-2 bench step: per-call host time (CLONOS_STEP_PROBE)
+# Host-side probe of the config-2 bench step: per-call host time (CLONOS_STEP_PROBE)
 # and host phases inside the engine (CLONOS_HOST_PROF), plus a kernel trace of the same run.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-OUT=${1:-gpurun_out/r3probe}
+OUT=${1:-gpurun_out/probe}
 mkdir -p "$OUT"
 C2="--steps 20 --warmup 3 --no-cpu-baseline --no-config3 --no-inflight --no-config4 --no-config1"
 echo probe && CLONOS_STEP_PROBE=1 CLONOS_HOST_PROF=1 timeout -k 10 300 python -u bench.py $C2 > "$OUT/probe.json" 2> "$OUT/probe.err" &&

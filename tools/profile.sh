@@ -7,6 +7,7 @@
 #   c2_sq1..c2_sq3            SQ counter groups (instructions, waits, LDS, VALU lane cycles), config 2
 #   c3_trace, c3_fetch, c3_write, c3_sq1..c3_sq3   the same for config 3 (tools/bench_config3.py)
 #   ifl_trace                 rocprofv3 --stats over the in-flight replay leg alone
+#   c4_trace                  rocprofv3 --stats over the config-4 / config-5 legs alone
 # Counters only ever with --kernel-trace (no sys/runtime trace); one group per pass, each
 # within the per-block limits; every GPU step has its own time limit; steps chained with &&.
 set -euo pipefail
@@ -35,4 +36,6 @@ pmc c3_sq1 "$SQ1" python3 tools/bench_config3.py $C3 && pmc c3_sq2 "$SQ2" python
 pmc c3_sq3 "$SQ3" python3 tools/bench_config3.py $C3 &&
 echo "ifl" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ifl_trace" -o run --output-format csv -- \
     python3 bench.py --inflight-only --no-cpu-baseline > "$OUT/ifl_trace.log" 2>&1 &&
+echo "c4" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/c4_trace" -o run --output-format csv -- \
+    python3 bench.py --config4-only > "$OUT/c4_trace.log" 2>&1 &&
 echo "done"

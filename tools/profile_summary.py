@@ -101,7 +101,8 @@ os.makedirs(prof, exist_ok=True)
 bench = [l for l in open(f"{src}/bench.json").read().strip().splitlines() if l.startswith("{")][-1]
 open(os.path.join(prof, f"{tag}_bench.json"), "w").write(bench + "\n")
 b = json.loads(bench)
-for d, name in (("trace", "kernel_stats"), ("c3_trace", "config3_kernel_stats"), ("ifl_trace", "inflight_kernel_stats")):
+for d, name in (("trace", "kernel_stats"), ("c3_trace", "config3_kernel_stats"), ("ifl_trace", "inflight_kernel_stats"),
+                ("c4_trace", "config4_kernel_stats")):
     for f in glob.glob(f"{src}/{d}/**/*kernel_stats.csv", recursive=True):
         shutil.copy(f, os.path.join(prof, f"{tag}_{name}.csv"))
 timed = {}
@@ -121,7 +122,7 @@ pmc = {"config2": decode_table("c2", b["config"]["log_bytes_per_gpu"]),
                "hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH correction)"}
 json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc_decode.json"), "w"), indent=1)
 traffic = {}
-NAMES = {"k_decode_count": "decode_count", "k_decode_emit": "decode_emit", "k_gather_seg": "slice_gather"}
+NAMES = {"k_decode_count": "decode_count", "k_decode_emit": "decode_emit", "k_gather": "slice_gather"}
 for k, name in NAMES.items():
     r = pmc["config2"].get(k, {}).get("derived", {})
     if "hbm_bytes" in r:
