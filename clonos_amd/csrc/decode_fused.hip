@@ -1353,7 +1353,7 @@ __device__ __forceinline__ uint32_t tiny_tiles(const TileDesc* __restrict__ tile
          !(ctl.skip_bad && gp(ctl.span_bad)[td.span]);
   }
   const uint64_t okm = __ballot(ok);
-  const uint32_t m = (uint32_t)__builtin_ctzll(~okm);  // the run: leading lanes
+  const uint32_t m = ~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u;  // the run: leading lanes
   if (m == 0) return 0;
   // 0 ok, 1 invalid record (a bad tag or a record past the span end), 3 a tag this path does not take
   uint32_t why = 0, rec = 0, wide = 0;

@@ -72,3 +72,24 @@ def test_small_log_errors_equal_robust(kind):
         x = ei.value
         errs.append((x.status, x.err_span, x.err_off, x.err_tag, x.n_rec))
     assert errs[0] == errs[1] and errs[0][1] == 123
+
+
+def test_full_runs_of_small_spans():
+    """More small spans than 64 per count block (262 144 spans of 300 bytes): the lane path
+    takes full runs of 64 tiles; every span's records are counted and placed exactly."""
+    from clonos_amd import synth
+    rng = np.random.default_rng(11)
+    n_spans, per = 262144, 60
+    kd = synth.KINDS["buffer_built"]
+    blob, _ = synth.build(np.zeros(n_spans * per, np.int64), [kd], {0: [rng.integers(0, 1 << 31, n_spans * per)]})
+    L = per * 5
+    spans = [(i * L, L) for i in range(n_spans)]
+    with Engine(segment_bytes=16384, pool_segments=64, timing=True) as eng:
+        dec = eng.decode_host(blob, spans)
+        st = eng.kernel_stats()
+    assert "decode_fallback" not in st and "decode_span_fallback" not in st
+    assert dec.n_rec == n_spans * per
+    np.testing.assert_array_equal(np.diff(dec.span_rec_base.astype(np.int64)), per)
+    b = blob.tobytes()
+    for s in rng.integers(0, n_spans, 40):
+        assert_span_equal(dec, int(s), b[s * L:(s + 1) * L])
