@@ -54,15 +54,12 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_COUNT_LM
 #define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
 #endif
-#ifndef CLG_TINY
-#define CLG_TINY 1  // 1: small whole spans a lane each in the count pass (tiny_tiles)
-#endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
-constexpr uint32_t kZTiny = 1024;                      // small whole spans: a lane each in the count pass
+constexpr uint32_t kZTiny = kZTinySpan;                // small whole spans: a lane each (pass 0)
 
 // ---------------------------------------------------------------------------------
 // 128-bit region bitmaps (bit i <-> byte r0 + i of the lane's aligned region r0).
@@ -1329,93 +1326,84 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   }
 }
 
-// Small complete spans, one lane each.  A batch of many small logs (config 4: 65 536
-// subpartition logs of 320 bytes) gives one tile per span, and a wave spent on a 320-byte
-// tile costs as much as one on 8 KiB.  When tile t is a whole span of at most kZTiny bytes,
-// lane i takes tile t + i of the run of such tiles (at most 64, inside the chunk) and walks
-// its span alone from HBM through a 16-byte window: fixed-length records only (Order,
-// Timestamp, RNG, BufferBuilt, IgnoreCheckpoint -- their lengths need no field), with the
-// reference's bounds; it writes the tile's count and record-start bitmap words (emit reads
-// the words of the regions the tile reaches).  A record of another tag anywhere in the run
-// (TimerTrigger, SourceCheckpoint, Serializable: lengths from fields) sends the whole run to
-// the wave path; an invalid tag or a record past the span end marks the span bad (abort
-// reason 1), as count_tile does.  Returns the tiles handled (0: none; ~0: the batch aborts).
-__device__ __forceinline__ uint32_t tiny_tiles(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                               const FusedCtl& ctl, const uint32_t t, const uint32_t t1,
-                                               const uint32_t lane) {
-  const uint32_t ti = t + lane;
-  TileDesc td{};
-  bool ok = false;
-  if (ti < t1) {
-    td = tiles[ti];
-    const SpanDesc sd = spans[td.span];
-    ok = sd.n_tiles == 1 && td.span_off == 0 && td.len > 0 && td.len <= kZTiny && td.len == sd.len &&
-         !(ctl.skip_bad && gp(ctl.span_bad)[td.span]);
-  }
-  const uint64_t okm = __ballot(ok);
-  const uint32_t m = ~okm ? (uint32_t)__builtin_ctzll(~okm) : 64u;  // the run: leading lanes
-  if (m == 0) return 0;
-  // 0 ok, 1 invalid record (a bad tag or a record past the span end), 3 a tag this path does not take
+// Pass 0 (batches holding them): small whole spans, a lane each.  A batch of many small logs
+// (config 4: 65 536 subpartition logs of 320 bytes) gives one tile per span, and a wave spent
+// on a 320-byte tile costs as much as one on 8 KiB.  Lane i of block b takes tile 64 b + i
+// when it is a whole span of at most kZTiny bytes and walks the span alone from HBM through a
+// 16-byte window: fixed-length records only (Order, Timestamp, RNG, BufferBuilt,
+// IgnoreCheckpoint -- lengths need no field), with the reference's bounds.  It writes the
+// tile's count and record-start bitmap words (emit reads the words of the regions the tile
+// reaches) and marks the tile done in st_x (unused for a whole-span tile: no successor
+// enters at its exit), so the count pass skips it.  A TimerTrigger / SourceCheckpoint /
+// Serializable record leaves the tile to the count pass; an invalid record marks the span
+// bad (abort reason 1), as count_tile does.  A separate kernel: inside the count kernel the
+// walk's registers cost the wave path 16 VGPRs and an occupancy step.
+constexpr uint64_t kZTinyDone = 1ull << 62;  // st_x word of a tile pass 0 counted
+__device__ __forceinline__ bool tiny_tile(const TileDesc& td, const SpanDesc& sd) {
+  return sd.n_tiles == 1 && td.span_off == 0 && td.len > 0 && td.len <= kZTiny && td.len == sd.len;
+}
+__global__ __launch_bounds__(64) void k_decode_count_tiny(const TileDesc* __restrict__ tiles,
+                                                          const SpanDesc* __restrict__ spans, FusedCtl ctl) {
+  const uint32_t ti = blockIdx.x * 64 + threadIdx.x;
+  if (ti >= ctl.n_tiles) return;
+  const TileDesc td = tiles[ti];
+  if (!tiny_tile(td, spans[td.span]) || (ctl.skip_bad && gp(ctl.span_bad)[td.span])) return;
+  // 0 ok, 1 invalid record (a bad tag or a record past the span end), 3 a tag this path leaves
   uint32_t why = 0, rec = 0, wide = 0;
-  if (lane < m) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
-    const uint32_t end = td.delta + td.len;
-    uint32_t a = td.delta, wb = 0xFFFFFFFFu, cur = 0;
-    u32x4 w{};
-    uint64_t blo = 0, bhi = 0;
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    auto* bits = gp(reinterpret_cast<u64x2*>(ctl.bits)) + (uint64_t)ti * 64;
-    // fixed lengths by tag (0: takes fields or invalid)
-    constexpr uint32_t kLut = 2u | 9u << 4 | 5u << 8 | 13u << 24 | 5u << 28;
-    while (a < end) {
-      if ((a >> 4) != wb) {  // the 16-byte window holding the tag
-        wb = a >> 4;
-        w = src[wb];
-      }
-      const uint32_t q = a & 15u;
-      const uint32_t dw = q < 8u ? (q < 4u ? w.x : w.y) : (q < 12u ? w.z : w.w);
-      const uint32_t tg = (dw >> (8u * (q & 3u))) & 0xFFu;
-      const uint32_t L = tg < 8u ? (kLut >> (4u * tg)) & 0xFu : 0u;
-      if (!L) {
-        why = (tg == CLG_TAG_SERIALIZABLE || tg == CLG_TAG_TIMER_TRIGGER || tg == CLG_TAG_SOURCE_CHECKPOINT) ? 3u : 1u;
-        break;
-      }
-      if (a + L > end) {  // (the true chain's bound: an invalid record, count_tile's reason 1)
-        why = 1u;
-        break;
-      }
-      for (const uint32_t r = a >> 7; cur < r; ++cur) {  // the regions before this start are complete
-        u64x2 v;
-        v.x = blo;
-        v.y = bhi;
-        bits[cur] = v;
-        blo = bhi = 0;
-      }
-      const uint32_t i = a & 127u;
-      if (i < 64u) blo |= 1ull << i; else bhi |= 1ull << (i - 64u);
-      ++rec;
-      wide += tg == CLG_TAG_IGNORE_CHECKPOINT ? 1u : 0u;
-      a += L;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
+  auto* bits = gp(reinterpret_cast<u64x2*>(ctl.bits)) + (uint64_t)ti * 64;
+  const uint32_t end = td.delta + td.len;
+  uint32_t a = td.delta, wb = 0xFFFFFFFFu, cur = 0;
+  u32x4 w{};
+  uint64_t blo = 0, bhi = 0;
+  constexpr uint32_t kLut = 2u | 9u << 4 | 5u << 8 | 13u << 24 | 5u << 28;  // fixed lengths (0: fields)
+  while (a < end) {
+    if ((a >> 4) != wb) {  // the 16-byte window holding the tag
+      wb = a >> 4;
+      w = src[wb];
     }
-    if (!why) {
-      for (const uint32_t r = (end - 1) >> 7; cur <= r; ++cur) {
-        u64x2 v;
-        v.x = blo;
-        v.y = bhi;
-        bits[cur] = v;
-        blo = bhi = 0;
-      }
-      gp(ctl.cnt)[ti] = pack_cnt(rec, wide);
+    const uint32_t q = a & 15u;
+    const uint32_t dw = q < 8u ? (q < 4u ? w.x : w.y) : (q < 12u ? w.z : w.w);
+    const uint32_t tg = (dw >> (8u * (q & 3u))) & 0xFFu;
+    const uint32_t L = tg < 8u ? (kLut >> (4u * tg)) & 0xFu : 0u;
+    if (!L) {
+      why = (tg == CLG_TAG_SERIALIZABLE || tg == CLG_TAG_TIMER_TRIGGER || tg == CLG_TAG_SOURCE_CHECKPOINT) ? 3u : 1u;
+      break;
     }
+    if (a + L > end) {  // (the true chain's bound: an invalid record, count_tile's reason 1)
+      why = 1u;
+      break;
+    }
+    for (const uint32_t r = a >> 7; cur < r; ++cur) {  // the regions before this start are complete
+      u64x2 v;
+      v.x = blo;
+      v.y = bhi;
+      bits[cur] = v;
+      blo = bhi = 0;
+    }
+    const uint32_t i = a & 127u;
+    if (i < 64u) blo |= 1ull << i; else bhi |= 1ull << (i - 64u);
+    ++rec;
+    wide += tg == CLG_TAG_IGNORE_CHECKPOINT ? 1u : 0u;
+    a += L;
   }
-  if (__any(why == 3u)) return 0;  // the run takes the wave path (its words are rewritten there)
-  if (lane < m && why) {
+  if (why == 3u) return;  // the count pass takes this tile (its words are rewritten there)
+  if (why == 0u) {
+    for (const uint32_t r = (end - 1) >> 7; cur <= r; ++cur) {
+      u64x2 v;
+      v.x = blo;
+      v.y = bhi;
+      bits[cur] = v;
+      blo = bhi = 0;
+    }
+    gp(ctl.cnt)[ti] = pack_cnt(rec, wide);
+  } else {
     raise_abort(ctl, why, ti);
     if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + td.span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!ctl.span_bad && __any(why != 0u)) return 0xFFFFFFFFu;  // the batch aborts (no per-span fallback)
-  return m;
+  gp(ctl.st_x)[ti] = kZTinyDone;
 }
 
 // Pass 1 kernel.  Persistent grid (at most what the device keeps resident, see
@@ -1463,14 +1451,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
-    if (CLG_TINY && !J && z.first && z.last && z.td.len <= kZTiny && !ctl.nodep && !ctl.prof) {
-      const uint32_t m = tiny_tiles(tiles, spans, ctl, t, t1, lane);  // small whole spans, a lane each
-      if (m == 0xFFFFFFFFu) return;
-      if (m) {
-        t += m - 1;
-        continue;
-      }
-    }
+    if (!J && ctl.tiny && z.first && z.last && z.td.len <= kZTiny && gp(ctl.st_x)[t] == kZTinyDone)
+      continue;  // (wave-uniform) pass 0 counted this small whole span
     const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
@@ -1821,6 +1803,8 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
       ZLAUNCH(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
     else
       ZLAUNCH(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+  } else if (phase == 4) {
+    ZLAUNCH(k_decode_count_tiny, dim3((nt + 63) / 64), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits

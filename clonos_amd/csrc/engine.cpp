@@ -1056,6 +1056,7 @@ struct clg_engine {
     std::vector<clg::SegSpan> runs;     // log spans: tiles generated on the device
     std::vector<uint32_t> segtab;       // concatenated segment indices of the runs' logs
     uint32_t n_tiles = 0;
+    uint32_t n_tiny = 0;                // whole spans of one tile and at most kZTinySpan bytes
     uint32_t unit = 0;                  // device-planning tile window
     int64_t only = -1;                  // >= 0: plan only this span of the batch (as span 0)
   };
@@ -1086,6 +1087,7 @@ struct clg_engine {
       o += take;
       sd.n_tiles++;
     }
+    p.n_tiny += (sd.n_tiles == 1 && len <= clg::kZTinySpan) ? 1u : 0u;
     p.spans.push_back(sd);
     p.n_tiles = uint32_t(p.tiles.size());
   }
@@ -1096,6 +1098,7 @@ struct clg_engine {
     if (const uint32_t U = p.unit) {  // device planning
       const uint32_t cnt = len > 0 ? (uint32_t(start + len - 1) / U - uint32_t(start) / U + 1) : 0;
       p.spans.push_back(clg::SpanDesc{p.n_tiles, cnt, uint64_t(len)});
+      p.n_tiny += (cnt == 1 && uint32_t(len) <= clg::kZTinySpan) ? 1u : 0u;
       if (cnt) {  // only the segments the span covers go into the table (phys rebased on them)
         const uint32_t s0 = uint32_t(start) / C(), s1 = uint32_t(start + len - 1) / C() + 1;
         p.runs.push_back(clg::SegSpan{p.segtab.size(), uint32_t(start) - s0 * C(), uint32_t(len), s, p.n_tiles, 0});
@@ -1122,6 +1125,7 @@ struct clg_engine {
       }
       ph += int32_t(take);
     }
+    p.n_tiny += (sd.n_tiles == 1 && uint32_t(len) <= clg::kZTinySpan) ? 1u : 0u;
     p.spans.push_back(sd);
     p.n_tiles = uint32_t(p.tiles.size());
   }
@@ -1173,20 +1177,25 @@ struct clg_engine {
     return CLG_OK;
   }
   // The count pass's chunks of about equal cost: a tile costs its bytes plus a fixed 1 KiB
-  // (tiles of one span are taken as equally long), and block b takes the tiles whose
-  // cumulative cost passes b / G of the total.  ch[0 .. G]: boundaries, ch[G] = n_tiles.
-  static void count_chunks(const DecodePlan& p, uint32_t G, std::vector<uint32_t>& ch) {
+  // (tiles of one span are taken as equally long; a small whole span that pass 0 counted, a
+  // skip), and block b takes the tiles whose cumulative cost passes b / G of the total.
+  // ch[0 .. G]: boundaries, ch[G] = n_tiles.
+  static void count_chunks(const DecodePlan& p, uint32_t G, bool tiny, std::vector<uint32_t>& ch) {
     ch.assign(size_t(G) + 1, p.n_tiles);
     ch[0] = 0;
-    constexpr double kTileCost = 1024.0;
+    constexpr double kTileCost = 1024.0, kTinyCost = 64.0;  // (pass 0 counted the small whole spans)
+    auto cost = [&](const clg::SpanDesc& s) {
+      return tiny && s.n_tiles == 1 && s.len <= clg::kZTinySpan ? kTinyCost : double(s.len) / s.n_tiles + kTileCost;
+    };
     double total = 0;
-    for (const auto& s : p.spans) total += double(s.len) + kTileCost * s.n_tiles;
+    for (const auto& s : p.spans)
+      if (s.n_tiles) total += cost(s) * s.n_tiles;
     const double target = total / G;
     double acc = 0, next = target;
     uint32_t b = 1;
     for (const auto& s : p.spans) {
       if (!s.n_tiles) continue;
-      const double c = double(s.len) / s.n_tiles + kTileCost, end = acc + c * s.n_tiles;
+      const double c = cost(s), end = acc + c * s.n_tiles;
       while (b < G && next <= end) {  // boundary inside this span: the first tile past it
         const double k = (next - acc) / c;
         ch[b++] = s.first_tile + std::min<uint32_t>(s.n_tiles, uint32_t(k) + (k > double(uint32_t(k)) ? 1u : 0u));
@@ -1331,7 +1340,11 @@ struct clg_engine {
     // chunks of equal cost when blocks take several tiles of spans of different sizes
     const uint32_t G = clg::decode_count_grid(jser, nt);
     const bool chunked = G && nt > G && ns > 1;
-    if (chunked) count_chunks(p, G, chunk_buf);
+    const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
+    const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
+    // pass 0 (small whole spans, a lane each) for batches without Serializable tables
+    const bool tiny = p.n_tiny && !jser && !prof_path && !getenv("CLONOS_FUSED_NODEP");
+    if (chunked) count_chunks(p, G, tiny, chunk_buf);
     PlanLayout L;
     CHK(stage_plan(p, d_ztiles, &L, chunked ? &chunk_buf : nullptr));
     clg::DecodeOut o{};
@@ -1345,8 +1358,6 @@ struct clg_engine {
     CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
-    const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
-    const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
     if (zdbg) CHK(d_dbg.ensure(16 * 4 + 64 * 32));
     if (prof_path) CHK(d_prof.ensure(size_t(nt) * 64));
     if (jser) {
@@ -1366,6 +1377,7 @@ struct clg_engine {
     ctl.span_bad = d_zbad.as<uint32_t>();
     ctl.skip_bad = 0;
     ctl.chunk = chunked ? reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_chunk) : nullptr;
+    ctl.tiny = tiny ? 1u : 0u;
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -1385,6 +1397,7 @@ struct clg_engine {
       HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
+      if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
       for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
         if (ph == 3 && !jser) continue;
         const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;

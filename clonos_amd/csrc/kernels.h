@@ -210,13 +210,15 @@ struct FusedCtl {
   // beside a few large ones (config 4: 320-byte subpartition logs, 22 KB main logs) would
   // otherwise give a few blocks chunks of only large tiles and make them the critical path.
   const uint32_t* chunk;
+  uint32_t tiny;  // pass 0 ran (k_decode_count_tiny): small whole spans are counted already
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
+constexpr uint32_t kZTinySpan = 1024;   // whole spans up to this many bytes: pass 0, a lane each
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
 // 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
 // abort[7] != 0: phase 3 found Serializable candidates (any tile)
-// phase 0: count, 1: scan, 2: emit, 3: Serializable tables
+// phase 0: count, 1: scan, 2: emit, 3: Serializable tables, 4: small whole spans (before 0)
 // Per-span fallback: cnt[t] of every tile of bad span bad[i] := t == its first tile ?
 // packed[i] (the robust decode's wide << 31 | records) : 0.
 int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const uint64_t* d_packed, uint32_t n_bad,
