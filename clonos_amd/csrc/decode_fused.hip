@@ -876,9 +876,13 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
 // Pass 1 for one tile, given its true entry e_true (aligned coordinate): spec walks,
 // true chain, exit checks, then the tile's record / wide-record counts and its
 // record-start bitmap (1 KiB) for the emit pass.  *x_true = the tile's exit.  must_exit:
-// the exit the successor already uses (kZCanon: none).  false once the batch aborted.
+// the exit the successor already uses (kZCanon: none).  Returns 0, or the reason the chain
+// went wrong (the caller decides what it means): 1 an invalid record, 2 the last record
+// does not end at the span end, 5 a Serializable record without tables -- no counts
+// written -- or 3: the exit is not must_exit (counts written: the tile itself is right,
+// the successor entered at the wrong place).
 template <bool J>
-__device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
+__device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z, const uint32_t e_true,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
                                            const uint32_t lane, uint32_t* x_out, const JL& jl,
                                            const TileDesc* __restrict__ tiles = nullptr,
@@ -908,12 +912,26 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   };
   Res r = merge(entry);
   uint32_t steps0 = r.steps, steps_more = 0, iters = 0;
+  // A chain that keeps its offset from the speculative one in every region (records at odd
+  // offsets of a run of 2-byte Order records, where every speculative chain is even) changes
+  // one lane per pass: 64 passes.  When two passes in a row each changed one lane by the same
+  // shift, the lanes above it take that shift too (a guess: the next pass checks it, and
+  // every pass still settles its lowest changed lane for good).
+  uint32_t shift = 0;
   for (int it = 0; it <= 64; ++it) {
     const uint32_t prev = __shfl_up(r.exit, 1);
-    const uint32_t want = lane == 0 ? e_true : prev;
-    const bool ch = want != entry;
-    if (!__any(ch)) break;
+    uint32_t want = lane == 0 ? e_true : prev;
+    bool ch = want != entry;
+    const uint64_t cm = __ballot(ch);
+    if (!cm) break;
     ++iters;
+    const uint32_t low = (uint32_t)__builtin_ctzll(cm);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)(want - entry), (int)low);
+    if ((cm & (cm - 1)) == 0 && d == shift && lane > low) {
+      want = entry + d;
+      ch = true;
+    }
+    shift = (cm & (cm - 1)) == 0 ? d : 0u;
     if (ch) {
       entry = want;
       r = merge(want);
@@ -953,13 +971,8 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
       d[7] = r.exit | r.bad << 31;
     }
   }
-  if (reason && !ctl.nodep) {
-    if (lane == 0) {
-      raise_abort(ctl, reason, t);
-      if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + z.td.span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return false;
-  }
+  if (ctl.nodep) reason = 0;
+  if (reason && reason != 3u) return reason;
 
   ZPHASE(3);
   // ---- counts and the record-start bitmap for the emit pass
@@ -977,7 +990,7 @@ __device__ __forceinline__ bool count_tile(const uint32_t t, const ZTile& z, con
   gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = out_bits;
   ZPHASE(4);
 #undef ZPHASE
-  return true;
+  return reason;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1406,13 +1419,141 @@ __global__ __launch_bounds__(64) void k_decode_count_tiny(const TileDesc* __rest
   gp(ctl.st_x)[ti] = kZTinyDone;
 }
 
+// Chunk-boundary repair.  A chunk enters at its predecessor's published canonical exit.
+// Where the predecessor's true exit differs (a record the canonical walk cannot measure --
+// longer than a tile, or a chunk's last tile lying wholly inside one -- crosses the chunk
+// end), or where a chain from a published entry goes wrong, the block records a request
+// instead of failing the span.  k_decode_repair then serves the requests in chunk order:
+// from the true exit of the tile before the chunk it counts tiles again until the new
+// chain's exit equals the old chain's (from there on the two agree), the span ends, or the
+// chain fails (then the span is bad, for real).  Then any tile of that chunk's first span
+// still without an exit failed on the true chain: its span is bad.
+constexpr uint64_t kZExValid = 1ull << 63;  // ex[t]: the tile's exit (span offset) is known
+
+// A request: chunk c's flag (idempotent, so a chunk asked for twice is served once) and the
+// request count, which lets k_decode_repair return at once in the usual batch.
+__device__ __forceinline__ void push_repair(const FusedCtl& ctl, uint32_t c) {
+  gp(ctl.rep_flag)[c] = 1u;
+  atomicAdd(ctl.rep + 1, 1u);
+}
+__device__ __forceinline__ void mark_bad(const FusedCtl& ctl, uint32_t reason, uint32_t t, uint32_t span) {
+  raise_abort(ctl, reason, t);
+  if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// First tile of chunk c of the count pass's G chunks (c = G: n_tiles).
+__device__ __forceinline__ uint32_t chunk_first(const FusedCtl& ctl, uint32_t c, uint32_t K, uint32_t G) {
+  if (c >= G) return ctl.n_tiles;
+  return ctl.chunk ? ctl.chunk[c] : min(ctl.n_tiles, c * K);
+}
+// After chunk c's request: a tile of its first span without an exit failed for real.
+__device__ __forceinline__ void check_chunk(const FusedCtl& ctl, const TileDesc* __restrict__ tiles, uint32_t f,
+                                            uint32_t ce, uint32_t lane) {
+  const uint32_t span = tiles[f].span;
+  uint32_t bad = 0xFFFFFFFFu;
+  for (uint32_t i = f + lane; i < ce; i += 64) {
+    if (tiles[i].span != span) break;
+    if (!(ld_agent(&ctl.ex[i]) & kZExValid)) {
+      bad = i;
+      break;
+    }
+  }
+  const uint64_t m = __ballot(bad != 0xFFFFFFFFu);
+  if (m && lane == (uint32_t)__builtin_ctzll(m)) mark_bad(ctl, 1, bad, span);
+}
+
+// Tile t staged (image, and with tables the map and table) and counted from entry xs (span
+// offset); *x = its exit (span offset).  count_tile's reason.
+template <bool J>
+__device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                 const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_j, uint32_t lane,
+                                                 uint32_t t, const ZTile& z, uint64_t xs, uint32_t must_exit,
+                                                 const SpecR* walked, uint64_t* x) {
+  constexpr bool kLm = CLG_COUNT_LM != 0;
+  const uint32_t nt = ctl.n_tiles;
+  const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
+  const uint64_t ee = xs - z.td.span_off + z.lo;
+  const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+  JL jl{nullptr, nullptr, nullptr};
+  JLPre pre{};
+  if (J) pre = jl_prefetch(ctl, t, lane);
+  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
+  if (J && kLm) build_lm(z, s_img, s_j, lane);
+  if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
+  else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
+  uint32_t x_true;
+  const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked);
+  *x = z.td.span_off + (x_true - z.lo);
+  return why;
+}
+
+// Tiles a repair walk may find where the old chain had an exit too, a different one.  Past
+// that the two are taken to be chains that never meet -- a run of channel-0 Order records
+// ("00 00") at odd offsets, where every chunk entered on the even chain -- and the span goes
+// to the robust pipeline instead of a walk to its end (one wave counts about a tile per 50 us
+// with nothing to hide its latencies).  Tiles where the old chain had failed (entered inside
+// a long record) do not count: a run of long records a short gap apart needs a long walk.
+constexpr uint32_t kZWalkDisagree = 4;
+
+// Chunk c's request (k_decode_repair).  *walk_end: past the last tile a walk reached.
+template <bool J>
+__device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                            const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_j, uint32_t lane,
+                                            uint32_t f, uint32_t ce, uint32_t* walk_end) {
+  if (f == 0 || f >= ce || tiles[f].span_off == 0) return;  // the chunk starts its span
+  if (f >= *walk_end) {  // (else a walk has rewritten this chunk's entry already)
+    const uint64_t xe = ld_agent(&ctl.ex[f - 1]);
+    if (!(xe & kZExValid)) {  // the tile before failed: its span (this chunk's first) is bad
+      if (lane == 0) mark_bad(ctl, 1, f - 1, tiles[f].span);
+      return;
+    }
+    uint64_t xs = xe & ~kZExValid;
+    if (xs != (ld_agent(&ctl.st_x[f - 1]) & ~(1ull << 63))) {  // entered elsewhere: walk from the true exit
+      uint32_t disagree = 0;
+      for (uint32_t t = f; t < ctl.n_tiles; ++t) {
+        const ZTile z = ztile(tiles, spans, t, lane);
+        *walk_end = t + 1;
+        uint64_t x = xs;
+        uint32_t why = 0;
+        if (!z.last && xs >= z.td.span_off + z.td.len) {  // wholly inside a record: no starts
+          typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+          gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = u64x2{0, 0};
+          if (lane == 0) gp(ctl.cnt)[t] = 0;
+        } else {
+          why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x);
+          __syncthreads();  // the image is reused
+        }
+        if (why) {
+          if (lane == 0) mark_bad(ctl, why, t, z.td.span);
+          break;
+        }
+        const uint64_t xv = kZExValid | x;
+        uint32_t old = 0;
+        if (lane == 0) {
+          const uint64_t o = ld_agent(&ctl.ex[t]);
+          old = o == xv ? 1u : (o & kZExValid) ? 2u : 0u;  // 1 the same, 2 another exit, 0 none
+          st_agent(&ctl.ex[t], xv);
+        }
+        old = __shfl(old, 0);
+        if (old == 1u || z.last) break;  // resynchronised, or the span ends
+        if (old == 2u && ++disagree > kZWalkDisagree) {  // chains that do not meet: the span goes robust
+          if (lane == 0) mark_bad(ctl, 3, t, z.td.span);
+          break;
+        }
+        xs = x;
+      }
+    }
+  }
+  check_chunk(ctl, tiles, f, ce, lane);  // its failures past the walk are real
+}
+
 // Pass 1 kernel.  Persistent grid (at most what the device keeps resident, see
-// launch_decode_fused); block b decodes the contiguous chunk of tiles [b K, (b + 1) K).
+// launch_decode_fused); block b decodes the chunk of tiles [chunk[b], chunk[b + 1]).
 // Inside a chunk a tile's entry is its predecessor's true exit.  Across chunks: each block
 // first publishes the canonical exit of its chunk's last tile (no waiting before that),
 // and a chunk's first tile enters at the previous chunk's published exit, which that
-// chunk's last tile must then reproduce.  Blocks are all resident and publish first, so
-// the one wait always ends; a wait past kZSpinLimit cycles aborts the batch instead.
+// chunk's last tile then checks (a mismatch: a repair request, above).  Blocks are all
+// resident and publish first, so the one wait always ends; a wait past kZSpinLimit cycles
+// aborts the batch instead.
 // 128 VGPRs (4 waves per SIMD by registers, 3.25 by LDS with tables): count<J> 0.396 to
 // 0.376 ms on the config-3 subset, count<false> (88 VGPRs) unaffected.  The same bound on
 // k_decode_jser made it slower (0.26 to 0.28 ms), so that kernel keeps its 150.
@@ -1425,13 +1566,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
-  const uint32_t t0 = ctl.chunk ? ctl.chunk[blockIdx.x] : blockIdx.x * K;
-  const uint32_t t1 = ctl.chunk ? ctl.chunk[blockIdx.x + 1] : min(nt, t0 + K);
-  if (t0 >= t1) return;
+  const uint32_t t0 = chunk_first(ctl, blockIdx.x, K, gridDim.x), t1 = chunk_first(ctl, blockIdx.x + 1, K, gridDim.x);
   // the chunk's last tile: publish its canonical exit (span offset) for the next chunk
   uint32_t x_pub = kZCanon;
   SpecR sp_last{{0, 0}, {0, 0}, 0, 0, 0};  // its speculative walk, reused when the loop reaches it
-  {
+  if (t0 < t1) {
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
@@ -1448,12 +1587,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
   uint64_t x_prev = 0;  // previous tile's exit, span offset
   uint32_t bad_span = 0xFFFFFFFFu;  // a span whose chain went wrong: its later tiles are skipped
+  uint32_t sus_span = 0xFFFFFFFFu;  // the chunk's first span, entered at a published exit
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
     if (!J && ctl.tiny && z.first && z.last && z.td.len <= kZTiny && gp(ctl.st_x)[t] == kZTinyDone)
       continue;  // (wave-uniform) pass 0 counted this small whole span
-    const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
     if (z.first || ctl.nodep) {
@@ -1467,32 +1606,82 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       for (;;) {
         v = ld_agent(&ctl.st_x[t - 1]);
         if (v) break;
-        if (ld_agent32(ctl.abort)) return;
+        if (ld_agent32(ctl.abort + 4)) return;  // another wait timed out: the batch goes robust
         if (!backoff(nb, w0)) {
           if (lane == 0) raise_abort(ctl, 4, t);
           return;
         }
       }
       xs = v & ~(1ull << 63);
+      sus_span = z.td.span;
     }
-    const uint64_t ee = xs - z.td.span_off + z.lo;
-    const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
-    JLPre pre{};
-    if (J) pre = jl_prefetch(ctl, t, lane);
-    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
-    if (J && kLm) build_lm(z, s_img, s_j, lane);
-    if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
-    else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
-    uint32_t x_true;
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
-    if (!count_tile<J>(t, z, e_true, t + 1 == t1 ? x_pub : kZCanon, ctl, s_img, lane, &x_true, jl, tiles,
-                       reuse ? &sp_last : nullptr)) {
-      if (!ctl.span_bad) return;
-      bad_span = z.td.span;  // the next span starts on a record boundary: go on there
+    uint64_t x;
+    const uint32_t why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, t + 1 == t1 ? x_pub : kZCanon,
+                                         reuse ? &sp_last : nullptr, &x);
+    if (why == 0u || why == 3u) {
+      x_prev = x;
+      if (lane == 0) {
+        st_agent(&ctl.ex[t], kZExValid | x);
+        if (why == 3u) {  // the chunk holding the next tile entered elsewhere (empty chunks skipped)
+          uint32_t c = blockIdx.x + 1;
+          while (chunk_first(ctl, c + 1, K, gridDim.x) == t1) ++c;
+          push_repair(ctl, c);
+        }
+      }
     } else {
-      x_prev = z.td.span_off + (x_true - z.lo);
+      const bool soft = why != 5u && z.td.span == sus_span;  // the published entry may be wrong
+      if (lane == 0) {
+        if (soft) push_repair(ctl, blockIdx.x);
+        else mark_bad(ctl, why, t, z.td.span);
+      }
+      if (!soft && !ctl.span_bad) return;
+      bad_span = z.td.span;  // the next span starts on a record boundary: go on there
     }
     __syncthreads();  // the image is reused by the next tile
+  }
+}
+
+// The repair requests, right after the count pass: one block per chunk (the count pass's
+// grid).  Block b serves the flagged chunks of the span holding chunk b's first tile, in
+// order, when b is that span's first flagged chunk; spans are independent, so their walks run
+// side by side.  In the usual batch (no requests) every block reads one word and returns.  A
+// loop of its own in the count kernel, the repairs took it from 93 to 121 VGPRs (128 to 179
+// with tables), and as a second loop after the chunk's, with tables, to 158.
+template <bool J>
+__global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                      FusedCtl ctl) {
+  __shared__ uint32_t s_img[kZImgDw];
+  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
+  // nothing to do, or the batch goes again anyway (4 a wait timed out, 5 Serializable records
+  // without tables: again with them, 6 a table overflowed)
+  if (ctl.nodep || !ld_agent32(ctl.rep + 1) || ld_agent32(ctl.abort + 4) || ld_agent32(ctl.abort + 5) ||
+      ld_agent32(ctl.abort + 6))
+    return;
+  const uint32_t G = gridDim.x, b = blockIdx.x, lane = threadIdx.x, K = (ctl.n_tiles + G - 1) / G;
+  if (!gp(ctl.rep_flag)[b]) return;
+  const uint32_t fb = chunk_first(ctl, b, K, G);
+  if (fb >= chunk_first(ctl, b + 1, K, G)) return;  // (an empty chunk is never asked for)
+  const uint32_t span = tiles[fb].span;
+  // an earlier flagged chunk of the same span: that chunk's block serves this one
+  for (uint32_t hi = b; hi > 0;) {
+    const uint32_t lo = hi > 64u ? hi - 64u : 0u, k = lo + lane;
+    const bool in = k < hi;
+    const uint32_t ft = in ? chunk_first(ctl, k, K, G) : 0u;
+    const uint32_t kt = in ? chunk_first(ctl, k + 1, K, G) : 0u;
+    // a chunk's flag is for its first tile's span: chunk k counts when that is this span (an
+    // empty chunk: no tiles, the scan goes on past it)
+    const bool empty = in && kt == ft, same = in && !empty && tiles[ft].span == span;
+    if (__any(same && gp(ctl.rep_flag)[k])) return;
+    if (!__all(!in || empty || same)) break;  // the span starts inside [lo, hi)
+    hi = lo;
+  }
+  uint32_t walk_end = 0;
+  for (uint32_t c = b; c < G; ++c) {
+    const uint32_t f = chunk_first(ctl, c, K, G), ce = chunk_first(ctl, c + 1, K, G);
+    if (f >= ce) continue;
+    if (tiles[f].span != span) break;
+    if (gp(ctl.rep_flag)[c]) serve_chunk<J>(tiles, spans, ctl, s_img, s_j, lane, f, ce, &walk_end);
   }
 }
 
@@ -1799,10 +1988,13 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     const uint32_t grid = decode_count_grid(ctl.jser != 0, nt);
     if (!grid) return CLG_E_DEVICE;
     const int j = ctl.jser ? 1 : 0;
-    if (j)
+    if (j) {
       ZLAUNCH(k_decode_count<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
-    else
+      ZLAUNCH(k_decode_repair<true>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    } else {
       ZLAUNCH(k_decode_count<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+      ZLAUNCH(k_decode_repair<false>, dim3(grid), dim3(64), 0, st, d_tiles, d_spans, ctl);
+    }
   } else if (phase == 4) {
     ZLAUNCH(k_decode_count_tiny, dim3((nt + 63) / 64), dim3(64), 0, st, d_tiles, d_spans, ctl);
   } else if (phase == 1) {

@@ -1349,13 +1349,15 @@ struct clg_engine {
     CHK(stage_plan(p, d_ztiles, &L, chunked ? &chunk_buf : nullptr));
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
-    // words: st_x[nt] cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] | abort[8] (u32); bits apart
-    const size_t nbk = (size_t(nt) + 1023) / 1024;
-    const size_t o_span = 3 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), words = o_ab + 4;
+    // words: st_x[nt] ex[nt] rep_flag[nt] (u8) cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] |
+    // abort[8] rep[2] (u32); bits apart.  st_x, ex and rep_flag are zeroed per batch.
+    const size_t nbk = (size_t(nt) + 1023) / 1024, fw = (size_t(nt) + 7) / 8;
+    const size_t o_cnt = 2 * size_t(nt) + fw;
+    const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), words = o_ab + 5;
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
-    CHK(h_zres.ensure((2 * size_t(ns) + 4) * 8));
+    CHK(h_zres.ensure((2 * size_t(ns) + 5) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     if (zdbg) CHK(d_dbg.ensure(16 * 4 + 64 * 32));
@@ -1366,7 +1368,7 @@ struct clg_engine {
       CHK(d_zjn.ensure(size_t(nt) * 4));
       CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
     }
-    clg::FusedCtl ctl{w, w + nt, w + 2 * size_t(nt), w + 3 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
+    clg::FusedCtl ctl{w, w + o_cnt, w + o_cnt + nt, w + o_cnt + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
@@ -1378,6 +1380,9 @@ struct clg_engine {
     ctl.skip_bad = 0;
     ctl.chunk = chunked ? reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_chunk) : nullptr;
     ctl.tiny = tiny ? 1u : 0u;
+    ctl.ex = w + nt;
+    ctl.rep_flag = reinterpret_cast<uint8_t*>(w + 2 * size_t(nt));
+    ctl.rep = ab + 8;
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -1393,8 +1398,8 @@ struct clg_engine {
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
       if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
-      HIPCHK(hipMemsetAsync(w, 0, size_t(nt) * 8, stream));
-      HIPCHK(hipMemsetAsync(ab, 0, 32, stream));
+      HIPCHK(hipMemsetAsync(w, 0, o_cnt * 8, stream));  // st_x, ex, rep_flag
+      HIPCHK(hipMemsetAsync(ab, 0, 40, stream));                // abort words, repair counters
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
       if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
@@ -1408,7 +1413,7 @@ struct clg_engine {
       if (evp) HIPCHK(hipEventRecord(evp[1], stream));
       // read the span ranges and abort words (emit ran right behind the scan: it returns at
       // once when the batch aborted, and its stores are bounded by the output capacity)
-      HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 5) * 8, hipMemcpyDeviceToHost, stream));
       if (jser) CHK(jarena_note(0));
       return CLG_OK;
     };
@@ -1456,6 +1461,7 @@ struct clg_engine {
     }
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
+    if (hab[9]) stats["decode_chunk_repair"].launches += hab[9];  // repair requests the count pass served
     const bool spilled = jser && jarena_spilled(0);  // a stream walk found the spill arena full
     if (spilled) CHK(jarena_grow());
     if (hab[0] || spilled) {

@@ -211,6 +211,12 @@ struct FusedCtl {
   // otherwise give a few blocks chunks of only large tiles and make them the critical path.
   const uint32_t* chunk;
   uint32_t tiny;  // pass 0 ran (k_decode_count_tiny): small whole spans are counted already
+  // Chunk-boundary repair (k_decode_count files, k_decode_repair serves): ex[t] = 1 << 63 |
+  // the tile's exit (span offset), 0 while unknown; rep_flag[c] = 1: chunk c needs a check;
+  // rep[1]: requests filed (rep[0] unused).  All zeroed per batch.
+  uint64_t* ex;
+  uint8_t* rep_flag;
+  uint32_t* rep;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan

@@ -2,14 +2,17 @@
 settle, cost only their own span.
 
 A TimerTrigger name of 40 KB or a Serializable stream of 9 KB anywhere in a batch used to
-send the whole batch to the robust pipeline.  Now only the span holding it may leave the
-fast path (the per-span fallback); each case is bit-exact against the oracle (16 KiB
-segments; a record may cross segments, tiles and the count pass's chunk boundaries).  SimpleDeterminantEncoder.java:228-242 (TimerTrigger
+send the whole batch to the robust pipeline, and in round 3 still its span (the per-span
+fallback).  Now such records stay on the fast path: a record that crosses a chunk boundary of
+the count pass is repaired there (k_decode_repair), and only a span the fast rules cannot
+settle goes robust.  Each case is bit-exact against the oracle (16 KiB segments; a record
+may cross segments, tiles and the count pass's chunk boundaries).  SimpleDeterminantEncoder.java:228-242 (TimerTrigger
 name), :273-287 (SourceCheckpoint reference), :333-341 (Serializable stream)."""
 import numpy as np
 import pytest
 
-from clonos_amd import Engine
+import _oracle as O
+from clonos_amd import ClonosError, Engine
 from clonos_amd import determinants as D
 from clonos_amd import synth
 from test_gpu_decode import assert_span_equal
@@ -19,6 +22,20 @@ pytestmark = pytest.mark.gpu
 
 def fell_back(eng) -> bool:
     return "decode_fallback" in eng.kernel_stats()
+
+
+def went_robust(eng) -> bool:
+    """Any robust decode: the whole batch or a span of it."""
+    ks = eng.kernel_stats()
+    return "decode_fallback" in ks or "decode_span_fallback" in ks
+
+
+def _join(spans):
+    blob, sp = b"", []
+    for b in spans:
+        sp.append((len(blob), len(b)))
+        blob += b
+    return blob, sp
 
 
 @pytest.fixture
@@ -43,10 +60,9 @@ def _long(kind: str, n: int, i: int = 0) -> bytes:
 @pytest.mark.parametrize("kind,n", [("timer", 40000), ("checkpoint", 20000), ("string", 9000),
                                     ("intarray", 9000), ("timer", 9000), ("string", 30000)])
 def test_long_record_span_alone(leng, kind, n):
-    """One long record in one span of a batch of twelve: at most that span leaves the fast path
-    (decode_span_fallback), never the whole batch (decode_fallback); bit-exact.  The spans are
-    large enough that the long one holds under a quarter of the batch's bytes (past that the
-    engine decodes the whole batch robustly, engine.cpp decode_span_fallback)."""
+    """One long record in one span of a batch of twelve: the batch stays on the fast path
+    (neither decode_span_fallback nor decode_fallback); bit-exact.  The batch is small, so
+    every count-pass chunk is one tile and the record crosses several chunk boundaries."""
     rng = np.random.default_rng(n)
     for pos in range(3):  # the long record at different offsets (tile / chunk phases)
         spans = [synth.config3_epoch(8000, rng)[0].tobytes() for _ in range(12)]
@@ -61,7 +77,7 @@ def test_long_record_span_alone(leng, kind, n):
             dec = leng.decode_host(blob, sp)
             for s_, b in enumerate(spans):
                 assert_span_equal(dec, s_, b)
-        assert not fell_back(leng), (kind, n, pos)
+        assert not went_robust(leng), (kind, n, pos, leng.kernel_stats())
 
 
 def test_config3_batch_with_long_records(leng):
@@ -88,7 +104,68 @@ def test_config3_batch_with_long_records(leng):
         dec = leng.decode_host(blob, sp)
         for s, b in enumerate(spans):
             assert_span_equal(dec, s, b)
-    assert not fell_back(leng)
+    assert not went_robust(leng), leng.kernel_stats()
+
+
+@pytest.mark.parametrize("n_spans,per_span", [(6, 4000), (16, 150000)])
+def test_many_long_records_repaired(leng, n_spans, per_span):
+    """Several long records per span (TimerTrigger names, SourceCheckpoint references and
+    Serializable streams of 9-40 KB), in a small batch (one tile per chunk) and in a 20 MB
+    one (a few tiles per chunk): the count pass repairs the chunks they cross
+    (decode_chunk_repair), nothing goes robust, bit-exact."""
+    rng = np.random.default_rng(per_span)
+    kinds = [("timer", 40000), ("intarray", 9000), ("checkpoint", 20000), ("string", 30000), ("timer", 12000)]
+    spans = []
+    for i in range(n_spans):
+        parts = [synth.config3_epoch(per_span // 4, rng)[0].tobytes()]
+        for j in range(2):
+            kind, n = kinds[(i + 2 * j) % len(kinds)]
+            parts.append(_long(kind, n, i + j))
+            parts.append(synth.config3_epoch(per_span // 4, rng)[0].tobytes())
+        spans.append(b"".join(parts))
+    blob, sp = _join(spans)
+    for _ in range(2):
+        leng.kernel_stats_reset()
+        dec = leng.decode_host(blob, sp)
+        for s, b in enumerate(spans):
+            assert_span_equal(dec, s, b)
+        ks = leng.kernel_stats()
+        assert not went_robust(leng), ks
+    assert "decode_chunk_repair" in ks, ks
+
+
+@pytest.mark.parametrize("bad", [b"\x08", b"\x01\x00\x00"])
+def test_error_after_long_record(leng, bad):
+    """A decode error a few records after a long record, where the count pass's chunk after
+    the record entered at a wrong place: the repair finds the error is real, and the error
+    (status, offset, tag) is the oracle's."""
+    rng = np.random.default_rng(len(bad))
+    buf = (synth.config3_epoch(3000, rng)[0].tobytes() + _long("timer", 40000, 1)
+           + synth.config3_epoch(500, rng)[0].tobytes() + bad + synth.config3_epoch(100, rng)[0].tobytes())
+    st, _, eo, et = O.decode(buf)
+    assert st != 0
+    with pytest.raises(ClonosError) as ex:
+        leng.decode_host(buf)
+    assert ex.value.status == st
+    assert ex.value.err_off == eo and ex.value.err_tag == et
+
+
+def test_sixty_long_records_in_two_spans(leng):
+    """60 long records in two spans, each crossing several one-tile chunks: every chunk they
+    cross is repaired, nothing goes robust, bit-exact."""
+    rng = np.random.default_rng(77)
+    parts = []
+    for i in range(60):
+        parts.append(synth.config3_epoch(200, rng)[0].tobytes())
+        parts.append(_long("timer", 20000, i))
+    spans = [b"".join(parts[:60]), b"".join(parts[60:])]
+    blob, sp = _join(spans)
+    leng.kernel_stats_reset()
+    dec = leng.decode_host(blob, sp)
+    for s, b in enumerate(spans):
+        assert_span_equal(dec, s, b)
+    assert not went_robust(leng), leng.kernel_stats()
+    assert leng.kernel_stats()["decode_chunk_repair"]["launches"] >= 60
 
 
 def _odd_chain(n):
@@ -99,9 +176,10 @@ def _odd_chain(n):
 
 
 def test_span_fallback_only_the_bad_spans(leng):
-    """Two spans the fast path cannot settle among 20 ordinary ones: only those two go
-    through the robust pipeline (decode_span_fallback, not the whole-batch decode_fallback),
-    and every span is bit-exact."""
+    """Two spans the fast path cannot settle among 20 ordinary ones (their chains and the
+    speculative ones never meet, so the chunk repair gives up on them after kZWalkDisagree
+    tiles): only those two go through the robust pipeline (decode_span_fallback, not the
+    whole-batch decode_fallback), and every span is bit-exact."""
     rng = np.random.default_rng(41)  # no Serializable records: the count pass runs without tables
     spans = [synth.config2_log(int(rng.integers(2000, 9000)), rng)[0].tobytes() for _ in range(20)]
     spans[7] = _odd_chain(30000)
@@ -120,7 +198,28 @@ def test_span_fallback_only_the_bad_spans(leng):
             assert_span_equal(dec, s, b)
         assert dec.span_rec_base[-1] == dec.n_rec
         st = leng.kernel_stats()
-        assert "decode_span_fallback" in st and "decode_fallback" not in st
+        assert "decode_span_fallback" in st and "decode_fallback" not in st, st
+
+
+def test_long_odd_chains_past_walk_cap(leng):
+    """Spans of 200 000 channel-0 Order records at odd offsets, beside ordinary spans: every
+    chunk of such a span entered on the even chain, so a repair walk would not meet the old
+    chain before the span's end; past its cap (kZWalkDisagree) those spans go robust.
+    Bit-exact either way."""
+    rng = np.random.default_rng(45)
+    spans = [synth.config2_log(20000, rng)[0].tobytes() for _ in range(12)]
+    for i in (2, 5, 9):
+        spans[i] = _odd_chain(200000)
+    blob, sp = b"", []
+    for i, b in enumerate(spans):
+        if i in (2, 5, 9):
+            blob += bytes(-len(blob) % 16)
+        sp.append((len(blob), len(b)))
+        blob += b
+    leng.kernel_stats_reset()
+    dec = leng.decode_host(blob, sp)
+    for s, b in enumerate(spans):
+        assert_span_equal(dec, s, b)
 
 
 def test_span_fallback_error_equals_robust():
