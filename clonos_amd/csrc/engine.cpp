@@ -749,9 +749,13 @@ struct clg_engine {
     }
     CHK(flush());
     CHK(gwait());  // the scatter below writes segments an in-flight gather may read
-    std::vector<clg::ScatterChunk> ch;
-    ch.reserve(n);
-    size_t total = 0;
+    // the chunks go straight into the pinned descriptor buffer (a config-4 batch has 66 k of
+    // them: a fresh vector per call cost page faults, and a copy)
+    size_t bound = 0;
+    for (uint32_t i = 0; i < n; ++i) bound += r[i].len / C() + 2;
+    CHK(h_desc.ensure(std::max<size_t>(1, bound) * sizeof(clg::ScatterChunk)));
+    clg::ScatterChunk* ch = h_desc.as<clg::ScatterChunk>();
+    size_t nch = 0, total = 0;
     std::unique_lock<std::mutex> pool_guard(pool_mu);  // once for the batch, not per log
     for (uint32_t i = 0; i < n; ++i) {
       r[i].status = CLG_OK;
@@ -773,7 +777,7 @@ struct clg_engine {
       while (left) {
         const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
         const uint32_t take = std::min<uint32_t>(left, C() - so);
-        ch.push_back(clg::ScatterChunk{seg_addr(l->segs[si]) + so, src, take, 0});
+        ch[nch++] = clg::ScatterChunk{seg_addr(l->segs[si]) + so, src, take, 0};
         p += int32_t(take);
         src += take;
         left -= take;
@@ -784,14 +788,12 @@ struct clg_engine {
       total += size_t(num_new);
     }
     pool_guard.unlock();
-    if (ch.empty()) return CLG_OK;
-    const size_t db = ch.size() * sizeof(clg::ScatterChunk);
-    CHK(h_desc.ensure(db));
+    if (!nch) return CLG_OK;
+    const size_t db = nch * sizeof(clg::ScatterChunk);
     CHK(d_desc.ensure(db));
-    memcpy(h_desc.p, ch.data(), db);
     HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, db, hipMemcpyHostToDevice, stream));
     CHK(timed("upstream_scatter", 2 * total, [&] {
-      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(ch.size()), bytes, stream);
+      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream);
     }));
     return sync();  // the caller's buffer and the pinned descriptors are free again
   }
@@ -1059,7 +1061,18 @@ struct clg_engine {
     uint32_t n_tiny = 0;                // whole spans of one tile and at most kZTinySpan bytes
     uint32_t unit = 0;                  // device-planning tile window
     int64_t only = -1;                  // >= 0: plan only this span of the batch (as span 0)
+    void reset() {  // empty, capacity kept (a config-4 plan is ~4 MB: fresh pages cost page faults)
+      tiles.clear();
+      spans.clear();
+      runs.clear();
+      segtab.clear();
+      n_tiles = n_tiny = unit = 0;
+      only = -1;
+    }
   };
+  // clg_decode_logs' plan and log ranges, kept between calls for their capacity
+  DecodePlan zplan;
+  std::vector<int32_t> zst, znb;
   // Span filter of a plan (the per-span fallback re-decodes single spans): false = skip.
   static bool plan_keep(const DecodePlan& p, uint32_t* s) {
     if (p.only < 0) return true;
@@ -2444,11 +2457,15 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   ENGINE_GUARD(e);
   if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
   CHK(e->flush());
-  std::vector<int32_t> st(n), nb(n);
+  std::vector<int32_t>& st = e->zst;
+  std::vector<int32_t>& nb = e->znb;
+  st.assign(n, 0);
+  nb.assign(n, 0);
   uint64_t total = 0;
   // the ranges and the fast decode's plan in one pass over the logs (per-log work of a
   // 66 k-log batch is bound by the cache misses on the log records)
-  clg_engine::DecodePlan pf;
+  clg_engine::DecodePlan& pf = e->zplan;
+  pf.reset();
   if (e->fused_decode) {
     pf.spans.reserve(n);
     pf.runs.reserve(n);
