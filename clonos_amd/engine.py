@@ -336,7 +336,7 @@ class Engine:
                     keep_bytes: bool = False) -> DecodedBatch:
         h = np.array([l.handle for l in logs], np.uint32)
         ep = np.array(start_epochs, np.int64)
-        total = sum(l.state()["writer"] for l in logs)
+        total = self.log_lengths(h)[1]  # logLength bounds every span (one native call for the batch)
         cap = total // 2 + len(logs) + 1
         wcap = total // 6 + len(logs) + 1
         d, arrs = self._host_outputs(cap, wcap)
@@ -349,7 +349,7 @@ class Engine:
         """clg_decode_logs_async into host arrays: returns at once; .wait() gives the batch."""
         h = np.array([l.handle for l in logs], np.uint32)
         ep = np.array(start_epochs, np.int64)
-        total = sum(l.state()["writer"] for l in logs)
+        total = self.log_lengths(h)[1]
         d, arrs = self._host_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
         base = np.zeros(len(logs) + 1, np.uint64)
         pd = PendingDecode(self, (h, ep, d, arrs, base), len(logs))
