@@ -295,14 +295,14 @@ def main():
     ifl = None
     if rank == 0 and world == 1 and not args.no_inflight:
         ifl = inflight_replay(args, torch, dev)
+    c1 = None
+    if rank == 0 and world == 1 and not args.no_config1:  # (before config 4 starts RCCL's threads)
+        c1 = config1(args, torch)
     c4 = c5 = None
     if not args.no_config4:  # every rank: the exchange is a collective
         if world == 1:
             eng.close()
         c4, c5 = config4(args, torch, dev, rank, world, dist, rehearse)
-    c1 = None
-    if rank == 0 and world == 1 and not args.no_config1:
-        c1 = config1(args, torch)
 
     if rank == 0:
         line = {
@@ -831,7 +831,9 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
             e_.close()
     # the robust pipeline alone (the fallback's throughput) and the long-record batch
     rob_ms, _, rob_k = timed_decode("clean", "robust", n_det)
-    long_ms, long_paths, _ = timed_decode("long", "auto", n_det + 2)
+    # the long-record batch against the clean one through the same harness (a fresh engine each)
+    clean_ms, _, clean_k = timed_decode("clean", "auto", n_det)
+    long_ms, long_paths, long_k = timed_decode("long", "auto", n_det + 2)
     out = {"workload": f"config3: {n_logs} subtask logs x {n_epochs} epochs x {per_epoch} mixed determinants "
                        "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
@@ -842,7 +844,11 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
                                "log_gbs": round(total / rob_ms / 1e6, 2), "kernels_ms": rob_k},
            "long_records": {"note": "the same batch with a 40 KB TimerTrigger name (log 37) and a 9 KB "
                                     "Serializable int[] stream (log 181) inserted at record boundaries",
-                            "ms_per_step": round(long_ms, 4), "vs_clean": round(long_ms / (el * 1e3), 4),
+                            "ms_per_step": round(long_ms, 4), "clean_ms_per_step": round(clean_ms, 4),
+                            "vs_clean": round(long_ms / clean_ms, 4),
+                            "pipeline_ms": long_k.get("decode_pipeline"), "clean_pipeline_ms": clean_k.get("decode_pipeline"),
+                            "pipeline_vs_clean": round(long_k["decode_pipeline"] / clean_k["decode_pipeline"], 4)
+                            if long_k.get("decode_pipeline") and clean_k.get("decode_pipeline") else None,
                             "fallbacks": long_paths}}
     if not args.no_cpu_baseline:  # the C++ oracle's decodeNext loop on host cores, whole workload once
         sys.path.insert(0, os.path.join(ROOT, "tests"))

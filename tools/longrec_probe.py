@@ -16,7 +16,8 @@ from clonos_amd import CausalLogID, Engine, _lib, synth  # noqa: E402
 from clonos_amd import determinants as D  # noqa: E402
 
 os.environ["CLONOS_FUSED_DEBUG"] = "1"
-N_LOGS, N_EP, PER = 64, 4, 40000
+FULL = os.environ.get("LONGREC_FULL") == "1"  # config 3's full shape (256 logs x 10 epochs)
+N_LOGS, N_EP, PER = (256, 10, 40000) if FULL else (64, 4, 40000)
 rng = np.random.default_rng(synth.SEED_CONFIG3)
 gen = [synth.config3_epoch(PER, rng, e) for e in range(N_EP)]
 epochs = [g[0] for g in gen]
@@ -63,13 +64,20 @@ def case(name, rec, log=37, ep=2, frac=0.5):
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / 3 * 1e3
         ks = eng.kernel_stats()
-        paths = sorted(k for k in ks if k in ("decode_fallback", "decode_span_fallback"))
+        paths = sorted(k for k in ks if k in ("decode_fallback", "decode_span_fallback", "decode_chunk_repair"))
+        kms = {k: round(v["ms"] / v["launches"], 4) for k, v in ks.items() if v["launches"] and v["ms"] > 0}
         print(json.dumps({"case": name, "rec_bytes": len(rec) if rec else 0, "ok": bool(ok), "ms": round(ms, 3),
-                          "paths": paths}), flush=True)
+                          "paths": paths, "kernels": kms}), flush=True)
     finally:
         eng.close()
 
 
+if FULL:
+    case("clean", None)
+    case("timer_40000", D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * 40000)), log=37, ep=4)
+    case("jser_intarr_2250", D.encode(D.SerializableDeterminant(D.jser_int_array(list(range(2250))))), log=181, ep=7)
+    case("clean", None)
+    sys.exit(0)
 case("clean", None)
 for n in (300, 2000, 7000, 9000, 40000):
     case(f"timer_{n}", D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * n)))
