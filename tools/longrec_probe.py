@@ -72,7 +72,52 @@ def case(name, rec, log=37, ep=2, frac=0.5):
         eng.close()
 
 
+def bench_layout(variant):
+    """bench.py config3's build_engine: every log's epochs rotated; its long-record variant."""
+    seg = 16384
+    long_tt = D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * 40000))
+    long_js = D.encode(D.SerializableDeterminant(D.jser_int_array(list(range(2250)))))
+
+    def with_long(e, rec):
+        k = int(gen[e][1][len(gen[e][1]) // 2])
+        return np.concatenate([epochs[e][:k], np.frombuffer(rec, np.uint8), epochs[e][k:]])
+    special = {(37, 4): with_long(4, long_tt), (181, 7): with_long(7, long_js)} if variant != "clean" else {}
+    if variant == "timer":
+        special.pop((181, 7))
+    if variant == "jser":
+        special.pop((37, 4))
+    per_log = sum(int(e.size) for e in epochs)
+    eng = Engine(segment_bytes=seg, pool_segments=N_LOGS * ((per_log + seg - 1) // seg + N_EP + 1) + 64, timing=True,
+                 ifl_pool_segments=16)
+    try:
+        hs = []
+        for v in range(N_LOGS):
+            l = eng.open_log(CausalLogID.main(v))
+            for e in range(N_EP):
+                b = special.get((v, (e + v) % N_EP))
+                l.processUpstreamDelta((b if b is not None else epochs[(e + v) % N_EP]).tobytes(), 0, e)
+            hs.append(l.handle)
+        eng.sync()
+        hs = np.array(hs, np.uint32)
+        starts = np.zeros(N_LOGS, np.int64)
+        base = np.zeros(N_LOGS + 1, np.uint64)
+        eng.decode_logs_device(hs, starts, dec, base)
+        torch.cuda.synchronize()
+        eng.kernel_stats_reset()
+        for _ in range(3):
+            eng.decode_logs_device(hs, starts, dec, base)
+        torch.cuda.synchronize()
+        ks = eng.kernel_stats()
+        print(json.dumps({"layout": variant, "n_rec": int(dec.n_rec),
+                          "stats": {k: (round(v["ms"] / v["launches"], 4) if v["ms"] else v["launches"])
+                                    for k, v in ks.items() if v["launches"]}}), flush=True)
+    finally:
+        eng.close()
+
+
 if FULL:
+    for v in ("clean", "both", "timer", "jser", "clean"):
+        bench_layout(v)
     case("clean", None)
     case("timer_40000", D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * 40000)), log=37, ep=4)
     case("jser_intarr_2250", D.encode(D.SerializableDeterminant(D.jser_int_array(list(range(2250))))), log=181, ep=7)
