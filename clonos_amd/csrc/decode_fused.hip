@@ -1636,7 +1636,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         else mark_bad(ctl, why, t, z.td.span);
       }
       if (!soft && !ctl.span_bad) return;
-      bad_span = z.td.span;  // the next span starts on a record boundary: go on there
+      if (soft)  // go on from the next tile's first byte (a guess; the repair checks it), so that
+        x_prev = z.td.span_off + z.td.len;  // the chunk's later tiles have exits to resync with
+      else
+        bad_span = z.td.span;  // the next span starts on a record boundary: go on there
     }
     __syncthreads();  // the image is reused by the next tile
   }
