@@ -1963,7 +1963,9 @@ uint32_t decode_count_grid(bool jser, uint32_t n_tiles) {
     if (hipGetDevice(&dev) != hipSuccess || oe != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
       return 0;
-    resident[j] = (per_cu > 1 ? per_cu - 1 : 1) * cus;  // one block per CU of margin
+    const char* m = getenv("CLONOS_COUNT_MARGIN");  // developer switch: blocks per CU left free (default 1)
+    const int margin = m ? atoi(m) : 1;
+    resident[j] = (per_cu > margin ? per_cu - margin : 1) * cus;
   }
   return n_tiles < (uint32_t)resident[j] ? n_tiles : (uint32_t)resident[j];
 }
