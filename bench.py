@@ -359,12 +359,11 @@ def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, su
       1. the new epoch of every owned log lands in HBM (batched device-input append);
       2. batched decode of that epoch of every owned log (SoA in HBM);
       3. replication (dist.Replicator.exchange): batched slice of the new bytes of every
-         owned log another rank wants -> all-gather over RCCL -> batched device-input
-         processUpstreamDelta into the replicas;
+         owned log for every rank that wants it -> all-to-alls over RCCL (counts, header
+         rows, payload) -> batched device-input processUpstreamDelta into the replicas;
       4. checkpoint completion of the previous epoch (job CAS + truncation of owned logs and
          replicas).
-    At N=1 every log is local: the replication moves nothing (its collective still runs on a
-    one-rank group).  Timing: K steps between barriers + device syncs, max over ranks."""
+    At N=1 every log is local: the replication has nothing to move and runs no collective.  Timing: K steps between barriers + device syncs, max over ranks."""
     import time as _t
     from clonos_amd import Engine, _lib, job as J, synth, dist as X
     own_group = None
@@ -410,7 +409,9 @@ def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, su
     dec.cap, dec.wcap, dec.out_kind = max(n_rec, 1), 16, _lib.CLG_MEM_DEVICE
     base = np.zeros(len(gids) + 1, np.uint64)
     bytes_owned = int(host.size)
-    payload_cap = int(per_log[np.isin(gids, plan.send)].sum()) + 64
+    # every request slices at most one epoch of its log (the bench appends one per step)
+    len_of = dict(zip(gids.tolist(), per_log.tolist()))
+    payload_cap = int(sum(len_of[int(x)] for x in plan.req_gid)) + 64
     phase = {"append": 0.0, "decode": 0.0, "exchange": 0.0, "truncate": 0.0}
     ex_tot = X.ExchangeStats()
 
@@ -470,7 +471,7 @@ def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, su
     return ({"workload": "config4: 5-stage DAG, p=128, full sharing (640 VertexIDs, 66176 logs: 1 main + 128 "
                         f"subpartition logs per producing vertex); per epoch {main_records} Order/Timestamp per main "
                         f"log, {sub_records} BufferBuilt per subpartition log; step = append + decode of owned logs "
-                        "+ replication exchange (slice -> all-gather -> processUpstreamDelta) + truncation",
+                        "+ replication exchange (slice -> all-to-all -> processUpstreamDelta) + truncation",
             "n_gpus": world, "steps": K, "ms_per_step": round(ms, 4),
             "determinants_per_s": round(tot_rec / (el / K), 1), "log_gbs": round(tot_bytes / (el / K) / 1e9, 2),
             "logs_per_rank": {"owned": len(gids), "sent": int(len(plan.send)), "replicas": int(len(plan.wanted))},

@@ -39,6 +39,11 @@ CLG_F_TIMING = 1
 CLG_F_ROBUST_DECODE = 2
 CLG_F_ASYNC_SLICE = 4
 CLG_FULL_SHARING = -1
+CLG_IFL_IN_MEMORY = 0
+CLG_IFL_SPILLABLE = 1
+CLG_IFL_CONTINUE = 1        # IflReplayReq.flags
+CLG_IFL_NULL_ITERATOR = 1   # IflReplayRes.flags
+CLG_IFL_REPLAYING = 2       # IflReplayRes.flags
 
 EXPORTED = [
     "clg_config_default", "clg_engine_create", "clg_engine_destroy", "clg_last_error", "clg_abi_version",
@@ -51,7 +56,7 @@ EXPORTED = [
     "clg_replay_prep", "clg_kernel_stats", "clg_kernel_stats_reset",
     "clg_response_put", "clg_response_write", "clg_response_read", "clg_response_merge", "clg_causal_log_id_hash",
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
-    "clg_ifl_open", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
+    "clg_ifl_open", "clg_ifl_open_typed", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
     "clg_ifl_replay_batch", "clg_replay_prepare_device", "clg_get_determinants_batch", "clg_response_put_batch",
 ]
 
@@ -208,12 +213,13 @@ CLG_DE_SEND = 1
 
 
 class IflReplayReq(C.Structure):
-    _fields_ = [("ifl", C.c_uint32), ("ignore_buffers", C.c_uint32), ("start_epoch", C.c_int64)]
+    _fields_ = [("ifl", C.c_uint32), ("ignore_buffers", C.c_uint32), ("start_epoch", C.c_int64),
+                ("max_buffers", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class IflReplayRes(C.Structure):
     _fields_ = [
-        ("status", C.c_int32), ("n_buffers", C.c_uint32), ("remaining", C.c_uint32), ("reserved", C.c_uint32),
+        ("status", C.c_int32), ("n_buffers", C.c_uint32), ("remaining", C.c_uint32), ("flags", C.c_uint32),
         ("out_off", C.c_uint64), ("len", C.c_uint64), ("sizes_off", C.c_uint64), ("end_epoch", C.c_int64),
     ]
 
@@ -298,6 +304,7 @@ def _load() -> C.CDLL:
         "clg_process_delta": (C.c_int, [P, C.c_uint32, C.c_uint32, P, C.c_uint64, C.c_uint32, i64p, P, C.c_uint32, u32p,
                                         u64p]),
         "clg_ifl_open": (C.c_int, [P, u32p]),
+        "clg_ifl_open_typed": (C.c_int, [P, C.c_uint32, u32p]),
         "clg_ifl_close": (C.c_int, [P, C.c_uint32]),
         "clg_ifl_log_batch": (C.c_int, [P, P, P, P, P, C.c_uint32, P, C.c_uint32]),
         "clg_ifl_notify_checkpoint_complete": (C.c_int, [P, C.c_uint32, C.c_int64]),

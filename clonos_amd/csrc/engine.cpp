@@ -276,8 +276,24 @@ struct IflBuf {
   std::vector<uint32_t> segs;
   uint32_t len;
 };
+// The spillable logger's replay iterator (SpilledReplayIterator.java:60-401): a consumer and a
+// prefetch EpochCursor (:306-394) over the live view tailMap(view) of the epochs.
+struct IflCursor {
+  int64_t ne = 0;    // nextEpoch
+  int64_t off = 0;   // nextEpochOffset
+  int64_t last = 0;  // lastEpoch
+  int64_t rem = 0;   // remaining
+};
+struct IflIter {
+  bool exists = false;  // currentIterator != null
+  int64_t view = 0;     // the tailMap's lower bound (getInFlightIterator's epochID)
+  IflCursor con, pre;
+};
 struct InFlight {
   bool open = false;
+  uint32_t type = CLG_IFL_IN_MEMORY;
+  bool replaying = false;  // spillable: isReplaying (:58)
+  IflIter it;              // spillable: currentIterator (:60)
   std::map<int64_t, std::vector<IflBuf>> epochs;
 };
 
@@ -3065,18 +3081,19 @@ static void ifl_release(clg_engine* e, std::vector<IflBuf>& bufs) {  // Buffer.r
   bufs.clear();
 }
 
-int clg_ifl_open(clg_engine* e, uint32_t* handle) {
+int clg_ifl_open(clg_engine* e, uint32_t* handle) { return clg_ifl_open_typed(e, CLG_IFL_IN_MEMORY, handle); }
+
+int clg_ifl_open_typed(clg_engine* e, uint32_t type, uint32_t* handle) {
   ENGINE_GUARD(e);
   if (!handle) return fail(CLG_E_INVALID_ARG, "null argument");
-  for (uint32_t i = 0; i < e->ifls.size(); ++i)
-    if (!e->ifls[i].open) {
-      e->ifls[i].open = true;
-      *handle = i;
-      return CLG_OK;
-    }
-  e->ifls.emplace_back();
-  e->ifls.back().open = true;
-  *handle = uint32_t(e->ifls.size() - 1);
+  if (type != CLG_IFL_IN_MEMORY && type != CLG_IFL_SPILLABLE) return fail(CLG_E_INVALID_ARG, "bad in-flight log type %u", type);
+  uint32_t i = 0;
+  while (i < e->ifls.size() && e->ifls[i].open) ++i;
+  if (i == e->ifls.size()) e->ifls.emplace_back();
+  e->ifls[i] = InFlight{};
+  e->ifls[i].open = true;
+  e->ifls[i].type = type;
+  *handle = i;
   return CLG_OK;
 }
 
@@ -3119,6 +3136,7 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
     dsrc = e->d_stage.as<uint8_t>();
   }
   uint64_t packed = 0;
+  uint32_t npe = 0;  // 1 + the first buffer whose spillable log() throws after appending
   for (uint32_t i = 0; i < n; ++i) {
     IflBuf b{{}, len[i]};
     const uint64_t src = in_kind == CLG_MEM_HOST ? packed : off[i];
@@ -3130,9 +3148,22 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
       ch.push_back(clg::ScatterChunk{e->ifl_addr(s), src + o, std::min(C, len[i] - o), 0});
     }
     packed += len[i];
-    e->ifls[ifl[i]].epochs[epoch[i]].push_back(std::move(b));
+    InFlight& f = e->ifls[ifl[i]];
+    f.epochs[epoch[i]].push_back(std::move(b));
+    if (f.type == CLG_IFL_SPILLABLE && f.replaying) {  // :98-99
+      if (!f.it.exists) {
+        npe = npe ? npe : i + 1;  // currentIterator is null: notifyNewBufferAdded throws
+      } else {                    // SpilledReplayIterator.notifyNewBufferAdded :262-277
+        for (IflCursor* c : {&f.it.pre, &f.it.con}) {
+          ++c->rem;
+          c->last = std::max(c->last, epoch[i]);
+        }
+      }
+    }
   }
-  if (ch.empty()) return CLG_OK;
+  if (ch.empty())
+    return npe ? fail(CLG_E_STATE, "log() of buffer %u while replaying without an iterator (NullPointerException)", npe - 1)
+               : CLG_OK;
   const size_t db = ch.size() * sizeof(clg::ScatterChunk);
   CHK(e->h_desc.ensure(db));
   CHK(e->d_desc.ensure(db));
@@ -3144,6 +3175,7 @@ int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, 
     return clg::launch_scatter(e->d_desc.as<clg::ScatterChunk>(), uint32_t(ch.size()), dsrc, e->stream);
   }));
   HIPCHK(hipStreamSynchronize(e->stream));  // staging buffers are reused; device input is the caller's
+  if (npe) return fail(CLG_E_STATE, "log() of buffer %u while replaying without an iterator (NullPointerException)", npe - 1);
   return CLG_OK;
 }
 
@@ -3174,10 +3206,53 @@ int clg_ifl_state(clg_engine* e, uint32_t h, int64_t* ids, uint32_t* nb, uint32_
   return CLG_OK;
 }
 
-// getInFlightIterator(start, ignore) :73-82 and a full drain of the ReplayIterator
-// (:114-167).  The iterator walks tailMap(start) by ++currentKey, so it only yields
-// contiguous epochs from `start`; a missing key throws inside next() right after the last
-// buffer before it was taken (:156 -> :133), so that buffer is lost to the caller.
+// ---- the spillable logger's iterator (SpilledReplayIterator.java), on host metadata ---------
+// Every EpochCursor step that reads the map through the live view tailMap(view) fails (returns
+// false) where the Java code throws: an epoch missing from the view (NullPointerException) or an
+// offset past its buffers (IndexOutOfBoundsException).
+static bool ifl_size(const InFlight& f, int64_t view, int64_t ep, int64_t* n) {  // log.get(ep).getEpochSize()
+  if (ep < view) return false;
+  const auto it = f.epochs.find(ep);
+  if (it == f.epochs.end()) return false;
+  *n = int64_t(it->second.size());
+  return true;
+}
+static bool ifl_advance(const InFlight& f, int64_t view, IflCursor& c) {  // advanceEpochIfNeeded :353-358
+  int64_t n;
+  if (!ifl_size(f, view, c.ne, &n)) return false;
+  if (c.off == n && c.ne != c.last) {
+    ++c.ne;
+    c.off = 0;
+  }
+  return true;
+}
+static bool ifl_cnext(const InFlight& f, int64_t view, IflCursor& c, const IflBuf** out) {  // next() :342-351
+  if (!ifl_advance(f, view, c)) return false;
+  const auto it = c.ne >= view ? f.epochs.find(c.ne) : f.epochs.end();
+  if (it == f.epochs.end() || c.off < 0 || c.off >= int64_t(it->second.size())) return false;
+  if (out) *out = &it->second[size_t(c.off)];
+  ++c.off;
+  --c.rem;
+  return ifl_advance(f, view, c);
+}
+static bool ifl_behind(const InFlight& f, int64_t view, IflCursor& a, IflCursor& b, bool* res) {  // behind() :364-367
+  if (!ifl_advance(f, view, a) || !ifl_advance(f, view, b)) return false;
+  *res = a.ne < b.ne || (a.ne == b.ne && a.off < b.off);
+  return true;
+}
+static void ifl_prefetch(const InFlight& f, IflIter& it) {  // prefetchNextBuffers :126-158 (exceptions swallowed)
+  while (it.pre.rem > 0)
+    if (!ifl_advance(f, it.view, it.pre) || !ifl_cnext(f, it.view, it.pre, nullptr)) return;
+}
+
+// getInFlightIterator(start, ignore) and the drain of its iterator, per logger type:
+//   in-memory (:73-82, ReplayIterator :114-167): walks tailMap(start) by ++currentKey, so it only
+//     yields contiguous epochs from `start`; a missing key throws inside next() right after the
+//     last buffer before it was taken (:156 -> :133), so that buffer is lost to the caller;
+//   spillable (:126-142, SpilledReplayIterator): the iterator is the logger's current one, its
+//     cursors stepped literally (above); max_buffers / CLG_IFL_CONTINUE drain it in parts.
+// Iterator state is worked on in copies and committed only when the gather runs, so a sizing
+// call (CLG_E_CAPACITY) changes nothing.
 int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t n, clg_ifl_replay_res* res,
                          void* out, uint64_t cap, uint32_t out_kind, uint32_t* sizes, int64_t* epochs,
                          uint64_t sizes_cap, uint64_t* total, uint64_t* total_buffers) {
@@ -3188,8 +3263,24 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
     const IflBuf* b;
     uint64_t dst;
   };
+  struct Work {  // a spillable logger's iterator state during this call
+    IflIter it;
+    bool replaying;
+  };
+  std::map<uint32_t, Work> work;
   std::vector<Pick> picks;
   uint64_t dst = 0, nbuf = 0;
+  auto take = [&](clg_ifl_replay_res& r, const IflBuf& b, int64_t ep) {
+    picks.push_back(Pick{&b, dst});
+    if (nbuf < sizes_cap) {
+      if (sizes) sizes[nbuf] = b.len;
+      if (epochs) epochs[nbuf] = ep;  // getEpoch() before this next()
+    }
+    dst += b.len;
+    r.len += b.len;
+    ++nbuf;
+    ++r.n_buffers;
+  };
   for (uint32_t i = 0; i < n; ++i) {
     clg_ifl_replay_res& r = res[i];
     const int64_t start = reqs[i].start_epoch;
@@ -3201,6 +3292,81 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
       continue;
     }
     const uint64_t ign = reqs[i].ignore_buffers;
+    if (f->type == CLG_IFL_SPILLABLE) {
+      auto wi = work.find(reqs[i].ifl);
+      if (wi == work.end()) wi = work.emplace(reqs[i].ifl, Work{f->it, f->replaying}).first;
+      Work& w = wi->second;
+      if (!(reqs[i].flags & CLG_IFL_CONTINUE)) {  // getInFlightIterator :126-142
+        w.replaying = true;
+        const auto first = f->epochs.lower_bound(start);
+        if (first == f->epochs.end()) {  // tailMap empty: null (the current iterator stays)
+          r.flags = CLG_IFL_NULL_ITERATOR | CLG_IFL_REPLAYING;
+          continue;
+        }
+        IflIter it;
+        it.exists = true;
+        it.view = start;
+        it.con.ne = first->first;
+        it.con.last = f->epochs.rbegin()->first;
+        for (auto jt = first; jt != f->epochs.end(); ++jt) it.con.rem += int64_t(jt->second.size());
+        it.pre = it.con;
+        bool ok = true;
+        for (uint64_t k = 0; k < ign && ok; ++k)  // the constructor's skip :98-101
+          ok = ifl_cnext(*f, it.view, it.con, nullptr) && ifl_cnext(*f, it.view, it.pre, nullptr);
+        if (!ok) {  // the constructor throws: no new iterator, isReplaying stays set
+          r.status = fail(CLG_E_STATE, "skip of %llu buffers fails inside the iterator's constructor",
+                          (unsigned long long)ign);
+          r.flags = CLG_IFL_REPLAYING;
+          continue;
+        }
+        ifl_prefetch(*f, it);  // :123
+        w.it = it;
+      } else if (!w.it.exists) {
+        r.status = fail(CLG_E_STATE, "no current in-flight iterator to continue");
+        r.flags = w.replaying ? CLG_IFL_REPLAYING : 0u;
+        continue;
+      }
+      IflIter& it = w.it;
+      r.remaining = uint32_t(std::max<int64_t>(it.con.rem, 0));
+      const uint32_t cap_n = reqs[i].max_buffers;
+      bool thrown = false;
+      while (it.con.rem > 0 && (cap_n == 0 || r.n_buffers < cap_n)) {  // next() :171-203
+        bool bh;
+        if (!ifl_behind(*f, it.view, it.con, it.pre, &bh)) {
+          thrown = true;
+          break;
+        }
+        if (!bh) {
+          ifl_prefetch(*f, it);
+          if (!ifl_behind(*f, it.view, it.con, it.pre, &bh) || !bh) {  // (not behind: it would wait forever)
+            thrown = true;
+            break;
+          }
+        }
+        const IflBuf* b = nullptr;
+        if (!ifl_advance(*f, it.view, it.con)) {  // getEpoch() :166-168
+          thrown = true;
+          break;
+        }
+        const int64_t ep = it.con.ne;
+        if (!ifl_cnext(*f, it.view, it.con, &b)) {
+          thrown = true;
+          break;
+        }
+        if (it.con.rem <= 0) w.replaying = false;  // :186-193
+        ifl_prefetch(*f, it);
+        take(r, *b, ep);
+      }
+      if (thrown) r.status = CLG_E_EPOCH_GAP;
+      IflCursor c = it.con;
+      r.end_epoch = ifl_advance(*f, it.view, c) ? c.ne : it.con.ne;
+      r.flags = w.replaying ? CLG_IFL_REPLAYING : 0u;
+      continue;
+    }
+    if (reqs[i].max_buffers || reqs[i].flags) {
+      r.status = fail(CLG_E_INVALID_ARG, "max_buffers / CLG_IFL_CONTINUE need a spillable in-flight log");
+      continue;
+    }
     auto it = f->epochs.find(start);
     if (it == f->epochs.end()) {  // :121-127 -- currentIterator == null, nothing left, currentKey = start
       if (ign) r.status = fail(CLG_E_STATE, "skip of %llu buffers on an empty iterator", (unsigned long long)ign);
@@ -3236,15 +3402,7 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
       for (const IflBuf& b : jt->second) {
         if (idx >= deliver) break;
         if (idx++ < ign) continue;
-        picks.push_back(Pick{&b, dst});
-        if (nbuf < sizes_cap) {
-          if (sizes) sizes[nbuf] = b.len;
-          if (epochs) epochs[nbuf] = jt->first;  // getEpoch() before this next()
-        }
-        dst += b.len;
-        r.len += b.len;
-        ++nbuf;
-        ++r.n_buffers;
+        take(r, b, jt->first);
       }
   }
   if (total) *total = dst;
@@ -3253,6 +3411,10 @@ int clg_ifl_replay_batch(clg_engine* e, const clg_ifl_replay_req* reqs, uint32_t
     return fail(CLG_E_CAPACITY, "in-flight replay needs %llu bytes / %llu sizes (cap %llu / %llu)",
                 (unsigned long long)dst, (unsigned long long)nbuf, (unsigned long long)cap,
                 (unsigned long long)sizes_cap);
+  for (auto& kv : work) {  // commit the spillable iterators
+    e->ifls[kv.first].it = kv.second.it;
+    e->ifls[kv.first].replaying = kv.second.replaying;
+  }
   std::vector<clg::GatherPiece> pieces;
   const uint32_t C = e->ifl_C;
   for (const Pick& p : picks)

@@ -10,13 +10,15 @@ depth (job.replication_masks).  Every rank builds the same canonical log table
 per-log step is a numpy gather over dense tables -- no per-log Python.  One exchange (per
 epoch, or per batch of buffers):
 
-  1. the owner slices the new bytes of every owned log that some other rank wants, for one
-     replication consumer per log: the engine's batched hasDelta/getOffset/getDelta
-     (clg_slice_batch), ONE device gather into the payload part of the send blob;
-  2. send blob = [header rows | payload]; one all-gather of the (header, payload) sizes,
-     one all-gather of the blobs padded to the largest (RCCL over xGMI with the "nccl"
-     backend; gloo on CPU), then ONE device->host copy of every rank's header region;
-  3. every rank applies the rows of the logs it wants with the batched processUpstreamDelta
+  1. the owner slices the new bytes of every owned log for every other rank that wants it
+     (each receiving rank is one consumer of the log, with its own offset): the engine's
+     batched hasDelta/getOffset/getDelta (clg_slice_batch), ONE device gather into a
+     payload buffer grouped by destination;
+  2. three all-to-alls with per-destination split sizes (RCCL over xGMI with the "nccl"
+     backend; gloo on CPU): the (rows, bytes) counts of every rank pair, the header rows,
+     the payload.  A rank receives only the logs within its sharing depth (at depth 1 only
+     its direct producers'), and with one rank no collective runs;
+  3. every rank applies the received rows with the batched processUpstreamDelta
      (clg_upstream_delta_batch) reading straight from the receive buffer in HBM.  The dedup
      rule of ThreadCausalLogImpl.java:117-154 makes re-delivery harmless.
 
@@ -46,12 +48,12 @@ from .engine import CausalLogID, Engine, ThreadCausalLog
 from .job import JobGraph, LogTable, owner_rank, replication_masks
 
 # One header row per delta (little-endian, 32 bytes): global log index, epoch,
-# offsetFromEpoch, length, payload offset inside the sender's payload.
+# offsetFromEpoch, length, payload offset inside the sender's payload for this receiver.
 HEADER = np.dtype([("gid", "<i4"), ("offset_from_epoch", "<i4"), ("epoch", "<i8"), ("len", "<u4"),
                    ("pad", "<u4"), ("payload_off", "<u8")])
 assert HEADER.itemsize == 32
 BLOB_ALIGN = 64
-REPLICATION_CHANNEL = (0xC1055EED00000000, 0x5EED)  # the replication consumer of every log
+REPLICATION_CHANNEL = (0xC1055EED00000000, 0x5EED)  # replication consumer; destination rank in ch_hi bits 16+
 
 # numpy views of the C request / result structs (include/clonos_engine.h)
 SLICE_REQ = np.dtype([("log", "<u4"), ("reserved", "<u4"), ("ch_lo", "<u8"), ("ch_hi", "<u8"), ("epoch", "<i8")])
@@ -67,48 +69,17 @@ def _align(n: int) -> int:
     return (n + BLOB_ALIGN - 1) // BLOB_ALIGN * BLOB_ALIGN
 
 
-def header_bytes(n_rows: int) -> int:
-    return _align(n_rows * HEADER.itemsize)
-
-
 # ---- collectives ------------------------------------------------------------------------
 def _to_comm(t, backend: str):
     """gloo moves host tensors; RCCL ("nccl") moves device tensors in place."""
     return t if (backend == "nccl" or not t.is_cuda) else t.cpu()
 
 
-def allgather_sizes(vals: Sequence[int], device, group=None) -> np.ndarray:
-    """int64[world, len(vals)]: every rank's `vals` (one tiny collective + one D2H)."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-    backend = dist.get_backend(group)
-    dev = device if backend == "nccl" else "cpu"
-    mine = torch.tensor(list(vals), dtype=torch.int64, device=dev)
-    out = torch.empty(world * len(vals), dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(out, mine, group=group)
-    return out.cpu().numpy().reshape(world, len(vals))
-
-
-def allgather_blobs(send, stride: int, group=None):
-    """All-gather one uint8 blob per rank, each padded to `stride`: rank r's blob starts
-    at recv[r * stride]."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-    backend = dist.get_backend(group)
-    src = _to_comm(send, backend)
-    padded = src if src.numel() == stride else torch.nn.functional.pad(src, (0, stride - src.numel()))
-    recv = torch.empty(world * stride, dtype=torch.uint8, device=padded.device)
-    dist.all_gather_into_tensor(recv, padded, group=group)
-    return recv if (recv.is_cuda or not send.is_cuda) else recv.to(send.device)
-
-
 # ---- replication ------------------------------------------------------------------------
 @dataclass
 class ExchangeStats:
-    sent_bytes: int = 0     # this rank's blob (header + payload)
-    recv_bytes: int = 0     # other ranks' blobs (header + payload)
+    sent_bytes: int = 0     # header rows + payload this rank sent
+    recv_bytes: int = 0     # header rows + payload this rank received
     applied: int = 0        # deltas applied to replicas
     applied_bytes: int = 0  # delta bytes those deltas carried
     skipped: int = 0        # rows for logs this rank does not want
@@ -116,8 +87,13 @@ class ExchangeStats:
 
 class ReplicationPlan:
     """The static part of sharing-depth replication for one rank: which owned logs it
-    sends, which logs it keeps replicas of, and the dense handle tables.  Built once per
-    job and rank (registerTask time), identically on every rank."""
+    sends to which rank, which logs it keeps replicas of, and the dense handle tables.
+    Built once per job and rank (registerTask time), identically on every rank.
+
+    Each receiving rank is one downstream consumer of every log it wants (its own consumer
+    offset per log, as each output channel is in FlatDeltaSerializerDeserializer.java:57-90),
+    so a rank receives exactly the logs within its sharing depth and nothing else: the
+    requests (req_gid, req_dest) are grouped by destination rank."""
 
     def __init__(self, table: LogTable, depth: int, rank: int, world: int,
                  need: Optional[np.ndarray] = None):
@@ -130,6 +106,11 @@ class ReplicationPlan:
         wanted_anywhere = need.any(axis=0)
         self.send = self.owned[wanted_anywhere[lv[self.owned]]]  # owned gids some rank wants
         self.wanted = np.nonzero(need[rank][lv])[0]               # gids this rank keeps replicas of
+        # one slice request per (sent log, destination rank that wants it), by destination
+        per_dest = [self.owned[need[r][lv[self.owned]]] if r != rank else self.owned[:0] for r in range(world)]
+        self.req_gid = np.concatenate(per_dest).astype(np.int64) if world else np.zeros(0, np.int64)
+        self.req_dest = np.repeat(np.arange(world, dtype=np.int64), [len(p) for p in per_dest])
+        self.n_to = np.array([len(p) for p in per_dest], np.int64)  # requests per destination
 
 
 class EngineIO:
@@ -149,8 +130,10 @@ class EngineIO:
         total = C.c_uint64()
         check(lib.clg_slice_batch(self.engine.handle, sreq.ctypes.data, n, sres.ctypes.data, out_ptr, cap,
                                   _lib.CLG_MEM_DEVICE, C.byref(total)))
-        if self.engine.async_slice:  # the collective reads the payload: wait for the gather
-            self.engine.sync()
+        if self.engine.async_slice:  # the collective reads the payload: order it after the gather
+            import torch
+            gs = lib.clg_gather_stream(self.engine.handle)
+            torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(gs))
         return total.value
 
     def apply(self, req: np.ndarray, recv) -> None:
@@ -184,7 +167,13 @@ class EngineIO:
 class Replicator:
     """Sharing-depth replication for one rank.  `io` does the byte work (EngineIO; the CPU
     tests pass a stand-in over the oracle).  owned_handles: gid -> handle of each owned log
-    that is sent; replicas of the wanted logs are opened here."""
+    that is sent; replicas of the wanted logs are opened here.
+
+    One exchange moves each destination only the logs it wants: the slices of all requests
+    land in one payload buffer grouped by destination (one batched slice), and three
+    collectives carry them -- an all-to-all of (rows, bytes) per destination pair, an
+    all-to-all of the header rows and an all-to-all of the payload, each with per-destination
+    split sizes.  With one rank there is nothing to move and no collective runs."""
 
     def __init__(self, io, plan: ReplicationPlan, device, owned_handles: Dict[int, int], group=None):
         self.io, self.plan, self.device, self.group = io, plan, device, group
@@ -195,83 +184,103 @@ class Replicator:
         self.replica_handle = np.full(n, -1, np.int64)
         for gid in plan.wanted:
             self.replica_handle[gid] = io.open_replica(plan.table.ids[gid])
-        missing = [int(g) for g in plan.send if self.handle[g] < 0]
+        missing = sorted({int(g) for g in plan.req_gid if self.handle[g] < 0})
         if missing:
             raise ValueError(f"no log handle for owned gids {missing[:8]}")
-        # prebuilt slice requests: one per sent log, the replication consumer
-        ns = len(plan.send)
-        self._sreq = np.zeros(max(ns, 1), SLICE_REQ)
-        self._sreq["log"][:ns] = self.handle[plan.send]
-        self._sreq["ch_lo"], self._sreq["ch_hi"] = REPLICATION_CHANNEL
-        self._sres = np.zeros(max(ns, 1), SLICE_RES)
-        self._blob = None
+        # prebuilt slice requests: one per (sent log, destination), the destination's consumer
+        nq = len(plan.req_gid)
+        self._sreq = np.zeros(max(nq, 1), SLICE_REQ)
+        self._sreq["log"][:nq] = self.handle[plan.req_gid]
+        self._sreq["ch_lo"][:nq] = REPLICATION_CHANNEL[0]
+        self._sreq["ch_hi"][:nq] = REPLICATION_CHANNEL[1] | (plan.req_dest.astype(np.uint64) << np.uint64(16))
+        self._sres = np.zeros(max(nq, 1), SLICE_RES)
+        self._payload = None
 
-    def build_blob(self, epoch: int, payload_cap: Optional[int] = None):
-        """Slice every sent log into the send blob.  Returns (blob, header rows, header
-        bytes, payload bytes)."""
+    def payload_bound(self) -> int:
+        """Bytes the requests' slices can need at most (their logs' lengths)."""
+        nq = len(self.plan.req_gid)
+        return self.io.payload_bound(self._sreq["log"][:nq]) if nq else 0
+
+    def build_payload(self, epoch: int, payload_cap: Optional[int] = None):
+        """Slice every request into the payload buffer (grouped by destination).  Returns
+        (payload, header rows by destination, rows per destination, bytes per destination)."""
         import torch
-        ns = len(self.plan.send)
-        hb = header_bytes(ns)
-        cap = payload_cap if payload_cap is not None else self.io.payload_bound(self._sreq["log"][:ns])
-        if self._blob is None or self._blob.numel() < hb + cap + BLOB_ALIGN:
-            self._blob = torch.empty(_align(hb + cap) + BLOB_ALIGN, dtype=torch.uint8, device=self.device)
-        blob = self._blob
-        self._sreq["epoch"][:ns] = epoch
-        total = self.io.slice(self._sreq, self._sres, ns, blob.data_ptr() + hb, cap) if ns else 0
-        res = self._sres[:ns]
+        plan = self.plan
+        nq = len(plan.req_gid)
+        cap = payload_cap if payload_cap is not None else self.payload_bound()
+        if self._payload is None or self._payload.numel() < cap + BLOB_ALIGN:
+            self._payload = torch.empty(_align(cap) + BLOB_ALIGN, dtype=torch.uint8, device=self.device)
+        self._sreq["epoch"][:nq] = epoch
+        if nq:
+            self.io.slice(self._sreq, self._sres, nq, self._payload.data_ptr(), cap)
+        res = self._sres[:nq]
         bad = np.nonzero(res["status"])[0]
         if bad.size:
             check(int(res["status"][bad[0]]))
         keep = np.nonzero((res["has_delta"] != 0) & (res["len"] > 0))[0]
+        dest = plan.req_dest[keep]
+        rows_to = np.bincount(dest, minlength=plan.world).astype(np.int64)
+        bytes_to = np.bincount(dest, weights=res["len"][keep], minlength=plan.world).astype(np.int64)
+        # each destination's payload starts where its first request's slice landed
+        start = np.concatenate([[0], np.cumsum(bytes_to)[:-1]]).astype(np.int64)
         rows = np.zeros(len(keep), HEADER)
-        rows["gid"] = self.plan.send[keep]
+        rows["gid"] = plan.req_gid[keep]
         rows["offset_from_epoch"] = res["offset_from_epoch"][keep]
         rows["epoch"] = epoch
         rows["len"] = res["len"][keep]
-        rows["payload_off"] = res["out_off"][keep]
-        return blob, rows, hb, int(total)
+        rows["payload_off"] = res["out_off"][keep].astype(np.int64) - start[dest]  # within its destination's part
+        return self._payload, rows, rows_to, bytes_to
 
     def exchange(self, epoch: int, payload_cap: Optional[int] = None) -> ExchangeStats:
         """One replication round for `epoch` (all ranks call it together)."""
         import torch
+        import torch.distributed as dist
         st = ExchangeStats()
-        blob, rows, hb, payload = self.build_blob(epoch, payload_cap)
-        head = np.zeros(hb // HEADER.itemsize, HEADER)
-        head[:len(rows)] = rows
-        blob[:hb].copy_(torch.from_numpy(head.view(np.uint8)))
-        used = hb + payload
-        st.sent_bytes = used
-        sizes = allgather_sizes([hb, payload, len(rows)], self.device, self.group)  # [world, 3]
-        stride = _align(int((sizes[:, 0] + sizes[:, 1]).max()))
-        send = blob[:stride] if blob.numel() >= stride else torch.nn.functional.pad(blob[:used], (0, stride - used))
-        recv = allgather_blobs(send, stride, self.group)
-        hmax = int(sizes[:, 0].max())
-        # one D2H copy of every header region; it also orders the host after the collective
-        heads = recv.view(self.plan.world, stride)[:, :hmax].cpu().numpy()
-        parts = []
-        for r in range(self.plan.world):
-            if r == self.plan.rank:
-                continue
-            st.recv_bytes += int(sizes[r, 0] + sizes[r, 1])
-            n = int(sizes[r, 2])
-            rr = heads[r, :n * HEADER.itemsize].view(HEADER)
-            src = np.uint64(r * stride + int(sizes[r, 0])) + rr["payload_off"].astype(np.uint64)
-            parts.append((rr, src))
-        if not parts:
+        plan = self.plan
+        if plan.world == 1:
             return st
-        rows_all = np.concatenate([p[0] for p in parts])
-        src_all = np.concatenate([p[1] for p in parts])
-        h = self.replica_handle[rows_all["gid"]]
+        payload, rows, rows_to, bytes_to = self.build_payload(epoch, payload_cap)
+        backend = dist.get_backend(self.group)
+        dev = self.device if backend == "nccl" else "cpu"
+        # 1. (rows, bytes) for every destination pair
+        mine = torch.from_numpy(np.stack([rows_to, bytes_to], 1).reshape(-1).copy()).to(dev)
+        theirs = torch.empty_like(mine)
+        dist.all_to_all_single(theirs, mine, group=self.group)
+        got = theirs.cpu().numpy().reshape(plan.world, 2)
+        rows_from, bytes_from = got[:, 0], got[:, 1]
+        st.sent_bytes = int(rows_to.sum()) * HEADER.itemsize + int(bytes_to.sum())
+        st.recv_bytes = int(rows_from.sum()) * HEADER.itemsize + int(bytes_from.sum())
+        # 2. header rows
+        hsend = torch.from_numpy(rows.view(np.uint8).copy()).to(dev)
+        hrecv = torch.empty(int(rows_from.sum()) * HEADER.itemsize, dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(hrecv, hsend, output_split_sizes=(rows_from * HEADER.itemsize).tolist(),
+                               input_split_sizes=(rows_to * HEADER.itemsize).tolist(), group=self.group)
+        # 3. payload
+        nrecv = int(bytes_from.sum())
+        recv = torch.empty(max(nrecv, 1) + BLOB_ALIGN, dtype=torch.uint8, device=dev)
+        psend = _to_comm(payload[:int(bytes_to.sum())], backend)
+        dist.all_to_all_single(recv[:nrecv], psend, output_split_sizes=bytes_from.tolist(),
+                               input_split_sizes=bytes_to.tolist(), group=self.group)
+        # the header read-back also orders the host after the collectives
+        rr = hrecv.cpu().numpy().view(HEADER)
+        if not len(rr):
+            return st
+        src_start = np.concatenate([[0], np.cumsum(bytes_from)[:-1]]).astype(np.uint64)
+        src_rank = np.repeat(np.arange(plan.world), rows_from)
+        src = src_start[src_rank] + rr["payload_off"].astype(np.uint64)
+        h = self.replica_handle[rr["gid"]]
         want = h >= 0
         st.skipped = int((~want).sum())
         n = int(want.sum())
         if n:
             req = np.zeros(n, DELTA_REQ)
             req["log"] = h[want]
-            req["offset_from_epoch"] = rows_all["offset_from_epoch"][want]
-            req["epoch"] = rows_all["epoch"][want]
-            req["src_off"] = src_all[want]
-            req["len"] = rows_all["len"][want]
+            req["offset_from_epoch"] = rr["offset_from_epoch"][want]
+            req["epoch"] = rr["epoch"][want]
+            req["src_off"] = src[want]
+            req["len"] = rr["len"][want]
+            if str(self.device).startswith("cuda") and not recv.is_cuda:  # gloo: into HBM once
+                recv = recv.to(self.device)
             self.io.apply(req, recv)
             bad = np.nonzero(req["status"])[0]
             if bad.size:
@@ -291,7 +300,8 @@ class MergedCopies:
     MERGE_GUARD bytes around them, ready for clg_replay_prepare_device as they lie.  Also as
     arrays (gids, offsets, lengths), which the batched consumers read."""
 
-    def __init__(self, buf, place: Optional[Dict[int, Tuple[int, int]]] = None, gids=None, offs=None, lens=None):
+    def __init__(self, buf, place: Optional[Dict[int, Tuple[int, int]]] = None, gids=None, offs=None, lens=None,
+                 ranks=None):
         self.buf = buf
         if place is not None:
             gids = np.fromiter(place.keys(), np.int64, len(place))
@@ -300,6 +310,7 @@ class MergedCopies:
         self.gids = np.asarray(gids if gids is not None else [], np.int64)
         self.offs = np.asarray(offs if offs is not None else [], np.int64)
         self.lens = np.asarray(lens if lens is not None else [], np.int64)
+        self.ranks = np.asarray(ranks if ranks is not None else np.full(len(self.gids), -1), np.int64)  # winner's rank
         self._place = place
 
     @property
@@ -383,4 +394,4 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     recv = inbound[np.lexsort((inbound, win_rank[inbound]))]
     lens = win_len[recv]
     offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(recv) else lens
-    return MergedCopies(buf, gids=gids[recv], offs=offs, lens=lens)
+    return MergedCopies(buf, gids=gids[recv], offs=offs, lens=lens, ranks=win_rank[recv])

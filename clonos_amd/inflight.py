@@ -7,6 +7,12 @@ Reference (I/ = flink-runtime/src/main/java/org/apache/flink/runtime/inflightlog
     notifyCheckpointComplete(cp)       :51-70
     getInFlightIterator(epoch, ignore) :73-82   (ReplayIterator :107-201)
     close()                            :90-94
+  SpillableSubpartitionInFlightLogger  I/SpillableSubpartitionInFlightLogger.java:45-341 (the
+                                       default, I/InFlightLogConfig.java:44; spill files not modelled)
+    log                                :84-103  (a buffer logged while replaying reaches the live
+                                                 iterator, I/SpilledReplayIterator.java:262-277)
+    getInFlightIterator                :126-142 (tailMap(epoch); null when empty;
+                                                 SpilledReplayIterator :60-401)
 
 The buffers live in HBM (the engine's segment pool); replays of many subpartitions are one
 batched gather on the GPU (clg_ifl_replay_batch).  The Java refcount bookkeeping
@@ -34,12 +40,17 @@ class InFlightReplay:
     getEpoch() once the last buffer was taken."""
 
     def __init__(self, status: int, buffers: List[bytes], remaining: int, epochs: Optional[List[int]] = None,
-                 end_epoch: int = 0):
+                 end_epoch: int = 0, flags: int = 0):
         self.status = status
         self.buffers = buffers
         self.remaining = remaining
         self.epochs = list(epochs) if epochs is not None else []
         self.end_epoch = end_epoch
+        self.flags = flags  # CLG_IFL_NULL_ITERATOR | CLG_IFL_REPLAYING (spillable)
+
+    @property
+    def null_iterator(self) -> bool:
+        return bool(self.flags & _lib.CLG_IFL_NULL_ITERATOR)
 
 
 class InFlightLogIterator:
@@ -85,13 +96,66 @@ class InFlightLogIterator:
             yield self.next()
 
 
-class InFlightLog:
-    """InMemorySubpartitionInFlightLogger over the engine's HBM pool."""
+class LiveInFlightLogIterator:
+    """The spillable logger's SpilledReplayIterator (:60-401) over the engine's current iterator:
+    `chunk` buffers per engine call, each exhausted chunk continued (CLG_IFL_CONTINUE) so that
+    buffers logged meanwhile are delivered too (notifyNewBufferAdded :262-277)."""
 
-    def __init__(self, engine):
+    def __init__(self, log: "InFlightLog", first: InFlightReplay, chunk: int):
+        self._log, self._chunk = log, chunk
+        self._rep, self._i = first, 0
+        self._left = first.remaining
+
+    def _refill(self):
+        if self._i < len(self._rep.buffers) or self._rep.status != _lib.CLG_OK:
+            return
+        rep = replay_batch(self._log.engine, [(self._log, 0, 0, self._chunk, _lib.CLG_IFL_CONTINUE)])[0]
+        if rep.status not in (_lib.CLG_OK, _lib.CLG_E_EPOCH_GAP):
+            check(rep.status)
+        self._rep, self._i, self._left = rep, 0, rep.remaining
+
+    def has_next(self) -> bool:  # consumerCursor.hasNext()
+        self._refill()
+        return self._i < len(self._rep.buffers) or self._rep.status == _lib.CLG_E_EPOCH_GAP
+
+    def next(self) -> bytes:
+        self._refill()
+        if self._i >= len(self._rep.buffers):
+            if self._rep.status == _lib.CLG_E_EPOCH_GAP:  # EpochCursor: log.get(epoch) == null
+                raise ClonosError(_lib.CLG_E_EPOCH_GAP, "in-flight log epoch gap (SpilledReplayIterator)")
+            raise StopIteration
+        b = self._rep.buffers[self._i]
+        self._i += 1
+        self._left -= 1
+        return b
+
+    def number_remaining(self) -> int:
+        return self._left
+
+    def get_epoch(self) -> int:  # consumerCursor.getNextEpoch() :166-168
+        self._refill()
+        if self._i < len(self._rep.epochs):
+            return self._rep.epochs[self._i]
+        return self._rep.end_epoch
+
+    def __iter__(self):
+        while self.has_next():
+            yield self.next()
+
+
+class InFlightLog:
+    """InMemorySubpartitionInFlightLogger (kind "in_memory") or SpillableSubpartitionInFlightLogger
+    (kind "spillable", the reference's default) over the engine's HBM pool."""
+
+    KINDS = {"in_memory": _lib.CLG_IFL_IN_MEMORY, "spillable": _lib.CLG_IFL_SPILLABLE}
+
+    def __init__(self, engine, kind: str = "in_memory"):
+        if kind not in self.KINDS:
+            raise ValueError(f"kind must be one of {sorted(self.KINDS)}")
         self.engine = engine
+        self.kind = kind
         h = C.c_uint32()
-        check(lib.clg_ifl_open(engine.handle, C.byref(h)))
+        check(lib.clg_ifl_open_typed(engine.handle, self.KINDS[kind], C.byref(h)))
         self.handle = h.value
 
     def log(self, buffer: bytes, epoch_id: int, is_finished: bool = True) -> None:  # :44-48
@@ -110,13 +174,22 @@ class InFlightLog:
                                 C.byref(n)))
         return [(int(ids[i]), int(cnt[i])) for i in range(n.value)]
 
-    def replay(self, start_epoch: int, ignore_buffers: int = 0) -> InFlightReplay:
-        return replay_batch(self.engine, [(self, start_epoch, ignore_buffers)])[0]
+    def replay(self, start_epoch: int, ignore_buffers: int = 0, max_buffers: int = 0) -> InFlightReplay:
+        return replay_batch(self.engine, [(self, start_epoch, ignore_buffers, max_buffers, 0)])[0]
 
-    def get_in_flight_iterator(self, epoch_id: int, ignore_buffers: int = 0) -> InFlightLogIterator:  # :73-82
-        rep = self.replay(epoch_id, ignore_buffers)
+    def replay_continue(self, max_buffers: int = 0) -> InFlightReplay:
+        """Spillable: the next buffers of the current iterator (CLG_IFL_CONTINUE)."""
+        return replay_batch(self.engine, [(self, 0, 0, max_buffers, _lib.CLG_IFL_CONTINUE)])[0]
+
+    def get_in_flight_iterator(self, epoch_id: int, ignore_buffers: int = 0, chunk: int = 64):
+        """in-memory :73-82 (the drained ReplayIterator); spillable :126-142 (None when tailMap(epoch)
+        is empty, else a live iterator taking `chunk` buffers per engine call)."""
+        spill = self.kind == "spillable"
+        rep = self.replay(epoch_id, ignore_buffers, chunk if spill else 0)
         if rep.status not in (_lib.CLG_OK, _lib.CLG_E_EPOCH_GAP):
-            check(rep.status)  # CLG_E_STATE: the skip loop itself threw (:78-79)
+            check(rep.status)  # CLG_E_STATE: the skip inside getInFlightIterator threw
+        if spill:
+            return None if rep.null_iterator else LiveInFlightLogIterator(self, rep, chunk)
         return InFlightLogIterator(rep, epoch_id)
 
     def close(self) -> None:  # :90-94 (a no-op once the engine itself is closed)
@@ -141,14 +214,17 @@ def log_batch(engine, items: Sequence[Tuple[InFlightLog, int, bytes]]) -> None:
                                 n, blob.ctypes.data, _lib.CLG_MEM_HOST))
 
 
-def make_requests(reqs: Sequence[Tuple[InFlightLog, int, int]]):
-    """The C request array for (log, start_epoch, ignore_buffers) triples; build it once to
-    replay the same subpartitions repeatedly."""
+def make_requests(reqs: Sequence[Tuple]):
+    """The C request array for (log, start_epoch, ignore_buffers[, max_buffers, flags]) tuples;
+    build it once to replay the same subpartitions repeatedly."""
     creq = (_lib.IflReplayReq * max(len(reqs), 1))()
-    for i, (f, start, ign) in enumerate(reqs):
+    for i, r in enumerate(reqs):
+        f, start, ign = r[:3]
         creq[i].ifl = f.handle
         creq[i].start_epoch = start
         creq[i].ignore_buffers = ign
+        if len(r) > 3:
+            creq[i].max_buffers, creq[i].flags = r[3], r[4]
     return creq
 
 
@@ -210,5 +286,5 @@ def replay_batch(engine, reqs: Sequence[Tuple[InFlightLog, int, int]]) -> List[I
             bufs.append(out[o:o + sz].tobytes())
             o += sz
         eps = [int(x) for x in epochs[r.sizes_off:r.sizes_off + r.n_buffers]]
-        reps.append(InFlightReplay(r.status, bufs, r.remaining, eps, int(r.end_epoch)))
+        reps.append(InFlightReplay(r.status, bufs, r.remaining, eps, int(r.end_epoch), int(r.flags)))
     return reps

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 3
+#define CLG_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -456,53 +456,86 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
                                uint64_t* total);
 
 /* ---- in-flight (data) log (RT/inflightlogging/, I/ below) -------------------------------------
- * InFlightLog I/InFlightLog.java:32-55, implementation InMemorySubpartitionInFlightLogger
- * I/InMemorySubpartitionInFlightLogger.java:28-207: per subpartition, the data buffers sent in
- * each epoch, kept in HBM (the engine's in-flight pool, clg_config.ifl_*; a buffer spans
- * ceil(len / ifl_segment_bytes) segments) until a checkpoint completes.  The Java side keeps
- * refcounts; the engine owns the bytes.  A full pool is CLG_E_NOSPACE with nothing logged:
- * the caller applies backpressure (waits for a checkpoint to free epochs) and retries. */
-int clg_ifl_open(clg_engine* e, uint32_t* handle);
-/* close() :90-94: all buffers released. */
+ * InFlightLog I/InFlightLog.java:32-55, two implementations (I/InFlightLogConfig.java:44 picks
+ * one by taskmanager.inflight.type, default "spillable"):
+ *   CLG_IFL_IN_MEMORY  InMemorySubpartitionInFlightLogger I/InMemorySubpartitionInFlightLogger.java:28-207
+ *   CLG_IFL_SPILLABLE  SpillableSubpartitionInFlightLogger I/SpillableSubpartitionInFlightLogger.java:45-341
+ *                      with SpilledReplayIterator I/SpilledReplayIterator.java:60-401 (replay semantics;
+ *                      the spill files are not modelled -- every buffer stays in HBM, i.e. no spill
+ *                      has completed, which is the deterministic case of the reference)
+ * Per subpartition, the data buffers sent in each epoch, kept in HBM (the engine's in-flight pool,
+ * clg_config.ifl_*; a buffer spans ceil(len / ifl_segment_bytes) segments) until a checkpoint
+ * completes.  The Java side keeps refcounts; the engine owns the bytes.  A full pool is
+ * CLG_E_NOSPACE with nothing logged: the caller applies backpressure (waits for a checkpoint to
+ * free epochs) and retries. */
+#define CLG_IFL_IN_MEMORY 0u
+#define CLG_IFL_SPILLABLE 1u
+int clg_ifl_open(clg_engine* e, uint32_t* handle); /* CLG_IFL_IN_MEMORY */
+int clg_ifl_open_typed(clg_engine* e, uint32_t type, uint32_t* handle);
+/* close() (in-memory :90-94, spillable :151-157): all buffers released. */
 int clg_ifl_close(clg_engine* e, uint32_t ifl);
-/* log(buffer, epochID, isFinished) :44-48, batched: buffer i = bytes[off[i], off[i] + len[i])
- * appended to ifl[i] in epoch[i], in order (host or device input). */
+/* log(buffer, epochID, isFinished) (in-memory :44-48, spillable :84-103), batched: buffer i =
+ * bytes[off[i], off[i] + len[i]) appended to ifl[i] in epoch[i], in order (host or device input).
+ * Spillable: a buffer logged while the log is replaying (between getInFlightIterator and the
+ * drain of its last buffer) reaches the live iterator (notifyNewBufferAdded,
+ * SpilledReplayIterator.java:262-277).  When the log is replaying but getInFlightIterator has
+ * never returned an iterator (its first call found nothing, :132-135), the reference's log()
+ * throws a NullPointerException after appending (:98-99): every buffer is appended and the
+ * status is CLG_E_STATE. */
 int clg_ifl_log_batch(clg_engine* e, const uint32_t* ifl, const int64_t* epoch, const uint64_t* off,
                       const uint32_t* len, uint32_t n, const uint8_t* bytes, uint32_t in_kind);
-/* notifyCheckpointComplete :51-70: epochs < checkpoint_id are dropped, their segments freed. */
+/* notifyCheckpointComplete (in-memory :51-70, spillable :106-123): epochs < checkpoint_id are
+ * dropped, their segments freed. */
 int clg_ifl_notify_checkpoint_complete(clg_engine* e, uint32_t ifl, int64_t checkpoint_id);
 /* Epochs and buffer counts (ascending epoch), for parity tests. */
 int clg_ifl_state(clg_engine* e, uint32_t ifl, int64_t* epoch_ids, uint32_t* n_buffers, uint32_t cap,
                   uint32_t* n_epochs);
-/* getInFlightIterator(startEpochID, ignoreBuffers) :73-82 + draining the ReplayIterator
- * (:107-201), batched: for request i the buffers the iterator yields after skipping
- * ignore_buffers are gathered by one kernel, back to back in request order, into `out`
- * at out_off (len bytes); their sizes go to sizes[sizes_off ...] (n_buffers entries).
- * remaining = the iterator's numberRemaining() after the skip: the buffers of every epoch
- * >= start when start itself holds buffers, else 0 (:121-127: a start epoch that is absent,
- * e.g. already truncated, yields nothing).  An epoch without buffers between start and
- * the last epoch (K buffers before it): next() advances past each returned buffer (:156)
- * and throws at the gap (:133), so the K-th buffer is never delivered -- buffers
- * [ignore_buffers, K-1) are gathered and status is CLG_E_EPOCH_GAP: getInFlightIterator
- * itself succeeds and only the next() after the last gathered buffer throws.  A skip that
- * throws inside getInFlightIterator (:78-79) -- ignore_buffers >= K at a gap, beyond the
- * buffers available without one, or any skip when start is absent -- is CLG_E_STATE, nothing
- * gathered.  epochs (optional, indexed like sizes) receives each buffer's epoch: the
- * iterator's getEpoch() (:181-183, its currentKey) right before the next() that returns
- * it, which PipelinedSubpartition.getReplayedBufferUnsafe (:306-320) stamps on the
- * BufferAndBacklog; end_epoch is getEpoch() after the last buffer was taken (or after the
- * skip when none is).  CLG_E_CAPACITY (bytes or sizes): *total / *total_buffers hold the
- * required sizes and no bytes are gathered. */
+/* getInFlightIterator(startEpochID, ignoreBuffers) + draining the iterator, batched: for request
+ * i the buffers the iterator yields after skipping ignore_buffers are gathered by one kernel,
+ * back to back in request order, into `out` at out_off (len bytes); their sizes go to
+ * sizes[sizes_off ...] (n_buffers entries).  remaining = the iterator's numberRemaining() after
+ * the skip.  epochs (optional, indexed like sizes) receives each buffer's epoch: the iterator's
+ * getEpoch() right before the next() that returns it, which
+ * PipelinedSubpartition.getReplayedBufferUnsafe (:306-320) stamps on the BufferAndBacklog;
+ * end_epoch is getEpoch() after the last buffer was taken (or after the skip when none is).
+ * CLG_E_CAPACITY (bytes or sizes): *total / *total_buffers hold the required sizes, no bytes are
+ * gathered and no iterator state changes.
+ *
+ * In-memory (ReplayIterator :107-201): the buffers of every epoch >= start when start itself holds
+ * buffers, else nothing (:121-127: a start epoch that is absent, e.g. already truncated, yields
+ * nothing).  An epoch without buffers between start and the last epoch (K buffers before it):
+ * next() advances past each returned buffer (:156) and throws at the gap (:133), so the K-th
+ * buffer is never delivered -- buffers [ignore_buffers, K-1) are gathered and status is
+ * CLG_E_EPOCH_GAP.  A skip that throws inside getInFlightIterator (:78-79) -- ignore_buffers >= K
+ * at a gap, beyond the buffers available without one, or any skip when start is absent -- is
+ * CLG_E_STATE, nothing gathered.
+ *
+ * Spillable (getInFlightIterator :126-142, SpilledReplayIterator, EpochCursor :306-394): the
+ * iterator covers tailMap(start) -- the epochs >= start, from the first one present.  Empty (or a
+ * closed log): no iterator (res.flags CLG_IFL_NULL_ITERATOR, nothing gathered).  Its cursors step
+ * epoch IDs one by one, so an epoch missing between the first and the last makes the iterator
+ * throw: a skip reaching past it is CLG_E_STATE (inside the constructor); otherwise the prefetch
+ * cursor stops at it in the constructor and the consumer's first next() throws (no buffer is
+ * delivered, CLG_E_EPOCH_GAP).  The iterator stays the log's current one: max_buffers (0: all)
+ * bounds how many are taken per request, and a request with CLG_IFL_CONTINUE takes the next
+ * buffers of the current iterator (start and ignore_buffers unused), including buffers logged
+ * since.  Taking its last buffer ends the replay (res.flags loses CLG_IFL_REPLAYING).
+ * max_buffers and CLG_IFL_CONTINUE are spillable-only (CLG_E_INVALID_ARG otherwise). */
+#define CLG_IFL_CONTINUE 1u       /* clg_ifl_replay_req.flags: continue the current iterator */
+#define CLG_IFL_NULL_ITERATOR 1u  /* clg_ifl_replay_res.flags: getInFlightIterator returned null */
+#define CLG_IFL_REPLAYING 2u      /* clg_ifl_replay_res.flags: the log is replaying after the call */
 typedef struct clg_ifl_replay_req {
   uint32_t ifl;
   uint32_t ignore_buffers;
   int64_t start_epoch;
+  uint32_t max_buffers; /* spillable: at most this many buffers taken (0: all) */
+  uint32_t flags;       /* CLG_IFL_CONTINUE */
 } clg_ifl_replay_req;
 typedef struct clg_ifl_replay_res {
   int32_t status;
   uint32_t n_buffers;
   uint32_t remaining;
-  uint32_t reserved;
+  uint32_t flags; /* CLG_IFL_NULL_ITERATOR | CLG_IFL_REPLAYING */
   uint64_t out_off;
   uint64_t len;
   uint64_t sizes_off;

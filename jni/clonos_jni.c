@@ -458,11 +458,12 @@ JNIEXPORT jint JNICALL FN(nReplayPrepare)(JNIEnv* env, jclass cls, jlong e, jsho
   return s;
 }
 
-/* ---- in-flight (data) log: InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207) ---- */
-JNIEXPORT jint JNICALL FN(nIflOpen)(JNIEnv* env, jclass cls, jlong e, jintArray out) {
+/* ---- in-flight (data) log: InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207) or
+ * SpillableSubpartitionInFlightLogger (:45-341), by type (CLG_IFL_IN_MEMORY / CLG_IFL_SPILLABLE) ---- */
+JNIEXPORT jint JNICALL FN(nIflOpen)(JNIEnv* env, jclass cls, jlong e, jint type, jintArray out) {
   (void)cls;
   uint32_t h = 0;
-  int s = clg_ifl_open(ENG(e), &h);
+  int s = clg_ifl_open_typed(ENG(e), (uint32_t)type, &h);
   put_int(env, out, (jint)h);
   return s;
 }
@@ -520,17 +521,22 @@ JNIEXPORT jint JNICALL FN(nIflNotifyCheckpointComplete)(JNIEnv* env, jclass cls,
   return clg_ifl_notify_checkpoint_complete(ENG(e), (uint32_t)ifl, cp);
 }
 
-/* getInFlightIterator(epoch, ignoreBuffers) :73-82 drained into `out` (buffers back to back)
- * and `sizes` (i32 per buffer).  res = {status, buffers, numberRemaining, bytes, required
- * bytes, required buffers}; the call's status is CLG_E_CAPACITY when out/sizes are short. */
+/* getInFlightIterator(epoch, ignoreBuffers) drained into `out` (buffers back to back) and
+ * `sizes` (i32 per buffer), at most maxBuffers (0: all; spillable only), or the next buffers of
+ * the current iterator (flags CLG_IFL_CONTINUE, spillable only).  res = {status, buffers,
+ * numberRemaining, bytes, required bytes, required buffers, end epoch, result flags}; the
+ * call's status is CLG_E_CAPACITY when out/sizes are short (nothing taken then). */
 JNIEXPORT jint JNICALL FN(nIflReplay)(JNIEnv* env, jclass cls, jlong e, jint ifl, jlong start, jint ignore,
-                                      jobject out, jobject sizes, jobject epochs, jlongArray res) {
+                                      jint maxBuffers, jint flags, jobject out, jobject sizes, jobject epochs,
+                                      jlongArray res) {
   (void)cls;
   clg_ifl_replay_req q;
   memset(&q, 0, sizeof q);
   q.ifl = (uint32_t)ifl;
   q.ignore_buffers = (uint32_t)ignore;
   q.start_epoch = start;
+  q.max_buffers = (uint32_t)maxBuffers;
+  q.flags = (uint32_t)flags;
   clg_ifl_replay_res r;
   memset(&r, 0, sizeof r);
   uint64_t total = 0, nbuf = 0;
@@ -540,8 +546,8 @@ JNIEXPORT jint JNICALL FN(nIflReplay)(JNIEnv* env, jclass cls, jlong e, jint ifl
   int s = clg_ifl_replay_batch(ENG(e), &q, 1, &r, addr(env, out, 0), cap(env, out), CLG_MEM_HOST,
                                (uint32_t*)addr(env, sizes, 0), (int64_t*)addr(env, epochs, 0), n_sizes, &total,
                                &nbuf);
-  jlong w[7] = {r.status, (jlong)r.n_buffers, (jlong)r.remaining, (jlong)r.len, (jlong)total, (jlong)nbuf,
-                (jlong)r.end_epoch};
-  (*env)->SetLongArrayRegion(env, res, 0, 7, w);
+  jlong w[8] = {r.status, (jlong)r.n_buffers, (jlong)r.remaining, (jlong)r.len, (jlong)total, (jlong)nbuf,
+                (jlong)r.end_epoch, (jlong)r.flags};
+  (*env)->SetLongArrayRegion(env, res, 0, 8, w);
   return s;
 }

@@ -38,6 +38,12 @@ public final class ClonosEngine implements AutoCloseable {
 	public static final int CLG_E_NO_LOG = -14;
 	public static final int CLG_E_NOT_BUFFER_BUILT = -15;
 	public static final int CLG_E_EPOCH_GAP = -16;
+	// in-flight log types (InFlightLogConfig.java:44, taskmanager.inflight.type) and replay flags
+	public static final int CLG_IFL_IN_MEMORY = 0;
+	public static final int CLG_IFL_SPILLABLE = 1;
+	public static final int CLG_IFL_CONTINUE = 1;
+	public static final int CLG_IFL_NULL_ITERATOR = 1;
+	public static final int CLG_IFL_REPLAYING = 2;
 
 	/** The engine's default job (clg_config sharing depth). */
 	public static final int DEFAULT_JOB = 0;
@@ -114,7 +120,7 @@ public final class ClonosEngine implements AutoCloseable {
 			case CLG_E_CONSUMER_BACKWARDS: // ThreadCausalLogImpl.java:215-218
 				return new RuntimeException("Consumer went backwards: " + msg);
 			case CLG_E_NO_CONSUMER: // :245 / :256 dereference a missing ConsumerOffset
-			case CLG_E_EPOCH_GAP: // InMemorySubpartitionInFlightLogger.ReplayIterator :133
+			case CLG_E_EPOCH_GAP: // ReplayIterator :133 / SpilledReplayIterator.EpochCursor (log.get(epoch) == null)
 			case CLG_E_NO_LOG: // flatThreadCausalLogs.get(id) == null
 				return new NullPointerException(msg);
 			case CLG_E_NOT_BUFFER_BUILT: // ReplayingState.SubpartitionRecoveryThread :172-177
@@ -167,17 +173,19 @@ public final class ClonosEngine implements AutoCloseable {
 	static native int nLogOpen(long engine, int job, short vertexId, boolean isMain, long irpLower, long irpUpper,
 							   byte subpartition, int[] out);
 	static native int nLogClose(long engine, int log);
-	// in-flight (data) log, InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207)
-	static native int nIflOpen(long engine, int[] out);
+	// in-flight (data) log, InMemorySubpartitionInFlightLogger (inflightlogging/, :28-207) or
+	// SpillableSubpartitionInFlightLogger (:45-341): type CLG_IFL_IN_MEMORY / CLG_IFL_SPILLABLE
+	static native int nIflOpen(long engine, int type, int[] out);
 	static native int nIflClose(long engine, int ifl);
 	static native int nIflLog(long engine, int ifl, long epoch, ByteBuffer direct, int off, int len);
 	/** n buffers staged back to back in `direct` (lens[i] bytes, epoch epochs[i]), logged in order. */
 	static native int nIflLogBatch(long engine, int ifl, long[] epochs, int[] lens, ByteBuffer direct, int n);
 	static native int nIflNotifyCheckpointComplete(long engine, int ifl, long checkpointId);
-	/** res = {status, n_buffers, remaining, len, total, total_buffers, end_epoch}; sizes (i32) and
-	 *  epochs (i64, native order) receive one entry per buffer. */
-	static native int nIflReplay(long engine, int ifl, long startEpoch, int ignoreBuffers, ByteBuffer out,
-		ByteBuffer sizes, ByteBuffer epochs, long[] res);
+	/** res = {status, n_buffers, remaining, len, total, total_buffers, end_epoch, flags}; sizes (i32)
+	 *  and epochs (i64, native order) receive one entry per buffer.  maxBuffers (0: all) and
+	 *  flags CLG_IFL_CONTINUE (take from the current iterator) apply to spillable logs only. */
+	static native int nIflReplay(long engine, int ifl, long startEpoch, int ignoreBuffers, int maxBuffers, int flags,
+		ByteBuffer out, ByteBuffer sizes, ByteBuffer epochs, long[] res);
 	/** bytes = direct buffer holding encoded records (SimpleDeterminantEncoder.encodeTo). */
 	static native int nAppend(long engine, int log, long epoch, ByteBuffer direct, int off, int len);
 	static native int nUpstreamDelta(long engine, int log, long epoch, int offsetFromEpoch, ByteBuffer direct,

@@ -1,10 +1,15 @@
 /*
  * InFlightLog over the MI355X engine (C-ABI clg_ifl_*, jni/clonos_jni.c): a drop-in for
- * InMemorySubpartitionInFlightLogger (InMemorySubpartitionInFlightLogger.java:28-207).
- * Buffer bytes are copied into HBM on log() and the Java Buffer is recycled at once; a
- * replay gathers every buffer from the start epoch in one GPU call and hands them out as
- * Buffers taken from the in-flight buffer pool.  Wiring: InMemoryInFlightLogFactory
- * returns `new EngineInFlightLog(engine)` instead of the in-memory logger.
+ * InMemorySubpartitionInFlightLogger (InMemorySubpartitionInFlightLogger.java:28-207) and for
+ * the default SpillableSubpartitionInFlightLogger (SpillableSubpartitionInFlightLogger.java:45-341,
+ * InFlightLogConfig.java:44), by type.  Buffer bytes are copied into HBM on log() and the Java
+ * Buffer is recycled at once; a replay gathers buffers from HBM in GPU calls and hands them out
+ * as Buffers taken from the in-flight buffer pool.  In-memory: one call drains the whole
+ * iterator.  Spillable: the iterator is live (SpilledReplayIterator.notifyNewBufferAdded :262):
+ * it takes REPLAY_CHUNK buffers per call and continues the engine's current iterator, so buffers
+ * logged during the replay reach it.  Wiring: InMemoryInFlightLogFactory returns
+ * `new EngineInFlightLog(engine, CLG_IFL_IN_MEMORY)` and SpillableInFlightLogFactory
+ * `new EngineInFlightLog(engine, CLG_IFL_SPILLABLE)` (INTEGRATION.md).
  */
 package org.apache.flink.runtime.inflightlogging;
 
@@ -22,7 +27,9 @@ public class EngineInFlightLog implements InFlightLog {
 
 	private final ClonosEngine engine;
 	private final int ifl;
+	private final int type;
 	private BufferPool inFlightBufferPool;
+	private static final int REPLAY_CHUNK = 64; // spillable: buffers taken per engine call
 
 	// log() stages buffers host-side and hands them to the engine in batches (one upload and
 	// one scatter kernel per batch instead of a GPU round trip per network buffer); every other
@@ -38,11 +45,19 @@ public class EngineInFlightLog implements InFlightLog {
 	// thread touches the stage or submits, so buffers reach the engine once and in log() order
 	private boolean submitting;
 	private boolean closed;
+	// a checkpoint completed while a batch waited for pool space: truncated right after the
+	// batch is accepted (Long.MIN_VALUE: none), so the notifier never waits for the batch
+	private long pendingTruncation = Long.MIN_VALUE;
 
 	public EngineInFlightLog(ClonosEngine engine) {
+		this(engine, CLG_IFL_IN_MEMORY);
+	}
+
+	public EngineInFlightLog(ClonosEngine engine, int type) {
 		this.engine = engine;
+		this.type = type;
 		int[] h = new int[1];
-		check(nIflOpen(engine.handle(), h));
+		check(nIflOpen(engine.handle(), type, h));
 		this.ifl = h[0];
 	}
 
@@ -97,6 +112,10 @@ public class EngineInFlightLog implements InFlightLog {
 
 	// Backpressure: a full in-flight pool (CLG_E_NOSPACE, nothing logged) waits until a
 	// checkpoint completes and frees epochs (notifyCheckpointComplete wakes us), then retries.
+	// Every in-flight log of the engine shares one pool, and the reference notifies the
+	// subpartitions one after another on one thread (EpochTrackerImpl.java:140-142), so the
+	// notifier must not wait for this batch: the truncation it records is applied here, once
+	// the batch is accepted.
 	private void submit(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
 		submitting = true;
 		try {
@@ -107,7 +126,13 @@ public class EngineInFlightLog implements InFlightLog {
 				}
 				waitQuietly();
 			}
-			check(st);
+			long cp = pendingTruncation;
+			pendingTruncation = Long.MIN_VALUE;
+			if (cp != Long.MIN_VALUE && (st == CLG_OK || st == CLG_E_STATE)) {
+				// the batch was logged before the notification: its epochs below cp go too
+				check(nIflNotifyCheckpointComplete(engine.handle(), ifl, cp));
+			}
+			check(st); // CLG_E_STATE: spillable log() while replaying without an iterator (:98-99, NPE)
 		} finally {
 			submitting = false;
 			notifyAll();
@@ -115,16 +140,17 @@ public class EngineInFlightLog implements InFlightLog {
 	}
 
 	@Override
-	public synchronized void notifyCheckpointComplete(long checkpointId) { // :51-70
+	public synchronized void notifyCheckpointComplete(long checkpointId) { // in-memory :51-70, spillable :106-123
 		// free the pool first: a log() waiting for space (backpressure) can then finish
 		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
 		notifyAll();
-		awaitNoSubmit();
-		// staged buffers of truncated epochs never reach HBM, and a batch that was waiting
-		// for space when this call began is truncated too: the reference truncates every
-		// buffer logged before the notification
+		// staged buffers of truncated epochs never reach HBM; a batch waiting for space right now
+		// is truncated by submit() once it is accepted (the reference truncates every buffer
+		// logged before the notification)
 		dropStagedBelow(checkpointId);
-		check(nIflNotifyCheckpointComplete(engine.handle(), ifl, checkpointId));
+		if (submitting) {
+			pendingTruncation = Math.max(pendingTruncation, checkpointId);
+		}
 	}
 
 	private void dropStagedBelow(long checkpointId) {
@@ -155,20 +181,88 @@ public class EngineInFlightLog implements InFlightLog {
 	@Override
 	public synchronized InFlightLogIterator<Buffer> getInFlightIterator(long startEpochID, int ignoreBuffers) {
 		flush();
-		long[] res = new long[7];
-		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, null, null, null, res);
+		if (type == CLG_IFL_SPILLABLE) { // :126-142
+			Chunk c = fetch(startEpochID, ignoreBuffers, 0);
+			if ((c.flags & CLG_IFL_NULL_ITERATOR) != 0) {
+				return null; // tailMap(epochID) is empty
+			}
+			return new LiveReplay(c);
+		}
+		Chunk c = fetch(startEpochID, ignoreBuffers, 0);
+		return new Replay(c);
+	}
+
+	/** One engine call: a new iterator (flags 0) or the next buffers of the current one
+	 *  (CLG_IFL_CONTINUE), sized first, then gathered into direct buffers. */
+	private Chunk fetch(long startEpochID, int ignoreBuffers, int flags) {
+		int max = type == CLG_IFL_SPILLABLE ? REPLAY_CHUNK : 0;
+		long[] res = new long[8];
+		int st = nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, max, flags, null, null, null, res);
 		if (st != CLG_OK && st != CLG_E_CAPACITY) {
 			check(st);
 		}
 		ByteBuffer out = ByteBuffer.allocateDirect((int) Math.max(1, res[4]));
 		ByteBuffer sizes = ByteBuffer.allocateDirect((int) Math.max(4, 4 * res[5])).order(ByteOrder.nativeOrder());
 		ByteBuffer epochs = ByteBuffer.allocateDirect((int) Math.max(8, 8 * res[5])).order(ByteOrder.nativeOrder());
-		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, out, sizes, epochs, res));
+		check(nIflReplay(engine.handle(), ifl, startEpochID, ignoreBuffers, max, flags, out, sizes, epochs, res));
 		int status = (int) res[0];
-		if (status != CLG_OK && status != CLG_E_EPOCH_GAP) { // the skip loop inside getInFlightIterator threw (:78-79)
+		if (status != CLG_OK && status != CLG_E_EPOCH_GAP) { // the skip inside getInFlightIterator threw
 			throw inFlightException(status, nLastError());
 		}
-		return new Replay(out, sizes, epochs, (int) res[1], (int) res[2], res[6], status);
+		return new Chunk(out, sizes, epochs, (int) res[1], (int) res[2], res[6], status, (int) res[7]);
+	}
+
+	/** Buffers of one engine call. */
+	private static final class Chunk {
+		final ByteBuffer bytes;
+		final ByteBuffer sizes;
+		final ByteBuffer epochs;
+		final int count;
+		final int remaining; // numberRemaining() before these buffers were taken
+		final long endEpoch;
+		final int status;
+		final int flags;
+		int next;
+		int pos;
+
+		Chunk(ByteBuffer bytes, ByteBuffer sizes, ByteBuffer epochs, int count, int remaining, long endEpoch,
+			int status, int flags) {
+			this.bytes = bytes;
+			this.sizes = sizes;
+			this.epochs = epochs;
+			this.count = count;
+			this.remaining = remaining;
+			this.endEpoch = endEpoch;
+			this.status = status;
+			this.flags = flags;
+		}
+
+		boolean has() {
+			return next < count;
+		}
+
+		long epoch() {
+			return next < count ? epochs.getLong(8 * next) : endEpoch;
+		}
+	}
+
+	private Buffer materialise(Chunk c, boolean advance) {
+		int n = c.sizes.getInt(4 * c.next);
+		Buffer b;
+		try {
+			b = inFlightBufferPool.requestBufferBlocking();
+		} catch (IOException | InterruptedException e) {
+			throw new RuntimeException(e);
+		}
+		ByteBuffer src = c.bytes.duplicate();
+		src.position(c.pos).limit(c.pos + n);
+		b.getMemorySegment().put(0, src, n);
+		b.setSize(n);
+		if (advance) {
+			c.pos += n;
+			c.next++;
+		}
+		return b;
 	}
 
 	@Override
@@ -190,70 +284,38 @@ public class EngineInFlightLog implements InFlightLog {
 		return inFlightBufferPool;
 	}
 
-	/** The drained ReplayIterator (:107-201): buffers materialised from the gathered bytes. */
+	/** The drained in-memory ReplayIterator (:107-201): buffers materialised from the gathered bytes. */
 	private final class Replay extends InFlightLogIterator<Buffer> {
-		private final ByteBuffer bytes;
-		private final ByteBuffer sizes;
-		private final ByteBuffer epochs;
-		private final int count;
-		private final long endEpoch;
-		private final int status;
-		private int next;
+		private final Chunk c;
 		private int left;
-		private int pos;
 
-		Replay(ByteBuffer bytes, ByteBuffer sizes, ByteBuffer epochs, int count, int remaining, long endEpoch,
-			int status) {
-			this.bytes = bytes;
-			this.sizes = sizes;
-			this.epochs = epochs;
-			this.count = count;
-			this.left = remaining;
-			this.endEpoch = endEpoch;
-			this.status = status;
+		Replay(Chunk c) {
+			this.c = c;
+			this.left = c.remaining;
 		}
 
 		@Override
 		public boolean hasNext() {
 			// at a gap the reference still sees the last buffer before it (:146-149); next() throws (:156 -> :133)
-			return next < count || status == CLG_E_EPOCH_GAP;
-		}
-
-		private Buffer materialise(boolean advance) {
-			int n = sizes.getInt(4 * next);
-			Buffer b;
-			try {
-				b = inFlightBufferPool.requestBufferBlocking();
-			} catch (IOException | InterruptedException e) {
-				throw new RuntimeException(e);
-			}
-			ByteBuffer src = bytes.duplicate();
-			src.position(pos).limit(pos + n);
-			b.getMemorySegment().put(0, src, n);
-			b.setSize(n);
-			if (advance) {
-				pos += n;
-				next++;
-				left--;
-			}
-			return b;
+			return c.has() || c.status == CLG_E_EPOCH_GAP;
 		}
 
 		@Override
 		public Buffer next() {
-			if (next >= count) {
-				check(status); // CLG_E_EPOCH_GAP -> the reference's NullPointerException
+			if (!c.has()) {
+				check(c.status); // CLG_E_EPOCH_GAP -> the reference's NullPointerException
 				throw new java.util.NoSuchElementException();
 			}
-			return materialise(true);
+			left--;
+			return materialise(c, true);
 		}
 
 		@Override
 		public Buffer peekNext() {
-			if (next >= count) {
+			if (!c.has()) {
 				throw new java.util.NoSuchElementException();
 			}
-			return materialise(false);
+			return materialise(c, false);
 		}
 
 		@Override
@@ -266,12 +328,90 @@ public class EngineInFlightLog implements InFlightLog {
 		 *  the BufferAndBacklog -- and, once drained, the epoch the iterator stopped in. */
 		@Override
 		public long getEpoch() {
-			return next < count ? epochs.getLong(8 * next) : endEpoch;
+			return c.epoch();
 		}
 
 		@Override
 		public void close() {
-			next = count;
+			c.next = c.count;
+		}
+	}
+
+	/** The spillable logger's live SpilledReplayIterator (:60-401): REPLAY_CHUNK buffers per engine
+	 *  call; an exhausted chunk continues the engine's current iterator, which also holds the
+	 *  buffers logged since (notifyNewBufferAdded :262-277).  A gap makes the engine report
+	 *  CLG_E_EPOCH_GAP, and next() throws the reference's NullPointerException there. */
+	private final class LiveReplay extends InFlightLogIterator<Buffer> {
+		private Chunk c;
+		private int left;
+
+		LiveReplay(Chunk first) {
+			this.c = first;
+			this.left = first.remaining;
+		}
+
+		/** The next chunk when this one is used up (buffers logged meanwhile included). */
+		private void refill() {
+			synchronized (EngineInFlightLog.this) {
+				if (c.has() || c.status != CLG_OK) {
+					return;
+				}
+				flush();
+				Chunk n = fetch(0, 0, CLG_IFL_CONTINUE);
+				left = n.remaining;
+				c = n;
+			}
+		}
+
+		@Override
+		public boolean hasNext() { // consumerCursor.hasNext(): remaining > 0
+			refill();
+			return c.has() || c.status == CLG_E_EPOCH_GAP;
+		}
+
+		@Override
+		public Buffer next() {
+			refill();
+			if (!c.has()) {
+				check(c.status);
+				throw new java.util.NoSuchElementException();
+			}
+			left--;
+			return materialise(c, true);
+		}
+
+		@Override
+		public Buffer peekNext() {
+			refill();
+			if (!c.has()) {
+				check(c.status);
+				throw new java.util.NoSuchElementException();
+			}
+			return materialise(c, false);
+		}
+
+		@Override
+		public int numberRemaining() {
+			return left;
+		}
+
+		@Override
+		public long getEpoch() { // consumerCursor.getNextEpoch() :166-168
+			refill();
+			return c.epoch();
+		}
+
+		@Override
+		public void close() { // :232-253: the rest is taken and recycled
+			synchronized (EngineInFlightLog.this) {
+				while (c.status == CLG_OK && (c.has() || left > 0)) {
+					c.next = c.count;
+					refill();
+					if (!c.has()) {
+						break;
+					}
+				}
+			}
 		}
 	}
 }

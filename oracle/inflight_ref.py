@@ -110,3 +110,183 @@ class InFlightLogRef:
         except IteratorNPE:
             return "gap", out, remaining, eps, end
         return "ok", out, remaining, eps, it.current_key
+
+
+# ---- SpillableSubpartitionInFlightLogger (the reference's default, InFlightLogConfig.java:44) ----
+# S = SpillableSubpartitionInFlightLogger.java, SI = SpilledReplayIterator.java (same directory).
+# The spill files are not modelled: no flush ever completes, so every buffer stays in memory
+# (never "recycled") and the prefetcher never waits for a read -- the deterministic case.
+# Java exceptions are IteratorNPE here (NullPointerException / IndexOutOfBoundsException).
+class _View:
+    """tailMap(view) of the logger's live epoch map (S:133): keys >= view."""
+
+    def __init__(self, log: dict, view: int):
+        self.log, self.view = log, view
+
+    def get(self, e):
+        if e < self.view or e not in self.log:
+            raise IteratorNPE(f"log.get({e}) == null")
+        return self.log[e]
+
+
+class EpochCursor:  # SI:306-394
+    def __init__(self, view: _View):
+        keys = sorted(k for k in view.log if k >= view.view)
+        self.v = view
+        self.next_epoch = keys[0]      # :316 firstKey
+        self.next_off = 0
+        self.last_epoch = keys[-1]     # :318 lastKey
+        self.remaining = sum(len(view.log[k]) for k in keys)
+
+    def copy(self):
+        c = EpochCursor.__new__(EpochCursor)
+        c.__dict__.update(self.__dict__)
+        return c
+
+    def has_next(self):  # :324-326
+        return self.remaining > 0
+
+    def _advance(self):  # :353-358
+        if self.next_off == len(self.v.get(self.next_epoch)) and self.next_epoch != self.last_epoch:
+            self.next_epoch += 1
+            self.next_off = 0
+
+    def get_next_epoch(self):  # :328-331
+        self._advance()
+        return self.next_epoch
+
+    def get_next_epoch_offset(self):  # :333-336
+        self._advance()
+        return self.next_off
+
+    def next(self):  # :342-351
+        self._advance()
+        bufs = self.v.get(self.next_epoch)
+        if self.next_off >= len(bufs):
+            raise IteratorNPE("buffers.get(offset) past the epoch (IndexOutOfBoundsException)")
+        b = bufs[self.next_off]
+        self.next_off += 1
+        self.remaining -= 1
+        self._advance()
+        return b
+
+    def behind(self, other):  # :364-367
+        return (self.get_next_epoch() < other.get_next_epoch() or
+                (self.get_next_epoch() == other.get_next_epoch() and
+                 self.get_next_epoch_offset() < other.get_next_epoch_offset()))
+
+    def notify_new_buffer(self, epoch):  # :389-393
+        self.remaining += 1
+        if epoch > self.last_epoch:
+            self.last_epoch = epoch
+
+
+class SpilledReplayIterator:  # SI:60-277
+    def __init__(self, owner, view: _View, ignore: int):
+        self.owner = owner
+        self.consumer = EpochCursor(view)   # :92
+        self.prefetch = EpochCursor(view)   # :93
+        for _ in range(ignore):             # :98-101
+            self.consumer.next()
+            self.prefetch.next()
+        self._prefetch()                    # :123
+
+    def _prefetch(self):  # :126-158, exceptions printed and swallowed
+        try:
+            while self.prefetch.has_next():
+                self.prefetch.get_next_epoch()
+                self.prefetch.next()   # in memory: retainBuffer only
+        except IteratorNPE:
+            pass
+
+    def number_remaining(self):  # :160-163
+        return self.consumer.remaining
+
+    def get_epoch(self):  # :165-168
+        return self.consumer.get_next_epoch()
+
+    def has_next(self):  # :255-260
+        return self.consumer.has_next()
+
+    def next(self):  # :170-203
+        while not self.consumer.behind(self.prefetch):
+            self._prefetch()
+            if not self.consumer.behind(self.prefetch):
+                raise IteratorNPE("next() would wait forever (nothing left to prefetch)")
+        b = self.consumer.next()
+        if not self.consumer.has_next():
+            self.owner.replaying = False    # :186-187
+        self._prefetch()
+        return b
+
+    def notify_new_buffer_added(self, epoch):  # :262-277
+        self.prefetch.notify_new_buffer(epoch)
+        self.consumer.notify_new_buffer(epoch)
+
+
+class SpillableInFlightLogRef:
+    """SpillableSubpartitionInFlightLogger (S:45-341) without the disk: log, notifyCheckpointComplete,
+    getInFlightIterator (a live iterator over tailMap(epochID)) and the isReplaying flag."""
+
+    def __init__(self):
+        self.sliced = {}
+        self.replaying = False   # S:58
+        self.current = None      # S:60
+        self.closed = False
+
+    def log(self, buf: bytes, epoch: int):  # S:84-103
+        if self.closed:
+            return
+        self.sliced.setdefault(epoch, []).append(bytes(buf))
+        if self.replaying:
+            if self.current is None:
+                raise IteratorNPE("currentIterator == null in log()")  # S:98-99, after the append
+            self.current.notify_new_buffer_added(epoch)
+
+    def notify_checkpoint_complete(self, cp: int):  # S:106-123
+        for k in [k for k in self.sliced if k < cp]:
+            del self.sliced[k]
+
+    def get_in_flight_iterator(self, start: int, ignore: int):  # S:126-142
+        if self.closed:
+            return None
+        self.replaying = True
+        if not any(k >= start for k in self.sliced):
+            return None
+        self.current = SpilledReplayIterator(self, _View(self.sliced, start), ignore)  # may raise (constructor)
+        return self.current
+
+    def take(self, it, max_buffers: int = 0):
+        """(status, buffers, remaining, epochs, end_epoch) for draining `it` (at most max_buffers,
+        0: all), as clg_ifl_replay_batch reports one request: 'ok' or 'gap' (next() threw)."""
+        remaining = it.number_remaining()
+        out, eps = [], []
+        try:
+            while it.has_next() and (max_buffers == 0 or len(out) < max_buffers):
+                e = it.get_epoch()
+                out.append(it.next())
+                eps.append(e)
+        except IteratorNPE:
+            return "gap", out, remaining, eps, it.consumer.next_epoch
+        try:
+            end = it.get_epoch()
+        except IteratorNPE:
+            end = it.consumer.next_epoch
+        return "ok", out, remaining, eps, end
+
+    def replay_full(self, start: int, ignore: int, max_buffers: int = 0):
+        """A new iterator and its first `max_buffers` buffers: (status, buffers, remaining,
+        epochs, end_epoch); status 'null' (no iterator) or 'state' (the constructor threw)."""
+        try:
+            it = self.get_in_flight_iterator(start, ignore)
+        except IteratorNPE:
+            return "state", [], 0, [], None
+        if it is None:
+            return "null", [], 0, [], None
+        return self.take(it, max_buffers)
+
+    def continue_full(self, max_buffers: int = 0):
+        """The next buffers of the current iterator (CLG_IFL_CONTINUE)."""
+        if self.current is None:
+            return "state", [], 0, [], None
+        return self.take(self.current, max_buffers)

@@ -1,7 +1,7 @@
-"""CPU, world_size 2 over gloo: the sharing-depth replication protocol of
-clonos_amd/dist.py (canonical log table, send blobs of gid-keyed rows, all-gather of sizes
-and padded blobs, one header read-back, the wanted-log filter, per-epoch re-delivery) and
-the cross-GPU replay-prep merge.  The byte store is the oracle's ThreadCausalLogImpl model
+"""CPU, world sizes 2, 4 and 8 over gloo: the sharing-depth replication protocol of
+clonos_amd/dist.py (canonical log table, per-destination consumers and requests, the
+all-to-alls of counts, header rows and payload, per-epoch re-delivery, depth -1 and 1) and
+the cross-GPU replay-prep merge (all-reduce MAX with ties to the highest rank, all-to-all).  The byte store is the oracle's ThreadCausalLogImpl model
 (test infrastructure standing in for the engine, which needs a GPU; the same protocol
 over real engines is tests/test_gpu_dist.py)."""
 import os
@@ -75,7 +75,7 @@ class OracleIO:
             ctypes.memmove(out_ptr + dst, d, len(d))
             sres[i] = (st, 1, ofe, len(d), dst)
             dst += len(d)
-        assert X.REPLICATION_CHANNEL == (int(sreq["ch_lo"][0]), int(sreq["ch_hi"][0]))
+        assert X.REPLICATION_CHANNEL == (int(sreq["ch_lo"][0]), int(sreq["ch_hi"][0]) & 0xFFFF)
         return dst
 
     def apply(self, req, recv):
@@ -100,6 +100,12 @@ def worker(rank, world, port, q, depth):
         io = OracleIO()
         owned = {int(gid): io.new_log() for gid in plan.owned}
         rep = X.Replicator(io, plan, "cpu", {gid: h for gid, h in owned.items() if gid in set(plan.send.tolist())})
+        # each destination gets exactly the logs it wants, once
+        need_all = J.replication_masks(g, depth, world)
+        for r in range(world):
+            mine_to_r = plan.req_gid[plan.req_dest == r]
+            expect = [int(x) for x in plan.owned if r != rank and need_all[r][table.vertex[x]]]
+            assert mine_to_r.tolist() == expect
         for ep in range(EPOCHS):
             for half in range(2):  # two exchanges per epoch: re-delivery must be a no-op
                 for gid, h in owned.items():
@@ -108,7 +114,7 @@ def worker(rank, world, port, q, depth):
                     if part:
                         assert io.logs[h].append(ep, part) == 0
                 st = rep.exchange(ep)
-                assert st.skipped >= 0
+                assert st.skipped == 0  # a rank is sent only the logs it wants
         # every wanted replica holds exactly the owner's bytes; nothing else was opened
         need = J.replication_masks(g, depth, world)[rank]
         got = 0
@@ -144,9 +150,10 @@ def run_world(target, *args, world=2):
     return res
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("depth", [-1, 1])
-def test_replication_gloo_world2(depth):
-    res = run_world(worker, depth)
+def test_replication_gloo(depth, world):
+    res = run_world(worker, depth, world=world)
     assert sum(info for _, _, info in res) > 0
 
 
@@ -155,8 +162,28 @@ def test_header_layout():
     rows = np.zeros(3, X.HEADER)
     rows["gid"] = [7, 0, 66175]
     rows["len"] = [5, 0, 17]
-    assert X.HEADER.itemsize == 32 and X.header_bytes(3) == 128
+    assert X.HEADER.itemsize == 32
     assert np.frombuffer(rows.tobytes(), X.HEADER)["gid"].tolist() == [7, 0, 66175]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_plan_depth1_sends_direct_producers_only(world):
+    """At depth 1 a rank receives the logs of its subtasks' direct producers only (config 1's
+    sharing depth), so the requests to it are exactly those; at world 1 there are none."""
+    from clonos_amd import dist as X
+    from clonos_amd import job as J
+    g = J.dag(4, 8)
+    table = J.LogTable(g)
+    need = J.replication_masks(g, 1, world)
+    plans = [X.ReplicationPlan(table, 1, r, world, need) for r in range(world)]
+    for dst in range(world):
+        got = sorted(int(x) for p in plans for x in p.req_gid[p.req_dest == dst])
+        assert got == plans[dst].wanted.tolist()
+        stages = {int(table.vertex[x]) // 8 for x in got}
+        own_stages = {v // 8 for v in range(32) if J.owner_rank(v, world) == dst}
+        assert all(s + 1 in own_stages for s in stages)  # only a stage right below one it hosts
+    if world == 1:
+        assert len(plans[0].req_gid) == 0
 
 
 def test_plan_partitions_logs():
@@ -193,7 +220,7 @@ def merge_worker(rank, world, port, q):
         g = J.dag(STAGES, PAR)
         table = J.LogTable(g)
         failed = [1, 5]  # a connected pair (stage 0 subtask 1 -> stage 1 subtask 1)
-        dest_of = {1: 1, 5: 0}
+        dest_of = {1: 1 % world, 5: 0}
         full = {gid: records(table.ids[gid], 0, 200) for gid in range(len(table)) if table.vertex[gid] in failed}
         rng = np.random.default_rng(9)
         cut = {gid: [int(rng.integers(0, len(b) + 1)) for _ in range(world)] for gid, b in full.items()}
@@ -202,6 +229,10 @@ def merge_worker(rank, world, port, q):
         store = OracleStore(full, cut, rank)
         merged = X.merge_responses(store, table, failed, store.handles, {1: 0, 5: 0}, dest_of, "cpu")
         got = merged.as_dict()
+        # the winner is the longest copy; equal lengths go to the highest rank
+        for gid, rk in zip(merged.gids.tolist(), merged.ranks.tolist()):
+            lens = cut[gid]
+            assert lens[rk] == max(lens) and rk == max(r for r in range(world) if lens[r] == max(lens))
         for o, nb in merged.place.values():  # guard bytes around every winner
             assert o >= X.MERGE_GUARD and o + nb + X.MERGE_GUARD <= merged.buf.numel()
 
@@ -246,7 +277,8 @@ class OracleStore:
         return sum(len(self.copies[int(h)]) for h in handles)
 
 
-def test_merge_gloo_world2():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_merge_gloo(world):
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
-    res = run_world(merge_worker)
+    res = run_world(merge_worker, world=world)
     assert sum(info for _, _, info in res) == 2 * (1 + 4)  # both failed vertices' logs

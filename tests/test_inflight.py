@@ -131,3 +131,56 @@ def test_host_iterator_mirrors_reference_iterator():
                     mine.next()
                 break
             assert mine.next() == want
+
+
+# ---- the spillable logger (the reference's default, InFlightLogConfig.java:44) ------------------
+def test_spillable_satisfies_inflightlogtest():
+    """InFlightLogTest's three assertions (iteratorCountTest 18; logCheckpointCompleteTest 12 and
+    logIterationTest hasNext after truncating epoch 0 and replaying from 0) all hold for
+    SpillableSubpartitionInFlightLogger's tailMap iterator (:133) -- the two the in-memory code
+    fails (test_checkpoint_complete_then_iterate_from_truncated_epoch) pin this oracle."""
+    from inflight_ref import SpillableInFlightLogRef
+    log = SpillableInFlightLogRef()
+    populate(log)
+    assert log.get_in_flight_iterator(0, 0).number_remaining() == 15 + 3
+    log = SpillableInFlightLogRef()
+    populate(log)
+    log.notify_checkpoint_complete(1)
+    it = log.get_in_flight_iterator(0, 0)
+    assert it.number_remaining() == 10 + 2 and it.has_next()
+    got = []
+    while it.has_next():
+        got.append(it.next())
+    assert got == [bytes([e, i]) * 32 for e in (1, 2) for i in range(6)]
+    assert not log.replaying
+
+
+def test_spillable_gap_throws_before_any_buffer():
+    """The prefetch cursor runs into the missing epoch inside the constructor (the exception is
+    swallowed there, SpilledReplayIterator :155-157); the consumer's first next() then throws
+    from behind() (:175) -- no buffer is delivered.  A skip across the gap throws in the
+    constructor (getInFlightIterator fails)."""
+    from inflight_ref import SpillableInFlightLogRef
+    log = SpillableInFlightLogRef()
+    for e, b in ((5, b"a"), (5, b"b"), (7, b"c")):
+        log.log(b, e)
+    assert log.replay_full(5, 0) == ("gap", [], 3, [], 5)
+    assert log.replay_full(5, 2)[0] == "gap"
+    assert log.replay_full(5, 3)[0] == "state"
+    assert log.replay_full(6, 0) == ("ok", [b"c"], 1, [7], 7)  # tailMap(6) starts at 7
+    assert log.replay_full(8, 0)[0] == "null"
+
+
+def test_spillable_live_append_and_npe():
+    from inflight_ref import IteratorNPE, SpillableInFlightLogRef
+    log = SpillableInFlightLogRef()
+    assert log.get_in_flight_iterator(0, 0) is None and log.replaying
+    with pytest.raises(IteratorNPE):  # currentIterator == null (:98-99), after the append
+        log.log(b"x", 0)
+    assert log.sliced == {0: [b"x"]}
+    it = log.get_in_flight_iterator(0, 0)
+    log.log(b"y", 0)  # reaches the live iterator
+    log.log(b"z", 1)
+    assert [it.next() for _ in range(3)] == [b"x", b"y", b"z"] and not log.replaying
+    log.log(b"w", 1)  # replay over: not delivered to the old iterator
+    assert not it.has_next()
