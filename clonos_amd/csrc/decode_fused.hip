@@ -47,12 +47,18 @@ namespace clg {
 // l walks row l: with a pitch of 35 dwords (co-prime with the 32 banks) the lanes' reads
 // start on distinct banks.  Rows: the tile, then the halo + zero pad.
 constexpr uint32_t kZRowDw = kZRegion / 4;  // 32
-constexpr uint32_t kZPad = 3;
+#ifndef CLG_ZPAD
+#define CLG_ZPAD 3
+#endif
+constexpr uint32_t kZPad = CLG_ZPAD;
 constexpr uint32_t kZPitch = kZRowDw + kZPad;
 constexpr uint32_t kZRows = kZTile / kZRegion + 2;
 constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_COUNT_LM
 #define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
+#endif
+#ifndef CLG_COUNT_PREFETCH
+#define CLG_COUNT_PREFETCH 1  // 1: the count pass without tables issues the next tile's loads during a walk
 #endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
@@ -104,9 +110,13 @@ __device__ __forceinline__ uint64_t fld_be64(const ZBytes& b, uint32_t k) { retu
 // LDS byte offset of aligned coordinate a (rows of 128 bytes at a pitch of 140 bytes):
 // a + 12 (a >> 7) in one full-rate op (left to itself the compiler picks v_mad_u64_u32).
 __device__ __forceinline__ uint32_t zoff(uint32_t a) {
-  uint32_t off;
-  asm("v_mad_u32_u24 %0, %1, 12, %2" : "=v"(off) : "v"(a >> 7), "v"(a));
-  return off;
+  if constexpr (kZPad == 0) {
+    return a;
+  } else {
+    uint32_t off;
+    asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(off) : "v"(a >> 7), "v"(a), "i"(4 * kZPad));
+    return off;
+  }
 }
 typedef const __attribute__((address_space(3))) uint8_t lds_u8;
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
@@ -530,51 +540,86 @@ __device__ __forceinline__ uint64_t pack_cnt(uint32_t rec, uint32_t wide) { retu
 // whole halo (every tile but a span's last two, normally), the halo bytes are loaded
 // together with the tile, so staging costs one memory latency; otherwise the halo is found
 // by walking the span's tiles.
-template <uint32_t kHaloMax = kZHalo, uint32_t kRows = kZRows>
-__device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
-                                            const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
-                                            const uint32_t hi, const TileDesc* n1 = nullptr) {
-  static_assert((kZTile + 15 + kHaloMax + 64 + 127) / 128 <= kRows, "image rows: tile + halo + zero pad");
-  const uint32_t t1 = sd.first_tile + sd.n_tiles;
-  const uint64_t after = td.span_off + td.len;
-  const uint64_t rem = sd.len > after ? sd.len - after : 0;
-  const uint32_t halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
-  const uint32_t img_end = hi + halo;
-  const bool next_ok = n1 && halo && t + 1 < t1 && n1->span_off == after && n1->len >= halo;
-  const bool near = kHaloMax <= 64u && next_ok;  // one byte per lane
-  const bool far = kHaloMax > 64u && next_ok;    // phase 3: up to 1 KiB, 16-byte words
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  uint32_t hb = 0;
-  u32x4 hv[2] = {};
+// A tile's words in registers between stage_issue (loads in flight) and stage_finish (LDS
+// stores): the count pass issues the next tile's loads right after staging the current one,
+// so their memory latency passes during the current tile's walk.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kZLoads = (int)(kZTile / 16 / 64);
+struct StagePre {
+  u32x4 v[kZLoads];
+  u32x4 hv[2];
+  uint32_t hb;
+};
+template <uint32_t kHaloMax = kZHalo>
+struct StageGeom {
+  uint32_t t1, halo, img_end;
+  uint64_t after;
+  bool near, far;
+  __device__ __forceinline__ StageGeom(const TileDesc& td, const SpanDesc& sd, uint32_t t, uint32_t hi,
+                                       const TileDesc* n1) {
+    t1 = sd.first_tile + sd.n_tiles;
+    after = td.span_off + td.len;
+    const uint64_t rem = sd.len > after ? sd.len - after : 0;
+    halo = rem < (uint64_t)kHaloMax ? (uint32_t)rem : kHaloMax;
+    img_end = hi + halo;
+    const bool next_ok = n1 && halo && t + 1 < t1 && n1->span_off == after && n1->len >= halo;
+    near = kHaloMax <= 64u && next_ok;  // one byte per lane
+    far = kHaloMax > 64u && next_ok;    // phase 3: up to 1 KiB, 16-byte words
+  }
+};
+// Every lane issues its 8 loads (and its halo byte / words) -- the tile is at most 512 x 16 B.
+template <uint32_t kHaloMax = kZHalo>
+__device__ __forceinline__ void stage_issue(const TileDesc& td, const SpanDesc& sd, const uint32_t t, const uint32_t lane,
+                                            const uint32_t hi, const TileDesc* n1, StagePre& P) {
   static_assert(kHaloMax <= 64u * 16u * 2u - 32u, "halo words: two per lane");
+  const StageGeom<kHaloMax> G(td, sd, t, hi, n1);
+  const uint32_t words = (hi + 15) >> 4;
+  const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
+#pragma unroll
+  for (int i = 0; i < kZLoads; ++i) {  // branch-free: lanes past the tile re-read its last word
+    const uint32_t w = lane + 64u * (uint32_t)i;
+    P.v[i] = src[w < words ? w : words - 1u];
+  }
+  P.hb = 0;
+  if (G.near && lane < G.halo) P.hb = gp(n1->abase)[n1->delta + lane];
+  if (G.far) {
+    const uint32_t nw = (n1->delta + G.halo + 15u) >> 4;
+    const CLG_GLOBAL u32x4* src1 = gp(reinterpret_cast<const u32x4*>(n1->abase));
+    P.hv[0] = lane < nw ? src1[lane] : u32x4{0, 0, 0, 0};
+    P.hv[1] = lane + 64u < nw ? src1[lane + 64u] : u32x4{0, 0, 0, 0};
+  }
+}
+
+// Stage tile t into the padded row layout: the tile (16-byte loads, all in flight before
+// any LDS store), a halo of the span's next bytes, a zero pad, then every row's pad dwords.
+// kHaloMax bytes of halo (kZHalo for count / emit; phase 3 stages more so that whole
+// Serializable streams near the tile end are in LDS); kRows rows of image.  n1: the next
+// tile's descriptor when the caller has it.  If that tile continues the span and holds the
+// whole halo (every tile but a span's last two, normally), the halo bytes are loaded
+// together with the tile, so staging costs one memory latency; otherwise the halo is found
+// by walking the span's tiles.  P: the words stage_issue loaded (same tile, same n1).
+template <uint32_t kHaloMax = kZHalo, uint32_t kRows = kZRows>
+__device__ __forceinline__ void stage_finish(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
+                                             const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
+                                             const uint32_t hi, const TileDesc* n1, const StagePre& P) {
+  static_assert((kZTile + 15 + kHaloMax + 64 + 127) / 128 <= kRows, "image rows: tile + halo + zero pad");
+  const StageGeom<kHaloMax> G(td, sd, t, hi, n1);
+  const uint32_t t1 = G.t1, halo = G.halo, img_end = G.img_end;
+  const uint64_t after = G.after;
+  const bool near = G.near, far = G.far;
+  const uint32_t hb = P.hb;
+  const u32x4* hv = P.hv;
   {
-    // every lane issues its 8 loads (and its halo byte) before any LDS store (the tile is at
-    // most 512 x 16 B)
     const uint32_t words = (hi + 15) >> 4;
-    const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(td.abase));
-    constexpr int kLoads = (int)(kZTile / 16 / 64);
-    u32x4 v[kLoads];
 #pragma unroll
-    for (int i = 0; i < kLoads; ++i) {  // branch-free: lanes past the tile re-read its last word
-      const uint32_t w = lane + 64u * (uint32_t)i;
-      v[i] = src[w < words ? w : words - 1u];
-    }
-    if (near && lane < halo) hb = gp(n1->abase)[n1->delta + lane];
-    if (far) {
-      const uint32_t nw = (n1->delta + halo + 15u) >> 4;
-      const CLG_GLOBAL u32x4* src1 = gp(reinterpret_cast<const u32x4*>(n1->abase));
-      if (lane < nw) hv[0] = src1[lane];
-      if (lane + 64u < nw) hv[1] = src1[lane + 64u];
-    }
-#pragma unroll
-    for (int i = 0; i < kLoads; ++i) {
+    for (int i = 0; i < kZLoads; ++i) {
       const uint32_t w = lane + 64u * (uint32_t)i;
       if (w < words) {
         uint32_t* d = s_img + (w >> 3) * kZPitch + 4u * (w & 7u);
-        d[0] = v[i].x;
-        d[1] = v[i].y;
-        d[2] = v[i].z;
-        d[3] = v[i].w;
+        d[0] = P.v[i].x;
+        d[1] = P.v[i].y;
+        d[2] = P.v[i].z;
+        d[3] = P.v[i].w;
       }
     }
   }
@@ -650,6 +695,16 @@ __device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& 
     s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
   }
   __syncthreads();
+}
+
+
+template <uint32_t kHaloMax = kZHalo, uint32_t kRows = kZRows>
+__device__ __forceinline__ void stage_image(const TileDesc& td, const SpanDesc& sd, const uint32_t t,
+                                            const TileDesc* __restrict__ tiles, uint32_t* s_img, const uint32_t lane,
+                                            const uint32_t hi, const TileDesc* n1 = nullptr) {
+  StagePre P;
+  stage_issue<kHaloMax>(td, sd, t, lane, hi, n1, P);
+  stage_finish<kHaloMax, kRows>(td, sd, t, tiles, s_img, lane, hi, n1, P);
 }
 
 // ---------------------------------------------------------------------------------
@@ -886,7 +941,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
                                            const uint32_t lane, uint32_t* x_out, const JL& jl,
                                            const TileDesc* __restrict__ tiles = nullptr,
-                                           const SpecR* walked = nullptr) {
+                                           const SpecR* walked = nullptr, uint64_t* cnt_out = nullptr) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
@@ -983,6 +1038,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
     wide += __shfl_xor(wide, off);
   }
   if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(rec, wide);
+  if (cnt_out) *cnt_out = pack_cnt(rec, wide);
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   u64x2 out_bits;
   out_bits.x = r.bm.lo;
@@ -1156,22 +1212,31 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
   return JL{bits, rank, len, lm};
 }
 
+// Emit's LDS: the image, record starts of the window by output position and the
+// Serializable table.  With Serializable tables (J: the batches with many wide records) the
+// entries are 32-bit and, reused in place, also hold the window's wide records (position |
+// window index << 16) for a compacted wide pass; without, 16-bit entries and wide records
+// decoded inline (same 2 KiB of LDS either way).
 template <bool J>
-__global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                                    FusedCtl ctl, DecodeOut out) {
-  __shared__ uint32_t s_img[kZImgDw];
-  // record starts of the window by output position.  With Serializable tables (J: the
-  // batches with many wide records) the entries are 32-bit and, reused in place, also hold
-  // the window's wide records (position | window index << 16) for a compacted wide pass;
-  // without, 16-bit entries and wide records decoded inline (same 2 KiB of LDS either way).
+struct EmitLds {
   using PosT = typename std::conditional<J, uint32_t, uint16_t>::type;
-  constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
-  __shared__ PosT s_pos[kWin];
-  __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  const uint32_t t = blockIdx.x, lane = threadIdx.x;
-  if (ld_agent32(ctl.abort)) return;
+  static constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
+  uint32_t img[kZImgDw];
+  PosT pos[kWin];
+  uint32_t j[J ? 2 * kZJBitsDw + kZJCap : 1];
+};
+
+// Pass 3 for tile t whose first record is record `base` of the batch (wide<<31 | records).
+template <bool J>
+__device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                          const FusedCtl& ctl, const DecodeOut& out, const uint32_t t,
+                                          const uint32_t lane, const uint64_t base, EmitLds<J>& L) {
+  using PosT = typename EmitLds<J>::PosT;
+  constexpr uint32_t kWin = EmitLds<J>::kWin;
+  uint32_t* const s_img = L.img;
+  PosT* const s_pos = L.pos;
+  uint32_t* const s_j = L.j;
   const TileDesc td = tiles[t];
-  if (ctl.skip_bad && gp(ctl.span_bad)[td.span]) return;  // the robust output fills this span
   const TileDesc n1 = tiles[t + 1 < ctl.n_tiles ? t + 1 : t];  // halo source, loaded beside td
   const SpanDesc sd = spans[td.span];
   const uint32_t lo = td.delta, hi = td.delta + td.len;
@@ -1180,7 +1245,6 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
   if (lane * kZRegion >= hi) bits = u64x2{0, 0};  // past the tile (the lane path of small spans skips them)
-  const uint64_t base = gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock];
   JLPre pre{};
   if (J) pre = jl_prefetch(ctl, t, lane);
   stage_image(td, sd, t, tiles, s_img, lane, hi, &n1);
@@ -1339,6 +1403,16 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   }
 }
 
+template <bool J>
+__global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                    FusedCtl ctl, DecodeOut out) {
+  __shared__ EmitLds<J> L;
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  if (ld_agent32(ctl.abort)) return;
+  if (ctl.skip_bad && gp(ctl.span_bad)[tiles[t].span]) return;  // the robust output fills this span
+  emit_tile<J>(tiles, spans, ctl, out, t, lane, gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock], L);
+}
+
 // Pass 0 (batches holding them): small whole spans, a lane each.  A batch of many small logs
 // (config 4: 65 536 subpartition logs of 320 bytes) gives one tile per span, and a wave spent
 // on a 320-byte tile costs as much as one on 8 KiB.  Lane i of block b takes tile 64 b + i
@@ -1467,7 +1541,9 @@ template <bool J>
 __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                  const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_j, uint32_t lane,
                                                  uint32_t t, const ZTile& z, uint64_t xs, uint32_t must_exit,
-                                                 const SpecR* walked, uint64_t* x) {
+                                                 const SpecR* walked, uint64_t* x, uint64_t* cnt_out = nullptr,
+                                                 StagePre* pf = nullptr, bool pf_ready = false,
+                                                 uint32_t pf_next = 0xFFFFFFFFu) {
   constexpr bool kLm = CLG_COUNT_LM != 0;
   const uint32_t nt = ctl.n_tiles;
   const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
@@ -1476,12 +1552,21 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
   JL jl{nullptr, nullptr, nullptr};
   JLPre pre{};
   if (J) pre = jl_prefetch(ctl, t, lane);
-  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
+  if (pf) {  // staged from registers; then tile pf_next's loads go out, to land during this walk
+    if (!pf_ready) stage_issue(z.td, z.sd, t, lane, z.hi, &n1, *pf);
+    stage_finish(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1, *pf);
+    if (pf_next < nt) {
+      const TileDesc td2 = tiles[pf_next], n2 = tiles[pf_next + 1 < nt ? pf_next + 1 : pf_next];
+      stage_issue(td2, spans[td2.span], pf_next, lane, td2.delta + td2.len, &n2, *pf);
+    }
+  } else {
+    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
+  }
   if (J && kLm) build_lm(z, s_img, s_j, lane);
   if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
   else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
   uint32_t x_true;
-  const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked);
+  const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked, cnt_out);
   *x = z.td.span_off + (x_true - z.lo);
   return why;
 }
@@ -1588,6 +1673,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   uint64_t x_prev = 0;  // previous tile's exit, span offset
   uint32_t bad_span = 0xFFFFFFFFu;  // a span whose chain went wrong: its later tiles are skipped
   uint32_t sus_span = 0xFFFFFFFFu;  // the chunk's first span, entered at a published exit
+  // without tables (88-93 VGPRs) the next tile's loads are issued during this tile's walk:
+  // its 32 VGPRs fit below 128, the 4 waves per SIMD the LDS allows anyway
+  constexpr bool kPre = !J && CLG_COUNT_PREFETCH != 0;
+  StagePre pf;
+  uint32_t pf_t = 0xFFFFFFFFu;  // the tile whose loads pf holds
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
@@ -1617,8 +1707,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
     uint64_t x;
+    const uint32_t nxt = t + 1 < t1 ? t + 1 : 0xFFFFFFFFu;
     const uint32_t why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, t + 1 == t1 ? x_pub : kZCanon,
-                                         reuse ? &sp_last : nullptr, &x);
+                                         reuse ? &sp_last : nullptr, &x, nullptr, kPre ? &pf : nullptr, pf_t == t, nxt);
+    pf_t = nxt;
     if (why == 0u || why == 3u) {
       x_prev = x;
       if (lane == 0) {
@@ -1686,6 +1778,89 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
     if (tiles[f].span != span) break;
     if (gp(ctl.rep_flag)[c]) serve_chunk<J>(tiles, spans, ctl, s_img, s_j, lane, f, ce, &walk_end);
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Small batches in one launch (config 1: an epoch of 44 logs, 73 KB, where the three-pass
+// sequence's ~15 queue operations cost more than the decode).  One wave per span: it counts
+// the span's tiles in order (count_staged: the first tile enters at the span start, each next
+// one at its predecessor's exit), publishes the span's counts, sums the counts of every
+// earlier span (look-back: earlier blocks were dispatched first and never wait on later ones,
+// so the waits end), then emits the tiles (emit_tile) from that base.  A span whose chain
+// goes wrong -- an invalid record, a Serializable record (no tables here) -- flags the batch
+// and the host decodes it the usual way, which classifies the error; a wait past
+// kZSpinLimit flags it too.  res: see launch_decode_small (kernels.h).
+// ---------------------------------------------------------------------------------
+constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
+                                                     const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
+                                                     DecodeOut out, uint64_t* agg, uint64_t* res) {
+  __shared__ EmitLds<false> L;  // its image serves the count pass too
+  __shared__ uint64_t s_cnt[kZSmallTiles];
+  const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  const SpanDesc sd = spans[s];
+  uint64_t mine = 0, x = 0;
+  bool bad = sd.n_tiles > kZSmallTiles;
+  for (uint32_t k = 0; k < sd.n_tiles && !bad; ++k) {
+    const uint32_t t = sd.first_tile + k;
+    const ZTile z = ztile(tiles, spans, t, lane);
+    uint64_t c = 0;
+    const uint32_t why = count_staged<false>(tiles, spans, ctl, L.img, nullptr, lane, t, z, k ? x : z.td.span_off,
+                                             kZCanon, nullptr, &x, &c);
+    bad = why != 0u;
+    if (lane == 0) s_cnt[k] = c;
+    mine += c;
+    __syncthreads();  // the image is reused
+  }
+  if (lane == 0) st_agent(&agg[s], kZAggSet | (bad ? kZAggBad : 0ull) | mine);
+  // look-back: every earlier span's counts
+  uint64_t pre = 0;
+  bool any_bad = bad;
+  for (uint32_t j0 = 0; j0 < s && !any_bad; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    uint64_t v = 0;
+    if (j < s) {
+      uint32_t nb = 1;
+      const uint64_t w0 = __builtin_amdgcn_s_memtime();
+      while (!((v = ld_agent(&agg[j])) & kZAggSet))
+        if (!backoff(nb, w0)) {
+          v = kZAggSet | kZAggBad;
+          break;
+        }
+    }
+    any_bad = __any((v & kZAggBad) != 0ull);
+    uint64_t c = v & kZAggCnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    pre += c;
+  }
+  if (any_bad) {
+    if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  uint64_t b = pre;
+  for (uint32_t k = 0; k < sd.n_tiles; ++k) {
+    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + k, lane, b, L);
+    b += s_cnt[k];
+    __syncthreads();
+  }
+  if (lane == 0) {
+    res[3 + s] = pre;
+    if (s + 1 == n_spans) {
+      res[0] = b & ((1ull << 31) - 1);
+      res[1] = b >> 31;
+    }
+  }
+}
+
+int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* res, void* stream) {
+  if (!n_spans) return CLG_OK;
+  ctl.n_tiles = n_tiles;
+  hipLaunchKernelGGL(k_decode_small, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_spans, ctl,
+                     out, agg, res);
+  return launch_status(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------------
@@ -1954,20 +2129,26 @@ int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
 }
 
 uint32_t decode_count_grid(bool jser, uint32_t n_tiles) {
-  static int resident[2] = {0, 0};  // blocks the device keeps resident for the count kernel
+  constexpr int kMaxDev = 64;
+  static int resident[kMaxDev][2] = {};  // per device: blocks the device keeps resident for the count kernel
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
   const int j = jser ? 1 : 0;
-  if (!resident[j]) {
-    int dev = 0, per_cu = 0, cus = 0;
+  if (!resident[dev][j]) {
+    int per_cu = 0, cus = 0;
     const hipError_t oe = j ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<true>, 64, 0)
                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_count<false>, 64, 0);
-    if (hipGetDevice(&dev) != hipSuccess || oe != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+    if (oe != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        per_cu < 1 || cus < 1)
       return 0;
-    const char* m = getenv("CLONOS_COUNT_MARGIN");  // developer switch: blocks per CU left free (default 1)
-    const int margin = m ? atoi(m) : 1;
-    resident[j] = (per_cu > margin ? per_cu - margin : 1) * cus;
+    // developer switch: blocks per CU left free (default 1), clamped to [0, per_cu - 1] -- a
+    // grid larger than the device keeps resident would leave waiting blocks unscheduled
+    const char* m = getenv("CLONOS_COUNT_MARGIN");
+    int margin = m ? atoi(m) : 1;
+    margin = margin < 0 ? 0 : (margin > per_cu - 1 ? per_cu - 1 : margin);
+    resident[dev][j] = (per_cu - margin) * cus;
   }
-  return n_tiles < (uint32_t)resident[j] ? n_tiles : (uint32_t)resident[j];
+  return n_tiles < (uint32_t)resident[dev][j] ? n_tiles : (uint32_t)resident[dev][j];
 }
 
 // Checked launch: a configuration error names its kernel and grid (stderr) and is returned.

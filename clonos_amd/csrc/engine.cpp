@@ -485,6 +485,7 @@ struct clg_engine {
   PinBuf h_plan;  // decode plans (upload_plan)
   DevBuf d_plan;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
+  bool small_decode = true;  // CLG_F_NO_SMALL_DECODE / CLONOS_SMALL=0: no single-launch small batches
 
   // timing
   std::map<std::string, Stat> stats;
@@ -1557,6 +1558,130 @@ struct clg_engine {
     if (r.pa) timings.push_back(PendingTiming{"decode_pipeline", r.pa, r.pb, log_bytes + 13 * nrec + 25 * nwide});
     return finish_out(out, nrec, nwide);
   }
+  // ---------------------------------------------------------------- small batches
+  // A batch of at most kSmallBytes in spans of at most kZSmallTiles tiles, without
+  // Serializable tables, decodes in ONE launch (k_decode_small, decode_fused.hip): the plan
+  // goes up in one copy, and the kernel writes host outputs straight into pinned memory, so
+  // the call is copy + launch + one wait -- the three-pass sequence is about 15 queue
+  // operations, which for config 1 (44 logs, 73 KB) cost more than the decode.  A span that
+  // goes wrong sends the batch down the usual path.  CLG_F_NO_SMALL_DECODE (or CLONOS_SMALL=0,
+  // a developer switch) turns it off.
+  static constexpr uint64_t kSmallBytes = 1u << 20;
+  static constexpr uint32_t kSmallSpans = 4096;
+  static constexpr uint64_t kSmallHostOut = 32u << 20;  // pinned output bytes at most (cap-sized)
+  PinBuf h_small_out, h_small_res;
+  DevBuf d_small;
+  bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
+    if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
+        p.only >= 0)
+      return false;
+    if (out->out_kind != CLG_MEM_DEVICE && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
+    for (const auto& sd : p.spans)
+      if (sd.n_tiles > clg::kZSmallTiles) return false;
+    return true;
+  }
+  // The plan's device-planned runs as host-built tiles (k_expand_tiles' rule, on the host).
+  void host_tiles(DecodePlan& p) {
+    if (p.runs.empty()) return;
+    const uint32_t U = p.unit, Cb = C();
+    p.tiles.resize(p.n_tiles);
+    for (const auto& r : p.runs) {
+      const uint32_t w0 = r.phys / U, w1 = (r.phys + r.len - 1) / U;
+      for (uint32_t w = w0; w <= w1; ++w) {
+        const uint32_t s0 = std::max(w * U, r.phys), e1 = std::min((w + 1) * U, r.phys + r.len);
+        const uint32_t si = s0 / Cb, so = s0 % Cb;
+        p.tiles[r.first + (w - w0)] = clg::TileDesc{seg_addr(segtab_at(p, r.segtab_off + si)) + (so & ~15u), so & 15u,
+                                                    e1 - s0, uint32_t(r.dst), 0, uint64_t(s0 - r.phys)};
+      }
+    }
+    p.runs.clear();
+    p.segtab.clear();
+    p.unit = 0;
+  }
+  static uint32_t segtab_at(const DecodePlan& p, uint64_t i) { return p.segtab[size_t(i)]; }
+  int run_small(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted) {
+    HostTimer ht(this, "host_decode_small");
+    *aborted = false;
+    reset_result(out);
+    host_tiles(p);
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    PlanLayout L;
+    CHK(stage_plan(p, d_ztiles, &L));
+    // outputs: the caller's device arrays, or pinned host memory the kernel writes directly
+    clg::DecodeOut o{};
+    const bool host = out->out_kind != CLG_MEM_DEVICE;
+    const uint64_t cap = std::max<uint64_t>(1, out->cap), wcap = std::max<uint64_t>(1, out->wcap);
+    uint64_t at[10] = {0};
+    const uint64_t sz[9] = {cap * 4, cap, cap * 8, wcap * 4, wcap * 4, wcap * 8, wcap * 4, wcap * 4, wcap};
+    for (int i = 0; i < 9; ++i) at[i + 1] = (at[i] + sz[i] + 15) & ~uint64_t(15);
+    if (host) {
+      CHK(h_small_out.ensure(at[9] + 16));
+      uint8_t* hb = h_small_out.as<uint8_t>();
+      o = clg::DecodeOut{reinterpret_cast<uint32_t*>(hb + at[0]), hb + at[1], reinterpret_cast<int64_t*>(hb + at[2]),
+                         reinterpret_cast<uint32_t*>(hb + at[3]), reinterpret_cast<int32_t*>(hb + at[4]),
+                         reinterpret_cast<int64_t*>(hb + at[5]), reinterpret_cast<uint32_t*>(hb + at[6]),
+                         reinterpret_cast<uint32_t*>(hb + at[7]), hb + at[8], out->cap, out->wcap};
+    } else {
+      o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
+                         out->w_var_len, out->w_sub, out->cap, out->wcap};
+    }
+    // scratch: per-tile counts and record-start bitmaps, per-span look-back words
+    CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
+    CHK(d_small.ensure((size_t(nt) + ns) * 8));
+    CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
+    uint64_t* res = h_small_res.as<uint64_t>();
+    res[0] = res[1] = res[2] = 0;
+    uint64_t* cnt = d_small.as<uint64_t>();
+    uint64_t* agg = cnt + nt;
+    clg::FusedCtl ctl{};
+    ctl.cnt = cnt;
+    ctl.bits = d_zbits.as<uint64_t>();
+    ctl.n_tiles = nt;
+    ctl.warm = spec_warm(false);
+    HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemsetAsync(agg, 0, size_t(ns) * 8, stream));
+    const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (timing) {
+      ea = get_event();
+      eb = get_event();
+      HIPCHK(hipEventRecord(ea, stream));
+    }
+    CHK(clg::launch_decode_small(reinterpret_cast<const clg::TileDesc*>(d_plan.p), nt,
+                                 reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
+                                 agg, res, stream));
+    if (timing) HIPCHK(hipEventRecord(eb, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    if (res[2]) {
+      if (timing) ev_pool.insert(ev_pool.end(), {ea, eb});
+      *aborted = true;
+      return CLG_OK;
+    }
+    constexpr uint64_t kRecMask = (1ull << 31) - 1;
+    const uint64_t nrec = res[0], nwide = res[1];
+    if (span_rec_base) {
+      for (uint32_t s = 0; s < ns; ++s) span_rec_base[s] = res[3 + s] & kRecMask;
+      span_rec_base[ns] = nrec;
+    }
+    if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    out->n_rec = nrec;
+    out->n_wide = nwide;
+    if (host) {
+      const uint64_t r = std::min(nrec, out->cap), w = std::min(nwide, out->wcap);
+      const uint8_t* hb = h_small_out.as<uint8_t>();
+      void* dst[9] = {out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off, out->w_var_len,
+                      out->w_sub};
+      const uint64_t n[9] = {r * 4, r, r * 8, w * 4, w * 4, w * 8, w * 4, w * 4, w};
+      for (int i = 0; i < 9; ++i)
+        if (n[i]) memcpy(dst[i], hb + at[i], n[i]);
+    }
+    if (nrec > out->cap || nwide > out->wcap)
+      return fail(CLG_E_CAPACITY, "decode produced %llu records / %llu wide rows, capacity %llu / %llu",
+                  (unsigned long long)nrec, (unsigned long long)nwide, (unsigned long long)out->cap,
+                  (unsigned long long)out->wcap);
+    return CLG_OK;
+  }
+
   // Decode dispatcher: fused single pass first, robust pipeline on abort.  `build(plan,
   // tile_bytes)` fills a plan for the given tile geometry.
   template <class Build>
@@ -1571,6 +1696,11 @@ struct clg_engine {
         build(pf, clg::kZTile);
       }
       bool aborted = false, need_jser = false;
+      if (small_ok(pf, log_bytes, out)) {
+        CHK(run_small(pf, log_bytes, out, span_rec_base, &aborted));
+        if (!aborted) return CLG_OK;
+        stats["decode_small_fallback"].launches++;
+      }
       CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, jser_hint, &need_jser));
       if (!aborted) return CLG_OK;
       return after_abort(pf, build, log_bytes, out, span_rec_base, need_jser);
@@ -2005,6 +2135,7 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->cfg = *cfg;
   const char* dm = getenv("CLONOS_DECODE");
   e->fused_decode = !(cfg->flags & CLG_F_ROBUST_DECODE) && !(dm && !strcmp(dm, "robust"));
+  e->small_decode = !(cfg->flags & CLG_F_NO_SMALL_DECODE) && !(getenv("CLONOS_SMALL") && atoi(getenv("CLONOS_SMALL")) == 0);
   if (const char* ja = getenv("CLONOS_JSER_ARENA"))  // initial spill arena bytes (tests: force its growth)
     e->jarena_bytes = std::max<size_t>(256, size_t(strtoull(ja, nullptr, 0)));
   HIPCHK(hipSetDevice(cfg->device));

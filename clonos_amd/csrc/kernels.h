@@ -237,6 +237,16 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
 // per tile); CLG_E_DEVICE as 0.
 uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 
+// Small batches in one launch (k_decode_small): one wave per span counts the span's tiles,
+// publishes its counts, sums every earlier span's (look-back), emits.  Spans of at most
+// kZSmallTiles tiles, batches without Serializable tables.  Results go to `res` (host-mapped
+// pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any span failed
+// (the host then decodes the batch the usual way), res[3 + s] span s's first record.  agg:
+// n_spans zeroed words.
+constexpr uint32_t kZSmallTiles = 8;
+int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* res, void* stream);
+
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
 // segment.  Pieces are produced per slice request and split at segment boundaries.

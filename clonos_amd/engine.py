@@ -120,13 +120,14 @@ class Engine:
                  sharing_depth: int = _lib.CLG_FULL_SHARING, timing: bool = False, decode: str = "auto",
                  async_slice: bool = False, ifl_segment_bytes: Optional[int] = None,
                  ifl_pool_segments: Optional[int] = None, host_tail_bytes: Optional[int] = None):
-        """decode: "auto" = fast three-pass decode, robust multi-pass pipeline on abort;
-        "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
+        """decode: "auto" = single-launch decode for small batches, else the fast three-pass
+        decode, robust multi-pass pipeline on abort; "three_pass" = no single-launch path
+        (CLG_F_NO_SMALL_DECODE); "robust" = the robust pipeline only (CLG_F_ROBUST_DECODE).  async_slice: device-output
         slices return once queued on the gather stream (CLG_F_ASYNC_SLICE); sync() before
         reading them.  ifl_*: the in-flight log's own pool (default: the same geometry as the
         determinant pool)."""
-        if decode not in ("auto", "robust"):
-            raise ValueError(f"decode must be 'auto' or 'robust', not {decode!r}")
+        if decode not in ("auto", "three_pass", "robust"):
+            raise ValueError(f"decode must be 'auto', 'three_pass' or 'robust', not {decode!r}")
         cfg = _lib.Config()
         lib.clg_config_default(C.byref(cfg))
         cfg.segment_bytes = segment_bytes
@@ -138,6 +139,7 @@ class Engine:
         cfg.ifl_segment_bytes = ifl_segment_bytes if ifl_segment_bytes is not None else segment_bytes
         cfg.ifl_pool_segments = ifl_pool_segments if ifl_pool_segments is not None else pool_segments
         cfg.flags = ((_lib.CLG_F_TIMING if timing else 0) | (_lib.CLG_F_ROBUST_DECODE if decode == "robust" else 0)
+                     | (_lib.CLG_F_NO_SMALL_DECODE if decode == "three_pass" else 0)
                      | (_lib.CLG_F_ASYNC_SLICE if async_slice else 0))
         h = C.c_void_p()
         check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))

@@ -105,6 +105,8 @@ typedef struct clg_config {
 #define CLG_F_TIMING 1u        /* record per-kernel HIP event timings (clg_kernel_stats) */
 #define CLG_F_ROBUST_DECODE 2u /* skip the fast three-pass decode; always use the robust
                                   multi-pass pipeline (the fallback the fused kernel aborts to) */
+#define CLG_F_NO_SMALL_DECODE 8u /* batches up to 1 MiB also take the three-pass decode, not the
+                                   single-launch small-batch one (tests of the three-pass path) */
 #define CLG_F_ASYNC_SLICE 4u   /* slices into device memory (clg_slice_batch, CLG_MEM_DEVICE)
                                   return once queued on the engine's gather stream and overlap
                                   later decodes; the output is ready after clg_sync or once

@@ -24,7 +24,7 @@ def fell_back(eng) -> bool:
 
 @pytest.fixture(params=[256, 16384])
 def feng(request):
-    e = Engine(segment_bytes=request.param, pool_segments=(1 << 26) // request.param, timing=True)
+    e = Engine(segment_bytes=request.param, pool_segments=(1 << 26) // request.param, timing=True, decode="three_pass")
     yield e
     e.close()
 

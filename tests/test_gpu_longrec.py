@@ -40,7 +40,7 @@ def _join(spans):
 
 @pytest.fixture
 def leng():
-    e = Engine(segment_bytes=16384, pool_segments=1 << 14, timing=True)
+    e = Engine(segment_bytes=16384, pool_segments=1 << 14, timing=True, decode="three_pass")
     yield e
     e.close()
 
@@ -240,7 +240,7 @@ def test_span_fallback_error_equals_robust():
         blob += b
     errs = []
     for mode in ("auto", "robust"):
-        e = Engine(segment_bytes=16384, pool_segments=1 << 13, timing=True, decode=mode)
+        e = Engine(segment_bytes=16384, pool_segments=1 << 13, timing=True, decode=mode if mode == "robust" else "three_pass")
         try:
             with pytest.raises(ClonosError) as ei:
                 e.decode_host(blob, sp)

@@ -1,0 +1,146 @@
+"""GPU: the single-launch small-batch decode (k_decode_small: one wave per span, look-back over
+the earlier spans' counts, host outputs written straight into pinned memory) == the CPU
+oracle's decodeNext loop, bit-exact; batches it does not finish (an invalid record, a
+Serializable record) fall back to the three-pass path with the same result."""
+import numpy as np
+import pytest
+
+import _oracle as O
+from clonos_amd import ClonosError, Engine, synth
+from test_gpu_decode import assert_span_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _eng(**kw):
+    return Engine(segment_bytes=kw.pop("segment_bytes", 16384), pool_segments=4096, timing=True, **kw)
+
+
+def _launches(eng, name):
+    return eng.kernel_stats().get(name, {}).get("launches", 0)
+
+
+def test_config1_decode_takes_the_small_path():
+    rng = np.random.default_rng(synth.SEED_CONFIG1)
+    graph, data = synth.config1_job(rng)
+    with _eng(sharing_depth=1) as eng:
+        logs = {lid: eng.open_log(lid) for lid in data}
+        for lid, b in data.items():
+            logs[lid].appendDeterminant(b, 0)
+        lids = list(data)
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        assert _launches(eng, "decode_small") == 1 and _launches(eng, "decode_small_fallback") == 0
+        assert _launches(eng, "decode_count") == 0
+        for s, l in enumerate(lids):
+            assert_span_equal(dec, s, data[l])
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("seg", [256, 16384])
+def test_small_random_spans_multi_tile(seed, seg):
+    """Spans of 0 .. 8 tiles (up to ~64 KB), every non-Serializable tag, logs across segments."""
+    rng = np.random.default_rng(0x5A11 + seed)
+    with _eng(segment_bytes=seg) as eng:
+        from clonos_amd import CausalLogID
+        bufs, logs = [], []
+        for i in range(int(rng.integers(1, 60))):
+            n = int(rng.choice([0, 1, 5, 50, 400, 3000, 9000]))
+            b = synth.random_log(n, rng, allow_serializable=False)
+            if len(b) > 60000:
+                b = b[:0]
+            lg = eng.open_log(CausalLogID.main(i))
+            if b:
+                lg.appendDeterminant(b, 0)
+            bufs.append(b)
+            logs.append(lg)
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs(logs, [0] * len(logs))
+        assert _launches(eng, "decode_small") == 1 and _launches(eng, "decode_small_fallback") == 0
+        for s, b in enumerate(bufs):
+            assert_span_equal(dec, s, b)
+        assert dec.span_rec_base[-1] == dec.n_rec
+
+
+def test_small_host_input_spans():
+    rng = np.random.default_rng(3)
+    parts = [synth.random_log(int(rng.integers(0, 300)), rng, allow_serializable=False) for _ in range(200)]
+    blob, spans = b"", []
+    for p in parts:
+        blob += bytes(int(rng.integers(0, 17)))
+        spans.append((len(blob), len(p)))
+        blob += p
+    with _eng() as eng:
+        eng.kernel_stats_reset()
+        dec = eng.decode_host(blob, spans)
+        assert _launches(eng, "decode_small") == 1
+        for s, p in enumerate(parts):
+            assert_span_equal(dec, s, p)
+
+
+def test_small_error_falls_back_with_the_reference_error():
+    rng = np.random.default_rng(4)
+    good = [synth.random_log(200, rng, allow_serializable=False) for _ in range(10)]
+    bad = good[3][:37] + bytes([9]) + good[3][37:]  # tag 9 at a record start? (the oracle decides)
+    spans_b = good[:3] + [bad] + good[4:]
+    blob = b"".join(spans_b)
+    offs = np.cumsum([0] + [len(b) for b in spans_b])
+    with _eng() as eng:
+        eng.kernel_stats_reset()
+        try:
+            dec = eng.decode_host(blob, [(int(offs[i]), len(b)) for i, b in enumerate(spans_b)])
+            got = None
+        except ClonosError as e:
+            got = e.status
+        st, _, _, _ = O.decode(bad)
+        assert _launches(eng, "decode_small") == 1
+        if st != 0:
+            assert got == st and _launches(eng, "decode_small_fallback") == 1
+        else:
+            assert got is None
+            for s, b in enumerate(spans_b):
+                assert_span_equal(dec, s, b)
+
+
+def test_small_serializable_falls_back():
+    rng = np.random.default_rng(5)
+    buf = synth.random_log(500, rng, allow_serializable=True)
+    with _eng() as eng:
+        eng.kernel_stats_reset()
+        dec = eng.decode_host(buf)
+        assert_span_equal(dec, 0, buf)
+        if b"\x03\xac\xed\x00\x05" in buf:
+            assert _launches(eng, "decode_small_fallback") >= 1
+
+
+def test_small_device_outputs():
+    import torch
+    from clonos_amd import _lib, CausalLogID
+    rng = np.random.default_rng(6)
+    with _eng() as eng:
+        bufs = [synth.random_log(int(rng.integers(1, 800)), rng, allow_serializable=False) for _ in range(30)]
+        logs = []
+        for i, b in enumerate(bufs):
+            lg = eng.open_log(CausalLogID.main(i))
+            lg.appendDeterminant(b, 0)
+            logs.append(lg)
+        n_cap = sum(len(b) for b in bufs) // 2 + 1
+        dev = torch.device("cuda", 0)
+        o = [torch.empty(n_cap, dtype=t, device=dev) for t in (torch.int32, torch.uint8, torch.int64)]
+        ow = [torch.empty(n_cap, dtype=t, device=dev) for t in
+              (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
+        d = _lib.Decoded()
+        d.off, d.tag, d.v0 = [t.data_ptr() for t in o]
+        d.w_idx, d.w_rc, d.w_v1, d.w_var_off, d.w_var_len, d.w_sub = [t.data_ptr() for t in ow]
+        d.cap, d.wcap, d.out_kind = n_cap, n_cap, _lib.CLG_MEM_DEVICE
+        base = np.zeros(len(bufs) + 1, np.uint64)
+        eng.kernel_stats_reset()
+        eng.decode_logs_device(np.array([l.handle for l in logs], np.uint32), np.zeros(len(logs), np.int64), d, base)
+        assert _launches(eng, "decode_small") == 1
+        tag = o[1][:d.n_rec].cpu().numpy()
+        v0 = o[2][:d.n_rec].cpu().numpy()
+        for s, b in enumerate(bufs):
+            st, r, _, _ = O.decode(b)
+            lo, hi = int(base[s]), int(base[s + 1])
+            np.testing.assert_array_equal(tag[lo:hi], r["tag"])
+            np.testing.assert_array_equal(v0[lo:hi], r["v0"])

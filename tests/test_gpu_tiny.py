@@ -27,7 +27,7 @@ def _fixed_log(rng, nbytes):
     return out
 
 
-def _logs_decode(bufs, decode="auto"):
+def _logs_decode(bufs, decode="three_pass"):
     with Engine(segment_bytes=16384, pool_segments=len(bufs) + 64, timing=True, decode=decode) as eng:
         logs = []
         for v, b in enumerate(bufs):
@@ -84,7 +84,7 @@ def test_full_runs_of_small_spans():
     blob, _ = synth.build(np.zeros(n_spans * per, np.int64), [kd], {0: [rng.integers(0, 1 << 31, n_spans * per)]})
     L = per * 5
     spans = [(i * L, L) for i in range(n_spans)]
-    with Engine(segment_bytes=16384, pool_segments=64, timing=True) as eng:
+    with Engine(segment_bytes=16384, pool_segments=64, timing=True, decode="three_pass") as eng:
         dec = eng.decode_host(blob, spans)
         st = eng.kernel_stats()
     assert "decode_fallback" not in st and "decode_span_fallback" not in st
