@@ -57,8 +57,13 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_COUNT_LM
 #define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
 #endif
+#ifndef CLG_WARM_PRED
+#define CLG_WARM_PRED 0  // 1: the speculative warm-up as straight-line predicated steps (kZWarmUnroll per test)
+#endif
+constexpr int kZWarmUnroll = 4;
 #ifndef CLG_COUNT_PREFETCH
-#define CLG_COUNT_PREFETCH 1  // 1: the count pass without tables issues the next tile's loads during a walk
+#define CLG_COUNT_PREFETCH 0  // 1: the count pass without tables issues the next tile's loads during a walk
+                              // (measured: config-2 count 0.185 against 0.175 ms without; 127 VGPRs)
 #endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
@@ -336,10 +341,22 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
   {
     constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
     constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
+#if CLG_WARM_PRED
+    // straight-line steps, lanes past rs standing still: no branch per step, one wave-wide
+    // test per kZWarmUnroll steps
+    while (__any(q < rs)) {
+#pragma unroll
+      for (int k = 0; k < kZWarmUnroll; ++k) {
+        const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
+        q = q < rs ? q + (L > 1u ? L : 1u) : q;
+      }
+    }
+#else
     while (q < rs) {
       const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
       q += L > 1u ? L : 1u;
     }
+#endif
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
@@ -690,11 +707,13 @@ __device__ __forceinline__ void stage_finish(const TileDesc& td, const SpanDesc&
     bb[rb(img_end + lane)] = 0;  // zero pad (64 bytes) so 16-byte reads near the end are defined
   }
   __syncthreads();
-  for (uint32_t i = lane; i < (kRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
-    const uint32_t row = i / kZPad, j = i - row * kZPad;
-    s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
+  if constexpr (kZPad > 0) {
+    for (uint32_t i = lane; i < (kRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
+      const uint32_t row = i / kZPad, j = i - row * kZPad;
+      s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
+    }
+    __syncthreads();
   }
-  __syncthreads();
 }
 
 
@@ -747,11 +766,21 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
   const bool on = z.rs < z.re;
   const uint32_t r0 = lane * kZRegion;
   uint32_t c[kZRowDw];
-  // TimerTrigger / SourceCheckpoint bytes: word h, bit 32 s + 8 b + k <-> byte 64 h + 32 s + 4 k + b
+  // TimerTrigger / SourceCheckpoint bytes: word h, bit 32 s + 8 b + k <-> dword 16 h + 8 s + k of
+  // the lane's set, byte b
   uint64_t cw0 = 0, cw1 = 0;
+  // The lane's dwords: its row (dword j of row `lane`), or without row pads (pitch 32, where a
+  // row-per-lane read puts all 32 lanes of a group on one bank) dword 64 j + lane of the tile,
+  // so the lanes of a read touch 64 consecutive dwords.
+  constexpr bool kCols = kZPad == 0;
+  uint32_t onm = 0;  // (kCols) bit j: dword 64 j + lane's row meets the tile
 #pragma unroll
   for (uint32_t j = 0; j < kZRowDw; ++j) {
-    const uint32_t x = T[lane * kZPitch + j];
+    const uint32_t x = kCols ? T[64u * j + lane] : T[lane * kZPitch + j];
+    if (kCols) {
+      const uint32_t rr = 2u * j + (lane >> 5);  // the dword's row
+      onm |= (kZRegion * rr < z.hi && kZRegion * rr + kZRegion > z.lo ? 1u : 0u) << j;
+    }
     // 0xFF in every byte holding a tag (< 8): bytes with none of bits 3-7 set
     const uint32_t h = x & 0xF8F8F8F8u;
     const uint32_t zz = (h - 0x01010101u) & ~h & 0x80808080u;
@@ -760,7 +789,7 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
     const uint64_t f = (uint64_t)((__builtin_amdgcn_perm(kLmCand, 0u, x) & vm) >> (7u - (j & 7u))) << (32u * ((j >> 3) & 1u));
     if (j < 16u) cw0 |= f; else cw1 |= f;
   }
-  if (!on) cw0 = cw1 = 0;
+  if (!kCols && !on) cw0 = cw1 = 0;
   // the lanes' candidates into the list, in lane order
   const uint32_t nc = (uint32_t)(__popcll(cw0) + __popcll(cw1));
   uint32_t incl = nc;
@@ -777,9 +806,10 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
     while (m) {
       const uint32_t i = (uint32_t)__builtin_ctzll(m);
       m &= m - 1u;
-      const uint32_t a = r0 + 64u * hh + 32u * (i >> 5) + 4u * (i & 7u) + ((i >> 3) & 3u);
+      const uint32_t jj = 16u * hh + 8u * (i >> 5) + (i & 7u), b = (i >> 3) & 3u;  // the lane's dword, byte
+      const uint32_t a = kCols ? 4u * (64u * jj + lane) + b : r0 + 4u * jj + b;
       // (a row may run past the tile: those bytes are no candidates)
-      if (idx < kZLmList) list[idx] = a >= z.rs && a < z.re ? a : 0xFFFFu;
+      if (idx < kZLmList) list[idx] = (kCols ? a >= z.lo && a < z.hi : a >= z.rs && a < z.re) ? a : 0xFFFFu;
       ++idx;
     }
   }
@@ -791,7 +821,11 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
     list[k] = a | code << 16;
   }
   __syncthreads();  // every lane has read the image
-  if (on) {
+  if (kZPad == 0) {
+#pragma unroll
+    for (uint32_t j = 0; j < kZRowDw; ++j)
+      if ((onm >> j) & 1u) T[64u * j + lane] = c[j];
+  } else if (on) {
 #pragma unroll
     for (uint32_t j = 0; j < kZRowDw; ++j) T[lane * kZPitch + j] = c[j];
   }
@@ -1579,6 +1613,45 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
 // a long record) do not count: a run of long records a short gap apart needs a long walk.
 constexpr uint32_t kZWalkDisagree = 4;
 
+// A tile (not its span's last) whose bytes are all zero, entered at span offset xs: a run of
+// Order records of channel 0 ("00 00", SimpleDeterminantEncoder.java:120-121, any channel byte
+// is valid), the reference's output while one input channel carries every buffer
+// (CausalBufferOrderService.java:112).  Its records start at xs, xs + 2, ... below the tile end,
+// so its counts, start bitmap and exit follow without a walk -- the repair walk crosses long
+// runs, where the published chain has the other parity in every tile, at one load per tile.
+// Returns false (nothing written) unless every loaded byte is zero.
+__device__ __forceinline__ bool zero_tile_walk(const ZTile& z, uint64_t xs, const FusedCtl& ctl, uint32_t t,
+                                               uint32_t lane, uint64_t* x) {
+  const uint32_t words = (z.hi + 15) >> 4;
+  const CLG_GLOBAL u32x4* src = gp(reinterpret_cast<const u32x4*>(z.td.abase));
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < kZLoads; ++i) {
+    const uint32_t w = lane + 64u * (uint32_t)i;
+    const u32x4 v = src[w < words ? w : words - 1u];
+    any |= v.x | v.y | v.z | v.w;
+  }
+  if (__any(any != 0u)) return false;
+  const uint32_t e = (uint32_t)(xs - z.td.span_off) + z.lo;  // aligned coordinate of the entry, < hi
+  const uint32_t n = (z.hi - e + 1u) >> 1;                  // starts e, e + 2, ... < hi
+  const uint32_t r0 = lane * kZRegion;
+  const uint64_t pat = (e & 1u) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+  auto word = [&](uint32_t b0) -> uint64_t {  // starts among positions b0 .. b0 + 63
+    uint64_t m = pat;
+    if (e > b0) m = e - b0 >= 64u ? 0ull : m & (~0ull << (e - b0));
+    if (z.hi < b0 + 64u) m = z.hi <= b0 ? 0ull : m & ((1ull << (z.hi - b0)) - 1ull);
+    return m;
+  };
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  u64x2 bits;
+  bits.x = word(r0);
+  bits.y = word(r0 + 64u);
+  gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = bits;
+  if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(n, 0);
+  *x = z.td.span_off + (e + 2u * n - z.lo);
+  return true;
+}
+
 // Chunk c's request (k_decode_repair).  *walk_end: past the last tile a walk reached.
 template <bool J>
 __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
@@ -1599,10 +1672,13 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
         *walk_end = t + 1;
         uint64_t x = xs;
         uint32_t why = 0;
+        bool zero = false;
         if (!z.last && xs >= z.td.span_off + z.td.len) {  // wholly inside a record: no starts
           typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
           gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = u64x2{0, 0};
           if (lane == 0) gp(ctl.cnt)[t] = 0;
+        } else if (!z.last && zero_tile_walk(z, xs, ctl, t, lane, &x)) {
+          zero = true;  // a run of Order(channel 0) records: settled without a walk
         } else {
           why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x);
           __syncthreads();  // the image is reused
@@ -1620,7 +1696,7 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
         }
         old = __shfl(old, 0);
         if (old == 1u || z.last) break;  // resynchronised, or the span ends
-        if (old == 2u && ++disagree > kZWalkDisagree) {  // chains that do not meet: the span goes robust
+        if (old == 2u && !zero && ++disagree > kZWalkDisagree) {  // chains that do not meet: the span goes robust
           if (lane == 0) mark_bad(ctl, 3, t, z.td.span);
           break;
         }
@@ -1795,10 +1871,12 @@ constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ul
 
 __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
                                                      const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
-                                                     DecodeOut out, uint64_t* agg, uint64_t* res) {
+                                                     DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
   __shared__ EmitLds<false> L;  // its image serves the count pass too
   __shared__ uint64_t s_cnt[kZSmallTiles];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
+  for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
   const SpanDesc sd = spans[s];
   uint64_t mine = 0, x = 0;
   bool bad = sd.n_tiles > kZSmallTiles;
@@ -1820,14 +1898,15 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
   for (uint32_t j0 = 0; j0 < s && !any_bad; j0 += 64) {
     const uint32_t j = j0 + lane;
     uint64_t v = 0;
-    if (j < s) {
-      uint32_t nb = 1;
+    if (j < s) {  // a short poll: the waits here are a span's count (microseconds), not a batch's
       const uint64_t w0 = __builtin_amdgcn_s_memtime();
-      while (!((v = ld_agent(&agg[j])) & kZAggSet))
-        if (!backoff(nb, w0)) {
+      while (!((v = ld_agent(&agg[j])) & kZAggSet)) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
           v = kZAggSet | kZAggBad;
           break;
         }
+      }
     }
     any_bad = __any((v & kZAggBad) != 0ull);
     uint64_t c = v & kZAggCnt;
@@ -1855,11 +1934,11 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
 }
 
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* res, void* stream) {
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream) {
   if (!n_spans) return CLG_OK;
   ctl.n_tiles = n_tiles;
   hipLaunchKernelGGL(k_decode_small, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_spans, ctl,
-                     out, agg, res);
+                     out, agg, agg_next, res);
   return launch_status(hipGetLastError());
 }
 

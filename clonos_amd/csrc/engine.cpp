@@ -1567,10 +1567,11 @@ struct clg_engine {
   // goes wrong sends the batch down the usual path.  CLG_F_NO_SMALL_DECODE (or CLONOS_SMALL=0,
   // a developer switch) turns it off.
   static constexpr uint64_t kSmallBytes = 1u << 20;
-  static constexpr uint32_t kSmallSpans = 4096;
+  static constexpr uint32_t kSmallSpans = clg::kZSmallSpans;
   static constexpr uint64_t kSmallHostOut = 32u << 20;  // pinned output bytes at most (cap-sized)
   PinBuf h_small_out, h_small_res;
   DevBuf d_small;
+  bool small_flip = false;
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
         p.only >= 0)
@@ -1627,19 +1628,24 @@ struct clg_engine {
     }
     // scratch: per-tile counts and record-start bitmaps, per-span look-back words
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
-    CHK(d_small.ensure((size_t(nt) + ns) * 8));
     CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
     uint64_t* res = h_small_res.as<uint64_t>();
     res[0] = res[1] = res[2] = 0;
-    uint64_t* cnt = d_small.as<uint64_t>();
-    uint64_t* agg = cnt + nt;
+    // look-back words: two buffers of kSmallSpans, zeroed once; each call zeroes the other
+    if (!d_small.p) {
+      CHK(d_small.ensure((2 * size_t(kSmallSpans) + clg::kZSmallTiles * size_t(kSmallSpans)) * 8));
+      HIPCHK(hipMemsetAsync(d_small.p, 0, 2 * size_t(kSmallSpans) * 8, stream));
+    }
+    uint64_t* agg = d_small.as<uint64_t>() + (small_flip ? kSmallSpans : 0);
+    uint64_t* agg_next = d_small.as<uint64_t>() + (small_flip ? 0 : kSmallSpans);
+    small_flip = !small_flip;
+    uint64_t* cnt = d_small.as<uint64_t>() + 2 * size_t(kSmallSpans);
     clg::FusedCtl ctl{};
     ctl.cnt = cnt;
     ctl.bits = d_zbits.as<uint64_t>();
     ctl.n_tiles = nt;
     ctl.warm = spec_warm(false);
     HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
-    HIPCHK(hipMemsetAsync(agg, 0, size_t(ns) * 8, stream));
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     hipEvent_t ea = nullptr, eb = nullptr;
     if (timing) {
@@ -1649,7 +1655,7 @@ struct clg_engine {
     }
     CHK(clg::launch_decode_small(reinterpret_cast<const clg::TileDesc*>(d_plan.p), nt,
                                  reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
-                                 agg, res, stream));
+                                 agg, agg_next, res, stream));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     HIPCHK(hipStreamSynchronize(stream));
     if (res[2]) {

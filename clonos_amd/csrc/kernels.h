@@ -242,10 +242,12 @@ uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 // kZSmallTiles tiles, batches without Serializable tables.  Results go to `res` (host-mapped
 // pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any span failed
 // (the host then decodes the batch the usual way), res[3 + s] span s's first record.  agg:
-// n_spans zeroed words.
+// kZSmallSpans zeroed words; the kernel zeroes all of agg_next for the next call (the host
+// alternates two buffers, so no memset is queued).
 constexpr uint32_t kZSmallTiles = 8;
+constexpr uint32_t kZSmallSpans = 4096;  // spans per small batch at most (look-back buffer size)
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* res, void* stream);
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one

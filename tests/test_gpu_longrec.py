@@ -175,11 +175,11 @@ def _odd_chain(n):
     return D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * n
 
 
-def test_span_fallback_only_the_bad_spans(leng):
-    """Two spans the fast path cannot settle among 20 ordinary ones (their chains and the
-    speculative ones never meet, so the chunk repair gives up on them after kZWalkDisagree
-    tiles): only those two go through the robust pipeline (decode_span_fallback, not the
-    whole-batch decode_fallback), and every span is bit-exact."""
+def test_zero_runs_settled_without_fallback(leng):
+    """Two spans whose true chains sit on odd offsets of long channel-0 Order runs ("00 00"),
+    among 20 ordinary ones: every chunk entered on the even chain, and the chunk-repair walk
+    crosses the all-zero tiles without walking them (zero_tile_walk) -- nothing goes robust,
+    every span bit-exact."""
     rng = np.random.default_rng(41)  # no Serializable records: the count pass runs without tables
     spans = [synth.config2_log(int(rng.integers(2000, 9000)), rng)[0].tobytes() for _ in range(20)]
     spans[7] = _odd_chain(30000)
@@ -197,15 +197,14 @@ def test_span_fallback_only_the_bad_spans(leng):
         for s, b in enumerate(spans):
             assert_span_equal(dec, s, b)
         assert dec.span_rec_base[-1] == dec.n_rec
-        st = leng.kernel_stats()
-        assert "decode_span_fallback" in st and "decode_fallback" not in st, st
+        assert not went_robust(leng), leng.kernel_stats()
 
 
 def test_long_odd_chains_past_walk_cap(leng):
     """Spans of 200 000 channel-0 Order records at odd offsets, beside ordinary spans: every
-    chunk of such a span entered on the even chain, so a repair walk would not meet the old
-    chain before the span's end; past its cap (kZWalkDisagree) those spans go robust.
-    Bit-exact either way."""
+    chunk of such a span entered on the even chain, so a repair walk does not meet the old
+    chain before the span's end.  Its all-zero tiles are settled without a walk and do not
+    count towards kZWalkDisagree, so nothing goes robust; bit-exact."""
     rng = np.random.default_rng(45)
     spans = [synth.config2_log(20000, rng)[0].tobytes() for _ in range(12)]
     for i in (2, 5, 9):
@@ -220,6 +219,7 @@ def test_long_odd_chains_past_walk_cap(leng):
     dec = leng.decode_host(blob, sp)
     for s, b in enumerate(spans):
         assert_span_equal(dec, s, b)
+    assert not went_robust(leng), leng.kernel_stats()
 
 
 def test_span_fallback_error_equals_robust():
@@ -247,7 +247,8 @@ def test_span_fallback_error_equals_robust():
             x = ei.value
             errs.append((x.status, x.err_span, x.err_off, x.err_tag, x.n_rec))
             if mode == "auto":
-                assert "decode_span_fallback" in e.kernel_stats()
+                ks = e.kernel_stats()
+                assert "decode_span_fallback" in ks and "decode_fallback" not in ks, ks
         finally:
             e.close()
     assert errs[0] == errs[1] and errs[0][1] == 9

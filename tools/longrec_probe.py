@@ -121,6 +121,11 @@ if FULL:
     case("clean", None)
     case("timer_40000", D.encode(D.TimerTriggerDeterminant(7, 1, D.INTERNAL, b"T" * 40000)), log=37, ep=4)
     case("jser_intarr_2250", D.encode(D.SerializableDeterminant(D.jser_int_array(list(range(2250))))), log=181, ep=7)
+    # 64 KB runs of channel-0 Order records ("00 00") across chunk ends, both parities
+    for frac in (0.3, 0.7):
+        case(f"zero_run_64k_odd_{frac}", D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * 32768,
+             log=37, ep=4, frac=frac)
+        case(f"zero_run_64k_even_{frac}", D.encode(D.OrderDeterminant(0)) * 32768, log=37, ep=4, frac=frac)
     case("clean", None)
     sys.exit(0)
 case("clean", None)
