@@ -73,6 +73,71 @@ constexpr int kZSer = -2;                              // Serializable stream: w
 constexpr uint32_t kZTiny = kZTinySpan;                // small whole spans: a lane each (pass 0)
 
 // ---------------------------------------------------------------------------------
+// Wave-wide sums, scans and lane shifts through DPP (cross-lane moves inside the VALU): a
+// __shfl is a ds_bpermute, an LDS round trip each, and the count pass's per-tile reductions
+// were six of them in a row (CLG_DPP=0: the __shfl forms, for A/B).
+// ---------------------------------------------------------------------------------
+#ifndef CLG_DPP
+#define CLG_DPP 1
+#endif
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, false);
+}
+// inclusive scan over the 64 lanes (row_shr 1/2/4/8, then row_bcast 15 / 31)
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, uint32_t lane) {
+#if CLG_DPP
+  const uint32_t rl = lane & 15u;
+  uint32_t t;
+  t = dpp_mov<0x111>(v);
+  if (rl >= 1u) v += t;
+  t = dpp_mov<0x112>(v);
+  if (rl >= 2u) v += t;
+  t = dpp_mov<0x114>(v);
+  if (rl >= 4u) v += t;
+  t = dpp_mov<0x118>(v);
+  if (rl >= 8u) v += t;
+  t = dpp_mov<0x142>(v);
+  if ((lane & 31u) >= 16u) v += t;
+  t = dpp_mov<0x143>(v);
+  if (lane >= 32u) v += t;
+  return v;
+#else
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(v, off);
+    if ((int)lane >= off) v += y;
+  }
+  return v;
+#endif
+}
+// the sum over the 64 lanes, in every lane
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#if CLG_DPP
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x124>(v);  // row_ror:4
+  v += dpp_mov<0x128>(v);  // row_ror:8
+  v += dpp_mov<0x142>(v);  // row_bcast:15
+  v += dpp_mov<0x143>(v);  // row_bcast:31 (lane 63 holds the total)
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+#else
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+#endif
+}
+// lane l gets lane l - 1's value (lane 0: its own)
+__device__ __forceinline__ uint32_t wave_prev_u32(uint32_t v) {
+#if CLG_DPP
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
+#else
+  return __shfl_up(v, 1);
+#endif
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// ---------------------------------------------------------------------------------
 // 128-bit region bitmaps (bit i <-> byte r0 + i of the lane's aligned region r0).
 // ---------------------------------------------------------------------------------
 struct Bits {
@@ -792,13 +857,8 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
   if (!kCols && !on) cw0 = cw1 = 0;
   // the lanes' candidates into the list, in lane order
   const uint32_t nc = (uint32_t)(__popcll(cw0) + __popcll(cw1));
-  uint32_t incl = nc;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += y;
-  }
-  const uint32_t n = min((uint32_t)__shfl(incl, 63), kZLmList);
+  const uint32_t incl = wave_scan_u32(nc, lane);
+  const uint32_t n = min(lane63(incl), kZLmList);
   uint32_t idx = incl - nc;
 #pragma unroll 1
   for (uint32_t hh = 0; hh < 2; ++hh) {
@@ -950,7 +1010,7 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
   const bool on = lane >= c0 && z.rs < z.re;
   uint32_t cx = on ? sp.exit : z.rs, entry = kZCanon;
   for (int it = 0; it <= 64; ++it) {
-    const uint32_t prev = __shfl_up(cx, 1);
+    const uint32_t prev = wave_prev_u32(cx);
     const uint32_t want = lane <= c0 ? kZCanon : prev;
     const bool ch = want != entry;
     if (!__any(ch)) break;
@@ -959,7 +1019,7 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
       cx = on ? canon_walk_r<J>(s_img, z.re, z.end_a, want, sp, jl, g) : want;
     }
   }
-  return __shfl(cx, 63);
+  return lane63(cx);
 }
 
 // Pass 1 for one tile, given its true entry e_true (aligned coordinate): spec walks,
@@ -991,7 +1051,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   // ---- true chain: lanes merge from guessed entries (the previous lane's speculative
   // exit; lane 0 the true entry), then lanes whose entry changed re-merge until the chain
   // is consistent (each pass fixes at least the lowest changed lane)
-  const uint32_t guess = __shfl_up(sp.exit, 1);
+  const uint32_t guess = wave_prev_u32(sp.exit);
   uint32_t entry = lane == 0 ? e_true : guess;
   const GSpan g{tiles, t, z.sd.first_tile + z.sd.n_tiles, lo, z.td.span_off};
   auto merge = [&](uint32_t from) -> Res {
@@ -1008,7 +1068,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   // every pass still settles its lowest changed lane for good).
   uint32_t shift = 0;
   for (int it = 0; it <= 64; ++it) {
-    const uint32_t prev = __shfl_up(r.exit, 1);
+    const uint32_t prev = wave_prev_u32(r.exit);
     uint32_t want = lane == 0 ? e_true : prev;
     bool ch = want != entry;
     const uint64_t cm = __ballot(ch);
@@ -1036,7 +1096,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
     }
     if (lane == 0) ctl.prof[(uint64_t)t * 8 + 5] = (uint64_t)m0 | (uint64_t)m1 << 20 | (uint64_t)iters << 40;
   }
-  const uint32_t x_true = __shfl(r.exit, 63);
+  const uint32_t x_true = lane63(r.exit);
   *x_out = x_true;
   // the true chain meets an invalid record (1) or a Serializable one without tables (5):
   // the lowest such lane decides (lanes above it may have run from guessed entries)
@@ -1065,12 +1125,9 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
 
   ZPHASE(3);
   // ---- counts and the record-start bitmap for the emit pass
-  uint32_t rec = bcount(r.bm), wide = bcount(r.wb);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    rec += __shfl_xor(rec, off);
-    wide += __shfl_xor(wide, off);
-  }
+  // one packed sum: a tile holds at most 4096 records, its lanes at most 64 each
+  const uint32_t pk = wave_sum_u32(bcount(r.bm) | bcount(r.wb) << 16);
+  const uint32_t rec = pk & 0xFFFFu, wide = pk >> 16;
   if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(rec, wide);
   if (cnt_out) *cnt_out = pack_cnt(rec, wide);
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -1286,13 +1343,8 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
   if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
   const uint32_t r0 = lane * kZRegion;
   const uint32_t cnt = (uint32_t)(__popcll(bits.x) + __popcll(bits.y));
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off);
-    if ((int)lane >= off) incl += y;
-  }
-  const uint32_t total = __shfl(incl, 63);
+  const uint32_t incl = wave_scan_u32(cnt, lane);
+  const uint32_t total = lane63(incl);
   const uint64_t rec0 = base & ((1ull << 31) - 1), wide0 = base >> 31;
   // wave-uniform output bases (scalar registers; per-lane 32-bit offsets) and one capacity
   // test per tile instead of one per record

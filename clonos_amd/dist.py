@@ -367,6 +367,19 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     key = np.full(max(n, 1), -1, np.int64)
     if len(held):
         key[held] = (io.copy_lengths(handles, epochs) << 8) | rank
+    if world == 1:  # every copy is this rank's: the winners are gathered in place, nothing moves
+        win = key[:n]
+        mine = np.nonzero(win >= 0)[0]
+        lens = (win[mine] >> 8).astype(np.int64)
+        tot = int(lens.sum())
+        buf = torch.empty(MERGE_GUARD + max(tot, 1) + MERGE_GUARD, dtype=torch.uint8, device=device)
+        if tot:
+            got = io.copy_batch(handles[np.searchsorted(held, mine)], epochs[np.searchsorted(held, mine)], buf,
+                                MERGE_GUARD)
+            if got != tot:
+                raise RuntimeError(f"logs changed during the merge ({got} != {tot} bytes)")
+        offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(mine) else lens
+        return MergedCopies(buf, gids=gids[mine], offs=offs, lens=lens, ranks=np.zeros(len(mine), np.int64))
     dev = device if backend == "nccl" else "cpu"
     kt = torch.from_numpy(key).to(dev)
     dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=group)

@@ -277,7 +277,7 @@ class OracleStore:
         return sum(len(self.copies[int(h)]) for h in handles)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_merge_gloo(world):
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
     res = run_world(merge_worker, world=world)
