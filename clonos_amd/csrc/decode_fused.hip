@@ -838,14 +838,13 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
   // row-per-lane read puts all 32 lanes of a group on one bank) dword 64 j + lane of the tile,
   // so the lanes of a read touch 64 consecutive dwords.
   constexpr bool kCols = kZPad == 0;
-  uint32_t onm = 0;  // (kCols) bit j: dword 64 j + lane's row meets the tile
+  // (kCols) bit j: the row of dword 64 j + lane, 2 j + (lane >> 5), meets the tile (rows from 0,
+  // since lo < 16, to (hi - 1) >> 7)
+  const int32_t jmax = z.hi > z.lo ? ((int32_t)((z.hi - 1u) >> 7) - (int32_t)(lane >> 5)) >> 1 : -1;
+  const uint32_t onm = jmax < 0 ? 0u : (jmax >= 31 ? 0xFFFFFFFFu : (2u << jmax) - 1u);
 #pragma unroll
   for (uint32_t j = 0; j < kZRowDw; ++j) {
     const uint32_t x = kCols ? T[64u * j + lane] : T[lane * kZPitch + j];
-    if (kCols) {
-      const uint32_t rr = 2u * j + (lane >> 5);  // the dword's row
-      onm |= (kZRegion * rr < z.hi && kZRegion * rr + kZRegion > z.lo ? 1u : 0u) << j;
-    }
     // 0xFF in every byte holding a tag (< 8): bytes with none of bits 3-7 set
     const uint32_t h = x & 0xF8F8F8F8u;
     const uint32_t zz = (h - 0x01010101u) & ~h & 0x80808080u;
@@ -1022,6 +1021,15 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
   return lane63(cx);
 }
 
+// Where lane `lane`'s speculative warm-up starts, warm bytes before its region start rs.
+// Without row pads every region starts on bank 0, so the lanes' first reads would all hit
+// one bank: there the warm-up grows by 4 (lane & 7) bytes, putting eight start banks in each
+// group of lanes (the walk is a function of the tile's bytes either way).
+__device__ __forceinline__ uint32_t warm_start(uint32_t rs, uint32_t lo, uint32_t warm, uint32_t lane) {
+  const uint32_t w = kZPad == 0 ? warm + 4u * (lane & 7u) : warm;
+  return rs >= lo + w ? rs - w : lo;
+}
+
 // Pass 1 for one tile, given its true entry e_true (aligned coordinate): spec walks,
 // true chain, exit checks, then the tile's record / wide-record counts and its
 // record-start bitmap (1 KiB) for the emit pass.  *x_true = the tile's exit.  must_exit:
@@ -1035,14 +1043,15 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
                                            const uint32_t must_exit, const FusedCtl& ctl, const uint32_t* s_img,
                                            const uint32_t lane, uint32_t* x_out, const JL& jl,
                                            const TileDesc* __restrict__ tiles = nullptr,
-                                           const SpecR* walked = nullptr, uint64_t* cnt_out = nullptr) {
+                                           const SpecR* walked = nullptr, uint64_t* cnt_out = nullptr,
+                                           uint64_t* bm_out = nullptr) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
   // ---- speculative walk of the lane's region (with warm-up), starts in registers (walked:
   // the chunk prologue's walk of this same tile, a function of the tile's bytes only)
-  const uint32_t ws = rs >= lo + ctl.warm ? rs - ctl.warm : lo;
+  const uint32_t ws = warm_start(rs, lo, ctl.warm, lane);
   const SpecR sp = walked ? *walked
                           : rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
                                     : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
@@ -1130,6 +1139,10 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   const uint32_t rec = pk & 0xFFFFu, wide = pk >> 16;
   if (lane == 0) gp(ctl.cnt)[t] = pack_cnt(rec, wide);
   if (cnt_out) *cnt_out = pack_cnt(rec, wide);
+  if (bm_out) {
+    bm_out[0] = r.bm.lo;
+    bm_out[1] = r.bm.hi;
+  }
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   u64x2 out_bits;
   out_bits.x = r.bm.lo;
@@ -1321,7 +1334,8 @@ struct EmitLds {
 template <bool J>
 __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, const DecodeOut& out, const uint32_t t,
-                                          const uint32_t lane, const uint64_t base, EmitLds<J>& L) {
+                                          const uint32_t lane, const uint64_t base, EmitLds<J>& L,
+                                          const uint64_t* bm_in = nullptr) {
   using PosT = typename EmitLds<J>::PosT;
   constexpr uint32_t kWin = EmitLds<J>::kWin;
   uint32_t* const s_img = L.img;
@@ -1334,11 +1348,13 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
   const uint64_t ea = sd.len - td.span_off + td.delta;
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  u64x2 bits = gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
+  // bm_in: the lane's bitmap words straight from the count, the image still staged in L.img
+  // (the single-launch small decode); else both from memory
+  u64x2 bits = bm_in ? u64x2{bm_in[0], bm_in[1]} : gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
   if (lane * kZRegion >= hi) bits = u64x2{0, 0};  // past the tile (the lane path of small spans skips them)
   JLPre pre{};
   if (J) pre = jl_prefetch(ctl, t, lane);
-  stage_image(td, sd, t, tiles, s_img, lane, hi, &n1);
+  if (!bm_in) stage_image(td, sd, t, tiles, s_img, lane, hi, &n1);
   JL jl{nullptr, nullptr, nullptr};
   if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
   const uint32_t r0 = lane * kZRegion;
@@ -1629,7 +1645,7 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
                                                  uint32_t t, const ZTile& z, uint64_t xs, uint32_t must_exit,
                                                  const SpecR* walked, uint64_t* x, uint64_t* cnt_out = nullptr,
                                                  StagePre* pf = nullptr, bool pf_ready = false,
-                                                 uint32_t pf_next = 0xFFFFFFFFu) {
+                                                 uint32_t pf_next = 0xFFFFFFFFu, uint64_t* bm_out = nullptr) {
   constexpr bool kLm = CLG_COUNT_LM != 0;
   const uint32_t nt = ctl.n_tiles;
   const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
@@ -1652,7 +1668,8 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
   if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
   else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
   uint32_t x_true;
-  const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked, cnt_out);
+  const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked, cnt_out,
+                                     bm_out);
   *x = z.td.span_off + (x_true - z.lo);
   return why;
 }
@@ -1790,7 +1807,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
       if (J && kLm) build_lm(z, s_img, s_j, lane);
       if (J && kLm) jl = load_jl_map(ctl, t1 - 1, s_j, lane, s_img, jl_prefetch(ctl, t1 - 1, lane));
       else if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
-      const uint32_t ws = z.rs >= z.lo + ctl.warm ? z.rs - ctl.warm : z.lo;
+      const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane);
       sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
       x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
@@ -1930,18 +1947,18 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
   // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
   for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
   const SpanDesc sd = spans[s];
-  uint64_t mine = 0, x = 0;
+  uint64_t mine = 0, x = 0, bm[2] = {0, 0};
   bool bad = sd.n_tiles > kZSmallTiles;
   for (uint32_t k = 0; k < sd.n_tiles && !bad; ++k) {
     const uint32_t t = sd.first_tile + k;
     const ZTile z = ztile(tiles, spans, t, lane);
     uint64_t c = 0;
+    if (k) __syncthreads();  // the image is reused (the last tile's stays for emit)
     const uint32_t why = count_staged<false>(tiles, spans, ctl, L.img, nullptr, lane, t, z, k ? x : z.td.span_off,
-                                             kZCanon, nullptr, &x, &c);
+                                             kZCanon, nullptr, &x, &c, nullptr, false, 0xFFFFFFFFu, bm);
     bad = why != 0u;
     if (lane == 0) s_cnt[k] = c;
     mine += c;
-    __syncthreads();  // the image is reused
   }
   if (lane == 0) st_agent(&agg[s], kZAggSet | (bad ? kZAggBad : 0ull) | mine);
   // look-back: every earlier span's counts
@@ -1970,11 +1987,18 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
+  __syncthreads();  // s_cnt
   uint64_t b = pre;
-  for (uint32_t k = 0; k < sd.n_tiles; ++k) {
-    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + k, lane, b, L);
-    b += s_cnt[k];
+  for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) b += s_cnt[k];
+  if (sd.n_tiles) {  // the last tile first: its image and bitmap are still here
+    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
+    b += s_cnt[sd.n_tiles - 1];
+  }
+  uint64_t e = pre;
+  for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) {
     __syncthreads();
+    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + k, lane, e, L);
+    e += s_cnt[k];
   }
   if (lane == 0) {
     res[3 + s] = pre;

@@ -1659,7 +1659,7 @@ struct clg_engine {
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     HIPCHK(hipStreamSynchronize(stream));
     if (res[2]) {
-      if (timing) ev_pool.insert(ev_pool.end(), {ea, eb});
+      if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, 0});
       *aborted = true;
       return CLG_OK;
     }

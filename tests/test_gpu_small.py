@@ -44,7 +44,8 @@ def test_small_random_spans_multi_tile(seed, seg):
     with _eng(segment_bytes=seg) as eng:
         from clonos_amd import CausalLogID
         bufs, logs = [], []
-        sizes = [0, 1, 5, 50, 400, 3000, 9000] if seg == 16384 else [0, 1, 5, 50, 200]  # <= 8 tiles per span
+        # <= 8 tiles per span (records average ~28 bytes)
+        sizes = [0, 1, 5, 50, 400, 1500] if seg == 16384 else [0, 1, 5, 20, 40]
         for i in range(int(rng.integers(1, 60))):
             n = int(rng.choice(sizes))
             b = synth.random_log(n, rng, allow_serializable=False)
@@ -94,7 +95,7 @@ def test_small_error_falls_back_with_the_reference_error():
         except ClonosError as e:
             got = e.status
         st, _, _, _ = O.decode(bad)
-        assert _launches(eng, "decode_small") == 1
+        assert _launches(eng, "decode_small") == 1  # launched (and, on an error, fallen back)
         if st != 0:
             assert got == st and _launches(eng, "decode_small_fallback") == 1
         else:

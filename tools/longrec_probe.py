@@ -23,7 +23,7 @@ gen = [synth.config3_epoch(PER, rng, e) for e in range(N_EP)]
 epochs = [g[0] for g in gen]
 dev = torch.device("cuda", 0)
 n_det = N_LOGS * N_EP * PER
-cap = max(n_det, N_LOGS * 400001) + 16
+cap = max(n_det, N_LOGS * 400001) + 65536  # room for an inserted run of short records
 o = [torch.empty(cap, dtype=t, device=dev) for t in (torch.int32, torch.uint8, torch.int64)]
 ow = [torch.empty(n_det // 2 + 16, dtype=t, device=dev)
       for t in (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
