@@ -1787,8 +1787,15 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
 // 128 VGPRs (4 waves per SIMD by registers, 3.25 by LDS with tables): count<J> 0.396 to
 // 0.376 ms on the config-3 subset, count<false> (88 VGPRs) unaffected.  The same bound on
 // k_decode_jser made it slower (0.26 to 0.28 ms), so that kernel keeps its 150.
+// Waves per SIMD the count kernel is compiled for (its VGPR bound): 4 (128 VGPRs), except with
+// tables and no row pads, where 128 VGPRs spilled into the walks (config-3 count +60 %) -- 3.
+#ifndef CLG_COUNT_J_WAVES
+#define CLG_COUNT_J_WAVES 0  // developer switch: waves per SIMD for count<J> (0: the default below)
+#endif
 template <bool J>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+constexpr int kZCountWaves = (J && CLG_COUNT_J_WAVES) ? CLG_COUNT_J_WAVES : ((J && kZPad == 0) ? 3 : 4);
+template <bool J>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves<J>))) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
@@ -1944,6 +1951,15 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
   __shared__ EmitLds<false> L;  // its image serves the count pass too
   __shared__ uint64_t s_cnt[kZSmallTiles];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
+  // developer diagnostics (CLONOS_SMALL_PROF): per span, shader-clock and 100 MHz real-time stamps
+  // at the start, after the count, after the look-back and at the end
+  auto stamp = [&](uint32_t i) {
+    if (ctl.prof && lane == 0) {
+      ctl.prof[(uint64_t)s * 8 + 2 * i] = __builtin_amdgcn_s_memtime();
+      ctl.prof[(uint64_t)s * 8 + 2 * i + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  stamp(0);
   // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
   for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
   const SpanDesc sd = spans[s];
@@ -1960,6 +1976,7 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     if (lane == 0) s_cnt[k] = c;
     mine += c;
   }
+  stamp(1);
   if (lane == 0) st_agent(&agg[s], kZAggSet | (bad ? kZAggBad : 0ull) | mine);
   // look-back: every earlier span's counts
   uint64_t pre = 0;
@@ -1987,6 +2004,7 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
+  stamp(2);
   __syncthreads();  // s_cnt
   uint64_t b = pre;
   for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) b += s_cnt[k];
@@ -2000,6 +2018,7 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + k, lane, e, L);
     e += s_cnt[k];
   }
+  stamp(3);
   if (lane == 0) {
     res[3 + s] = pre;
     if (s + 1 == n_spans) {

@@ -1645,6 +1645,12 @@ struct clg_engine {
     ctl.bits = d_zbits.as<uint64_t>();
     ctl.n_tiles = nt;
     ctl.warm = spec_warm(false);
+    const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
+    if (sprof) {
+      CHK(d_prof.ensure(size_t(ns) * 64));
+      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(ns) * 64, stream));
+      ctl.prof = d_prof.as<uint64_t>();
+    }
     HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     hipEvent_t ea = nullptr, eb = nullptr;
@@ -1658,6 +1664,26 @@ struct clg_engine {
                                  agg, agg_next, res, stream));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    if (sprof) {  // per phase: the span range of (clock ticks, us) since the earliest start
+      std::vector<uint64_t> hp(size_t(ns) * 8);
+      HIPCHK(hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost));
+      uint64_t c0 = ~0ull, r0 = ~0ull;
+      for (uint32_t s = 0; s < ns; ++s) {
+        c0 = std::min(c0, hp[s * 8]);
+        r0 = std::min(r0, hp[s * 8 + 1]);
+      }
+      for (int i = 0; i < 4; ++i) {
+        uint64_t cmin = ~0ull, cmax = 0, rmin = ~0ull, rmax = 0;
+        for (uint32_t s = 0; s < ns; ++s) {
+          cmin = std::min(cmin, hp[s * 8 + 2 * i] - c0);
+          cmax = std::max(cmax, hp[s * 8 + 2 * i] - c0);
+          rmin = std::min(rmin, hp[s * 8 + 2 * i + 1] - r0);
+          rmax = std::max(rmax, hp[s * 8 + 2 * i + 1] - r0);
+        }
+        fprintf(stderr, "[clonos] small decode stamp %d: clock %llu..%llu  real %.2f..%.2f us\n", i,
+                (unsigned long long)cmin, (unsigned long long)cmax, rmin / 100.0, rmax / 100.0);
+      }
+    }
     if (res[2]) {
       if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, 0});
       *aborted = true;

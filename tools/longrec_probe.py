@@ -33,7 +33,7 @@ dec.w_idx, dec.w_rc, dec.w_v1, dec.w_var_off, dec.w_var_len, dec.w_sub = [t.data
 dec.cap, dec.wcap, dec.out_kind = cap, n_det // 2 + 16, _lib.CLG_MEM_DEVICE
 
 
-def case(name, rec, log=37, ep=2, frac=0.5):
+def case(name, rec, log=37, ep=2, frac=0.5, n_ins=1):
     seg = 16384
     per_log = sum(int(e.size) for e in epochs) + (len(rec) if rec else 0)
     eng = Engine(segment_bytes=seg, pool_segments=N_LOGS * ((per_log + seg - 1) // seg + N_EP + 1) + 64, timing=True,
@@ -55,7 +55,7 @@ def case(name, rec, log=37, ep=2, frac=0.5):
         base = np.zeros(N_LOGS + 1, np.uint64)
         print(f"--- {name}", file=sys.stderr, flush=True)
         eng.decode_logs_device(hs, starts, dec, base)
-        ok = dec.err_status == 0 and dec.n_rec == n_det + (1 if rec else 0)
+        ok = dec.err_status == 0 and dec.n_rec == n_det + (n_ins if rec else 0)
         torch.cuda.synchronize()
         eng.kernel_stats_reset()
         t0 = time.perf_counter()
@@ -124,8 +124,8 @@ if FULL:
     # 64 KB runs of channel-0 Order records ("00 00") across chunk ends, both parities
     for frac in (0.3, 0.7):
         case(f"zero_run_64k_odd_{frac}", D.encode(D.TimestampDeterminant(5)) + D.encode(D.OrderDeterminant(0)) * 32768,
-             log=37, ep=4, frac=frac)
-        case(f"zero_run_64k_even_{frac}", D.encode(D.OrderDeterminant(0)) * 32768, log=37, ep=4, frac=frac)
+             log=37, ep=4, frac=frac, n_ins=32769)
+        case(f"zero_run_64k_even_{frac}", D.encode(D.OrderDeterminant(0)) * 32768, log=37, ep=4, frac=frac, n_ins=32768)
     case("clean", None)
     sys.exit(0)
 case("clean", None)
