@@ -42,13 +42,17 @@
 namespace clg {
 
 // LDS image: row r holds aligned bytes [kZRegion r, kZRegion (r + 1)) at a pitch of kZPitch
-// dwords; the kZPad dwords after a row repeat the first kZPad dwords of the next row, so
-// up to four consecutive dwords read from any dword of a row stay inside its pitch.  Lane
-// l walks row l: with a pitch of 35 dwords (co-prime with the 32 banks) the lanes' reads
-// start on distinct banks.  Rows: the tile, then the halo + zero pad.
+// dwords; with pads (kZPad > 0) the kZPad dwords after a row repeat the first kZPad dwords of
+// the next row, so up to four consecutive dwords read from any dword of a row stay inside its
+// pitch, and with a pitch of 35 dwords (co-prime with the 32 banks) the lanes' row walks start
+// on distinct banks.  The default is no pads: the image is the bytes themselves (an address is
+// the aligned coordinate, two VALU fewer per walk step), the warm-ups start 4 (lane & 7)
+// bytes apart instead (warm_start), and build_lm reads column-wise.  Rows: the tile, then the
+// halo + zero pad.
 constexpr uint32_t kZRowDw = kZRegion / 4;  // 32
 #ifndef CLG_ZPAD
-#define CLG_ZPAD 3
+#define CLG_ZPAD 0  // 3: rows at a 35-dword pitch (measured: config-2 count 0.179 -> 0.164 ms, config-3 emit
+                    // 0.363 -> 0.335 ms without pads; tools/ab.sh)
 #endif
 constexpr uint32_t kZPad = CLG_ZPAD;
 constexpr uint32_t kZPitch = kZRowDw + kZPad;
@@ -1960,6 +1964,8 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     }
   };
   stamp(0);
+  FusedCtl cc = ctl;  // the count / emit helpers' own stamps (count_tile's ZPHASE) stay off
+  cc.prof = nullptr;
   // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
   for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
   const SpanDesc sd = spans[s];
@@ -1970,7 +1976,7 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     const ZTile z = ztile(tiles, spans, t, lane);
     uint64_t c = 0;
     if (k) __syncthreads();  // the image is reused (the last tile's stays for emit)
-    const uint32_t why = count_staged<false>(tiles, spans, ctl, L.img, nullptr, lane, t, z, k ? x : z.td.span_off,
+    const uint32_t why = count_staged<false>(tiles, spans, cc, L.img, nullptr, lane, t, z, k ? x : z.td.span_off,
                                              kZCanon, nullptr, &x, &c, nullptr, false, 0xFFFFFFFFu, bm);
     bad = why != 0u;
     if (lane == 0) s_cnt[k] = c;
@@ -2009,13 +2015,13 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
   uint64_t b = pre;
   for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) b += s_cnt[k];
   if (sd.n_tiles) {  // the last tile first: its image and bitmap are still here
-    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
+    emit_tile<false>(tiles, spans, cc, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
     b += s_cnt[sd.n_tiles - 1];
   }
   uint64_t e = pre;
   for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) {
     __syncthreads();
-    emit_tile<false>(tiles, spans, ctl, out, sd.first_tile + k, lane, e, L);
+    emit_tile<false>(tiles, spans, cc, out, sd.first_tile + k, lane, e, L);
     e += s_cnt[k];
   }
   stamp(3);

@@ -1664,24 +1664,17 @@ struct clg_engine {
                                  agg, agg_next, res, stream));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     HIPCHK(hipStreamSynchronize(stream));
-    if (sprof) {  // per phase: the span range of (clock ticks, us) since the earliest start
+    if (sprof) {
       std::vector<uint64_t> hp(size_t(ns) * 8);
       HIPCHK(hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost));
-      uint64_t c0 = ~0ull, r0 = ~0ull;
-      for (uint32_t s = 0; s < ns; ++s) {
-        c0 = std::min(c0, hp[s * 8]);
-        r0 = std::min(r0, hp[s * 8 + 1]);
-      }
-      for (int i = 0; i < 4; ++i) {
-        uint64_t cmin = ~0ull, cmax = 0, rmin = ~0ull, rmax = 0;
-        for (uint32_t s = 0; s < ns; ++s) {
-          cmin = std::min(cmin, hp[s * 8 + 2 * i] - c0);
-          cmax = std::max(cmax, hp[s * 8 + 2 * i] - c0);
-          rmin = std::min(rmin, hp[s * 8 + 2 * i + 1] - r0);
-          rmax = std::max(rmax, hp[s * 8 + 2 * i + 1] - r0);
-        }
-        fprintf(stderr, "[clonos] small decode stamp %d: clock %llu..%llu  real %.2f..%.2f us\n", i,
-                (unsigned long long)cmin, (unsigned long long)cmax, rmin / 100.0, rmax / 100.0);
+      uint64_t r0 = ~0ull;
+      for (uint32_t s = 0; s < ns; ++s) r0 = std::min(r0, hp[s * 8 + 1]);
+      for (uint32_t s = 0; s < ns; ++s) {  // per span: start, then each phase's ticks and us
+        const uint64_t* q = &hp[s * 8];
+        fprintf(stderr, "[clonos] small decode span %u: start %.2f us  count %llu/%.2f  lookback %llu/%.2f  emit %llu/%.2f\n",
+                s, (q[1] - r0) / 100.0, (unsigned long long)(q[2] - q[0]), (q[3] - q[1]) / 100.0,
+                (unsigned long long)(q[4] - q[2]), (q[5] - q[3]) / 100.0, (unsigned long long)(q[6] - q[4]),
+                (q[7] - q[5]) / 100.0);
       }
     }
     if (res[2]) {

@@ -25,6 +25,7 @@ lg = [logs[l] for l in lids]
 h = np.array([l.handle for l in lg], np.uint32)
 ep = np.zeros(len(lg), np.int64)
 total = sum(len(b) for b in data.values())
+print(json.dumps({"span_bytes": [len(data[l]) for l in lids]}), flush=True)
 dev = torch.device("cuda", 0)
 cap, wcap = total // 2 + 64, total // 6 + 64
 o = [torch.empty(cap, dtype=t, device=dev) for t in (torch.int32, torch.uint8, torch.int64)]
