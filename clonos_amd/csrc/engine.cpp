@@ -24,6 +24,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <optional>
 #include <vector>
 
 #include "../../include/clonos_engine.h"
@@ -1647,10 +1648,11 @@ struct clg_engine {
     ctl.warm = spec_warm(false);
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
-      CHK(d_prof.ensure(size_t(ns) * 64));
-      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(ns) * 64, stream));
+      CHK(d_prof.ensure(size_t(ns + nt) * 64));
+      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(ns + nt) * 64, stream));
       ctl.prof = d_prof.as<uint64_t>();
     }
+    std::optional<HostTimer> hsub(std::in_place, this, "host_small_submit");  // (CLONOS_HOST_PROF sub-stages)
     HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     hipEvent_t ea = nullptr, eb = nullptr;
@@ -1663,9 +1665,11 @@ struct clg_engine {
                                  reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
                                  agg, agg_next, res, stream));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
+    hsub.emplace(this, "host_small_wait");
     HIPCHK(hipStreamSynchronize(stream));
+    hsub.emplace(this, "host_small_finish");
     if (sprof) {
-      std::vector<uint64_t> hp(size_t(ns) * 8);
+      std::vector<uint64_t> hp(size_t(ns + nt) * 8);
       HIPCHK(hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost));
       uint64_t r0 = ~0ull;
       for (uint32_t s = 0; s < ns; ++s) r0 = std::min(r0, hp[s * 8 + 1]);
@@ -1675,6 +1679,13 @@ struct clg_engine {
                 s, (q[1] - r0) / 100.0, (unsigned long long)(q[2] - q[0]), (q[3] - q[1]) / 100.0,
                 (unsigned long long)(q[4] - q[2]), (q[5] - q[3]) / 100.0, (unsigned long long)(q[6] - q[4]),
                 (q[7] - q[5]) / 100.0);
+      }
+      for (uint32_t t = 0; t < nt; ++t) {  // per tile (count_tile): walk, merge, counts ticks; merge steps, passes
+        const uint64_t* q = &hp[(ns + t) * 8];
+        fprintf(stderr, "[clonos] small decode tile %u: walk %llu  merge %llu  counts %llu  steps %llu/%llu  passes %llu\n", t,
+                (unsigned long long)(q[2] - q[1]), (unsigned long long)(q[3] - q[2]), (unsigned long long)(q[4] - q[3]),
+                (unsigned long long)(q[5] & 0xFFFFF), (unsigned long long)((q[5] >> 20) & 0xFFFFF),
+                (unsigned long long)(q[5] >> 40));
       }
     }
     if (res[2]) {
