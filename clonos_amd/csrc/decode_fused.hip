@@ -71,6 +71,10 @@ constexpr int kZWarmUnroll = 4;
 #endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
+#ifndef CLG_EMIT_PAIR
+#define CLG_EMIT_PAIR 2
+#endif
+constexpr int kZEmitPair = CLG_EMIT_PAIR;              // emit: records per lane per pass (loads hoisted)
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
@@ -1394,71 +1398,88 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
     __syncthreads();
     const uint32_t nw = total - w0 < kWin ? total - w0 : kWin;
     uint32_t nwide = 0;  // wide records of the window so far (wave-uniform)
-    for (uint32_t i0 = 0; i0 < nw; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const bool act = i < nw;
-      const uint32_t a = act ? s_pos[i] : lo;
-      const uint32_t kk = rk(a >> 2), sh = 8u * (a & 3u);
-      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
-      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
-      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
-      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-      uint32_t tg = x0 & 0xFFu;
-      const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
-      // v0 without branches: Order's channel byte, Timestamp's big-endian i64, else (RNG,
-      // BufferBuilt) a big-endian i32; wide records get theirs in the wide pass
-      const bool is_ts = tg == CLG_TAG_TIMESTAMP;
-      const uint32_t be32 = __builtin_bswap32(blo);
-      const uint32_t v_lo = is_ts ? __builtin_bswap32(bhi)
-                                  : (tg == CLG_TAG_ORDER ? (uint32_t)(int32_t)(int8_t)(blo & 0xFFu) : be32);
-      const uint32_t v_hi = is_ts ? be32 : (uint32_t)((int32_t)v_lo >> 31);
-      const int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
-      const bool wide_rec = act && is_wide((int)tg);
-      const uint64_t wm = __ballot(wide_rec);
-      if constexpr (J) {
-        if (act) {
-          const uint32_t so = (uint32_t)(td.span_off + (a - lo));
-          if (fits || rec0 + w0 + i < out.cap) {
-            const uint32_t j = w0 + i;
-            o_off[j] = so;
-            o_tag[j] = (uint8_t)tg;
-            if (!wide_rec) o_v0[j] = v0;
+    // two records per lane per pass, both loaded before either is decoded: the positions' and
+    // image reads of the second overlap the first's (a wave alone on its SIMD -- the
+    // single-launch small decode -- waits on every read otherwise)
+    for (uint32_t i0 = 0; i0 < nw; i0 += 64u * kZEmitPair) {
+      uint32_t a2[kZEmitPair], dd[kZEmitPair][4];
+#pragma unroll
+      for (int h = 0; h < kZEmitPair; ++h) {
+        const uint32_t i = i0 + 64u * h + lane;
+        a2[h] = i < nw ? s_pos[i] : lo;
+      }
+#pragma unroll
+      for (int h = 0; h < kZEmitPair; ++h) {
+        const uint32_t kk = rk(a2[h] >> 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dd[h][q] = s_img[kk + q];
+      }
+#pragma unroll
+      for (int h = 0; h < kZEmitPair; ++h) {
+        const uint32_t i = i0 + 64u * h + lane;
+        const bool act = i < nw;
+        const uint32_t a = a2[h], sh = 8u * (a & 3u);
+        const uint32_t d0 = dd[h][0], d1 = dd[h][1], d2 = dd[h][2], d3 = dd[h][3];
+        const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
+        const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+        const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+        uint32_t tg = x0 & 0xFFu;
+        const uint32_t blo = (x0 >> 8) | (x1 << 24), bhi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
+        // v0 without branches: Order's channel byte, Timestamp's big-endian i64, else (RNG,
+        // BufferBuilt) a big-endian i32; wide records get theirs in the wide pass
+        const bool is_ts = tg == CLG_TAG_TIMESTAMP;
+        const uint32_t be32 = __builtin_bswap32(blo);
+        const uint32_t v_lo = is_ts ? __builtin_bswap32(bhi)
+                                    : (tg == CLG_TAG_ORDER ? (uint32_t)(int32_t)(int8_t)(blo & 0xFFu) : be32);
+        const uint32_t v_hi = is_ts ? be32 : (uint32_t)((int32_t)v_lo >> 31);
+        const int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
+        const bool wide_rec = act && is_wide((int)tg);
+        const uint64_t wm = __ballot(wide_rec);
+        if constexpr (J) {
+          if (act) {
+            const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+            if (fits || rec0 + w0 + i < out.cap) {
+              const uint32_t j = w0 + i;
+              o_off[j] = so;
+              o_tag[j] = (uint8_t)tg;
+              if (!wide_rec) o_v0[j] = v0;
+            }
+            // compaction in place: every entry below i0 + 64 kZEmitPair has been read already
+            if (wide_rec) s_pos[nwide + (uint32_t)__popcll(wm & ((1ull << lane) - 1ull))] = a | i << 16;
           }
-          // compaction in place: every entry below i0 + 64 has been read already
-          if (wide_rec) s_pos[nwide + (uint32_t)__popcll(wm & ((1ull << lane) - 1ull))] = a | i << 16;
-        }
-        nwide += (uint32_t)__popcll(wm);
-      } else {
-        Rec rr{};
-        int64_t v = v0;
-        if (wide_rec) {
-          uint32_t tgu;
-          const int L = zlen(s_img, a, end_a, &tgu);
-          decode_fields(ZBytes{s_img, a}, (int)tg, (int64_t)L, rr);
-          v = rr.v0;
-        }
-        if (act) {
-          const uint32_t so = (uint32_t)(td.span_off + (a - lo));
-          const uint64_t g = rec0 + w0 + i;
-          if (fits || g < out.cap) {
-            const uint32_t j = w0 + i;
-            o_off[j] = so;
-            o_tag[j] = (uint8_t)tg;
-            o_v0[j] = v;
-          }
+          nwide += (uint32_t)__popcll(wm);
+        } else {
+          Rec rr{};
+          int64_t v = v0;
           if (wide_rec) {
-            const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
-            if (wi < out.wcap) {
-              gp(out.w_idx)[wi] = (uint32_t)g;
-              gp(out.w_rc)[wi] = rr.rc;
-              gp(out.w_v1)[wi] = rr.v1;
-              gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
-              gp(out.w_var_len)[wi] = rr.var_len;
-              gp(out.w_sub)[wi] = rr.sub;
+            uint32_t tgu;
+            const int L = zlen(s_img, a, end_a, &tgu);
+            decode_fields(ZBytes{s_img, a}, (int)tg, (int64_t)L, rr);
+            v = rr.v0;
+          }
+          if (act) {
+            const uint32_t so = (uint32_t)(td.span_off + (a - lo));
+            const uint64_t g = rec0 + w0 + i;
+            if (fits || g < out.cap) {
+              const uint32_t j = w0 + i;
+              o_off[j] = so;
+              o_tag[j] = (uint8_t)tg;
+              o_v0[j] = v;
+            }
+            if (wide_rec) {
+              const uint64_t wi = wide + (uint64_t)__popcll(wm & ((1ull << lane) - 1ull));
+              if (wi < out.wcap) {
+                gp(out.w_idx)[wi] = (uint32_t)g;
+                gp(out.w_rc)[wi] = rr.rc;
+                gp(out.w_v1)[wi] = rr.v1;
+                gp(out.w_var_off)[wi] = rr.var_off ? so + rr.var_off : 0u;
+                gp(out.w_var_len)[wi] = rr.var_len;
+                gp(out.w_sub)[wi] = rr.sub;
+              }
             }
           }
+          wide += (uint64_t)__popcll(wm);
         }
-        wide += (uint64_t)__popcll(wm);
       }
     }
     __syncthreads();
@@ -1949,9 +1970,15 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
 // ---------------------------------------------------------------------------------
 constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ull << 62) - 1;
 
-__global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
-                                                     const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
-                                                     DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
+// the wave's outputs are written: count it done (res[3 + n_spans], system scope, release)
+__device__ __forceinline__ void small_done(uint64_t* res, uint32_t n_spans, uint32_t lane) {
+  __syncthreads();  // every lane's stores before lane 0's release
+  if (lane == 0) __hip_atomic_fetch_add(res + 3 + n_spans, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                             uint32_t n_spans, const FusedCtl& ctl, const DecodeOut& out, uint64_t* agg,
+                                             uint64_t* agg_next, uint64_t* res) {
   __shared__ EmitLds<false> L;  // its image serves the count pass too
   __shared__ uint64_t s_cnt[kZSmallTiles];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
@@ -1964,8 +1991,8 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
     }
   };
   stamp(0);
-  FusedCtl cc = ctl;  // the count / emit helpers' own stamps (count_tile's ZPHASE) stay off
-  cc.prof = nullptr;
+  FusedCtl cc = ctl;  // count_tile's own stamps (ZPHASE, per tile) after the spans'
+  cc.prof = ctl.prof ? ctl.prof + (uint64_t)n_spans * 8 : nullptr;
   // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
   for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
   const SpanDesc sd = spans[s];
@@ -2008,6 +2035,7 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
   }
   if (any_bad) {
     if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    small_done(res, n_spans, lane);
     return;
   }
   stamp(2);
@@ -2032,14 +2060,33 @@ __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict_
       res[1] = b >> 31;
     }
   }
+  small_done(res, n_spans, lane);
+}
+
+__global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
+                                                     const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
+                                                     DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
+  decode_small(tiles, spans, n_spans, ctl, out, agg, agg_next, res);
+}
+// The plan in the kernel arguments (read through the argument segment's address).
+__global__ __launch_bounds__(64) void k_decode_small_arg(const SmallPlanArg plan, uint32_t n_spans, FusedCtl ctl,
+                                                         DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
+  decode_small(plan.tiles, plan.spans, n_spans, ctl, out, agg, agg_next, res);
 }
 
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream) {
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
+                        const SmallPlanArg* plan) {
   if (!n_spans) return CLG_OK;
   ctl.n_tiles = n_tiles;
-  hipLaunchKernelGGL(k_decode_small, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_spans, ctl,
-                     out, agg, agg_next, res);
+  if (plan) {
+    if (n_tiles > kZSmallArgTiles || n_spans > kZSmallArgSpans) return CLG_E_INVALID_ARG;
+    hipLaunchKernelGGL(k_decode_small_arg, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, *plan, n_spans, ctl, out,
+                       agg, agg_next, res);
+  } else {
+    hipLaunchKernelGGL(k_decode_small, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_spans,
+                       ctl, out, agg, agg_next, res);
+  }
   return launch_status(hipGetLastError());
 }
 

@@ -347,13 +347,14 @@ struct DevBuf {
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: device atomics reach the host at once
   int ensure(size_t n) {
     if (n <= cap) return CLG_OK;
     if (p) hipHostFree(p);
     p = nullptr;
     size_t c = std::max(n, cap * 2);
     c = (c + 255) & ~size_t(255);
-    hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, c, flags);
     if (e != hipSuccess) {
       cap = 0;
       return fail(CLG_E_DEVICE, "hipHostMalloc(%zu) failed: %s", c, hipGetErrorString(e));
@@ -1570,8 +1571,9 @@ struct clg_engine {
   static constexpr uint64_t kSmallBytes = 1u << 20;
   static constexpr uint32_t kSmallSpans = clg::kZSmallSpans;
   static constexpr uint64_t kSmallHostOut = 32u << 20;  // pinned output bytes at most (cap-sized)
-  PinBuf h_small_out, h_small_res;
+  PinBuf h_small_out, h_small_res{nullptr, 0, hipHostMallocCoherent};  // (res: polled while the kernel runs)
   DevBuf d_small;
+  clg::SmallPlanArg small_arg;
   bool small_flip = false;
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
@@ -1607,8 +1609,15 @@ struct clg_engine {
     reset_result(out);
     host_tiles(p);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    // the plan: in the launch's arguments when it fits (no copy queued), else one copy
+    const bool arg_plan = nt <= clg::kZSmallArgTiles && ns <= clg::kZSmallArgSpans;
     PlanLayout L;
-    CHK(stage_plan(p, d_ztiles, &L));
+    if (arg_plan) {
+      memcpy(small_arg.tiles, p.tiles.data(), size_t(nt) * sizeof(clg::TileDesc));
+      memcpy(small_arg.spans, p.spans.data(), size_t(ns) * sizeof(clg::SpanDesc));
+    } else {
+      CHK(stage_plan(p, d_ztiles, &L));
+    }
     // outputs: the caller's device arrays, or pinned host memory the kernel writes directly
     clg::DecodeOut o{};
     const bool host = out->out_kind != CLG_MEM_DEVICE;
@@ -1629,9 +1638,10 @@ struct clg_engine {
     }
     // scratch: per-tile counts and record-start bitmaps, per-span look-back words
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
-    CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
+    CHK(h_small_res.ensure((4 + size_t(ns)) * 8));
     uint64_t* res = h_small_res.as<uint64_t>();
     res[0] = res[1] = res[2] = 0;
+    res[3 + ns] = 0;  // waves done
     // look-back words: two buffers of kSmallSpans, zeroed once; each call zeroes the other
     if (!d_small.p) {
       CHK(d_small.ensure((2 * size_t(kSmallSpans) + clg::kZSmallTiles * size_t(kSmallSpans)) * 8));
@@ -1645,7 +1655,11 @@ struct clg_engine {
     ctl.cnt = cnt;
     ctl.bits = d_zbits.as<uint64_t>();
     ctl.n_tiles = nt;
-    ctl.warm = spec_warm(false);
+    static const int small_warm = [] {  // developer switch: the small path's warm-up bytes
+      const char* v = getenv("CLONOS_SMALL_WARM");
+      return v ? atoi(v) : -1;
+    }();
+    ctl.warm = small_warm >= 0 ? uint32_t(small_warm) : spec_warm(false);
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
       CHK(d_prof.ensure(size_t(ns + nt) * 64));
@@ -1653,7 +1667,7 @@ struct clg_engine {
       ctl.prof = d_prof.as<uint64_t>();
     }
     std::optional<HostTimer> hsub(std::in_place, this, "host_small_submit");  // (CLONOS_HOST_PROF sub-stages)
-    HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
+    if (!arg_plan) HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     hipEvent_t ea = nullptr, eb = nullptr;
     if (timing) {
@@ -1663,10 +1677,25 @@ struct clg_engine {
     }
     CHK(clg::launch_decode_small(reinterpret_cast<const clg::TileDesc*>(d_plan.p), nt,
                                  reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
-                                 agg, agg_next, res, stream));
+                                 agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     hsub.emplace(this, "host_small_wait");
-    HIPCHK(hipStreamSynchronize(stream));
+    // wait: every wave counts itself done after its last store (system-scope release), so
+    // polling that word returns sooner than the stream's completion signal; the stream stays
+    // ordered for what follows.  Events (timing) and diagnostics wait on the stream.
+    bool polled = false;
+    if (!timing && !sprof) {
+      volatile uint64_t* done = res + 3 + ns;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t k = 0;; ++k) {
+        if (__atomic_load_n(const_cast<uint64_t*>(done), __ATOMIC_ACQUIRE) >= ns) {
+          polled = true;
+          break;
+        }
+        if ((k & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
+      }
+    }
+    if (!polled) HIPCHK(hipStreamSynchronize(stream));
     hsub.emplace(this, "host_small_finish");
     if (sprof) {
       std::vector<uint64_t> hp(size_t(ns + nt) * 8);

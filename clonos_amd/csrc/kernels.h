@@ -241,13 +241,23 @@ uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 // publishes its counts, sums every earlier span's (look-back), emits.  Spans of at most
 // kZSmallTiles tiles, batches without Serializable tables.  Results go to `res` (host-mapped
 // pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any span failed
-// (the host then decodes the batch the usual way), res[3 + s] span s's first record.  agg:
-// kZSmallSpans zeroed words; the kernel zeroes all of agg_next for the next call (the host
-// alternates two buffers, so no memset is queued).
+// (the host then decodes the batch the usual way), res[3 + s] span s's first record,
+// res[3 + n_spans] the number of waves done (each adds 1 with a system-scope release after its
+// last store: the host may poll it instead of waiting on the stream).  agg: kZSmallSpans zeroed
+// words; the kernel zeroes all of agg_next for the next call (the host alternates two buffers,
+// so no memset is queued).  plan (host memory, optional): a plan of at most kZSmallArgTiles
+// tiles and kZSmallArgSpans spans goes in the launch's own arguments instead of d_tiles /
+// d_spans, so no copy is queued before the launch.
 constexpr uint32_t kZSmallTiles = 8;
 constexpr uint32_t kZSmallSpans = 4096;  // spans per small batch at most (look-back buffer size)
+constexpr uint32_t kZSmallArgTiles = 64, kZSmallArgSpans = 64;
+struct SmallPlanArg {  // 3 KiB: with the other arguments inside the 4 KiB kernel-argument limit
+  TileDesc tiles[kZSmallArgTiles];
+  SpanDesc spans[kZSmallArgSpans];
+};
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
-                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream);
+                        FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
+                        const SmallPlanArg* plan = nullptr);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one
