@@ -11,6 +11,7 @@ exception: CorruptDeterminantArrayException, RuntimeException("Consumer went bac
 from __future__ import annotations
 
 import ctypes as C
+import sys
 from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -144,6 +145,8 @@ class Engine:
         h = C.c_void_p()
         check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))
         self._h = h
+        self._out_buf: Optional[np.ndarray] = None  # _pooled_outputs
+        self._out_cache = None
         self.segment_bytes = segment_bytes
         self.sharing_depth = sharing_depth
         self.async_slice = async_slice
@@ -293,16 +296,47 @@ class Engine:
         return bool(applied.value)
 
     # ---- decode -------------------------------------------------------------------------
+    # (name, dtype, itemsize, side table?) of clg_decoded's host arrays
+    _OUT_FIELDS = (("off", np.uint32, 4, 0), ("tag", np.uint8, 1, 0), ("v0", np.int64, 8, 0), ("w_idx", np.uint32, 4, 1),
+                   ("w_rc", np.int32, 4, 1), ("w_v1", np.int64, 8, 1), ("w_var_off", np.uint32, 4, 1),
+                   ("w_var_len", np.uint32, 4, 1), ("w_sub", np.uint8, 1, 1))
+
     @staticmethod
-    def _host_outputs(cap: int, wcap: int):
-        arrs = dict(off=np.empty(cap, np.uint32), tag=np.empty(cap, np.uint8), v0=np.empty(cap, np.int64),
-                    w_idx=np.empty(wcap, np.uint32), w_rc=np.empty(wcap, np.int32), w_v1=np.empty(wcap, np.int64),
-                    w_var_off=np.empty(wcap, np.uint32), w_var_len=np.empty(wcap, np.uint32),
-                    w_sub=np.empty(wcap, np.uint8))
+    def _host_outputs(cap: int, wcap: int, buf: Optional[np.ndarray] = None):
+        """The SoA output arrays as views of one host buffer (one allocation, one pointer),
+        and their clg_decoded.  buf: a buffer to carve them from (large enough), else a new one."""
+        offs, at = [], 0
+        for _, _, isz, wide in Engine._OUT_FIELDS:
+            offs.append(at)
+            at = (at + isz * (wcap if wide else cap) + 15) & ~15
+        if buf is None or buf.size < at:
+            buf = np.empty(max(at, 16), np.uint8)
+        b0 = buf.ctypes.data
         d = _lib.Decoded()
-        for k, a in arrs.items():
-            setattr(d, k, _np_ptr(a))
+        arrs = {}
+        for (k, dt, isz, wide), o in zip(Engine._OUT_FIELDS, offs):
+            arrs[k] = buf[o:o + isz * (wcap if wide else cap)].view(dt)
+            setattr(d, k, b0 + o)
         d.cap, d.wcap, d.out_kind = cap, wcap, _lib.CLG_MEM_HOST
+        return d, arrs
+
+    def _pooled_outputs(self, cap: int, wcap: int):
+        """_host_outputs from the engine's reusable buffer when no earlier result still holds
+        it (every returned array is a view of it, so a live batch keeps its reference count up):
+        its pages stay mapped, so the outputs are not page-faulted in again on every call, and
+        for the same capacities the views and clg_decoded of the last call serve again."""
+        buf, key = self._out_buf, (cap, wcap)
+        # references when free: the attribute, `buf`, getrefcount's argument, the 9 cached views
+        if buf is not None and sys.getrefcount(buf) > 3 + len(self._OUT_FIELDS):
+            buf = self._out_buf = self._out_cache = None
+        if buf is not None and self._out_cache is not None and self._out_cache[0] == key:
+            d, arrs = self._out_cache[1], self._out_cache[2]
+            d.n_rec = d.n_wide = 0
+            return d, arrs
+        self._out_cache = None  # (its views would hold the old buffer)
+        d, arrs = self._host_outputs(cap, wcap, buf)
+        self._out_buf = arrs["off"].base
+        self._out_cache = (key, d, arrs)
         return d, arrs
 
     def _finish(self, st, d, arrs, base, n_spans, spans_bytes):
@@ -327,7 +361,7 @@ class Engine:
         sl = np.array([s[1] for s in spans], np.uint64)
         cap = int(sl.sum()) // 2 + len(spans) + 1
         wcap = int(sl.sum()) // 6 + len(spans) + 1
-        d, arrs = self._host_outputs(cap, wcap)
+        d, arrs = self._pooled_outputs(cap, wcap)
         base = np.zeros(len(spans) + 1, np.uint64)
         st = lib.clg_decode_host(self._h, _np_ptr(buf), _np_ptr(so), _np_ptr(sl), len(spans), C.byref(d),
                                  _np_ptr(base))
@@ -341,7 +375,7 @@ class Engine:
         total = self.log_lengths(h)[1]  # logLength bounds every span (one native call for the batch)
         cap = total // 2 + len(logs) + 1
         wcap = total // 6 + len(logs) + 1
-        d, arrs = self._host_outputs(cap, wcap)
+        d, arrs = self._pooled_outputs(cap, wcap)
         base = np.zeros(len(logs) + 1, np.uint64)
         st = lib.clg_decode_logs(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base))
         sb = [np.frombuffer(l.getDeterminants(e), np.uint8) for l, e in zip(logs, start_epochs)] if keep_bytes else None
@@ -352,7 +386,7 @@ class Engine:
         h = np.array([l.handle for l in logs], np.uint32)
         ep = np.array(start_epochs, np.int64)
         total = self.log_lengths(h)[1]
-        d, arrs = self._host_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
+        d, arrs = self._pooled_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
         base = np.zeros(len(logs) + 1, np.uint64)
         pd = PendingDecode(self, (h, ep, d, arrs, base), len(logs))
         check(lib.clg_decode_logs_async(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base)))
@@ -455,7 +489,7 @@ class Engine:
         winner = np.zeros(max(len(blobs), 1), np.uint32)
         nk = C.c_uint32()
         total = int(lens.sum())
-        d, arrs = self._host_outputs(total // 2 + len(blobs) + 1, total // 6 + len(blobs) + 1)
+        d, arrs = self._pooled_outputs(total // 2 + len(blobs) + 1, total // 6 + len(blobs) + 1)
         base = np.zeros(len(blobs) + 1, np.uint64)
         st = lib.clg_replay_prep(self._h, _np_ptr(keys), _np_ptr(data), _np_ptr(offs), _np_ptr(lens), len(blobs),
                                  _np_ptr(winner), C.byref(nk), C.byref(d), _np_ptr(base))
