@@ -253,15 +253,21 @@ def main():
     roof = None
     if dom:
         ach = kern[dom]["gbs"]
-        traffic = None
+        # traffic: HBM bytes per launch from the last round profile's PMC passes (not measured
+        # in this run: counters need rocprofv3 --pmc), with where and when they were collected
+        traffic, tsrc = None, None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
             try:
-                traffic = json.load(open(pmc_path)).get(dom)
+                pt = json.load(open(pmc_path))
+                kt = pt.get("kernels", pt)
+                traffic = kt.get(dom)
+                tsrc = {"file": "profiles/pmc_traffic.json", "git_head": pt.get("git_head"), "date": pt.get("date"),
+                        "tag": pt.get("tag"), "measured_in_this_run": False}
             except Exception:
                 traffic = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic}
+                "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic, "traffic_source": tsrc}
     # decode pipeline as a whole (HIP events from its first kernel's start to emit's end, on
     # the engine's stream) against its algorithmic bytes
     dec_ms = kern_iso["decode_pipeline"]["avg_ms"] if "decode_pipeline" in kern_iso else None

@@ -496,13 +496,178 @@ __device__ __forceinline__ SpecR lm_spec_walk(const uint32_t* M, uint32_t ws, ui
   return s;
 }
 
+// ---------------------------------------------------------------------------------
+// Two chains per lane in lockstep (CLG_SPEC_PAIR).  A walk step is one dependent LDS read
+// and a few VALU, so a lane's walk is a chain of read latencies.  The region's two 64-byte
+// halves are walked at once: chain A warms up before rs and walks the low half, chain B warms
+// up before the high half (wsb; its warm-up covers the low half's bytes) and walks the high
+// half; each step issues both reads before using either.  Where A's exit is a start of B's
+// chain the two are one chain from there on (a step is a function of the position), so the
+// region's bitmaps are A's low half and B's high half from that start: the result equals
+// spec_walk_t's exactly.  Where it is not (B's warm-up did not meet A's chain), A goes on
+// through the high half alone, as spec_walk_t would.
+// ---------------------------------------------------------------------------------
+#ifndef CLG_SPEC_PAIR
+#define CLG_SPEC_PAIR 1
+#endif
+// the lean warm-up step: fixed-length tags, one byte past wide ones
+__device__ __forceinline__ uint32_t warm_len(uint32_t tg) {
+  constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
+  constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
+  const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
+  return L > 1u ? L : 1u;
+}
+// spec_step's length rule for a tag already read (0: step one byte); *wide for a wide record
+template <bool J, bool SAFE>
+__device__ __forceinline__ uint32_t spec_len_tag(const uint32_t* T, uint32_t q, uint32_t tg, uint32_t end_a, const JL& jl,
+                                                 bool* wide) {
+  constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16 | (J ? 0x40u : 0u) << 24;  // tags 0..3
+  constexpr uint32_t kHi = 0x40u | 0x40u << 8 | 0x40u << 16 | 5u << 24;       // tags 4..7
+  const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
+  uint32_t L = c;
+  *wide = false;
+  if (c >= 0x40u) {  // rare: the length needs fields of the record
+    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
+      L = 13;
+    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
+      L = jl_len(jl, q);
+      L = L <= (uint32_t)kZSpecMax ? L : 0u;
+    } else {
+      L = zspec_var(T, q, end_a, tg);
+    }
+    if (!SAFE) L = q + L <= end_a ? L : 0u;
+    *wide = L != 0u;
+  } else if (!SAFE) {
+    L = q + L <= end_a ? L : 0u;
+  }
+  return L;
+}
+// the region's bitmaps from chain A (low half, exit qa) and chain B (high half from mid, its
+// exit qb), or A continued through the high half (step(q, sb, wb) -> next q)
+template <class Step>
+__device__ __forceinline__ SpecR pair_join(SpecR s, uint32_t mid, uint32_t re, uint32_t r0, uint32_t qa, uint32_t qb,
+                                           uint64_t sba, uint64_t wba, uint64_t sbb, uint64_t wbb, Step&& step) {
+  s.sb.lo = sba;
+  s.wb.lo = wba;
+  if (qa >= re) {  // A's last record reaches past the region: no start of the high half is A's
+    s.sb.hi = s.wb.hi = 0;
+    s.exit = qa;
+  } else if ((sbb >> (qa - mid)) & 1ull) {  // A meets B at qa: B's chain from there
+    const uint64_t m = ~0ull << (qa - mid);
+    s.sb.hi = sbb & m;
+    s.wb.hi = wbb & m;
+    s.exit = qb;
+  } else {  // B's warm-up missed A's chain: A alone through the high half (rare)
+    uint64_t sh = 0, wh = 0;
+    uint32_t q = qa;
+    while (q < re) q = step(q, sh, wh);
+    s.sb.hi = sh;
+    s.wb.hi = wh;
+    s.exit = q;
+  }
+  s.bad = spec_bad(s, r0);
+  return s;
+}
+template <bool J, bool SAFE>
+__device__ __forceinline__ SpecR spec_walk_pair(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
+                                                uint32_t end_a, uint32_t r0, const JL& jl) {
+  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
+  const uint32_t mid = r0 + 64u;  // (the caller: rs < mid < re)
+  uint32_t qa = ws, qb = wsb;
+  while (qa < rs || qb < mid) {  // both warm-ups
+    const uint32_t ta = zb8(T, qa < rs ? qa : rs), tb = zb8(T, qb < mid ? qb : mid);
+    qa = qa < rs ? qa + warm_len(ta) : qa;
+    qb = qb < mid ? qb + warm_len(tb) : qb;
+  }
+  s.first = qa;
+  uint64_t sba = 0, wba = 0, sbb = 0, wbb = 0;
+  while (qa < mid || qb < re) {  // A over the low half, B over the high half
+    const bool ia = qa < mid, ib = qb < re;
+    const uint32_t pa = ia ? qa : rs, pb = ib ? qb : mid;
+    const uint32_t ta = zb8(T, pa), tb = zb8(T, pb);
+    bool wa, wb;
+    const uint32_t La = spec_len_tag<J, SAFE>(T, pa, ta, end_a, jl, &wa);
+    const uint32_t Lb = spec_len_tag<J, SAFE>(T, pb, tb, end_a, jl, &wb);
+    const uint64_t ma = ia ? 1ull << (qa & 63u) : 0ull, mb = ib ? 1ull << (qb & 63u) : 0ull;
+    sba |= ma;
+    sbb |= mb;
+    wba |= wa ? ma : 0ull;
+    wbb |= wb ? mb : 0ull;
+    qa = ia ? qa + (La > 1u ? La : 1u) : qa;
+    qb = ib ? qb + (Lb > 1u ? Lb : 1u) : qb;
+  }
+  return pair_join(s, mid, re, r0, qa, qb, sba, wba, sbb, wbb, [&](uint32_t q, uint64_t& sh, uint64_t& wh) {
+    return spec_step<J, SAFE>(T, q, end_a, jl, sh, wh);
+  });
+}
+// the same over the step-code map (lm_spec_walk's rule)
+__device__ __forceinline__ SpecR lm_spec_walk_pair(const uint32_t* M, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
+                                                   uint32_t r0) {
+  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
+  const uint32_t mid = r0 + 64u;
+  uint32_t qa = ws, qb = wsb;
+  while (qa < rs || qb < mid) {
+    const uint32_t ca = lm8(M, qa < rs ? qa : rs) & 0x7Fu, cb = lm8(M, qb < mid ? qb : mid) & 0x7Fu;
+    qa = qa < rs ? qa + (ca > 1u ? ca : 1u) : qa;
+    qb = qb < mid ? qb + (cb > 1u ? cb : 1u) : qb;
+  }
+  s.first = qa;
+  uint64_t sba = 0, wba = 0, sbb = 0, wbb = 0;
+  while (qa < mid || qb < re) {
+    const bool ia = qa < mid, ib = qb < re;
+    const uint32_t ca = lm8(M, ia ? qa : rs), cb = lm8(M, ib ? qb : mid);
+    if (ia) {
+      sba |= 1ull << (qa & 63u);
+      wba |= (uint64_t)(ca >> 7) << (qa & 63u);
+      qa += (ca & 0x7Fu) > 1u ? (ca & 0x7Fu) : 1u;
+    }
+    if (ib) {
+      sbb |= 1ull << (qb & 63u);
+      wbb |= (uint64_t)(cb >> 7) << (qb & 63u);
+      qb += (cb & 0x7Fu) > 1u ? (cb & 0x7Fu) : 1u;
+    }
+  }
+  return pair_join(s, mid, re, r0, qa, qb, sba, wba, sbb, wbb,
+                   [&](uint32_t q, uint64_t& sh, uint64_t& wh) { return lm_step(M, q, sh, wh); });
+}
+
+#ifndef CLG_SPEC_PAIR_CHECK
+#define CLG_SPEC_PAIR_CHECK 0  // developer check: every paired walk against the single one (printf)
+#endif
 template <bool J>
-__device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
-                                                uint32_t r0, const JL& jl) {
-  if (J && jl.lm) return lm_spec_walk(jl.lm, ws, rs, re, r0);
+__device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
+                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair);
+#if CLG_SPEC_PAIR_CHECK
+__device__ uint32_t g_pair_mismatch;
+#endif
+template <bool J>
+__device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
+                                                uint32_t end_a, uint32_t r0, const JL& jl) {
+  // pairs where the region reaches well into its high half
+  const bool pair = CLG_SPEC_PAIR && rs < r0 + 64u && re >= r0 + 80u;
+#if CLG_SPEC_PAIR_CHECK
+  const SpecR a = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair);
+  const SpecR b = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, false);
+  if (a.sb.lo != b.sb.lo || a.sb.hi != b.sb.hi || a.wb.lo != b.wb.lo || a.wb.hi != b.wb.hi || a.first != b.first ||
+      a.exit != b.exit || a.bad != b.bad) {
+    if (atomicAdd(&g_pair_mismatch, 1u) < 8u)
+      printf("[clonos] spec pair mismatch: r0 %u rs %u re %u ws %u wsb %u exit %u/%u first %u/%u bad %u/%u\n", r0, rs,
+             re, ws, wsb, a.exit, b.exit, a.first, b.first, a.bad, b.bad);
+  }
+  return b;
+#else
+  return spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair);
+#endif
+}
+template <bool J>
+__device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
+                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair) {
+  if (J && jl.lm) return pair ? lm_spec_walk_pair(jl.lm, ws, wsb, rs, re, r0) : lm_spec_walk(jl.lm, ws, rs, re, r0);
   // lanes whose records cannot run past the span end (all but the last tile's) skip the test
-  return re + 16u <= end_a ? spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl)
-                           : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
+  if (re + 16u <= end_a)
+    return pair ? spec_walk_pair<J, true>(T, ws, wsb, rs, re, end_a, r0, jl) : spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl);
+  return pair ? spec_walk_pair<J, false>(T, ws, wsb, rs, re, end_a, r0, jl)
+              : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
 }
 
 // True chain from entry e (e >= rs) merged with the speculative chain: walk until the true
@@ -1059,9 +1224,9 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   const uint32_t lo = z.lo, rs = z.rs, re = z.re, end_a = z.end_a;
   // ---- speculative walk of the lane's region (with warm-up), starts in registers (walked:
   // the chunk prologue's walk of this same tile, a function of the tile's bytes only)
-  const uint32_t ws = warm_start(rs, lo, ctl.warm, lane);
+  const uint32_t ws = warm_start(rs, lo, ctl.warm, lane), wsb = warm_start(lane * kZRegion + 64u, lo, ctl.warm, lane);
   const SpecR sp = walked ? *walked
-                          : rs < re ? spec_walk_fast<J>(s_img, ws, rs, re, end_a, lane * kZRegion, jl)
+                          : rs < re ? spec_walk_fast<J>(s_img, ws, wsb, rs, re, end_a, lane * kZRegion, jl)
                                     : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
 
   ZPHASE(2);
@@ -1840,7 +2005,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       if (J && kLm) jl = load_jl_map(ctl, t1 - 1, s_j, lane, s_img, jl_prefetch(ctl, t1 - 1, lane));
       else if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
       const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane);
-      sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, z.rs, z.re, z.end_a, lane * kZRegion, jl)
+      const uint32_t wsb = warm_start(lane * kZRegion + 64u, z.lo, ctl.warm, lane);
+      sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
       x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));

@@ -127,6 +127,17 @@ for k, name in NAMES.items():
     r = pmc["config2"].get(k, {}).get("derived", {})
     if "hbm_bytes" in r:
         traffic[name] = r["hbm_bytes"]
+# provenance: the code the counters were collected on and when (bench.py reports it beside
+# roofline.traffic, which it reads from this file rather than measuring in its own run)
+import datetime, subprocess
+try:
+    head = subprocess.run(["git", "-C", os.path.dirname(prof) or ".", "rev-parse", "--short", "HEAD"],
+                          capture_output=True, text=True, timeout=10).stdout.strip() or None
+except Exception:
+    head = None
+traffic = {"kernels": traffic, "git_head": head, "tag": tag,
+           "date": datetime.datetime.fromtimestamp(os.path.getmtime(f"{src}/bench.json")).strftime("%Y-%m-%d %H:%M"),
+           "source": f"profiles/{tag}_pmc_decode.json (config 2, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
 json.dump(traffic, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
 for cfg in ("config2", "config3"):
     print(cfg)
