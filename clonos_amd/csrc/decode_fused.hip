@@ -2521,6 +2521,36 @@ int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream) {
   return launch_status(hipGetLastError());
 }
 
+// grid (bad spans, 16): block (i, y) takes rows y, y + 16, ... of 256 each of span i
+__global__ __launch_bounds__(256) void k_sf_place(const SfPlace* __restrict__ place, DecodeOut sc, DecodeOut out,
+                                                  FusedCtl ctl) {
+  const SfPlace p = place[blockIdx.x];
+  const uint64_t base = gp(ctl.span_lo)[p.span];
+  const uint64_t R = base & ((1ull << 31) - 1), W = base >> 31;
+  const uint64_t step = 256ull * gridDim.y, first = 256ull * blockIdx.y + threadIdx.x;
+  if (R + p.nrec <= out.cap)
+    for (uint64_t k = first; k < p.nrec; k += step) {
+      gp(out.off)[R + k] = gp(sc.off)[p.rbase + k];
+      gp(out.tag)[R + k] = gp(sc.tag)[p.rbase + k];
+      gp(out.v0)[R + k] = gp(sc.v0)[p.rbase + k];
+    }
+  if (W + p.nwide <= out.wcap)
+    for (uint64_t k = first; k < p.nwide; k += step) {
+      const uint64_t j = p.wbase + k;
+      gp(out.w_idx)[W + k] = gp(sc.w_idx)[j] + (uint32_t)(R - p.rbase);
+      gp(out.w_rc)[W + k] = gp(sc.w_rc)[j];
+      gp(out.w_v1)[W + k] = gp(sc.w_v1)[j];
+      gp(out.w_var_off)[W + k] = gp(sc.w_var_off)[j];
+      gp(out.w_var_len)[W + k] = gp(sc.w_var_len)[j];
+      gp(out.w_sub)[W + k] = gp(sc.w_sub)[j];
+    }
+}
+int launch_sf_place(const SfPlace* d_place, uint32_t n_bad, DecodeOut scratch, DecodeOut out, FusedCtl ctl, void* stream) {
+  if (!n_bad) return CLG_OK;
+  hipLaunchKernelGGL(k_sf_place, dim3(n_bad, 16), dim3(256), 0, (hipStream_t)stream, d_place, scratch, out, ctl);
+  return launch_status(hipGetLastError());
+}
+
 uint32_t decode_count_grid(bool jser, uint32_t n_tiles) {
   constexpr int kMaxDev = 64;
   static int resident[kMaxDev][2] = {};  // per device: blocks the device keeps resident for the count kernel

@@ -1079,14 +1079,14 @@ struct clg_engine {
     uint32_t n_tiles = 0;
     uint32_t n_tiny = 0;                // whole spans of one tile and at most kZTinySpan bytes
     uint32_t unit = 0;                  // device-planning tile window
-    int64_t only = -1;                  // >= 0: plan only this span of the batch (as span 0)
+    const std::vector<uint32_t>* only = nullptr;  // plan only these spans (ascending), as spans 0, 1, ...
     void reset() {  // empty, capacity kept (a config-4 plan is ~4 MB: fresh pages cost page faults)
       tiles.clear();
       spans.clear();
       runs.clear();
       segtab.clear();
       n_tiles = n_tiny = unit = 0;
-      only = -1;
+      only = nullptr;
     }
   };
   // clg_decode_logs' plan and log ranges, kept between calls for their capacity
@@ -1094,9 +1094,10 @@ struct clg_engine {
   std::vector<int32_t> zst, znb;
   // Span filter of a plan (the per-span fallback re-decodes single spans): false = skip.
   static bool plan_keep(const DecodePlan& p, uint32_t* s) {
-    if (p.only < 0) return true;
-    if (*s != uint32_t(p.only)) return false;
-    *s = 0;
+    if (!p.only) return true;
+    const auto it = std::lower_bound(p.only->begin(), p.only->end(), *s);
+    if (it == p.only->end() || *it != *s) return false;
+    *s = uint32_t(it - p.only->begin());
     return true;
   }
 
@@ -1577,7 +1578,7 @@ struct clg_engine {
   bool small_flip = false;
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
-        p.only >= 0)
+        p.only)
       return false;
     if (out->out_kind != CLG_MEM_DEVICE && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     for (const auto& sd : p.spans)
@@ -1775,14 +1776,17 @@ struct clg_engine {
     return run_decode(p, log_bytes, out, span_rec_base);
   }
 
-  // Per-span fallback after a fast run whose chains went wrong in a few spans only (a
-  // decode error, a record the fast rules cannot place): those spans are decoded one by one
-  // by the robust pipeline into scratch, their counts injected into the fast run's per-tile
-  // counts, scan and emit re-run for the other spans (emit skips the bad ones), and the
-  // robust records copied into place (their wide rows' record indices moved by the span's
-  // record base).  *done = false: not applicable (too many or too large bad spans), the
+  // Per-span fallback after a fast run whose chains went wrong in some spans only (a
+  // decode error, a record the fast rules cannot place): those spans are decoded together in
+  // one robust run into scratch, their counts injected into the fast run's per-tile counts,
+  // scan and emit re-run for the other spans (emit skips the bad ones), and the robust
+  // records placed by one kernel (k_sf_place; their wide rows' record indices moved to the
+  // batch's).  *done = false: not applicable (too many or too large bad spans), the
   // caller decodes the whole batch robustly.  The result equals the whole-batch robust
   // decode's: every span's records, the first error of the lowest span.
+  // at most this many bad spans, and three quarters of the bytes: past that the whole batch
+  // goes robust (one run either way; the fast run's second half is the saving)
+  static constexpr uint32_t kSfMaxSpans = 8192;
   template <class Build>
   int span_fallback(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                     bool* done) {
@@ -1797,16 +1801,11 @@ struct clg_engine {
         bad.push_back(s);
         bad_bytes += pf.spans[s].len;
       }
-    if (bad.empty() || bad.size() > 64 || bad_bytes > log_bytes / 4) return CLG_OK;
+    if (bad.empty() || bad.size() > kSfMaxSpans || bad_bytes > log_bytes / 4 * 3) return CLG_OK;
     stats["decode_span_fallback"].launches++;
     const uint32_t nb = uint32_t(bad.size());
-    // scratch: per bad span the robust decode's records (13 B) and wide rows (25 B)
-    std::vector<uint64_t> rec_at(nb + 1, 0), wide_at(nb + 1, 0);
-    for (uint32_t i = 0; i < nb; ++i) {
-      rec_at[i + 1] = rec_at[i] + pf.spans[bad[i]].len / 2 + 1;
-      wide_at[i + 1] = wide_at[i] + pf.spans[bad[i]].len / 6 + 1;
-    }
-    const uint64_t RC = rec_at[nb], WC = wide_at[nb];
+    // scratch: the robust decode's records (13 B) and wide rows (25 B) of the bad spans
+    const uint64_t RC = bad_bytes / 2 + nb + 1, WC = bad_bytes / 6 + nb + 1;  // (records are >= 2 B, wide >= 6 B)
     CHK(d_sf_rec.ensure(RC * 13 + 64));
     CHK(d_sf_wide.ensure(WC * 25 + 64));
     uint8_t* rb = d_sf_rec.as<uint8_t>();
@@ -1820,53 +1819,63 @@ struct clg_engine {
     auto* s_wvl = s_wvo + WC;
     auto* s_wv1 = reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(s_wvl + WC) + 8 - (uintptr_t(s_wvl + WC) & 7));
     auto* s_wsub = reinterpret_cast<uint8_t*>(s_wv1 + WC);
-    std::vector<uint64_t> packed(nb), nrec(nb), nwide(nb);
+    std::vector<uint64_t> packed(nb), nrec(nb), nwide(nb), rbase(nb), wbase(nb);
     int e_status = CLG_OK, e_tag = 0;
     uint32_t e_span = 0;
     int64_t e_off = -1;
-    for (uint32_t i = 0; i < nb; ++i) {
+    {  // every bad span in ONE robust run (spans 0 .. nb-1 of its plan), into scratch
       DecodePlan sp;
-      sp.only = bad[i];
+      sp.only = &bad;
       build(sp, uint32_t(clg::kTile));
       clg_decoded so{};
-      so.off = s_off + rec_at[i];
-      so.tag = s_tag + rec_at[i];
-      so.v0 = s_v0 + rec_at[i];
-      so.w_idx = s_widx + wide_at[i];
-      so.w_rc = s_wrc + wide_at[i];
-      so.w_v1 = s_wv1 + wide_at[i];
-      so.w_var_off = s_wvo + wide_at[i];
-      so.w_var_len = s_wvl + wide_at[i];
-      so.w_sub = s_wsub + wide_at[i];
-      so.cap = rec_at[i + 1] - rec_at[i];
-      so.wcap = wide_at[i + 1] - wide_at[i];
+      so.off = s_off;
+      so.tag = s_tag;
+      so.v0 = s_v0;
+      so.w_idx = s_widx;
+      so.w_rc = s_wrc;
+      so.w_v1 = s_wv1;
+      so.w_var_off = s_wvo;
+      so.w_var_len = s_wvl;
+      so.w_sub = s_wsub;
+      so.cap = RC;
+      so.wcap = WC;
       so.out_kind = CLG_MEM_DEVICE;
-      uint64_t sbase[2];
-      const int st = run_decode(sp, pf.spans[bad[i]].len, &so, sbase);
+      const int st = run_decode(sp, bad_bytes, &so, nullptr);
       if (st != CLG_OK && so.err_status == CLG_OK) return st;  // an engine failure, not a decode error
-      if (so.err_status != CLG_OK && e_status == CLG_OK) {     // bad[] ascends: the lowest span's error
+      if (so.err_status != CLG_OK) {  // the lowest bad span's error (bad[] ascends)
         e_status = so.err_status;
-        e_span = bad[i];
+        e_span = bad[so.err_span];
         e_off = so.err_off;
         e_tag = so.err_tag;
       }
-      nrec[i] = so.n_rec;
-      nwide[i] = so.n_wide;
-      if (nrec[i] >= (1ull << 31) || nwide[i] >= (1ull << 32)) return CLG_OK;  // past the fast counts' packing
-      packed[i] = nwide[i] << 31 | nrec[i];
+      // per span: records, wide rows and their places in the scratch (run_decode's span results)
+      const clg::SpanRes* hres = h_sres.as<clg::SpanRes>();
+      for (uint32_t i = 0; i < nb; ++i) {
+        nrec[i] = hres[i].n_rec;
+        nwide[i] = hres[i].n_wide;
+        rbase[i] = hres[i].rec_base;
+        wbase[i] = hres[i].wide_base;
+        if (nrec[i] >= (1ull << 31) || nwide[i] >= (1ull << 32)) return CLG_OK;  // past the fast counts' packing
+        packed[i] = nwide[i] << 31 | nrec[i];
+      }
     }
     // the fast run again over the good spans: its plan back in place (the robust runs used
     // the shared span table), the bad spans' counts injected, scan and emit
     PlanLayout L;
     CHK(stage_plan(pf, d_ztiles, &L));
     CHK(enqueue_plan(pf, L, d_ztiles));
-    CHK(d_sf_meta.ensure(size_t(nb) * 12 + 64));
-    std::vector<uint8_t> meta(size_t(nb) * 12 + 8);
+    // meta: the packed counts, the bad spans, then the placement rows (16-byte aligned)
+    const size_t o_place = (size_t(nb) * 12 + 15) & ~size_t(15), mb = o_place + size_t(nb) * sizeof(clg::SfPlace);
+    CHK(d_sf_meta.ensure(mb + 64));
+    std::vector<uint8_t> meta(mb + 8);
     memcpy(meta.data(), packed.data(), size_t(nb) * 8);
     memcpy(meta.data() + size_t(nb) * 8, bad.data(), size_t(nb) * 4);
-    HIPCHK(hipMemcpyAsync(d_sf_meta.p, meta.data(), size_t(nb) * 12, hipMemcpyHostToDevice, stream));
+    auto* pl = reinterpret_cast<clg::SfPlace*>(meta.data() + o_place);
+    for (uint32_t i = 0; i < nb; ++i) pl[i] = clg::SfPlace{rbase[i], nrec[i], wbase[i], nwide[i], bad[i], 0};
+    HIPCHK(hipMemcpyAsync(d_sf_meta.p, meta.data(), mb, hipMemcpyHostToDevice, stream));
     clg::FusedCtl ctl = zlast.ctl;
     ctl.skip_bad = 1;
+    ctl.chunk = nullptr;  // (the count pass's chunk table is not staged again: scan and emit never read it)
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
     CHK(clg::launch_decode_inject(zs, reinterpret_cast<const uint32_t*>(d_sf_meta.as<uint8_t>() + size_t(nb) * 8),
@@ -1874,31 +1883,15 @@ struct clg_engine {
     HIPCHK(hipMemsetAsync(ctl.abort, 0, 32, stream));
     CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, zlast.o, stream, 1));
     CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, zlast.o, stream, 2));
+    // the robust records into place, at the bases the scan gave the bad spans (one launch)
+    const clg::DecodeOut sc{s_off, s_tag, s_v0, s_widx, s_wrc, s_wv1, s_wvo, s_wvl, s_wsub, RC, WC};
+    CHK(clg::launch_sf_place(reinterpret_cast<const clg::SfPlace*>(d_sf_meta.as<uint8_t>() + o_place), nb, sc, zlast.o,
+                             ctl, stream));
     uint64_t* hz = h_zres.as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     if (reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns))[0]) return CLG_OK;  // (cannot happen) whole batch
-    // the robust records into place
     constexpr uint64_t kRecMask = (1ull << 31) - 1;
-    const clg::DecodeOut& o = zlast.o;
-    for (uint32_t i = 0; i < nb; ++i) {
-      const uint64_t R = hz[bad[i]] & kRecMask, W = hz[bad[i]] >> 31;
-      if (nrec[i] && R + nrec[i] <= o.cap) {
-        HIPCHK(hipMemcpyAsync(o.off + R, s_off + rec_at[i], nrec[i] * 4, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.tag + R, s_tag + rec_at[i], nrec[i], hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.v0 + R, s_v0 + rec_at[i], nrec[i] * 8, hipMemcpyDeviceToDevice, stream));
-      }
-      if (nwide[i] && W + nwide[i] <= o.wcap) {
-        const uint64_t w = wide_at[i], n = nwide[i];
-        HIPCHK(hipMemcpyAsync(o.w_idx + W, s_widx + w, n * 4, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.w_rc + W, s_wrc + w, n * 4, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.w_v1 + W, s_wv1 + w, n * 8, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.w_var_off + W, s_wvo + w, n * 4, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.w_var_len + W, s_wvl + w, n * 4, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(o.w_sub + W, s_wsub + w, n, hipMemcpyDeviceToDevice, stream));
-        CHK(clg::launch_add_u32(o.w_idx + W, n, uint32_t(R), stream));  // span-local -> batch record index
-      }
-    }
     uint64_t tr = 0, tw = 0;
     for (uint32_t s = 0; s < ns; ++s) {
       if (span_rec_base) span_rec_base[s] = tr;

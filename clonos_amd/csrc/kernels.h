@@ -231,6 +231,14 @@ int launch_decode_inject(const SpanDesc* d_spans, const uint32_t* d_bad, const u
                          FusedCtl ctl, void* stream);
 // x[i] += delta for i < n (the robust output's wide-row record indices moved into place).
 int launch_add_u32(uint32_t* d_x, uint64_t n, uint32_t delta, void* stream);
+// Per-span fallback, last step: bad span i's robust records (scratch rows [rbase, rbase + nrec),
+// wide rows [wbase, wbase + nwide)) into the batch output at the span's bases from the re-run
+// scan (ctl.span_lo), the wide rows' record indices moved by (batch base - rbase).
+struct SfPlace {
+  uint64_t rbase, nrec, wbase, nwide;
+  uint32_t span, pad;
+};
+int launch_sf_place(const SfPlace* d_place, uint32_t n_bad, DecodeOut scratch, DecodeOut out, FusedCtl ctl, void* stream);
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 // The count pass's grid for n_tiles tiles (the blocks the device keeps resident, at most one

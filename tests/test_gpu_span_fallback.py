@@ -1,0 +1,86 @@
+"""GPU: the per-span fallback with many bad spans -- every bad span in ONE robust run, the
+records placed by one kernel (engine.cpp span_fallback, decode_fused.hip k_sf_place).  A
+config-3-like batch where a third of the spans hold a decode error (an invalid tag, a
+truncated record, a bad enum, a negative name length) is decoded by the fast path with the
+fallback and by the robust pipeline alone: every output array, every span's record base and
+the first error (status, span, offset, tag) are identical, and the oracle agrees with each
+good span.  SimpleDeterminantEncoder.decodeNext (:78-342)."""
+import numpy as np
+import pytest
+
+import _oracle as O
+from clonos_amd import Engine, _lib, synth
+from clonos_amd import determinants as D
+from clonos_amd._lib import lib
+from clonos_amd.engine import _np_ptr
+
+pytestmark = pytest.mark.gpu
+
+
+def _corrupt(b: bytes, offs, rng, kind: int) -> bytes:
+    k = int(offs[int(rng.integers(1, max(2, len(offs) - 1)))])
+    if kind == 0:  # an invalid tag where a record starts
+        return b[:k] + b"\x0b" + b[k:]
+    if kind == 1:  # a record past the span end
+        return b + D.encode(D.TimestampDeterminant(3))[:6]
+    if kind == 2:  # a TimerTrigger with an out-of-range type ordinal (bad enum)
+        r = bytearray(D.encode(D.TimerTriggerDeterminant(1, 2, D.INTERNAL, b"x")))
+        r[13] = 9
+        return b[:k] + bytes(r) + b[k:]
+    r = bytearray(D.encode(D.TimerTriggerDeterminant(1, 2, 6, b"abcd")))  # a negative name length
+    r[14:18] = (0xFFFFFFF0).to_bytes(4, "big")
+    return b[:k] + bytes(r) + b[k:]
+
+
+def _raw_decode(eng, blob, spans):
+    buf = np.frombuffer(blob, np.uint8)
+    so = np.array([s[0] for s in spans], np.uint64)
+    sl = np.array([s[1] for s in spans], np.uint64)
+    cap, wcap = int(sl.sum()) // 2 + len(spans) + 1, int(sl.sum()) // 6 + len(spans) + 1
+    d, arrs = Engine._host_outputs(cap, wcap)
+    base = np.zeros(len(spans) + 1, np.uint64)
+    st = lib.clg_decode_host(eng.handle, _np_ptr(buf), _np_ptr(so), _np_ptr(sl), len(spans), _lib.C.byref(d),
+                             _np_ptr(base))
+    nr, nw = d.n_rec, d.n_wide
+    return (st, d.err_status, d.err_span, d.err_off, d.err_tag, nr, nw,
+            {k: v[:nr if k in ("off", "tag", "v0") else nw].copy() for k, v in arrs.items()}, base.copy())
+
+
+@pytest.mark.parametrize("n_spans,every", [(60, 3), (600, 5)])
+def test_many_bad_spans_equal_robust(n_spans, every):
+    rng = np.random.default_rng(n_spans)
+    spans_b, bad = [], []
+    for i in range(n_spans):
+        b, offs = synth.config3_epoch(int(rng.integers(300, 3000)), rng)
+        b = b.tobytes()
+        if i % every == 1:
+            b = _corrupt(b, offs, rng, len(bad) % 4)
+            bad.append(i)
+        spans_b.append(b)
+    blob, spans = b"", []
+    for b in spans_b:
+        spans.append((len(blob), len(b)))
+        blob += b
+    res = {}
+    for mode in ("three_pass", "robust"):
+        with Engine(segment_bytes=16384, pool_segments=1 << 12, timing=True, decode=mode) as eng:
+            res[mode] = _raw_decode(eng, blob, spans)
+            if mode == "three_pass":
+                ks = eng.kernel_stats()
+                assert "decode_span_fallback" in ks and "decode_fallback" not in ks, ks
+    a, r = res["three_pass"], res["robust"]
+    assert a[0] != 0 and a[:7] == r[:7]  # status, error fields, record and wide-row counts
+    assert a[2] == bad[0]  # the lowest bad span's error
+    for k in a[7]:
+        np.testing.assert_array_equal(a[7][k], r[7][k], err_msg=k)
+    np.testing.assert_array_equal(a[8], r[8])
+    # every good span against the oracle
+    rec0 = a[8]
+    for s in range(0, n_spans, 7):
+        if s in bad:
+            continue
+        st, rr, _, _ = O.decode(spans_b[s])
+        assert st == 0
+        lo, hi = int(rec0[s]), int(rec0[s + 1])
+        np.testing.assert_array_equal(a[7]["off"][lo:hi], rr["off"])
+        np.testing.assert_array_equal(a[7]["v0"][lo:hi], rr["v0"])
