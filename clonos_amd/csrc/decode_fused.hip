@@ -72,7 +72,7 @@ constexpr int kZWarmUnroll = 4;
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
 #ifndef CLG_EMIT_PAIR
-#define CLG_EMIT_PAIR 2
+#define CLG_EMIT_PAIR 1  // 2 measured the same (config-2 emit 0.220 ms either way, config 3 0.329 / 0.331)
 #endif
 constexpr int kZEmitPair = CLG_EMIT_PAIR;              // emit: records per lane per pass (loads hoisted)
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
@@ -508,7 +508,8 @@ __device__ __forceinline__ SpecR lm_spec_walk(const uint32_t* M, uint32_t ws, ui
 // through the high half alone, as spec_walk_t would.
 // ---------------------------------------------------------------------------------
 #ifndef CLG_SPEC_PAIR
-#define CLG_SPEC_PAIR 1
+#define CLG_SPEC_PAIR 0  // measured slower: config-2 count 0.161 -> 0.209 ms, config 3 0.365 -> 0.45 (the walk is
+                         // issue-bound, not latency-bound: the second chain's VALU cost more than its overlap saved)
 #endif
 // the lean warm-up step: fixed-length tags, one byte past wide ones
 __device__ __forceinline__ uint32_t warm_len(uint32_t tg) {

@@ -1611,7 +1611,11 @@ struct clg_engine {
     host_tiles(p);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     // the plan: in the launch's arguments when it fits (no copy queued), else one copy
-    const bool arg_plan = nt <= clg::kZSmallArgTiles && ns <= clg::kZSmallArgSpans;
+    static const int small_mode = [] {  // developer switch: bit 0 no argument plan, bit 1 no polling
+      const char* v = getenv("CLONOS_SMALL_MODE");
+      return v ? atoi(v) : 0;
+    }();
+    const bool arg_plan = !(small_mode & 1) && nt <= clg::kZSmallArgTiles && ns <= clg::kZSmallArgSpans;
     PlanLayout L;
     if (arg_plan) {
       memcpy(small_arg.tiles, p.tiles.data(), size_t(nt) * sizeof(clg::TileDesc));
@@ -1685,7 +1689,7 @@ struct clg_engine {
     // polling that word returns sooner than the stream's completion signal; the stream stays
     // ordered for what follows.  Events (timing) and diagnostics wait on the stream.
     bool polled = false;
-    if (!timing && !sprof) {
+    if (!timing && !sprof && !(small_mode & 2)) {
       volatile uint64_t* done = res + 3 + ns;
       const auto t0 = std::chrono::steady_clock::now();
       for (uint32_t k = 0;; ++k) {
