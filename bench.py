@@ -526,7 +526,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
     g = table.graph
     failed = failed_vertices(g, np.random.default_rng(0xC1050005))
     dest_of = {v: J.owner_rank(v, world) for v in failed}
-    fg = np.nonzero(np.isin(table.vertex, failed))[0]
+    fg = table.gids_of(failed)
     copies = {}
     for gid in fg:
         h = owned.get(int(gid), -1)

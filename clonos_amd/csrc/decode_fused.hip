@@ -2137,12 +2137,6 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
 // ---------------------------------------------------------------------------------
 constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ull << 62) - 1;
 
-// the wave's outputs are written: count it done (res[3 + n_spans], system scope, release)
-__device__ __forceinline__ void small_done(uint64_t* res, uint32_t n_spans, uint32_t lane) {
-  __syncthreads();  // every lane's stores before lane 0's release
-  if (lane == 0) __hip_atomic_fetch_add(res + 3 + n_spans, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                              uint32_t n_spans, const FusedCtl& ctl, const DecodeOut& out, uint64_t* agg,
                                              uint64_t* agg_next, uint64_t* res) {
@@ -2202,7 +2196,6 @@ __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles,
   }
   if (any_bad) {
     if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    small_done(res, n_spans, lane);
     return;
   }
   stamp(2);
@@ -2227,7 +2220,6 @@ __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles,
       res[1] = b >> 31;
     }
   }
-  small_done(res, n_spans, lane);
 }
 
 __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,

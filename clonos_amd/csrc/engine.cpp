@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -424,6 +425,68 @@ struct XGuard {
   EngineLock& l;
   explicit XGuard(EngineLock& l_) : l(l_) { l.lock(); }
   ~XGuard() { l.unlock(); }
+};
+
+// A few host threads for the per-log loops of very large batches (config 4: 66 k logs per
+// decode, truncation): run(fn) calls fn(part, parts) once per part, the calling thread taking
+// part 0; workers spin briefly for the next job, then sleep.  Jobs only ever come from the
+// holder of the engine lock, one at a time.
+class WorkPool {
+ public:
+  explicit WorkPool(unsigned n) : n_(n ? n : 1) {
+    for (unsigned i = 1; i < n_; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~WorkPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return n_; }
+  void run(const std::function<void(unsigned, unsigned)>& fn) {
+    if (n_ == 1) {
+      fn(0, 1);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &fn;
+      left_.store(n_ - 1, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    fn(0, n_);
+    while (left_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+  }
+
+ private:
+  void loop(unsigned i) {
+    uint64_t seen = 0;
+    for (;;) {
+      // a short spin (the next job of a batch comes within microseconds), then sleep
+      for (int k = 0; k < 20000 && gen_.load(std::memory_order_acquire) == seen; ++k) std::this_thread::yield();
+      const std::function<void(unsigned, unsigned)>* job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+        if (stop_) return;
+        seen = gen_.load(std::memory_order_acquire);
+        job = job_;
+      }
+      (*job)(i, n_);
+      left_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  unsigned n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<unsigned> left_{0};
+  const std::function<void(unsigned, unsigned)>* job_ = nullptr;
+  bool stop_ = false;
 };
 
 }  // namespace
@@ -1091,6 +1154,19 @@ struct clg_engine {
   };
   // clg_decode_logs' plan and log ranges, kept between calls for their capacity
   DecodePlan zplan;
+  // host threads for batches of very many logs (CLONOS_HOST_THREADS, default 8; 1: none)
+  std::unique_ptr<WorkPool> host_pool;
+  WorkPool* workers() {
+    if (!host_pool) {
+      const char* v = getenv("CLONOS_HOST_THREADS");
+      int n = v ? atoi(v) : 8;
+      const int hw = int(std::thread::hardware_concurrency());
+      n = std::max(1, std::min(n, hw > 0 ? hw : 1));
+      host_pool = std::make_unique<WorkPool>(unsigned(n));
+    }
+    return host_pool.get();
+  }
+  static constexpr uint32_t kParallelLogs = 8192;  // logs per batch from which the loops split
   std::vector<int32_t> zst, znb;
   // Span filter of a plan (the per-span fallback re-decodes single spans): false = skip.
   static bool plan_keep(const DecodePlan& p, uint32_t* s) {
@@ -1163,6 +1239,83 @@ struct clg_engine {
     p.n_tiles = uint32_t(p.tiles.size());
   }
 
+  // clg_decode_logs' ranges and device-planned fast plan (plan_log_span's spans, runs and
+  // segment table, in the same order) on the host threads: per part of the logs their ranges
+  // and sizes, then the parts' offsets, then each part writes its entries in place.  false:
+  // not applicable (no device planning) or a log failed -- the caller runs the serial loop,
+  // which reports the error.
+  bool plan_parallel(DecodePlan& p, const uint32_t* log, const int64_t* start_epoch, uint32_t n, uint64_t* total) {
+    const uint32_t U = tile_unit(clg::kZTile), Cb = C();
+    if (!U) return false;
+    WorkPool* wp = workers();
+    const unsigned P = wp->size();
+    struct Part {
+      uint64_t bytes = 0, tiles = 0, runs = 0, segs = 0, tiny = 0;
+      bool bad = false;
+    };
+    std::vector<Part> part(P);
+    std::vector<int32_t>& st = zst;
+    std::vector<int32_t>& nb = znb;
+    const uint32_t per = (n + P - 1) / P;
+    auto cnt_of = [&](int32_t start, int32_t len) -> uint32_t {
+      return len > 0 ? uint32_t(start + len - 1) / U - uint32_t(start) / U + 1 : 0u;
+    };
+    wp->run([&](unsigned k, unsigned) {
+      Part& q = part[k];
+      for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
+        Log* l;
+        if (get_log(log[i], &l) != CLG_OK ||
+            (l->depth != 0 && determinants_range(*l, start_epoch[i], &st[i], &nb[i]) != CLG_OK)) {
+          q.bad = true;
+          return;
+        }
+        const uint32_t c = cnt_of(st[i], nb[i]);
+        q.bytes += uint64_t(nb[i]);
+        q.tiles += c;
+        q.tiny += (c == 1 && uint32_t(nb[i]) <= clg::kZTinySpan) ? 1u : 0u;
+        if (c) {
+          ++q.runs;
+          q.segs += uint32_t(st[i] + nb[i] - 1) / Cb - uint32_t(st[i]) / Cb + 1;
+        }
+      }
+    });
+    std::vector<Part> at(P + 1);
+    for (unsigned k = 0; k < P; ++k) {
+      if (part[k].bad) return false;
+      at[k + 1].bytes = at[k].bytes + part[k].bytes;
+      at[k + 1].tiles = at[k].tiles + part[k].tiles;
+      at[k + 1].runs = at[k].runs + part[k].runs;
+      at[k + 1].segs = at[k].segs + part[k].segs;
+      at[k + 1].tiny = at[k].tiny + part[k].tiny;
+    }
+    if (at[P].tiles >= (1ull << 32)) return false;
+    p.reset();
+    p.unit = U;
+    p.spans.resize(n);
+    p.runs.resize(at[P].runs);
+    p.segtab.resize(at[P].segs);
+    p.n_tiles = uint32_t(at[P].tiles);
+    p.n_tiny = uint32_t(at[P].tiny);
+    wp->run([&](unsigned k, unsigned) {
+      uint64_t tile = at[k].tiles, run = at[k].runs, seg = at[k].segs;
+      for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
+        const Log& l = logs[log[i]];
+        const int32_t start = st[i], len = nb[i];
+        const uint32_t c = cnt_of(start, len);
+        p.spans[i] = clg::SpanDesc{uint32_t(tile), c, uint64_t(len)};
+        if (c) {  // plan_log_span's device-planning entries
+          const uint32_t s0 = uint32_t(start) / Cb, s1 = uint32_t(start + len - 1) / Cb + 1;
+          p.runs[run++] = clg::SegSpan{seg, uint32_t(start) - s0 * Cb, uint32_t(len), i, uint32_t(tile), 0};
+          std::copy(l.segs.begin() + s0, l.segs.begin() + s1, p.segtab.begin() + seg);
+          seg += s1 - s0;
+        }
+        tile += c;
+      }
+    });
+    *total = at[P].bytes;
+    return true;
+  }
+
   static void reset_result(clg_decoded* out) {
     out->n_rec = out->n_wide = 0;
     out->err_status = CLG_OK;
@@ -1202,6 +1355,19 @@ struct clg_engine {
     CHK(h_plan.ensure(L->hb + 64));
     CHK(d_plan.ensure(L->hb));
     uint8_t* hd = h_plan.as<uint8_t>();
+    if (L->hb >= kParallelCopy) {  // a config-4 plan is ~3 MB: the host threads copy it
+      const std::pair<const void*, size_t> part[5] = {
+          {p.tiles.data(), tb}, {p.runs.data(), rb}, {p.segtab.data(), gb}, {p.spans.data(), sb},
+          {cb ? chunk->data() : nullptr, cb}};
+      const size_t dst[5] = {0, L->o_runs, L->o_seg, L->o_spans, L->o_chunk};
+      workers()->run([&](unsigned k, unsigned P) {
+        for (int j = 0; j < 5; ++j) {
+          const size_t n = part[j].second, a = n * k / P, b = n * (k + 1) / P;
+          if (b > a) memcpy(hd + dst[j] + a, static_cast<const uint8_t*>(part[j].first) + a, b - a);
+        }
+      });
+      return CLG_OK;
+    }
     memcpy(hd, p.tiles.data(), tb);
     memcpy(hd + L->o_runs, p.runs.data(), rb);
     memcpy(hd + L->o_seg, p.segtab.data(), gb);
@@ -1209,6 +1375,7 @@ struct clg_engine {
     if (cb) memcpy(hd + L->o_chunk, chunk->data(), cb);
     return CLG_OK;
   }
+  static constexpr size_t kParallelCopy = 1u << 20;
   // The count pass's chunks of about equal cost: a tile costs its bytes plus a fixed 1 KiB
   // (tiles of one span are taken as equally long; a small whole span that pass 0 counted, a
   // skip), and block b takes the tiles whose cumulative cost passes b / G of the total.
@@ -1572,7 +1739,7 @@ struct clg_engine {
   static constexpr uint64_t kSmallBytes = 1u << 20;
   static constexpr uint32_t kSmallSpans = clg::kZSmallSpans;
   static constexpr uint64_t kSmallHostOut = 32u << 20;  // pinned output bytes at most (cap-sized)
-  PinBuf h_small_out, h_small_res{nullptr, 0, hipHostMallocCoherent};  // (res: polled while the kernel runs)
+  PinBuf h_small_out, h_small_res;
   DevBuf d_small;
   clg::SmallPlanArg small_arg;
   bool small_flip = false;
@@ -1611,7 +1778,7 @@ struct clg_engine {
     host_tiles(p);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     // the plan: in the launch's arguments when it fits (no copy queued), else one copy
-    static const int small_mode = [] {  // developer switch: bit 0 no argument plan, bit 1 no polling
+    static const int small_mode = [] {  // developer switch: bit 0 no argument plan
       const char* v = getenv("CLONOS_SMALL_MODE");
       return v ? atoi(v) : 0;
     }();
@@ -1643,10 +1810,9 @@ struct clg_engine {
     }
     // scratch: per-tile counts and record-start bitmaps, per-span look-back words
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
-    CHK(h_small_res.ensure((4 + size_t(ns)) * 8));
+    CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
     uint64_t* res = h_small_res.as<uint64_t>();
     res[0] = res[1] = res[2] = 0;
-    res[3 + ns] = 0;  // waves done
     // look-back words: two buffers of kSmallSpans, zeroed once; each call zeroes the other
     if (!d_small.p) {
       CHK(d_small.ensure((2 * size_t(kSmallSpans) + clg::kZSmallTiles * size_t(kSmallSpans)) * 8));
@@ -1664,7 +1830,9 @@ struct clg_engine {
       const char* v = getenv("CLONOS_SMALL_WARM");
       return v ? atoi(v) : -1;
     }();
-    ctl.warm = small_warm >= 0 ? uint32_t(small_warm) : spec_warm(false);
+    // warm-up 32 B: a lone wave per span waits on every step, and shorter warm-ups cost fewer
+    // merges than they save (config 1: the kernel 65 -> 62 us at 32 or 16 B, 63 at 48)
+    ctl.warm = small_warm >= 0 ? uint32_t(small_warm) : 32u;
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
       CHK(d_prof.ensure(size_t(ns + nt) * 64));
@@ -1685,22 +1853,7 @@ struct clg_engine {
                                  agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     hsub.emplace(this, "host_small_wait");
-    // wait: every wave counts itself done after its last store (system-scope release), so
-    // polling that word returns sooner than the stream's completion signal; the stream stays
-    // ordered for what follows.  Events (timing) and diagnostics wait on the stream.
-    bool polled = false;
-    if (!timing && !sprof && !(small_mode & 2)) {
-      volatile uint64_t* done = res + 3 + ns;
-      const auto t0 = std::chrono::steady_clock::now();
-      for (uint32_t k = 0;; ++k) {
-        if (__atomic_load_n(const_cast<uint64_t*>(done), __ATOMIC_ACQUIRE) >= ns) {
-          polled = true;
-          break;
-        }
-        if ((k & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
-      }
-    }
-    if (!polled) HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(hipStreamSynchronize(stream));
     hsub.emplace(this, "host_small_finish");
     if (sprof) {
       std::vector<uint64_t> hp(size_t(ns + nt) * 8);
@@ -2694,12 +2847,16 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   }
   {
     clg_engine::HostTimer ht(e, "host_decode_plan");
-    for (uint32_t i = 0; i < n; ++i) {
-      Log* l;
-      CHK(e->get_log(log[i], &l));
-      if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
-      total += uint64_t(nb[i]);
-      if (e->fused_decode) e->plan_log_span(pf, *l, st[i], nb[i], i, clg::kZTile);
+    if (!(n >= clg_engine::kParallelLogs && e->fused_decode && e->plan_parallel(pf, log, start_epoch, n, &total))) {
+      total = 0;
+      pf.reset();
+      for (uint32_t i = 0; i < n; ++i) {
+        Log* l;
+        CHK(e->get_log(log[i], &l));
+        if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
+        total += uint64_t(nb[i]);
+        if (e->fused_decode) e->plan_log_span(pf, *l, st[i], nb[i], i, clg::kZTile);
+      }
     }
   }
   auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {  // re-plans (fallbacks)

@@ -249,9 +249,7 @@ uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 // publishes its counts, sums every earlier span's (look-back), emits.  Spans of at most
 // kZSmallTiles tiles, batches without Serializable tables.  Results go to `res` (host-mapped
 // pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any span failed
-// (the host then decodes the batch the usual way), res[3 + s] span s's first record,
-// res[3 + n_spans] the number of waves done (each adds 1 with a system-scope release after its
-// last store: the host may poll it instead of waiting on the stream).  agg: kZSmallSpans zeroed
+// (the host then decodes the batch the usual way), res[3 + s] span s's first record.  agg: kZSmallSpans zeroed
 // words; the kernel zeroes all of agg_next for the next call (the host alternates two buffers,
 // so no memset is queued).  plan (host memory, optional): a plan of at most kZSmallArgTiles
 // tiles and kZSmallArgSpans spans goes in the launch's own arguments instead of d_tiles /

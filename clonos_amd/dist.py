@@ -351,7 +351,7 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     backend = dist.get_backend(group)
     # every per-log step below is an array operation: a failed task has 129 logs at p=128
     fv = np.unique(np.fromiter((int(v) for v in failed), np.int64))
-    gids = np.nonzero(np.isin(table.vertex, fv))[0]
+    gids = table.gids_of(fv)
     n = len(gids)
     vslot = np.searchsorted(fv, table.vertex[gids])  # each log's failed vertex, as an index into fv
     ep_of = np.array([start_epochs[int(v)] for v in fv], np.int64)
