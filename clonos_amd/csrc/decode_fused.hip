@@ -291,10 +291,11 @@ __device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
 }
 
 struct Res {
-  Bits bm, wb;     // true record starts in the region / wide ones
+  Bits bm, wb;     // true record starts in the region / wide ones (bad: those before the failing record)
   uint32_t exit;   // first true start >= re (bad: the speculative exit)
   uint32_t bad;    // true chain hits an invalid record (1) or, without tables, a Serializable one (2)
   uint32_t steps;  // true steps taken (diagnostics)
+  uint32_t fail;   // bad: the failing record's start (aligned coordinate)
 };
 
 // True step lengths of the fixed-length tags (nibble per tag; 15: Serializable,
@@ -678,7 +679,7 @@ __device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws,
 // rejects the record, *why set).
 template <class Step>
 __device__ __forceinline__ Res merge_walk_h(uint32_t re, uint32_t end_a, uint32_t e, const SpecR& s, Step&& step) {
-  Res r{{0, 0}, {0, 0}, e, 0, 0};
+  Res r{{0, 0}, {0, 0}, e, 0, 0, 0};
   if (e >= re) return r;
   const uint32_t r0 = (re - 1u) & ~(kZRegion - 1u);
   uint32_t p = e, why = 0;
@@ -713,6 +714,9 @@ __device__ __forceinline__ Res merge_walk_h(uint32_t re, uint32_t end_a, uint32_
   } else if (st == 2u) {
     r.bad = why;
     r.exit = s.exit;
+    r.bm = pb;  // the true starts before the failing record
+    r.wb = pw;
+    r.fail = p;
   } else {
     r.bm = pb;
     r.wb = pw;
@@ -770,6 +774,10 @@ __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
 }
 // abort[0]: nonzero once any tile aborted (polled by waiting tiles); abort[r], r = 1..4:
 // ~(lowest tile that aborted for reason r), for diagnostics.
+// An invalid record at span offset so on a true chain of span `span` (the lowest one wins).
+__device__ __forceinline__ void note_error(const FusedCtl& ctl, uint32_t span, uint64_t so) {
+  if (ctl.span_err && so != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(ctl.span_err + span), (unsigned long long)so);
+}
 __device__ __forceinline__ void raise_abort(const FusedCtl& c, uint32_t reason, uint32_t t) {
   __hip_atomic_store(c.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_max(c.abort + reason, ~t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1218,7 +1226,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
                                            const uint32_t lane, uint32_t* x_out, const JL& jl,
                                            const TileDesc* __restrict__ tiles = nullptr,
                                            const SpecR* walked = nullptr, uint64_t* cnt_out = nullptr,
-                                           uint64_t* bm_out = nullptr) {
+                                           uint64_t* bm_out = nullptr, uint32_t* fail_out = nullptr) {
 #define ZPHASE(i) \
   if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
   ZPHASE(1);
@@ -1238,7 +1246,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   uint32_t entry = lane == 0 ? e_true : guess;
   const GSpan g{tiles, t, z.sd.first_tile + z.sd.n_tiles, lo, z.td.span_off};
   auto merge = [&](uint32_t from) -> Res {
-    if (rs >= re) return Res{{0, 0}, {0, 0}, from, 0, 0};
+    if (rs >= re) return Res{{0, 0}, {0, 0}, from, 0, 0, 0};
     if (J && jl.lm) return merge_walk_lm(s_img, re, end_a, from, sp, jl, g);
     return merge_walk_r<J>(s_img, re, end_a, from, sp, jl);
   };
@@ -1304,7 +1312,20 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
     }
   }
   if (ctl.nodep) reason = 0;
-  if (reason && reason != 3u) return reason;
+  // an invalid record on the true chain with errors kept (ctl.span_err): the tile's counts and
+  // bits cover the records before it -- the lanes below the failing one, and its starts before
+  // the failing record -- so that a confirmed error costs its span no second decode
+  uint32_t fail_a = 0xFFFFFFFFu;
+  if (reason == 1u && badm && ctl.span_err) {
+    const uint32_t bl = (uint32_t)__builtin_ctzll(badm);
+    fail_a = (uint32_t)__shfl((int)r.fail, (int)bl);
+    if (lane > bl) {
+      r.bm = Bits{0, 0};
+      r.wb = Bits{0, 0};
+    }
+  }
+  if (fail_out) *fail_out = fail_a;
+  if (reason && reason != 3u && fail_a == 0xFFFFFFFFu) return reason;
 
   ZPHASE(3);
   // ---- counts and the record-start bitmap for the emit pass
@@ -1703,6 +1724,7 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
   if (ld_agent32(ctl.abort)) return;
   if (ctl.skip_bad && gp(ctl.span_bad)[tiles[t].span]) return;  // the robust output fills this span
+  if (ctl.span_err && tiles[t].span_off > gp(ctl.span_err)[tiles[t].span]) return;  // past a kept error
   emit_tile<J>(tiles, spans, ctl, out, t, lane, gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock], L);
 }
 
@@ -1770,7 +1792,7 @@ __global__ __launch_bounds__(64) void k_decode_count_tiny(const TileDesc* __rest
     a += L;
   }
   if (why == 3u) return;  // the count pass takes this tile (its words are rewritten there)
-  if (why == 0u) {
+  if (why == 0u || ctl.span_err) {  // (an invalid record with errors kept: the records before it)
     for (const uint32_t r = (end - 1) >> 7; cur <= r; ++cur) {
       u64x2 v;
       v.x = blo;
@@ -1779,9 +1801,11 @@ __global__ __launch_bounds__(64) void k_decode_count_tiny(const TileDesc* __rest
       blo = bhi = 0;
     }
     gp(ctl.cnt)[ti] = pack_cnt(rec, wide);
-  } else {
+  }
+  if (why) {
     raise_abort(ctl, why, ti);
     if (ctl.span_bad) __hip_atomic_store(ctl.span_bad + td.span, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    note_error(ctl, td.span, (uint64_t)(a - td.delta));  // (a whole span: span offset = a - delta)
   }
   gp(ctl.st_x)[ti] = kZTinyDone;
 }
@@ -1796,6 +1820,7 @@ __global__ __launch_bounds__(64) void k_decode_count_tiny(const TileDesc* __rest
 // chain fails (then the span is bad, for real).  Then any tile of that chunk's first span
 // still without an exit failed on the true chain: its span is bad.
 constexpr uint64_t kZExValid = 1ull << 63;  // ex[t]: the tile's exit (span offset) is known
+constexpr uint64_t kZExFail = 1ull << 62;   // ex[t] (not valid): its chain met an invalid record at span offset ex & ~flag
 
 // A request: chunk c's flag (idempotent, so a chunk asked for twice is served once) and the
 // request count, which lets k_decode_repair return at once in the usual batch.
@@ -1825,7 +1850,12 @@ __device__ __forceinline__ void check_chunk(const FusedCtl& ctl, const TileDesc*
     }
   }
   const uint64_t m = __ballot(bad != 0xFFFFFFFFu);
-  if (m && lane == (uint32_t)__builtin_ctzll(m)) mark_bad(ctl, 1, bad, span);
+  if (m && lane == (uint32_t)__builtin_ctzll(m)) {
+    mark_bad(ctl, 1, bad, span);
+    // the chain that failed there is the true one (the repair walk met it before): its position
+    const uint64_t e = ld_agent(&ctl.ex[bad]);
+    if (e & kZExFail) note_error(ctl, span, e & ~kZExFail);
+  }
 }
 
 // Tile t staged (image, and with tables the map and table) and counted from entry xs (span
@@ -1836,7 +1866,8 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
                                                  uint32_t t, const ZTile& z, uint64_t xs, uint32_t must_exit,
                                                  const SpecR* walked, uint64_t* x, uint64_t* cnt_out = nullptr,
                                                  StagePre* pf = nullptr, bool pf_ready = false,
-                                                 uint32_t pf_next = 0xFFFFFFFFu, uint64_t* bm_out = nullptr) {
+                                                 uint32_t pf_next = 0xFFFFFFFFu, uint64_t* bm_out = nullptr,
+                                                 uint64_t* fail_so = nullptr) {
   constexpr bool kLm = CLG_COUNT_LM != 0;
   const uint32_t nt = ctl.n_tiles;
   const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
@@ -1858,10 +1889,11 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
   if (J && kLm) build_lm(z, s_img, s_j, lane);
   if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
   else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
-  uint32_t x_true;
+  uint32_t x_true, fa = 0xFFFFFFFFu;
   const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked, cnt_out,
-                                     bm_out);
+                                     bm_out, fail_so ? &fa : nullptr);
   *x = z.td.span_off + (x_true - z.lo);
+  if (fail_so) *fail_so = fa != 0xFFFFFFFFu ? z.td.span_off + (fa - z.lo) : ~0ull;
   return why;
 }
 
@@ -1940,8 +1972,11 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
         } else if (!z.last && zero_tile_walk(z, xs, ctl, t, lane, &x)) {
           zero = true;  // a run of Order(channel 0) records: settled without a walk
         } else {
-          why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x);
+          uint64_t fso = ~0ull;
+          why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x, nullptr, nullptr,
+                                false, 0xFFFFFFFFu, nullptr, &fso);
           __syncthreads();  // the image is reused
+          if (why == 1u && lane == 0) note_error(ctl, z.td.span, fso);  // (the walk's entry is the true one)
         }
         if (why) {
           if (lane == 0) mark_bad(ctl, why, t, z.td.span);
@@ -2052,8 +2087,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
     uint64_t x;
     const uint32_t nxt = t + 1 < t1 ? t + 1 : 0xFFFFFFFFu;
+    uint64_t fso = ~0ull;
     const uint32_t why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, t + 1 == t1 ? x_pub : kZCanon,
-                                         reuse ? &sp_last : nullptr, &x, nullptr, kPre ? &pf : nullptr, pf_t == t, nxt);
+                                         reuse ? &sp_last : nullptr, &x, nullptr, kPre ? &pf : nullptr, pf_t == t, nxt,
+                                         nullptr, &fso);
     pf_t = nxt;
     if (why == 0u || why == 3u) {
       x_prev = x;
@@ -2068,8 +2105,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
     } else {
       const bool soft = why != 5u && z.td.span == sus_span;  // the published entry may be wrong
       if (lane == 0) {
-        if (soft) push_repair(ctl, blockIdx.x);
-        else mark_bad(ctl, why, t, z.td.span);
+        if (soft) {
+          push_repair(ctl, blockIdx.x);
+          if (why == 1u && fso != ~0ull) st_agent(&ctl.ex[t], kZExFail | fso);  // for check_chunk, if real
+        } else {
+          mark_bad(ctl, why, t, z.td.span);
+          if (why == 1u) note_error(ctl, z.td.span, fso);  // the entry is the true chain's
+        }
       }
       if (!soft && !ctl.span_bad) return;
       if (soft)  // go on from the next tile's first byte (a guess; the repair checks it), so that

@@ -1573,6 +1573,7 @@ struct clg_engine {
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
+    CHK(d_zerr.ensure(std::max<size_t>(1, ns) * 8));
     CHK(h_zres.ensure((2 * size_t(ns) + 5) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
@@ -1594,6 +1595,7 @@ struct clg_engine {
     if (jser) CHK(jarena_reset(&ctl.jar));
     ctl.span_bad = d_zbad.as<uint32_t>();
     ctl.skip_bad = 0;
+    ctl.span_err = keep_errors ? d_zerr.as<uint64_t>() : nullptr;
     ctl.chunk = chunked ? reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_chunk) : nullptr;
     ctl.tiny = tiny ? 1u : 0u;
     ctl.ex = w + nt;
@@ -1617,6 +1619,7 @@ struct clg_engine {
       HIPCHK(hipMemsetAsync(w, 0, o_cnt * 8, stream));  // st_x, ex, rep_flag
       HIPCHK(hipMemsetAsync(ab, 0, 40, stream));                // abort words, repair counters
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
+      if (keep_errors) HIPCHK(hipMemsetAsync(d_zerr.p, 0xFF, std::max<size_t>(1, ns) * 8, stream));  // ~0: none
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
       if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
       for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
@@ -1740,6 +1743,14 @@ struct clg_engine {
   static constexpr uint32_t kSmallSpans = clg::kZSmallSpans;
   static constexpr uint64_t kSmallHostOut = 32u << 20;  // pinned output bytes at most (cap-sized)
   PinBuf h_small_out, h_small_res;
+  // Decode errors kept on the fast path (FusedCtl::span_err; CLONOS_KEEP_ERRORS=0 turns it off,
+  // a developer switch): a span whose error the full rules confirm keeps the fast run's records
+  // before it, and only spans whose chains went wrong otherwise go to the robust pipeline.
+  const bool keep_errors = [] {
+    const char* v = getenv("CLONOS_KEEP_ERRORS");
+    return !(v && atoi(v) == 0);
+  }();
+  DevBuf d_zerr, d_sf_cls;
   DevBuf d_small;
   clg::SmallPlanArg small_arg;
   bool small_flip = false;
@@ -1951,6 +1962,39 @@ struct clg_engine {
     const uint32_t ns = uint32_t(pf.spans.size()), nt = pf.n_tiles;
     std::vector<uint32_t> flag(ns);
     HIPCHK(hipMemcpy(flag.data(), d_zbad.p, size_t(ns) * 4, hipMemcpyDeviceToHost));
+    // spans with an error position (kept errors): the full rules classify the record there on
+    // the GPU; a confirmed error keeps the fast run's records before it (k_err_classify)
+    std::vector<uint32_t> kept;
+    std::vector<uint64_t> kept_off;
+    std::vector<int32_t> kept_res;
+    if (zlast.ctl.span_err) {
+      std::vector<uint64_t> err(ns);
+      HIPCHK(hipMemcpy(err.data(), zlast.ctl.span_err, size_t(ns) * 8, hipMemcpyDeviceToHost));
+      std::vector<uint32_t> cand;
+      for (uint32_t s = 0; s < ns; ++s)
+        if (flag[s] && err[s] != ~0ull) cand.push_back(s);
+      if (!cand.empty()) {
+        const uint32_t nc = uint32_t(cand.size());
+        CHK(d_sf_cls.ensure(size_t(nc) * 12 + 64));
+        HIPCHK(hipMemcpyAsync(d_sf_cls.p, cand.data(), size_t(nc) * 4, hipMemcpyHostToDevice, stream));
+        auto* cres = reinterpret_cast<int32_t*>(d_sf_cls.as<uint8_t>() + ((size_t(nc) * 4 + 15) & ~size_t(15)));
+        clg::JArena jar;
+        CHK(jarena_reset(&jar));
+        CHK(clg::launch_err_classify(d_ztiles.as<clg::TileDesc>(), d_spans.as<clg::SpanDesc>(), d_sf_cls.as<uint32_t>(),
+                                     nc, zlast.ctl, cres, jar, stream));
+        std::vector<int32_t> cr(size_t(nc) * 2);
+        HIPCHK(hipMemcpyAsync(cr.data(), cres, cr.size() * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        for (uint32_t i = 0; i < nc; ++i)
+          if (cr[2 * i] < 0) {  // confirmed: not a bad span any more
+            flag[cand[i]] = 0;
+            kept.push_back(cand[i]);
+            kept_off.push_back(err[cand[i]]);
+            kept_res.push_back(cr[2 * i]);
+            kept_res.push_back(cr[2 * i + 1]);
+          }
+      }
+    }
     std::vector<uint32_t> bad;
     uint64_t bad_bytes = 0;
     for (uint32_t s = 0; s < ns; ++s)
@@ -1958,8 +2002,9 @@ struct clg_engine {
         bad.push_back(s);
         bad_bytes += pf.spans[s].len;
       }
-    if (bad.empty() || bad.size() > kSfMaxSpans || bad_bytes > log_bytes / 4 * 3) return CLG_OK;
-    stats["decode_span_fallback"].launches++;
+    if ((bad.empty() && kept.empty()) || bad.size() > kSfMaxSpans || bad_bytes > log_bytes / 4 * 3) return CLG_OK;
+    if (!kept.empty()) stats["decode_kept_errors"].launches++;
+    if (!bad.empty()) stats["decode_span_fallback"].launches++;
     const uint32_t nb = uint32_t(bad.size());
     // scratch: the robust decode's records (13 B) and wide rows (25 B) of the bad spans
     const uint64_t RC = bad_bytes / 2 + nb + 1, WC = bad_bytes / 6 + nb + 1;  // (records are >= 2 B, wide >= 6 B)
@@ -1980,7 +2025,7 @@ struct clg_engine {
     int e_status = CLG_OK, e_tag = 0;
     uint32_t e_span = 0;
     int64_t e_off = -1;
-    {  // every bad span in ONE robust run (spans 0 .. nb-1 of its plan), into scratch
+    if (nb) {  // every bad span in ONE robust run (spans 0 .. nb-1 of its plan), into scratch
       DecodePlan sp;
       sp.only = &bad;
       build(sp, uint32_t(clg::kTile));
@@ -2016,11 +2061,21 @@ struct clg_engine {
         packed[i] = nwide[i] << 31 | nrec[i];
       }
     }
+    // the lowest span's error: the robust run's or a kept one's (kept[] ascends)
+    if (!kept.empty() && (e_status == CLG_OK || kept[0] < e_span)) {
+      e_status = kept_res[0];
+      e_span = kept[0];
+      e_off = int64_t(kept_off[0]);
+      e_tag = kept_res[1];
+    }
     // the fast run again over the good spans: its plan back in place (the robust runs used
-    // the shared span table), the bad spans' counts injected, scan and emit
+    // the shared span table), the bad spans' counts injected, scan and emit (kept errors: the
+    // tiles past the error hold no records, emit stops there)
     PlanLayout L;
-    CHK(stage_plan(pf, d_ztiles, &L));
-    CHK(enqueue_plan(pf, L, d_ztiles));
+    if (nb) {
+      CHK(stage_plan(pf, d_ztiles, &L));
+      CHK(enqueue_plan(pf, L, d_ztiles));
+    }
     // meta: the packed counts, the bad spans, then the placement rows (16-byte aligned)
     const size_t o_place = (size_t(nb) * 12 + 15) & ~size_t(15), mb = o_place + size_t(nb) * sizeof(clg::SfPlace);
     CHK(d_sf_meta.ensure(mb + 64));

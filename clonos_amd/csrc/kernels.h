@@ -217,6 +217,10 @@ struct FusedCtl {
   uint64_t* ex;
   uint8_t* rep_flag;
   uint32_t* rep;
+  // Decode errors kept on the fast path: span_err[s] = the lowest span offset where a true
+  // chain of span s met an invalid record (~0: none; atomicMin), and the tile holding it
+  // writes the counts and start bits of the records before it.  null: off.
+  uint64_t* span_err;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
@@ -239,6 +243,13 @@ struct SfPlace {
   uint32_t span, pad;
 };
 int launch_sf_place(const SfPlace* d_place, uint32_t n_bad, DecodeOut scratch, DecodeOut out, FusedCtl ctl, void* stream);
+// Per-span fallback, first step (kernels.hip): bad span bad[i] with a recorded error position
+// (ctl.span_err) -- the record there classified by decodeNext's full rules.  An invalid record
+// (res[2 i] = its status < 0, res[2 i + 1] = its tag, as int8): the span keeps the fast run's
+// records before it (span_bad cleared, its tiles past the error get no records).  Else (a
+// valid record there: res[2 i] = 0) the span stays bad for the robust pipeline.
+int launch_err_classify(const TileDesc* d_tiles, const SpanDesc* d_spans, const uint32_t* d_bad, uint32_t n_bad,
+                        FusedCtl ctl, int32_t* d_res, JArena ar, void* stream);
 int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, void* stream, uint32_t phase);
 // The count pass's grid for n_tiles tiles (the blocks the device keeps resident, at most one

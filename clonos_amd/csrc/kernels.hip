@@ -304,7 +304,8 @@ __global__ __launch_bounds__(64) void k_dec_tables(const TileDesc* __restrict__ 
 
 // ==================================================================================
 // Pass 2: resolve tile entries per span.  One block per span; thread 0 walks the
-// span's tiles over an LDS cache of their aggregates (loaded cooperatively).
+// span's tiles over an LDS cache of their aggregates (loaded cooperatively), with the
+// concrete walks made beforehand in parallel from guessed entries (k_dec_resolve).
 // ==================================================================================
 constexpr int kResolveChunk = 96;  // tiles cached in LDS per step (96*64*8 = 48 KiB)
 
@@ -356,12 +357,30 @@ __device__ int tile_eval_concrete(const TileDesc* tiles, const SpanDesc& sd, uin
   return CLG_OK;
 }
 
+// A tile's concrete evaluation from a guessed entry, made by its own thread before the
+// serial walk reaches it.
+struct PreEval {
+  uint32_t entry;  // the guessed entry (0xFFFFFFFF: none made)
+  uint32_t exit, c, w, lim;
+  int32_t st, err_tag;
+  int64_t err_off;
+};
+
+// One block per span.  The walk from tile to tile is serial (a tile's entry is its
+// predecessor's exit), but a tile whose entry misses its table (a record from the previous
+// tile reaching 64 B or more into it, or a dead table entry) needs a concrete walk over HBM,
+// and those walks are what cost: one thread walking them one after another took config 3
+// 77 ms.  So first every thread takes tiles of the chunk and, where the predecessor's
+// candidates all left by one exit (TileConv.exit), walks its tile from that entry; then
+// thread 0's serial walk takes the result wherever the actual entry is the guessed one, and
+// walks concretely only where it is not.
 __global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      const uint64_t* __restrict__ agg, const TileConv* __restrict__ conv,
                                                      TileRes* __restrict__ tres, SpanRes* __restrict__ sres,
                                                      const uint32_t* __restrict__ span_flags, JArena ar) {
   __shared__ uint64_t s_agg[kResolveChunk * kEntries];
   __shared__ uint32_t s_len[kResolveChunk];
+  __shared__ PreEval s_pre[kResolveChunk];
   __shared__ uint64_t s_state[4];  // entry, rec, wide, done
   const uint32_t s = blockIdx.x;
   if (span_flags && !span_flags[s]) return;
@@ -381,6 +400,24 @@ __global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict_
     for (uint32_t i = threadIdx.x; i < nt * kEntries; i += blockDim.x)
       s_agg[i] = agg[(uint64_t)(sd.first_tile + base) * kEntries + i];
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) s_len[i] = tiles[sd.first_tile + base + i].len;
+    __syncthreads();
+    // the guessed entries' concrete walks, a thread per tile
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+      const uint32_t t = sd.first_tile + base + i;
+      PreEval pe;
+      pe.entry = 0xFFFFFFFFu;
+      const uint32_t g = base + i == 0 ? 0u : conv[t - 1].exit;  // (the span's first tile: entry 0)
+      if (g != kExitErr && g < s_len[i]) {
+        const uint64_t x = g < (uint32_t)kEntries ? s_agg[i * kEntries + g] : (uint64_t)kExitFar;
+        if ((uint32_t)x == kExitErr || (uint32_t)x == kExitFar) {
+          pe.entry = g;
+          pe.err_off = -1;
+          pe.err_tag = 0;
+          pe.st = tile_eval_concrete(tiles, sd, t, conv[t], g, &pe.exit, &pe.c, &pe.w, &pe.err_off, &pe.err_tag, &pe.lim, ar);
+        }
+      }
+      s_pre[i] = pe;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       uint64_t e = s_state[0], rec = s_state[1], wide = s_state[2];
@@ -410,7 +447,21 @@ __global__ __launch_bounds__(256) void k_dec_resolve(const TileDesc* __restrict_
         uint32_t c, w;
         if (xr == kExitErr || xr == kExitFar) {
           uint32_t lim;
-          const int st = tile_eval_concrete(tiles, sd, t, conv[t], (uint32_t)e, &xr, &c, &w, &err_off, &err_tag, &lim, ar);
+          int st;
+          const PreEval& pe = s_pre[i];
+          if (pe.entry == (uint32_t)e) {  // walked already, from this very entry
+            xr = pe.exit;
+            c = pe.c;
+            w = pe.w;
+            lim = pe.lim;
+            st = pe.st;
+            if (st != CLG_OK) {
+              err_off = pe.err_off;
+              err_tag = pe.err_tag;
+            }
+          } else {
+            st = tile_eval_concrete(tiles, sd, t, conv[t], (uint32_t)e, &xr, &c, &w, &err_off, &err_tag, &lim, ar);
+          }
           r.limit = lim;
           if (st != CLG_OK) {
             status = st;
@@ -720,6 +771,49 @@ int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDe
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_dec_tables, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, d_agg, d_conv,
                      d_span_flags, ar);
+  return ok(hipGetLastError());
+}
+
+// Kept decode errors (FusedCtl::span_err): one block per bad span.  Thread 0 reads the record
+// at the recorded position by decodeNext's full rules (rec_len_slow over the span's tiles);
+// an invalid record confirms the error (its status and tag out, the span's bad flag cleared,
+// the counts of its tiles past the error zeroed -- the tile holding it counted the records
+// before it already).  A valid record there, or a walker short of spill space, leaves the
+// span bad: the robust pipeline decodes it as before.
+__global__ __launch_bounds__(256) void k_err_classify(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                      const uint32_t* __restrict__ bad, FusedCtl ctl, int32_t* res,
+                                                      JArena ar) {
+  __shared__ int32_t s_st;
+  const uint32_t i = blockIdx.x, s = bad[i];
+  const SpanDesc sd = spans[s];
+  const uint64_t E = ctl.span_err[s];
+  if (threadIdx.x == 0) {
+    int32_t st = 0, tag = 0;
+    if (E < sd.len && sd.n_tiles) {
+      SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, sd.first_tile, sd.len, ar};
+      AtSpan b{&sr, E};
+      const int64_t L = rec_len_slow(b, sd.len - E);
+      if (L == CLG_E_CORRUPT_TAG || L == CLG_E_TRUNCATED || L == CLG_E_BAD_ENUM || L == CLG_E_NEG_LEN ||
+          L == CLG_E_BAD_SERIAL) {
+        st = (int32_t)L;
+        tag = (int8_t)sr.at(E);
+      }
+    }
+    res[2 * i] = st;
+    res[2 * i + 1] = tag;
+    s_st = st;
+  }
+  __syncthreads();
+  if (s_st >= 0) return;
+  for (uint32_t k = threadIdx.x; k < sd.n_tiles; k += 256)
+    if (tiles[sd.first_tile + k].span_off > E) ctl.cnt[sd.first_tile + k] = 0;
+  if (threadIdx.x == 0) ctl.span_bad[s] = 0;
+}
+int launch_err_classify(const TileDesc* d_tiles, const SpanDesc* d_spans, const uint32_t* d_bad, uint32_t n_bad,
+                        FusedCtl ctl, int32_t* d_res, JArena ar, void* stream) {
+  if (!n_bad) return CLG_OK;
+  hipLaunchKernelGGL(k_err_classify, dim3(n_bad), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_bad, ctl, d_res,
+                     ar);
   return ok(hipGetLastError());
 }
 

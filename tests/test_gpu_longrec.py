@@ -248,7 +248,9 @@ def test_span_fallback_error_equals_robust():
             errs.append((x.status, x.err_span, x.err_off, x.err_tag, x.n_rec))
             if mode == "auto":
                 ks = e.kernel_stats()
-                assert "decode_span_fallback" in ks and "decode_fallback" not in ks, ks
+                # the error span keeps its records before the error (decode_kept_errors); only a
+                # span the fast rules cannot settle would go robust (decode_span_fallback)
+                assert ("decode_span_fallback" in ks or "decode_kept_errors" in ks) and "decode_fallback" not in ks, ks
         finally:
             e.close()
     assert errs[0] == errs[1] and errs[0][1] == 9

@@ -1,10 +1,16 @@
-"""GPU: the per-span fallback with many bad spans -- every bad span in ONE robust run, the
-records placed by one kernel (engine.cpp span_fallback, decode_fused.hip k_sf_place).  A
-config-3-like batch where a third of the spans hold a decode error (an invalid tag, a
-truncated record, a bad enum, a negative name length) is decoded by the fast path with the
-fallback and by the robust pipeline alone: every output array, every span's record base and
-the first error (status, span, offset, tag) are identical, and the oracle agrees with each
-good span.  SimpleDeterminantEncoder.decodeNext (:78-342)."""
+"""GPU: decode errors in many spans.  A config-3-like batch where a third (or a fifth) of the
+spans hold a decode error (an invalid tag, a truncated record, a bad enum, a negative name
+length) is decoded three ways:
+  * the fast path keeping the errors (the default: the count pass records each span's error
+    position and the records before it, k_err_classify confirms the error by the full rules,
+    no robust decode -- decode_kept_errors);
+  * the fast path with errors not kept (CLONOS_KEEP_ERRORS=0): every bad span in ONE robust
+    run, the records placed by one kernel (engine.cpp span_fallback, k_sf_place);
+  * the robust pipeline alone.
+Every output array, every span's record base and the first error (status, span, offset, tag)
+are identical, and the oracle agrees with each good span.  SimpleDeterminantEncoder.decodeNext
+(:78-342)."""
+import os
 import numpy as np
 import pytest
 
@@ -62,18 +68,29 @@ def test_many_bad_spans_equal_robust(n_spans, every):
         spans.append((len(blob), len(b)))
         blob += b
     res = {}
-    for mode in ("three_pass", "robust"):
-        with Engine(segment_bytes=16384, pool_segments=1 << 12, timing=True, decode=mode) as eng:
-            res[mode] = _raw_decode(eng, blob, spans)
-            if mode == "three_pass":
+    for mode, keep in (("three_pass", "1"), ("three_pass", "0"), ("robust", "1")):
+        os.environ["CLONOS_KEEP_ERRORS"] = keep
+        try:
+            with Engine(segment_bytes=16384, pool_segments=1 << 12, timing=True, decode=mode) as eng:
+                res[mode, keep] = _raw_decode(eng, blob, spans)
                 ks = eng.kernel_stats()
-                assert "decode_span_fallback" in ks and "decode_fallback" not in ks, ks
-    a, r = res["three_pass"], res["robust"]
-    assert a[0] != 0 and a[:7] == r[:7]  # status, error fields, record and wide-row counts
-    assert a[2] == bad[0]  # the lowest bad span's error
-    for k in a[7]:
-        np.testing.assert_array_equal(a[7][k], r[7][k], err_msg=k)
-    np.testing.assert_array_equal(a[8], r[8])
+        finally:
+            del os.environ["CLONOS_KEEP_ERRORS"]
+        if mode == "three_pass":
+            assert "decode_fallback" not in ks, ks
+            if keep == "1":  # every error confirmed and kept: no robust decode at all
+                assert "decode_kept_errors" in ks and "decode_span_fallback" not in ks, ks
+            else:
+                assert "decode_span_fallback" in ks and "decode_kept_errors" not in ks, ks
+    r = res["robust", "1"]
+    for key in (("three_pass", "1"), ("three_pass", "0")):
+        a = res[key]
+        assert a[0] != 0 and a[:7] == r[:7], key  # status, error fields, record and wide-row counts
+        assert a[2] == bad[0]  # the lowest bad span's error
+        for k in a[7]:
+            np.testing.assert_array_equal(a[7][k], r[7][k], err_msg=f"{key} {k}")
+        np.testing.assert_array_equal(a[8], r[8])
+    a = res["three_pass", "1"]
     # every good span against the oracle
     rec0 = a[8]
     for s in range(0, n_spans, 7):
