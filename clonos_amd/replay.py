@@ -196,17 +196,22 @@ def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, Determ
     """The accumulated responses of failed vertices whose copies arrived by the cross-GPU merge
     (dist.merge_responses): entries point into the merge's receive buffer, in HBM under RCCL
     (prepare_replay(..., device_input=True)).  One batched put per vertex."""
-    gids = merged.gids
-    place = np.stack([merged.offs, merged.lens], 1).astype(np.uint64) if len(gids) else np.zeros((0, 2), np.uint64)
+    gids = np.asarray(merged.gids, np.int64)
     ids = table_ids(table)
-    base = np.uint64(merged.buf.data_ptr())
+    # the entries grouped by vertex once (a stable sort keeps each vertex's entries in the
+    # merge's order), then one contiguous slice per vertex
     vert = table.vertex[gids] if len(gids) else np.zeros(0, np.int64)
+    order = np.argsort(vert, kind="stable")
+    vs = vert[order]
+    ids_o = ids[gids[order]]
+    ptr_o = np.asarray(merged.offs, np.uint64)[order] + np.uint64(merged.buf.data_ptr())
+    len_o = np.asarray(merged.lens, np.uint64)[order]
     out = {}
     for v in vertices:
-        sel = np.nonzero(vert == v)[0]
-        ev = DeterminantResponseEvent(True, v, capacity=max(1, len(sel)))
-        if len(sel):
-            ev.put_device_batch(ids[gids[sel]], place[sel, 0] + base, place[sel, 1], merged.buf)
+        lo, hi = int(np.searchsorted(vs, v, "left")), int(np.searchsorted(vs, v, "right"))
+        ev = DeterminantResponseEvent(True, v, capacity=max(1, hi - lo))
+        if hi > lo:
+            ev.put_device_batch(ids_o[lo:hi], ptr_o[lo:hi], len_o[lo:hi], merged.buf)
         out[v] = ev
     return out
 

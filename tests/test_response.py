@@ -194,3 +194,44 @@ def test_buffer_sizes_oracle():
     with pytest.raises(ValueError) as ei:
         R.buffer_sizes(ok + b"\x00\x01" + ok)
     assert ei.value.args[0] == (R.E_NOT_BUFFER_BUILT, 15, 0)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_put_batch_matches_oracle(seed):
+    """clg_response_put_batch (one sort instead of a scan per put) against the oracle's puts one
+    by one: pre-existing entries, keys put twice inside a batch, batches that cross the resize
+    thresholds and a bucket of 9 colliding ids (the small-table treeify resize) -- the same
+    wire bytes, hence the same iteration order, and the same table capacity."""
+    from clonos_amd.replay import log_id_array
+    rng = np.random.default_rng(500 + seed)
+    vertices = rng.integers(-50, 50, size=6)
+    keys = [_rand_id(rng, vertices) for _ in range(int(rng.integers(20, 200)))]
+    if seed % 2:  # a bucket of colliding ids as well (test_collisions_trigger_small_table_resize)
+        seen = {}
+        for s in range(-128, 128):
+            for lo in range(0, 64):
+                k = R.LogId.subpartition(1, lo, 0, s)
+                h = k.java_hash() & 0xFFFFFFFF
+                seen.setdefault((h ^ (h >> 16)) & 15, []).append(k)
+        keys += max(seen.values(), key=len)[:9]
+    keys += [keys[int(i)] for i in rng.integers(0, len(keys), 10)]  # puts of keys already there
+    vals = [rng.integers(0, 256, size=int(rng.integers(0, 30)), dtype=np.uint8).tobytes() for _ in keys]
+    o = R.Response(True, 7, 1)
+    p = DeterminantResponseEvent(True, 7, 1, capacity=len(keys) + 1)
+    pre = int(rng.integers(0, len(keys) // 2))
+    for k, v in zip(keys[:pre], vals[:pre]):  # some entries there already
+        o.dets.put(k, v)
+        p.put(_to_cl(k), v)
+    for k, v in zip(keys[pre:], vals[pre:]):
+        o.dets.put(k, v)
+    bufs = [np.frombuffer(v, np.uint8) if v else np.zeros(1, np.uint8) for v in vals[pre:]]
+    at = pre
+    while at < len(keys):  # the rest in batches of 8 .. 60 puts
+        m = min(len(keys) - at, int(rng.integers(8, 61)))
+        ids = log_id_array([_to_cl(k) for k in keys[at:at + m]])
+        ptrs = np.array([b.ctypes.data for b in bufs[at - pre:at - pre + m]], np.uint64)
+        lens = np.array([len(v) for v in vals[at:at + m]], np.uint64)
+        p.put_device_batch(ids, ptrs, lens, bufs)
+        at += m
+    assert p.write() == o.write()
+    assert p._c.table_cap == o.dets.cap
