@@ -1104,7 +1104,9 @@ struct clg_engine {
 
   // notifyCheckpointComplete :398-435 (flushes first so no staged byte lives in a dropped
   // component).
-  int checkpoint_complete(Log& l, int64_t cp) {
+  int checkpoint_complete(Log& l, int64_t cp) { return checkpoint_complete(l, cp, free_segs); }
+  // (freed: where the dropped segments go -- a host thread's own list in the parallel truncation)
+  int checkpoint_complete(Log& l, int64_t cp, std::vector<uint32_t>& freed) {
     const int32_t R = compute_if_absent(l, cp)->offset;  // (read before the erase moves entries)
     l.epochs.erase_below(cp);
     if (R < 0 || R > l.writer) return fail(CLG_E_STATE, "readerIndex %d outside [0, %d]", R, l.writer);
@@ -1118,7 +1120,7 @@ struct clg_engine {
         drop = size_t(R) / C();
         move = int32_t(drop * C());
       }
-      for (size_t i = 0; i < drop; ++i) free_segs.push_back(l.segs[i]);
+      for (size_t i = 0; i < drop; ++i) freed.push_back(l.segs[i]);
       l.segs.erase_front(drop);
     }
     l.epochs.rebase(move);
@@ -2851,8 +2853,41 @@ int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) 
   j.latest_cp = cp;
   CHK(e->flush());
   clg_engine::HostTimer ht(e, "host_truncate_all");
-  for (auto& l : e->logs)
-    if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
+  if (e->logs.size() >= clg_engine::kParallelLogs) {
+    // 66 k logs (config 4): the host threads take parts of the log table.  A log whose epochs
+    // below cp hold shared EpochStart objects (a consumer refers to them) is left to this
+    // thread (their blocks go back to a per-thread free list); each part collects its freed
+    // segments, which join the pool after.
+    WorkPool* wp = e->workers();
+    const unsigned P = wp->size();
+    const size_t nl = e->logs.size(), per = (nl + P - 1) / P;
+    std::vector<std::vector<uint32_t>> freed(P), later(P);
+    std::vector<int> st(P, CLG_OK);
+    wp->run([&](unsigned k, unsigned) {
+      for (size_t i = k * per; i < std::min(nl, (k + 1) * per); ++i) {
+        Log& l = e->logs[i];
+        if (!l.open || l.job != job) continue;
+        bool shared = false;
+        for (const EpochEnt& x : l.epochs) {
+          if (x.id >= cp) break;
+          shared |= x.shared != nullptr;
+        }
+        if (shared) {
+          later[k].push_back(uint32_t(i));
+          continue;
+        }
+        if ((st[k] = e->checkpoint_complete(l, cp, freed[k])) != CLG_OK) return;
+      }
+    });
+    for (unsigned k = 0; k < P; ++k) e->free_segs.insert(e->free_segs.end(), freed[k].begin(), freed[k].end());
+    for (unsigned k = 0; k < P; ++k)
+      if (st[k] != CLG_OK) return fail(st[k], "checkpoint completion failed on a log (state outside its bounds)");
+    for (unsigned k = 0; k < P; ++k)
+      for (uint32_t i : later[k]) CHK(e->checkpoint_complete(e->logs[i], cp));
+  } else {
+    for (auto& l : e->logs)
+      if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
+  }
   if (applied) *applied = 1;
   return CLG_OK;
 }
