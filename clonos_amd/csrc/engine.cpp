@@ -831,6 +831,10 @@ struct clg_engine {
     }
     CHK(flush());
     CHK(gwait());  // the scatter below writes segments an in-flight gather may read
+    if (n >= kParallelLogs) {
+      int st = CLG_OK;
+      if (upstream_parallel(r, n, bytes, &st)) return st;
+    }
     // the chunks go straight into the pinned descriptor buffer (a config-4 batch has 66 k of
     // them: a fresh vector per call cost page faults, and a copy)
     size_t bound = 0;
@@ -878,6 +882,122 @@ struct clg_engine {
       return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream);
     }));
     return sync();  // the caller's buffer and the pinned descriptors are free again
+  }
+
+  // upstream_batch's device-input loop on the host threads, for batches of many distinct logs
+  // (config 4: 66 k): per part each request's new bytes and the segments it needs; then, in
+  // request order, the segments taken from the pool (a request the pool cannot serve gets
+  // CLG_E_NOSPACE with nothing taken, a gap CLG_E_GAP after its segments were added -- as one by
+  // one) and each request's place among the scatter chunks; then per part the segments
+  // attached, the chunks written and the logs advanced.  false: not applicable (a log twice).
+  std::vector<uint8_t> up_seen;
+  struct UpPlan {
+    int32_t num_new;
+    uint32_t need, chunks;
+    uint64_t seg_from, ch_from;
+  };
+  std::vector<UpPlan> up_plan;
+  bool upstream_parallel(clg_delta_req* r, uint32_t n, const uint8_t* bytes, int* out_st) {
+    up_seen.assign(logs.size(), 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t h = r[i].log;
+      if (h < logs.size()) {
+        if (up_seen[h]) return false;  // two deltas of one log apply in order: the serial loop
+        up_seen[h] = 1;
+      }
+    }
+    WorkPool* wp = workers();
+    const unsigned P = wp->size();
+    const uint32_t per = (n + P - 1) / P, Cb = C();
+    up_plan.resize(n);
+    wp->run([&](unsigned k, unsigned) {
+      for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
+        UpPlan& u = up_plan[i];
+        u = UpPlan{0, 0, 0, 0, 0};
+        r[i].status = CLG_OK;
+        Log* l;
+        if ((r[i].status = get_log(r[i].log, &l)) != CLG_OK || r[i].len == 0) continue;
+        auto es = compute_if_absent(*l, r[i].epoch);
+        const int32_t cur = l->writer - es->offset;
+        const int32_t num_new = (r[i].offset_from_epoch + int32_t(r[i].len)) - cur;
+        if (num_new <= 0) continue;
+        const int64_t need_bytes = int64_t(l->writer) + num_new - capacity(*l);
+        u.num_new = num_new;
+        u.need = need_bytes > 0 ? uint32_t((need_bytes + Cb - 1) / Cb) : 0u;
+      }
+    });
+    std::unique_lock<std::mutex> pool_guard(pool_mu);
+    const size_t top = free_segs.size();
+    size_t taken = 0, nch = 0, total = 0;
+    for (uint32_t i = 0; i < n; ++i) {  // request order: the pool and the chunk list
+      UpPlan& u = up_plan[i];
+      if (!u.num_new) continue;
+      if (u.need > top - taken) {
+        r[i].status = fail(CLG_E_NOSPACE, "segment pool exhausted (need %u, free %zu)", u.need, top - taken);
+        u.num_new = 0;
+        u.need = 0;
+        continue;
+      }
+      u.seg_from = taken;
+      taken += u.need;
+      if (u.num_new > int32_t(r[i].len)) {  // the segments stay (:136-143), nothing is written
+        const Log& l = logs[r[i].log];
+        r[i].status = fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d",
+                           r[i].offset_from_epoch, r[i].len, l.writer - l.epochs.find(r[i].epoch)->offset);
+        u.num_new = 0;
+        continue;
+      }
+      const uint32_t p = uint32_t(logs[r[i].log].writer);
+      u.chunks = (p + uint32_t(u.num_new) - 1) / Cb - p / Cb + 1;
+      u.ch_from = nch;
+      nch += u.chunks;
+      total += size_t(u.num_new);
+    }
+    if (int st = h_desc.ensure(std::max<size_t>(1, nch) * sizeof(clg::ScatterChunk)); st != CLG_OK) {
+      *out_st = st;
+      return true;
+    }
+    clg::ScatterChunk* ch = h_desc.as<clg::ScatterChunk>();
+    wp->run([&](unsigned k, unsigned) {
+      for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
+        const UpPlan& u = up_plan[i];
+        if (!u.need && !u.num_new) continue;
+        Log& l = logs[r[i].log];
+        for (uint32_t j = 0; j < u.need; ++j) l.segs.push_back(free_segs[top - 1 - (u.seg_from + j)]);  // pop order
+        if (!u.num_new) continue;
+        int32_t p = l.writer;
+        uint64_t src = r[i].src_off + (r[i].len - uint32_t(u.num_new));
+        uint32_t left = uint32_t(u.num_new);
+        uint64_t c = u.ch_from;
+        while (left) {
+          const uint32_t si = uint32_t(p) / Cb, so = uint32_t(p) % Cb;
+          const uint32_t take = std::min<uint32_t>(left, Cb - so);
+          ch[c++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, 0};
+          p += int32_t(take);
+          src += take;
+          left -= take;
+        }
+        l.writer += u.num_new;
+        l.flushed = l.writer;
+        reset_tail(l);  // these bytes go to HBM only
+      }
+    });
+    free_segs.resize(top - taken);
+    pool_guard.unlock();
+    *out_st = CLG_OK;
+    if (!nch) return true;
+    const size_t db = nch * sizeof(clg::ScatterChunk);
+    if ((*out_st = d_desc.ensure(db)) != CLG_OK) return true;
+    if (hipMemcpyAsync(d_desc.p, h_desc.p, db, hipMemcpyHostToDevice, stream) != hipSuccess) {
+      *out_st = fail(CLG_E_DEVICE, "hipMemcpyAsync failed");
+      return true;
+    }
+    if ((*out_st = timed("upstream_scatter", 2 * total, [&] {
+           return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream);
+         })) != CLG_OK)
+      return true;
+    *out_st = sync();
+    return true;
   }
 
   int has_delta(uint32_t h, ChKey k, int64_t epoch, int32_t* out) {  // :196-240
