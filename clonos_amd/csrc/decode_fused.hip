@@ -1516,23 +1516,27 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
 // entries are 32-bit and, reused in place, also hold the window's wide records (position |
 // window index << 16) for a compacted wide pass; without, 16-bit entries and wide records
 // decoded inline (same 2 KiB of LDS either way).
-template <bool J>
+// CW: the window's wide records compacted and decoded in a pass of their own (32-bit
+// entries); else decoded inline (16-bit entries).  Batches with tables always compact; the
+// single-launch small decode compacts too (config 1's window logs hold a TimerTrigger every
+// ten records or so, and inline each one took the whole wave through the wide decode).
+template <bool J, bool CW = J>
 struct EmitLds {
-  using PosT = typename std::conditional<J, uint32_t, uint16_t>::type;
-  static constexpr uint32_t kWin = J ? kZEmitWin : kZWin;
+  using PosT = typename std::conditional<CW, uint32_t, uint16_t>::type;
+  static constexpr uint32_t kWin = CW ? kZEmitWin : kZWin;
   uint32_t img[kZImgDw];
   PosT pos[kWin];
   uint32_t j[J ? 2 * kZJBitsDw + kZJCap : 1];
 };
 
 // Pass 3 for tile t whose first record is record `base` of the batch (wide<<31 | records).
-template <bool J>
+template <bool J, bool CW = J>
 __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, const DecodeOut& out, const uint32_t t,
-                                          const uint32_t lane, const uint64_t base, EmitLds<J>& L,
+                                          const uint32_t lane, const uint64_t base, EmitLds<J, CW>& L,
                                           const uint64_t* bm_in = nullptr) {
-  using PosT = typename EmitLds<J>::PosT;
-  constexpr uint32_t kWin = EmitLds<J>::kWin;
+  using PosT = typename EmitLds<J, CW>::PosT;
+  constexpr uint32_t kWin = EmitLds<J, CW>::kWin;
   uint32_t* const s_img = L.img;
   PosT* const s_pos = L.pos;
   uint32_t* const s_j = L.j;
@@ -1622,7 +1626,7 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
         const int64_t v0 = (int64_t)((uint64_t)v_hi << 32 | v_lo);
         const bool wide_rec = act && is_wide((int)tg);
         const uint64_t wm = __ballot(wide_rec);
-        if constexpr (J) {
+        if constexpr (CW) {
           if (act) {
             const uint32_t so = (uint32_t)(td.span_off + (a - lo));
             if (fits || rec0 + w0 + i < out.cap) {
@@ -1672,7 +1676,7 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
     __syncthreads();
     // the window's wide records, 64 at a time: field decoding and side-table rows run with
     // every lane busy instead of inside the record loop's divergent branch
-    for (uint32_t k0 = 0; J && k0 < nwide; k0 += 64) {
+    for (uint32_t k0 = 0; CW && k0 < nwide; k0 += 64) {
       const uint32_t k = k0 + lane;
       if (k < nwide) {
         const uint32_t e = s_pos[k], a = e & 0xFFFFu, i = e >> 16;
@@ -1695,7 +1699,7 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
         const bool ser = tg == CLG_TAG_SERIALIZABLE, tt = tg == CLG_TAG_TIMER_TRIGGER, sc = tg == CLG_TAG_SOURCE_CHECKPOINT;
         const uint32_t b13 = (x[3] >> 8) & 0xFFu, b21 = (x[5] >> 8) & 0xFFu, b22 = (x[5] >> 16) & 0xFFu;
         const bool tt_name = tt && b13 == 6u, sc_ref = sc && b22 != 0u;
-        const uint32_t jlen = ser ? jl_len(jl, a) : 0u;
+        const uint32_t jlen = J && ser ? jl_len(jl, a) : 0u;  // (without tables no Serializable record gets here)
         const uint32_t L = ser ? jlen : tt_name ? 18u + be32(14) : tt ? 14u : sc_ref ? 27u + be32(23) : sc ? 23u : 13u;
         const uint32_t var_off = ser ? 1u : tt_name ? 18u : sc_ref ? 27u : 0u;
         const int64_t v0 = ser ? (int64_t)L - 1 : (int64_t)((uint64_t)be32(5) << 32 | be32(9));
@@ -2182,7 +2186,7 @@ constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ul
 __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                              uint32_t n_spans, const FusedCtl& ctl, const DecodeOut& out, uint64_t* agg,
                                              uint64_t* agg_next, uint64_t* res) {
-  __shared__ EmitLds<false> L;  // its image serves the count pass too
+  __shared__ EmitLds<false, true> L;  // its image serves the count pass too
   __shared__ uint64_t s_cnt[kZSmallTiles];
   const uint32_t s = blockIdx.x, lane = threadIdx.x;
   // developer diagnostics (CLONOS_SMALL_PROF): per span, shader-clock and 100 MHz real-time stamps
@@ -2245,13 +2249,13 @@ __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles,
   uint64_t b = pre;
   for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) b += s_cnt[k];
   if (sd.n_tiles) {  // the last tile first: its image and bitmap are still here
-    emit_tile<false>(tiles, spans, cc, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
+    emit_tile<false, true>(tiles, spans, cc, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
     b += s_cnt[sd.n_tiles - 1];
   }
   uint64_t e = pre;
   for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) {
     __syncthreads();
-    emit_tile<false>(tiles, spans, cc, out, sd.first_tile + k, lane, e, L);
+    emit_tile<false, true>(tiles, spans, cc, out, sd.first_tile + k, lane, e, L);
     e += s_cnt[k];
   }
   stamp(3);
