@@ -40,6 +40,8 @@ import ctypes as C
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import itertools
+
 import numpy as np
 
 from . import _lib
@@ -356,10 +358,11 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     vslot = np.searchsorted(fv, table.vertex[gids])  # each log's failed vertex, as an index into fv
     ep_of = np.array([start_epochs[int(v)] for v in fv], np.int64)
     dest = np.array([dest_of[int(v)] for v in fv], np.int64)[vslot]
-    ck = np.fromiter(copies.keys(), np.int64, len(copies))
-    cv = np.fromiter(copies.values(), np.int64, len(copies))
-    srt = np.argsort(ck)
-    ck, cv = ck[srt], cv[srt]
+    kv = np.fromiter(itertools.chain.from_iterable(copies.items()), np.int64, 2 * len(copies)).reshape(-1, 2)
+    ck, cv = kv[:, 0], kv[:, 1]
+    if len(ck) > 1 and not (ck[1:] > ck[:-1]).all():  # (callers usually build it in gid order)
+        srt = np.argsort(ck)
+        ck, cv = ck[srt], cv[srt]
     pos = np.minimum(np.searchsorted(ck, gids), max(len(ck) - 1, 0))
     held = np.nonzero(ck[pos] == gids)[0] if len(ck) else np.zeros(0, np.int64)  # logs this rank holds
     handles = cv[pos[held]]
@@ -374,8 +377,8 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
         tot = int(lens.sum())
         buf = torch.empty(MERGE_GUARD + max(tot, 1) + MERGE_GUARD, dtype=torch.uint8, device=device)
         if tot:
-            got = io.copy_batch(handles[np.searchsorted(held, mine)], epochs[np.searchsorted(held, mine)], buf,
-                                MERGE_GUARD)
+            sel = np.searchsorted(held, mine)
+            got = io.copy_batch(handles[sel], epochs[sel], buf, MERGE_GUARD)
             if got != tot:
                 raise RuntimeError(f"logs changed during the merge ({got} != {tot} bytes)")
         offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(mine) else lens
