@@ -1966,7 +1966,7 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
       for (uint32_t t = f; t < ctl.n_tiles; ++t) {
         const ZTile z = ztile(tiles, spans, t, lane);
         *walk_end = t + 1;
-        uint64_t x = xs;
+        uint64_t x = xs, fso = ~0ull;
         uint32_t why = 0;
         bool zero = false;
         if (!z.last && xs >= z.td.span_off + z.td.len) {  // wholly inside a record: no starts
@@ -1976,14 +1976,18 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
         } else if (!z.last && zero_tile_walk(z, xs, ctl, t, lane, &x)) {
           zero = true;  // a run of Order(channel 0) records: settled without a walk
         } else {
-          uint64_t fso = ~0ull;
           why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x, nullptr, nullptr,
                                 false, 0xFFFFFFFFu, nullptr, &fso);
           __syncthreads();  // the image is reused
           if (why == 1u && lane == 0) note_error(ctl, z.td.span, fso);  // (the walk's entry is the true one)
         }
         if (why) {
-          if (lane == 0) mark_bad(ctl, why, t, z.td.span);
+          if (lane == 0) {
+            mark_bad(ctl, why, t, z.td.span);
+            // the tile's word: this chain's failure, not the count pass's from another entry
+            // (a later chunk check of this tile must not take that one for real)
+            st_agent(&ctl.ex[t], why == 1u && fso != ~0ull ? kZExFail | fso : 0ull);
+          }
           break;
         }
         const uint64_t xv = kZExValid | x;

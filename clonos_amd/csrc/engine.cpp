@@ -465,8 +465,12 @@ class WorkPool {
   void loop(unsigned i) {
     uint64_t seen = 0;
     for (;;) {
-      // a short spin (the next job of a batch comes within microseconds), then sleep
-      for (int k = 0; k < 20000 && gen_.load(std::memory_order_acquire) == seen; ++k) std::this_thread::yield();
+      // a short spin (the next job of a batch comes within microseconds), then sleep: a longer
+      // one burns the box's CPU quota between batches
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_.load(std::memory_order_acquire) == seen &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50))
+        std::this_thread::yield();
       const std::function<void(unsigned, unsigned)>* job;
       {
         std::unique_lock<std::mutex> g(mu_);
@@ -892,7 +896,7 @@ struct clg_engine {
   // attached, the chunks written and the logs advanced.  false: not applicable (a log twice).
   std::vector<uint8_t> up_seen;
   struct UpPlan {
-    int32_t num_new;
+    int32_t num_new, writer, cur;  // (the log's writer and offset in the epoch, read in the first pass)
     uint32_t need, chunks;
     uint64_t seg_from, ch_from;
   };
@@ -913,7 +917,7 @@ struct clg_engine {
     wp->run([&](unsigned k, unsigned) {
       for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
         UpPlan& u = up_plan[i];
-        u = UpPlan{0, 0, 0, 0, 0};
+        u = UpPlan{0, 0, 0, 0, 0, 0, 0};
         r[i].status = CLG_OK;
         Log* l;
         if ((r[i].status = get_log(r[i].log, &l)) != CLG_OK || r[i].len == 0) continue;
@@ -923,6 +927,8 @@ struct clg_engine {
         if (num_new <= 0) continue;
         const int64_t need_bytes = int64_t(l->writer) + num_new - capacity(*l);
         u.num_new = num_new;
+        u.writer = l->writer;
+        u.cur = cur;
         u.need = need_bytes > 0 ? uint32_t((need_bytes + Cb - 1) / Cb) : 0u;
       }
     });
@@ -941,13 +947,12 @@ struct clg_engine {
       u.seg_from = taken;
       taken += u.need;
       if (u.num_new > int32_t(r[i].len)) {  // the segments stay (:136-143), nothing is written
-        const Log& l = logs[r[i].log];
         r[i].status = fail(CLG_E_GAP, "upstream delta leaves a gap: offsetFromEpoch %d, %u bytes, log at %d",
-                           r[i].offset_from_epoch, r[i].len, l.writer - l.epochs.find(r[i].epoch)->offset);
+                           r[i].offset_from_epoch, r[i].len, u.cur);
         u.num_new = 0;
         continue;
       }
-      const uint32_t p = uint32_t(logs[r[i].log].writer);
+      const uint32_t p = uint32_t(u.writer);  // (no log record touched in this serial pass)
       u.chunks = (p + uint32_t(u.num_new) - 1) / Cb - p / Cb + 1;
       u.ch_from = nch;
       nch += u.chunks;
