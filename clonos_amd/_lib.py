@@ -35,6 +35,7 @@ STATUS_NAMES = {v: k for k, v in globals().items() if k.startswith("CLG_E_") or 
 
 CLG_MEM_HOST = 0
 CLG_MEM_DEVICE = 1
+CLG_MEM_MAPPED = 2  # host memory registered with clg_host_register (the small decode writes it directly)
 CLG_F_TIMING = 1
 CLG_F_ROBUST_DECODE = 2
 CLG_F_ASYNC_SLICE = 4
@@ -59,6 +60,7 @@ EXPORTED = [
     "clg_replay_prepare", "clg_encode_batch", "clg_enrich_batch", "clg_process_delta",
     "clg_ifl_open", "clg_ifl_open_typed", "clg_ifl_close", "clg_ifl_log_batch", "clg_ifl_notify_checkpoint_complete", "clg_ifl_state",
     "clg_ifl_replay_batch", "clg_replay_prepare_device", "clg_get_determinants_batch", "clg_response_put_batch",
+    "clg_host_register", "clg_host_unregister",
 ]
 
 
@@ -287,6 +289,8 @@ def _load() -> C.CDLL:
         "clg_decode_logs": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_decode_logs_async": (C.c_int, [P, P, P, C.c_uint32, C.POINTER(Decoded), P]),
         "clg_decode_wait": (C.c_int, [P]),
+        "clg_host_register": (C.c_int, [P, C.c_uint64]),
+        "clg_host_unregister": (C.c_int, [P]),
         "clg_replay_prep": (C.c_int, [P, P, P, P, P, C.c_uint32, P, u32p, C.POINTER(Decoded), P]),
         "clg_kernel_stats": (C.c_int, [P, C.POINTER(KernelStat), C.c_uint32, u32p]),
         "clg_kernel_stats_reset": (C.c_int, [P]),

@@ -495,6 +495,24 @@ class WorkPool {
 
 }  // namespace
 
+// clg_host_register's ranges: host base -> device address (for CLG_MEM_MAPPED outputs)
+namespace {
+struct Mapped {
+  uintptr_t host;
+  uint64_t bytes;
+  uintptr_t dev;
+};
+std::mutex g_map_mu;
+std::vector<Mapped> g_mapped;
+// The device address of registered host memory at h (0: not inside a registered range).
+uintptr_t clg_mapped_device_address(const void* h) {
+  std::lock_guard<std::mutex> g(g_map_mu);
+  for (const Mapped& m : g_mapped)
+    if (uintptr_t(h) >= m.host && uintptr_t(h) < m.host + m.bytes) return m.dev + (uintptr_t(h) - m.host);
+  return 0;
+}
+}  // namespace
+
 namespace clg_internal {  // error text for the host-only translation units (response.cpp)
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 }  // namespace clg_internal
@@ -1687,9 +1705,12 @@ struct clg_engine {
     const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
     // pass 0 (small whole spans, a lane each) for batches without Serializable tables
     const bool tiny = p.n_tiny && !jser && !prof_path && !getenv("CLONOS_FUSED_NODEP");
+    std::optional<HostTimer> hsub(std::in_place, this, "host_launch_chunks");  // (CLONOS_HOST_PROF sub-stages)
     if (chunked) count_chunks(p, G, tiny, chunk_buf);
     PlanLayout L;
+    hsub.emplace(this, "host_launch_stage");
     CHK(stage_plan(p, d_ztiles, &L, chunked ? &chunk_buf : nullptr));
+    hsub.emplace(this, "host_launch_enqueue");
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
     // words: st_x[nt] ex[nt] rep_flag[nt] (u8) cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] |
@@ -1885,9 +1906,23 @@ struct clg_engine {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
         p.only)
       return false;
-    if (out->out_kind != CLG_MEM_DEVICE && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
+    if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
+    if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
     for (const auto& sd : p.spans)
       if (sd.n_tiles > clg::kZSmallTiles) return false;
+    return true;
+  }
+  // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered)
+  static bool mapped_outputs(const clg_decoded& out, clg::DecodeOut* o) {
+    void* h[9] = {out.off, out.tag, out.v0, out.w_idx, out.w_rc, out.w_v1, out.w_var_off, out.w_var_len, out.w_sub};
+    uintptr_t d[9];
+    for (int i = 0; i < 9; ++i)
+      if (!(d[i] = clg_mapped_device_address(h[i]))) return false;
+    if (o)
+      *o = clg::DecodeOut{reinterpret_cast<uint32_t*>(d[0]), reinterpret_cast<uint8_t*>(d[1]), reinterpret_cast<int64_t*>(d[2]),
+                          reinterpret_cast<uint32_t*>(d[3]), reinterpret_cast<int32_t*>(d[4]), reinterpret_cast<int64_t*>(d[5]),
+                          reinterpret_cast<uint32_t*>(d[6]), reinterpret_cast<uint32_t*>(d[7]), reinterpret_cast<uint8_t*>(d[8]),
+                          out.cap, out.wcap};
     return true;
   }
   // The plan's device-planned runs as host-built tiles (k_expand_tiles' rule, on the host).
@@ -1930,7 +1965,7 @@ struct clg_engine {
     }
     // outputs: the caller's device arrays, or pinned host memory the kernel writes directly
     clg::DecodeOut o{};
-    const bool host = out->out_kind != CLG_MEM_DEVICE;
+    const bool host = out->out_kind == CLG_MEM_HOST;
     const uint64_t cap = std::max<uint64_t>(1, out->cap), wcap = std::max<uint64_t>(1, out->wcap);
     uint64_t at[10] = {0};
     const uint64_t sz[9] = {cap * 4, cap, cap * 8, wcap * 4, wcap * 4, wcap * 8, wcap * 4, wcap * 4, wcap};
@@ -1942,6 +1977,8 @@ struct clg_engine {
                          reinterpret_cast<uint32_t*>(hb + at[3]), reinterpret_cast<int32_t*>(hb + at[4]),
                          reinterpret_cast<int64_t*>(hb + at[5]), reinterpret_cast<uint32_t*>(hb + at[6]),
                          reinterpret_cast<uint32_t*>(hb + at[7]), hb + at[8], out->cap, out->wcap};
+    } else if (out->out_kind == CLG_MEM_MAPPED) {  // registered host memory: written from the GPU directly
+      mapped_outputs(*out, &o);
     } else {
       o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
                          out->w_var_len, out->w_sub, out->cap, out->wcap};
@@ -2516,6 +2553,35 @@ void clg_config_default(clg_config* cfg) {
 }
 
 int clg_abi_version(void) { return CLG_ABI_VERSION; }
+
+
+int clg_host_register(void* p, uint64_t bytes) {
+  if (!p || !bytes) return fail(CLG_E_INVALID_ARG, "null or empty range");
+  hipError_t er = hipHostRegister(p, size_t(bytes), hipHostRegisterMapped);
+  if (er != hipSuccess) return fail(CLG_E_DEVICE, "hipHostRegister(%llu bytes): %s", (unsigned long long)bytes,
+                                     hipGetErrorString(er));
+  void* d = nullptr;
+  er = hipHostGetDevicePointer(&d, p, 0);
+  if (er != hipSuccess) {
+    (void)hipHostUnregister(p);
+    return fail(CLG_E_DEVICE, "hipHostGetDevicePointer: %s", hipGetErrorString(er));
+  }
+  std::lock_guard<std::mutex> g(g_map_mu);
+  g_mapped.push_back(Mapped{uintptr_t(p), bytes, uintptr_t(d)});
+  return CLG_OK;
+}
+
+int clg_host_unregister(void* p) {
+  {
+    std::lock_guard<std::mutex> g(g_map_mu);
+    auto it = std::find_if(g_mapped.begin(), g_mapped.end(), [&](const Mapped& m) { return m.host == uintptr_t(p); });
+    if (it == g_mapped.end()) return fail(CLG_E_INVALID_ARG, "range not registered");
+    g_mapped.erase(it);
+  }
+  const hipError_t er = hipHostUnregister(p);
+  return er == hipSuccess ? CLG_OK : fail(CLG_E_DEVICE, "hipHostUnregister: %s", hipGetErrorString(er));
+}
+
 
 const char* clg_last_error(void) { return g_err.c_str(); }
 

@@ -11,6 +11,7 @@ exception: CorruptDeterminantArrayException, RuntimeException("Consumer went bac
 from __future__ import annotations
 
 import ctypes as C
+import mmap
 import sys
 from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
@@ -147,6 +148,7 @@ class Engine:
         self._h = h
         self._out_buf: Optional[np.ndarray] = None  # _pooled_outputs
         self._out_cache = None
+        self._out_mapped = False
         self.segment_bytes = segment_bytes
         self.sharing_depth = sharing_depth
         self.async_slice = async_slice
@@ -156,6 +158,7 @@ class Engine:
     # ---- lifecycle ----------------------------------------------------------------
     def close(self):
         if self._h:
+            self._out_release()
             lib.clg_engine_destroy(self._h)
             self._h = None
 
@@ -302,13 +305,18 @@ class Engine:
                    ("w_var_len", np.uint32, 4, 1), ("w_sub", np.uint8, 1, 1))
 
     @staticmethod
-    def _host_outputs(cap: int, wcap: int, buf: Optional[np.ndarray] = None):
-        """The SoA output arrays as views of one host buffer (one allocation, one pointer),
-        and their clg_decoded.  buf: a buffer to carve them from (large enough), else a new one."""
+    def _out_bytes(cap: int, wcap: int) -> Tuple[List[int], int]:
         offs, at = [], 0
         for _, _, isz, wide in Engine._OUT_FIELDS:
             offs.append(at)
             at = (at + isz * (wcap if wide else cap) + 15) & ~15
+        return offs, at
+
+    @staticmethod
+    def _host_outputs(cap: int, wcap: int, buf: Optional[np.ndarray] = None):
+        """The SoA output arrays as views of one host buffer (one allocation, one pointer),
+        and their clg_decoded.  buf: a buffer to carve them from (large enough), else a new one."""
+        offs, at = Engine._out_bytes(cap, wcap)
         if buf is None or buf.size < at:
             buf = np.empty(max(at, 16), np.uint8)
         b0 = buf.ctypes.data
@@ -327,17 +335,34 @@ class Engine:
         for the same capacities the views and clg_decoded of the last call serve again."""
         buf, key = self._out_buf, (cap, wcap)
         # references when free: the attribute, `buf`, getrefcount's argument, the 9 cached views
-        if buf is not None and sys.getrefcount(buf) > 3 + len(self._OUT_FIELDS):
-            buf = self._out_buf = self._out_cache = None
+        if buf is not None and (sys.getrefcount(buf) > 3 + len(self._OUT_FIELDS) or buf.size < self._out_bytes(cap, wcap)[1]):
+            self._out_release()
+            buf = None
         if buf is not None and self._out_cache is not None and self._out_cache[0] == key:
             d, arrs = self._out_cache[1], self._out_cache[2]
             d.n_rec = d.n_wide = 0
             return d, arrs
         self._out_cache = None  # (its views would hold the old buffer)
+        if buf is None:  # page-aligned (an anonymous mapping; the views' base is this array), and
+            # registered for the device (clg_host_register): the single-launch small decode writes
+            # the outputs straight into it (CLG_MEM_MAPPED)
+            need = (max(self._out_bytes(cap, wcap)[1], 1 << 16) + 4095) & ~4095
+            buf = np.frombuffer(mmap.mmap(-1, need), np.uint8)
+            self._out_mapped = self._h is not None and lib.clg_host_register(_np_ptr(buf), need) == _lib.CLG_OK
         d, arrs = self._host_outputs(cap, wcap, buf)
-        self._out_buf = arrs["off"].base
+        if self._out_mapped:
+            d.out_kind = _lib.CLG_MEM_MAPPED
+        self._out_buf = buf
         self._out_cache = (key, d, arrs)
         return d, arrs
+
+    def _out_release(self):
+        """Drop the pooled output buffer (unregistered first: a batch the caller keeps stays
+        valid as ordinary host memory)."""
+        if self._out_buf is not None and self._out_mapped:
+            lib.clg_host_unregister(_np_ptr(self._out_buf))
+        self._out_buf = self._out_cache = None
+        self._out_mapped = False
 
     def _finish(self, st, d, arrs, base, n_spans, spans_bytes):
         if st != _lib.CLG_OK:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 4
+#define CLG_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -59,7 +59,16 @@ enum {
                                     ReplayIterator NPEs at logToReplay.get(++currentKey), :133) */
 };
 
-enum { CLG_MEM_HOST = 0, CLG_MEM_DEVICE = 1 };
+/* CLG_MEM_MAPPED: host memory registered with clg_host_register.  For decode outputs
+ * (clg_decoded.out_kind) the single-launch small decode writes it straight from the GPU (no
+ * staging copy); every other path treats it as CLG_MEM_HOST. */
+enum { CLG_MEM_HOST = 0, CLG_MEM_DEVICE = 1, CLG_MEM_MAPPED = 2 };
+
+/* Pin and map [p, p + bytes) of host memory for the device (hipHostRegister, mapped); a
+ * caller that keeps its output buffers across decodes registers them once.  Unregister
+ * before the memory is freed. */
+int clg_host_register(void* p, uint64_t bytes);
+int clg_host_unregister(void* p);
 
 /* Determinant tags (Determinant.java:23-34). */
 enum {

@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_struct_sizes():
     from clonos_amd import _lib
-    assert _lib.lib.clg_abi_version() == 4
+    assert _lib.lib.clg_abi_version() == 5
     assert ctypes.sizeof(_lib.IflReplayRes) == 48
     assert ctypes.sizeof(_lib.IflReplayReq) == 24
     assert ctypes.sizeof(_lib.CausalLogIdC) == 24

@@ -8,13 +8,17 @@ import numpy as np
 from clonos_amd.engine import Engine
 
 
-class _E:  # the two attributes _pooled_outputs uses, without a GPU engine
+class _E:  # what _pooled_outputs uses, without a GPU engine (no handle: nothing registered)
     _OUT_FIELDS = Engine._OUT_FIELDS
     _host_outputs = staticmethod(Engine._host_outputs)
+    _out_bytes = staticmethod(Engine._out_bytes)
+    _out_release = Engine._out_release
 
     def __init__(self):
         self._out_buf = None
         self._out_cache = None
+        self._out_mapped = False
+        self._h = None
 
 
 def test_layout_matches_pointers():
@@ -32,6 +36,9 @@ def test_layout_matches_pointers():
 
 def test_pool_never_overwrites_a_live_batch():
     e = _E()
+    d0, a0 = Engine._pooled_outputs(e, 100, 10)
+    assert a0["off"].base is e._out_buf and e._out_buf.ctypes.data % 4096 == 0  # page-aligned, views on it
+    del a0
     d, a = Engine._pooled_outputs(e, 100, 10)
     a["off"][:3] = [1, 2, 3]
     kept = a["v0"][:2], a["off"][:5]
@@ -46,6 +53,7 @@ def test_pool_never_overwrites_a_live_batch():
     d3, a3 = Engine._pooled_outputs(e, 100, 10)
     assert id(e._out_buf) == second and d3 is d2  # free again: reused, views and struct too
     del a3
-    Engine._pooled_outputs(e, 5000, 10)  # larger than the buffer: a new one
-    assert id(e._out_buf) != second
+    small = e._out_buf.size
+    Engine._pooled_outputs(e, 50000, 10)  # larger than the buffer: a new one
+    assert e._out_buf.size > small
     assert sys.getrefcount(e._out_buf) > 3  # the cache's views hold it
