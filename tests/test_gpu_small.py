@@ -146,3 +146,35 @@ def test_small_device_outputs():
             lo, hi = int(base[s]), int(base[s + 1])
             np.testing.assert_array_equal(tag[lo:hi], r["tag"])
             np.testing.assert_array_equal(v0[lo:hi], r["v0"])
+
+
+def test_small_mapped_outputs_kept_batches_stay_intact():
+    """decode_logs' outputs are views of the engine's pooled, registered host buffer
+    (CLG_MEM_MAPPED): the small decode writes them from the GPU.  A batch the caller keeps is
+    never overwritten -- the next decode gets a new buffer -- and both equal the oracle; once
+    the kept batch is dropped the pool's buffer is reused."""
+    from clonos_amd import _lib
+    rng = np.random.default_rng(synth.SEED_CONFIG1)
+    graph, data = synth.config1_job(rng)
+    with _eng(sharing_depth=1) as eng:
+        logs = {lid: eng.open_log(lid) for lid in data}
+        for lid, b in data.items():
+            logs[lid].appendDeterminant(b, 0)
+        lids = list(data)
+        first = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        assert eng._out_mapped and eng._out_cache[1].out_kind == _lib.CLG_MEM_MAPPED
+        snap = first.v0.copy()
+        buf1 = eng._out_buf.ctypes.data
+        second = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        assert eng._out_buf.ctypes.data != buf1  # the kept batch holds the first buffer
+        np.testing.assert_array_equal(first.v0, snap)
+        for dec in (first, second):
+            for s, l in enumerate(lids):
+                assert_span_equal(dec, s, data[l])
+        del first, dec
+        buf2 = eng._out_buf.ctypes.data
+        del second
+        third = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        assert eng._out_buf.ctypes.data == buf2  # free again: reused
+        for s, l in enumerate(lids):
+            assert_span_equal(third, s, data[l])
