@@ -146,9 +146,7 @@ class Engine:
         h = C.c_void_p()
         check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))
         self._h = h
-        self._out_buf: Optional[np.ndarray] = None  # _pooled_outputs
-        self._out_cache = None
-        self._out_mapped = False
+        self._out_slots: List[dict] = []  # _pooled_outputs
         self.segment_bytes = segment_bytes
         self.sharing_depth = sharing_depth
         self.async_slice = async_slice
@@ -328,41 +326,66 @@ class Engine:
         d.cap, d.wcap, d.out_kind = cap, wcap, _lib.CLG_MEM_HOST
         return d, arrs
 
+    _OUT_SLOTS = 3  # pooled output buffers (a caller usually keeps one batch while asking for the next)
+
     def _pooled_outputs(self, cap: int, wcap: int):
-        """_host_outputs from the engine's reusable buffer when no earlier result still holds
-        it (every returned array is a view of it, so a live batch keeps its reference count up):
-        its pages stay mapped, so the outputs are not page-faulted in again on every call, and
-        for the same capacities the views and clg_decoded of the last call serve again."""
-        buf, key = self._out_buf, (cap, wcap)
-        # references when free: the attribute, `buf`, getrefcount's argument, the 9 cached views
-        if buf is not None and (sys.getrefcount(buf) > 3 + len(self._OUT_FIELDS) or buf.size < self._out_bytes(cap, wcap)[1]):
-            self._out_release()
-            buf = None
-        if buf is not None and self._out_cache is not None and self._out_cache[0] == key:
-            d, arrs = self._out_cache[1], self._out_cache[2]
+        """_host_outputs from one of the engine's reusable buffers that no earlier result still
+        holds (every returned array is a view of its buffer, so a live batch keeps the buffer's
+        reference count up): the pages stay mapped -- not faulted in on every call -- and
+        registered for the device (clg_host_register), so the single-launch small decode writes
+        the outputs straight into them (CLG_MEM_MAPPED).  For the same capacities the views and
+        clg_decoded of the slot's last call serve again."""
+        key, need = (cap, wcap), self._out_bytes(cap, wcap)[1]
+        pick = None
+        for sl in self._out_slots:
+            # references when free: the slot, getrefcount's argument, and the cached views
+            free = sys.getrefcount(sl["buf"]) <= 2 + (len(self._OUT_FIELDS) if sl["cache"] is not None else 0)
+            if free and sl["buf"].size >= need:
+                pick = sl
+                break
+        if pick is None:
+            if len(self._out_slots) >= self._OUT_SLOTS:  # all held (or too small): the oldest leaves the pool
+                self._slot_release(self._out_slots.pop(0))
+            size = (max(need, 1 << 16) + 4095) & ~4095  # page-aligned: an anonymous mapping
+            buf = np.frombuffer(mmap.mmap(-1, size), np.uint8)
+            mapped = self._h is not None and lib.clg_host_register(_np_ptr(buf), size) == _lib.CLG_OK
+            pick = {"buf": buf, "mapped": mapped, "cache": None}
+            self._out_slots.append(pick)
+        else:  # the most recent last (by identity: the slots hold arrays)
+            self._out_slots = [sl for sl in self._out_slots if sl is not pick] + [pick]
+        if pick["cache"] is not None and pick["cache"][0] == key:
+            d, arrs = pick["cache"][1], pick["cache"][2]
             d.n_rec = d.n_wide = 0
             return d, arrs
-        self._out_cache = None  # (its views would hold the old buffer)
-        if buf is None:  # page-aligned (an anonymous mapping; the views' base is this array), and
-            # registered for the device (clg_host_register): the single-launch small decode writes
-            # the outputs straight into it (CLG_MEM_MAPPED)
-            need = (max(self._out_bytes(cap, wcap)[1], 1 << 16) + 4095) & ~4095
-            buf = np.frombuffer(mmap.mmap(-1, need), np.uint8)
-            self._out_mapped = self._h is not None and lib.clg_host_register(_np_ptr(buf), need) == _lib.CLG_OK
-        d, arrs = self._host_outputs(cap, wcap, buf)
-        if self._out_mapped:
+        pick["cache"] = None  # (its views would hold the buffer)
+        d, arrs = self._host_outputs(cap, wcap, pick["buf"])
+        if pick["mapped"]:
             d.out_kind = _lib.CLG_MEM_MAPPED
-        self._out_buf = buf
-        self._out_cache = (key, d, arrs)
+        pick["cache"] = (key, d, arrs)
         return d, arrs
 
+    def _slot_release(self, sl):
+        """A pooled buffer leaves the pool: unregistered (a batch the caller keeps stays valid as
+        ordinary host memory)."""
+        if sl["mapped"]:
+            lib.clg_host_unregister(_np_ptr(sl["buf"]))
+        sl["cache"] = None
+
     def _out_release(self):
-        """Drop the pooled output buffer (unregistered first: a batch the caller keeps stays
-        valid as ordinary host memory)."""
-        if self._out_buf is not None and self._out_mapped:
-            lib.clg_host_unregister(_np_ptr(self._out_buf))
-        self._out_buf = self._out_cache = None
-        self._out_mapped = False
+        while self._out_slots:
+            self._slot_release(self._out_slots.pop())
+
+    @property
+    def _out_buf(self):  # the most recently used pooled buffer (tests)
+        return self._out_slots[-1]["buf"] if self._out_slots else None
+
+    @property
+    def _out_cache(self):
+        return self._out_slots[-1]["cache"] if self._out_slots else None
+
+    @property
+    def _out_mapped(self):
+        return bool(self._out_slots) and self._out_slots[-1]["mapped"]
 
     def _finish(self, st, d, arrs, base, n_spans, spans_bytes):
         if st != _lib.CLG_OK:

@@ -175,6 +175,6 @@ def test_small_mapped_outputs_kept_batches_stay_intact():
         buf2 = eng._out_buf.ctypes.data
         del second
         third = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
-        assert eng._out_buf.ctypes.data == buf2  # free again: reused
+        assert eng._out_buf.ctypes.data in (buf1, buf2) and len(eng._out_slots) == 2  # free again: reused
         for s, l in enumerate(lids):
             assert_span_equal(third, s, data[l])

@@ -10,14 +10,17 @@ from clonos_amd.engine import Engine
 
 class _E:  # what _pooled_outputs uses, without a GPU engine (no handle: nothing registered)
     _OUT_FIELDS = Engine._OUT_FIELDS
+    _OUT_SLOTS = Engine._OUT_SLOTS
     _host_outputs = staticmethod(Engine._host_outputs)
     _out_bytes = staticmethod(Engine._out_bytes)
+    _slot_release = Engine._slot_release
     _out_release = Engine._out_release
+    _out_buf = Engine._out_buf
+    _out_cache = Engine._out_cache
+    _out_mapped = Engine._out_mapped
 
     def __init__(self):
-        self._out_buf = None
-        self._out_cache = None
-        self._out_mapped = False
+        self._out_slots = []
         self._h = None
 
 
@@ -43,17 +46,26 @@ def test_pool_never_overwrites_a_live_batch():
     a["off"][:3] = [1, 2, 3]
     kept = a["v0"][:2], a["off"][:5]
     del a
-    first = id(e._out_buf)
+    first = e._out_buf.ctypes.data
     d2, a2 = Engine._pooled_outputs(e, 100, 10)
-    assert id(e._out_buf) != first  # the kept slices hold the first buffer
+    assert e._out_buf.ctypes.data != first  # the kept slices hold the first buffer: a second slot
     a2["off"][:3] = 7
     assert list(kept[1][:3]) == [1, 2, 3]
-    del kept, a2
-    second = id(e._out_buf)
+    del a2
+    second = e._out_buf.ctypes.data
     d3, a3 = Engine._pooled_outputs(e, 100, 10)
-    assert id(e._out_buf) == second and d3 is d2  # free again: reused, views and struct too
+    assert e._out_buf.ctypes.data == second and d3 is d2  # free again: reused, views and struct too
     del a3
-    small = e._out_buf.size
-    Engine._pooled_outputs(e, 50000, 10)  # larger than the buffer: a new one
+    # the caller keeps one batch while asking for the next: two slots alternate, no new buffer
+    seen = set()
+    prev = None
+    for _ in range(6):
+        d, a = Engine._pooled_outputs(e, 100, 10)
+        seen.add(e._out_buf.ctypes.data)
+        prev = a  # noqa: F841 (held across the next call)
+    assert len(e._out_slots) <= Engine._OUT_SLOTS and len(seen) <= 2
+    assert list(kept[1][:3]) == [1, 2, 3]  # (the kept batch is never handed out)
+    del prev, a, kept
+    small = max(sl["buf"].size for sl in e._out_slots)
+    Engine._pooled_outputs(e, 50000, 10)  # larger than every buffer: a new one
     assert e._out_buf.size > small
-    assert sys.getrefcount(e._out_buf) > 3  # the cache's views hold it
