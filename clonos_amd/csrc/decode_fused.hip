@@ -1207,8 +1207,14 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
 // Without row pads every region starts on bank 0, so the lanes' first reads would all hit
 // one bank: there the warm-up grows by 4 (lane & 7) bytes, putting eight start banks in each
 // group of lanes (the walk is a function of the tile's bytes either way).
+#ifndef CLG_WARM_STAGGER
+#define CLG_WARM_STAGGER 0  // 0: 4 (lane & 7) bytes; 1: 4 ((lane >> 1) & 15); 2: 4 ((lane >> 1) & 7)
+#endif
 __device__ __forceinline__ uint32_t warm_start(uint32_t rs, uint32_t lo, uint32_t warm, uint32_t lane) {
-  const uint32_t w = kZPad == 0 ? warm + 4u * (lane & 7u) : warm;
+  // (regions start 32 dwords apart: banks 0 and 32 by lane parity -- the stagger's dword
+  // offsets spread them: lane & 7 gives 8 banks, (lane >> 1) & 15 with the parity 32)
+  const uint32_t st = CLG_WARM_STAGGER == 1 ? ((lane >> 1) & 15u) : CLG_WARM_STAGGER == 2 ? ((lane >> 1) & 7u) : (lane & 7u);
+  const uint32_t w = kZPad == 0 ? warm + 4u * st : warm;
   return rs >= lo + w ? rs - w : lo;
 }
 
