@@ -1208,13 +1208,16 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
 // one bank: there the warm-up grows by 4 (lane & 7) bytes, putting eight start banks in each
 // group of lanes (the walk is a function of the tile's bytes either way).
 #ifndef CLG_WARM_STAGGER
-#define CLG_WARM_STAGGER 0  // 0: 4 (lane & 7) bytes; 1: 4 ((lane >> 1) & 15); 2: 4 ((lane >> 1) & 7)
+#define CLG_WARM_STAGGER 1  // 0: 4 (lane & 7) bytes; 1: 4 ((lane >> 1) & 15); 2: 4 ((lane >> 1) & 7)
 #endif
+constexpr uint32_t kZWarmFlat = 1u << 31;  // FusedCtl::warm flag: no stagger (a lone wave: latency first)
 __device__ __forceinline__ uint32_t warm_start(uint32_t rs, uint32_t lo, uint32_t warm, uint32_t lane) {
-  // (regions start 32 dwords apart: banks 0 and 32 by lane parity -- the stagger's dword
-  // offsets spread them: lane & 7 gives 8 banks, (lane >> 1) & 15 with the parity 32)
+  // Regions start 32 dwords apart, so the lanes' first reads hit banks 0 and 32 only (by lane
+  // parity) and, walking at similar speeds, keep colliding.  The stagger's dword offsets
+  // spread them: (lane >> 1) & 15 with the parity gives 32 banks (config-2 count 0.165 ->
+  // 0.153 ms against lane & 7's 8 banks; tools/ab.sh), at 30 B more warm-up on average.
   const uint32_t st = CLG_WARM_STAGGER == 1 ? ((lane >> 1) & 15u) : CLG_WARM_STAGGER == 2 ? ((lane >> 1) & 7u) : (lane & 7u);
-  const uint32_t w = kZPad == 0 ? warm + 4u * st : warm;
+  const uint32_t w = (warm & kZWarmFlat) ? (warm & ~kZWarmFlat) : (kZPad == 0 ? warm + 4u * st : warm);
   return rs >= lo + w ? rs - w : lo;
 }
 

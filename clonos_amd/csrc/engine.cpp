@@ -2007,7 +2007,8 @@ struct clg_engine {
     }();
     // warm-up 32 B: a lone wave per span waits on every step, and shorter warm-ups cost fewer
     // merges than they save (config 1: the kernel 65 -> 62 us at 32 or 16 B, 63 at 48)
-    ctl.warm = small_warm >= 0 ? uint32_t(small_warm) : 32u;
+    static const bool small_stagger = getenv("CLONOS_SMALL_STAGGER") != nullptr;  // developer switch
+    ctl.warm = (small_warm >= 0 ? uint32_t(small_warm) : 32u) | (small_stagger ? 0u : (1u << 31));
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
       CHK(d_prof.ensure(size_t(ns + nt) * 64));

@@ -197,7 +197,7 @@ struct FusedCtl {
   uint32_t jser;
   uint32_t jwork_cap;  // capacity of the general-walker work list
   uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
-  uint32_t warm;    // speculative warm-up bytes before each region
+  uint32_t warm;    // speculative warm-up bytes before each region (| 1 << 31: not staggered by lane)
   JArena jar;       // the stream walker's spill arena (k_decode_jser_general)
   // Per-span fallback: a tile whose chain goes wrong (reasons 1-3, 5) sets span_bad[span]
   // and the count pass goes on with the next span; the host decodes the bad spans with the
