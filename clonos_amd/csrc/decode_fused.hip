@@ -2409,6 +2409,9 @@ constexpr int kZJReg = 4;  // candidates a lane keeps in registers (more: second
 constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser_general fills it
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
+#ifndef CLG_JSER_ROT
+#define CLG_JSER_ROT 1  // the magic scan's rows read from a per-lane starting dword (A/B switch)
+#endif
 __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_cand, const uint32_t t,
                                           const uint32_t lane, bool* flagged) {
@@ -2430,6 +2433,26 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   const uint32_t r0 = lane * kZRegion;
   const uint32_t* row = s_img + lane * kZPitch;
   uint64_t edm = 0;  // bit j: dword j (0..33) holds an ED byte
+#if CLG_JSER_ROT
+  // Without row pads the rows start 32 dwords apart, so reading dword j of every row at once
+  // hits two banks (a 32-way conflict: 7.4 cycles per LDS instruction).  Each lane starts its
+  // pass at its own dword (lane & 31) and wraps, so the wave's reads spread over the banks.
+  const uint32_t rot = kZPad == 0 ? (lane & 31u) : 0u;
+  for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
+    uint32_t D[17], J[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 17; ++j) {
+      const uint32_t k = j0 + j + rot;
+      J[j] = k >= kZRowDw + 2u ? k - (kZRowDw + 2u) : k;
+      D[j] = row[J[j]];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 17; ++j) {
+      const uint32_t e = D[j] ^ 0xEDEDEDEDu;
+      edm |= (((e - 0x01010101u) & ~e & 0x80808080u) ? 1ull : 0ull) << J[j];
+    }
+  }
+#else
   for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
     uint32_t D[17];
 #pragma unroll
@@ -2440,6 +2463,7 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
       edm |= (((e - 0x01010101u) & ~e & 0x80808080u) ? 1ull : 0ull) << (j0 + j);
     }
   }
+#endif
   uint64_t sm = (edm | (edm >> 1)) & 0xFFFFFFFFull;  // dwords where a magic may start
   while (sm) {
     const uint32_t j = (uint32_t)__builtin_ctzll(sm);
