@@ -2410,7 +2410,7 @@ constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
 #ifndef CLG_JSER_ROT
-#define CLG_JSER_ROT 1  // the magic scan's rows read from a per-lane starting dword (A/B switch)
+#define CLG_JSER_ROT 0  // rotated magic-scan row reads (A/B on MI355X: jser 0.262 vs 0.262 ms, config-3 subset; off)
 #endif
 __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_cand, const uint32_t t,

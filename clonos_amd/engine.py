@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes as C
 import mmap
 import sys
+import threading
 from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -147,6 +148,9 @@ class Engine:
         check(lib.clg_engine_create(C.byref(cfg), C.byref(h)))
         self._h = h
         self._out_slots: List[dict] = []  # _pooled_outputs
+        self._in_sc = None  # _in_scratch
+        self._in_mu = threading.Lock()  # its user
+        self._pool_mu = threading.Lock()  # slot picks (a picked slot is busy until _finish)
         self.segment_bytes = segment_bytes
         self.sharing_depth = sharing_depth
         self.async_slice = async_slice
@@ -303,18 +307,21 @@ class Engine:
                    ("w_var_len", np.uint32, 4, 1), ("w_sub", np.uint8, 1, 1))
 
     @staticmethod
-    def _out_bytes(cap: int, wcap: int) -> Tuple[List[int], int]:
+    def _out_bytes(cap: int, wcap: int, bcap: int = 0) -> Tuple[List[int], int]:
+        """Offsets of the nine arrays (16-byte aligned), then of span_rec_base (bcap entries)."""
         offs, at = [], 0
         for _, _, isz, wide in Engine._OUT_FIELDS:
             offs.append(at)
             at = (at + isz * (wcap if wide else cap) + 15) & ~15
-        return offs, at
+        offs.append(at)
+        return offs, at + 8 * bcap
 
     @staticmethod
-    def _host_outputs(cap: int, wcap: int, buf: Optional[np.ndarray] = None):
+    def _host_outputs(cap: int, wcap: int, buf: Optional[np.ndarray] = None, bcap: int = 0):
         """The SoA output arrays as views of one host buffer (one allocation, one pointer),
-        and their clg_decoded.  buf: a buffer to carve them from (large enough), else a new one."""
-        offs, at = Engine._out_bytes(cap, wcap)
+        and their clg_decoded.  buf: a buffer to carve them from (large enough), else a new one.
+        bcap: also a span_rec_base array ("base") of that many entries."""
+        offs, at = Engine._out_bytes(cap, wcap, bcap)
         if buf is None or buf.size < at:
             buf = np.empty(max(at, 16), np.uint8)
         b0 = buf.ctypes.data
@@ -323,46 +330,83 @@ class Engine:
         for (k, dt, isz, wide), o in zip(Engine._OUT_FIELDS, offs):
             arrs[k] = buf[o:o + isz * (wcap if wide else cap)].view(dt)
             setattr(d, k, b0 + o)
+        if bcap:
+            arrs["base"] = buf[offs[-1]:offs[-1] + 8 * bcap].view(np.uint64)
         d.cap, d.wcap, d.out_kind = cap, wcap, _lib.CLG_MEM_HOST
         return d, arrs
 
+    @staticmethod
+    def _slot_capacity(size: int, cap: int, wcap: int, bcap: int) -> Tuple[int, int, int]:
+        """The largest capacities in the proportions of (cap, wcap) -- and at least 256 span
+        entries -- whose arrays fit a slot of `size` bytes; (cap, wcap, bcap) when they do not."""
+        b = max(bcap, 256)
+        k = (size - 8 * b - 160) / max(13 * cap + 25 * wcap, 1)  # 160: more than the padding
+        if k < 1.0:
+            return cap, wcap, bcap
+        return int(cap * k), int(wcap * k), b
+
     _OUT_SLOTS = 3  # pooled output buffers (a caller usually keeps one batch while asking for the next)
 
-    def _pooled_outputs(self, cap: int, wcap: int):
+    @staticmethod
+    def _slot_free(sl) -> bool:
+        # not between its pick and _finish, and references when free: the slot, getrefcount's
+        # argument, and the cached views
+        return not sl["busy"] and sys.getrefcount(sl["buf"]) <= 2 + (
+            len(sl["cache"][2]) if sl["cache"] is not None else 0)
+
+    def _slot_done(self, arrs) -> None:
+        """The decode that picked the slot of `arrs` has made its result (or failed)."""
+        for sl in self._out_slots:
+            if sl["cache"] is not None and sl["cache"][2] is arrs:
+                sl["busy"] = False
+
+    def _slot_use(self, pick):
+        """The slot becomes busy and the most recent (by identity: the slots hold arrays); its
+        cached clg_decoded, views and byref, counts reset."""
+        pick["busy"] = True
+        if self._out_slots[-1] is not pick:
+            self._out_slots = [sl for sl in self._out_slots if sl is not pick] + [pick]
+        _, d, arrs, ref = pick["cache"]
+        d.n_rec = d.n_wide = 0
+        return d, arrs, ref
+
+    def _pooled_outputs(self, cap: int, wcap: int, bcap: int = 0):
         """_host_outputs from one of the engine's reusable buffers that no earlier result still
         holds (every returned array is a view of its buffer, so a live batch keeps the buffer's
         reference count up): the pages stay mapped -- not faulted in on every call -- and
         registered for the device (clg_host_register), so the single-launch small decode writes
-        the outputs straight into them (CLG_MEM_MAPPED).  For the same capacities the views and
-        clg_decoded of the slot's last call serve again."""
-        key, need = (cap, wcap), self._out_bytes(cap, wcap)[1]
+        the outputs straight into them (CLG_MEM_MAPPED).  The views are carved at the slot's
+        whole capacity (_slot_capacity) and serve again for every request they cover.
+        Returns (clg_decoded, arrays, byref(clg_decoded))."""
+        with self._pool_mu:
+            return self._pooled_pick(cap, wcap, bcap)
+
+    def _pooled_pick(self, cap: int, wcap: int, bcap: int):
+        need = self._out_bytes(cap, wcap, bcap)[1]
         pick = None
         for sl in self._out_slots:
-            # references when free: the slot, getrefcount's argument, and the cached views
-            free = sys.getrefcount(sl["buf"]) <= 2 + (len(self._OUT_FIELDS) if sl["cache"] is not None else 0)
-            if free and sl["buf"].size >= need:
+            c = sl["cache"]
+            if c is not None and c[0][0] >= cap and c[0][1] >= wcap and c[0][2] >= bcap and self._slot_free(sl):
+                return self._slot_use(sl)
+            if pick is None and sl["buf"].size >= need and self._slot_free(sl):
                 pick = sl
-                break
         if pick is None:
-            if len(self._out_slots) >= self._OUT_SLOTS:  # all held (or too small): the oldest leaves the pool
-                self._slot_release(self._out_slots.pop(0))
+            idle = [i for i, sl in enumerate(self._out_slots) if not sl["busy"]]
+            if len(self._out_slots) >= self._OUT_SLOTS and idle:  # all held (or too small): the oldest
+                self._slot_release(self._out_slots.pop(idle[0]))  # not being decoded into leaves the pool
             size = (max(need, 1 << 16) + 4095) & ~4095  # page-aligned: an anonymous mapping
             buf = np.frombuffer(mmap.mmap(-1, size), np.uint8)
             mapped = self._h is not None and lib.clg_host_register(_np_ptr(buf), size) == _lib.CLG_OK
-            pick = {"buf": buf, "mapped": mapped, "cache": None}
+            pick = {"buf": buf, "mapped": mapped, "cache": None, "busy": False}
             self._out_slots.append(pick)
-        else:  # the most recent last (by identity: the slots hold arrays)
-            self._out_slots = [sl for sl in self._out_slots if sl is not pick] + [pick]
-        if pick["cache"] is not None and pick["cache"][0] == key:
-            d, arrs = pick["cache"][1], pick["cache"][2]
-            d.n_rec = d.n_wide = 0
-            return d, arrs
         pick["cache"] = None  # (its views would hold the buffer)
-        d, arrs = self._host_outputs(cap, wcap, pick["buf"])
+        key = self._slot_capacity(pick["buf"].size, cap, wcap, bcap)
+        d, arrs = self._host_outputs(*key[:2], pick["buf"], key[2])
         if pick["mapped"]:
             d.out_kind = _lib.CLG_MEM_MAPPED
-        pick["cache"] = (key, d, arrs)
-        return d, arrs
+        pick["cache"] = (key, d, arrs, C.byref(d))
+        pick["bptr"] = arrs["base"].ctypes.data if "base" in arrs else 0
+        return self._slot_use(pick)
 
     def _slot_release(self, sl):
         """A pooled buffer leaves the pool: unregistered (a batch the caller keeps stays valid as
@@ -388,15 +432,19 @@ class Engine:
         return bool(self._out_slots) and self._out_slots[-1]["mapped"]
 
     def _finish(self, st, d, arrs, base, n_spans, spans_bytes):
-        if st != _lib.CLG_OK:
-            err = _lib.ClonosError(st, lib.clg_last_error().decode(errors="replace"))
-            err.err_span, err.err_off, err.err_tag = d.err_span, d.err_off, d.err_tag
-            err.n_rec = d.n_rec
-            raise err
-        nr, nw = d.n_rec, d.n_wide
-        return DecodedBatch(arrs["off"][:nr], arrs["tag"][:nr], arrs["v0"][:nr], arrs["w_idx"][:nw],
-                            arrs["w_rc"][:nw], arrs["w_v1"][:nw], arrs["w_var_off"][:nw], arrs["w_var_len"][:nw],
-                            arrs["w_sub"][:nw], base[:n_spans + 1], spans_bytes)
+        """The batch as slices of the slot's views (they hold its buffer); the slot's pick ends."""
+        try:
+            if st != _lib.CLG_OK:
+                err = _lib.ClonosError(st, lib.clg_last_error().decode(errors="replace"))
+                err.err_span, err.err_off, err.err_tag = d.err_span, d.err_off, d.err_tag
+                err.n_rec = d.n_rec
+                raise err
+            nr, nw = d.n_rec, d.n_wide
+            return DecodedBatch(arrs["off"][:nr], arrs["tag"][:nr], arrs["v0"][:nr], arrs["w_idx"][:nw],
+                                arrs["w_rc"][:nw], arrs["w_v1"][:nw], arrs["w_var_off"][:nw],
+                                arrs["w_var_len"][:nw], arrs["w_sub"][:nw], base[:n_spans + 1], spans_bytes)
+        finally:
+            self._slot_done(arrs)
 
     def decode_host(self, data: Union[bytes, np.ndarray], spans: Optional[Sequence[Tuple[int, int]]] = None
                     ) -> DecodedBatch:
@@ -409,35 +457,74 @@ class Engine:
         sl = np.array([s[1] for s in spans], np.uint64)
         cap = int(sl.sum()) // 2 + len(spans) + 1
         wcap = int(sl.sum()) // 6 + len(spans) + 1
-        d, arrs = self._pooled_outputs(cap, wcap)
+        d, arrs, ref = self._pooled_outputs(cap, wcap)
         base = np.zeros(len(spans) + 1, np.uint64)
-        st = lib.clg_decode_host(self._h, _np_ptr(buf), _np_ptr(so), _np_ptr(sl), len(spans), C.byref(d),
-                                 _np_ptr(base))
+        st = lib.clg_decode_host(self._h, _np_ptr(buf), _np_ptr(so), _np_ptr(sl), len(spans), ref, _np_ptr(base))
         return self._finish(st, d, arrs, base, len(spans),
                             [buf[int(o):int(o) + int(n)] for o, n in zip(so, sl)])
 
     def decode_logs(self, logs: Sequence["ThreadCausalLog"], start_epochs: Sequence[int],
                     keep_bytes: bool = False) -> DecodedBatch:
-        h = np.array([l.handle for l in logs], np.uint32)
-        ep = np.array(start_epochs, np.int64)
-        total = self.log_lengths(h)[1]  # logLength bounds every span (one native call for the batch)
-        cap = total // 2 + len(logs) + 1
-        wcap = total // 6 + len(logs) + 1
-        d, arrs = self._pooled_outputs(cap, wcap)
-        base = np.zeros(len(logs) + 1, np.uint64)
-        st = lib.clg_decode_logs(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base))
+        n = len(logs)
+        own = self._in_mu.acquire(blocking=False)  # the reused handle / epoch arrays, else new ones
+        try:
+            sc = self._in_scratch(n) if own else self._in_arrays(n)
+            h, ep = sc[0][:n], sc[1][:n]
+            h[:] = [l.handle for l in logs]
+            ep[:] = start_epochs
+            # a free registered slot whose capacity covers the batch decodes without logLength;
+            # a batch beyond it fails with CLG_E_CAPACITY (nothing changed) and is sized below
+            fast = self._pooled_fast(n)
+            st = _lib.CLG_E_CAPACITY
+            if fast is not None:
+                d, arrs, ref, bptr = fast
+                st = lib.clg_decode_logs(self._h, sc[2], sc[3], n, ref, bptr)
+                if st == _lib.CLG_E_CAPACITY:
+                    self._slot_done(arrs)
+            if st == _lib.CLG_E_CAPACITY:
+                total = self.log_lengths(h)[1]  # logLength bounds every span (one native call for the batch)
+                d, arrs, ref = self._pooled_outputs(total // 2 + n + 1, total // 6 + n + 1, n + 1)
+                st = lib.clg_decode_logs(self._h, sc[2], sc[3], n, ref, arrs["base"].ctypes.data)
+        finally:
+            if own:
+                self._in_mu.release()
         sb = [np.frombuffer(l.getDeterminants(e), np.uint8) for l, e in zip(logs, start_epochs)] if keep_bytes else None
-        return self._finish(st, d, arrs, base, len(logs), sb)
+        return self._finish(st, d, arrs, arrs["base"], n, sb)
+
+    def _in_scratch(self, n: int):
+        """Reused handle / epoch arrays of decode_logs, with their addresses."""
+        sc = self._in_sc
+        if sc is None or sc[0].size < n:
+            sc = self._in_sc = self._in_arrays(max(64, 1 << max(n - 1, 0).bit_length()))
+        return sc
+
+    @staticmethod
+    def _in_arrays(n: int):
+        h, ep = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.int64)
+        return h, ep, h.ctypes.data, ep.ctypes.data
+
+    def _pooled_fast(self, n_spans: int):
+        """A free registered slot with a span_rec_base of n_spans + 1 entries (its views carved at
+        its whole capacity), or None."""
+        with self._pool_mu:
+            for sl in self._out_slots:
+                c = sl["cache"]
+                if c is not None and sl["mapped"] and c[0][2] > n_spans and self._slot_free(sl):
+                    return self._slot_use(sl) + (sl["bptr"],)
+        return None
 
     def decode_logs_async(self, logs: Sequence["ThreadCausalLog"], start_epochs: Sequence[int]) -> "PendingDecode":
         """clg_decode_logs_async into host arrays: returns at once; .wait() gives the batch."""
         h = np.array([l.handle for l in logs], np.uint32)
         ep = np.array(start_epochs, np.int64)
         total = self.log_lengths(h)[1]
-        d, arrs = self._pooled_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
+        d, arrs, ref = self._pooled_outputs(total // 2 + len(logs) + 1, total // 6 + len(logs) + 1)
         base = np.zeros(len(logs) + 1, np.uint64)
         pd = PendingDecode(self, (h, ep, d, arrs, base), len(logs))
-        check(lib.clg_decode_logs_async(self._h, _np_ptr(h), _np_ptr(ep), len(logs), C.byref(d), _np_ptr(base)))
+        st = lib.clg_decode_logs_async(self._h, _np_ptr(h), _np_ptr(ep), len(logs), ref, _np_ptr(base))
+        if st != _lib.CLG_OK:
+            self._slot_done(arrs)
+            check(st)
         return pd
 
     def decode_logs_device(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
@@ -537,7 +624,7 @@ class Engine:
         winner = np.zeros(max(len(blobs), 1), np.uint32)
         nk = C.c_uint32()
         total = int(lens.sum())
-        d, arrs = self._pooled_outputs(total // 2 + len(blobs) + 1, total // 6 + len(blobs) + 1)
+        d, arrs, _ = self._pooled_outputs(total // 2 + len(blobs) + 1, total // 6 + len(blobs) + 1)
         base = np.zeros(len(blobs) + 1, np.uint64)
         st = lib.clg_replay_prep(self._h, _np_ptr(keys), _np_ptr(data), _np_ptr(offs), _np_ptr(lens), len(blobs),
                                  _np_ptr(winner), C.byref(nk), C.byref(d), _np_ptr(base))

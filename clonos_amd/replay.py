@@ -251,7 +251,7 @@ def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResp
         main_bytes += int(e["len"][e["id"]["is_main"] != 0].sum())
         sub_bytes += int(e["len"][e["id"]["is_main"] == 0].sum())  # a bound: the table may name fewer
     cap = main_bytes // 2 + n + 1
-    d, arrs = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
+    d, arrs, _ = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
     base = np.zeros(n + 1, np.uint64)
     sizes = np.empty(max(1, sub_bytes // 5), np.int32)
     sbase = np.zeros(n_sub + 1, np.uint64)
@@ -286,7 +286,7 @@ def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponse
                          for s in subs)
     n_sub = sum(len(j[2]) for j in jobs)
     cap = main_bytes // 2 + n + 1
-    d, arrs = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
+    d, arrs, _ = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
     base = np.zeros(n + 1, np.uint64)
     sizes = np.empty(max(1, sub_bytes // 5), np.int32)
     sbase = np.zeros(n_sub + 1, np.uint64)

@@ -178,3 +178,26 @@ def test_small_mapped_outputs_kept_batches_stay_intact():
         assert eng._out_buf.ctypes.data in (buf1, buf2) and len(eng._out_slots) == 2  # free again: reused
         for s, l in enumerate(lids):
             assert_span_equal(third, s, data[l])
+
+
+def test_pooled_capacity_exceeded_is_decoded_again_sized():
+    """decode_logs first tries the free registered slot at its whole capacity, without
+    logLength; a batch with more records than the slot holds fails there with CLG_E_CAPACITY
+    (nothing changed) and is decoded again into a slot sized from logLength."""
+    rng = np.random.default_rng(synth.SEED_CONFIG1)
+    graph, data = synth.config1_job(rng)
+    with _eng(sharing_depth=1) as eng:
+        logs = {lid: eng.open_log(lid) for lid in data}
+        for lid, b in data.items():
+            logs[lid].appendDeterminant(b, 0)
+        lids = list(data)
+        first = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        cap = eng._out_cache[0][0]
+        del first
+        big = bytes(synth.config2_log(cap + 5000, rng)[0])  # more records than the slot holds
+        logs[lids[0]].appendDeterminant(big, 0)
+        dec = eng.decode_logs([logs[l] for l in lids], [0] * len(lids))
+        assert eng._out_cache[0][0] > cap and dec.n_rec > cap
+        assert_span_equal(dec, 0, data[lids[0]] + big)
+        for s, l in enumerate(lids[1:], 1):
+            assert_span_equal(dec, s, data[l])
