@@ -836,6 +836,7 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
             ks = e_.kernel_stats()
             paths = sorted(k for k in ks if k in ("decode_fallback", "decode_span_fallback"))
             kms = {k: round(v["ms"] / v["launches"], 4) for k, v in ks.items() if v["launches"] and v["ms"] > 0}
+            kms["dp_spans"] = ks.get("robust_dp_spans", {}).get("launches", 0) // steps  # (robust: spans the DP took)
             return ms, paths, kms
         finally:
             e_.close()

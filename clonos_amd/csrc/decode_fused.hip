@@ -275,19 +275,44 @@ struct JL {
   // count pass (load_jl_map): no bitmap or ranks, the entries' positions (sorted) instead
   const uint32_t* pos = nullptr;
   uint32_t n = 0;
+  // a tile with more than kZJCap entries: the rest stay in HBM (the overflow arena), sorted
+  // after the first kZJCap: on of them at opos / olen
+  const uint32_t* opos = nullptr;
+  const uint32_t* olen = nullptr;
+  uint32_t on = 0;
 };
-__device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
-  if (!j.bits) {  // sorted positions: binary search (the count pass's rare slow path)
-    uint32_t lo = 0, hi = j.n;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (j.pos[mid] < a) lo = mid + 1; else hi = mid;
-    }
-    return lo < j.n && j.pos[lo] == a ? j.len[lo] : 0u;
+// (The LDS table and the overflow entries are read by separate loads under a branch: a
+// select between the two pointers compiles to a flat load.)
+template <class P_>
+__device__ __forceinline__ uint32_t jl_search(P_ P, uint32_t n, uint32_t a) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P[mid] < a) lo = mid + 1; else hi = mid;
   }
+  return lo;
+}
+// Bitmap + ranks (load_jl).  j.on is wave-uniform (a scalar branch): a tile without overflow
+// entries skips the HBM read, which -- predicated per lane, or waited for where the caller
+// next wrote the register -- made every tile wait for its output stores at each wide record
+// (config-3 emit 0.336 -> 0.386 ms).
+__device__ __forceinline__ uint32_t jl_len_bits(const JL& j, uint32_t a) {
   const uint32_t w = j.bits[a >> 5], b = a & 31u;
   if (!((w >> b) & 1u)) return 0u;
-  return j.len[j.rank[a >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))];
+  const uint32_t r = j.rank[a >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u));
+  if (j.on && r >= kZJCap) {
+    const uint32_t L = gp(j.olen)[r - kZJCap];
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), inside the branch
+    return L;
+  }
+  return ((const __attribute__((address_space(3))) uint32_t*)j.len)[r];
+}
+__device__ __forceinline__ uint32_t jl_len(const JL& j, uint32_t a) {
+  if (!j.bits) {  // sorted positions: binary search (the count pass's rare slow path)
+    const uint32_t k = jl_search(j.pos, j.n, a);
+    return k < j.n && j.pos[k] == a ? j.len[k] : 0u;
+  }
+  return jl_len_bits(j, a);
 }
 
 struct Res {
@@ -1455,28 +1480,60 @@ __device__ __forceinline__ JLPre jl_prefetch(const FusedCtl& ctl, uint32_t t, ui
   const uint64_t b = (uint64_t)t * kZJCap + lane;  // inside the table even past its entries
   return JLPre{gp(ctl.jn)[t], gp(ctl.jpos)[b], gp(ctl.jlen)[b]};
 }
+// Entry i of tile t's table: its slot in jpos / jlen (past kZJCap: the overflow arena).
+__device__ __forceinline__ uint64_t jslot(const FusedCtl& ctl, uint32_t t, uint32_t i) {
+  return i < kZJCap ? (uint64_t)t * kZJCap + i
+                    : (uint64_t)ctl.n_tiles * kZJCap + gp(ctl.jbase)[t] + (i - kZJCap);
+}
+// The overflow entries of tile t (n entries in all) into j.
+__device__ __forceinline__ void jl_overflow(const FusedCtl& ctl, uint32_t t, uint32_t n, JL& j) {
+  n = __builtin_amdgcn_readfirstlane(n);  // (the same in every lane: the scalar unit branches on it)
+  if (n <= kZJCap) return;
+  const uint64_t s = jslot(ctl, t, kZJCap);
+  j.opos = ctl.jpos + s;
+  j.olen = ctl.jlen + s;
+  j.on = n - kZJCap;
+}
+// The count pass walks the map, and looks a Serializable record up only where its code is 0
+// (an invalid stream) or 0x80 (longer than kZLmMax): so the LDS list holds just the entries
+// longer than kZLmMax -- at most a tile / kZLmMax of them, whatever the tile's entry count --
+// in position order (a ballot per 64), and a position not in it reads as invalid.  More than
+// kZJCap such entries (overlapping false candidates): abort reason 6, the batch goes robust.
 __device__ __forceinline__ JL load_jl_map(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane, uint32_t* lm,
                                          const JLPre& pre) {
   uint32_t* pos = s_j;
   uint32_t* len = s_j + kZJCap;
-  const uint32_t n = min(pre.n, kZJCap);
   __syncthreads();  // every row of the map is written (build_lm) before codes go over them
-  for (uint32_t i = lane; i < n; i += 64) {
-    const bool p0 = i == lane;
-    const uint32_t a = p0 ? pre.a : gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
-    const uint32_t L = p0 ? pre.L : gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
-    pos[i] = a;
-    len[i] = L;
-    lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
+  uint32_t kept = 0;
+  for (uint32_t i0 = 0; i0 < pre.n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    uint32_t a = 0, L = 0;
+    if (i < pre.n) {
+      const bool p0 = i0 == 0;
+      const uint64_t sl = p0 ? 0 : jslot(ctl, t, i);
+      a = p0 ? pre.a : gp(ctl.jpos)[sl];
+      L = p0 ? pre.L : gp(ctl.jlen)[sl];
+      lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
+    }
+    const bool keep = i < pre.n && L <= 0x7FFFFFFFu && L > kZLmMax;
+    const uint64_t m = __ballot(keep);
+    const uint32_t at = kept + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (keep && at < kZJCap) {
+      pos[at] = a;
+      len[at] = L;
+    }
+    kept += (uint32_t)__popcll(m);
   }
+  if (kept > kZJCap && lane == 0) raise_abort(ctl, 6, t);
   __syncthreads();  // the map's rows (written before the call) and the codes above
   JL j{nullptr, nullptr, len, lm};
   j.pos = pos;
-  j.n = n;
+  j.n = min(kept, kZJCap);
   return j;
 }
 
-// Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths.
+// Stage tile t's Serializable table into LDS (J passes): bitmap, per-dword ranks, lengths
+// (the first kZJCap; the bitmap and ranks cover every entry).
 // lm: the count pass's step-code map (built, barrier passed): Serializable codes go into it.
 __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t* s_j, uint32_t lane,
                                      uint32_t* lm = nullptr, const JLPre* pre = nullptr) {
@@ -1485,12 +1542,13 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
   uint32_t* len = s_j + 2 * kZJBitsDw;
   for (uint32_t i = lane; i < kZJBitsDw; i += 64) bits[i] = 0;
   __syncthreads();
-  const uint32_t n = min(pre ? pre->n : gp(ctl.jn)[t], kZJCap);
+  const uint32_t n = pre ? pre->n : gp(ctl.jn)[t];
   for (uint32_t i = lane; i < n; i += 64) {
     const bool p0 = pre && i == lane;
-    const uint32_t a = p0 ? pre->a : gp(ctl.jpos)[(uint64_t)t * kZJCap + i];
-    const uint32_t L = p0 ? pre->L : gp(ctl.jlen)[(uint64_t)t * kZJCap + i];
-    len[i] = L;
+    const uint64_t sl = p0 ? 0 : jslot(ctl, t, i);
+    const uint32_t a = p0 ? pre->a : gp(ctl.jpos)[sl];
+    const uint32_t L = p0 ? pre->L : gp(ctl.jlen)[sl];
+    if (i < kZJCap) len[i] = L;
     atomicOr(&bits[a >> 5], 1u << (a & 31u));
     if (lm) lm8_set(lm, a, lm_code(L <= 0x7FFFFFFFu ? (int)L : 0, true));
   }
@@ -1517,7 +1575,9 @@ __device__ __forceinline__ JL load_jl(const FusedCtl& ctl, uint32_t t, uint32_t*
     run += c[k];
   }
   __syncthreads();
-  return JL{bits, rank, len, lm};
+  JL j{bits, rank, len, lm};
+  jl_overflow(ctl, t, n, j);
+  return j;
 }
 
 // Emit's LDS: the image, record starts of the window by output position and the
@@ -1708,7 +1768,7 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
         const bool ser = tg == CLG_TAG_SERIALIZABLE, tt = tg == CLG_TAG_TIMER_TRIGGER, sc = tg == CLG_TAG_SOURCE_CHECKPOINT;
         const uint32_t b13 = (x[3] >> 8) & 0xFFu, b21 = (x[5] >> 8) & 0xFFu, b22 = (x[5] >> 16) & 0xFFu;
         const bool tt_name = tt && b13 == 6u, sc_ref = sc && b22 != 0u;
-        const uint32_t jlen = J && ser ? jl_len(jl, a) : 0u;  // (without tables no Serializable record gets here)
+        const uint32_t jlen = J && ser ? jl_len_bits(jl, a) : 0u;  // (without tables no Serializable record gets here)
         const uint32_t L = ser ? jlen : tt_name ? 18u + be32(14) : tt ? 14u : sc_ref ? 27u + be32(23) : sc ? 23u : 13u;
         const uint32_t var_off = ser ? 1u : tt_name ? 18u : sc_ref ? 27u : 0u;
         const int64_t v0 = ser ? (int64_t)L - 1 : (int64_t)((uint64_t)be32(5) << 32 | be32(9));
@@ -2490,20 +2550,51 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
     if ((int)lane >= off) ex += y;
   }
   const uint32_t total = __shfl(ex, 63);
+  // past kZJCap candidates the rest go to the overflow arena (a tile of short Serializable
+  // strings holds up to ~300); arena exhausted: abort reason 6, the host grows it and retries
+  uint32_t ob = 0;
   if (lane == 0) {
-    gp(ctl.jn)[t] = total;
+    uint32_t n = total;
     if (total && !*flagged) __hip_atomic_store(ctl.abort + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (total > kZJCap) raise_abort(ctl, 6, t);
+    if (total > kZJCap) {
+      ob = atomicAdd(ctl.jwork + 1, total - kZJCap);
+      if (ob + (total - kZJCap) > ctl.jovf_cap) {
+        raise_abort(ctl, 6, t);
+        n = kZJCap;  // (the batch runs again: no pass reads past the arena meanwhile)
+      } else {
+        gp(ctl.jbase)[t] = ob;
+      }
+    }
+    gp(ctl.jn)[t] = n;
   }
+  ob = __shfl(ob, 0);
+  const bool ovf_ok = total <= kZJCap || ob + (total - kZJCap) <= ctl.jovf_cap;
   *flagged = *flagged || total;  // one flag store per block
-  const uint32_t t1 = z.sd.first_tile + z.sd.n_tiles;
   uint32_t idx = ex - nm;
-  (void)t1;
-  // the tile's candidates in order into LDS, then their lengths 64 at a time (a lane holds
-  // ~1 candidate on average: computed in place, the inline parser ran once per register
-  // slot with few lanes active)
+  // A candidate's stream length (inline shapes; else the general walker's work list) into
+  // table slot sl.
+  auto measure = [&](uint32_t a, uint64_t sl) {
+    const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
+    bool general;
+    const uint64_t L = jser_inline_len(s_img, a, img_end, avail, &general);
+    gp(ctl.jpos)[sl] = a;
+    gp(ctl.jlen)[sl] = general ? kZJGeneral : (L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u);
+    if (general) {  // nested objects, arrays, ...: k_decode_jser_general walks the grammar
+      const uint32_t w = atomicAdd(ctl.jwork, 1u);
+      if (w < ctl.jwork_cap) {
+        ctl.jwork[2 + w] = (uint32_t)sl;
+        ctl.jwork[2 + ctl.jwork_cap + w] = t;
+      } else {
+        raise_abort(ctl, 6, t);
+      }
+    }
+  };
+  // the tile's first kZJCap candidates in order into LDS, then their lengths 64 at a time (a
+  // lane holds ~1 candidate on average: computed in place, the inline parser ran once per
+  // register slot with few lanes active); any past them measured in place, into the arena
   auto put = [&](uint32_t a) {
     if (idx < kZJCap) s_cand[idx] = a;
+    else if (ovf_ok) measure(a, (uint64_t)ctl.n_tiles * kZJCap + ob + (idx - kZJCap));
     ++idx;
   };
   if (!nm) {
@@ -2523,19 +2614,7 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   }
   __syncthreads();
   const uint32_t nc = total < kZJCap ? total : kZJCap;
-  for (uint32_t k = lane; k < nc; k += 64) {
-    const uint32_t a = s_cand[k];
-    const uint64_t avail = (uint64_t)(z.end_a - a);  // record start to span end
-    bool general;
-    const uint64_t L = jser_inline_len(s_img, a, img_end, avail, &general);
-    gp(ctl.jpos)[(uint64_t)t * kZJCap + k] = a;
-    gp(ctl.jlen)[(uint64_t)t * kZJCap + k] = general ? kZJGeneral : (L <= 0x7FFFFFF0ull ? (uint32_t)L : 0u);
-    if (general) {  // nested objects, arrays, ...: k_decode_jser_general walks the grammar
-      const uint32_t w = atomicAdd(ctl.jwork, 1u);
-      if (w < ctl.jwork_cap) ctl.jwork[1 + w] = t * kZJCap + k;
-      else raise_abort(ctl, 6, t);
-    }
-  }
+  for (uint32_t k = lane; k < nc; k += 64) measure(s_cand[k], (uint64_t)t * kZJCap + k);
   if (ctl.prof && lane == 0) {  // developer diagnostics: stage / scan+lengths cycles
     ctl.prof[(uint64_t)t * 8 + 6] = c1 - c0;
     ctl.prof[(uint64_t)t * 8 + 7] = (c2 - c1) | (__builtin_amdgcn_s_memtime() - c2) << 32;
@@ -2561,7 +2640,7 @@ __global__ __launch_bounds__(64) void k_decode_jser_general(const TileDesc* __re
                                                             const SpanDesc* __restrict__ spans, FusedCtl ctl) {
   const uint32_t n = min(ld_agent32(ctl.jwork), ctl.jwork_cap);
   for (uint32_t i = blockIdx.x * 64 + threadIdx.x; i < n; i += gridDim.x * 64) {
-    const uint32_t item = ctl.jwork[1 + i], t = item / kZJCap;
+    const uint32_t item = ctl.jwork[2 + i], t = ctl.jwork[2 + ctl.jwork_cap + i];
     const TileDesc td = tiles[t];
     const SpanDesc sd = spans[td.span];
     const uint32_t a = ctl.jpos[item];

@@ -545,6 +545,8 @@ struct clg_engine {
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
   DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
+  uint32_t zjovf_cap = 1u << 16;  // their overflow arena's entries (grown on demand)
+  uint32_t zjwork_min = 0;        // the general walker's work list: at least this many items
   DevBuf d_zbad;                     // fast decode: per-span "chain went wrong" flags
   DevBuf d_sf_meta, d_sf_rec, d_sf_wide;  // per-span fallback: bad-span list, robust outputs
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
@@ -1525,29 +1527,65 @@ struct clg_engine {
   // (tiles of one span are taken as equally long; a small whole span that pass 0 counted, a
   // skip), and block b takes the tiles whose cumulative cost passes b / G of the total.
   // ch[0 .. G]: boundaries, ch[G] = n_tiles.
-  static void count_chunks(const DecodePlan& p, uint32_t G, bool tiny, std::vector<uint32_t>& ch) {
+  // Batches of many spans: the cost sums per part of the spans on the host threads, then
+  // each part places the boundaries that fall in it (the same boundaries as one pass).
+  void count_chunks(const DecodePlan& p, uint32_t G, bool tiny, std::vector<uint32_t>& ch) {
     ch.assign(size_t(G) + 1, p.n_tiles);
     ch[0] = 0;
     constexpr double kTileCost = 1024.0, kTinyCost = 64.0;  // (pass 0 counted the small whole spans)
     auto cost = [&](const clg::SpanDesc& s) {
       return tiny && s.n_tiles == 1 && s.len <= clg::kZTinySpan ? kTinyCost : double(s.len) / s.n_tiles + kTileCost;
     };
-    double total = 0;
-    for (const auto& s : p.spans)
-      if (s.n_tiles) total += cost(s) * s.n_tiles;
-    const double target = total / G;
-    double acc = 0, next = target;
-    uint32_t b = 1;
-    for (const auto& s : p.spans) {
-      if (!s.n_tiles) continue;
-      const double c = cost(s), end = acc + c * s.n_tiles;
-      while (b < G && next <= end) {  // boundary inside this span: the first tile past it
-        const double k = (next - acc) / c;
-        ch[b++] = s.first_tile + std::min<uint32_t>(s.n_tiles, uint32_t(k) + (k > double(uint32_t(k)) ? 1u : 0u));
-        next = target * b;
+    const size_t ns = p.spans.size();
+    const unsigned P = ns >= kParallelLogs ? workers()->size() : 1u;
+    std::vector<double> part(P + 1, 0.0);
+    auto range = [&](unsigned k, size_t* a, size_t* b) {
+      *a = ns * k / P;
+      *b = ns * (k + 1) / P;
+    };
+    auto sums = [&](unsigned k, unsigned) {
+      size_t a, b;
+      range(k, &a, &b);
+      double t = 0;
+      for (size_t i = a; i < b; ++i)
+        if (p.spans[i].n_tiles) t += cost(p.spans[i]) * p.spans[i].n_tiles;
+      part[k + 1] = t;
+    };
+    if (P > 1) workers()->run(sums); else sums(0, 1);
+    for (unsigned k = 0; k < P; ++k) part[k + 1] += part[k];
+    if (!(part[P] > 0)) return;  // (no tiles)
+    const double target = part[P] / G;
+    // part k places boundaries [bstart(k), bstart(k + 1)): those past the cost before it
+    auto bstart = [&](unsigned k) -> uint32_t {
+      if (k == 0) return 1u;
+      if (k >= P) return G;
+      uint32_t b = uint32_t(std::min<double>(double(G), std::max(1.0, std::floor(part[k] / target))));
+      while (b > 1 && target * (b - 1) > part[k]) --b;
+      while (b < G && target * b <= part[k]) ++b;
+      return b;
+    };
+    auto place = [&](unsigned k, unsigned) {
+      size_t a, e;
+      range(k, &a, &e);
+      double acc = part[k];
+      uint32_t b = bstart(k);
+      const uint32_t bend = bstart(k + 1);
+      double next = target * b;
+      for (size_t i = a; i < e && b < bend; ++i) {
+        const auto& s = p.spans[i];
+        if (!s.n_tiles) continue;
+        const double c = cost(s), end = acc + c * s.n_tiles;
+        while (b < bend && next <= end) {  // boundary inside this span: the first tile past it
+          const double kk = (next - acc) / c;
+          ch[b++] = s.first_tile + std::min<uint32_t>(s.n_tiles, uint32_t(kk) + (kk > double(uint32_t(kk)) ? 1u : 0u));
+          next = target * b;
+        }
+        acc = end;
       }
-      acc = end;
-    }
+      const uint32_t past = e < ns ? p.spans[e].first_tile : p.n_tiles;  // (rounding: the part's end)
+      while (b < bend) ch[b++] = past;
+    };
+    if (P > 1) workers()->run(place); else place(0, 1);
   }
   std::vector<uint32_t> chunk_buf;
   // Device half: upload, span table, tiles (expanded on the device from the runs).
@@ -1727,20 +1765,23 @@ struct clg_engine {
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     if (zdbg) CHK(d_dbg.ensure(16 * 4 + 64 * 32));
     if (prof_path) CHK(d_prof.ensure(size_t(nt) * 64));
+    const uint32_t jwork_cap = std::max<uint32_t>(uint32_t(nt) * 16 + 1024, zjwork_min);
     if (jser) {
-      CHK(d_zjpos.ensure(size_t(nt) * clg::kZJCap * 4));
-      CHK(d_zjlen.ensure(size_t(nt) * clg::kZJCap * 4));
-      CHK(d_zjn.ensure(size_t(nt) * 4));
-      CHK(d_zjwork.ensure((size_t(nt) * 16 + 1025) * 4));
+      CHK(d_zjpos.ensure((size_t(nt) * clg::kZJCap + zjovf_cap) * 4));
+      CHK(d_zjlen.ensure((size_t(nt) * clg::kZJCap + zjovf_cap) * 4));
+      CHK(d_zjn.ensure(size_t(nt) * 8));  // jn, jbase
+      CHK(d_zjwork.ensure((2 * size_t(jwork_cap) + 2) * 4));
     }
     clg::FusedCtl ctl{w, w + o_cnt, w + o_cnt + nt, w + o_cnt + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
                       getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
-                      jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, uint32_t(nt) * 16 + 1024,
+                      jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, jwork_cap,
                       jser ? d_zjwork.as<uint32_t>() : nullptr, spec_warm(jser), clg::JArena{}};
     if (jser) CHK(jarena_reset(&ctl.jar));
+    ctl.jbase = jser ? d_zjn.as<uint32_t>() + nt : nullptr;
+    ctl.jovf_cap = zjovf_cap;
     ctl.span_bad = d_zbad.as<uint32_t>();
     ctl.skip_bad = 0;
     ctl.span_err = keep_errors ? d_zerr.as<uint64_t>() : nullptr;
@@ -1763,7 +1804,7 @@ struct clg_engine {
       CHK(enqueue_plan(p, L, d_ztiles));
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
-      if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 4, stream));
+      if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 8, stream));  // work items, overflow entries
       HIPCHK(hipMemsetAsync(w, 0, o_cnt * 8, stream));  // st_x, ex, rep_flag
       HIPCHK(hipMemsetAsync(ab, 0, 40, stream));                // abort words, repair counters
       HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
@@ -1831,6 +1872,16 @@ struct clg_engine {
     if (hab[9]) stats["decode_chunk_repair"].launches += hab[9];  // repair requests the count pass served
     const bool spilled = jser && jarena_spilled(0);  // a stream walk found the spill arena full
     if (spilled) CHK(jarena_grow());
+    // Serializable tables: the overflow arena or the walker's work list was full (reason 6)
+    bool grown = false;
+    if (jser && hab[6]) {
+      uint32_t used[2];
+      HIPCHK(hipMemcpy(used, d_zjwork.p, 8, hipMemcpyDeviceToHost));
+      if (used[0] > r.ctl.jwork_cap) zjwork_min = std::max(zjwork_min, 2 * used[0]);
+      if (used[1] > zjovf_cap) zjovf_cap = std::max<uint32_t>(2 * used[1], 2 * zjovf_cap);
+      grown = used[0] > r.ctl.jwork_cap || used[1] > r.ctl.jovf_cap;
+      stats["decode_jser_grow"].launches++;
+    }
     if (hab[0] || spilled) {
       if (ea) {
         ev_pool.push_back(ea);
@@ -1843,7 +1894,8 @@ struct clg_engine {
       *aborted = true;
       // Serializable records were met without tables: other aborts may be consequences
       // (entries guessed across them), so the tables decide; a second abort goes robust
-      *need_jser = !jser && hab[5] && !spilled;
+      // (a table arena that was full, now grown: the same, once)
+      *need_jser = (!jser && hab[5] && !spilled) || (jser && (spilled || grown));
       r.span_local = !*need_jser && !spilled && !hab[4] && !hab[6];
       zlast = r;
       if (getenv("CLONOS_FUSED_DEBUG"))
@@ -2298,10 +2350,12 @@ struct clg_engine {
   int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                   bool need_jser) {
     bool aborted = true, nj = false;
-    if (need_jser) {
+    // with the tables; again (at most twice) while a table arena was full and has grown
+    for (int tries = 0; need_jser && tries < 3; ++tries) {
       stats["decode_jser_retry"].launches++;
       CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, true, &nj));
       if (!aborted) return CLG_OK;
+      need_jser = nj;
     }
     if (zlast.span_local && !nj) {
       bool done = false;
@@ -2439,6 +2493,15 @@ struct clg_engine {
                                       d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags,
                                       stream);
     }));
+    if (cfg.flags & CLG_F_TIMING) {  // diagnostics: spans the convergence-point tier leaves to the DP
+      std::vector<uint32_t> hf(ns);
+      HIPCHK(hipMemcpyAsync(hf.data(), flags, size_t(ns) * 4, hipMemcpyDeviceToHost, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      uint64_t nf = 0;
+      for (uint32_t f : hf) nf += f != 0;
+      stats["robust_dp_spans"].launches += nf;
+      stats["robust_spans"].launches += ns;
+    }
     // robust DP pipeline for flagged spans only (early exit elsewhere)
     CHK(timed("robust_dp_tables", 0, [&] {
       return clg::launch_decode_tables(dt, nt, ds, d_agg.as<uint64_t>(), d_conv.as<clg::TileConv>(), flags, jar, stream);

@@ -196,7 +196,8 @@ struct FusedCtl {
   uint32_t* jn;
   uint32_t jser;
   uint32_t jwork_cap;  // capacity of the general-walker work list
-  uint32_t* jwork;     // [0]: items, then (t * kZJCap + i) per candidate needing the walker
+  uint32_t* jwork;     // [0]: items, [1]: overflow entries taken, then [2, 2 + cap): the items'
+                       // table slots, [2 + cap, 2 + 2 cap): their tiles
   uint32_t warm;    // speculative warm-up bytes before each region (| 1 << 31: not staggered by lane)
   JArena jar;       // the stream walker's spill arena (k_decode_jser_general)
   // Per-span fallback: a tile whose chain goes wrong (reasons 1-3, 5) sets span_bad[span]
@@ -221,12 +222,18 @@ struct FusedCtl {
   // chain of span s met an invalid record (~0: none; atomicMin), and the tile holding it
   // writes the counts and start bits of the records before it.  null: off.
   uint64_t* span_err;
+  // Serializable tables past kZJCap entries: entry i >= kZJCap of tile t at slot
+  // n_tiles * kZJCap + jbase[t] + i - kZJCap of jpos / jlen (jovf_cap slots in all, taken
+  // with jwork[1]; exhausted: abort reason 6, the host grows the arena and runs again).
+  uint32_t* jbase;
+  uint32_t jovf_cap;
 };
-constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile (more: abort reason 6)
+constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile in LDS (more: the overflow arena)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
 constexpr uint32_t kZTinySpan = 1024;   // whole spans up to this many bytes: pass 0, a lane each
 // abort reasons: 1 invalid record on the true chain, 2 span end, 3 exit mismatch,
-// 4 wait timeout, 5 Serializable record met without tables, 6 table overflow;
+// 4 wait timeout, 5 Serializable record met without tables, 6 a Serializable arena or work
+// list full (the host grows it and runs again);
 // abort[7] != 0: phase 3 found Serializable candidates (any tile)
 // phase 0: count, 1: scan, 2: emit, 3: Serializable tables, 4: small whole spans (before 0)
 // Per-span fallback: cnt[t] of every tile of bad span bad[i] := t == its first tile ?

@@ -248,3 +248,37 @@ def test_fused_device_output_large(feng):
         assert_span_equal(dec, s, b)
     if feng.segment_bytes >= 8192:
         assert not fell_back(feng)
+
+
+@pytest.mark.parametrize("kind", ["strings", "nulls"])
+def test_fused_dense_serializable_overflow(feng, kind):
+    """Tiles holding more Serializable streams than the 256 table entries kept in LDS: short
+    strings (9-21 byte records, ~500 per 8 KiB tile) and TC_NULL streams (6 bytes, ~1300 per
+    tile, every one through the general walker's work list).  The entries past 256 go to the
+    overflow arena in HBM (the arena or the work list grows and the batch runs again when
+    they are full), so the batch stays on the fast path (16 KiB segments) -- it used to abort
+    to the robust pipeline -- and matches the oracle bit for bit, over several spans."""
+    rng = np.random.default_rng(41 if kind == "strings" else 43)
+    parts = []
+    for s in range(3):
+        recs = []
+        for i in range(int(rng.integers(30000, 60000))):
+            if i % 97 == 0:
+                recs.append(synth.random_determinant(rng, allow_serializable=False))
+            elif kind == "strings":
+                recs.append(D.SerializableDeterminant(D.jser_string("s" * int(rng.integers(0, 13)))))
+            else:
+                recs.append(D.SerializableDeterminant(D.jser_null()))
+        parts.append(b"".join(D.encode(r) for r in recs))
+    blob, spans = b"", []
+    for p in parts:
+        spans.append((len(blob), len(p)))
+        blob += p
+    for _ in range(2):  # the batch that grows the arenas, then one that fits
+        feng.kernel_stats_reset()
+        dec = feng.decode_host(blob, spans)
+        for s, p in enumerate(parts):
+            assert_span_equal(dec, s, p)
+        ks = feng.kernel_stats()
+        if feng.segment_bytes == 16384:
+            assert not fell_back(feng) and "decode_span_fallback" not in ks, ks
