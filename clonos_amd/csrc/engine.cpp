@@ -853,8 +853,10 @@ struct clg_engine {
       }
       return CLG_OK;
     }
+    std::optional<HostTimer> hsub(std::in_place, this, "host_up_wait");  // (CLONOS_HOST_PROF sub-stages)
     CHK(flush());
     CHK(gwait());  // the scatter below writes segments an in-flight gather may read
+    hsub.reset();
     if (n >= kParallelLogs) {
       int st = CLG_OK;
       if (upstream_parallel(r, n, bytes, &st)) return st;
@@ -922,6 +924,7 @@ struct clg_engine {
   };
   std::vector<UpPlan> up_plan;
   bool upstream_parallel(clg_delta_req* r, uint32_t n, const uint8_t* bytes, int* out_st) {
+    std::optional<HostTimer> hsub(std::in_place, this, "host_up_seen");
     up_seen.assign(logs.size(), 0);
     for (uint32_t i = 0; i < n; ++i) {
       const uint32_t h = r[i].log;
@@ -934,7 +937,15 @@ struct clg_engine {
     const unsigned P = wp->size();
     const uint32_t per = (n + P - 1) / P, Cb = C();
     up_plan.resize(n);
+    // per part: segments, chunks and bytes it needs, and whether a request leaves a gap
+    struct UpPart {
+      uint64_t need = 0, chunks = 0, bytes = 0;
+      bool gap = false;
+    };
+    std::vector<UpPart> upart(P + 1);
+    hsub.emplace(this, "host_up_pass1");
     wp->run([&](unsigned k, unsigned) {
+      UpPart q;
       for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
         UpPlan& u = up_plan[i];
         u = UpPlan{0, 0, 0, 0, 0, 0, 0};
@@ -950,12 +961,37 @@ struct clg_engine {
         u.writer = l->writer;
         u.cur = cur;
         u.need = need_bytes > 0 ? uint32_t((need_bytes + Cb - 1) / Cb) : 0u;
+        q.need += u.need;
+        if (num_new > int32_t(r[i].len)) {
+          q.gap = true;
+        } else {
+          const uint32_t p = uint32_t(u.writer);
+          u.chunks = (p + uint32_t(num_new) - 1) / Cb - p / Cb + 1;
+          q.chunks += u.chunks;
+          q.bytes += uint64_t(num_new);
+        }
       }
+      upart[k + 1] = q;
     });
+    hsub.emplace(this, "host_up_serial");
     std::unique_lock<std::mutex> pool_guard(pool_mu);
     const size_t top = free_segs.size();
     size_t taken = 0, nch = 0, total = 0;
-    for (uint32_t i = 0; i < n; ++i) {  // request order: the pool and the chunk list
+    bool any_gap = false;
+    for (unsigned k = 0; k < P; ++k) {
+      any_gap |= upart[k + 1].gap;
+      upart[k + 1].need += upart[k].need;
+      upart[k + 1].chunks += upart[k].chunks;
+      upart[k + 1].bytes += upart[k].bytes;
+    }
+    // every request served (the usual batch): each part places its own segments and chunks
+    // from the parts' prefix in the second pass, as the request-order loop below would
+    const bool placed_in_parts = !any_gap && upart[P].need <= top;
+    if (placed_in_parts) {
+      taken = upart[P].need;
+      nch = upart[P].chunks;
+      total = upart[P].bytes;
+    } else for (uint32_t i = 0; i < n; ++i) {  // request order: the pool and the chunk list
       UpPlan& u = up_plan[i];
       if (!u.num_new) continue;
       if (u.need > top - taken) {
@@ -972,9 +1008,7 @@ struct clg_engine {
         u.num_new = 0;
         continue;
       }
-      const uint32_t p = uint32_t(u.writer);  // (no log record touched in this serial pass)
-      u.chunks = (p + uint32_t(u.num_new) - 1) / Cb - p / Cb + 1;
-      u.ch_from = nch;
+      u.ch_from = nch;  // (u.chunks from the first pass: no log record touched here)
       nch += u.chunks;
       total += size_t(u.num_new);
     }
@@ -983,9 +1017,17 @@ struct clg_engine {
       return true;
     }
     clg::ScatterChunk* ch = h_desc.as<clg::ScatterChunk>();
+    hsub.emplace(this, "host_up_pass2");
     wp->run([&](unsigned k, unsigned) {
+      uint64_t sf = upart[k].need, cf = upart[k].chunks;
       for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
-        const UpPlan& u = up_plan[i];
+        UpPlan& u = up_plan[i];
+        if (placed_in_parts && u.num_new) {
+          u.seg_from = sf;
+          sf += u.need;
+          u.ch_from = cf;
+          cf += u.chunks;
+        }
         if (!u.need && !u.num_new) continue;
         Log& l = logs[r[i].log];
         for (uint32_t j = 0; j < u.need; ++j) l.segs.push_back(free_segs[top - 1 - (u.seg_from + j)]);  // pop order
@@ -1009,6 +1051,7 @@ struct clg_engine {
     });
     free_segs.resize(top - taken);
     pool_guard.unlock();
+    hsub.emplace(this, "host_up_gpu");
     *out_st = CLG_OK;
     if (!nch) return true;
     const size_t db = nch * sizeof(clg::ScatterChunk);
@@ -1401,6 +1444,7 @@ struct clg_engine {
       bool bad = false;
     };
     std::vector<Part> part(P);
+    std::optional<HostTimer> hsub(std::in_place, this, "host_plan_pass1");
     std::vector<int32_t>& st = zst;
     std::vector<int32_t>& nb = znb;
     const uint32_t per = (n + P - 1) / P;
@@ -1436,6 +1480,7 @@ struct clg_engine {
       at[k + 1].tiny = at[k].tiny + part[k].tiny;
     }
     if (at[P].tiles >= (1ull << 32)) return false;
+    hsub.emplace(this, "host_plan_pass2");
     p.reset();
     p.unit = U;
     p.spans.resize(n);
