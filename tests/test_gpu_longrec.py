@@ -254,3 +254,29 @@ def test_span_fallback_error_equals_robust():
         finally:
             e.close()
     assert errs[0] == errs[1] and errs[0][1] == 9
+
+
+@pytest.mark.parametrize("parity", ["odd", "even"])
+@pytest.mark.parametrize("frac", [0.3, 0.7])
+def test_config3_batch_with_zero_run(leng, parity, frac):
+    """The verdict's other case: a config-3 batch (Serializable tables on) with a 64 KB run of
+    channel-0 Order records ("00 00": a valid record at every offset) inserted at a record
+    boundary of one span, crossing many chunk ends of the count pass; odd (after a 9-byte
+    Timestamp) and even.  Bit-exact against the oracle, every span."""
+    rng = np.random.default_rng(0xC1050003)
+    run = (D.encode(D.TimestampDeterminant(5)) if parity == "odd" else b"") + D.encode(D.OrderDeterminant(0)) * 32768
+    spans = []
+    for i in range(12):
+        b, offs = synth.config3_epoch(20000, rng)
+        b = b.tobytes()
+        if i == 5:
+            k = int(offs[int(len(offs) * frac)])
+            b = b[:k] + run + b[k:]
+        spans.append(b)
+    blob, sp = _join(spans)
+    for _ in range(2):
+        leng.kernel_stats_reset()
+        dec = leng.decode_host(blob, sp)
+        for s, b in enumerate(spans):
+            assert_span_equal(dec, s, b)
+        assert dec.n_rec == 12 * 20000 + 32768 + (parity == "odd")
