@@ -584,6 +584,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
                     got = ra.sizes[b0:b0 + int(ra.count[j])].tolist()
                     assert ra.status[j] == 0 and got == R.buffer_sizes(merged.get(x, b""))
                     j += 1
+            eng.kernel_stats_reset()  # (the timed steps' kernels and host stages below)
             continue
         ph["merge"] += t1 - t0
         ph["replay_prep"] += t2 - t1
@@ -592,6 +593,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
         if ra is not None:
             n_main_rec += int(ra.main.n_rec)
             n_sizes += int(ra.count.sum())
+    c5_stats = eng.kernel_stats()
     dev_t = "cpu" if rehearse else dev
     mx = torch.tensor([ph["merge"], ph["replay_prep"], ph["truncate"], ph["merge"] + ph["replay_prep"] + ph["truncate"]],
                       dtype=torch.float64, device=dev_t)
@@ -610,6 +612,8 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
                                         "truncate": round(t_ms, 4)},
             "winner_bytes_per_step": int(wb), "main_records_per_step": int(nm), "buffer_sizes_per_step": int(nsz),
             "replay_gbs": round(wb / ((m_ms + r_ms) * 1e-3) / 1e9, 3) if m_ms + r_ms > 0 else None,
+            "kernels_rank0": {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5))
+                              for k, v in c5_stats.items() if v["launches"]},
             "transport": "gloo rehearsal" if rehearse else "RCCL (nccl backend)"}
 
 

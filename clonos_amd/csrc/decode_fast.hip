@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict
   }
   __syncthreads();
   if (s_overflow) {
-    if (threadIdx.x == 0) span_flags[s] = 1u;
+    if (threadIdx.x == 0) span_flags[s] = 2u;  // (2: a table overflowed, 1: a chain broke; diagnostics)
     return;
   }
   if (!s_irregular) {

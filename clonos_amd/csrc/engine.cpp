@@ -2542,9 +2542,13 @@ struct clg_engine {
       std::vector<uint32_t> hf(ns);
       HIPCHK(hipMemcpyAsync(hf.data(), flags, size_t(ns) * 4, hipMemcpyDeviceToHost, stream));
       HIPCHK(hipStreamSynchronize(stream));
-      uint64_t nf = 0;
-      for (uint32_t f : hf) nf += f != 0;
+      uint64_t nf = 0, no = 0;
+      for (uint32_t f : hf) {
+        nf += f != 0;
+        no += f == 2;
+      }
       stats["robust_dp_spans"].launches += nf;
+      stats["robust_dp_spans_overflow"].launches += no;
       stats["robust_spans"].launches += ns;
     }
     // robust DP pipeline for flagged spans only (early exit elsewhere)

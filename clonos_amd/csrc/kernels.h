@@ -141,7 +141,10 @@ struct JArena {
   unsigned long long* used;
 };
 
-constexpr int kCands = 32;     // candidate entries per region (covers every fixed-layout record)
+#ifndef CLG_FCANDS
+#define CLG_FCANDS 32
+#endif
+constexpr int kCands = CLG_FCANDS;  // candidate entries per region (covers every fixed-layout record; <= 64)
 constexpr int kJserCap = 256;  // Serializable stream-length table entries per tile
 
 // Serializable stream lengths per tile, sorted by position (aligned coordinates):
