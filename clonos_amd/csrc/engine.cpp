@@ -571,6 +571,7 @@ struct clg_engine {
   hipEvent_t gdone[2] = {nullptr, nullptr};
   uint32_t gseq = 0;
   PinBuf h_rmeta;
+  PinBuf h_rout;  // replay-prep: the subpartition results, read back in one place (pinned)
   PinBuf h_plan;  // decode plans (upload_plan)
   DevBuf d_plan;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
@@ -2005,8 +2006,12 @@ struct clg_engine {
       return false;
     if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
+    static const uint32_t max_tiles = [] {  // tuning aid: tiles per span the single launch takes
+      const char* v = getenv("CLONOS_SMALL_MAXTILES");
+      return v ? std::min<uint32_t>(uint32_t(atoi(v)), clg::kZSmallTiles) : clg::kZSmallTiles;
+    }();
     for (const auto& sd : p.spans)
-      if (sd.n_tiles > clg::kZSmallTiles) return false;
+      if (sd.n_tiles > max_tiles) return false;
     return true;
   }
   // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered)
@@ -3336,6 +3341,10 @@ int clg_replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, cl
 int clg_replay_prepare_device(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out) {
   return replay_prepare(e, v, n, out, true);
 }
+// Pinned read-back of replay-prep's subpartition results: sizes, then count, err_off (8 B
+// each), status, err_tag (4 B each) per subpartition, as they lie on the device.
+static size_t o_rout_cnt(uint64_t n_sizes) { return (size_t(n_sizes) * 4 + 15) & ~size_t(15); }
+static size_t o_rout_end(uint32_t ns, uint64_t n_sizes) { return o_rout_cnt(n_sizes) + size_t(ns) * 24 + 64; }
 static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out, bool dev_in) {
   ENGINE_GUARD(e);
   if (!out || !out->main || !out->main_rec_base || (n && !v)) return fail(CLG_E_INVALID_ARG, "null argument");
@@ -3454,12 +3463,13 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
       return clg::launch_bufsizes_classify(d_spans, ns, d_first, d_count, d_status, d_eoff, d_etag, a, e->stream);
     };
     d_sub_status = d_status;
-    if (n_sizes)
-      HIPCHK(hipMemcpyAsync(out->buffer_sizes, e->d_rsizes.p, n_sizes * 4, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out->sub_count, d_count, ns * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out->sub_err_off, d_eoff, ns * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out->sub_status, d_status, ns * 4, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(out->sub_err_tag, d_etag, ns * 4, hipMemcpyDeviceToHost, e->stream));
+    // read back into pinned memory (asynchronous; into the caller's pageable arrays each copy
+    // was a staged synchronous one), copied out after the decode's sync below
+    CHK(e->h_rout.ensure(o_rout_end(ns, n_sizes)));
+    uint8_t* hr = e->h_rout.as<uint8_t>();
+    if (n_sizes) HIPCHK(hipMemcpyAsync(hr, e->d_rsizes.p, n_sizes * 4, hipMemcpyDeviceToHost, e->stream));
+    // count, err_off, status, err_tag: adjacent on the device (d_first's block): one copy
+    HIPCHK(hipMemcpyAsync(hr + o_rout_cnt(n_sizes), d_count, size_t(ns) * 24, hipMemcpyDeviceToHost, e->stream));
   }
   // main logs: the batched decode (span i = vertex i)
   auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
@@ -3468,14 +3478,23 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
   CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
   CHK(e->sync());
   // a Serializable walk in a subpartition buffer found the spill arena full: again, larger
+  uint8_t* hr = e->h_rout.as<uint8_t>();
+  const size_t oc = o_rout_cnt(n_sizes);
   while (ns && e->jarena_spilled(1)) {
     CHK(e->jarena_grow());
     clg::JArena jar;
     CHK(e->jarena_reset(&jar));
     CHK(classify(jar));
     CHK(e->jarena_note(1));
-    HIPCHK(hipMemcpyAsync(out->sub_status, d_sub_status, ns * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(hr + oc + size_t(ns) * 16, d_sub_status, size_t(ns) * 4, hipMemcpyDeviceToHost, e->stream));
     CHK(e->sync());
+  }
+  if (ns) {
+    if (n_sizes) memcpy(out->buffer_sizes, hr, n_sizes * 4);
+    memcpy(out->sub_count, hr + oc, size_t(ns) * 8);
+    memcpy(out->sub_err_off, hr + oc + size_t(ns) * 8, size_t(ns) * 8);
+    memcpy(out->sub_status, hr + oc + size_t(ns) * 16, size_t(ns) * 4);
+    memcpy(out->sub_err_tag, hr + oc + size_t(ns) * 20, size_t(ns) * 4);
   }
   return CLG_OK;
 }
