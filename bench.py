@@ -534,6 +534,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
             h = int(rep.replica_handle[gid])
         if h >= 0:
             copies[int(gid)] = h
+    copies_arr = X.copy_arrays(copies)  # (once: the merge takes the arrays every step)
     mine = [v for v in failed if dest_of[v] == rank]
     subs_of = {v: [int(x) for x in fg if int(table.vertex[x]) == v and not table.ids[x].is_main] for v in mine}
     ids = table_ids(table)
@@ -552,7 +553,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
         eng.sync()
         dist.barrier()
         t0 = _t.perf_counter()
-        mc = X.merge_responses(io, table, failed, copies, {v: e - 1 for v in failed}, dest_of, dev)
+        mc = X.merge_responses(io, table, failed, copies_arr, {v: e - 1 for v in failed}, dest_of, dev)
         sync()
         t1 = _t.perf_counter()
         ra = None

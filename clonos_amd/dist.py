@@ -329,12 +329,25 @@ class MergedCopies:
         return {g: self.bytes_of(g) for g in self.place}
 
 
-def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int, int],
+def copy_arrays(copies) -> Tuple[np.ndarray, np.ndarray]:
+    """merge_responses' `copies` as (gids ascending, handles): from a dict gid -> handle, or
+    already such a pair (a caller that merges every step converts its dict once)."""
+    if isinstance(copies, tuple):
+        return copies
+    kv = np.fromiter(itertools.chain.from_iterable(copies.items()), np.int64, 2 * len(copies)).reshape(-1, 2)
+    ck, cv = kv[:, 0], kv[:, 1]
+    if len(ck) > 1 and not (ck[1:] > ck[:-1]).all():  # (callers usually build it in gid order)
+        srt = np.argsort(ck)
+        ck, cv = ck[srt], cv[srt]
+    return ck, cv
+
+
+def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
                     start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None) -> MergedCopies:
     """Cross-GPU DeterminantResponseEvent.merge for the logs of the failed vertices.
 
     copies: gid -> io handle of this rank's copy (owned log or replica) of a log of a failed
-    vertex; start_epochs: failed VertexID -> the epoch the request asks from
+    vertex (a dict, or copy_arrays' pair); start_epochs: failed VertexID -> the epoch the request asks from
     (respondToDeterminantRequest -> getDeterminants(startEpoch), JobCausalLogImpl.java:
     188-204); dest_of: failed VertexID -> rank hosting its replacement.
 
@@ -358,11 +371,7 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies: Dict[int
     vslot = np.searchsorted(fv, table.vertex[gids])  # each log's failed vertex, as an index into fv
     ep_of = np.array([start_epochs[int(v)] for v in fv], np.int64)
     dest = np.array([dest_of[int(v)] for v in fv], np.int64)[vslot]
-    kv = np.fromiter(itertools.chain.from_iterable(copies.items()), np.int64, 2 * len(copies)).reshape(-1, 2)
-    ck, cv = kv[:, 0], kv[:, 1]
-    if len(ck) > 1 and not (ck[1:] > ck[:-1]).all():  # (callers usually build it in gid order)
-        srt = np.argsort(ck)
-        ck, cv = ck[srt], cv[srt]
+    ck, cv = copy_arrays(copies)
     pos = np.minimum(np.searchsorted(ck, gids), max(len(ck) - 1, 0))
     held = np.nonzero(ck[pos] == gids)[0] if len(ck) else np.zeros(0, np.int64)  # logs this rank holds
     handles = cv[pos[held]]

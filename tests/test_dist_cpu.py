@@ -229,6 +229,9 @@ def merge_worker(rank, world, port, q):
         store = OracleStore(full, cut, rank)
         merged = X.merge_responses(store, table, failed, store.handles, {1: 0, 5: 0}, dest_of, "cpu")
         got = merged.as_dict()
+        # the copies as copy_arrays' pair (what a caller merging every step passes): the same
+        again = X.merge_responses(store, table, failed, X.copy_arrays(store.handles), {1: 0, 5: 0}, dest_of, "cpu")
+        assert again.as_dict() == got and (again.ranks == merged.ranks).all()
         # the winner is the longest copy; equal lengths go to the highest rank
         for gid, rk in zip(merged.gids.tolist(), merged.ranks.tolist()):
             lens = cut[gid]
