@@ -207,8 +207,10 @@ def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, Determ
     ptr_o = np.asarray(merged.offs, np.uint64)[order] + np.uint64(merged.buf.data_ptr())
     len_o = np.asarray(merged.lens, np.uint64)[order]
     out = {}
-    for v in vertices:
-        lo, hi = int(np.searchsorted(vs, v, "left")), int(np.searchsorted(vs, v, "right"))
+    va = np.asarray(list(vertices), np.int64)
+    los = np.searchsorted(vs, va, "left").tolist()
+    his = np.searchsorted(vs, va, "right").tolist()
+    for v, lo, hi in zip(va.tolist(), los, his):
         ev = DeterminantResponseEvent(True, v, capacity=max(1, hi - lo))
         if hi > lo:
             ev.put_device_batch(ids_o[lo:hi], ptr_o[lo:hi], len_o[lo:hi], merged.buf)
@@ -248,8 +250,10 @@ def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResp
         n_sub += len(t)
         vs[i] = _lib.ReplayVertex(C.pointer(acc._c), C.cast(t.ctypes.data, C.POINTER(_lib.CausalLogIdC)), len(t), vid, 0)
         e = acc.entries()
-        main_bytes += int(e["len"][e["id"]["is_main"] != 0].sum())
-        sub_bytes += int(e["len"][e["id"]["is_main"] == 0].sum())  # a bound: the table may name fewer
+        ln = e["len"]
+        mb = int(ln[e["id"]["is_main"] != 0].sum())
+        main_bytes += mb
+        sub_bytes += int(ln.sum()) - mb  # a bound: the table may name fewer
     cap = main_bytes // 2 + n + 1
     d, arrs, _ = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
     base = np.zeros(n + 1, np.uint64)
