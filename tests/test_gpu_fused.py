@@ -282,3 +282,21 @@ def test_fused_dense_serializable_overflow(feng, kind):
         ks = feng.kernel_stats()
         if feng.segment_bytes == 16384:
             assert not fell_back(feng) and "decode_span_fallback" not in ks, ks
+
+
+@pytest.mark.parametrize("where", [0.2, 0.9])
+def test_fused_dense_serializable_error_past_lds_entries(feng, where):
+    """A dense tile of short strings whose invalid stream (a truncated string: its length
+    runs past the span end, or a bad type code) sits past the 256 entries LDS holds: the
+    error is the oracle's (status, offset, tag), from the table's overflow entries."""
+    rng = np.random.default_rng(47)
+    recs = [D.encode(D.SerializableDeterminant(D.jser_string("s" * int(rng.integers(0, 13)))))
+            for _ in range(20000)]
+    k = int(len(recs) * where)
+    recs[k] = b"\x03\xac\xed\x00\x05\x99"  # magic, then no valid type code
+    buf = b"".join(recs)
+    st, r, eo, et = O.decode(buf)
+    assert st != 0
+    with pytest.raises(ClonosError) as ei:
+        feng.decode_host(buf)
+    assert ei.value.status == st and ei.value.err_off == eo and ei.value.err_tag == et
