@@ -487,3 +487,76 @@ def test_many_logs_batched_upstream_and_truncation():
         for i in rng.choice(n_logs, 400, replace=False):
             assert logs[i].state() == oracle[i].state(), i
             assert logs[i].getDeterminants(2) == oracle[i].get_determinants(2)[1], i
+
+
+def _parallel_upstream_round(eng, logs, rng, ep, gap_at, n_recs=(1, 6), prev=None):
+    """One device-input batch, one request per log (the engine's per-part path above 8192
+    logs): fresh epochs, some empty, one gap, and (prev: the previous round's parts) every
+    third log re-delivering its previous delta (nothing new: the dedup)."""
+    import torch
+    from clonos_amd import _lib
+    from clonos_amd import dist as X
+    host = bytearray()
+    reqs = np.zeros(len(logs), X.DELTA_REQ)
+    parts = []
+    for i, l in enumerate(logs):
+        e, off = ep, 0
+        b = synth.random_log(int(rng.integers(*n_recs)), rng, allow_serializable=False)
+        if prev is not None and i % 3 == 0:
+            b, off, e = prev[i]
+        elif i % 97 == 5:
+            b = b""  # empty delta
+        elif i == gap_at:
+            off = 3  # offsetFromEpoch past the epoch's end in the log: a gap
+        reqs[i] = (l.handle, off, e, len(host), len(b), 0)
+        host += b
+        parts.append((b, off, e))
+    d = torch.frombuffer(bytearray(host or b"\0"), dtype=torch.uint8).to("cuda")
+    _lib.lib.clg_upstream_delta_batch(eng.handle, reqs.ctypes.data, len(reqs), d.data_ptr(), _lib.CLG_MEM_DEVICE)
+    torch.cuda.synchronize()
+    return reqs["status"].copy(), parts
+
+
+def test_parallel_upstream_batch_matches_oracle_and_serial():
+    """A device-input upstream batch of 9000 logs (one request each, so the engine places
+    segments and scatter chunks per part of the requests) with a gap, empty deltas and
+    re-deliveries: every status and every log's bytes equal the oracle's
+    ThreadCausalLogImpl.processUpstreamDelta (:117-154) and the one-thread engine's; then a
+    batch the pool cannot serve whole gives the same statuses in both engines (the
+    request-order path)."""
+    import os
+    n_logs, seg = 9000, 256
+    res = {}
+    for threads in ("8", "1"):
+        old = os.environ.get("CLONOS_HOST_THREADS")
+        os.environ["CLONOS_HOST_THREADS"] = threads
+        try:
+            rng = np.random.default_rng(91)
+            with Engine(segment_bytes=seg, pool_segments=n_logs * 4 + 100, ifl_pool_segments=16) as eng:
+                logs = [eng.open_log(CausalLogID.main(v)) for v in range(n_logs)]
+                oracle = [O.OracleLog(seg) for _ in range(n_logs)]
+                sts, prev = [], None
+                for ep in range(2):
+                    # epoch 0 with a gap (the request-order path), epoch 1 without (per part)
+                    st, parts = _parallel_upstream_round(eng, logs, rng, ep, gap_at=1234 if ep == 0 else -1,
+                                                         prev=prev)
+                    for i, (b, off, e) in enumerate(parts):
+                        assert int(st[i]) == oracle[i].upstream(b, off, e), (threads, ep, i)
+                    assert (st != 0).sum() == (1 if ep == 0 else 0)
+                    sts.append(st)
+                    prev = parts
+                for i in range(0, n_logs, 37):
+                    assert logs[i].getDeterminants(0) == oracle[i].get_determinants(0)[1], i
+                    assert logs[i].state() == oracle[i].state(), i
+                # the pool cannot hold this batch: request order decides who gets segments
+                st_big, _ = _parallel_upstream_round(eng, logs, rng, 2, gap_at=-1, n_recs=(100, 200))
+                assert (st_big != 0).any() and (st_big == 0).any()
+                res[threads] = (sts, st_big, [logs[i].getDeterminants(0) for i in range(0, n_logs, 53)])
+        finally:
+            if old is None:
+                os.environ.pop("CLONOS_HOST_THREADS", None)
+            else:
+                os.environ["CLONOS_HOST_THREADS"] = old
+    a, b = res["8"], res["1"]
+    assert all((x == y).all() for x, y in zip(a[0], b[0]))
+    assert (a[1] == b[1]).all() and a[2] == b[2]
