@@ -560,3 +560,28 @@ def test_parallel_upstream_batch_matches_oracle_and_serial():
     a, b = res["8"], res["1"]
     assert all((x == y).all() for x, y in zip(a[0], b[0]))
     assert (a[1] == b[1]).all() and a[2] == b[2]
+
+
+def test_many_span_decode_chunked_on_host_threads():
+    """A decode of 9000 logs (the count pass's equal-cost chunk boundaries placed per part of
+    the spans on the host threads): bit-exact against the oracle on a sample and on the fast
+    path (a wrong chunk table would leave tiles uncounted and send the batch robust)."""
+    rng = np.random.default_rng(93)
+    n_logs, seg = 9000, 4096
+    with Engine(segment_bytes=seg, pool_segments=n_logs * 4, timing=True, ifl_pool_segments=16) as eng:
+        logs, blobs = [], []
+        for v in range(n_logs):
+            l = eng.open_log(CausalLogID.main(v))
+            n = int(rng.integers(1, 400)) if v % 50 else int(rng.integers(2000, 6000))  # a few long logs
+            b = synth.random_log(n, rng, allow_serializable=False)
+            l.processUpstreamDelta(b, 0, 0)
+            logs.append(l)
+            blobs.append(b)
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs(logs, [0] * n_logs)
+        ks = eng.kernel_stats()
+        assert "decode_count" in ks and "decode_fallback" not in ks and "decode_span_fallback" not in ks, ks
+        from test_gpu_decode import assert_span_equal
+        for s in list(range(0, n_logs, 97)) + [n_logs - 1]:
+            assert_span_equal(dec, s, blobs[s])
+        assert dec.n_rec == sum(len(O.decode(b)[1]["tag"]) for b in blobs[::1])
