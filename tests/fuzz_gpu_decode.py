@@ -1,8 +1,9 @@
 """GPU decode fuzzer (a checker, run by hand on a GPU box; not collected by pytest):
 random batches of spans -- every tag, Serializable streams, long records, zero runs, dense
 short strings, byte flips that make decode errors -- decoded by the engine (auto, and the
-three-pass path) and compared with the C++ oracle's decodeNext loop span by span: bit-exact
-records, or the lowest failing span's (status, offset, tag).  Prints one JSON line per
+three-pass path), and the same bytes as logs in 4 KiB HBM segments delivered over a few
+epochs (decode_logs from a random start epoch), compared with the C++ oracle's decodeNext
+loop span by span: bit-exact records, or the lowest failing span's (status, offset, tag).  Prints one JSON line per
 round; stops at the first mismatch with its seed.
 usage: python tests/fuzz_gpu_decode.py [--minutes M] [--seed S]"""
 import argparse
@@ -87,9 +88,49 @@ def check(eng, spans):
     return None
 
 
+def check_logs(eng, spans, rng):
+    """The spans as logs in HBM segments (each delivered as upstream deltas over a few epochs),
+    decoded from a random start epoch: each log's getDeterminants(start) against the oracle."""
+    from clonos_amd import CausalLogID
+    logs, start, want = [], [], []
+    for i, b in enumerate(spans):
+        l = eng.open_log(CausalLogID.main(i % 30000))
+        n_ep = int(rng.integers(1, 4))
+        cuts = sorted(int(x) for x in rng.integers(0, len(b) + 1, n_ep - 1)) if len(b) else [0] * (n_ep - 1)
+        bounds = [0] + cuts + [len(b)]
+        for e in range(n_ep):
+            part = b[bounds[e]:bounds[e + 1]]
+            if part:
+                l.processUpstreamDelta(part, 0, e)
+        logs.append(l)
+        start.append(int(rng.integers(0, n_ep)))
+        want.append(l.getDeterminants(start[-1]))
+    try:
+        errs = [(s, O.decode(b)) for s, b in enumerate(want)]
+        bad = [(s, r) for s, r in errs if r[0] != 0]
+        try:
+            dec = eng.decode_logs(logs, start)
+        except ClonosError as e:
+            if not bad:
+                return f"logs: unexpected error {e.status} span {e.err_span}"
+            s, (st, _, eo, et) = bad[0]
+            if (e.status, e.err_span, e.err_off, e.err_tag) != (st, s, eo, et):
+                return f"logs: error {(e.status, e.err_span, e.err_off, e.err_tag)} != oracle {(st, s, eo, et)}"
+            return None
+        if bad:
+            return "logs: no error, the oracle has one"
+        for s, b in enumerate(want):
+            assert_span_equal(dec, s, b)
+        return None
+    finally:
+        for l in logs:
+            l.close()
+
+
 rng0 = np.random.default_rng(args.seed)
 engines = {"auto": Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True),
            "three_pass": Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True, decode="three_pass")}
+log_eng = Engine(segment_bytes=4096, pool_segments=1 << 19, timing=True)  # logs over 4 KiB segments
 t_end = time.time() + args.minutes * 60
 rnd = 0
 while time.time() < t_end:
@@ -108,6 +149,10 @@ while time.time() < t_end:
         if msg:
             print(json.dumps({"round": rnd, "seed": seed, "engine": name, "FAIL": msg}), flush=True)
             sys.exit(1)
+    msg = check_logs(log_eng, spans, rng)
+    if msg:
+        print(json.dumps({"round": rnd, "seed": seed, "engine": "logs", "FAIL": msg}), flush=True)
+        sys.exit(1)
     ks = engines["auto"].kernel_stats()
     paths = sorted(k for k in ks if k in ("decode_fallback", "decode_span_fallback", "decode_kept_errors",
                                           "decode_jser_retry", "decode_jser_grow", "decode_small"))
@@ -115,6 +160,6 @@ while time.time() < t_end:
     print(json.dumps({"round": rnd, "seed": seed, "spans": n, "bytes": sum(len(b) for b in spans), "ok": True,
                       "paths": paths}), flush=True)
     rnd += 1
-for e in engines.values():
+for e in list(engines.values()) + [log_eng]:
     e.close()
 print(json.dumps({"rounds": rnd, "ok": True}), flush=True)
