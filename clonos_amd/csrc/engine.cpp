@@ -2600,6 +2600,9 @@ struct clg_engine {
         std::vector<uint32_t> hd(size_t(nt) * clg::kFPoints);
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
         fwrite(hd.data(), 4, hd.size(), fp);
+        std::vector<clg::LaneSeg> hl(size_t(nt) * clg::kFPoints);
+        hipMemcpy(hl.data(), d_lanes.p, hl.size() * sizeof(clg::LaneSeg), hipMemcpyDeviceToHost);
+        fwrite(hl.data(), sizeof(clg::LaneSeg), hl.size(), fp);
         fclose(fp);
       }
     }
