@@ -344,6 +344,12 @@ __device__ LaneSeg parse_segment(const FastCtx& c, const uint32_t* s_c, int l, b
         seg.end = (uint8_t)m;
         seg.cnt = cnt;
         seg.wcnt = w;
+      } else if (m >= kFPoints && pos >= c.hi && c.t + 1 < c.t1 && pos - c.hi < 0xFFFFu) {
+        // every next-tile point passed: the chain's next start, in the next tile (kEndFar)
+        seg.end = kEndFar;
+        seg.far = (uint16_t)(pos - c.hi);
+        seg.cnt = cnt;
+        seg.wcnt = w;
       }
       return seg;
     }
@@ -452,9 +458,9 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   lanes[(uint64_t)t * kFPoints + lane] = seg;
   const uint64_t own_kept = __ballot(lane < (uint32_t)kFOwn && kept != kConvUnknown);
   const int f = own_kept ? __builtin_ctzll(own_kept) : kFPoints;
-  const uint32_t g_end = seg.end, g_cnt = seg.cnt, g_w = seg.wcnt;
+  const uint32_t g_end = seg.end, g_cnt = seg.cnt, g_w = seg.wcnt, g_far = seg.far;
   uint64_t valid = 0;
-  uint32_t cnt = 0, w = 0;
+  uint32_t cnt = 0, w = 0, far = 0;
   int v = f;
   while (v < kFOwn) {
     const uint32_t e = __builtin_amdgcn_readlane(g_end, v);
@@ -462,12 +468,14 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
     valid |= 1ull << v;
     cnt += __builtin_amdgcn_readlane(g_cnt, v);
     w += __builtin_amdgcn_readlane(g_w, v);
+    if (e == kEndFar) far = __builtin_amdgcn_readlane(g_far, v);
     v = (int)e;
   }
   if (lane == 0) {
     TileSum sm{};
     sm.f = f < kFOwn ? (uint8_t)f : kEndFail;
-    sm.x = (v >= kFOwn && v < kFPoints) ? (uint8_t)(v - kFOwn) : kEndFail;
+    sm.x = v == (int)kEndFar ? kEndFar : (v >= kFOwn && v < kFPoints) ? (uint8_t)(v - kFOwn) : kEndFail;
+    sm.far = (uint16_t)far;
     sm.cnt = cnt;
     sm.wcnt = w;
     sm.valid = valid;
@@ -519,6 +527,8 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
 }
 
 // ---- pass F2: per-span resolution ------------------------------------------------------
+// *exit_idx: the next tile's point index, or -1 - far (a kEndFar exit, `far` bytes past the
+// tile end).
 __device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* valid, uint32_t* cnt, uint32_t* wcnt,
                            int* exit_idx) {
   uint64_t vm = 0;
@@ -530,6 +540,13 @@ __device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* va
     vm |= 1ull << v;
     c += gs.cnt;
     w += gs.wcnt;
+    if (gs.end == kEndFar) {
+      *valid = vm;
+      *cnt = c;
+      *wcnt = w;
+      *exit_idx = -1 - (int)gs.far;
+      return true;
+    }
     v = gs.end;
   }
   if (v >= kFPoints) return false;
@@ -540,10 +557,58 @@ __device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* va
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict__ spans, const LaneSeg* __restrict__ lanes,
+// A chain that enters tile t at aligned coordinate `entry` (a kEndFar exit of the tile
+// before): walked record by record from HBM (exact lengths) to the first of the tile's own
+// kept points it lands on.  *e: the own point the chain goes on from -- that point itself when
+// the entry is one; else point 0, rewritten to start at the entry with the walk as (the head
+// of) its segment, so that the chain, the counts and the emit (which parses cnt records from
+// conv[0]) go through it like any other.  false: the walk fails or passes every own point
+// (the span goes to the DP).
+__device__ bool enter_far(const TileDesc* tiles, const SpanDesc& sd, uint32_t t, uint32_t entry, uint32_t* conv,
+                          LaneSeg* lanes, JArena ar, int* e) {
+  const TileDesc td = tiles[t];
+  SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, ar};
+  uint32_t* cv = conv + (uint64_t)t * kFPoints;
+  LaneSeg* ls = lanes + (uint64_t)t * kFPoints;
+  int m = next_kept(cv, 0);
+  uint32_t pos = entry, c = 0, w = 0;
+  for (uint32_t it = 0; it < kMaxSegRecords; ++it) {
+    while (m < kFOwn && cv[m] < pos) m = next_kept(cv, m + 1);
+    if (m >= kFOwn) return false;
+    if (cv[m] == pos) {
+      if (c == 0) {  // the entry is a kept point
+        *e = m;
+        return true;
+      }
+      LaneSeg head{(uint8_t)m, 0, 0, c, w};
+      if (m == 0) {  // the walk ends on point 0: it heads point 0's own segment
+        head = ls[0];
+        head.cnt += c;
+        head.wcnt += w;
+      }
+      ls[0] = head;
+      cv[0] = entry;
+      *e = 0;
+      return true;
+    }
+    const uint64_t so = td.span_off + (pos - td.delta);
+    if (so >= sd.len) return false;
+    AtSpan b{&sr, so};
+    const int tag = (int)b(0);
+    const int64_t L = rec_len_slow(b, sd.len - so);
+    if (L <= 0) return false;
+    ++c;
+    w += is_wide(tag);
+    pos += (uint32_t)L;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_fast_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                      uint32_t* __restrict__ conv, LaneSeg* __restrict__ lanes,
                                                       const TileSum* __restrict__ sums, const uint32_t* __restrict__ jn,
                                                       FastRes* __restrict__ fres, SpanRes* __restrict__ sres,
-                                                      uint32_t* __restrict__ span_flags) {
+                                                      uint32_t* __restrict__ span_flags, JArena ar) {
   __shared__ uint64_t s_r[256], s_w[256];
   __shared__ uint32_t s_irregular, s_overflow;
   __shared__ uint64_t s_carry_r, s_carry_w;
@@ -620,6 +685,13 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const SpanDesc* __restrict
       uint64_t vm;
       uint32_t c, w;
       int x;
+      if (e < 0) {  // the tile before left by a kEndFar exit: enter at that record start
+        const uint32_t entry = tiles[t].delta + (uint32_t)(-1 - e);
+        if (!enter_far(tiles, sd, t, entry, conv, lanes, ar, &e)) {
+          fallback = true;
+          break;
+        }
+      }
       if (!chain_from(lanes, t, e, &vm, &c, &w, &x)) {
         fallback = true;
         break;
@@ -769,11 +841,12 @@ int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
   return ok(hipGetLastError());
 }
 
-int launch_fast_resolve(const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes, const TileSum* d_sums,
-                        const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream) {
+int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, uint32_t* d_conv,
+                        LaneSeg* d_lanes, const TileSum* d_sums, const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres,
+                        uint32_t* d_span_flags, JArena ar, void* stream) {
   if (!n_spans) return CLG_OK;
-  hipLaunchKernelGGL(k_fast_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_spans, d_lanes, d_sums, d_jn,
-                     d_fres, d_sres, d_span_flags);
+  hipLaunchKernelGGL(k_fast_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_lanes,
+                     d_sums, d_jn, d_fres, d_sres, d_span_flags, ar);
   return ok(hipGetLastError());
 }
 

@@ -2539,9 +2539,9 @@ struct clg_engine {
                                    d_sums.as<clg::TileSum>(), dbg, nullptr, stream);
     }));
     CHK(timed("robust_resolve", uint64_t(nt) * 32, [&] {
-      return clg::launch_fast_resolve(ds, ns, d_lanes.as<clg::LaneSeg>(), d_sums.as<clg::TileSum>(),
-                                      d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(), d_sres.as<clg::SpanRes>(), flags,
-                                      stream);
+      return clg::launch_fast_resolve(dt, ds, ns, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(),
+                                      d_sums.as<clg::TileSum>(), d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(),
+                                      d_sres.as<clg::SpanRes>(), flags, jar, stream);
     }));
     if (cfg.flags & CLG_F_TIMING) {  // diagnostics: spans the convergence-point tier leaves to the DP
       std::vector<uint32_t> hf(ns);

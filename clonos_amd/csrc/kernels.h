@@ -108,18 +108,23 @@ constexpr uint32_t kConvUnknown = 0xFFFFFFFFu;
 struct LaneSeg {
   uint8_t end;
   uint8_t flags;
-  uint16_t pad;
+  uint16_t far;   // end == kEndFar: the chain's next record start, bytes past the tile end
   uint32_t cnt;
   uint32_t wcnt;
 };
 constexpr uint8_t kEndFail = 0xFF;
+// The segment passed every next-tile point (all three off the chain: a long record across
+// the next tile's first region starts) and stops at a record start in the next tile instead;
+// the resolve walks the next tile from there to one of its own points.
+constexpr uint8_t kEndFar = 0xFE;
 
 // Tile summary assuming the tile's entry is its first kept point f.
 struct TileSum {
   uint32_t cnt, wcnt;
   uint8_t f;      // first kept own point (kEndFail: none)
-  uint8_t x;      // exit: next tile's point index (0..kFNext-1) the chain lands on; kEndFail = none
-  uint8_t pad[2];
+  uint8_t x;      // exit: next tile's point index (0..kFNext-1) the chain lands on; kEndFail = none;
+                  // kEndFar: a record start `far` bytes past the tile end
+  uint16_t far;
   uint32_t pad2;
   uint64_t valid; // own lanes on the chain from f
 };
@@ -163,8 +168,9 @@ struct JserTabs {
 int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t* d_conv, JserTabs J,
                      uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, uint64_t* d_prof, void* stream);
 int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream);
-int launch_fast_resolve(const SpanDesc* d_spans, uint32_t n_spans, const LaneSeg* d_lanes, const TileSum* d_sums,
-                        const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres, uint32_t* d_span_flags, void* stream);
+int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, uint32_t* d_conv,
+                        LaneSeg* d_lanes, const TileSum* d_sums, const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres,
+                        uint32_t* d_span_flags, JArena ar, void* stream);
 int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
                      JserTabs J, const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
                      const uint32_t* d_span_flags, DecodeOut out, void* stream);

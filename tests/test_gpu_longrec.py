@@ -280,3 +280,23 @@ def test_config3_batch_with_zero_run(leng, parity, frac):
         for s, b in enumerate(spans):
             assert_span_equal(dec, s, b)
         assert dec.n_rec == 12 * 20000 + 32768 + (parity == "odd")
+
+
+def test_robust_config3_far_exits_bit_exact():
+    """The robust pipeline alone on config-3 logs (10 epochs each): Serializable Integers (82 B)
+    across 16 KiB tile ends leave all three next-tile points of a tile off the chain, so the
+    last segment ends at a record start in the next tile (kEndFar) and the resolve enters the
+    next tile there.  Every record equals the oracle's and no span needs the DP tables."""
+    rng = np.random.default_rng(0xC1050003)
+    gen = [synth.config3_epoch(40000, rng, e) for e in range(10)]
+    spans = [b"".join(gen[(e + v) % 10][0].tobytes() for e in range(10)) for v in range(4)]
+    blob, sp = _join(spans)
+    e = Engine(segment_bytes=16384, pool_segments=1 << 13, timing=True, decode="robust")
+    try:
+        dec = e.decode_host(blob, sp)
+        for s, b in enumerate(spans):
+            assert_span_equal(dec, s, b)
+        ks = e.kernel_stats()
+        assert ks.get("robust_dp_spans", {}).get("launches", 0) == 0, ks
+    finally:
+        e.close()
