@@ -486,6 +486,61 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
 }
 
 // ---- Serializable stream-length tables for deferred tiles --------------------------------
+// Record length of the candidate at a for the two common stream shapes, over a byte reader
+// (the fused path's inline shapes, decode_fused.hip jser_inline_len / jser_flat_len): a
+// TC_STRING, and one TC_OBJECT whose class and superclasses are fresh TC_CLASSDESCs with flags
+// SC_SERIALIZABLE only, primitive fields only and an empty annotation.  *general: some other
+// shape -- the grammar walker decides.  0 with *general clear: the stream runs past the span.
+template <class R>
+__device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* general) {
+  auto b = [&](uint32_t q) { return (uint32_t)r.at(q); };
+  auto u16 = [&](uint32_t q) { return b(q) << 8 | b(q + 1); };
+  *general = false;
+  if (avail < 8) {
+    *general = true;
+    return 0u;
+  }
+  const uint32_t tc = b(a + 5);
+  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+    const uint64_t L = 8ull + u16(a + 6);
+    return L <= avail ? (uint32_t)L : 0u;
+  }
+  *general = true;
+  if (tc != jser::TC_OBJECT) return 0u;
+  const uint64_t lim = avail < 4096 ? avail : 4096;  // (longer: the walker)
+  uint32_t p = a + 6, data = 0;
+  for (int depth = 0;; ++depth) {
+    if (p + 1 > a + lim || depth > 8) return 0u;
+    const uint32_t c = b(p);  // [TC_CLASSDESC][className length u16] or [TC_NULL]
+    if (c == jser::TC_NULL) {  // no (further) superclass
+      ++p;
+      break;
+    }
+    if (c != jser::TC_CLASSDESC || p + 3 > a + lim) return 0u;
+    p += 3 + u16(p + 1) + 8;  // className, serialVersionUID
+    if (p + 3 > a + lim) return 0u;
+    if (b(p) != jser::SC_SERIALIZABLE) return 0u;
+    const uint32_t nf = u16(p + 1);
+    if (nf & 0x8000u) return 0u;
+    p += 3;
+    for (uint32_t i = 0; i < nf; ++i) {
+      if (p + 3 > a + lim) return 0u;
+      const uint32_t ft = b(p);  // [typecode][fieldName length u16]
+      const uint32_t sz = ft == 'B' || ft == 'Z' ? 1u : ft == 'C' || ft == 'S' ? 2u : ft == 'I' || ft == 'F' ? 4u
+                          : ft == 'J' || ft == 'D' ? 8u : 0u;
+      if (!sz) return 0u;
+      data += sz;
+      p += 3 + u16(p + 1);
+    }
+    if (p + 1 > a + lim || b(p) != jser::TC_ENDBLOCKDATA) return 0u;
+    ++p;
+  }
+  p += data;
+  if (p > a + lim) return 0u;
+  *general = false;
+  return p - a;
+}
+
 __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   JserTabs J) {
   __shared__ uint32_t s_tile[kImageDwords];
@@ -516,8 +571,13 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   TileReader tr{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
   for (uint32_t a = rs; a < re; ++a) {
     if (t_u8(s_tile, a) != CLG_TAG_SERIALIZABLE || t_be32(s_tile, a + 1) != kSerMagic) continue;
-    AtTileSpan b{&tr, a};
-    const int64_t L = rec_len_slow(b, sd.len - (td.span_off + (a - td.delta)));  // walker: 1 + stream length
+    const uint64_t avail = sd.len - (td.span_off + (a - td.delta));
+    bool general;
+    int64_t L = jser_inline_len_r(tr, a, avail, &general);  // the common shapes inline
+    if (general) {
+      AtTileSpan b{&tr, a};
+      L = rec_len_slow(b, avail);  // walker: 1 + stream length
+    }
     if (idx < (uint32_t)kJserCap) {
       J.pos[(uint64_t)t * kJserCap + idx] = a;
       J.len[(uint64_t)t * kJserCap + idx] = L > 1 ? (uint32_t)(L - 1) : 0u;
