@@ -41,6 +41,7 @@ CLG_F_ROBUST_DECODE = 2
 CLG_F_ASYNC_SLICE = 4
 CLG_F_NO_SMALL_DECODE = 8
 CLG_FULL_SHARING = -1
+CLG_DECODE_MAX_INFLIGHT = 2  # asynchronous decodes queued before the first wait
 CLG_IFL_IN_MEMORY = 0
 CLG_IFL_SPILLABLE = 1
 CLG_IFL_CONTINUE = 1        # IflReplayReq.flags

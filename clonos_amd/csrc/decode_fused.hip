@@ -1457,6 +1457,94 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
   gp(ctl.span_hi)[s] = gp(ctl.base)[t1] + gp(ctl.boff)[t1 / kZScanBlock] + gp(ctl.cnt)[t1];
 }
 
+// Pass 2 in one launch (phase 5): scan1's per-block bases, the block offsets by a decoupled
+// look-back (a ticket gives each workgroup its block, so it only ever waits for blocks that
+// started before it), and the span ranges -- span_hi of every span whose last tile is in the
+// block, also into the host's read-back buffer with the abort words, so the host needs no
+// copy after the decode.  Three launches were ~25 us between count and emit beside the slice
+// gather, and the read-back copy another ~45 us (its blit kernel waits for CU slots too).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 1ull << 63, kLbVal = kLbAgg - 1;
+__global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict__ tiles,
+                                                     const SpanDesc* __restrict__ spans, uint32_t n_spans,
+                                                     FusedCtl ctl) {
+  __shared__ uint64_t s_w[4];
+  __shared__ uint64_t s_pre;
+  __shared__ uint32_t s_blk;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t nt = ctl.n_tiles;
+  if (tid == 0) s_blk = atomicAdd(reinterpret_cast<unsigned int*>(ctl.lb), 1u);
+  __syncthreads();
+  const uint32_t blk = s_blk;
+  volatile uint32_t* hab = ctl.h_res ? reinterpret_cast<volatile uint32_t*>(ctl.h_res + 2ull * n_spans) : nullptr;
+  if (blk == 0 && hab && tid < 10u) hab[tid] = ld_agent32(ctl.abort + tid);  // final: count and repair ran
+  if (ld_agent32(ctl.abort)) return;  // (every block: nothing writes it during this kernel)
+  const uint32_t i0 = blk * kZScanBlock + tid * 4u;
+  uint64_t v[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = i0 + j < nt ? gp(ctl.cnt)[i0 + j] : 0ull;
+    sum += v[j];
+  }
+  const uint64_t incl = wave_incl_scan(sum, lane);
+  if (lane == 63u) s_w[wv] = incl;
+  __syncthreads();
+  uint64_t run = incl - sum;
+  for (uint32_t k = 0; k < wv; ++k) run += s_w[k];
+  uint64_t lb_[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lb_[j] = run;
+    if (i0 + j < nt) gp(ctl.base)[i0 + j] = run;
+    run += v[j];
+  }
+  if (tid == 0) {
+    const uint64_t total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    uint64_t* W = ctl.lb + 1;
+    uint64_t pre = 0;
+    if (blk == 0) {
+      st_agent(&W[0], kLbPre | total);
+    } else {
+      st_agent(&W[blk], kLbAgg | total);
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      for (uint32_t j = blk - 1;;) {
+        const uint64_t x = ld_agent(&W[j]);
+        if (!(x & (kLbAgg | kLbPre))) {
+          if (__builtin_amdgcn_s_memtime() - t0 > kZSpinLimit) {  // (cannot happen: earlier tickets run)
+            raise_abort(ctl, 4, 0u);  // a wait timed out: the batch goes robust
+            if (hab) {
+              hab[4] = ~0u;
+              hab[0] = 1u;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        pre += x & kLbVal;
+        if (x & kLbPre) break;
+        --j;
+      }
+      st_agent(&W[blk], kLbPre | (pre + total));
+    }
+    gp(ctl.boff)[blk] = pre;
+    s_pre = pre;
+  }
+  __syncthreads();
+  const uint64_t pre = s_pre;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t t = i0 + j;
+    if (t >= nt) break;
+    const uint32_t sp = tiles[t].span;
+    const SpanDesc sd = spans[sp];
+    if (t + 1 == sd.first_tile + sd.n_tiles) {  // the span's last tile
+      const uint64_t hi = pre + lb_[j] + v[j];
+      gp(ctl.span_hi)[sp] = hi;
+      if (ctl.h_res) reinterpret_cast<volatile uint64_t*>(ctl.h_res)[n_spans + sp] = hi;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Pass 3 for one tile: record starts dropped into LDS by output index (from the bitmap),
 // then consecutive lanes decode consecutive records, so each SoA store of the wave is one
@@ -2761,6 +2849,9 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     }
   } else if (phase == 4) {
     ZLAUNCH(k_decode_count_tiny, dim3((nt + 63) / 64), dim3(64), 0, st, d_tiles, d_spans, ctl);
+  } else if (phase == 5) {  // scan, block offsets and span ranges in one launch (ctl.lb zeroed)
+    const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
+    ZLAUNCH(k_decode_scan, dim3(nb), dim3(256), 0, st, d_tiles, d_spans, n_spans, ctl);
   } else if (phase == 1) {
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     if (nb > 1024u) return CLG_E_INVALID_ARG;  // > 1M tiles (8 GiB) per batch: the host splits

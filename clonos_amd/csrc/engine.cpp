@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -504,11 +505,13 @@ struct Mapped {
 };
 std::mutex g_map_mu;
 std::vector<Mapped> g_mapped;
-// The device address of registered host memory at h (0: not inside a registered range).
-uintptr_t clg_mapped_device_address(const void* h) {
+// The device address of registered host memory [h, h + n) (0: not wholly inside one
+// registered range).
+uintptr_t clg_mapped_device_address(const void* h, uint64_t n) {
   std::lock_guard<std::mutex> g(g_map_mu);
   for (const Mapped& m : g_mapped)
-    if (uintptr_t(h) >= m.host && uintptr_t(h) < m.host + m.bytes) return m.dev + (uintptr_t(h) - m.host);
+    if (uintptr_t(h) >= m.host && uintptr_t(h) < m.host + m.bytes && n <= m.host + m.bytes - uintptr_t(h))
+      return m.dev + (uintptr_t(h) - m.host);
   return 0;
 }
 }  // namespace
@@ -539,7 +542,13 @@ struct clg_engine {
   std::mutex dirty_mu;  // dirty, idem
 
   // staging / scratch
-  PinBuf h_stage, h_desc, h_sres, h_zres, h_outs;
+  PinBuf h_stage, h_desc, h_sres, h_outs;
+  // Per decode slot (0: synchronous calls; 1, 2: the asynchronous decodes in flight): the
+  // read-back of span ranges and abort words, the staged plan, the end-of-read-back event.
+  static constexpr uint32_t kSlots = 1 + CLG_DECODE_MAX_INFLIGHT;
+  PinBuf h_zres_s[kSlots], h_plan_s[kSlots];
+  hipEvent_t zdone[kSlots] = {};
+  uint32_t plan_slot = 0;  // the slot stage_plan / enqueue_plan use (launch_fused sets it)
   DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
@@ -572,7 +581,6 @@ struct clg_engine {
   uint32_t gseq = 0;
   PinBuf h_rmeta;
   PinBuf h_rout;  // replay-prep: the subpartition results, read back in one place (pinned)
-  PinBuf h_plan;  // decode plans (upload_plan)
   DevBuf d_plan;
   bool fused_decode = true;  // CLG_F_ROBUST_DECODE / CLONOS_DECODE=robust: robust pipeline only
   bool small_decode = true;  // CLG_F_NO_SMALL_DECODE / CLONOS_SMALL=0: no single-launch small batches
@@ -1150,23 +1158,42 @@ struct clg_engine {
     return sync();
   }
 
+  // The gather's descriptors, staged: runs | segment table; *o: where each part starts.
+  // (Tried and removed: pieces in source order -- every consumer's piece of one segment back
+  // to back on one XCD, for L2 hits -- took the isolated config-2 gather from 0.39 to 0.43 ms
+  // and cost 0.1 ms of host grouping per step.)
+  static size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
+  static size_t gather_desc_layout(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab,
+                                   size_t o[2]) {
+    o[0] = 0;
+    o[1] = al16(runs.size() * sizeof(clg::SegSpan));
+    return o[1] + segtab.size() * 4;
+  }
+  static void gather_desc_fill(uint8_t* h, const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab,
+                               const size_t o[2]) {
+    memcpy(h + o[0], runs.data(), runs.size() * sizeof(clg::SegSpan));
+    memcpy(h + o[1], segtab.data(), segtab.size() * 4);
+  }
+  int gather_expand(const uint8_t* d, const std::vector<clg::SegSpan>& runs, const size_t o[2], uint32_t n_pieces,
+                    clg::GatherPiece* pieces, hipStream_t on) {
+    return clg::launch_expand_pieces(reinterpret_cast<const clg::SegSpan*>(d), uint32_t(runs.size()), n_pieces,
+                                     reinterpret_cast<const uint32_t*>(d + o[1]), pool, C(), pieces, on);
+  }
+
   // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
   int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                       uint64_t total, void* out, uint32_t out_kind) {
     if (runs.empty() || !n_pieces) return CLG_OK;
     if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
       return gather_runs_async(runs, segtab, n_pieces, total, out);
-    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
-    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    size_t o[2];
+    const size_t hb = gather_desc_layout(runs, segtab, o);
     CHK(h_desc.ensure(hb));
     CHK(d_desc.ensure(hb));
     CHK(d_pieces.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
-    memcpy(h_desc.p, runs.data(), rb);
-    memcpy(h_desc.as<uint8_t>() + o_seg, segtab.data(), gb);
+    gather_desc_fill(h_desc.as<uint8_t>(), runs, segtab, o);
     HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
-    CHK(clg::launch_expand_pieces(d_desc.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
-                                  reinterpret_cast<const uint32_t*>(d_desc.as<uint8_t>() + o_seg), pool, C(),
-                                  d_pieces.as<clg::GatherPiece>(), stream));
+    CHK(gather_expand(d_desc.as<uint8_t>(), runs, o, n_pieces, d_pieces.as<clg::GatherPiece>(), stream));
     uint8_t* dout;
     if (out_kind == CLG_MEM_DEVICE) {
       dout = static_cast<uint8_t*>(out);
@@ -1189,22 +1216,19 @@ struct clg_engine {
     const uint32_t set = gseq++ & 1u;
     if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
     else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
-    const size_t rb = runs.size() * sizeof(clg::SegSpan), gb = segtab.size() * sizeof(uint32_t);
-    const size_t o_seg = (rb + 15) & ~size_t(15), hb = o_seg + gb;
+    size_t o[2];
+    const size_t hb = gather_desc_layout(runs, segtab, o);
     PinBuf& hd = h_gdesc[set];
     DevBuf& dd = d_gdesc[set];
     DevBuf& dp = d_gpieces[set];
     CHK(hd.ensure(hb));
     CHK(dd.ensure(hb));
     CHK(dp.ensure(size_t(n_pieces) * sizeof(clg::GatherPiece)));
-    memcpy(hd.p, runs.data(), rb);
-    memcpy(hd.as<uint8_t>() + o_seg, segtab.data(), gb);
+    gather_desc_fill(hd.as<uint8_t>(), runs, segtab, o);
     // no wait on `stream`: every pool write (flush, upstream scatter) has completed when
     // its call returned, and decodes only read the pool
     HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
-    CHK(clg::launch_expand_pieces(dd.as<clg::SegSpan>(), uint32_t(runs.size()), n_pieces,
-                                  reinterpret_cast<const uint32_t*>(dd.as<uint8_t>() + o_seg), pool, C(),
-                                  dp.as<clg::GatherPiece>(), gstream));
+    CHK(gather_expand(dd.as<uint8_t>(), runs, o, n_pieces, dp.as<clg::GatherPiece>(), gstream));
     CHK(timed("slice_gather", 2 * total, [&] {
       return clg::launch_gather(dp.as<clg::GatherPiece>(), n_pieces, static_cast<uint8_t*>(out), gstream);
     }, gstream));
@@ -1545,6 +1569,7 @@ struct clg_engine {
     L->o_spans = (L->o_seg + gb + 15) & ~size_t(15);
     L->o_chunk = (L->o_spans + sb + 15) & ~size_t(15);
     L->hb = L->o_chunk + cb;
+    PinBuf& h_plan = h_plan_s[plan_slot];
     CHK(h_plan.ensure(L->hb + 64));
     CHK(d_plan.ensure(L->hb));
     uint8_t* hd = h_plan.as<uint8_t>();
@@ -1636,7 +1661,7 @@ struct clg_engine {
   std::vector<uint32_t> chunk_buf;
   // Device half: upload, span table, tiles (expanded on the device from the runs).
   int enqueue_plan(const DecodePlan& p, const PlanLayout& L, DevBuf& dtiles) {
-    HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(d_plan.p, h_plan_s[plan_slot].p, L.hb, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_spans.p, d_plan.as<uint8_t>() + L.o_spans, L.sb, hipMemcpyDeviceToDevice, stream));
     if (!p.runs.empty()) {
       CHK(clg::launch_expand_tiles(reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + L.o_runs),
@@ -1717,8 +1742,7 @@ struct clg_engine {
       }
     }
     if (settling && own_wait() && out->out_kind == CLG_MEM_DEVICE) {
-      HIPCHK(hipStreamSynchronize(stream));
-      collect_timings(true);
+      collect_timings(true);  // (finish_fused waited for the run's read-back, which follows emit)
     } else {
       CHK(sync());
     }
@@ -1760,6 +1784,22 @@ struct clg_engine {
     CHK(launch_fused(p, log_bytes, out, jser, &r));
     return finish_fused(p, r, out, span_rec_base, aborted, need_jser);
   }
+  // Records and wide rows per span from the read-back span_hi words (hz[ns + s], packed
+  // wide << 31 | records): spans hold consecutive record ranges in span order, so a span's
+  // range starts where the previous span with tiles ended.  span_rec_base[0 .. ns].
+  static void span_totals(const DecodePlan& p, const uint64_t* hz, uint64_t* span_rec_base, uint64_t* nrec,
+                          uint64_t* nwide) {
+    constexpr uint64_t kRecMask = (1ull << 31) - 1;
+    const uint32_t ns = uint32_t(p.spans.size());
+    uint64_t prev = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (span_rec_base) span_rec_base[s] = prev & kRecMask;
+      if (p.spans[s].n_tiles) prev = hz[ns + s];
+    }
+    if (span_rec_base) span_rec_base[ns] = prev & kRecMask;
+    *nrec = prev & kRecMask;
+    *nwide = prev >> 31;
+  }
   // more than 8 GiB in one batch: the offsets pass covers 2^20 tiles
   static bool fused_fits(const DecodePlan& p) { return p.n_tiles <= (1u << 20); }
 
@@ -1775,6 +1815,12 @@ struct clg_engine {
     clg::FusedCtl ctl{};
     clg::DecodeOut o{};
     bool span_local = false;
+    // its decode slot (read-back buffer, staged plan, jser arena note), and for a queued
+    // decode the event after its read-back, which its completion waits for (not the stream:
+    // a later decode may be queued behind it)
+    uint32_t slot = 0;
+    hipEvent_t done = nullptr;
+    int note() const { return slot ? int(1 + slot) : 0; }
   };
   FusedRun zlast;  // the last finished fast run
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
@@ -1793,6 +1839,11 @@ struct clg_engine {
     if (chunked) count_chunks(p, G, tiny, chunk_buf);
     PlanLayout L;
     hsub.emplace(this, "host_launch_stage");
+    struct SlotScope {  // stage_plan / enqueue_plan use this run's slot
+      uint32_t& s;
+      SlotScope(uint32_t& s_, uint32_t v) : s(s_) { s = v; }
+      ~SlotScope() { s = 0; }
+    } slot_scope(plan_slot, r->slot);
     CHK(stage_plan(p, d_ztiles, &L, chunked ? &chunk_buf : nullptr));
     hsub.emplace(this, "host_launch_enqueue");
     clg::DecodeOut o{};
@@ -1801,11 +1852,13 @@ struct clg_engine {
     // abort[8] rep[2] (u32); bits apart.  st_x, ex and rep_flag are zeroed per batch.
     const size_t nbk = (size_t(nt) + 1023) / 1024, fw = (size_t(nt) + 7) / 8;
     const size_t o_cnt = 2 * size_t(nt) + fw;
-    const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), words = o_ab + 5;
+    const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), o_lb = o_ab + 5;
+    const size_t words = o_lb + 1 + nbk;  // (the one-launch scan's ticket and look-back words)
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
     CHK(d_zerr.ensure(std::max<size_t>(1, ns) * 8));
+    PinBuf& h_zres = h_zres_s[r->slot];
     CHK(h_zres.ensure((2 * size_t(ns) + 5) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
@@ -1836,6 +1889,9 @@ struct clg_engine {
     ctl.ex = w + nt;
     ctl.rep_flag = reinterpret_cast<uint8_t*>(w + 2 * size_t(nt));
     ctl.rep = ab + 8;
+    ctl.lb = w + o_lb;
+    ctl.h_res = h_zres.as<uint64_t>();  // the scan writes the result here: no read-back copy
+    memset(h_zres.p, 0, (2 * size_t(ns) + 5) * 8);  // (a batch without tiles runs no scan)
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -1847,28 +1903,53 @@ struct clg_engine {
     // unchanged.  Split into parts whose count ran beside the previous part's emit on a second
     // stream it was slower: config 2 0.44 -> 0.46 / 0.53 ms in 2 / 4 parts.)
     auto enqueue = [&](hipEvent_t* ev, hipEvent_t* evp) -> int {
-      CHK(enqueue_plan(p, L, d_ztiles));
+      // the plan up in one copy, then one launch for the set-up: tiles from the runs, the span
+      // table, and the zeroed control words (st_x, ex, rep_flag; abort words and repair
+      // counters; bad-span flags; kept-error offsets ~0; the jser work counters)
+      HIPCHK(hipMemcpyAsync(d_plan.p, h_plan_s[plan_slot].p, L.hb, hipMemcpyHostToDevice, stream));
+      {
+        clg::PrepArgs pa{};
+        const bool runs = !p.runs.empty();
+        pa.runs = reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + L.o_runs);
+        pa.n_runs = uint32_t(p.runs.size());
+        pa.n_tiles = runs ? nt : 0;
+        pa.segtab = reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_seg);
+        pa.pool = pool;
+        pa.C = C();
+        pa.U = p.unit;
+        pa.tiles = d_ztiles.as<clg::TileDesc>();
+        const size_t nsw = std::max<size_t>(1, ns);
+        pa.r[0] = clg::PrepRange{d_spans.as<uint32_t>(), reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_spans),
+                                 L.sb / 4, 0, 0};
+        pa.r[1] = clg::PrepRange{reinterpret_cast<uint32_t*>(w), nullptr, o_cnt * 2, 0, 0};
+        pa.r[2] = clg::PrepRange{ab, nullptr, 10 + 2 * (1 + nbk), 0, 0};  // abort words, repair counters, look-back
+        pa.r[3] = clg::PrepRange{d_zbad.as<uint32_t>(), nullptr, nsw, 0, 0};
+        pa.r[4] = clg::PrepRange{d_zerr.as<uint32_t>(), nullptr, keep_errors ? nsw * 2 : 0, 0xFFFFFFFFu, 0};
+        pa.r[5] = clg::PrepRange{jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, jser ? 2u : 0u, 0, 0};
+        pa.r[6] = clg::PrepRange{d_ztiles.as<uint32_t>(), reinterpret_cast<const uint32_t*>(d_plan.p), runs ? 0 : L.tb / 4, 0, 0};
+        CHK(clg::launch_decode_prep(pa, stream));
+      }
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
-      if (jser) HIPCHK(hipMemsetAsync(d_zjwork.p, 0, 8, stream));  // work items, overflow entries
-      HIPCHK(hipMemsetAsync(w, 0, o_cnt * 8, stream));  // st_x, ex, rep_flag
-      HIPCHK(hipMemsetAsync(ab, 0, 40, stream));                // abort words, repair counters
-      HIPCHK(hipMemsetAsync(d_zbad.p, 0, std::max<size_t>(1, ns) * 4, stream));
-      if (keep_errors) HIPCHK(hipMemsetAsync(d_zerr.p, 0xFF, std::max<size_t>(1, ns) * 8, stream));  // ~0: none
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
       if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
-      for (int ph : {3, 0, 1, 2}) {  // jser tables, count, offsets, emit
+      for (int ph : {3, 0, 5, 2}) {  // jser tables, count, offsets (one launch), emit
         if (ph == 3 && !jser) continue;
-        const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 1 ? 2 : 3;
+        const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 5 ? 2 : 3;
         if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
         CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, uint32_t(ph)));
         if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
       }
       if (evp) HIPCHK(hipEventRecord(evp[1], stream));
-      // read the span ranges and abort words (emit ran right behind the scan: it returns at
-      // once when the batch aborted, and its stores are bounded by the output capacity)
-      HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 5) * 8, hipMemcpyDeviceToHost, stream));
-      if (jser) CHK(jarena_note(0));
+      // the span ranges and abort words are in h_zres already (the scan wrote them; emit ran
+      // right behind it: it returns at once when the batch aborted, and its stores are bounded
+      // by the output capacity)
+      if (jser) CHK(jarena_note(r->note()));
+      if (r->slot) {
+        if (!zdone[r->slot]) HIPCHK(hipEventCreateWithFlags(&zdone[r->slot], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(zdone[r->slot], stream));
+        r->done = zdone[r->slot];
+      }
       return CLG_OK;
     };
     hipEvent_t ev[8] = {}, evp[2] = {};
@@ -1899,10 +1980,11 @@ struct clg_engine {
     const bool jser = r.jser, zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
     const uint64_t log_bytes = r.log_bytes;
     hipEvent_t ea = r.ea, eb = r.eb;
-    uint64_t* hz = h_zres.as<uint64_t>();
+    uint64_t* hz = h_zres_s[r.slot].as<uint64_t>();
     {
       HostTimer hw(this, "host_decode_wait");
-      HIPCHK(hipStreamSynchronize(stream));
+      if (r.done) HIPCHK(hipEventSynchronize(r.done));  // (a later decode may be queued behind it)
+      else HIPCHK(hipStreamSynchronize(stream));
     }
     HostTimer ht(this, "host_decode_finish");
     if (const char* prof_path = getenv("CLONOS_SCAN_PHASES")) {
@@ -1916,7 +1998,7 @@ struct clg_engine {
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[9]) stats["decode_chunk_repair"].launches += hab[9];  // repair requests the count pass served
-    const bool spilled = jser && jarena_spilled(0);  // a stream walk found the spill arena full
+    const bool spilled = jser && jarena_spilled(r.note());  // a stream walk found the spill arena full
     if (spilled) CHK(jarena_grow());
     // Serializable tables: the overflow arena or the walker's work list was full (reason 6)
     bool grown = false;
@@ -1961,17 +2043,8 @@ struct clg_engine {
       }
       return CLG_OK;
     }
-    constexpr uint64_t kRecMask = (1ull << 31) - 1;
     uint64_t nrec = 0, nwide = 0;
-    const std::vector<clg::SpanDesc>& sp = p.spans;
-    for (uint32_t s = 0; s < ns; ++s) {
-      if (span_rec_base) span_rec_base[s] = nrec;
-      if (sp[s].n_tiles == 0) continue;
-      const uint64_t a = hz[s], b = hz[ns + s];
-      nrec += (b & kRecMask) - (a & kRecMask);
-      nwide += (b >> 31) - (a >> 31);
-    }
-    if (span_rec_base) span_rec_base[ns] = nrec;
+    span_totals(p, hz, span_rec_base, &nrec, &nwide);
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     // the pipeline's algorithmic bytes: log bytes read + the SoA rows
     if (r.pa) timings.push_back(PendingTiming{"decode_pipeline", r.pa, r.pb, log_bytes + 13 * nrec + 25 * nwide});
@@ -2014,12 +2087,15 @@ struct clg_engine {
       if (sd.n_tiles > max_tiles) return false;
     return true;
   }
-  // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered)
+  // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered, or
+  // its cap / wcap elements reach past its registered range -- the caller's staging path then)
   static bool mapped_outputs(const clg_decoded& out, clg::DecodeOut* o) {
     void* h[9] = {out.off, out.tag, out.v0, out.w_idx, out.w_rc, out.w_v1, out.w_var_off, out.w_var_len, out.w_sub};
+    const uint64_t c = std::max<uint64_t>(1, out.cap), w = std::max<uint64_t>(1, out.wcap);
+    const uint64_t n[9] = {c * 4, c, c * 8, w * 4, w * 4, w * 8, w * 4, w * 4, w};
     uintptr_t d[9];
     for (int i = 0; i < 9; ++i)
-      if (!(d[i] = clg_mapped_device_address(h[i]))) return false;
+      if (!(d[i] = clg_mapped_device_address(h[i], n[i]))) return false;
     if (o)
       *o = clg::DecodeOut{reinterpret_cast<uint32_t*>(d[0]), reinterpret_cast<uint8_t*>(d[1]), reinterpret_cast<int64_t*>(d[2]),
                           reinterpret_cast<uint32_t*>(d[3]), reinterpret_cast<int32_t*>(d[4]), reinterpret_cast<int64_t*>(d[5]),
@@ -2118,7 +2194,7 @@ struct clg_engine {
       ctl.prof = d_prof.as<uint64_t>();
     }
     std::optional<HostTimer> hsub(std::in_place, this, "host_small_submit");  // (CLONOS_HOST_PROF sub-stages)
-    if (!arg_plan) HIPCHK(hipMemcpyAsync(d_plan.p, h_plan.p, L.hb, hipMemcpyHostToDevice, stream));
+    if (!arg_plan) HIPCHK(hipMemcpyAsync(d_plan.p, h_plan_s[0].p, L.hb, hipMemcpyHostToDevice, stream));
     const bool timing = (cfg.flags & CLG_F_TIMING) != 0;
     hipEvent_t ea = nullptr, eb = nullptr;
     if (timing) {
@@ -2366,20 +2442,13 @@ struct clg_engine {
     const clg::DecodeOut sc{s_off, s_tag, s_v0, s_widx, s_wrc, s_wv1, s_wvo, s_wvl, s_wsub, RC, WC};
     CHK(clg::launch_sf_place(reinterpret_cast<const clg::SfPlace*>(d_sf_meta.as<uint8_t>() + o_place), nb, sc, zlast.o,
                              ctl, stream));
-    uint64_t* hz = h_zres.as<uint64_t>();
+    CHK(h_zres_s[0].ensure((2 * size_t(ns) + 5) * 8));
+    uint64_t* hz = h_zres_s[0].as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     if (reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns))[0]) return CLG_OK;  // (cannot happen) whole batch
-    constexpr uint64_t kRecMask = (1ull << 31) - 1;
     uint64_t tr = 0, tw = 0;
-    for (uint32_t s = 0; s < ns; ++s) {
-      if (span_rec_base) span_rec_base[s] = tr;
-      if (pf.spans[s].n_tiles == 0) continue;
-      const uint64_t a = hz[s], b = hz[ns + s];
-      tr += (b & kRecMask) - (a & kRecMask);
-      tw += (b >> 31) - (a >> 31);
-    }
-    if (span_rec_base) span_rec_base[ns] = tr;
+    span_totals(pf, hz, span_rec_base, &tr, &tw);
     *done = true;
     CHK(finish_out(out, tr, tw));
     if (e_status != CLG_OK) {
@@ -2424,52 +2493,140 @@ struct clg_engine {
   // that needs the engine exclusively (see ENGINE_GUARD), so a pending decode never sees
   // its inputs change.  Slices into device memory on the gather stream and consumer seeks
   // leave it pending: they only read log segments and move consumer offsets.
+  // Up to CLG_DECODE_MAX_INFLIGHT decodes are queued at once, each with its own slot (read-
+  // back words, staged plan, completion event), so decode i+1's kernels are on the stream
+  // before the host completes decode i and the GPU never waits for the host in between.
+  // The device scratch (control words, bitmaps, tables) is shared and stream-ordered: the
+  // fast path of decode i only needs its read-back.  A decode whose fast run aborted while a
+  // later one was already queued has lost its scratch to that one, so it is decoded again
+  // from its plan builder, and so are the later ones (rare: they may share its outputs).
   struct PendingDecode {
-    bool active = false;
+    bool active = false;  // queued on the GPU, not yet completed
+    bool redo = false;    // its fast run's scratch is void: decode again when completed
     DecodePlan plan;
     FusedRun run;
+    uint64_t log_bytes = 0;
     clg_decoded* out = nullptr;
     uint64_t* span_rec_base = nullptr;
     std::function<void(DecodePlan&, uint32_t)> build;
-    bool unwaited = false;  // queued by clg_decode_logs_async, status not yet taken by clg_decode_wait
-    int status = CLG_OK;  // result of the last settled decode, for clg_decode_wait
+    int status = CLG_OK;  // its result, for the clg_decode_wait that pairs with it
     std::string err;      // and its error text
-  } pend;
+  };
+  std::deque<PendingDecode> pq;  // queued by clg_decode_logs_async, not yet waited for (oldest first)
+  // the largest queued plan so far (the scratch is sized for it): a larger one is queued only
+  // once nothing is in flight, since growing a buffer frees the one the GPU may still read
+  uint64_t hw_tiles = 0, hw_spans = 0, hw_runs = 0, hw_segs = 0;
+  bool hw_jser = false;
 
+  bool any_active(size_t from = 0) const {
+    for (size_t i = from; i < pq.size(); ++i)
+      if (pq[i].active) return true;
+    return false;
+  }
+  // A decode the async call completed at once (not queued): its status goes to the wait.
+  // Engine failures (not a decode result) return from the call instead, with nothing queued.
+  int push_settled(int st, clg_decoded* out) {
+    if (st != CLG_OK && st != CLG_E_CAPACITY && out->err_status == CLG_OK) return st;
+    PendingDecode d;
+    d.status = st;
+    if (st != CLG_OK) d.err = g_err;
+    pq.push_back(std::move(d));
+    return CLG_OK;
+  }
   int decode_async(std::function<void(DecodePlan&, uint32_t)> build, uint64_t log_bytes, clg_decoded* out,
                    uint64_t* span_rec_base) {
-    pend.status = CLG_OK;
-    if (!(fused_decode && log_bytes / 2 < (1ull << 31))) return decode(build, log_bytes, out, span_rec_base);
+    const bool fast = fused_decode && log_bytes / 2 < (1ull << 31);
     DecodePlan pf;
-    build(pf, clg::kZTile);
+    if (fast) build(pf, clg::kZTile);
+    const bool queue = fast && !pf.spans.empty() && fused_fits(pf);
+    // what the queued decodes' completions need must not be overwritten by this one's kernels:
+    // host outputs go through shared staging arrays, and a scratch buffer that has to grow
+    // frees the old one
+    bool clash = !queue;
+    for (const auto& d : pq)
+      if (d.active && d.out->out_kind != CLG_MEM_DEVICE) clash = true;
+    if (queue && (pf.n_tiles > hw_tiles || pf.spans.size() > hw_spans || pf.runs.size() > hw_runs ||
+                  pf.segtab.size() > hw_segs || (jser_hint && !hw_jser)))
+      clash = true;
+    if (clash) CHK(settle());
+    if (!queue) {  // nothing to queue, or too large for the fast path: decoded now
+      if (fast && pf.spans.empty()) {
+        reset_result(out);
+        return push_settled(CLG_OK, out);
+      }
+      return push_settled(decode(build, log_bytes, out, span_rec_base), out);
+    }
     reset_result(out);
-    if (pf.spans.empty()) return CLG_OK;
-    if (!fused_fits(pf)) return decode(build, log_bytes, out, span_rec_base);
+    uint32_t slot = 1;  // a slot no queued decode holds
+    for (; slot < kSlots; ++slot) {
+      bool used = false;
+      for (const auto& d : pq)
+        if (d.active && d.run.slot == slot) used = true;
+      if (!used) break;
+    }
+    if (slot == kSlots) return fail(CLG_E_STATE, "no free decode slot");  // (cannot happen: bounded by the caller)
     FusedRun r;
+    r.slot = slot;
     CHK(launch_fused(pf, log_bytes, out, jser_hint, &r));
-    pend.active = true;
-    pend.unwaited = true;
-    pend.plan = std::move(pf);
-    pend.run = r;
-    pend.out = out;
-    pend.span_rec_base = span_rec_base;
-    pend.build = std::move(build);
+    hw_tiles = std::max<uint64_t>(hw_tiles, pf.n_tiles);
+    hw_spans = std::max<uint64_t>(hw_spans, pf.spans.size());
+    hw_runs = std::max<uint64_t>(hw_runs, pf.runs.size());
+    hw_segs = std::max<uint64_t>(hw_segs, pf.segtab.size());
+    hw_jser = hw_jser || r.jser;
+    PendingDecode d;
+    d.active = true;
+    d.plan = std::move(pf);
+    d.run = r;
+    d.log_bytes = log_bytes;
+    d.out = out;
+    d.span_rec_base = span_rec_base;
+    d.build = std::move(build);
+    pq.push_back(std::move(d));
     return CLG_OK;
   }
 
-  int settle() {
-    if (!pend.active) return CLG_OK;
-    pend.active = false;
-    bool aborted = false, need_jser = false;
-    settling = true;
-    int st = finish_fused(pend.plan, pend.run, pend.out, pend.span_rec_base, &aborted, &need_jser);
-    settling = false;
-    if (st == CLG_OK && aborted)
-      st = after_abort(pend.plan, pend.build, pend.run.log_bytes, pend.out, pend.span_rec_base, need_jser);
-    pend.status = st;
-    if (st != CLG_OK) pend.err = g_err;
-    pend.build = nullptr;
-    return CLG_OK;  // the decode's own status goes to clg_decode_wait
+  // Completes the queued decodes [0, upto] (all: upto = SIZE_MAX), oldest first.
+  int settle(size_t upto = SIZE_MAX) {
+    for (size_t i = 0; i < pq.size() && i <= upto; ++i) {
+      PendingDecode& d = pq[i];
+      if (!d.active) continue;
+      d.active = false;
+      int st;
+      if (d.redo) {  // a decode before it aborted after this one was queued
+        CHK(sync());
+        st = decode(d.build, d.log_bytes, d.out, d.span_rec_base);
+      } else {
+        bool aborted = false, need_jser = false;
+        settling = true;
+        st = finish_fused(d.plan, d.run, d.out, d.span_rec_base, &aborted, &need_jser);
+        settling = false;
+        if (st == CLG_OK && aborted) {
+          if (any_active(i + 1)) {  // its scratch went to the later decodes: all of them again
+            stats["decode_async_redo"].launches++;
+            CHK(sync());
+            for (size_t j = i + 1; j < pq.size(); ++j)
+              if (pq[j].active) pq[j].redo = true;
+            st = decode(d.build, d.log_bytes, d.out, d.span_rec_base);
+          } else {
+            st = after_abort(d.plan, d.build, d.log_bytes, d.out, d.span_rec_base, need_jser);
+          }
+        }
+      }
+      d.status = st;
+      if (st != CLG_OK) d.err = g_err;
+      d.build = nullptr;
+      d.plan = DecodePlan();
+    }
+    return CLG_OK;  // the decodes' own statuses go to clg_decode_wait
+  }
+  // clg_decode_wait: the oldest queued decode, completed; its status
+  int wait_oldest(std::string* err) {
+    if (pq.empty()) return CLG_OK;
+    CHK(settle(0));
+    const int st = pq.front().status;
+    if (st != CLG_OK) *err = pq.front().err;
+    pq.pop_front();
+    return st;
   }
 
   // The robust pipeline; again with a grown spill arena while a Serializable stream walk
@@ -2723,17 +2880,20 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   if (const char* ja = getenv("CLONOS_JSER_ARENA"))  // initial spill arena bytes (tests: force its growth)
     e->jarena_bytes = std::max<size_t>(256, size_t(strtoull(ja, nullptr, 0)));
   HIPCHK(hipSetDevice(cfg->device));
-  HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   {
     // The device-output slice gather (HBM-bound) runs beside the next decode (VALU-bound):
     // its queue gets the higher priority so its workgroups are dispatched first
-    // (CLONOS_GATHER_PRIO=0: same priority as the decode stream).
+    // (CLONOS_GATHER_PRIO=0: same priority as the decode stream; 2: the decode stream's
+    // queue higher instead, so the decode's short set-up, scan and read-back launches do not
+    // wait behind the gather's workgroups).
     const char* gp = getenv("CLONOS_GATHER_PRIO");
+    const int mode = gp ? atoi(gp) : 1;
     int lo = 0, hi = 0;
-    if (!(gp && !strcmp(gp, "0")) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-      HIPCHK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, hi));
-    else
-      HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+    const bool prio = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo;
+    if (prio && mode == 2) HIPCHK(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, hi));
+    else HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (prio && mode == 1) HIPCHK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, hi));
+    else HIPCHK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
   }
   HIPCHK(hipEventCreateWithFlags(&e->gready, hipEventDisableTiming));
   const size_t pool_bytes = size_t(cfg->segment_bytes) * cfg->pool_segments;
@@ -2771,6 +2931,8 @@ void clg_engine_destroy(clg_engine* e) {
     hipEventDestroy(t.b);
   }
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  for (auto ev : e->zdone)
+    if (ev) hipEventDestroy(ev);
   if (e->pool_alloc) hipFree(e->pool_alloc);
   if (e->ifl_alloc) hipFree(e->ifl_alloc);
   hipStreamDestroy(e->stream);
@@ -3271,12 +3433,12 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
 
 int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
                           clg_decoded* out, uint64_t* span_rec_base) {
-  ENGINE_GUARD(e);
+  ENGINE_GUARD_KEEP(e);  // (the queued decodes stay queued)
   if (!out || (n && (!log || !start_epoch))) return fail(CLG_E_INVALID_ARG, "null argument");
-  // one decode per wait: a second one would overwrite the first one's status
-  if (e->pend.unwaited)
-    return fail(CLG_E_STATE, "the previous asynchronous decode was not waited for (clg_decode_wait)");
-  CHK(e->flush());
+  // every queued decode's status is kept for its wait
+  if (e->pq.size() >= CLG_DECODE_MAX_INFLIGHT)
+    return fail(CLG_E_STATE, "%d asynchronous decodes are not waited for (clg_decode_wait)", CLG_DECODE_MAX_INFLIGHT);
+  CHK(e->flush());  // (stream-ordered after the queued decodes, past their ranges)
   std::vector<uint32_t> hs(log, log + n);
   std::vector<int32_t> st(n), nb(n);
   uint64_t total = 0;
@@ -3298,11 +3460,9 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
 
 int clg_decode_wait(clg_engine* e) {
   ENGINE_GUARD_KEEP(e);
-  e->settle();
-  const int st = e->pend.status;
-  e->pend.status = CLG_OK;
-  e->pend.unwaited = false;
-  return st == CLG_OK ? CLG_OK : fail(st, "%s", e->pend.err.c_str());
+  std::string err;
+  const int st = e->wait_oldest(&err);
+  return st == CLG_OK ? CLG_OK : fail(st, "%s", err.c_str());
 }
 
 int clg_replay_prep(clg_engine* e, const uint64_t* key, const uint8_t* bytes, const uint64_t* off, const uint64_t* len,

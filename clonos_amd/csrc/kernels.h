@@ -236,6 +236,13 @@ struct FusedCtl {
   // with jwork[1]; exhausted: abort reason 6, the host grows the arena and runs again).
   uint32_t* jbase;
   uint32_t jovf_cap;
+  // The one-launch scan (phase 5, k_decode_scan): lb[0] a ticket counter, lb[1 + b] block b's
+  // look-back word (1 << 62 | its total, then 1 << 63 | its inclusive prefix); all zeroed per
+  // batch.  h_res: host memory the host reads the batch's result from -- span_hi at
+  // [n_spans + s], the abort words as u32 at [2 n_spans] -- written by that kernel, so no
+  // read-back copy is queued (null: none).
+  uint64_t* lb;
+  uint64_t* h_res;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile in LDS (more: the overflow arena)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
@@ -331,6 +338,27 @@ int launch_expand_pieces(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_pi
                          const uint8_t* pool, uint32_t seg_bytes, GatherPiece* d_out, void* stream);
 int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_tiles, const uint32_t* d_segtab,
                         const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream);
+// The fast decode's set-up in one launch: n_tiles tiles expanded from the runs (as
+// k_expand_tiles; 0: none), then each word range r[] copied from src or filled with val.
+constexpr int kPrepRanges = 7;
+struct PrepRange {
+  uint32_t* dst;
+  const uint32_t* src;  // null: fill
+  uint64_t n;           // 32-bit words
+  uint32_t val;
+  uint32_t pad;
+};
+struct PrepArgs {
+  const SegSpan* runs;
+  uint32_t n_runs, n_tiles;
+  const uint32_t* segtab;
+  const uint8_t* pool;
+  uint32_t C, U;
+  TileDesc* tiles;
+  uint64_t total;  // (set by the launcher)
+  PrepRange r[kPrepRanges];
+};
+int launch_decode_prep(PrepArgs a, void* stream);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);

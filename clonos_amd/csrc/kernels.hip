@@ -21,22 +21,8 @@
 namespace clg {
 
 // ==================================================================================
-// Append scatter: one wave per chunk.
-// ==================================================================================
-__global__ __launch_bounds__(256) void k_scatter(const ScatterChunk* __restrict__ chunks, uint32_t n,
-                                                 const uint8_t* __restrict__ src) {
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t c = wave; c < n; c += nwaves) {
-    const ScatterChunk ch = chunks[c];
-    for (uint32_t i = lane; i < ch.len; i += 64) ch.dst[i] = src[ch.src + i];
-  }
-}
-
-// ==================================================================================
-// Gather (delta slice): one block per piece; destination-aligned 16-byte chunks, the
-// source realigned in registers with v_alignbyte (shift is uniform per piece).
+// Byte-range copies (gather pieces, scatter chunks): destination-aligned 16-byte chunks, the
+// source realigned in registers with v_alignbyte (the shift is uniform per range).
 // ==================================================================================
 __device__ __forceinline__ uint32_t fsh(uint32_t hi, uint32_t lo, uint32_t s) {
   return s ? __builtin_amdgcn_alignbyte(hi, lo, s) : lo;
@@ -52,41 +38,45 @@ __device__ __forceinline__ uint4 funnel16(const uint4 lo, const uint4 hi, uint32
   }
 }
 
-// Each thread takes up to kGatherK destination chunks (256 threads apart) and issues all
-// their source loads before any store.  Chunks that straddle the piece's ends are written
-// byte by byte from the same registers (no dependent loads).  Source reads may touch up to
-// 16 bytes either side of the piece's source range: the pool has guard bytes both ends.
-constexpr int kGatherK = 4;
+// [src, src + len) -> [dst, dst + len) by NT threads (tid 0..NT-1).  Each thread takes up to
+// kCopyK destination chunks (NT apart) and issues all their source loads before any store.
+// Chunks that straddle the range's ends are written byte by byte from the same registers (no
+// dependent loads).  A source load is issued only for an aligned 16-byte word that holds a
+// byte of the range, so it never leaves the pages the range lies on (a caller's buffer ending
+// at an unmapped page is safe).
+constexpr int kCopyK = 4;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
-  const GatherPiece p = pieces[blockIdx.x];
-  if (p.len == 0) return;
-  const uintptr_t d0 = (uintptr_t)(out + p.dst), d1 = d0 + p.len;
+template <uint32_t NT>
+__device__ __forceinline__ void copy_range(const uint8_t* src, uint8_t* dst, uint32_t len, uint32_t tid) {
+  if (len == 0) return;
+  const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + len;
   const uintptr_t a0 = d0 & ~(uintptr_t)15;
-  const uintptr_t sdelta = (uintptr_t)p.src - d0;  // src address = dst address + sdelta
+  const uintptr_t sdelta = (uintptr_t)src - d0;  // src address = dst address + sdelta
+  const uintptr_t s0 = (uintptr_t)src, s1 = s0 + len;
   const uint32_t m = (uint32_t)(sdelta & 15);
   const uint32_t nch = (uint32_t)((((d1 + 15) & ~(uintptr_t)15) - a0) >> 4);
-  for (uint32_t j0 = 0; j0 < nch; j0 += kGatherK * 256) {
-    uint4 lo[kGatherK], hi[kGatherK];
+  for (uint32_t j0 = 0; j0 < nch; j0 += kCopyK * NT) {
+    uint4 lo[kCopyK], hi[kCopyK];
 #pragma unroll
-    for (int k = 0; k < kGatherK; ++k) {
-      const uint32_t j = j0 + threadIdx.x + 256u * (uint32_t)k;
+    for (int k = 0; k < kCopyK; ++k) {
+      const uint32_t j = j0 + tid + NT * (uint32_t)k;
+      lo[k] = hi[k] = make_uint4(0, 0, 0, 0);
       if (j < nch) {
         const uintptr_t sa = (a0 + 16u * (uintptr_t)j + sdelta) & ~(uintptr_t)15;
-        lo[k] = *reinterpret_cast<const uint4*>(sa);
-        if (m) hi[k] = *reinterpret_cast<const uint4*>(sa + 16);
+        if (sa + 16 > s0 && sa < s1) lo[k] = *reinterpret_cast<const uint4*>(sa);
+        if (m && sa + 32 > s0 && sa + 16 < s1) hi[k] = *reinterpret_cast<const uint4*>(sa + 16);
       }
     }
 #pragma unroll
-    for (int k = 0; k < kGatherK; ++k) {
-      const uint32_t j = j0 + threadIdx.x + 256u * (uint32_t)k;
+    for (int k = 0; k < kCopyK; ++k) {
+      const uint32_t j = j0 + tid + NT * (uint32_t)k;
       if (j < nch) {
         const uintptr_t c = a0 + 16u * (uintptr_t)j;
         const uint4 v = m ? funnel16(lo[k], hi[k], m) : lo[k];
         if (c >= d0 && c + 16 <= d1) {
           const u32x4 nv = {v.x, v.y, v.z, v.w};
           __builtin_nontemporal_store(nv, reinterpret_cast<u32x4*>(c));
-        } else {  // piece edge: the bytes inside [d0, d1)
+        } else {  // range edge: the bytes inside [d0, d1)
           const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int x = 0; x < 16; ++x)
@@ -95,6 +85,33 @@ __global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ 
       }
     }
   }
+}
+
+// ==================================================================================
+// Append scatter: one wave per chunk (chunks are at most one segment; config 4's are
+// mostly a few hundred bytes), 16-byte stores.
+// ==================================================================================
+__global__ __launch_bounds__(256) void k_scatter(const ScatterChunk* __restrict__ chunks, uint32_t n,
+                                                 const uint8_t* __restrict__ src) {
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t c = wave; c < n; c += nwaves) {
+    const ScatterChunk ch = chunks[c];
+    copy_range<64>(src + ch.src, ch.dst, ch.len, lane);
+  }
+}
+
+// ==================================================================================
+// Gather (delta slice): one block per piece.
+// ==================================================================================
+__global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ pieces, uint8_t* __restrict__ out) {
+  // blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one; speed only, never
+  // correctness): XCD x takes a contiguous range of pieces, so a request's consecutive
+  // pieces (one source run, one destination run) stay in one L2
+  const uint32_t nb = gridDim.x, b = blockIdx.x, q = nb >> 3, rm = nb & 7u, x = b & 7u;
+  const GatherPiece p = pieces[x * q + (x < rm ? x : rm) + (b >> 3)];
+  copy_range<256>(p.src, out + p.dst, p.len, threadIdx.x);
 }
 
 // ==================================================================================
@@ -122,12 +139,9 @@ __global__ __launch_bounds__(256) void k_expand_pieces(const SegSpan* __restrict
   out[g] = GatherPiece{pool + (size_t)segtab[r.segtab_off + w] * C + (s0 - w * C), r.dst + (s0 - r.phys), e1 - s0, 0};
 }
 
-__global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict__ spans, uint32_t n_spans,
-                                                      uint32_t n_tiles, const uint32_t* __restrict__ segtab,
-                                                      const uint8_t* __restrict__ pool, uint32_t C, uint32_t U,
-                                                      TileDesc* __restrict__ out) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_tiles) return;
+__device__ __forceinline__ void expand_tile(const SegSpan* __restrict__ spans, uint32_t n_spans,
+                                            const uint32_t* __restrict__ segtab, const uint8_t* __restrict__ pool,
+                                            uint32_t C, uint32_t U, TileDesc* __restrict__ out, uint32_t g) {
   const SegSpan r = spans[find_run(spans, n_spans, g)];
   const uint32_t w = r.phys / U + (g - r.first);
   const uint32_t s0 = w * U > r.phys ? w * U : r.phys;
@@ -135,6 +149,37 @@ __global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict_
   const uint32_t si = s0 / C, so = s0 % C;
   out[g] = TileDesc{pool + (size_t)segtab[r.segtab_off + si] * C + (so & ~15u), so & 15u, e1 - s0, (uint32_t)r.dst, 0,
                     (uint64_t)(s0 - r.phys)};
+}
+__global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict__ spans, uint32_t n_spans,
+                                                      uint32_t n_tiles, const uint32_t* __restrict__ segtab,
+                                                      const uint8_t* __restrict__ pool, uint32_t C, uint32_t U,
+                                                      TileDesc* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_tiles) expand_tile(spans, n_spans, segtab, pool, C, U, out, g);
+}
+
+// The fast decode's set-up in one launch (it was a device copy, the tile expansion and four
+// or five memsets, each a few microseconds of launch on the decode's critical path): item i
+// < n_tiles expands tile i from the runs, the rest walk the word ranges in order (a copy
+// where src is set, else a fill with val).
+__global__ __launch_bounds__(256) void k_decode_prep(PrepArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.total; i += stride) {
+    uint64_t k = i;
+    if (k < a.n_tiles) {
+      expand_tile(a.runs, a.n_runs, a.segtab, a.pool, a.C, a.U, a.tiles, (uint32_t)k);
+      continue;
+    }
+    k -= a.n_tiles;
+#pragma unroll
+    for (int r = 0; r < kPrepRanges; ++r) {
+      if (k < a.r[r].n) {
+        a.r[r].dst[k] = a.r[r].src ? a.r[r].src[k] : a.r[r].val;
+        break;
+      }
+      k -= a.r[r].n;
+    }
+  }
 }
 
 // ==================================================================================
@@ -757,6 +802,15 @@ int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_til
   if (!n_tiles) return CLG_OK;
   hipLaunchKernelGGL(k_expand_tiles, dim3((n_tiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_spans, n_spans,
                      n_tiles, d_segtab, pool, seg_bytes, unit, d_out);
+  return launch_status(hipGetLastError());
+}
+
+int launch_decode_prep(PrepArgs a, void* stream) {
+  a.total = a.n_tiles;
+  for (int r = 0; r < kPrepRanges; ++r) a.total += a.r[r].n;
+  if (!a.total) return CLG_OK;
+  const uint64_t want = (a.total + 255) / 256, blocks = want < 2048 ? want : 2048;
+  hipLaunchKernelGGL(k_decode_prep, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return launch_status(hipGetLastError());
 }
 

@@ -14,10 +14,11 @@ epoch, or per batch of buffers):
      (each receiving rank is one consumer of the log, with its own offset): the engine's
      batched hasDelta/getOffset/getDelta (clg_slice_batch), ONE device gather into a
      payload buffer grouped by destination;
-  2. three all-to-alls with per-destination split sizes (RCCL over xGMI with the "nccl"
-     backend; gloo on CPU): the (rows, bytes) counts of every rank pair, the header rows,
-     the payload.  A rank receives only the logs within its sharing depth (at depth 1 only
-     its direct producers'), and with one rank no collective runs;
+  2. two all-to-alls (RCCL over xGMI with the "nccl" backend; gloo on CPU): the header
+     rows, one per planned (log, destination) request, with static split sizes every rank
+     knows from the plan; then, after one read-back of the headers, the payload with the
+     split sizes they carry.  A rank receives only the logs within its sharing depth (at
+     depth 1 only its direct producers'), and with one rank no collective runs;
   3. every rank applies the received rows with the batched processUpstreamDelta
      (clg_upstream_delta_batch) reading straight from the receive buffer in HBM.  The dedup
      rule of ThreadCausalLogImpl.java:117-154 makes re-delivery harmless.
@@ -113,6 +114,12 @@ class ReplicationPlan:
         self.req_gid = np.concatenate(per_dest).astype(np.int64) if world else np.zeros(0, np.int64)
         self.req_dest = np.repeat(np.arange(world, dtype=np.int64), [len(p) for p in per_dest])
         self.n_to = np.array([len(p) for p in per_dest], np.int64)  # requests per destination
+        # header rows every other rank sends here (one per its planned request for this rank):
+        # static, so the header all-to-all needs no count exchange first
+        mine_needed = need[rank][lv]
+        src_of = owner[lv]
+        self.n_from = np.array([int(((src_of == r) & mine_needed).sum()) if r != rank else 0 for r in range(world)],
+                               np.int64)
 
 
 class EngineIO:
@@ -172,10 +179,10 @@ class Replicator:
     that is sent; replicas of the wanted logs are opened here.
 
     One exchange moves each destination only the logs it wants: the slices of all requests
-    land in one payload buffer grouped by destination (one batched slice), and three
-    collectives carry them -- an all-to-all of (rows, bytes) per destination pair, an
-    all-to-all of the header rows and an all-to-all of the payload, each with per-destination
-    split sizes.  With one rank there is nothing to move and no collective runs."""
+    land in one payload buffer grouped by destination (one batched slice), and two
+    collectives carry them -- an all-to-all of the header rows (static split sizes: one row
+    per planned request) and an all-to-all of the payload (split sizes from the headers).
+    With one rank there is nothing to move and no collective runs."""
 
     def __init__(self, io, plan: ReplicationPlan, device, owned_handles: Dict[int, int], group=None):
         self.io, self.plan, self.device, self.group = io, plan, device, group
@@ -205,7 +212,8 @@ class Replicator:
 
     def build_payload(self, epoch: int, payload_cap: Optional[int] = None):
         """Slice every request into the payload buffer (grouped by destination).  Returns
-        (payload, header rows by destination, rows per destination, bytes per destination)."""
+        (payload, one header row per planned request -- len 0 where there is no delta --,
+        bytes per destination)."""
         import torch
         plan = self.plan
         nq = len(plan.req_gid)
@@ -219,60 +227,63 @@ class Replicator:
         bad = np.nonzero(res["status"])[0]
         if bad.size:
             check(int(res["status"][bad[0]]))
-        keep = np.nonzero((res["has_delta"] != 0) & (res["len"] > 0))[0]
-        dest = plan.req_dest[keep]
-        rows_to = np.bincount(dest, minlength=plan.world).astype(np.int64)
-        bytes_to = np.bincount(dest, weights=res["len"][keep], minlength=plan.world).astype(np.int64)
-        # each destination's payload starts where its first request's slice landed
+        ln = np.where(res["has_delta"] != 0, res["len"], 0).astype(np.int64)
+        # clg_slice_batch packs the slices back to back in request order (requests are grouped
+        # by destination), so each destination's part is contiguous; checked, not assumed
+        out_off = res["out_off"].astype(np.int64)
+        packed = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64) if nq else out_off
+        keep = ln > 0
+        if not np.array_equal(out_off[keep], packed[keep]):
+            raise RuntimeError("slice outputs are not packed in request order")
+        bytes_to = np.bincount(plan.req_dest, weights=ln, minlength=plan.world).astype(np.int64)
         start = np.concatenate([[0], np.cumsum(bytes_to)[:-1]]).astype(np.int64)
-        rows = np.zeros(len(keep), HEADER)
-        rows["gid"] = plan.req_gid[keep]
-        rows["offset_from_epoch"] = res["offset_from_epoch"][keep]
+        rows = np.zeros(nq, HEADER)
+        rows["gid"] = plan.req_gid
+        rows["offset_from_epoch"] = np.where(keep, res["offset_from_epoch"], 0)
         rows["epoch"] = epoch
-        rows["len"] = res["len"][keep]
-        rows["payload_off"] = res["out_off"][keep].astype(np.int64) - start[dest]  # within its destination's part
-        return self._payload, rows, rows_to, bytes_to
+        rows["len"] = ln
+        rows["payload_off"] = np.where(keep, packed - start[plan.req_dest], 0)  # within its destination's part
+        return self._payload, rows, bytes_to
 
     def exchange(self, epoch: int, payload_cap: Optional[int] = None) -> ExchangeStats:
-        """One replication round for `epoch` (all ranks call it together)."""
+        """One replication round for `epoch` (all ranks call it together): two all-to-alls
+        and one read-back.  The header rows go first with STATIC split sizes (one row per
+        planned request, ReplicationPlan.n_to / n_from, so no count exchange precedes them);
+        their read-back gives the payload's split sizes and the apply requests; then the
+        payload."""
         import torch
         import torch.distributed as dist
         st = ExchangeStats()
         plan = self.plan
         if plan.world == 1:
             return st
-        payload, rows, rows_to, bytes_to = self.build_payload(epoch, payload_cap)
+        payload, rows, bytes_to = self.build_payload(epoch, payload_cap)
         backend = dist.get_backend(self.group)
         dev = self.device if backend == "nccl" else "cpu"
-        # 1. (rows, bytes) for every destination pair
-        mine = torch.from_numpy(np.stack([rows_to, bytes_to], 1).reshape(-1).copy()).to(dev)
-        theirs = torch.empty_like(mine)
-        dist.all_to_all_single(theirs, mine, group=self.group)
-        got = theirs.cpu().numpy().reshape(plan.world, 2)
-        rows_from, bytes_from = got[:, 0], got[:, 1]
-        st.sent_bytes = int(rows_to.sum()) * HEADER.itemsize + int(bytes_to.sum())
-        st.recv_bytes = int(rows_from.sum()) * HEADER.itemsize + int(bytes_from.sum())
-        # 2. header rows
+        # 1. header rows, static splits
         hsend = torch.from_numpy(rows.view(np.uint8).copy()).to(dev)
-        hrecv = torch.empty(int(rows_from.sum()) * HEADER.itemsize, dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(hrecv, hsend, output_split_sizes=(rows_from * HEADER.itemsize).tolist(),
-                               input_split_sizes=(rows_to * HEADER.itemsize).tolist(), group=self.group)
-        # 3. payload
+        hrecv = torch.empty(int(plan.n_from.sum()) * HEADER.itemsize, dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(hrecv, hsend, output_split_sizes=(plan.n_from * HEADER.itemsize).tolist(),
+                               input_split_sizes=(plan.n_to * HEADER.itemsize).tolist(), group=self.group)
+        rr = hrecv.cpu().numpy().view(HEADER)  # the one read-back (it also orders the host after the collective)
+        src_rank = np.repeat(np.arange(plan.world), plan.n_from)
+        bytes_from = np.bincount(src_rank, weights=rr["len"].astype(np.int64), minlength=plan.world).astype(np.int64)
+        st.sent_bytes = int(rows_sent(rows)) * HEADER.itemsize + int(bytes_to.sum())
+        st.recv_bytes = int(rows_sent(rr)) * HEADER.itemsize + int(bytes_from.sum())
+        # 2. payload
         nrecv = int(bytes_from.sum())
         recv = torch.empty(max(nrecv, 1) + BLOB_ALIGN, dtype=torch.uint8, device=dev)
         psend = _to_comm(payload[:int(bytes_to.sum())], backend)
         dist.all_to_all_single(recv[:nrecv], psend, output_split_sizes=bytes_from.tolist(),
                                input_split_sizes=bytes_to.tolist(), group=self.group)
-        # the header read-back also orders the host after the collectives
-        rr = hrecv.cpu().numpy().view(HEADER)
-        if not len(rr):
+        live = rr["len"] > 0
+        if not live.any():
             return st
         src_start = np.concatenate([[0], np.cumsum(bytes_from)[:-1]]).astype(np.uint64)
-        src_rank = np.repeat(np.arange(plan.world), rows_from)
         src = src_start[src_rank] + rr["payload_off"].astype(np.uint64)
         h = self.replica_handle[rr["gid"]]
-        want = h >= 0
-        st.skipped = int((~want).sum())
+        want = live & (h >= 0)
+        st.skipped = int((live & (h < 0)).sum())
         n = int(want.sum())
         if n:
             req = np.zeros(n, DELTA_REQ)
@@ -290,6 +301,11 @@ class Replicator:
             st.applied = n
             st.applied_bytes = int(req["len"].sum())
         return st
+
+
+def rows_sent(rows: np.ndarray) -> int:
+    """Header rows that carry a delta (the rest are the static slots of requests with none)."""
+    return int((rows["len"] > 0).sum())
 
 
 # ---- replay-prep merge across GPUs ---------------------------------------------------------

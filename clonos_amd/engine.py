@@ -10,6 +10,7 @@ exception: CorruptDeterminantArrayException, RuntimeException("Consumer went bac
 """
 from __future__ import annotations
 
+import collections
 import ctypes as C
 import mmap
 import sys
@@ -20,7 +21,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple, Union
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib
+from ._lib import ClonosError, check, lib
 from . import determinants as D
 
 ChannelLike = Union[Tuple[int, int], int]
@@ -156,6 +157,7 @@ class Engine:
         self.async_slice = async_slice
         self.device = device
         self._logs = {}
+        self._queued = collections.deque()  # queued asynchronous decodes, oldest first (clg_decode_wait is FIFO)
 
     # ---- lifecycle ----------------------------------------------------------------
     def close(self):
@@ -514,7 +516,9 @@ class Engine:
         return None
 
     def decode_logs_async(self, logs: Sequence["ThreadCausalLog"], start_epochs: Sequence[int]) -> "PendingDecode":
-        """clg_decode_logs_async into host arrays: returns at once; .wait() gives the batch."""
+        """clg_decode_logs_async into host arrays: returns at once; .wait() gives the batch.
+        Up to CLG_DECODE_MAX_INFLIGHT may be queued; their waits complete them in queue order
+        (waiting for a later one first completes the earlier ones, whose results are kept)."""
         h = np.array([l.handle for l in logs], np.uint32)
         ep = np.array(start_epochs, np.int64)
         total = self.log_lengths(h)[1]
@@ -525,6 +529,7 @@ class Engine:
         if st != _lib.CLG_OK:
             self._slot_done(arrs)
             check(st)
+        self._queued.append(pd)
         return pd
 
     def decode_logs_device(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
@@ -536,15 +541,21 @@ class Engine:
     def decode_logs_device_async(self, handles: np.ndarray, start_epochs: np.ndarray, dec: _lib.Decoded,
                                  base: np.ndarray) -> None:
         """clg_decode_logs_async: queues the decode and returns; `dec`, `base` and the output
-        arrays stay untouched by the caller until decode_wait()."""
-        self._pending = (handles, start_epochs, dec, base)  # kept alive until the wait
+        arrays stay untouched by the caller until the decode_wait() that pairs with it (FIFO;
+        up to CLG_DECODE_MAX_INFLIGHT queued, each with its own outputs)."""
+        keep = (handles, start_epochs, dec, base)  # kept alive until the wait
         check(lib.clg_decode_logs_async(self._h, _np_ptr(handles), _np_ptr(start_epochs), len(handles),
                                         C.byref(dec), _np_ptr(base)))
+        self._queued.append(keep)
 
     def decode_wait(self) -> None:
-        """clg_decode_wait: completes a pending asynchronous decode and raises its error."""
+        """clg_decode_wait: completes the oldest queued asynchronous decode and raises its error."""
+        if self._queued and isinstance(self._queued[0], PendingDecode):
+            self._queued[0].wait()
+            return
         st = lib.clg_decode_wait(self._h)
-        self._pending = None
+        if self._queued:
+            self._queued.popleft()
         check(st)
 
     # ---- piggybacked deltas (AbstractDeltaSerializerDeserializer) ---------------------------
@@ -645,15 +656,38 @@ class Engine:
 
 
 class PendingDecode:
-    """A queued clg_decode_logs_async; holds the output arrays until wait()."""
+    """A queued clg_decode_logs_async; holds the output arrays until wait().  The engine
+    completes its queued decodes in order (clg_decode_wait is FIFO): waiting for this one
+    first waits for the ones queued before it, whose results (or errors) they keep."""
 
     def __init__(self, engine: "Engine", keep, n_spans: int):
         self._e, self._keep, self._n = engine, keep, n_spans
+        self._done = False
+        self._res = None  # (result, exception)
+
+    def _complete(self) -> None:
+        q = self._e._queued
+        assert q and q[0] is self
+        st = lib.clg_decode_wait(self._e._h)
+        q.popleft()
+        self._done = True
+        _, _, d, arrs, base = self._keep
+        try:
+            self._res = (self._e._finish(st, d, arrs, base, self._n, None), None)
+        except ClonosError as ex:
+            self._res = (None, ex)
 
     def wait(self) -> DecodedBatch:
-        st = lib.clg_decode_wait(self._e._h)
-        _, _, d, arrs, base = self._keep
-        return self._e._finish(st, d, arrs, base, self._n, None)
+        while not self._done:
+            head = self._e._queued[0]
+            if isinstance(head, PendingDecode):
+                head._complete()
+            else:  # an earlier device-output decode: its status is its own caller's to take
+                raise RuntimeError("an earlier decode_logs_device_async is not waited for (decode_wait)")
+        res, ex = self._res
+        if ex is not None:
+            raise ex
+        return res
 
 
 class ThreadCausalLog:

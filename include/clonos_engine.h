@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CLG_ABI_VERSION 5
+#define CLG_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -287,17 +287,22 @@ int clg_decode_host(clg_engine* e, const uint8_t* bytes, const uint64_t* span_of
 int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
                     clg_decoded* out, uint64_t* span_rec_base);
 /* Asynchronous clg_decode_logs: returns once the decode is queued on the engine stream, so
- * the caller can plan and queue other work (e.g. the slices of the same step) while it
- * runs.  `out`, its arrays and span_rec_base must stay valid, and are not to be read, until
- * clg_decode_wait returns, which completes the decode (fallback paths included) and
- * returns its status.  Every other call that needs the engine exclusively completes a
- * pending decode first (its status is then kept for clg_decode_wait); clg_slice_batch into
- * device memory with CLG_F_ASYNC_SLICE and the consumer seeks leave it pending. */
+ * the caller can plan and queue other work (e.g. the slices of the same step, or the next
+ * batch's decode) while it runs.  `out`, its arrays and span_rec_base must stay valid, and
+ * are not to be read, until the clg_decode_wait that pairs with this call returns, which
+ * completes the decode (fallback paths included) and returns its status.  Every other call
+ * that needs the engine exclusively completes the pending decodes first (their statuses are
+ * kept for clg_decode_wait); clg_slice_batch into device memory with CLG_F_ASYNC_SLICE and
+ * the consumer seeks leave them pending.
+ * Up to CLG_DECODE_MAX_INFLIGHT decodes may be queued before the first is waited for, so the
+ * GPU runs decode i+1 while the host completes decode i; give each its own output arrays.
+ * One more is CLG_E_STATE (no decode's status is ever dropped). */
+#define CLG_DECODE_MAX_INFLIGHT 2
 int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* start_epoch, uint32_t n,
                           clg_decoded* out, uint64_t* span_rec_base);
-/* Completes the pending decode and returns ITS status.  One asynchronous decode at a time:
- * clg_decode_logs_async before the previous one was waited for is CLG_E_STATE (so no
- * decode's error is ever overwritten by the next one's). */
+/* Completes the OLDEST decode clg_decode_logs_async queued and not yet waited for, and
+ * returns ITS status (FIFO: one wait per queued decode, in queue order).  A later decode
+ * still running on the GPU is not waited for.  With nothing queued: CLG_OK. */
 int clg_decode_wait(clg_engine* e);
 
 /* ---- replay-prep (DeterminantResponseEvent.merge + LogReplayer decode) ----------------

@@ -76,7 +76,7 @@ public class EngineInFlightLog implements InFlightLog {
 		}
 		if (n > STAGE_BYTES) { // larger than the stage: a batch of its own
 			ByteBuffer direct = nio.isDirect() ? nio.slice() : ByteBuffer.allocateDirect(n).put(nio.duplicate());
-			submit(new long[]{epochID}, new int[]{n}, direct, 1);
+			check(submit(new long[]{epochID}, new int[]{n}, direct, 1));
 			return;
 		}
 		stage.put(nio.duplicate());
@@ -90,9 +90,18 @@ public class EngineInFlightLog implements InFlightLog {
 		if (staged == 0) {
 			return;
 		}
-		submit(stagedEpochs, stagedLens, stage, staged);
-		stage.clear();
-		staged = 0;
+		int st = submit(stagedEpochs, stagedLens, stage, staged);
+		if (accepted(st)) { // logged (CLG_E_STATE too: every buffer was appended first), so never again
+			stage.clear();
+			staged = 0;
+		}
+		check(st);
+	}
+
+	/** The engine appended the batch: CLG_OK, or CLG_E_STATE (spillable log() while replaying
+	 *  without an iterator, :98-99, after the buffers were appended). */
+	private static boolean accepted(int st) {
+		return st == CLG_OK || st == CLG_E_STATE;
 	}
 
 	private void awaitNoSubmit() {
@@ -116,7 +125,11 @@ public class EngineInFlightLog implements InFlightLog {
 	// subpartitions one after another on one thread (EpochTrackerImpl.java:140-142), so the
 	// notifier must not wait for this batch: the truncation it records is applied here, once
 	// the batch is accepted.
-	private void submit(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
+	// The batch's arrays and bytes are the live stage while it waits (wait() releases the
+	// monitor): nothing else touches them until it returns (log() and flush() wait for the
+	// submit, notifyCheckpointComplete leaves the stage to pendingTruncation).  Returns the
+	// engine's status; the caller clears what was accepted, then raises.
+	private int submit(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
 		submitting = true;
 		try {
 			int st;
@@ -128,11 +141,14 @@ public class EngineInFlightLog implements InFlightLog {
 			}
 			long cp = pendingTruncation;
 			pendingTruncation = Long.MIN_VALUE;
-			if (cp != Long.MIN_VALUE && (st == CLG_OK || st == CLG_E_STATE)) {
+			if (cp != Long.MIN_VALUE && accepted(st)) {
 				// the batch was logged before the notification: its epochs below cp go too
-				check(nIflNotifyCheckpointComplete(engine.handle(), ifl, cp));
+				int tst = nIflNotifyCheckpointComplete(engine.handle(), ifl, cp);
+				if (st == CLG_OK) {
+					st = tst;
+				}
 			}
-			check(st); // CLG_E_STATE: spillable log() while replaying without an iterator (:98-99, NPE)
+			return st; // CLG_E_STATE: spillable log() while replaying without an iterator (:98-99, NPE)
 		} finally {
 			submitting = false;
 			notifyAll();
@@ -146,10 +162,13 @@ public class EngineInFlightLog implements InFlightLog {
 		notifyAll();
 		// staged buffers of truncated epochs never reach HBM; a batch waiting for space right now
 		// is truncated by submit() once it is accepted (the reference truncates every buffer
-		// logged before the notification)
-		dropStagedBelow(checkpointId);
+		// logged before the notification).  While a batch is submitted the stage IS that batch
+		// (or empty: a large buffer goes alone after a flush), and submit() still reads its
+		// arrays and bytes, so it is left alone: pendingTruncation covers it
 		if (submitting) {
 			pendingTruncation = Math.max(pendingTruncation, checkpointId);
+		} else {
+			dropStagedBelow(checkpointId);
 		}
 	}
 

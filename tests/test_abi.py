@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
 
 def test_abi_version_and_struct_sizes():
     from clonos_amd import _lib
-    assert _lib.lib.clg_abi_version() == 5
+    assert _lib.lib.clg_abi_version() == 6
     assert ctypes.sizeof(_lib.IflReplayRes) == 48
     assert ctypes.sizeof(_lib.IflReplayReq) == 24
     assert ctypes.sizeof(_lib.CausalLogIdC) == 24
@@ -37,6 +37,8 @@ def test_abi_version_and_struct_sizes():
     assert ctypes.sizeof(_lib.DeltaReq) == 32
     assert ctypes.sizeof(_lib.Decoded) == 136
     assert ctypes.sizeof(_lib.KernelStat) == 56
+    hdr = open(os.path.join(ROOT, "include", "clonos_engine.h")).read()
+    assert re.search(r"#define CLG_DECODE_MAX_INFLIGHT (\d+)", hdr).group(1) == str(_lib.CLG_DECODE_MAX_INFLIGHT)
 
 
 def test_kernels_built_for_gfx950():

@@ -157,20 +157,123 @@ def test_repeated_shapes_new_bytes_no_timing():
                 lg.close()
 
 
-def test_second_async_before_wait_is_refused():
-    """Two asynchronous decodes back to back, the first failing: the second is refused
-    (CLG_E_STATE) instead of overwriting the first one's status, which the wait returns."""
+def test_third_async_before_wait_is_refused():
+    """Decodes queued back to back, the first failing: up to CLG_DECODE_MAX_INFLIGHT are
+    accepted, the next is refused (CLG_E_STATE) instead of dropping a status, and the waits
+    return each decode's own status in queue order."""
     rng = np.random.default_rng(4)
     good = synth.random_log(500, rng, allow_serializable=False)
     bad = bytes(good) + bytes([0x7F, 1, 2, 3])
+    assert _lib.CLG_DECODE_MAX_INFLIGHT == 2
     with Engine(segment_bytes=256, pool_segments=1 << 12) as eng:
         logs = logs_of(eng, [good, bad])
         pd = eng.decode_logs_async(logs, [1, 1])
-        with pytest.raises(ClonosError) as second:
+        pd2 = eng.decode_logs_async(logs[:1], [1])
+        with pytest.raises(ClonosError) as third:
             eng.decode_logs_async(logs[:1], [1])
-        assert second.value.status == _lib.CLG_E_STATE
+        assert third.value.status == _lib.CLG_E_STATE
         with pytest.raises(ClonosError) as first:
             pd.wait()
         assert first.value.status == _lib.CLG_E_CORRUPT_TAG and first.value.err_span == 1
+        assert pd2.wait().n_rec == len(O.decode(good)[1]["tag"])
         got = eng.decode_logs_async(logs[:1], [1]).wait()  # waited for: the next one is accepted
         assert got.n_rec == len(O.decode(good)[1]["tag"])
+
+
+def test_later_wait_completes_earlier_host_decodes():
+    """Waiting for the second of two queued decodes first: the first is completed on the way
+    and keeps its own result (and error) for its own wait."""
+    rng = np.random.default_rng(14)
+    a = [synth.random_log(int(rng.integers(100, 2000)), rng, allow_serializable=False) for _ in range(5)]
+    bad = bytes(a[0]) + bytes([0x7F, 1])
+    with Engine(segment_bytes=512, pool_segments=1 << 13) as eng:
+        logs = logs_of(eng, a + [bad])
+        p1 = eng.decode_logs_async(logs[5:], [1])
+        p2 = eng.decode_logs_async(logs[:5], [1] * 5)
+        check_oracle(p2.wait(), a)
+        with pytest.raises(ClonosError) as e1:
+            p1.wait()
+        assert e1.value.status == _lib.CLG_E_CORRUPT_TAG and e1.value.err_off == len(a[0])
+
+
+class DevOut:
+    """Caller-owned device output arrays (the bench's layout) and their clg_decoded."""
+
+    def __init__(self, cap, wcap):
+        self.t = [torch.empty(cap, dtype=torch.int32, device="cuda"), torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                  torch.empty(cap, dtype=torch.int64, device="cuda")]
+        self.w = [torch.empty(wcap, dtype=t, device="cuda") for t in
+                  (torch.int32, torch.int32, torch.int64, torch.int32, torch.int32, torch.uint8)]
+        d = self.dec = _lib.Decoded()
+        d.off, d.tag, d.v0 = [x.data_ptr() for x in self.t]
+        d.w_idx, d.w_rc, d.w_v1, d.w_var_off, d.w_var_len, d.w_sub = [x.data_ptr() for x in self.w]
+        d.cap, d.wcap, d.out_kind = cap, wcap, _lib.CLG_MEM_DEVICE
+        self.base = None
+
+    def check(self, ref):
+        torch.cuda.synchronize()
+        n, nw = int(self.dec.n_rec), int(self.dec.n_wide)
+        assert n == len(ref.tag) and nw == len(ref.w_idx)
+        np.testing.assert_array_equal(self.t[0][:n].cpu().numpy(), ref.off)
+        np.testing.assert_array_equal(self.t[1][:n].cpu().numpy(), ref.tag)
+        np.testing.assert_array_equal(self.t[2][:n].cpu().numpy(), ref.v0)
+        for x, f in zip(self.w, ("w_idx", "w_rc", "w_v1", "w_var_off", "w_var_len", "w_sub")):
+            np.testing.assert_array_equal(x[:nw].cpu().numpy(), getattr(ref, f), err_msg=f)
+        np.testing.assert_array_equal(self.base, ref.span_rec_base)
+
+
+@pytest.mark.parametrize("mix", ["config2", "config3"])
+def test_two_in_flight_device_outputs(mix):
+    """The pipelined bench step: decode i+1 queued (with its own device outputs) before
+    decode i is waited for, slices gathered on the second stream in between; every decode
+    equals the synchronous one (and the oracle), including a batch whose first fast run
+    aborts for want of Serializable tables while the next one is already queued (both are
+    decoded again: the redo path)."""
+    rng = np.random.default_rng(31)
+    if mix == "config2":
+        blobs = [synth.config2_log(int(rng.integers(5000, 40000)), rng)[0] for _ in range(9)]
+    else:
+        blobs = [synth.config3_epoch(int(rng.integers(2000, 6000)), rng, 0)[0] for _ in range(5)]
+    with Engine(segment_bytes=16384, pool_segments=1 << 12, async_slice=True, timing=True) as eng:
+        logs = logs_of(eng, blobs)
+        n = len(logs)
+        total = sum(int(b.size) for b in blobs)
+        sets = [DevOut(total // 2 + n + 1, total // 6 + n + 1) for _ in range(2)]
+        h = np.array([lg.handle for lg in logs], np.uint32)
+        groups = [h, h[::-1].copy(), h[: n // 2 + 1].copy()]  # batches of other shapes and orders
+        creq = (_lib.SliceReq * n)()
+        cres = (_lib.SliceRes * n)()
+        for i, lg in enumerate(logs):
+            creq[i].log, creq[i].consumer, creq[i].epoch = lg.handle, _lib.ChannelId(7, i), 1
+        sl = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+        refs = [eng.decode_logs([logs[int(np.nonzero(h == x)[0][0])] for x in g], [1] * len(g)) for g in groups]
+        if mix == "config3":  # a fresh engine state for the abort: the table hint off again
+            eng.close()
+            eng = Engine(segment_bytes=16384, pool_segments=1 << 12, async_slice=True, timing=True)
+            logs = logs_of(eng, blobs)
+            h2 = np.array([lg.handle for lg in logs], np.uint32)
+            groups = [h2[[int(np.nonzero(h == x)[0][0]) for x in g]] for g in groups]
+            for i, lg in enumerate(logs):
+                creq[i].log = lg.handle
+        queued = []
+        for k in range(7):
+            g = groups[k % 3]
+            so = sets[k % 2]
+            if len(queued) == 2:
+                j, o = queued.pop(0)
+                eng.decode_wait()
+                o.check(refs[j % 3])
+            so.base = np.zeros(len(g) + 1, np.uint64)
+            eng.decode_logs_device_async(g, np.ones(len(g), np.int64), so.dec, so.base)
+            queued.append((k, so))
+            eng.seek_consumers_raw(creq, np.zeros(n, np.int32), n)
+            assert eng.slice_batch_raw(creq, cres, n, sl.data_ptr(), sl.numel(), device=True) == total
+        while queued:
+            j, o = queued.pop(0)
+            eng.decode_wait()
+            o.check(refs[j % 3])
+        eng.sync()
+        assert sl[:total].cpu().numpy().tobytes() == b"".join(bytes(b) for b in blobs)
+        if mix == "config3":
+            assert eng.kernel_stats().get("decode_async_redo", {}).get("launches", 0) >= 1
+        eng.close()
