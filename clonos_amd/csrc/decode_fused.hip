@@ -658,23 +658,63 @@ __device__ __forceinline__ SpecR lm_spec_walk_pair(const uint32_t* M, uint32_t w
                    [&](uint32_t q, uint64_t& sh, uint64_t& wh) { return lm_step(M, q, sh, wh); });
 }
 
+// ---------------------------------------------------------------------------------
+// The lean speculative walk (FusedCtl::lean; batches without tables whose records are
+// almost all fixed-length, as config 2's Order / Timestamp): the warm-up's rule in the
+// region too -- fixed-length tags followed, anything else (wide tags included) one byte --
+// so a step has no branch for wide records, and the starts go into four 32-bit words (a
+// 32-bit shift and OR instead of a 64-bit shift and two ORs).  Its chain has no wide
+// records: a wide record on it is a skip, which spec_bad puts before the merge's meeting
+// point, so the true walk (full rules) crosses every wide record of the region itself and
+// the result is the same; only its cost grows with wide records, which is why the host
+// turns it off for batches that hold many (engine.cpp lean_hint).
+// ---------------------------------------------------------------------------------
+template <bool SAFE>
+__device__ __forceinline__ SpecR lean_walk(const uint32_t* T, uint32_t ws, uint32_t rs, uint32_t re, uint32_t end_a,
+                                           uint32_t r0) {
+  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
+  uint32_t q = ws;
+  while (q < rs) q += warm_len(zb8(T, q));
+  s.first = q;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t lim = re < r0 + 32u * (uint32_t)(k + 1) ? re : r0 + 32u * (uint32_t)(k + 1);
+    uint32_t b = 0;
+    while (q < lim) {
+      constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
+      constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
+      uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
+      if (!SAFE) L = q + L <= end_a ? L : 0u;
+      b |= 1u << (q & 31u);
+      q += L > 1u ? L : 1u;
+    }
+    w[k] = b;
+  }
+  s.sb.lo = (uint64_t)w[0] | (uint64_t)w[1] << 32;
+  s.sb.hi = (uint64_t)w[2] | (uint64_t)w[3] << 32;
+  s.exit = q;
+  s.bad = spec_bad(s, r0);
+  return s;
+}
+
 #ifndef CLG_SPEC_PAIR_CHECK
 #define CLG_SPEC_PAIR_CHECK 0  // developer check: every paired walk against the single one (printf)
 #endif
 template <bool J>
 __device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair);
+                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair, bool lean);
 #if CLG_SPEC_PAIR_CHECK
 __device__ uint32_t g_pair_mismatch;
 #endif
 template <bool J>
 __device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                uint32_t end_a, uint32_t r0, const JL& jl) {
+                                                uint32_t end_a, uint32_t r0, const JL& jl, bool lean = false) {
   // pairs where the region reaches well into its high half
   const bool pair = CLG_SPEC_PAIR && rs < r0 + 64u && re >= r0 + 80u;
 #if CLG_SPEC_PAIR_CHECK
-  const SpecR a = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair);
-  const SpecR b = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, false);
+  const SpecR a = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair, false);
+  const SpecR b = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, false, false);
   if (a.sb.lo != b.sb.lo || a.sb.hi != b.sb.hi || a.wb.lo != b.wb.lo || a.wb.hi != b.wb.hi || a.first != b.first ||
       a.exit != b.exit || a.bad != b.bad) {
     if (atomicAdd(&g_pair_mismatch, 1u) < 8u)
@@ -683,13 +723,14 @@ __device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, 
   }
   return b;
 #else
-  return spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair);
+  return spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair, lean);
 #endif
 }
 template <bool J>
 __device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair) {
+                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair, bool lean) {
   if (J && jl.lm) return pair ? lm_spec_walk_pair(jl.lm, ws, wsb, rs, re, r0) : lm_spec_walk(jl.lm, ws, rs, re, r0);
+  if (!J && lean) return re + 16u <= end_a ? lean_walk<true>(T, ws, rs, re, end_a, r0) : lean_walk<false>(T, ws, rs, re, end_a, r0);
   // lanes whose records cannot run past the span end (all but the last tile's) skip the test
   if (re + 16u <= end_a)
     return pair ? spec_walk_pair<J, true>(T, ws, wsb, rs, re, end_a, r0, jl) : spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl);
@@ -783,6 +824,87 @@ __device__ __forceinline__ Res merge_walk_r(const uint32_t* T, uint32_t re, uint
     *Lp = L;
     return true;
   });
+}
+
+// The true chain of a batch without tables (merge_walk_r<false>'s result) in a tight loop:
+// the fixed-length tags (Order, Timestamp, RNG, BufferBuilt) by one byte-permute lookup, and
+// ONE exit test per step for the three things that end the fast loop -- the chain met the
+// speculative one (at or past its last skip), a tag that needs the full rule (wide, invalid,
+// Serializable: length 0 in the table), a record past the span end.  The full rule then
+// takes that one record (merge_walk_r's step) and the loop goes on.  merge_walk_r's nested
+// rare branches cost about twice the VALU and SALU of this loop per step (the count pass's
+// ISA), and the merges are the count pass's second-largest phase after the speculative walk.
+#ifndef CLG_LEAN_MERGE
+#define CLG_LEAN_MERGE 1  // 0: lean batches merge with merge_walk_r (A/B)
+#endif
+__device__ __forceinline__ Res merge_walk_lean(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
+                                               const SpecR& s) {
+  Res r{{0, 0}, {0, 0}, e, 0, 0, 0};
+  if (e >= re) return r;
+  const uint32_t r0 = (re - 1u) & ~(kZRegion - 1u);
+  uint32_t p = e, why = 0;
+  Bits pb{0, 0}, pw{0, 0};
+  // 0: reached lim, 1: met the speculative chain, 2: an invalid record
+  auto run = [&](uint64_t sbw, uint64_t& pbw, uint64_t& pww, uint32_t lim) -> uint32_t {
+    while (p < lim) {
+      constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
+      constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
+      const uint32_t b = p & 63u;
+      const uint64_t m = 1ull << b;
+      const bool conv = (sbw & m) != 0ull && p >= s.bad;
+      const uint32_t tg = zb8(T, p);
+      const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
+      if (conv || L == 0u || p + L > end_a) {
+        if (conv) return 1u;
+        // the full rule for this record (merge_walk_r's step)
+        int v;
+        uint32_t y = 1u;
+        if (tg >= 8u) {
+          v = (int)kLenErr;
+        } else if (tg == CLG_TAG_SERIALIZABLE) {
+          v = (int)kLenErr;
+          y = zbe32(T, p + 1) == 0xACED0005u ? 2u : 1u;
+        } else if (L) {  // a fixed-length record past the span end
+          v = (int)kLenErr;
+        } else {
+          v = tg == CLG_TAG_IGNORE_CHECKPOINT ? 13 : zlen_var(T, p, end_a, tg, 0);
+        }
+        if (v <= 0 || p + (uint32_t)v > end_a || p + (uint32_t)v < p) {
+          why = v <= 0 ? y : 1u;
+          return 2u;
+        }
+        pbw |= m;
+        pww |= m;
+        p += (uint32_t)v;
+        ++r.steps;
+        continue;
+      }
+      pbw |= m;
+      p += L;
+      ++r.steps;
+    }
+    return 0u;
+  };
+  const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
+  uint32_t st = run(s.sb.lo, pb.lo, pw.lo, mid);
+  if (st == 0u) st = run(s.sb.hi, pb.hi, pw.hi, re);
+  if (st == 1u) {
+    const uint32_t i = p & 127u;
+    r.bm = bor(pb, bge(s.sb, i));
+    r.wb = bor(pw, bge(s.wb, i));
+    r.exit = s.exit;
+  } else if (st == 2u) {
+    r.bad = why;
+    r.exit = s.exit;
+    r.bm = pb;  // the true starts before the failing record
+    r.wb = pw;
+    r.fail = p;
+  } else {
+    r.bm = pb;
+    r.wb = pw;
+    r.exit = p;
+  }
+  return r;
 }
 
 // ---------------------------------------------------------------------------------
@@ -1241,7 +1363,10 @@ __device__ __forceinline__ uint32_t warm_start(uint32_t rs, uint32_t lo, uint32_
   // parity) and, walking at similar speeds, keep colliding.  The stagger's dword offsets
   // spread them: (lane >> 1) & 15 with the parity gives 32 banks (config-2 count 0.165 ->
   // 0.153 ms against lane & 7's 8 banks; tools/ab.sh), at 30 B more warm-up on average.
-  const uint32_t st = CLG_WARM_STAGGER == 1 ? ((lane >> 1) & 15u) : CLG_WARM_STAGGER == 2 ? ((lane >> 1) & 7u) : (lane & 7u);
+  // (3: (lane >> 1) & 31, every lane's first read on its own bank, at 30 B more warm-up again)
+  const uint32_t st = CLG_WARM_STAGGER == 1 ? ((lane >> 1) & 15u)
+                      : CLG_WARM_STAGGER == 2 ? ((lane >> 1) & 7u)
+                      : CLG_WARM_STAGGER == 3 ? ((lane >> 1) & 31u) : (lane & 7u);
   const uint32_t w = (warm & kZWarmFlat) ? (warm & ~kZWarmFlat) : (kZPad == 0 ? warm + 4u * st : warm);
   return rs >= lo + w ? rs - w : lo;
 }
@@ -1269,7 +1394,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   // the chunk prologue's walk of this same tile, a function of the tile's bytes only)
   const uint32_t ws = warm_start(rs, lo, ctl.warm, lane), wsb = warm_start(lane * kZRegion + 64u, lo, ctl.warm, lane);
   const SpecR sp = walked ? *walked
-                          : rs < re ? spec_walk_fast<J>(s_img, ws, wsb, rs, re, end_a, lane * kZRegion, jl)
+                          : rs < re ? spec_walk_fast<J>(s_img, ws, wsb, rs, re, end_a, lane * kZRegion, jl, ctl.lean != 0u)
                                     : SpecR{{0, 0}, {0, 0}, rs, rs, 0};
 
   ZPHASE(2);
@@ -1282,6 +1407,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   auto merge = [&](uint32_t from) -> Res {
     if (rs >= re) return Res{{0, 0}, {0, 0}, from, 0, 0, 0};
     if (J && jl.lm) return merge_walk_lm(s_img, re, end_a, from, sp, jl, g);
+    if (!J && CLG_LEAN_MERGE && ctl.lean) return merge_walk_lean(s_img, re, end_a, from, sp);
     return merge_walk_r<J>(s_img, re, end_a, from, sp, jl);
   };
   Res r = merge(entry);
@@ -2207,7 +2333,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       else if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
       const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane);
       const uint32_t wsb = warm_start(lane * kZRegion + 64u, z.lo, ctl.warm, lane);
-      sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl)
+      sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl, ctl.lean != 0u)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
       x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
       if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));

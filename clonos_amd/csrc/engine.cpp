@@ -559,6 +559,14 @@ struct clg_engine {
   DevBuf d_zbad;                     // fast decode: per-span "chain went wrong" flags
   DevBuf d_sf_meta, d_sf_rec, d_sf_wide;  // per-span fallback: bad-span list, robust outputs
   bool jser_hint = false;            // the last batches held Serializable records: build tables first
+  // The count pass's lean speculative walk (decode_fused.hip lean_walk) while the last fast
+  // decode's records were almost all fixed-length (wide rows under 1/16): its result is the
+  // same either way, its cost grows with wide records.  CLONOS_LEAN=0/1 forces it (developer).
+  bool lean_hint = true;
+  static int lean_env() {
+    static const int v = getenv("CLONOS_LEAN") ? atoi(getenv("CLONOS_LEAN")) : -1;
+    return v;
+  }
   DevBuf d_rmeta, d_rsizes;          // replay-prep: subpartition span tables / BufferBuilt sizes
   DevBuf d_encin, d_encw, d_encout;  // encode: staged host input, block prefixes, host-output staging
   DevBuf d_hdr;                      // piggyback: delta headers staged for the gather
@@ -1890,6 +1898,7 @@ struct clg_engine {
     ctl.rep_flag = reinterpret_cast<uint8_t*>(w + 2 * size_t(nt));
     ctl.rep = ab + 8;
     ctl.lb = w + o_lb;
+    ctl.lean = !jser && (lean_env() >= 0 ? lean_env() != 0 : lean_hint) ? 1u : 0u;
     ctl.h_res = h_zres.as<uint64_t>();  // the scan writes the result here: no read-back copy
     memset(h_zres.p, 0, (2 * size_t(ns) + 5) * 8);  // (a batch without tiles runs no scan)
     r->ctl = ctl;
@@ -2045,6 +2054,7 @@ struct clg_engine {
     }
     uint64_t nrec = 0, nwide = 0;
     span_totals(p, hz, span_rec_base, &nrec, &nwide);
+    if (!jser) lean_hint = nwide * 16 < nrec;
     if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     // the pipeline's algorithmic bytes: log bytes read + the SoA rows
     if (r.pa) timings.push_back(PendingTiming{"decode_pipeline", r.pa, r.pb, log_bytes + 13 * nrec + 25 * nwide});
@@ -2073,18 +2083,22 @@ struct clg_engine {
   DevBuf d_small;
   clg::SmallPlanArg small_arg;
   bool small_flip = false;
+  // Tiles per span the single launch takes: its wave counts and emits a span's tiles one
+  // after another, so a span of 6 tiles (config 5's 45 KB main logs) is a chain of six tile
+  // walks on one wave while the three-pass path spreads them over the GPU (config 1's logs
+  // are one tile).  CLONOS_SMALL_MAXTILES (read at engine creation) overrides: tuning, tests.
+  const uint32_t small_max_tiles = [] {
+    const char* v = getenv("CLONOS_SMALL_MAXTILES");
+    return std::min<uint32_t>(v ? uint32_t(atoi(v)) : 2u, clg::kZSmallTiles);
+  }();
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
         p.only)
       return false;
     if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
-    static const uint32_t max_tiles = [] {  // tuning aid: tiles per span the single launch takes
-      const char* v = getenv("CLONOS_SMALL_MAXTILES");
-      return v ? std::min<uint32_t>(uint32_t(atoi(v)), clg::kZSmallTiles) : clg::kZSmallTiles;
-    }();
     for (const auto& sd : p.spans)
-      if (sd.n_tiles > max_tiles) return false;
+      if (sd.n_tiles > small_max_tiles) return false;
     return true;
   }
   // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered, or

@@ -243,6 +243,7 @@ struct FusedCtl {
   // read-back copy is queued (null: none).
   uint64_t* lb;
   uint64_t* h_res;
+  uint32_t lean;  // batches without tables: the lean speculative walk (wide tags step one byte)
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile in LDS (more: the overflow arena)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan

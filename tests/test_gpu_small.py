@@ -12,6 +12,12 @@ from test_gpu_decode import assert_span_equal
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _small_up_to_8_tiles(monkeypatch):
+    """These tests hold spans of up to 8 tiles on the single launch (the default takes 2)."""
+    monkeypatch.setenv("CLONOS_SMALL_MAXTILES", "8")
+
+
 def _eng(**kw):
     return Engine(segment_bytes=kw.pop("segment_bytes", 16384), pool_segments=4096, timing=True, **kw)
 
@@ -201,3 +207,30 @@ def test_pooled_capacity_exceeded_is_decoded_again_sized():
         assert_span_equal(dec, 0, data[lids[0]] + big)
         for s, l in enumerate(lids[1:], 1):
             assert_span_equal(dec, s, data[l])
+
+
+def test_multi_tile_spans_default_to_three_pass(monkeypatch):
+    """By default the single launch takes spans of at most 2 tiles: a batch of 16 config-2
+    logs of ~45 KB (config 5's failed main logs, 6 tiles each) goes three-pass -- one wave
+    per span would walk its six tiles in a row -- with the same result."""
+    monkeypatch.delenv("CLONOS_SMALL_MAXTILES")
+    rng = np.random.default_rng(0xC5)
+    from clonos_amd import CausalLogID
+    with _eng() as eng:
+        bufs = [synth.config2_log(8000, rng)[0].tobytes() for _ in range(16)]
+        small = [synth.config2_log(900, rng)[0].tobytes() for _ in range(4)]  # <= 2 tiles each
+        logs = []
+        for i, b in enumerate(bufs + small):
+            lg = eng.open_log(CausalLogID.main(i))
+            lg.appendDeterminant(b, 0)
+            logs.append(lg)
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs(logs[:16], [0] * 16)
+        assert _launches(eng, "decode_small") == 0 and _launches(eng, "decode_count") == 1
+        for s, b in enumerate(bufs):
+            assert_span_equal(dec, s, b)
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs(logs[16:], [0] * 4)
+        assert _launches(eng, "decode_small") == 1
+        for s, b in enumerate(small):
+            assert_span_equal(dec, s, b)

@@ -52,6 +52,21 @@ def _raw_decode(eng, blob, spans):
             {k: v[:nr if k in ("off", "tag", "v0") else nw].copy() for k, v in arrs.items()}, base.copy())
 
 
+def check_spans_oracle(a, spans_b, key):
+    rec0, recs = a[8], a[7]
+    widx = recs["w_idx"].astype(np.int64)
+    for s, b in enumerate(spans_b):
+        st, rr, eo, _ = O.decode(b)
+        lo, hi = int(rec0[s]), int(rec0[s + 1])
+        assert hi - lo == len(rr["tag"]), (key, s, st)
+        for f in ("off", "tag", "v0"):
+            np.testing.assert_array_equal(recs[f][lo:hi], rr[f], err_msg=f"{key} span {s} {f}")
+        w = (widx >= lo) & (widx < hi)
+        np.testing.assert_array_equal(widx[w] - lo, rr["w_idx"].astype(np.int64), err_msg=f"{key} span {s} w_idx")
+        for f in ("w_rc", "w_v1", "w_var_off", "w_var_len", "w_sub"):
+            np.testing.assert_array_equal(recs[f][w], rr[f], err_msg=f"{key} span {s} {f}")
+
+
 @pytest.mark.parametrize("n_spans,every", [(60, 3), (600, 5)])
 def test_many_bad_spans_equal_robust(n_spans, every):
     rng = np.random.default_rng(n_spans)
@@ -90,14 +105,7 @@ def test_many_bad_spans_equal_robust(n_spans, every):
         for k in a[7]:
             np.testing.assert_array_equal(a[7][k], r[7][k], err_msg=f"{key} {k}")
         np.testing.assert_array_equal(a[8], r[8])
-    a = res["three_pass", "1"]
-    # every good span against the oracle
-    rec0 = a[8]
-    for s in range(0, n_spans, 7):
-        if s in bad:
-            continue
-        st, rr, _, _ = O.decode(spans_b[s])
-        assert st == 0
-        lo, hi = int(rec0[s]), int(rec0[s + 1])
-        np.testing.assert_array_equal(a[7]["off"][lo:hi], rr["off"])
-        np.testing.assert_array_equal(a[7]["v0"][lo:hi], rr["v0"])
+    # every span against the oracle, in every mode: a good span's records, a bad span's records
+    # up to its first error (decodeNext stops there), with their wide rows
+    for key, a in res.items():
+        check_spans_oracle(a, spans_b, key)
