@@ -1586,9 +1586,11 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
 // Pass 2 in one launch (phase 5): scan1's per-block bases, the block offsets by a decoupled
 // look-back (a ticket gives each workgroup its block, so it only ever waits for blocks that
 // started before it), and the span ranges -- span_hi of every span whose last tile is in the
-// block, also into the host's read-back buffer with the abort words, so the host needs no
-// copy after the decode.  Three launches were ~25 us between count and emit beside the slice
-// gather, and the read-back copy another ~45 us (its blit kernel waits for CU slots too).
+// block, and, for batches of few spans (ctl.h_res set), also into the host's read-back buffer
+// with the abort words, so the host needs no copy after the decode.  Three launches were ~25 us
+// between count and emit beside the slice gather, and the read-back copy another ~45 us (its
+// blit kernel waits for CU slots too).  Each host write is its own bus transaction, though: for
+// config 4's 66 k spans they took 2.5 ms, so many-span batches copy the words back instead.
 constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 1ull << 63, kLbVal = kLbAgg - 1;
 __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict__ tiles,
                                                      const SpanDesc* __restrict__ spans, uint32_t n_spans,
@@ -2684,7 +2686,7 @@ constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
 #ifndef CLG_JSER_ROT
-#define CLG_JSER_ROT 0  // rotated magic-scan row reads (A/B on MI355X: jser 0.262 vs 0.262 ms, config-3 subset; off)
+#define CLG_JSER_ROT 1  // rotated magic-scan row reads (A/B on MI355X, lane & 31: jser 0.262 vs 0.262 ms, config-3 subset)
 #endif
 __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_cand, const uint32_t t,
@@ -2710,8 +2712,9 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
 #if CLG_JSER_ROT
   // Without row pads the rows start 32 dwords apart, so reading dword j of every row at once
   // hits two banks (a 32-way conflict: 7.4 cycles per LDS instruction).  Each lane starts its
-  // pass at its own dword (lane & 31) and wraps, so the wave's reads spread over the banks.
-  const uint32_t rot = kZPad == 0 ? (lane & 31u) : 0u;
+  // pass at its own dword and wraps: lane l reads bank 32 (l & 1) + (j + (l >> 1)) mod 34, so
+  // the 64 reads of one instruction fall on distinct banks but for wrapped dwords 32-33
+  const uint32_t rot = kZPad == 0 ? ((lane >> 1) & 31u) : 0u;
   for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
     uint32_t D[17], J[17];
 #pragma unroll

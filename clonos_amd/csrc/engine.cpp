@@ -1808,6 +1808,7 @@ struct clg_engine {
     *nrec = prev & kRecMask;
     *nwide = prev >> 31;
   }
+  static constexpr uint32_t kHostResSpans = 1024;  // spans up to which the scan writes the host read-back
   // more than 8 GiB in one batch: the offsets pass covers 2^20 tiles
   static bool fused_fits(const DecodePlan& p) { return p.n_tiles <= (1u << 20); }
 
@@ -1899,7 +1900,11 @@ struct clg_engine {
     ctl.rep = ab + 8;
     ctl.lb = w + o_lb;
     ctl.lean = !jser && (lean_env() >= 0 ? lean_env() != 0 : lean_hint) ? 1u : 0u;
-    ctl.h_res = h_zres.as<uint64_t>();  // the scan writes the result here: no read-back copy
+    // the scan writes the result into the pinned read-back buffer itself (no copy queued after
+    // emit) while the spans are few: each span_hi is its own write across the bus, and for
+    // config 4's 66 k spans those took 2.5 ms -- there one copy after emit reads them back
+    const bool host_res = ns <= kHostResSpans;
+    ctl.h_res = host_res ? h_zres.as<uint64_t>() : nullptr;
     memset(h_zres.p, 0, (2 * size_t(ns) + 5) * 8);  // (a batch without tiles runs no scan)
     r->ctl = ctl;
     r->o = o;
@@ -1950,9 +1955,11 @@ struct clg_engine {
         if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
       }
       if (evp) HIPCHK(hipEventRecord(evp[1], stream));
-      // the span ranges and abort words are in h_zres already (the scan wrote them; emit ran
-      // right behind it: it returns at once when the batch aborted, and its stores are bounded
-      // by the output capacity)
+      // the span ranges and abort words: in h_zres already (the scan wrote them) or read back
+      // now (emit ran right behind the scan: it returns at once when the batch aborted, and its
+      // stores are bounded by the output capacity)
+      if (!host_res)
+        HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 5) * 8, hipMemcpyDeviceToHost, stream));
       if (jser) CHK(jarena_note(r->note()));
       if (r->slot) {
         if (!zdone[r->slot]) HIPCHK(hipEventCreateWithFlags(&zdone[r->slot], hipEventDisableTiming));
