@@ -1958,8 +1958,9 @@ struct clg_engine {
       // the span ranges and abort words: in h_zres already (the scan wrote them) or read back
       // now (emit ran right behind the scan: it returns at once when the batch aborted, and its
       // stores are bounded by the output capacity)
-      if (!host_res)
-        HIPCHK(hipMemcpyAsync(h_zres.p, ctl.span_lo, (2 * size_t(ns) + 5) * 8, hipMemcpyDeviceToHost, stream));
+      if (!host_res)  // span_hi and the abort words (adjacent; the host derives the ranges from span_hi)
+        HIPCHK(hipMemcpyAsync(h_zres.as<uint64_t>() + ns, ctl.span_hi, (size_t(ns) + 5) * 8, hipMemcpyDeviceToHost,
+                              stream));
       if (jser) CHK(jarena_note(r->note()));
       if (r->slot) {
         if (!zdone[r->slot]) HIPCHK(hipEventCreateWithFlags(&zdone[r->slot], hipEventDisableTiming));
