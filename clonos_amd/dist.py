@@ -359,7 +359,8 @@ def copy_arrays(copies) -> Tuple[np.ndarray, np.ndarray]:
 
 
 def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
-                    start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None) -> MergedCopies:
+                    start_epochs: Dict[int, int], dest_of: Dict[int, int], device, group=None,
+                    timing: Optional[Dict[str, float]] = None) -> MergedCopies:
     """Cross-GPU DeterminantResponseEvent.merge for the logs of the failed vertices.
 
     copies: gid -> io handle of this rank's copy (owned log or replica) of a log of a failed
@@ -393,19 +394,26 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
     handles = cv[pos[held]]
     epochs = ep_of[vslot[held]]
     key = np.full(max(n, 1), -1, np.int64)
+    import time as _time
+    t0 = _time.perf_counter()
     if len(held):
         key[held] = (io.copy_lengths(handles, epochs) << 8) | rank
+    if timing is not None:  # (developer: the bench's phase split)
+        timing["lengths"] = timing.get("lengths", 0.0) + _time.perf_counter() - t0
     if world == 1:  # every copy is this rank's: the winners are gathered in place, nothing moves
         win = key[:n]
         mine = np.nonzero(win >= 0)[0]
         lens = (win[mine] >> 8).astype(np.int64)
         tot = int(lens.sum())
         buf = torch.empty(MERGE_GUARD + max(tot, 1) + MERGE_GUARD, dtype=torch.uint8, device=device)
+        t1 = _time.perf_counter()
         if tot:
             sel = np.searchsorted(held, mine)
             got = io.copy_batch(handles[sel], epochs[sel], buf, MERGE_GUARD)
             if got != tot:
                 raise RuntimeError(f"logs changed during the merge ({got} != {tot} bytes)")
+        if timing is not None:
+            timing["gather"] = timing.get("gather", 0.0) + _time.perf_counter() - t1
         offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(mine) else lens
         return MergedCopies(buf, gids=gids[mine], offs=offs, lens=lens, ranks=np.zeros(len(mine), np.int64))
     dev = device if backend == "nccl" else "cpu"
