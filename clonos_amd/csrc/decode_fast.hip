@@ -60,7 +60,24 @@ struct FastCtx {
   uint32_t t, t1;     // this tile, end of the span's tile range
   uint32_t tables;    // Serializable tables exist (scan mode 1, emit)
   JserTabs J;
+  // the own tile's table staged in LDS (k_fast_scan mode 1, k_fast_emit; null: read J from
+  // HBM).  A lookup was a binary search of dependent HBM loads per Serializable record, per
+  // lane -- the robust emit took 10x the fast one on config 3
+  const uint32_t* lpos = nullptr;
+  const uint32_t* llen = nullptr;
+  uint32_t ln = 0;
 };
+// The tile's table into LDS (every lane of the wave calls it; it holds a barrier).
+__device__ __forceinline__ uint32_t stage_jtab(const JserTabs& J, uint32_t t, uint32_t* s_p, uint32_t* s_l,
+                                               uint32_t lane) {
+  const uint32_t n0 = J.n[t], n = n0 < (uint32_t)kJserCap ? n0 : (uint32_t)kJserCap;
+  for (uint32_t i = lane; i < n; i += 64) {
+    s_p[i] = J.pos[(uint64_t)t * kJserCap + i];
+    s_l[i] = J.len[(uint64_t)t * kJserCap + i];
+  }
+  __syncthreads();
+  return n;
+}
 
 // Span tile holding aligned coordinate a (a >= hi) and its local coordinate.
 __device__ __forceinline__ uint32_t far_tile(const FastCtx& c, uint32_t a, uint32_t* local) {
@@ -97,9 +114,13 @@ __device__ __forceinline__ int64_t fser_lookup(const FastCtx& c, uint32_t a, boo
   }
   uint32_t k = c.t, local = a;
   if (a >= c.hi) k = far_tile(c, a, &local);
-  const uint32_t n = c.J.n[k];
-  const int64_t j = jfind(c.J.pos + (uint64_t)k * kJserCap, c.J.len + (uint64_t)k * kJserCap,
-                          n < kJserCap ? n : kJserCap, local);
+  int64_t j;
+  if (k == c.t && c.lpos) {
+    j = jfind(c.lpos, c.llen, c.ln, local);
+  } else {
+    const uint32_t n = c.J.n[k];
+    j = jfind(c.J.pos + (uint64_t)k * kJserCap, c.J.len + (uint64_t)k * kJserCap, n < kJserCap ? n : kJserCap, local);
+  }
   if (j <= 0) return kLenErr;
   const int64_t L = 1 + j;
   return ((uint64_t)a + (uint64_t)L > c.end_a) ? kLenErr : L;
@@ -404,7 +425,10 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   if (lane < (uint32_t)kFOwn) fregion(td.delta, hi, (int)lane, &rs, &re);
   // No pre-scan for Serializable records: every record the BFS or the parse touches goes
   // through fser_lookup, which (mode 0, no tables yet) defers the tile.
-  const FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J};
+  __shared__ uint32_t s_jp[kJserCap], s_jl[kJserCap];
+  const uint32_t jn = mode == 1 ? stage_jtab(J, t, s_jp, s_jl, lane) : 0u;
+  const FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J,
+                  mode == 1 ? s_jp : nullptr, mode == 1 ? s_jl : nullptr, jn};
   bool defer = false;
   CLG_PHASE(2);
 
@@ -569,7 +593,16 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   // the walker reads the stream from the tile's LDS image (HBM only past the tile): byte by
   // byte from HBM it took config 3's 5 M streams 285 ms
   TileReader tr{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
+  // the candidates count_magic found, in position order: dwords holding a 03 byte, then their
+  // bytes (a byte-by-byte pass over the region read every byte from LDS)
   for (uint32_t a = rs; a < re; ++a) {
+    if ((a & 3u) == 0u || a == rs) {
+      const uint32_t w = t_dw(s_tile, a >> 2) ^ 0x03030303u;
+      if (!((w - 0x01010101u) & ~w & 0x80808080u)) {
+        a |= 3u;  // no 03 byte in this dword: on to the next
+        continue;
+      }
+    }
     if (t_u8(s_tile, a) != CLG_TAG_SERIALIZABLE || t_be32(s_tile, a + 1) != kSerMagic) continue;
     const uint64_t avail = sd.len - (td.span_off + (a - td.delta));
     bool general;
@@ -798,7 +831,9 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
   const LaneSeg seg = lanes[(uint64_t)t * kFPoints + lane];
   uint32_t pos = conv[(uint64_t)t * kFPoints + lane];
   const uint32_t img_end = stage_dense(s_img, td, tiles, t1, t, sd.len, kEmitHalo, lane);
-  const FastCtx c{s_img, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, 1u, J};
+  __shared__ uint32_t s_jp[kJserCap], s_jl[kJserCap];
+  const uint32_t jn = stage_jtab(J, t, s_jp, s_jl, lane);
+  const FastCtx c{s_img, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, 1u, J, s_jp, s_jl, jn};
 
   const uint32_t cn = mine ? seg.cnt : 0u;
   uint32_t ic = cn;

@@ -64,7 +64,7 @@ constexpr uint32_t kZImgDw = kZRows * kZPitch;
 #ifndef CLG_WARM_PRED
 #define CLG_WARM_PRED 0  // 1: the speculative warm-up as straight-line predicated steps (kZWarmUnroll per test)
 #endif
-constexpr int kZWarmUnroll = 4;
+[[maybe_unused]] constexpr int kZWarmUnroll = 4;
 #ifndef CLG_COUNT_PREFETCH
 #define CLG_COUNT_PREFETCH 0  // 1: the count pass without tables issues the next tile's loads during a walk
                               // (measured: config-2 count 0.185 against 0.175 ms without; 127 VGPRs)

@@ -9,6 +9,7 @@
 // behaviour (EpochStartOffset objects shared by reference with ConsumerOffset, Netty
 // component-granular discardReadComponents), but the bytes never leave HBM.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1379,12 +1380,28 @@ struct clg_engine {
   DecodePlan zplan;
   // host threads for batches of very many logs (CLONOS_HOST_THREADS, default 8; 1: none)
   std::unique_ptr<WorkPool> host_pool;
+  // The CPUs this process may use: its affinity mask, capped by a cgroup CPU quota (a GPU box
+  // shares its host between GPUs: 16 CPUs per GPU on the MI355X pool).
+  static int usable_cpus() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = int(std::thread::hardware_concurrency());
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long period = 0;
+      if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+        n = std::min<long long>(n, std::max<long long>(1, atoll(q) / period));
+      fclose(f);
+    }
+    return std::max(1, n);
+  }
+  // Host threads for the per-log loops: CLONOS_HOST_THREADS, else up to 16 of the usable CPUs.
+  // Config 4's step on one box (tools/r5_call6.sh): 2.49 ms with 16 against 3.1-3.4 ms with 8.
   WorkPool* workers() {
     if (!host_pool) {
       const char* v = getenv("CLONOS_HOST_THREADS");
-      int n = v ? atoi(v) : 8;
-      const int hw = int(std::thread::hardware_concurrency());
-      n = std::max(1, std::min(n, hw > 0 ? hw : 1));
+      const int n = std::max(1, std::min(v ? atoi(v) : 16, usable_cpus()));
       host_pool = std::make_unique<WorkPool>(unsigned(n));
     }
     return host_pool.get();
@@ -1684,8 +1701,20 @@ struct clg_engine {
 
   // Output arrays the kernels write: the caller's device arrays, or engine scratch that
   // finish_out copies to the caller's host arrays.
+  // Registered host outputs (CLG_MEM_MAPPED) of at most kMappedDirect bytes: the kernels write
+  // them through their device addresses, so no read-back copy and no host memcpy follow (for
+  // config 5's replay-prep decode, 1.7 MB of rows: 0.12 ms of finish_out).
+  static constexpr uint64_t kMappedDirect = 8ull << 20;
+  static bool mapped_direct(const clg_decoded& out) {
+    return out.out_kind == CLG_MEM_MAPPED && out.cap * 13 + out.wcap * 25 <= kMappedDirect &&
+           mapped_outputs(out, nullptr);
+  }
   int prep_out(clg_decoded* out, clg::DecodeOut* o) {
     const bool dev = out->out_kind == CLG_MEM_DEVICE;
+    if (mapped_direct(*out)) {
+      mapped_outputs(*out, o);
+      return CLG_OK;
+    }
     if (dev) {
       *o = clg::DecodeOut{out->off, out->tag, out->v0, out->w_idx, out->w_rc, out->w_v1, out->w_var_off,
                          out->w_var_len, out->w_sub, out->cap, out->wcap};
@@ -1720,7 +1749,7 @@ struct clg_engine {
   int finish_out(clg_decoded* out, uint64_t nrec, uint64_t nwide) {
     out->n_rec = nrec;
     out->n_wide = nwide;
-    if (out->out_kind != CLG_MEM_DEVICE) {
+    if (out->out_kind != CLG_MEM_DEVICE && !mapped_direct(*out)) {
       // the used part of each array into one pinned staging buffer (asynchronous copies; into
       // the caller's pageable arrays each copy was a synchronous staged transfer: 0.17 ms for
       // config 1's 44-log decode), then into the caller's arrays
@@ -3227,6 +3256,20 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   uint32_t n_pieces = 0;
   const uint32_t C = e->C();
   uint64_t dst = 0;
+  if (!out) {  // sizes only (the merge measures every copy first): no gather plan
+    for (uint32_t i = 0; i < n; ++i) {
+      Log* l;
+      CHK(e->get_log(log[i], &l));
+      int32_t s = 0, nb = 0;
+      if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &s, &nb));
+      len[i] = uint32_t(nb);
+      if (out_off) out_off[i] = dst;
+      dst += uint64_t(nb);
+    }
+    if (total) *total = dst;
+    return CLG_OK;
+  }
+  runs.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
     Log* l;
     CHK(e->get_log(log[i], &l));
@@ -3246,7 +3289,6 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
     dst += uint64_t(nb);
   }
   if (total) *total = dst;
-  if (!out) return CLG_OK;  // sizes only
   if (dst > cap) return fail(CLG_E_CAPACITY, "getDeterminants batch needs %llu bytes", (unsigned long long)dst);
   CHK(e->flush());
   return e->run_gather_runs(runs, segtab, n_pieces, dst, out, out_kind);
