@@ -29,8 +29,11 @@
 
 namespace clg {
 
+#define CLG_JPHASE(i) \
+  if (J.prof && lane == 0) J.prof[(uint64_t)t * 16 + (i)] = __builtin_amdgcn_s_memtime()
+
 constexpr uint32_t kScanHalo = 1024;  // covers the next tile's first kFNext regions + BFS overrun
-constexpr uint32_t kEmitHalo = 256;   // records crossing the tile end
+constexpr uint32_t kEmitHalo = 1024;  // the chain's last segment runs to a next-tile point (up to kFNext regions in)
 constexpr int kScanImgDwords = (kTile + kScanHalo + 64) / 4;
 constexpr int kEmitImgDwords = (kTile + kEmitHalo + 64) / 4;
 constexpr uint32_t kNoFar = 0xFFFFFFFFu;
@@ -38,7 +41,7 @@ constexpr int kMaxPops = 96;          // give up early: an unknown point only le
 constexpr uint32_t kMaxSegRecords = 1u << 20;
 constexpr uint32_t kSerMagic = 0xACED0005u;
 constexpr int kLenRare = -2;          // lean_len: use the general path
-constexpr int kEmitCap = 3072;        // record starts staged per emit window
+constexpr int kEmitCap = 1024;        // record starts staged per emit window (u16 start | u16 stream length)
 
 // Region l of a tile with valid aligned coordinates [lo, hi).
 __device__ __forceinline__ void fregion(uint32_t lo, uint32_t hi, int l, uint32_t* rs, uint32_t* re) {
@@ -66,6 +69,15 @@ struct FastCtx {
   const uint32_t* lpos = nullptr;
   const uint32_t* llen = nullptr;
   uint32_t ln = 0;
+  // the next tile of the span (t + 1 < t1): its table in LDS too, and its geometry -- the
+  // chain's last segment and the scan's next-tile points run through it, and each lookup there
+  // was a tile search plus a binary search of dependent HBM loads (config 3's robust emit:
+  // 6 ms, 9x the fast one)
+  const uint32_t* npos = nullptr;
+  const uint32_t* nlen = nullptr;
+  uint32_t nn = 0;
+  uint64_t n_off = 0;  // span offset of tile t + 1 (its first valid byte)
+  uint32_t n_len = 0, n_delta = 0;
 };
 // The tile's table into LDS (every lane of the wave calls it; it holds a barrier).
 __device__ __forceinline__ uint32_t stage_jtab(const JserTabs& J, uint32_t t, uint32_t* s_p, uint32_t* s_l,
@@ -79,21 +91,46 @@ __device__ __forceinline__ uint32_t stage_jtab(const JserTabs& J, uint32_t t, ui
   return n;
 }
 
+// The next tile's geometry and (tables) its table into LDS.  Every lane calls it (a barrier).
+__device__ __forceinline__ void stage_next(FastCtx& c, const JserTabs& J, bool tables, uint32_t* s_p, uint32_t* s_l,
+                                           uint32_t lane) {
+  if (c.t + 1 >= c.t1) return;
+  const TileDesc nd = c.tiles[c.t + 1];
+  c.n_off = nd.span_off;
+  c.n_len = nd.len;
+  c.n_delta = nd.delta;
+  if (tables) {
+    c.nn = stage_jtab(J, c.t + 1, s_p, s_l, lane);
+    c.npos = s_p;
+    c.nlen = s_l;
+  }
+}
+
 // Span tile holding aligned coordinate a (a >= hi) and its local coordinate.
 __device__ __forceinline__ uint32_t far_tile(const FastCtx& c, uint32_t a, uint32_t* local) {
   const uint64_t o = c.so + (a - c.lo);
+  if (c.n_len && o - c.n_off < c.n_len) {  // (o >= n_off: a >= hi)
+    *local = (uint32_t)(o - c.n_off) + c.n_delta;
+    return c.t + 1;
+  }
   uint32_t k = c.t + 1;
   while (k + 1 < c.t1 && o >= c.tiles[k].span_off + c.tiles[k].len) ++k;
   *local = (uint32_t)(o - c.tiles[k].span_off) + c.tiles[k].delta;
   return k;
 }
 
+// A byte of the span past the LDS image (tile t + 1 on), out of line: inlined at every byte
+// access of the general parsers, the tile search bloated the scan and emit code.
+__device__ __noinline__ int far_byte(const TileDesc* tiles, uint32_t t, uint32_t t1, uint64_t o) {
+  uint32_t k = t + 1;
+  while (k + 1 < t1 && o >= tiles[k].span_off + tiles[k].len) ++k;
+  return tiles[k].abase[(uint32_t)(o - tiles[k].span_off) + tiles[k].delta];
+}
+
 __device__ __forceinline__ int fbyte(const FastCtx& c, uint32_t a) {
   if (a < c.img_end) return (int)d_u8(c.T, a);
   if (a >= c.end_a) return -1;
-  uint32_t local;
-  const uint32_t k = far_tile(c, a, &local);
-  return c.tiles[k].abase[local];
+  return far_byte(c.tiles, c.t, c.t1, c.so + (a - c.lo));
 }
 
 __device__ __forceinline__ int64_t jfind(const uint32_t* pos, const uint32_t* len, uint32_t n, uint32_t key) {
@@ -117,6 +154,8 @@ __device__ __forceinline__ int64_t fser_lookup(const FastCtx& c, uint32_t a, boo
   int64_t j;
   if (k == c.t && c.lpos) {
     j = jfind(c.lpos, c.llen, c.ln, local);
+  } else if (k == c.t + 1 && c.npos) {
+    j = jfind(c.npos, c.nlen, c.nn, local);
   } else {
     const uint32_t n = c.J.n[k];
     j = jfind(c.J.pos + (uint64_t)k * kJserCap, c.J.len + (uint64_t)k * kJserCap, n < kJserCap ? n : kJserCap, local);
@@ -407,6 +446,7 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   __shared__ uint32_t s_img[kScanImgDwords];
 #define CLG_PHASE(i) \
   if (prof && lane == 0) prof[(uint64_t)t * 8 + (i)] = __builtin_amdgcn_s_memtime()
+
   __shared__ uint32_t s_c[kFPoints];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
@@ -427,8 +467,10 @@ __global__ __launch_bounds__(64) void k_fast_scan(const TileDesc* __restrict__ t
   // through fser_lookup, which (mode 0, no tables yet) defers the tile.
   __shared__ uint32_t s_jp[kJserCap], s_jl[kJserCap];
   const uint32_t jn = mode == 1 ? stage_jtab(J, t, s_jp, s_jl, lane) : 0u;
-  const FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J,
-                  mode == 1 ? s_jp : nullptr, mode == 1 ? s_jl : nullptr, jn};
+  FastCtx c{s_img, td.delta, hi, img_end, end_a, td.span_off, tiles, t, t1, mode, J,
+            mode == 1 ? s_jp : nullptr, mode == 1 ? s_jl : nullptr, jn};
+  __shared__ uint32_t s_np[kJserCap], s_nl[kJserCap];
+  stage_next(c, J, mode == 1, s_np, s_nl, lane);
   bool defer = false;
   CLG_PHASE(2);
 
@@ -575,11 +617,16 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   // deferred tiles, and the successor of a deferred tile (its segment crossing the tile
   // end, and its next-tile points, may land on Serializable records there)
   if (!J.defer[t] && !(t > sd.first_tile && J.defer[t - 1])) return;
+  CLG_JPHASE(0);
   SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, J.ar};
   stage_tile(s_tile, td, sr, lane);
+  CLG_JPHASE(1);
   const TileGeom g{td.delta, td.delta + td.len};
   const uint32_t rs = g.rs((int)lane), re = g.re((int)lane);
   const uint32_t nm = re > rs ? count_magic(s_tile, rs, re) : 0u;
+#ifndef CLG_JFILL_EXP
+#define CLG_JFILL_EXP 0  // developer A/B: 1 stage + count only, 2 no stream parse
+#endif
   uint32_t ex = nm;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -589,33 +636,66 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   const uint32_t total = __shfl(ex, 63);
   uint32_t idx = ex - nm;
   if (lane == 0) J.n[t] = total;
-  if (!nm) return;
-  // the walker reads the stream from the tile's LDS image (HBM only past the tile): byte by
-  // byte from HBM it took config 3's 5 M streams 285 ms
-  TileReader tr{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
-  // the candidates count_magic found, in position order: dwords holding a 03 byte, then their
-  // bytes (a byte-by-byte pass over the region read every byte from LDS)
-  for (uint32_t a = rs; a < re; ++a) {
-    if ((a & 3u) == 0u || a == rs) {
-      const uint32_t w = t_dw(s_tile, a >> 2) ^ 0x03030303u;
-      if (!((w - 0x01010101u) & ~w & 0x80808080u)) {
-        a |= 3u;  // no 03 byte in this dword: on to the next
-        continue;
+  CLG_JPHASE(2);
+  if (total == 0 || CLG_JFILL_EXP == 1) return;
+  // pass 1: the candidates count_magic found, in position order, into LDS by table index:
+  // dwords holding a 03 byte, then their bytes (a byte-by-byte pass over the region read every
+  // byte from LDS)
+  __shared__ uint32_t s_cand[kJserCap];
+  if (nm) {
+    for (uint32_t a = rs; a < re; ++a) {
+      if ((a & 3u) == 0u || a == rs) {
+        const uint32_t w = t_dw(s_tile, a >> 2) ^ 0x03030303u;
+        if (!((w - 0x01010101u) & ~w & 0x80808080u)) {
+          a |= 3u;  // no 03 byte in this dword: on to the next
+          continue;
+        }
       }
+      if (t_u8(s_tile, a) != CLG_TAG_SERIALIZABLE || t_be32(s_tile, a + 1) != kSerMagic) continue;
+      if (idx < (uint32_t)kJserCap) s_cand[idx] = a;
+      ++idx;
     }
-    if (t_u8(s_tile, a) != CLG_TAG_SERIALIZABLE || t_be32(s_tile, a + 1) != kSerMagic) continue;
+  }
+  __syncthreads();
+  // pass 2: one stream per lane.  Parsed where the scan found them, a lane's stream held the
+  // wave at each candidate position any lane reached: config 3's fill took 290 k cycles a tile
+  // for ~70 streams.  The parsers read the stream from the tile's LDS image (HBM only past the
+  // tile): byte by byte from HBM it took config 3's 5 M streams 285 ms
+  TileReader tr{reinterpret_cast<const uint8_t*>(s_tile), td.delta, td.delta + td.len, td.span_off, &sr};
+  uint32_t ncand = 0, ngen = 0;
+  const uint32_t nc = total < (uint32_t)kJserCap ? total : (uint32_t)kJserCap;
+  for (uint32_t i = lane; i < nc; i += 64) {
+    const uint32_t a = s_cand[i];
     const uint64_t avail = sd.len - (td.span_off + (a - td.delta));
-    bool general;
-    int64_t L = jser_inline_len_r(tr, a, avail, &general);  // the common shapes inline
+    bool general = false;
+    int64_t L = CLG_JFILL_EXP == 2 ? 80 : jser_inline_len_r(tr, a, avail, &general);  // the common shapes inline
+    ncand += 1;
+    ngen += general;
     if (general) {
-      AtTileSpan b{&tr, a};
+      // the walker through copies: its reader's address escapes into the call, and an escaping
+      // tr / sr would live in scratch for the whole kernel
+      SpanReader sr2 = sr;
+      TileReader tr2{tr.lds, tr.lo, tr.hi, tr.so, &sr2};
+      AtTileSpan b{&tr2, a};
       L = rec_len_slow(b, avail);  // walker: 1 + stream length
     }
-    if (idx < (uint32_t)kJserCap) {
-      J.pos[(uint64_t)t * kJserCap + idx] = a;
-      J.len[(uint64_t)t * kJserCap + idx] = L > 1 ? (uint32_t)(L - 1) : 0u;
+    J.pos[(uint64_t)t * kJserCap + i] = a;
+    J.len[(uint64_t)t * kJserCap + i] = L > 1 ? (uint32_t)(L - 1) : 0u;
+  }
+  if (J.prof) {
+    __syncthreads();
+    CLG_JPHASE(3);
+    uint32_t mx = ncand, sc = ncand, sg = ngen;
+    for (int off = 32; off; off >>= 1) {
+      mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+      sc += __shfl_xor(sc, off);
+      sg += __shfl_xor(sg, off);
     }
-    ++idx;
+    if (lane == 0) {
+      J.prof[(uint64_t)t * 16 + 4] = sc;
+      J.prof[(uint64_t)t * 16 + 5] = sg;
+      J.prof[(uint64_t)t * 16 + 6] = mx;
+    }
   }
 }
 
@@ -652,43 +732,35 @@ __device__ bool chain_from(const LaneSeg* lanes, uint32_t t, int e, uint64_t* va
 
 // A chain that enters tile t at aligned coordinate `entry` (a kEndFar exit of the tile
 // before): walked record by record from HBM (exact lengths) to the first of the tile's own
-// kept points it lands on.  *e: the own point the chain goes on from -- that point itself when
-// the entry is one; else point 0, rewritten to start at the entry with the walk as (the head
-// of) its segment, so that the chain, the counts and the emit (which parses cnt records from
-// conv[0]) go through it like any other.  false: the walk fails or passes every own point
-// (the span goes to the DP).
-__device__ bool enter_far(const TileDesc* tiles, const SpanDesc& sd, uint32_t t, uint32_t entry, uint32_t* conv,
-                          LaneSeg* lanes, JArena ar, int* e) {
+// kept points it lands on, *m, over *c records (*w wide).  false: the walk fails or passes
+// every own point (the span goes to the DP).  Reads only: far_apply makes the result visible.
+__device__ bool far_walk(const TileDesc* tiles, const SpanDesc& sd, uint32_t t, uint32_t entry, const uint32_t* conv,
+                         const JserTabs& J, int* m_out, uint32_t* c_out, uint32_t* w_out) {
+  const JArena ar = J.ar;
+  const uint32_t jn0 = J.n[t], jn = jn0 < (uint32_t)kJserCap ? jn0 : (uint32_t)kJserCap;
   const TileDesc td = tiles[t];
   SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, ar};
-  uint32_t* cv = conv + (uint64_t)t * kFPoints;
-  LaneSeg* ls = lanes + (uint64_t)t * kFPoints;
+  const uint32_t* cv = conv + (uint64_t)t * kFPoints;
   int m = next_kept(cv, 0);
   uint32_t pos = entry, c = 0, w = 0;
   for (uint32_t it = 0; it < kMaxSegRecords; ++it) {
     while (m < kFOwn && cv[m] < pos) m = next_kept(cv, m + 1);
     if (m >= kFOwn) return false;
     if (cv[m] == pos) {
-      if (c == 0) {  // the entry is a kept point
-        *e = m;
-        return true;
-      }
-      LaneSeg head{(uint8_t)m, 0, 0, c, w};
-      if (m == 0) {  // the walk ends on point 0: it heads point 0's own segment
-        head = ls[0];
-        head.cnt += c;
-        head.wcnt += w;
-      }
-      ls[0] = head;
-      cv[0] = entry;
-      *e = 0;
+      *m_out = m;
+      *c_out = c;
+      *w_out = w;
       return true;
     }
     const uint64_t so = td.span_off + (pos - td.delta);
     if (so >= sd.len) return false;
     AtSpan b{&sr, so};
     const int tag = (int)b(0);
-    const int64_t L = rec_len_slow(b, sd.len - so);
+    // a Serializable record's length from the tile's table when it has the record (the
+    // grammar walker reads the stream byte by byte from HBM)
+    int64_t L = tag == CLG_TAG_SERIALIZABLE && jn
+                    ? jfind(J.pos + (uint64_t)t * kJserCap, J.len + (uint64_t)t * kJserCap, jn, pos) : -1;
+    L = L > 0 && rd_be32(b, 1) == kSerMagic && (uint64_t)(L + 1) <= sd.len - so ? L + 1 : rec_len_slow(b, sd.len - so);
     if (L <= 0) return false;
     ++c;
     w += is_wide(tag);
@@ -697,11 +769,116 @@ __device__ bool enter_far(const TileDesc* tiles, const SpanDesc& sd, uint32_t t,
   return false;
 }
 
+// The chain goes on from own point *e: the landing point itself when the walk is empty;
+// else point 0, rewritten to start at the entry with the walk as (the head of) its segment,
+// so that the chain, the counts and the emit (which parses cnt records from conv[0]) go
+// through it like any other.
+__device__ int far_apply(uint32_t t, uint32_t entry, int m, uint32_t c, uint32_t w, uint32_t* conv, LaneSeg* lanes) {
+  if (c == 0) return m;
+  LaneSeg* ls = lanes + (uint64_t)t * kFPoints;
+  LaneSeg head{(uint8_t)m, 0, 0, c, w};
+  if (m == 0) {  // the walk ends on point 0: it heads point 0's own segment
+    head = ls[0];
+    head.cnt += c;
+    head.wcnt += w;
+  }
+  ls[0] = head;
+  conv[(uint64_t)t * kFPoints] = entry;
+  return 0;
+}
+
+// Exit codes: the next tile's point index (>= 0), or -1 - far (a kEndFar exit).
+__device__ __forceinline__ int sum_exit(const TileSum& sm) {
+  return sm.x == kEndFar ? -1 - (int)sm.far : (int)sm.x;
+}
+
+// The chain from own point e of tile t (sm: its summary from the first kept point f).  A chain
+// that reaches f is f's chain from there on (k_fast_scan summarised it): the walk stops there.
+// *head_c / *head_w: records before f (for the far case, which also rewrites point 0).
+__device__ bool chain_sum(const LaneSeg* lanes, uint32_t t, int e, const TileSum& sm, uint64_t* valid,
+                          uint32_t* cnt, uint32_t* wcnt, int* exit_idx) {
+  if (e == (int)sm.f && sm.f != kEndFail) {
+    if (sm.x == kEndFail) return false;
+    *valid = sm.valid;
+    *cnt = sm.cnt;
+    *wcnt = sm.wcnt;
+    *exit_idx = sum_exit(sm);
+    return true;
+  }
+  return chain_from(lanes, t, e, valid, cnt, wcnt, exit_idx);
+}
+
+// Speculative per-tile resolution (one thread per tile): the tile's entry is taken to be the
+// exit of the previous tile's chain from its first kept point (sums), which it is whenever
+// that tile was itself entered on its chain from f -- every tile of a span of short records,
+// and the tiles after a long record (a kEndFar exit), whose far walk lands on f.  The serial
+// pass accepts a tile's result when the true entry matches and redoes only the others.
+struct SpecRes {
+  uint64_t valid;
+  uint32_t cnt, wcnt;
+  int spec;     // the entry assumed (exit code of the tile before; 0 for the span's first tile)
+  int exit;     // exit code
+  int fm;       // far walk: the landing point (-1: none)
+  uint32_t fc, fw;
+  uint32_t ok;
+};
+
+__device__ SpecRes spec_tile(const TileDesc* tiles, const SpanDesc& sd, uint32_t i, const uint32_t* conv,
+                             const LaneSeg* lanes, const TileSum* sums, const JserTabs& J) {
+  const uint32_t t = sd.first_tile + i;
+  const TileSum sm = sums[t];
+  SpecRes r{};
+  r.fm = -1;
+  r.ok = 0;
+  r.spec = i == 0 ? 0 : sum_exit(sums[t - 1]);
+  if (i > 0 && sums[t - 1].x == kEndFail) return r;
+  int e = r.spec;
+  if (e < 0) {
+    const uint32_t entry = tiles[t].delta + (uint32_t)(-1 - e);
+    int m;
+    uint32_t c, w;
+    if (!far_walk(tiles, sd, t, entry, conv, J, &m, &c, &w)) return r;
+    if (c == 0) {
+      e = m;
+    } else {
+      r.fm = m;
+      r.fc = c;
+      r.fw = w;
+      // the chain from point 0 (rewritten): the walk, then m's chain
+      uint64_t vm;
+      uint32_t cc, ww;
+      int x;
+      if (!chain_sum(lanes, t, m, sm, &vm, &cc, &ww, &x)) return r;
+      if (m == 0) {  // point 0's own segment follows the walk: m's chain starts with it
+        r.valid = vm;
+      } else {
+        r.valid = vm | 1ull;
+      }
+      r.cnt = cc + c;
+      r.wcnt = ww + w;
+      r.exit = x;
+      r.ok = 1;
+      return r;
+    }
+  }
+  uint64_t vm;
+  uint32_t cc, ww;
+  int x;
+  if (!chain_sum(lanes, t, e, sm, &vm, &cc, &ww, &x)) return r;
+  r.valid = vm;
+  r.cnt = cc;
+  r.wcnt = ww;
+  r.exit = x;
+  r.ok = 1;
+  return r;
+}
+
 __global__ __launch_bounds__(256) void k_fast_resolve(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                       uint32_t* __restrict__ conv, LaneSeg* __restrict__ lanes,
-                                                      const TileSum* __restrict__ sums, const uint32_t* __restrict__ jn,
+                                                      const TileSum* __restrict__ sums, JserTabs J,
                                                       FastRes* __restrict__ fres, SpanRes* __restrict__ sres,
-                                                      uint32_t* __restrict__ span_flags, JArena ar) {
+                                                      uint32_t* __restrict__ span_flags) {
+  const uint32_t* jn = J.n;
   __shared__ uint64_t s_r[256], s_w[256];
   __shared__ uint32_t s_irregular, s_overflow;
   __shared__ uint64_t s_carry_r, s_carry_w;
@@ -768,36 +945,81 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const TileDesc* __restrict
     }
     return;
   }
-  // irregular: serial walk over the per-lane chains; a break goes to the DP pipeline
+  // irregular: every tile resolved speculatively in parallel (spec_tile), then a serial pass
+  // over the results accepts those whose entry was right and walks the others; a break goes
+  // to the DP pipeline.  (Serially from HBM, chain by chain, it was config 3's robust
+  // resolve: 3.2 ms, its spans broken by long Serializable records.)
+  __shared__ SpecRes s_spec[256];
+  __shared__ uint32_t s_fallback;
+  __shared__ int s_e;
   if (threadIdx.x == 0) {
-    uint64_t rec = 0, wide = 0;
-    int e = 0;
-    bool fallback = false;
-    for (uint32_t i = 0; i < sd.n_tiles; ++i) {
-      const uint32_t t = sd.first_tile + i;
-      uint64_t vm;
-      uint32_t c, w;
-      int x;
-      if (e < 0) {  // the tile before left by a kEndFar exit: enter at that record start
-        const uint32_t entry = tiles[t].delta + (uint32_t)(-1 - e);
-        if (!enter_far(tiles, sd, t, entry, conv, lanes, ar, &e)) {
+    s_fallback = 0;
+    s_e = 0;
+  }
+  __syncthreads();
+  for (uint32_t base = 0; base < sd.n_tiles; base += blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < sd.n_tiles) s_spec[threadIdx.x] = spec_tile(tiles, sd, i, conv, lanes, sums, J);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t n = sd.n_tiles - base < blockDim.x ? sd.n_tiles - base : blockDim.x;
+      uint64_t rec = s_carry_r, wide = s_carry_w;
+      int e = s_e;
+      bool fallback = false;
+      for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t t = sd.first_tile + base + j;
+        SpecRes& r = s_spec[j];
+        s_r[j] = rec;
+        s_w[j] = wide;
+        if (r.ok && r.spec == e) {  // accepted: point 0's rewrite (if any) is applied below
+          rec += r.cnt;
+          wide += r.wcnt;
+          e = r.exit;
+          continue;
+        }
+        r.fm = -1;
+        if (e < 0) {  // the tile before left by a kEndFar exit: enter at that record start
+          const uint32_t entry = tiles[t].delta + (uint32_t)(-1 - e);
+          int m;
+          uint32_t c, w;
+          if (!far_walk(tiles, sd, t, entry, conv, J, &m, &c, &w)) {
+            fallback = true;
+            break;
+          }
+          e = far_apply(t, entry, m, c, w, conv, lanes);
+        }
+        uint64_t vm;
+        uint32_t c, w;
+        int x;
+        if (!chain_from(lanes, t, e, &vm, &c, &w, &x)) {
           fallback = true;
           break;
         }
+        r.valid = vm;
+        rec += c;
+        wide += w;
+        e = x;
       }
-      if (!chain_from(lanes, t, e, &vm, &c, &w, &x)) {
-        fallback = true;
-        break;
-      }
-      fres[t] = FastRes{vm, rec, wide};
-      rec += c;
-      wide += w;
-      e = x;
+      s_carry_r = rec;
+      s_carry_w = wide;
+      s_e = e;
+      if (fallback) s_fallback = 1;
     }
-    if (!fallback && sd.n_tiles && e != 0) fallback = true;
+    __syncthreads();
+    if (s_fallback) break;
+    if (i < sd.n_tiles) {
+      const uint32_t t = sd.first_tile + i;
+      const SpecRes& r = s_spec[threadIdx.x];
+      if (r.fm >= 0) far_apply(t, tiles[t].delta + (uint32_t)(-1 - r.spec), r.fm, r.fc, r.fw, conv, lanes);
+      fres[t] = FastRes{r.valid, s_r[threadIdx.x], s_w[threadIdx.x]};
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const bool fallback = s_fallback || (sd.n_tiles && s_e != 0);
     SpanRes r{};
-    r.n_rec = rec;
-    r.n_wide = wide;
+    r.n_rec = s_carry_r;
+    r.n_wide = s_carry_w;
     r.status = CLG_OK;
     r.err_off = -1;
     sres[s] = r;
@@ -807,21 +1029,81 @@ __global__ __launch_bounds__(256) void k_fast_resolve(const TileDesc* __restrict
 
 // ---- pass F3: emit ---------------------------------------------------------------------
 // Phase A: each chain lane walks its segment and drops every record start (u16 image
-// coordinate) at its output index in LDS.  Phase B: lane i decodes the i-th record of the
-// window, so every SoA store of the wave covers consecutive output elements.
+// coordinate; a Serializable record's length above it, which phase A looked up already) at
+// its output index in LDS.  Phase B: lane i decodes the i-th record of the window from 8
+// dwords of the image, every tag's fields as selects (no per-tag branches, no second length
+// lookup), so every SoA store of the wave covers consecutive output elements.
+constexpr uint32_t kEmitLenNone = 0xFFFFu;  // a Serializable record too long for the entry: fdecode
+
+template <int O>
+__device__ __forceinline__ uint32_t xw(const uint32_t (&x)[7]) {  // bytes O..O+3 (LE) of the record
+  return (O & 3) == 0 ? x[O >> 2] : __builtin_amdgcn_alignbit(x[(O >> 2) + 1], x[O >> 2], 8 * (O & 3));
+}
+template <int O>
+__device__ __forceinline__ uint32_t xbe32(const uint32_t (&x)[7]) { return __builtin_bswap32(xw<O>(x)); }
+template <int O>
+__device__ __forceinline__ uint64_t xbe64(const uint32_t (&x)[7]) {
+  return (uint64_t)xbe32<O>(x) << 32 | xbe32<O + 4>(x);
+}
+template <int O>
+__device__ __forceinline__ uint32_t xb(const uint32_t (&x)[7]) { return (x[O >> 2] >> (8 * (O & 3))) & 0xFFu; }
+
+// Exact length of the record at a on the chain, from 8 dwords of the image: every tag's
+// length rule as selects (SimpleDeterminantEncoder.java:124-323), and a Serializable record's
+// from the own tile's table through the lane's cursor (its entries are in position order and
+// the lane walks forward: one compare per record instead of a binary search).  kLenRare:
+// near the image end, past the tile, or anything unexpected -- the general path decides.
+__device__ __forceinline__ int emit_len(const FastCtx& c, uint32_t a, int* tag, uint32_t* cur) {
+  // one round of LDS reads and every rule as selects: the lanes of a wave step through their
+  // segments together, and a branch per tag ran each rule's reads in turn at every step
+  const bool in = a + 32u <= c.img_end && a < c.hi;
+  const uint32_t ac = in ? a : 0u;
+  const uint32_t kk = ac >> 2, sh = 8u * (ac & 3u);
+  uint32_t d[8], x[7];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = c.T[kk + j];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) x[j] = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
+  const uint32_t tg = x[0] & 0xFFu;
+  *tag = (int)tg;
+  constexpr uint64_t lut = 2ull | 9ull << 4 | 5ull << 8 | 13ull << 24 | 5ull << 28;
+  const int ordT = (int)(int8_t)xb<13>(x), ordS = (int)(int8_t)xb<21>(x);
+  const int32_t nl = (int32_t)xbe32<14>(x), rl = (int32_t)xbe32<23>(x);
+  const bool var = xb<22>(x) != 0u;
+  const bool isT = tg == CLG_TAG_TIMER_TRIGGER, isS = tg == CLG_TAG_SOURCE_CHECKPOINT;
+  const bool isJ = tg == CLG_TAG_SERIALIZABLE;
+  const int64_t LT = ordT != 6 ? 14 : 18 + (int64_t)nl, LS = var ? 27 + (int64_t)rl : 23;
+  const bool okT = ordT >= 0 && ordT <= 6 && (ordT != 6 || nl >= 0);
+  const bool okS = ordS >= 0 && ordS <= 1 && (!var || rl >= 0);
+  int64_t L = isT ? LT : isS ? LS : (int64_t)((lut >> (4u * (tg & 15u))) & 0xFu);
+  bool ok = in && tg <= 7u && (!isT || okT) && (!isS || okS);
+  if (isJ) {
+    ok = ok && xw<1>(x) == 0x0500EDACu;  // LE of AC ED 00 05
+    uint32_t k = *cur;
+    while (k < c.ln && c.lpos[k] < a) ++k;
+    *cur = k;
+    const int64_t j = k < c.ln && c.lpos[k] == a ? (int64_t)c.llen[k] : -1;
+    ok = ok && j > 0;
+    L = 1 + j;
+  }
+  if (!ok || (uint64_t)L > (uint64_t)(c.end_a - a)) return kLenRare;
+  return (int)L;
+}
+
 __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   const uint32_t* __restrict__ conv, JserTabs J,
                                                   const LaneSeg* __restrict__ lanes, const FastRes* __restrict__ fres,
                                                   const SpanRes* __restrict__ sres, const uint32_t* __restrict__ span_flags,
                                                   DecodeOut out) {
   __shared__ uint32_t s_img[kEmitImgDwords];
-  __shared__ uint16_t s_pos[kEmitCap];
+  __shared__ uint32_t s_pos[kEmitCap];
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const TileDesc td = tiles[t];
   if (span_flags[td.span]) return;  // decoded by the DP pipeline
   const FastRes fr = fres[t];
   if (fr.valid == 0) return;
+  CLG_JPHASE(8);
   const SpanDesc sd = spans[td.span];
   const SpanRes sp = sres[td.span];
   const uint32_t t1 = sd.first_tile + sd.n_tiles;
@@ -831,9 +1113,13 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
   const LaneSeg seg = lanes[(uint64_t)t * kFPoints + lane];
   uint32_t pos = conv[(uint64_t)t * kFPoints + lane];
   const uint32_t img_end = stage_dense(s_img, td, tiles, t1, t, sd.len, kEmitHalo, lane);
+  CLG_JPHASE(9);
   __shared__ uint32_t s_jp[kJserCap], s_jl[kJserCap];
   const uint32_t jn = stage_jtab(J, t, s_jp, s_jl, lane);
-  const FastCtx c{s_img, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, 1u, J, s_jp, s_jl, jn};
+  FastCtx c{s_img, td.delta, td.delta + td.len, img_end, end_a, td.span_off, tiles, t, t1, 1u, J, s_jp, s_jl, jn};
+  __shared__ uint32_t s_np[kJserCap], s_nl[kJserCap];
+  stage_next(c, J, true, s_np, s_nl, lane);
+  CLG_JPHASE(10);
 
   const uint32_t cn = mine ? seg.cnt : 0u;
   uint32_t ic = cn;
@@ -846,44 +1132,77 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
   uint32_t idx = ic - cn, k = 0;
   const uint64_t rec0 = sp.rec_base + fr.rec_base;
   uint64_t wide = sp.wide_base + fr.wide_base;
+  uint32_t nfar = 0, nrare = 0;
+  // the lane's cursor into the own table: its first entry at or after the segment start
+  uint32_t jcur = 0;
+  if (cn) {
+    uint32_t hi_i = jn;
+    while (jcur < hi_i) {
+      const uint32_t mid = (jcur + hi_i) >> 1;
+      if (s_jp[mid] < pos) jcur = mid + 1; else hi_i = mid;
+    }
+  }
   for (uint32_t w0 = 0; w0 < total; w0 += kEmitCap) {
     const uint32_t wend = w0 + kEmitCap;
     while (k < cn && idx < wend) {  // phase A
-      s_pos[idx - w0] = (uint16_t)pos;
+      if (J.prof) {
+        nfar += pos + 27u >= img_end;
+        nrare += pos + 32u > img_end || (s_img[pos >> 2] >> (8 * (pos & 3)) & 0xFFu) - 3u <= 3u;
+      }
       int tag;
-      int L = lean_len(c, pos, &tag);
+      int L = emit_len(c, pos, &tag, &jcur);
       if (L == kLenRare) {
         bool defer = false;
         const int64_t LL = full_len(c, pos, &tag, &defer);
         L = LL > 0x7FFFFFF0ll ? (int)kLenErr : (int)LL;
       }
+      const uint32_t jl = tag == CLG_TAG_SERIALIZABLE && L > 1 && L - 1 < (int)kEmitLenNone ? (uint32_t)(L - 1)
+                                                                                             : kEmitLenNone;
+      s_pos[idx - w0] = (pos & 0xFFFFu) | jl << 16;
       pos += L > 0 ? (uint32_t)L : 1u;
       ++k;
       ++idx;
     }
     __syncthreads();
-    const uint32_t nw = total - w0 < (uint32_t)kEmitCap ? total - w0 : (uint32_t)kEmitCap;
+    CLG_JPHASE(11);
+#ifndef CLG_EMIT_EXP
+#define CLG_EMIT_EXP 0  // developer A/B: 1 no phase B
+#endif
+    const uint32_t nw = CLG_EMIT_EXP == 1 ? 0u : total - w0 < (uint32_t)kEmitCap ? total - w0 : (uint32_t)kEmitCap;
     for (uint32_t i0 = 0; i0 < nw; i0 += 64) {  // phase B
       const uint32_t i = i0 + lane;
       const bool act = i < nw;
-      const uint32_t a = act ? (uint32_t)s_pos[i] : td.delta;
-      // narrow records (Order / Timestamp / RNG / BufferBuilt) straight from 3 dwords
-      const bool in = a + 16u <= img_end;
+      const uint32_t ent = act ? s_pos[i] : td.delta;
+      const uint32_t a = ent & 0xFFFFu, jl = ent >> 16;
+      const bool in = a + 32u <= img_end;
       const uint32_t ac = in ? a : 0u;
       const uint32_t kk = ac >> 2, sh = 8u * (ac & 3u);
-      const uint32_t d0 = s_img[kk], d1 = s_img[kk + 1], d2 = s_img[kk + 2], d3 = s_img[kk + 3];
-      const uint32_t x0 = __builtin_amdgcn_alignbit(d1, d0, sh);
-      const uint32_t x1 = __builtin_amdgcn_alignbit(d2, d1, sh);
-      const uint32_t x2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-      uint32_t tg = x0 & 0xFFu;
-      const uint32_t lo = (x0 >> 8) | (x1 << 24), hi = (x1 >> 8) | (x2 << 24);  // bytes a+1..a+8 (LE)
-      int64_t v0 = tg == CLG_TAG_ORDER ? (int64_t)(int8_t)(lo & 0xFFu)
-                 : tg == CLG_TAG_TIMESTAMP ? (int64_t)__builtin_bswap64((uint64_t)hi << 32 | lo)
-                                           : (int64_t)(int32_t)__builtin_bswap32(lo);
-      const bool narrow = in && (tg <= 2u || tg == 7u) && tg != CLG_TAG_SERIALIZABLE;
+      uint32_t d[8], x[7];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = s_img[kk + j];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) x[j] = __builtin_amdgcn_alignbit(d[j + 1], d[j], sh);
+      uint32_t tg = x[0] & 0xFFu;
+      // every tag's fields (SimpleDeterminantEncoder readers :116-341), selected by tag
+      const int64_t be64_1 = (int64_t)xbe64<1>(x), be64_5 = (int64_t)xbe64<5>(x);
+      const int32_t be32_1 = (int32_t)xbe32<1>(x);
+      const bool wide_t = tg >= 3u && tg <= 6u;
+      int64_t v0 = tg == CLG_TAG_ORDER ? (int64_t)(int8_t)xb<1>(x)
+                 : tg == CLG_TAG_TIMESTAMP ? be64_1
+                 : tg == CLG_TAG_SERIALIZABLE ? (int64_t)jl
+                 : wide_t ? be64_5 : (int64_t)be32_1;
       Rec r{};
-      bool wide_rec = false;
-      if (act && !narrow) {  // wide or near the image end: the general decoder
+      r.rc = wide_t && tg != CLG_TAG_SERIALIZABLE ? be32_1 : 0;
+      r.v1 = tg == CLG_TAG_SOURCE_CHECKPOINT ? (int64_t)xbe64<13>(x) : 0;
+      const uint32_t b13 = xb<13>(x), b21 = xb<21>(x), b22 = xb<22>(x);
+      const bool tvar = tg == CLG_TAG_TIMER_TRIGGER && b13 == 6u;
+      const bool svar = tg == CLG_TAG_SOURCE_CHECKPOINT && b22 != 0u;
+      r.sub = (uint8_t)(tg == CLG_TAG_TIMER_TRIGGER ? b13 : tg == CLG_TAG_SOURCE_CHECKPOINT ? (b21 | (svar ? 0x80u : 0u)) : 0u);
+      r.var_off = tg == CLG_TAG_SERIALIZABLE ? 1u : tvar ? 18u : svar ? 27u : 0u;
+      r.var_len = tg == CLG_TAG_SERIALIZABLE ? jl : tvar ? xbe32<14>(x) : svar ? xbe32<23>(x) : 0u;
+      bool wide_rec = wide_t;
+      if (act && (!in || (tg == CLG_TAG_SERIALIZABLE && jl == kEmitLenNone))) {
+        // near the image end, or a Serializable stream too long for the entry: the general decoder
         if (fdecode(c, a, r)) {
           tg = r.tag;
           v0 = r.v0;
@@ -915,6 +1234,20 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
     }
     __syncthreads();
   }
+  CLG_JPHASE(12);
+  if (J.prof) {
+    uint32_t mx = cn, sf = nfar, sr = nrare;
+    for (int off = 32; off; off >>= 1) {
+      mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+      sf += __shfl_xor(sf, off);
+      sr += __shfl_xor(sr, off);
+    }
+    if (lane == 0) {
+      J.prof[(uint64_t)t * 16 + 13] = sf;
+      J.prof[(uint64_t)t * 16 + 14] = mx;
+      J.prof[(uint64_t)t * 16 + 15] = (uint64_t)total | (uint64_t)sr << 32;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -937,11 +1270,12 @@ int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
 }
 
 int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, uint32_t* d_conv,
-                        LaneSeg* d_lanes, const TileSum* d_sums, const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres,
+                        LaneSeg* d_lanes, const TileSum* d_sums, JserTabs J, FastRes* d_fres, SpanRes* d_sres,
                         uint32_t* d_span_flags, JArena ar, void* stream) {
   if (!n_spans) return CLG_OK;
+  J.ar = ar;
   hipLaunchKernelGGL(k_fast_resolve, dim3(n_spans), dim3(256), 0, (hipStream_t)stream, d_tiles, d_spans, d_conv, d_lanes,
-                     d_sums, d_jn, d_fres, d_sres, d_span_flags, ar);
+                     d_sums, J, d_fres, d_sres, d_span_flags);
   return ok(hipGetLastError());
 }
 

@@ -49,6 +49,14 @@ struct SpanReader {
   }
 };
 
+// A byte of the span through a fresh span reader, out of line: inlined at every byte the
+// stream parsers read, the tile search made the table fill's code several times larger.
+__device__ __noinline__ int span_byte_at(const TileDesc* tiles, uint32_t t0, uint32_t t1, uint32_t cur, uint64_t len,
+                                         uint64_t o) {
+  SpanReader r{tiles, t0, t1, cur, len, JArena{}};
+  return r.at(o);
+}
+
 // Byte reader for one tile: the LDS image for bytes inside the tile, the span reader
 // beyond it.  Coordinates are the tile's aligned coordinates.
 struct TileReader {
@@ -58,7 +66,7 @@ struct TileReader {
   SpanReader* sr;
   __device__ __forceinline__ int at(uint32_t a) {
     if (a < hi) return lds[lds_byte_addr(a)];
-    return sr->at(so + (a - lo));
+    return span_byte_at(sr->tiles, sr->t0, sr->t1, sr->cur, sr->len, so + (a - lo));
   }
   __device__ __forceinline__ uint64_t span_off(uint32_t a) const { return so + (a - lo); }
 };

@@ -551,7 +551,7 @@ struct clg_engine {
   hipEvent_t zdone[kSlots] = {};
   uint32_t plan_slot = 0;  // the slot stage_plan / enqueue_plan use (launch_fused sets it)
   DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
-  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_jpos, d_jlen, d_jn, d_defer;
+  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_rprof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
   DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
@@ -2718,7 +2718,12 @@ struct clg_engine {
     // fast path: fused scan (points + segments) -> per-span resolution -> emit
     clg::JArena jar;
     CHK(jarena_reset(&jar));
-    const clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>(), jar};
+    clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>(), jar};
+    const char* rprof_path = getenv("CLONOS_ROBUST_PHASES");  // developer diagnostics (stamps per tile)
+    if (rprof_path && d_rprof.ensure(std::max<size_t>(1, nt) * 16 * 8) == CLG_OK) {
+      J.prof = d_rprof.as<uint64_t>();
+      hipMemsetAsync(J.prof, 0, size_t(nt) * 128, stream);
+    }
     uint32_t* dbg = nullptr;
     if (getenv("CLONOS_DEBUG_DUMP") && d_dbg.ensure(std::max<size_t>(1, nt) * clg::kFPoints * 4) == CLG_OK)
       dbg = d_dbg.as<uint32_t>();
@@ -2748,7 +2753,7 @@ struct clg_engine {
     }));
     CHK(timed("robust_resolve", uint64_t(nt) * 32, [&] {
       return clg::launch_fast_resolve(dt, ds, ns, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(),
-                                      d_sums.as<clg::TileSum>(), d_jn.as<uint32_t>(), d_fres.as<clg::FastRes>(),
+                                      d_sums.as<clg::TileSum>(), J, d_fres.as<clg::FastRes>(),
                                       d_sres.as<clg::SpanRes>(), flags, jar, stream);
     }));
     if (cfg.flags & CLG_F_TIMING) {  // diagnostics: spans the convergence-point tier leaves to the DP
@@ -2789,6 +2794,15 @@ struct clg_engine {
       return clg::launch_decode_emit(dt, nt, ds, d_conv.as<clg::TileConv>(), d_tres.as<clg::TileRes>(),
                                      d_sres.as<clg::SpanRes>(), flags, o, jar, stream);
     }));
+    if (J.prof) {
+      std::vector<uint64_t> hp(size_t(nt) * 16);
+      hipMemcpyAsync(hp.data(), J.prof, hp.size() * 8, hipMemcpyDeviceToHost, stream);
+      hipStreamSynchronize(stream);
+      if (FILE* fp = fopen(rprof_path, "wb")) {
+        fwrite(hp.data(), 8, hp.size(), fp);
+        fclose(fp);
+      }
+    }
     if (const char* dump = getenv("CLONOS_DEBUG_DUMP")) {  // developer diagnostics only
       std::vector<uint32_t> hc(size_t(nt) * clg::kFPoints), hf(ns);
       std::vector<clg::TileSum> hs(nt);

@@ -161,6 +161,7 @@ struct JserTabs {
   uint32_t* n;
   uint32_t* defer;
   JArena ar;
+  uint64_t* prof = nullptr;  // developer diagnostics: 16 s_memtime stamps per tile (fill 0-7, emit 8-15)
 };
 
 // Fused convergence + segment pass.  mode 0: every tile (tiles meeting a Serializable
@@ -169,7 +170,7 @@ int launch_fast_scan(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
                      uint32_t mode, LaneSeg* d_lanes, TileSum* d_sums, uint32_t* d_dbg, uint64_t* d_prof, void* stream);
 int launch_jser_fill(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, JserTabs J, void* stream);
 int launch_fast_resolve(const TileDesc* d_tiles, const SpanDesc* d_spans, uint32_t n_spans, uint32_t* d_conv,
-                        LaneSeg* d_lanes, const TileSum* d_sums, const uint32_t* d_jn, FastRes* d_fres, SpanRes* d_sres,
+                        LaneSeg* d_lanes, const TileSum* d_sums, JserTabs J, FastRes* d_fres, SpanRes* d_sres,
                         uint32_t* d_span_flags, JArena ar, void* stream);
 int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, const uint32_t* d_conv,
                      JserTabs J, const LaneSeg* d_lanes, const FastRes* d_fres, const SpanRes* d_sres,
