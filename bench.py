@@ -575,6 +575,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
     ph = {"merge": 0.0, "replay_prep": 0.0, "truncate": 0.0}
     sub = {"responses": 0.0, "prepare": 0.0}  # replay_prep's parts: the merged events, clg_replay_prepare_device
     mt = {}  # merge's parts (rank 0): copy lengths, the winners' gather
+    pt = {}  # prepare's parts (rank 0): Python build, output allocation, the C call, result arrays
     win_bytes, n_main_rec, n_sizes = 0, 0, 0
     sync = torch.cuda.synchronize
     steps = args.config5_steps
@@ -595,7 +596,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
             mcd = mc if mc.buf.is_cuda else X.MergedCopies(mc.buf.to(dev), gids=mc.gids, offs=mc.offs, lens=mc.lens)
             accs = merged_responses(mcd, table, mine)
             t1b = _t.perf_counter()
-            ra = prepare_replay_raw(eng, [(v, accs[v], sub_tab[v]) for v in mine], device_input=True)
+            ra = prepare_replay_raw(eng, [(v, accs[v], sub_tab[v]) for v in mine], device_input=True, timing=pt)
             sub["responses"] += t1b - t1
             sub["prepare"] += _t.perf_counter() - t1b
         t2 = _t.perf_counter()
@@ -625,6 +626,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
             eng.kernel_stats_reset()  # (the timed steps' kernels and host stages below)
             sub = {k: 0.0 for k in sub}
             mt.clear()
+            pt.clear()
             continue
         ph["merge"] += t1 - t0
         ph["replay_prep"] += t2 - t1
@@ -652,6 +654,7 @@ def config5(args, torch, dev, rank, world, dist, rehearse, eng, table, plan, rep
                                         "truncate": round(t_ms, 4)},
             "replay_prep_parts_ms_rank0": {k: round(v * 1e3 / steps, 4) for k, v in sub.items()},
             "merge_parts_ms_rank0": {k: round(v * 1e3 / steps, 4) for k, v in mt.items()},
+            "prepare_parts_ms_rank0": {k: round(v * 1e3 / steps, 4) for k, v in pt.items()},
             "winner_bytes_per_step": int(wb), "main_records_per_step": int(nm), "buffer_sizes_per_step": int(nsz),
             "replay_gbs": round(wb / ((m_ms + r_ms) * 1e-3) / 1e9, 3) if m_ms + r_ms > 0 else None,
             "kernels_rank0": {k: dict(launches=v["launches"], avg_ms=round(v["ms"] / v["launches"], 5))

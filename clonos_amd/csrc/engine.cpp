@@ -551,6 +551,7 @@ struct clg_engine {
   hipEvent_t zdone[kSlots] = {};
   uint32_t plan_slot = 0;  // the slot stage_plan / enqueue_plan use (launch_fused sets it)
   DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
+  std::vector<uint64_t> tab_at;  // clg_get_determinants_batch: a log's place in the segment table (UINT64_MAX: none)
   DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_rprof, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
@@ -611,6 +612,15 @@ struct clg_engine {
       Stat& s = e->stats[name];
       s.launches++;
       s.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    // (sections of one call: the time since the last lap, under `lap_name`)
+    void lap(const char* lap_name) {
+      if (!e) return;
+      const auto now = std::chrono::steady_clock::now();
+      Stat& s = e->stats[lap_name];
+      s.launches++;
+      s.ms += std::chrono::duration<double, std::milli>(now - t0).count();
+      t0 = now;
     }
   };
   std::vector<PendingTiming> timings;
@@ -1146,7 +1156,7 @@ struct clg_engine {
   }
 
   int run_gather(const std::vector<clg::GatherPiece>& pieces, uint64_t total, void* out, uint32_t out_kind,
-                 const char* stat = "slice_gather") {
+                 const char* stat = "slice_gather", bool wait = true) {
     if (pieces.empty()) return CLG_OK;
     const size_t db = pieces.size() * sizeof(clg::GatherPiece);
     CHK(h_desc.ensure(db));
@@ -1164,7 +1174,7 @@ struct clg_engine {
       return clg::launch_gather(d_desc.as<clg::GatherPiece>(), uint32_t(pieces.size()), dout, stream);
     }));
     if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
-    return sync();
+    return wait || out_kind != CLG_MEM_DEVICE ? sync() : CLG_OK;
   }
 
   // The gather's descriptors, staged: runs | segment table; *o: where each part starts.
@@ -1189,12 +1199,93 @@ struct clg_engine {
                                      reinterpret_cast<const uint32_t*>(d + o[1]), pool, C(), pieces, on);
   }
 
+  // Segment-major gather plan (k_gather_seg) for runs that share logs -- config 2's 8
+  // consumers of each log slice overlapping suffixes of it, so the piece-per-run gather read
+  // each log segment from HBM about four times: the runs grouped by their log (segment table
+  // entry), each group's segment range, the blocks' prefix.  CLONOS_GATHER_SEG: 0 never, 1
+  // when there are at least 1.5 runs per log (default), 2 always (A/B).
+  const int gather_seg = [] {  // (read at engine creation)
+    const char* e = getenv("CLONOS_GATHER_SEG");
+    return e ? atoi(e) : 1;
+  }();
+  std::vector<uint32_t> gs_idx;
+  bool plan_gather_seg(const std::vector<clg::SegSpan>& runs, std::vector<clg::SegSpan>& sorted,
+                       std::vector<clg::GatherGroup>& groups, uint32_t* n_items) {
+    const int mode = gather_seg;
+    if (mode == 0 || runs.empty()) return false;
+    const uint32_t Cb = C();
+    gs_idx.resize(runs.size());
+    for (uint32_t i = 0; i < runs.size(); ++i) gs_idx[i] = i;
+    std::stable_sort(gs_idx.begin(), gs_idx.end(),
+                     [&](uint32_t a, uint32_t b) { return runs[a].segtab_off < runs[b].segtab_off; });
+    groups.clear();
+    sorted.clear();
+    sorted.reserve(runs.size());
+    uint64_t items = 0;
+    for (size_t i = 0; i < gs_idx.size();) {
+      size_t j = i;
+      uint32_t lo = UINT32_MAX, hi = 0;
+      while (j < gs_idx.size() && runs[gs_idx[j]].segtab_off == runs[gs_idx[i]].segtab_off) {
+        const clg::SegSpan& r = runs[gs_idx[j]];
+        lo = std::min(lo, r.phys / Cb);
+        hi = std::max(hi, uint32_t((uint64_t(r.phys) + r.len - 1) / Cb + 1));
+        sorted.push_back(r);
+        ++j;
+      }
+      groups.push_back(clg::GatherGroup{runs[gs_idx[i]].segtab_off, lo, uint32_t(items), uint32_t(i), uint32_t(j)});
+      items += hi - lo;
+      i = j;
+    }
+    if (items >= (1ull << 31)) return false;
+    if (mode == 1 && groups.size() * 3 > runs.size() * 2) return false;
+    *n_items = uint32_t(items);
+    return true;
+  }
+  std::vector<clg::SegSpan> gs_runs;
+  std::vector<clg::GatherGroup> gs_groups;
+  // The segment-major plan's descriptors: sorted runs | segment table | groups.
+  static size_t gather_seg_layout(size_t n_runs, size_t n_segtab, size_t n_groups, size_t o[3]) {
+    o[0] = 0;
+    o[1] = al16(n_runs * sizeof(clg::SegSpan));
+    o[2] = al16(o[1] + n_segtab * 4);
+    return o[2] + n_groups * sizeof(clg::GatherGroup);
+  }
+  void gather_seg_fill(uint8_t* h, const std::vector<uint32_t>& segtab, const size_t o[3]) {
+    memcpy(h + o[0], gs_runs.data(), gs_runs.size() * sizeof(clg::SegSpan));
+    memcpy(h + o[1], segtab.data(), segtab.size() * 4);
+    memcpy(h + o[2], gs_groups.data(), gs_groups.size() * sizeof(clg::GatherGroup));
+  }
+  int gather_seg_launch(const uint8_t* d, const size_t o[3], uint32_t n_items, uint8_t* out, hipStream_t on) {
+    return clg::launch_gather_seg(reinterpret_cast<const clg::GatherGroup*>(d + o[2]), uint32_t(gs_groups.size()),
+                                  n_items, reinterpret_cast<const clg::SegSpan*>(d + o[0]),
+                                  reinterpret_cast<const uint32_t*>(d + o[1]), pool, C(), out, on);
+  }
+
   // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
   int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                       uint64_t total, void* out, uint32_t out_kind) {
     if (runs.empty() || !n_pieces) return CLG_OK;
     if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
       return gather_runs_async(runs, segtab, n_pieces, total, out);
+    uint32_t n_items = 0;
+    if (plan_gather_seg(runs, gs_runs, gs_groups, &n_items)) {
+      size_t o[3];
+      const size_t hb = gather_seg_layout(gs_runs.size(), segtab.size(), gs_groups.size(), o);
+      CHK(h_desc.ensure(hb));
+      CHK(d_desc.ensure(hb));
+      gather_seg_fill(h_desc.as<uint8_t>(), segtab, o);
+      HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
+      uint8_t* dout;
+      if (out_kind == CLG_MEM_DEVICE) {
+        dout = static_cast<uint8_t*>(out);
+      } else {
+        CHK(d_out.ensure(total));
+        dout = d_out.as<uint8_t>();
+      }
+      CHK(timed("slice_gather", 2 * total, [&] { return gather_seg_launch(d_desc.as<uint8_t>(), o, n_items, dout, stream); }));
+      if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
+      return sync();
+    }
     size_t o[2];
     const size_t hb = gather_desc_layout(runs, segtab, o);
     CHK(h_desc.ensure(hb));
@@ -1225,6 +1316,23 @@ struct clg_engine {
     const uint32_t set = gseq++ & 1u;
     if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
     else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
+    uint32_t n_items = 0;
+    if (plan_gather_seg(runs, gs_runs, gs_groups, &n_items)) {
+      size_t o[3];
+      const size_t hb = gather_seg_layout(gs_runs.size(), segtab.size(), gs_groups.size(), o);
+      PinBuf& hd = h_gdesc[set];
+      DevBuf& dd = d_gdesc[set];
+      CHK(hd.ensure(hb));
+      CHK(dd.ensure(hb));
+      gather_seg_fill(hd.as<uint8_t>(), segtab, o);
+      HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
+      CHK(timed("slice_gather", 2 * total, [&] {
+        return gather_seg_launch(dd.as<uint8_t>(), o, n_items, static_cast<uint8_t*>(out), gstream);
+      }, gstream));
+      HIPCHK(hipEventRecord(gdone[set], gstream));
+      g_pending = true;
+      return CLG_OK;
+    }
     size_t o[2];
     const size_t hb = gather_desc_layout(runs, segtab, o);
     PinBuf& hd = h_gdesc[set];
@@ -3266,7 +3374,6 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
   if (n && (!log || !start_epoch || !len)) return fail(CLG_E_INVALID_ARG, "null argument");
   std::vector<clg::SegSpan> runs;
   std::vector<uint32_t> segtab;
-  std::unordered_map<uint32_t, uint64_t> tab_of;
   uint32_t n_pieces = 0;
   const uint32_t C = e->C();
   uint64_t dst = 0;
@@ -3284,24 +3391,34 @@ int clg_get_determinants_batch(clg_engine* e, const uint32_t* log, const int64_t
     return CLG_OK;
   }
   runs.reserve(n);
-  for (uint32_t i = 0; i < n; ++i) {
+  // each log's segment indices once in segtab: the log's place there, by handle (a hash map
+  // took 0.1 ms for config 5's 2 064 logs)
+  std::vector<uint64_t>& tab_at = e->tab_at;
+  if (tab_at.size() < e->logs.size()) tab_at.resize(e->logs.size(), UINT64_MAX);
+  std::vector<uint32_t> touched;
+  touched.reserve(n);
+  int st = CLG_OK;
+  for (uint32_t i = 0; i < n && st == CLG_OK; ++i) {
     Log* l;
-    CHK(e->get_log(log[i], &l));
+    if ((st = e->get_log(log[i], &l)) != CLG_OK) break;
     int32_t s = 0, nb = 0;
-    if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &s, &nb));
+    if (l->depth != 0 && (st = e->determinants_range(*l, start_epoch[i], &s, &nb)) != CLG_OK) break;
     len[i] = uint32_t(nb);
     if (out_off) out_off[i] = dst;
     if (nb > 0) {
-      auto ti = tab_of.find(log[i]);
-      if (ti == tab_of.end()) {
-        ti = tab_of.emplace(log[i], segtab.size()).first;
+      uint64_t& at = tab_at[log[i]];
+      if (at == UINT64_MAX) {
+        at = segtab.size();
+        touched.push_back(log[i]);
         segtab.insert(segtab.end(), l->segs.begin(), l->segs.end());
       }
-      runs.push_back(clg::SegSpan{ti->second, uint32_t(s), uint32_t(nb), dst, n_pieces, 0});
+      runs.push_back(clg::SegSpan{at, uint32_t(s), uint32_t(nb), dst, n_pieces, 0});
       n_pieces += uint32_t(s + nb - 1) / C - uint32_t(s) / C + 1;
     }
     dst += uint64_t(nb);
   }
+  for (uint32_t h : touched) tab_at[h] = UINT64_MAX;
+  if (st != CLG_OK) return st;
   if (total) *total = dst;
   if (dst > cap) return fail(CLG_E_CAPACITY, "getDeterminants batch needs %llu bytes", (unsigned long long)dst);
   CHK(e->flush());
@@ -3431,11 +3548,16 @@ int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) 
         if ((st[k] = e->checkpoint_complete(l, cp, freed[k])) != CLG_OK) return;
       }
     });
+    ht.lap("host_trunc_pool");
     for (unsigned k = 0; k < P; ++k) e->free_segs.insert(e->free_segs.end(), freed[k].begin(), freed[k].end());
     for (unsigned k = 0; k < P; ++k)
       if (st[k] != CLG_OK) return fail(st[k], "checkpoint completion failed on a log (state outside its bounds)");
-    for (unsigned k = 0; k < P; ++k)
+    size_t n_later = 0;
+    for (unsigned k = 0; k < P; ++k) {
+      n_later += later[k].size();
       for (uint32_t i : later[k]) CHK(e->checkpoint_complete(e->logs[i], cp));
+    }
+    ht.lap(n_later ? "host_trunc_later" : "host_trunc_free");
   } else {
     for (auto& l : e->logs)
       if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
@@ -3589,24 +3711,48 @@ static size_t o_rout_end(uint32_t ns, uint64_t n_sizes) { return o_rout_cnt(n_si
 static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n, clg_replay_out* out, bool dev_in) {
   ENGINE_GUARD(e);
   if (!out || !out->main || !out->main_rec_base || (n && !v)) return fail(CLG_E_INVALID_ARG, "null argument");
+  clg_engine::HostTimer lap(e, "host_replay_rest");  // (laps below: the sections)
   struct Piece {
     const uint8_t* p;
     uint64_t len;
   };
   std::vector<Piece> mains(n), subs;
-  // the accumulated map's entries by CausalLogID (equals :128-149), per vertex: O(entries +
-  // subpartitions) instead of a scan per subpartition
-  std::map<IdKey, uint32_t> index;
+  // the accumulated map's entries by CausalLogID (equals :128-149), per vertex: an
+  // open-addressing table, O(entries + subpartitions) (a std::map took 0.16 ms for config 5's
+  // 16 vertices x 129 entries)
+  std::vector<IdKey> keys;
+  std::vector<uint32_t> slot;  // entry index + 1 (0: empty)
+  uint64_t mask = 0;
   const clg_response* indexed = nullptr;
+  auto hkey = [](const IdKey& k) {
+    uint64_t h = uint64_t(uint16_t(k.v)) * 0x9E3779B97F4A7C15ull ^ uint64_t(k.main) << 17 ^ uint64_t(uint8_t(k.sub)) << 25;
+    h ^= uint64_t(k.lo) * 0xC2B2AE3D27D4EB4Full;
+    h ^= uint64_t(k.hi) * 0x165667B19E3779F9ull;
+    return h ^ h >> 31;
+  };
+  auto same = [](const IdKey& a, const IdKey& b) {
+    return a.v == b.v && a.main == b.main && a.sub == b.sub && a.lo == b.lo && a.hi == b.hi;
+  };
   auto lookup = [&](const clg_response* r, const clg_causal_log_id& id) -> Piece {
     if (!r) return Piece{nullptr, 0};
     if (r != indexed) {
-      index.clear();
-      for (uint32_t i = 0; i < r->n; ++i) index.emplace(key_of(0, r->entries[i].id), i);  // first of equal keys
+      uint64_t size = 16;
+      while (size < 2ull * r->n) size <<= 1;
+      mask = size - 1;
+      slot.assign(size, 0u);
+      keys.resize(r->n);
+      for (uint32_t i = 0; i < r->n; ++i) {
+        keys[i] = key_of(0, r->entries[i].id);
+        uint64_t h = hkey(keys[i]) & mask;
+        while (slot[h] && !same(keys[slot[h] - 1], keys[i])) h = (h + 1) & mask;
+        if (!slot[h]) slot[h] = i + 1;  // the first of equal keys
+      }
       indexed = r;
     }
-    const auto it = index.find(key_of(0, id));
-    return it == index.end() ? Piece{nullptr, 0} : Piece{r->entries[it->second].bytes, r->entries[it->second].len};
+    const IdKey k = key_of(0, id);
+    for (uint64_t h = hkey(k) & mask; slot[h]; h = (h + 1) & mask)
+      if (same(keys[slot[h] - 1], k)) return Piece{r->entries[slot[h] - 1].bytes, r->entries[slot[h] - 1].len};
+    return Piece{nullptr, 0};
   };
   for (uint32_t i = 0; i < n; ++i) {
     if (v[i].n_subpartitions && !v[i].subpartitions) return fail(CLG_E_INVALID_ARG, "null subpartition table");
@@ -3621,6 +3767,7 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
       subs.push_back(lookup(v[i].acc, sid));
     }
   }
+  lap.lap("host_replay_index");
   const uint32_t ns = uint32_t(subs.size());
   if (ns && (!out->sizes_base || !out->sub_count || !out->sub_status || !out->sub_err_off || !out->sub_err_tag))
     return fail(CLG_E_INVALID_ARG, "null subpartition output");
@@ -3650,7 +3797,8 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
       for (uint64_t o = 0; o < pc.len; o += 1u << 30)  // a piece's length is 32-bit
         pieces.push_back(clg::GatherPiece{pc.p + o, at[i] + o, uint32_t(std::min<uint64_t>(pc.len - o, 1u << 30)), 0});
     }
-    CHK(e->run_gather(pieces, total, e->d_stage.p, CLG_MEM_DEVICE, "replay_stage"));
+    // (no wait: the kernels below read the staged bytes on the same stream)
+    CHK(e->run_gather(pieces, total, e->d_stage.p, CLG_MEM_DEVICE, "replay_stage", false));
   } else {
     CHK(e->h_stage.ensure(total + 16));
     for (uint32_t i = 0; i < n + ns; ++i) {
@@ -3659,6 +3807,7 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
     }
     if (total) HIPCHK(hipMemcpyAsync(e->d_stage.p, e->h_stage.p, total, hipMemcpyHostToDevice, e->stream));
   }
+  lap.lap("host_replay_stage");
   const uint8_t* dst = e->d_stage.as<uint8_t>();
   // subpartition buffers first (their kernels only read the staged bytes)
   std::function<int(clg::JArena)> classify;
@@ -3712,11 +3861,13 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
     // count, err_off, status, err_tag: adjacent on the device (d_first's block): one copy
     HIPCHK(hipMemcpyAsync(hr + o_rout_cnt(n_sizes), d_count, size_t(ns) * 24, hipMemcpyDeviceToHost, e->stream));
   }
+  lap.lap("host_replay_sizes");
   // main logs: the batched decode (span i = vertex i)
   auto build = [&](clg_engine::DecodePlan& p, uint32_t T) {
     for (uint32_t i = 0; i < n; ++i) e->plan_host_span(p, dst + at[i], mains[i].len, i, T);
   };
   CHK(e->decode(build, main_bytes, out->main, out->main_rec_base));
+  lap.lap("host_replay_decode");
   CHK(e->sync());
   // a Serializable walk in a subpartition buffer found the spill arena full: again, larger
   uint8_t* hr = e->h_rout.as<uint8_t>();
@@ -3737,6 +3888,7 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
     memcpy(out->sub_status, hr + oc + size_t(ns) * 16, size_t(ns) * 4);
     memcpy(out->sub_err_tag, hr + oc + size_t(ns) * 20, size_t(ns) * 4);
   }
+  lap.lap("host_replay_finish");
   return CLG_OK;
 }
 

@@ -375,8 +375,10 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
     gathered in one call, grouped by destination, and one all-to-all carries them to the
     ranks hosting the replacements.  Returns this rank's MergedCopies (a log no rank holds
     is absent, as in the merged map)."""
+    import time as _time
     import torch
     import torch.distributed as dist
+    t_in = _time.perf_counter()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if world > 255:
         raise ValueError("rank must fit the packed key's low byte")
@@ -394,8 +396,9 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
     handles = cv[pos[held]]
     epochs = ep_of[vslot[held]]
     key = np.full(max(n, 1), -1, np.int64)
-    import time as _time
     t0 = _time.perf_counter()
+    if timing is not None:
+        timing["setup"] = timing.get("setup", 0.0) + t0 - t_in
     if len(held):
         key[held] = (io.copy_lengths(handles, epochs) << 8) | rank
     if timing is not None:  # (developer: the bench's phase split)
@@ -412,10 +415,15 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
             got = io.copy_batch(handles[sel], epochs[sel], buf, MERGE_GUARD)
             if got != tot:
                 raise RuntimeError(f"logs changed during the merge ({got} != {tot} bytes)")
+        t2 = _time.perf_counter()
         if timing is not None:
-            timing["gather"] = timing.get("gather", 0.0) + _time.perf_counter() - t1
+            timing["gather"] = timing.get("gather", 0.0) + t2 - t1
+            timing["alloc"] = timing.get("alloc", 0.0) + t1 - t0
         offs = MERGE_GUARD + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(mine) else lens
-        return MergedCopies(buf, gids=gids[mine], offs=offs, lens=lens, ranks=np.zeros(len(mine), np.int64))
+        res = MergedCopies(buf, gids=gids[mine], offs=offs, lens=lens, ranks=np.zeros(len(mine), np.int64))
+        if timing is not None:
+            timing["finish"] = timing.get("finish", 0.0) + _time.perf_counter() - t2
+        return res
     dev = device if backend == "nccl" else "cpu"
     kt = torch.from_numpy(key).to(dev)
     dist.all_reduce(kt, op=dist.ReduceOp.MAX, group=group)

@@ -20,6 +20,8 @@ import ctypes as C
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import time
+
 import numpy as np
 
 from . import _lib
@@ -71,6 +73,7 @@ class DeterminantResponseEvent:
         self._entries = (_lib.ResponseEntry * max(1, capacity))()
         self._c = _lib.Response(1 if found else 0, vertex_id, 0, correlation_id, 0, capacity, 0, 0, self._entries)
         self._keep: List[object] = []  # buffers the entries point into
+        self._bytes: Optional[Tuple[int, int]] = None  # (main log bytes, all bytes) when known (merged_responses)
 
     # ---- accessors (:71-89)
     def isFound(self) -> bool:
@@ -106,6 +109,7 @@ class DeterminantResponseEvent:
 
     # ---- map building (JobCausalLogImpl.respondToDeterminantRequest :197-199)
     def put(self, lid: CausalLogID, data: bytes) -> None:
+        self._bytes = None
         buf = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(1, np.uint8)
         self._keep.append(buf)
         self._grow(self._c.n + 1)
@@ -115,6 +119,7 @@ class DeterminantResponseEvent:
     def put_device(self, lid: CausalLogID, ptr: int, n: int, keep=None) -> None:
         """An entry whose bytes live in device memory (replay-prep over a cross-GPU merge's
         receive buffer, clg_replay_prepare_device); `keep` is held while the event lives."""
+        self._bytes = None
         if keep is not None:
             self._keep.append(keep)
         self._grow(self._c.n + 1)
@@ -125,6 +130,7 @@ class DeterminantResponseEvent:
         """Many device-memory entries in one call (clg_response_put_batch); ids: LOG_ID array."""
         if keep is not None:
             self._keep.append(keep)
+        self._bytes = None
         n = len(ids)
         self._grow(self._c.n + n)
         ids = np.ascontiguousarray(ids, LOG_ID)
@@ -160,6 +166,7 @@ class DeterminantResponseEvent:
         return ev, int(used.value)
 
     def merge(self, other: "DeterminantResponseEvent") -> None:
+        self._bytes = None
         self._grow(self._c.n + other._c.n)
         self._keep.extend(other._keep)
         check(lib.clg_response_merge(C.byref(self._c), C.byref(other._c)))
@@ -203,17 +210,25 @@ def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, Determ
     vert = table.vertex[gids] if len(gids) else np.zeros(0, np.int64)
     order = np.argsort(vert, kind="stable")
     vs = vert[order]
-    ids_o = ids[gids[order]]
-    ptr_o = np.asarray(merged.offs, np.uint64)[order] + np.uint64(merged.buf.data_ptr())
-    len_o = np.asarray(merged.lens, np.uint64)[order]
+    ids_o = np.ascontiguousarray(ids[gids[order]], LOG_ID)
+    ptr_o = np.ascontiguousarray(np.asarray(merged.offs, np.uint64)[order] + np.uint64(merged.buf.data_ptr()))
+    len_o = np.ascontiguousarray(np.asarray(merged.lens, np.uint64)[order])
+    # each vertex's byte totals, for prepare_replay_raw's output sizes (prefix sums, once)
+    c_all = np.concatenate([[0], np.cumsum(len_o, dtype=np.uint64)]).tolist()
+    c_main = np.concatenate([[0], np.cumsum(np.where(ids_o["is_main"] != 0, len_o, 0), dtype=np.uint64)]).tolist()
     out = {}
     va = np.asarray(list(vertices), np.int64)
     los = np.searchsorted(vs, va, "left").tolist()
     his = np.searchsorted(vs, va, "right").tolist()
+    # one put per vertex into the three arrays above (pointer arithmetic, no per-vertex views)
+    pi, pp, pl, isz = ids_o.ctypes.data, ptr_o.ctypes.data, len_o.ctypes.data, ids_o.itemsize
+    keep = (merged.buf, ids_o, ptr_o, len_o)
     for v, lo, hi in zip(va.tolist(), los, his):
         ev = DeterminantResponseEvent(True, v, capacity=max(1, hi - lo))
         if hi > lo:
-            ev.put_device_batch(ids_o[lo:hi], ptr_o[lo:hi], len_o[lo:hi], merged.buf)
+            ev._keep.append(keep)
+            check(lib.clg_response_put_batch(C.byref(ev._c), pi + lo * isz, pp + lo * 8, pl + lo * 8, hi - lo))
+        ev._bytes = (int(c_main[hi] - c_main[lo]), int(c_all[hi] - c_all[lo]))
         out[v] = ev
     return out
 
@@ -237,9 +252,11 @@ class ReplayArrays:
 
 
 def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, np.ndarray]],
-                       device_input: bool = False) -> ReplayArrays:
+                       device_input: bool = False, timing: Optional[Dict[str, float]] = None) -> ReplayArrays:
     """clg_replay_prepare over jobs (vertex_id, merged response, subpartition table as a
-    LOG_ID array in the task's order), without per-subpartition Python objects."""
+    LOG_ID array in the task's order), without per-subpartition Python objects.  timing:
+    (developer) seconds added per part -- build, alloc, call, finish."""
+    t0 = time.perf_counter()
     n = len(jobs)
     vs = (_lib.ReplayVertex * max(1, n))()
     tables = []
@@ -249,11 +266,15 @@ def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResp
         tables.append(t)
         n_sub += len(t)
         vs[i] = _lib.ReplayVertex(C.pointer(acc._c), C.cast(t.ctypes.data, C.POINTER(_lib.CausalLogIdC)), len(t), vid, 0)
-        e = acc.entries()
-        ln = e["len"]
-        mb = int(ln[e["id"]["is_main"] != 0].sum())
+        if acc._bytes is not None:
+            mb, ab = acc._bytes
+        else:
+            e = acc.entries()
+            ln = e["len"]
+            mb, ab = int(ln[e["id"]["is_main"] != 0].sum()), int(ln.sum())
         main_bytes += mb
-        sub_bytes += int(ln.sum()) - mb  # a bound: the table may name fewer
+        sub_bytes += ab - mb  # a bound: the table may name fewer
+    t1 = time.perf_counter()
     cap = main_bytes // 2 + n + 1
     d, arrs, _ = engine._pooled_outputs(cap, main_bytes // 6 + n + 1)
     base = np.zeros(n + 1, np.uint64)
@@ -266,9 +287,15 @@ def prepare_replay_raw(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResp
     out = _lib.ReplayOut(C.pointer(d), _np_ptr(base), _np_ptr(sizes), sizes.size, _np_ptr(sbase), _np_ptr(cnt),
                          _np_ptr(sst), _np_ptr(soff), _np_ptr(stag))
     fn = lib.clg_replay_prepare_device if device_input else lib.clg_replay_prepare
+    t2 = time.perf_counter()
     st = fn(engine.handle, vs, n, C.byref(out))
+    t3 = time.perf_counter()
     main = engine._finish(st, d, arrs, base, n, None)
-    return ReplayArrays(main, sizes, sbase[:n_sub], cnt[:n_sub], sst[:n_sub], soff[:n_sub], stag[:n_sub])
+    res = ReplayArrays(main, sizes, sbase[:n_sub], cnt[:n_sub], sst[:n_sub], soff[:n_sub], stag[:n_sub])
+    if timing is not None:
+        for k, v in (("build", t1 - t0), ("alloc", t2 - t1), ("call", t3 - t2), ("finish", time.perf_counter() - t3)):
+            timing[k] = timing.get(k, 0.0) + v
+    return res
 
 
 def prepare_replay(engine: Engine, jobs: Sequence[Tuple[int, DeterminantResponseEvent, Sequence[CausalLogID]]],

@@ -203,6 +203,53 @@ def test_seek_batch_then_slice(seg, shuffle):
             assert r.len == len(exp) and out[r.out_off:r.out_off + r.len].tobytes() == exp
 
 
+@pytest.mark.parametrize("seg,mode", [(512, "1"), (16384, "1"), (16384, "0"), (1024, "2")])
+def test_async_slice_many_consumers_per_log(seg, mode, monkeypatch):
+    """The asynchronous device-output slice of config 2's shape -- several consumers of each
+    log at random offsets, requests shuffled -- through the segment-major gather (one block
+    per log segment copying it for every request of that log; CLONOS_GATHER_SEG 1 = when
+    runs share logs, 2 = always) and through the piece gather (0): each request's bytes equal
+    its suffix of the log."""
+    import ctypes
+    from clonos_amd import _lib
+    monkeypatch.setenv("CLONOS_GATHER_SEG", mode)  # (read at engine creation)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    rng = np.random.default_rng(seg + int(mode))
+    with Engine(segment_bytes=seg, pool_segments=(1 << 22) // seg + 64, async_slice=True) as eng:
+        logs, bufs = [], []
+        for v in range(7):
+            log = eng.open_log(CausalLogID.main(v))
+            b, _ = synth.config2_log(int(rng.integers(10, 40000)), rng)
+            log.processUpstreamDelta(b.tobytes(), 0, 2)
+            logs.append(log)
+            bufs.append(b.tobytes())
+        reqs = [(i, (c + 1, i), int(rng.integers(0, len(bufs[i]) + 1))) for i in range(len(logs)) for c in range(8)]
+        reqs = [reqs[j] for j in rng.permutation(len(reqs))]
+        creq = (_lib.SliceReq * len(reqs))()
+        cres = (_lib.SliceRes * len(reqs))()
+        for k, (i, ch, _) in enumerate(reqs):
+            creq[k].log = logs[i].handle
+            creq[k].consumer = _lib.ChannelId(*ch)
+            creq[k].epoch = 2
+        total = sum(len(bufs[i]) - off for i, _, off in reqs)
+        dptr = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(dptr), ctypes.c_size_t(total + 64)) == 0
+        try:
+            for _ in range(2):  # twice: the second call reuses the descriptor sets
+                eng.seek_consumers_raw(creq, np.array([o for _, _, o in reqs], np.int32), len(reqs))
+                got = eng.slice_batch_raw(creq, cres, len(reqs), dptr.value, total + 64, device=True)
+                assert got == total
+                eng.sync()
+                host = np.empty(total + 1, np.uint8)
+                assert hip.hipMemcpy(ctypes.c_void_p(host.ctypes.data), dptr, ctypes.c_size_t(total), 2) == 0
+                for k, (i, ch, off) in enumerate(reqs):
+                    r = cres[k]
+                    assert r.status == 0 and r.len == len(bufs[i]) - off
+                    assert host[r.out_off:r.out_off + r.len].tobytes() == bufs[i][off:]
+        finally:
+            hip.hipFree(dptr)
+
+
 def test_capacity_reports_required_size():
     """clg_get_delta / clg_get_determinants with a short buffer: CLG_E_CAPACITY, *n = the
     size needed, consumer not advanced (the JNI layer sizes its direct buffer this way)."""
