@@ -1180,7 +1180,11 @@ struct clg_engine {
   // The gather's descriptors, staged: runs | segment table; *o: where each part starts.
   // (Tried and removed: pieces in source order -- every consumer's piece of one segment back
   // to back on one XCD, for L2 hits -- took the isolated config-2 gather from 0.39 to 0.43 ms
-  // and cost 0.1 ms of host grouping per step.)
+  // and cost 0.1 ms of host grouping per step.  Round 5: a segment-major gather, one block per
+  // log segment copying it for every consumer of that log (each segment read from HBM once):
+  // in the config-2 step the gather fell from 0.68 to 0.54 ms but the decode beside it rose
+  // from 0.62 to 0.75 and the step from 0.732 to 0.786 ms; isolated 0.46 against 0.39 ms.
+  // The re-reads are not what bounds the step.)
   static size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
   static size_t gather_desc_layout(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab,
                                    size_t o[2]) {
@@ -1199,93 +1203,12 @@ struct clg_engine {
                                      reinterpret_cast<const uint32_t*>(d + o[1]), pool, C(), pieces, on);
   }
 
-  // Segment-major gather plan (k_gather_seg) for runs that share logs -- config 2's 8
-  // consumers of each log slice overlapping suffixes of it, so the piece-per-run gather read
-  // each log segment from HBM about four times: the runs grouped by their log (segment table
-  // entry), each group's segment range, the blocks' prefix.  CLONOS_GATHER_SEG: 0 never, 1
-  // when there are at least 1.5 runs per log (default), 2 always (A/B).
-  const int gather_seg = [] {  // (read at engine creation)
-    const char* e = getenv("CLONOS_GATHER_SEG");
-    return e ? atoi(e) : 1;
-  }();
-  std::vector<uint32_t> gs_idx;
-  bool plan_gather_seg(const std::vector<clg::SegSpan>& runs, std::vector<clg::SegSpan>& sorted,
-                       std::vector<clg::GatherGroup>& groups, uint32_t* n_items) {
-    const int mode = gather_seg;
-    if (mode == 0 || runs.empty()) return false;
-    const uint32_t Cb = C();
-    gs_idx.resize(runs.size());
-    for (uint32_t i = 0; i < runs.size(); ++i) gs_idx[i] = i;
-    std::stable_sort(gs_idx.begin(), gs_idx.end(),
-                     [&](uint32_t a, uint32_t b) { return runs[a].segtab_off < runs[b].segtab_off; });
-    groups.clear();
-    sorted.clear();
-    sorted.reserve(runs.size());
-    uint64_t items = 0;
-    for (size_t i = 0; i < gs_idx.size();) {
-      size_t j = i;
-      uint32_t lo = UINT32_MAX, hi = 0;
-      while (j < gs_idx.size() && runs[gs_idx[j]].segtab_off == runs[gs_idx[i]].segtab_off) {
-        const clg::SegSpan& r = runs[gs_idx[j]];
-        lo = std::min(lo, r.phys / Cb);
-        hi = std::max(hi, uint32_t((uint64_t(r.phys) + r.len - 1) / Cb + 1));
-        sorted.push_back(r);
-        ++j;
-      }
-      groups.push_back(clg::GatherGroup{runs[gs_idx[i]].segtab_off, lo, uint32_t(items), uint32_t(i), uint32_t(j)});
-      items += hi - lo;
-      i = j;
-    }
-    if (items >= (1ull << 31)) return false;
-    if (mode == 1 && groups.size() * 3 > runs.size() * 2) return false;
-    *n_items = uint32_t(items);
-    return true;
-  }
-  std::vector<clg::SegSpan> gs_runs;
-  std::vector<clg::GatherGroup> gs_groups;
-  // The segment-major plan's descriptors: sorted runs | segment table | groups.
-  static size_t gather_seg_layout(size_t n_runs, size_t n_segtab, size_t n_groups, size_t o[3]) {
-    o[0] = 0;
-    o[1] = al16(n_runs * sizeof(clg::SegSpan));
-    o[2] = al16(o[1] + n_segtab * 4);
-    return o[2] + n_groups * sizeof(clg::GatherGroup);
-  }
-  void gather_seg_fill(uint8_t* h, const std::vector<uint32_t>& segtab, const size_t o[3]) {
-    memcpy(h + o[0], gs_runs.data(), gs_runs.size() * sizeof(clg::SegSpan));
-    memcpy(h + o[1], segtab.data(), segtab.size() * 4);
-    memcpy(h + o[2], gs_groups.data(), gs_groups.size() * sizeof(clg::GatherGroup));
-  }
-  int gather_seg_launch(const uint8_t* d, const size_t o[3], uint32_t n_items, uint8_t* out, hipStream_t on) {
-    return clg::launch_gather_seg(reinterpret_cast<const clg::GatherGroup*>(d + o[2]), uint32_t(gs_groups.size()),
-                                  n_items, reinterpret_cast<const clg::SegSpan*>(d + o[0]),
-                                  reinterpret_cast<const uint32_t*>(d + o[1]), pool, C(), out, on);
-  }
-
   // Batched gather from runs: pieces are generated on the device (k_expand_pieces).
   int run_gather_runs(const std::vector<clg::SegSpan>& runs, const std::vector<uint32_t>& segtab, uint32_t n_pieces,
                       uint64_t total, void* out, uint32_t out_kind) {
     if (runs.empty() || !n_pieces) return CLG_OK;
     if (out_kind == CLG_MEM_DEVICE && (cfg.flags & CLG_F_ASYNC_SLICE))
       return gather_runs_async(runs, segtab, n_pieces, total, out);
-    uint32_t n_items = 0;
-    if (plan_gather_seg(runs, gs_runs, gs_groups, &n_items)) {
-      size_t o[3];
-      const size_t hb = gather_seg_layout(gs_runs.size(), segtab.size(), gs_groups.size(), o);
-      CHK(h_desc.ensure(hb));
-      CHK(d_desc.ensure(hb));
-      gather_seg_fill(h_desc.as<uint8_t>(), segtab, o);
-      HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, hb, hipMemcpyHostToDevice, stream));
-      uint8_t* dout;
-      if (out_kind == CLG_MEM_DEVICE) {
-        dout = static_cast<uint8_t*>(out);
-      } else {
-        CHK(d_out.ensure(total));
-        dout = d_out.as<uint8_t>();
-      }
-      CHK(timed("slice_gather", 2 * total, [&] { return gather_seg_launch(d_desc.as<uint8_t>(), o, n_items, dout, stream); }));
-      if (out_kind != CLG_MEM_DEVICE) HIPCHK(hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, stream));
-      return sync();
-    }
     size_t o[2];
     const size_t hb = gather_desc_layout(runs, segtab, o);
     CHK(h_desc.ensure(hb));
@@ -1316,23 +1239,6 @@ struct clg_engine {
     const uint32_t set = gseq++ & 1u;
     if (gdone[set]) HIPCHK(hipEventSynchronize(gdone[set]));  // the gather two calls ago released this set
     else HIPCHK(hipEventCreateWithFlags(&gdone[set], hipEventDisableTiming));
-    uint32_t n_items = 0;
-    if (plan_gather_seg(runs, gs_runs, gs_groups, &n_items)) {
-      size_t o[3];
-      const size_t hb = gather_seg_layout(gs_runs.size(), segtab.size(), gs_groups.size(), o);
-      PinBuf& hd = h_gdesc[set];
-      DevBuf& dd = d_gdesc[set];
-      CHK(hd.ensure(hb));
-      CHK(dd.ensure(hb));
-      gather_seg_fill(hd.as<uint8_t>(), segtab, o);
-      HIPCHK(hipMemcpyAsync(dd.p, hd.p, hb, hipMemcpyHostToDevice, gstream));
-      CHK(timed("slice_gather", 2 * total, [&] {
-        return gather_seg_launch(dd.as<uint8_t>(), o, n_items, static_cast<uint8_t*>(out), gstream);
-      }, gstream));
-      HIPCHK(hipEventRecord(gdone[set], gstream));
-      g_pending = true;
-      return CLG_OK;
-    }
     size_t o[2];
     const size_t hb = gather_desc_layout(runs, segtab, o);
     PinBuf& hd = h_gdesc[set];
@@ -3533,7 +3439,12 @@ int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) 
     std::vector<std::vector<uint32_t>> freed(P), later(P);
     std::vector<int> st(P, CLG_OK);
     wp->run([&](unsigned k, unsigned) {
-      for (size_t i = k * per; i < std::min(nl, (k + 1) * per); ++i) {
+      const size_t i1 = std::min(nl, (k + 1) * per);
+      for (size_t i = k * per; i < i1; ++i) {
+        if (i + 8 < i1) {  // the Log objects ahead (per-log work is bound by their cache misses)
+          const char* q = reinterpret_cast<const char*>(&e->logs[i + 8]);
+          for (size_t b = 0; b < sizeof(Log); b += 64) __builtin_prefetch(q + b, 1);
+        }
         Log& l = e->logs[i];
         if (!l.open || l.job != job) continue;
         bool shared = false;
@@ -3724,11 +3635,14 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
   std::vector<uint32_t> slot;  // entry index + 1 (0: empty)
   uint64_t mask = 0;
   const clg_response* indexed = nullptr;
-  auto hkey = [](const IdKey& k) {
-    uint64_t h = uint64_t(uint16_t(k.v)) * 0x9E3779B97F4A7C15ull ^ uint64_t(k.main) << 17 ^ uint64_t(uint8_t(k.sub)) << 25;
-    h ^= uint64_t(k.lo) * 0xC2B2AE3D27D4EB4Full;
-    h ^= uint64_t(k.hi) * 0x165667B19E3779F9ull;
-    return h ^ h >> 31;
+  auto hkey = [](const IdKey& k) {  // splitmix64 finaliser over the fields (a vertex's keys differ in sub only)
+    auto mix = [](uint64_t z) {
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return z ^ (z >> 31);
+    };
+    return mix(mix(uint64_t(uint16_t(k.v)) | uint64_t(k.main) << 16 | uint64_t(uint8_t(k.sub)) << 24 ^ uint64_t(k.lo)) ^
+               uint64_t(k.hi));
   };
   auto same = [](const IdKey& a, const IdKey& b) {
     return a.v == b.v && a.main == b.main && a.sub == b.sub && a.lo == b.lo && a.hi == b.hi;
@@ -3754,6 +3668,7 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
       if (same(keys[slot[h] - 1], k)) return Piece{r->entries[slot[h] - 1].bytes, r->entries[slot[h] - 1].len};
     return Piece{nullptr, 0};
   };
+  subs.reserve(1024);
   for (uint32_t i = 0; i < n; ++i) {
     if (v[i].n_subpartitions && !v[i].subpartitions) return fail(CLG_E_INVALID_ARG, "null subpartition table");
     clg_causal_log_id mid{};

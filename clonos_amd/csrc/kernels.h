@@ -365,17 +365,6 @@ int launch_decode_prep(PrepArgs a, void* stream);
 // ---- launchers (kernels.hip) -----------------------------------------------------------
 int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream);
-// Segment-major gather: the runs of one log (one segment table entry range) form a group; a
-// block per (group, segment) copies that segment's part of every run of the group, so a
-// segment several consumers slice is read from HBM once and from L2 after.
-struct GatherGroup {
-  uint64_t segtab_off;  // the log's segment indices in the call's table
-  uint32_t seg_lo;      // first segment any run of the group touches
-  uint32_t item0;       // first block (prefix over groups)
-  uint32_t run0, run1;  // the group's runs in the sorted run list
-};
-int launch_gather_seg(const GatherGroup* d_groups, uint32_t n_groups, uint32_t n_items, const SegSpan* d_runs,
-                      const uint32_t* d_segtab, const uint8_t* pool, uint32_t seg_bytes, uint8_t* d_out, void* stream);
 // Robust pipeline (per-byte DP transfer tables); runs only on spans whose flag is set
 // (d_span_flags == nullptr: all spans).
 int launch_decode_tables(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans,

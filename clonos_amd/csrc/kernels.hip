@@ -114,31 +114,6 @@ __global__ __launch_bounds__(256) void k_gather(const GatherPiece* __restrict__ 
   copy_range<256>(p.src, out + p.dst, p.len, threadIdx.x);
 }
 
-// Segment-major gather (GatherGroup): block -> (group, segment) by a binary search over the
-// groups' first blocks; the segment's part of each of the group's runs, one after the other
-// (the first copy brings the segment into L2, the others hit it).
-__global__ __launch_bounds__(256) void k_gather_seg(const GatherGroup* __restrict__ groups, uint32_t n_groups,
-                                                    const SegSpan* __restrict__ runs, const uint32_t* __restrict__ segtab,
-                                                    const uint8_t* __restrict__ pool, uint32_t C,
-                                                    uint8_t* __restrict__ out) {
-  const uint32_t item = blockIdx.x;
-  uint32_t lo = 0, hi = n_groups;  // last group with item0 <= item
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (groups[mid].item0 <= item) lo = mid; else hi = mid;
-  }
-  const GatherGroup g = groups[lo];
-  const uint32_t w = g.seg_lo + (item - g.item0);
-  const uint64_t s0 = (uint64_t)w * C, s1 = s0 + C;
-  const uint8_t* src = pool + (size_t)segtab[g.segtab_off + w] * C;
-  for (uint32_t r = g.run0; r < g.run1; ++r) {
-    const SegSpan run = runs[r];
-    const uint64_t a = run.phys > s0 ? run.phys : s0;
-    const uint64_t e = (uint64_t)run.phys + run.len < s1 ? (uint64_t)run.phys + run.len : s1;
-    if (a < e) copy_range<256>(src + (a - s0), out + run.dst + (a - run.phys), (uint32_t)(e - a), threadIdx.x);
-  }
-}
-
 // ==================================================================================
 // Device-side planning: item g -> its run (binary search over first) -> window.
 // ==================================================================================
@@ -842,14 +817,6 @@ int launch_decode_prep(PrepArgs a, void* stream) {
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream) {
   if (!n) return CLG_OK;
   hipLaunchKernelGGL(k_gather, dim3(n), dim3(256), 0, (hipStream_t)stream, d_pieces, d_out);
-  return ok(hipGetLastError());
-}
-
-int launch_gather_seg(const GatherGroup* d_groups, uint32_t n_groups, uint32_t n_items, const SegSpan* d_runs,
-                      const uint32_t* d_segtab, const uint8_t* pool, uint32_t seg_bytes, uint8_t* d_out, void* stream) {
-  if (!n_items) return CLG_OK;
-  hipLaunchKernelGGL(k_gather_seg, dim3(n_items), dim3(256), 0, (hipStream_t)stream, d_groups, n_groups, d_runs, d_segtab,
-                     pool, seg_bytes, d_out);
   return ok(hipGetLastError());
 }
 

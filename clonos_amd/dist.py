@@ -345,6 +345,23 @@ class MergedCopies:
         return {g: self.bytes_of(g) for g in self.place}
 
 
+_GROUP_INFO: Dict[int, tuple] = {}
+
+
+def _group_info(group) -> Tuple[int, int, str]:
+    """(rank, world size, backend) of a process group, looked up once per group object (each
+    torch.distributed query goes through its logging wrapper: ~10 us apiece on the merge's
+    critical path).  The entry holds the group itself, so a re-initialised default group
+    (a new object) is looked up afresh."""
+    import torch.distributed as dist
+    g = group if group is not None else dist.group.WORLD
+    got = _GROUP_INFO.get(id(g))
+    if got is None or got[0] is not g:
+        got = (g, dist.get_rank(group), dist.get_world_size(group), dist.get_backend(group))
+        _GROUP_INFO[id(g)] = got
+    return got[1], got[2], got[3]
+
+
 def copy_arrays(copies) -> Tuple[np.ndarray, np.ndarray]:
     """merge_responses' `copies` as (gids ascending, handles): from a dict gid -> handle, or
     already such a pair (a caller that merges every step converts its dict once)."""
@@ -379,10 +396,9 @@ def merge_responses(io, table: LogTable, failed: Sequence[int], copies,
     import torch
     import torch.distributed as dist
     t_in = _time.perf_counter()
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rank, world, backend = _group_info(group)
     if world > 255:
         raise ValueError("rank must fit the packed key's low byte")
-    backend = dist.get_backend(group)
     # every per-log step below is an array operation: a failed task has 129 logs at p=128
     fv = np.unique(np.fromiter((int(v) for v in failed), np.int64))
     gids = table.gids_of(fv)

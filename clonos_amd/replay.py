@@ -210,25 +210,31 @@ def merged_responses(merged, table, vertices: Sequence[int]) -> Dict[int, Determ
     vert = table.vertex[gids] if len(gids) else np.zeros(0, np.int64)
     order = np.argsort(vert, kind="stable")
     vs = vert[order]
-    ids_o = np.ascontiguousarray(ids[gids[order]], LOG_ID)
+    # (rows moved as raw words: fancy indexing the structured array took 0.13 ms for 2 k rows)
+    ids_o = np.take(ids.view(np.uint64).reshape(len(ids), -1), gids[order], axis=0).view(LOG_ID).reshape(-1)
     ptr_o = np.ascontiguousarray(np.asarray(merged.offs, np.uint64)[order] + np.uint64(merged.buf.data_ptr()))
     len_o = np.ascontiguousarray(np.asarray(merged.lens, np.uint64)[order])
-    # each vertex's byte totals, for prepare_replay_raw's output sizes (prefix sums, once)
-    c_all = np.concatenate([[0], np.cumsum(len_o, dtype=np.uint64)]).tolist()
-    c_main = np.concatenate([[0], np.cumsum(np.where(ids_o["is_main"] != 0, len_o, 0), dtype=np.uint64)]).tolist()
     out = {}
     va = np.asarray(list(vertices), np.int64)
-    los = np.searchsorted(vs, va, "left").tolist()
-    his = np.searchsorted(vs, va, "right").tolist()
+    lo_a = np.searchsorted(vs, va, "left")
+    hi_a = np.searchsorted(vs, va, "right")
+    los, his = lo_a.tolist(), hi_a.tolist()
+    # each vertex's byte totals, for prepare_replay_raw's output sizes (prefix sums, once)
+    c_all = np.zeros(len(len_o) + 1, np.uint64)
+    np.cumsum(len_o, out=c_all[1:])
+    c_main = np.zeros(len(len_o) + 1, np.uint64)
+    np.cumsum(np.where(ids_o["is_main"] != 0, len_o, np.uint64(0)), out=c_main[1:])
+    t_all = (c_all[hi_a] - c_all[lo_a]).tolist()
+    t_main = (c_main[hi_a] - c_main[lo_a]).tolist()
     # one put per vertex into the three arrays above (pointer arithmetic, no per-vertex views)
     pi, pp, pl, isz = ids_o.ctypes.data, ptr_o.ctypes.data, len_o.ctypes.data, ids_o.itemsize
     keep = (merged.buf, ids_o, ptr_o, len_o)
-    for v, lo, hi in zip(va.tolist(), los, his):
+    for v, lo, hi, tm, ta in zip(va.tolist(), los, his, t_main, t_all):
         ev = DeterminantResponseEvent(True, v, capacity=max(1, hi - lo))
         if hi > lo:
             ev._keep.append(keep)
             check(lib.clg_response_put_batch(C.byref(ev._c), pi + lo * isz, pp + lo * 8, pl + lo * 8, hi - lo))
-        ev._bytes = (int(c_main[hi] - c_main[lo]), int(c_all[hi] - c_all[lo]))
+        ev._bytes = (tm, ta)
         out[v] = ev
     return out
 
