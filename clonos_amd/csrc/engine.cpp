@@ -2576,7 +2576,20 @@ struct clg_engine {
     std::function<void(DecodePlan&, uint32_t)> build;
     int status = CLG_OK;  // its result, for the clg_decode_wait that pairs with it
     std::string err;      // and its error text
+    int64_t min_epoch = INT64_MIN;  // the smallest start epoch it decodes from (INT64_MIN: unknown)
   };
+  // clg_truncate_all while decodes are queued (their ranges start at or above the checkpoint):
+  // the segments it frees wait here until no decode is queued (the queued kernels may still
+  // read them), and the logs' rebase generation tells a queued decode that re-plans (an abort's
+  // fallback) to look its ranges up again
+  std::vector<uint32_t> free_later;
+  uint64_t rebase_gen = 0;
+  int64_t q_min_epoch = INT64_MIN;  // clg_decode_logs_async -> decode_async: the call's smallest start epoch
+  void release_later() {
+    if (free_later.empty() || any_active()) return;
+    free_segs.insert(free_segs.end(), free_later.begin(), free_later.end());
+    free_later.clear();
+  }
   std::deque<PendingDecode> pq;  // queued by clg_decode_logs_async, not yet waited for (oldest first)
   // the largest queued plan so far (the scratch is sized for it): a larger one is queued only
   // once nothing is in flight, since growing a buffer frees the one the GPU may still read
@@ -2598,11 +2611,18 @@ struct clg_engine {
     pq.push_back(std::move(d));
     return CLG_OK;
   }
+  // queued decodes' plans, recycled (a config-4 plan is ~4 MB: fresh pages cost page faults)
+  std::vector<DecodePlan> plan_pool;
   int decode_async(std::function<void(DecodePlan&, uint32_t)> build, uint64_t log_bytes, clg_decoded* out,
-                   uint64_t* span_rec_base) {
+                   uint64_t* span_rec_base, DecodePlan* prebuilt = nullptr) {
     const bool fast = fused_decode && log_bytes / 2 < (1ull << 31);
     DecodePlan pf;
-    if (fast) build(pf, clg::kZTile);
+    if (prebuilt) {
+      pf = std::move(*prebuilt);  // (the fast plan, kZTile tiles)
+    } else if (fast) {
+      HostTimer hp(this, "host_decode_plan");
+      build(pf, clg::kZTile);
+    }
     const bool queue = fast && !pf.spans.empty() && fused_fits(pf);
     // what the queued decodes' completions need must not be overwritten by this one's kernels:
     // host outputs go through shared staging arrays, and a scratch buffer that has to grow
@@ -2646,6 +2666,7 @@ struct clg_engine {
     d.out = out;
     d.span_rec_base = span_rec_base;
     d.build = std::move(build);
+    d.min_epoch = q_min_epoch;
     pq.push_back(std::move(d));
     return CLG_OK;
   }
@@ -2680,8 +2701,13 @@ struct clg_engine {
       d.status = st;
       if (st != CLG_OK) d.err = g_err;
       d.build = nullptr;
+      if (plan_pool.size() < kSlots) {
+        d.plan.reset();
+        plan_pool.push_back(std::move(d.plan));
+      }
       d.plan = DecodePlan();
     }
+    release_later();
     return CLG_OK;  // the decodes' own statuses go to clg_decode_wait
   }
   // clg_decode_wait: the oldest queued decode, completed; its status
@@ -2691,6 +2717,7 @@ struct clg_engine {
     const int st = pq.front().status;
     if (st != CLG_OK) *err = pq.front().err;
     pq.pop_front();
+    release_later();
     return st;
   }
 
@@ -3420,12 +3447,30 @@ int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int3
 }
 
 int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) {  // JobCausalLogImpl :230-246
-  ENGINE_GUARD(e);
+  // Beside queued asynchronous decodes whose ranges start at or above cp (config 4's step:
+  // the host truncates while the GPU decodes the new epoch): the truncation only drops bytes
+  // below cp, so the queued kernels read nothing it frees -- its segments return to the pool
+  // once those decodes complete.  Otherwise (a decode from below cp, appends not yet flushed)
+  // the queued decodes complete first.
+  ENGINE_GUARD_KEEP(e);
+  bool defer = false;
+  if (e->any_active()) {
+    int64_t mn = INT64_MAX;
+    for (const auto& d : e->pq)
+      if (d.active) mn = std::min(mn, d.min_epoch);
+    const bool dirty = !e->dirty.empty();  // (appends not yet flushed: the flush below writes segments)
+    if (cp > mn || dirty) CHK(e->settle());
+    else defer = true;
+  } else {
+    e->release_later();
+  }
   if (applied) *applied = 0;
   if (job >= e->jobs.size() || !e->jobs[job].open) return fail(CLG_E_NO_LOG, "unknown job %u", job);
   Job& j = e->jobs[job];
   if (j.latest_cp >= cp) return CLG_OK;  // the CAS: only a newer checkpoint fans out
   j.latest_cp = cp;
+  ++e->rebase_gen;
+  std::vector<uint32_t>& to = defer ? e->free_later : e->free_segs;
   CHK(e->flush());
   clg_engine::HostTimer ht(e, "host_truncate_all");
   if (e->logs.size() >= clg_engine::kParallelLogs) {
@@ -3460,18 +3505,18 @@ int clg_truncate_all(clg_engine* e, uint32_t job, int64_t cp, int32_t* applied) 
       }
     });
     ht.lap("host_trunc_pool");
-    for (unsigned k = 0; k < P; ++k) e->free_segs.insert(e->free_segs.end(), freed[k].begin(), freed[k].end());
+    for (unsigned k = 0; k < P; ++k) to.insert(to.end(), freed[k].begin(), freed[k].end());
     for (unsigned k = 0; k < P; ++k)
       if (st[k] != CLG_OK) return fail(st[k], "checkpoint completion failed on a log (state outside its bounds)");
     size_t n_later = 0;
     for (unsigned k = 0; k < P; ++k) {
       n_later += later[k].size();
-      for (uint32_t i : later[k]) CHK(e->checkpoint_complete(e->logs[i], cp));
+      for (uint32_t i : later[k]) CHK(e->checkpoint_complete(e->logs[i], cp, to));
     }
     ht.lap(n_later ? "host_trunc_later" : "host_trunc_free");
   } else {
     for (auto& l : e->logs)
-      if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp));
+      if (l.open && l.job == job) CHK(e->checkpoint_complete(l, cp, to));
   }
   if (applied) *applied = 1;
   return CLG_OK;
@@ -3551,22 +3596,63 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
     return fail(CLG_E_STATE, "%d asynchronous decodes are not waited for (clg_decode_wait)", CLG_DECODE_MAX_INFLIGHT);
   CHK(e->flush());  // (stream-ordered after the queued decodes, past their ranges)
   std::vector<uint32_t> hs(log, log + n);
-  std::vector<int32_t> st(n), nb(n);
+  std::vector<int32_t> st, nb;
   uint64_t total = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    Log* l;
-    CHK(e->get_log(log[i], &l));
-    if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
-    total += uint64_t(nb[i]);
+  // many logs: the ranges and the fast plan on the host threads (clg_decode_logs' way), into
+  // a recycled plan
+  clg_engine::DecodePlan pf;
+  if (!e->plan_pool.empty()) {
+    pf = std::move(e->plan_pool.back());
+    e->plan_pool.pop_back();
   }
-  // by value: the robust fallback may re-plan when the decode is settled (the logs' ranges
-  // cannot change before that: every call that could change them settles first)
-  auto build = [e, hs = std::move(hs), st = std::move(st), nb = std::move(nb)](clg_engine::DecodePlan& p, uint32_t T) {
+  pf.reset();
+  bool planned = false;
+  if (n >= clg_engine::kParallelLogs && e->fused_decode) {
+    clg_engine::HostTimer ht(e, "host_decode_plan");
+    e->zst.assign(n, 0);  // (plan_parallel's ranges go here)
+    e->znb.assign(n, 0);
+    planned = e->plan_parallel(pf, log, start_epoch, n, &total);
+  }
+  if (planned) {
+    st.assign(e->zst.begin(), e->zst.begin() + n);
+    nb.assign(e->znb.begin(), e->znb.begin() + n);
+  } else {
+    total = 0;
+    st.assign(n, 0);
+    nb.assign(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      Log* l;
+      CHK(e->get_log(log[i], &l));
+      if (l->depth != 0) CHK(e->determinants_range(*l, start_epoch[i], &st[i], &nb[i]));
+      total += uint64_t(nb[i]);
+    }
+  }
+  // by value: the robust fallback may re-plan when the decode is settled.  Only a checkpoint
+  // truncation at or below every start epoch runs before that (clg_truncate_all settles
+  // otherwise); it rebases the logs, and a re-plan after it looks the ranges up again (the
+  // same bytes at their new offsets)
+  int64_t mn = INT64_MAX;
+  for (uint32_t i = 0; i < n; ++i) mn = std::min(mn, start_epoch[i]);
+  std::vector<int64_t> eps(start_epoch, start_epoch + n);
+  auto build = [e, hs = std::move(hs), st = std::move(st), nb = std::move(nb), eps = std::move(eps),
+                gen = e->rebase_gen](clg_engine::DecodePlan& p, uint32_t T) {
     p.spans.reserve(hs.size());
     p.runs.reserve(hs.size());
-    for (uint32_t i = 0; i < uint32_t(hs.size()); ++i) e->plan_log_span(p, e->logs[hs[i]], st[i], nb[i], i, T);
+    for (uint32_t i = 0; i < uint32_t(hs.size()); ++i) {
+      int32_t s = st[i], b = nb[i];
+      const Log& l = e->logs[hs[i]];
+      if (gen != e->rebase_gen && l.depth != 0 && e->determinants_range(l, eps[i], &s, &b) != CLG_OK) s = b = 0;
+      e->plan_log_span(p, l, s, b, i, T);
+    }
   };
-  return e->decode_async(build, total, out, span_rec_base);
+  e->q_min_epoch = n ? mn : INT64_MAX;
+  const int rc = e->decode_async(build, total, out, span_rec_base, planned ? &pf : nullptr);
+  e->q_min_epoch = INT64_MIN;
+  if (pf.spans.capacity() && e->plan_pool.size() < clg_engine::kSlots) {  // (not queued: the plan back)
+    pf.reset();
+    e->plan_pool.push_back(std::move(pf));
+  }
+  return rc;
 }
 
 int clg_decode_wait(clg_engine* e) {

@@ -277,3 +277,38 @@ def test_two_in_flight_device_outputs(mix):
         if mix == "config3":
             assert eng.kernel_stats().get("decode_async_redo", {}).get("launches", 0) >= 1
         eng.close()
+
+
+@pytest.mark.parametrize("kind", ["config2", "config3"])
+def test_truncate_beside_queued_decode(kind):
+    """clg_truncate_all while an asynchronous decode from the checkpoint epoch is queued (config
+    4's step): the decode's records equal the oracle's decode of the epochs it asked for, the
+    segments the truncation freed go back to the pool only once the decode is waited for, and a
+    fast run that aborts (config 3: the Serializable tables first) re-plans over the rebased
+    logs.  A truncation above a queued decode's start epoch completes that decode first."""
+    rng = np.random.default_rng(11)
+    if kind == "config2":
+        gen = lambda n: synth.config2_log(n, rng)[0]  # noqa: E731
+    else:
+        gen = lambda n: synth.config3_epoch(n, rng)[0]  # noqa: E731
+    n_logs, n_ep = 6, 4
+    with Engine(segment_bytes=1024, pool_segments=1 << 14) as eng:
+        logs = [eng.open_log(CausalLogID.main(v)) for v in range(n_logs)]
+        parts = [[] for _ in range(n_logs)]
+        for ep in range(n_ep):
+            for v, lg in enumerate(logs):
+                b = bytes(gen(int(rng.integers(200, 3000))))
+                lg.processUpstreamDelta(b, 0, ep)
+                parts[v].append(b)
+        used0, _ = eng.pool_stats()
+        pd = eng.decode_logs_async(logs, [2] * n_logs)
+        assert eng.truncate_all(2)
+        got = pd.wait()
+        check_oracle(got, [b"".join(p[2:]) for p in parts])
+        used1, _ = eng.pool_stats()
+        assert used1 < used0
+        same(eng.decode_logs(logs, [2] * n_logs), got)
+        pd = eng.decode_logs_async(logs, [2] * n_logs)
+        assert eng.truncate_all(3)  # above the queued decode's start: it completes first
+        same(pd.wait(), got)
+        check_oracle(eng.decode_logs(logs, [3] * n_logs), [b"".join(p[3:]) for p in parts])

@@ -629,3 +629,9 @@ def test_many_span_decode_chunked_on_host_threads():
         for s in list(range(0, n_logs, 97)) + [n_logs - 1]:
             assert_span_equal(dec, s, blobs[s])
         assert dec.n_rec == sum(len(O.decode(b)[1]["tag"]) for b in blobs[::1])
+        # the asynchronous decode of the same batch plans on the host threads too (twice: the
+        # second reuses the first's recycled plan): the same records
+        for _ in range(2):
+            got = eng.decode_logs_async(logs, [0] * n_logs).wait()
+            for f in ("off", "tag", "v0", "w_idx", "w_rc", "w_v1", "w_var_off", "w_var_len", "w_sub", "span_rec_base"):
+                np.testing.assert_array_equal(getattr(got, f), getattr(dec, f), err_msg=f)
