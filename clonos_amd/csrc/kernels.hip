@@ -162,12 +162,23 @@ __global__ __launch_bounds__(256) void k_expand_tiles(const SegSpan* __restrict_
 // or five memsets, each a few microseconds of launch on the decode's critical path): item i
 // < n_tiles expands tile i from the runs, the rest walk the word ranges in order (a copy
 // where src is set, else a fill with val).
+// A batch of few runs (config 2: 64 logs) searches them in LDS: from HBM the binary search
+// was a chain of dependent loads, and beside the previous step's slice gather each took
+// microseconds (the prep ran 30-95 us on the decode's critical path).
+constexpr uint32_t kPrepLdsRuns = 256;
 __global__ __launch_bounds__(256) void k_decode_prep(PrepArgs a) {
+  __shared__ SegSpan s_runs[kPrepLdsRuns];
+  const SegSpan* runs = a.runs;
+  if (a.n_tiles && a.n_runs <= kPrepLdsRuns) {
+    for (uint32_t i = threadIdx.x; i < a.n_runs; i += blockDim.x) s_runs[i] = a.runs[i];
+    __syncthreads();
+    runs = s_runs;
+  }
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.total; i += stride) {
     uint64_t k = i;
     if (k < a.n_tiles) {
-      expand_tile(a.runs, a.n_runs, a.segtab, a.pool, a.C, a.U, a.tiles, (uint32_t)k);
+      expand_tile(runs, a.n_runs, a.segtab, a.pool, a.C, a.U, a.tiles, (uint32_t)k);
       continue;
     }
     k -= a.n_tiles;
