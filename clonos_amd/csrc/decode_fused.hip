@@ -2557,6 +2557,111 @@ __device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles,
   }
 }
 
+// The same single launch with a block per tile, for small batches whose spans run over more
+// tiles (config 5's replay-prep decode: 16 main logs of ~45 KB, 6 tiles each, which the
+// three-pass sequence decoded in ~0.1 ms of launches and queue gaps).  Every block stages its
+// tile and walks it speculatively at once; then it takes its entry from the tile before's
+// published exit (the span start for a span's first tile), finishes the count, publishes its
+// exit and counts, sums every earlier tile's counts (look-back) and emits its tile from the
+// image it holds.  Blocks wait only on lower ones (dispatched first), so the waits end.  agg:
+// counts at [t], exits at [nt + t] (nt <= kZSmallSpans / 2).  res[3 + s] for the spans with
+// tiles (the host fills the empty ones).
+__device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ tiles,
+                                                   const SpanDesc* __restrict__ spans, uint32_t nt, const FusedCtl& ctl,
+                                                   const DecodeOut& out, uint64_t* agg, uint64_t* agg_next,
+                                                   uint64_t* res) {
+  __shared__ EmitLds<false, true> L;
+  const uint32_t t = blockIdx.x, lane = threadIdx.x;
+  for (uint32_t j = t + nt * lane; j < kZSmallSpans; j += 64u * nt) agg_next[j] = 0;
+  const ZTile z = ztile(tiles, spans, t, lane);
+  const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
+  stage_image(z.td, z.sd, t, tiles, L.img, lane, z.hi, &n1);
+  const JL jl{nullptr, nullptr, nullptr};
+  const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane), wsb = warm_start(lane * kZRegion + 64u, z.lo, ctl.warm, lane);
+  const SpecR sp = z.rs < z.re ? spec_walk_fast<false>(L.img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl,
+                                                       ctl.lean != 0u)
+                               : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+  // the entry: the span start, or the tile before's exit (one lane polls)
+  uint64_t xs = z.td.span_off;
+  bool bad = false;
+  if (!z.first) {
+    uint64_t v = 0;
+    if (lane == 0) {
+      const uint64_t w0 = __builtin_amdgcn_s_memtime();
+      while (!((v = ld_agent(&agg[nt + t - 1])) & kZAggSet)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
+          v = kZAggSet | kZAggBad;
+          break;
+        }
+      }
+    }
+    v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    bad = (v & kZAggBad) != 0ull;
+    xs = v & kZAggCnt;
+  }
+  uint64_t c = 0, x = 0, bm[2] = {0, 0};
+  if (!bad) {
+    const uint64_t ee = xs - z.td.span_off + z.lo;
+    const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+    uint32_t x_true;
+    const uint32_t why = count_tile<false>(t, z, e_true, kZCanon, ctl, L.img, lane, &x_true, jl, tiles, &sp, &c, bm);
+    x = z.td.span_off + (x_true - z.lo);
+    bad = why != 0u;
+  }
+  if (lane == 0) {
+    st_agent(&agg[nt + t], kZAggSet | (bad ? kZAggBad : 0ull) | (x & kZAggCnt));
+    st_agent(&agg[t], kZAggSet | (bad ? kZAggBad : 0ull) | c);
+  }
+  // look-back: every earlier tile's counts
+  uint64_t pre = 0;
+  bool any_bad = bad;
+  for (uint32_t j0 = 0; j0 < t && !any_bad; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    uint64_t v = 0;
+    if (j < t) {
+      const uint64_t w0 = __builtin_amdgcn_s_memtime();
+      while (!((v = ld_agent(&agg[j])) & kZAggSet)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
+          v = kZAggSet | kZAggBad;
+          break;
+        }
+      }
+    }
+    any_bad = __any((v & kZAggBad) != 0ull);
+    uint64_t cj = v & kZAggCnt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cj += __shfl_xor(cj, off);
+    pre += cj;
+  }
+  if (any_bad) {
+    if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  emit_tile<false, true>(tiles, spans, ctl, out, t, lane, pre, L, bm);
+  if (lane == 0) {
+    if (z.first) res[3 + z.td.span] = pre;
+    if (t + 1 == nt) {
+      res[0] = (pre + c) & ((1ull << 31) - 1);
+      res[1] = (pre + c) >> 31;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_decode_small_tiles(const TileDesc* __restrict__ tiles,
+                                                           const SpanDesc* __restrict__ spans, uint32_t n_tiles,
+                                                           FusedCtl ctl, DecodeOut out, uint64_t* agg,
+                                                           uint64_t* agg_next, uint64_t* res) {
+  decode_small_tiles(tiles, spans, n_tiles, ctl, out, agg, agg_next, res);
+}
+__global__ __launch_bounds__(64) void k_decode_small_tiles_arg(const SmallPlanArg plan, uint32_t n_tiles, FusedCtl ctl,
+                                                               DecodeOut out, uint64_t* agg, uint64_t* agg_next,
+                                                               uint64_t* res) {
+  decode_small_tiles(plan.tiles, plan.spans, n_tiles, ctl, out, agg, agg_next, res);
+}
+
 __global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
                                                      const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
                                                      DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
@@ -2570,9 +2675,21 @@ __global__ __launch_bounds__(64) void k_decode_small_arg(const SmallPlanArg plan
 
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
-                        const SmallPlanArg* plan) {
+                        const SmallPlanArg* plan, bool per_tile) {
   if (!n_spans) return CLG_OK;
   ctl.n_tiles = n_tiles;
+  if (per_tile) {
+    if (!n_tiles || 2 * n_tiles > kZSmallSpans) return CLG_E_INVALID_ARG;
+    if (plan) {
+      if (n_tiles > kZSmallArgTiles || n_spans > kZSmallArgSpans) return CLG_E_INVALID_ARG;
+      hipLaunchKernelGGL(k_decode_small_tiles_arg, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, *plan, n_tiles, ctl,
+                         out, agg, agg_next, res);
+    } else {
+      hipLaunchKernelGGL(k_decode_small_tiles, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_tiles,
+                         ctl, out, agg, agg_next, res);
+    }
+    return launch_status(hipGetLastError());
+  }
   if (plan) {
     if (n_tiles > kZSmallArgTiles || n_spans > kZSmallArgSpans) return CLG_E_INVALID_ARG;
     hipLaunchKernelGGL(k_decode_small_arg, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, *plan, n_spans, ctl, out,

@@ -2148,10 +2148,17 @@ struct clg_engine {
       return false;
     if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
-    for (const auto& sd : p.spans)
-      if (sd.n_tiles > small_max_tiles) return false;
-    return true;
+    bool long_span = false;
+    for (const auto& sd : p.spans) long_span |= sd.n_tiles > small_max_tiles;
+    // spans over more tiles: a block per tile (k_decode_small_tiles), up to its look-back size
+    return !long_span || (small_tiles && 2ull * p.n_tiles <= kSmallSpans);
   }
+  // The per-tile single launch for batches with longer spans (CLONOS_SMALL_TILES=0 turns it
+  // off: a developer switch; such batches then take the three-pass path)
+  const bool small_tiles = [] {
+    const char* v = getenv("CLONOS_SMALL_TILES");
+    return !(v && atoi(v) == 0);
+  }();
   // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered, or
   // its cap / wcap elements reach past its registered range -- the caller's staging path then)
   static bool mapped_outputs(const clg_decoded& out, clg::DecodeOut* o) {
@@ -2193,6 +2200,8 @@ struct clg_engine {
     reset_result(out);
     host_tiles(p);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    bool per_tile = false;  // (small_ok: spans over more tiles than a wave takes -> a block per tile)
+    for (const auto& sd : p.spans) per_tile |= sd.n_tiles > small_max_tiles;
     // the plan: in the launch's arguments when it fits (no copy queued), else one copy
     static const int small_mode = [] {  // developer switch: bit 0 no argument plan
       const char* v = getenv("CLONOS_SMALL_MODE");
@@ -2269,7 +2278,7 @@ struct clg_engine {
     }
     CHK(clg::launch_decode_small(reinterpret_cast<const clg::TileDesc*>(d_plan.p), nt,
                                  reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
-                                 agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr));
+                                 agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr, per_tile));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     hsub.emplace(this, "host_small_wait");
     HIPCHK(hipStreamSynchronize(stream));
@@ -2304,6 +2313,9 @@ struct clg_engine {
     if (span_rec_base) {
       for (uint32_t s = 0; s < ns; ++s) span_rec_base[s] = res[3 + s] & kRecMask;
       span_rec_base[ns] = nrec;
+      if (per_tile)  // (the kernel writes the spans with tiles: an empty span starts where the next one does)
+        for (uint32_t s = ns; s-- > 0;)
+          if (!p.spans[s].n_tiles) span_rec_base[s] = span_rec_base[s + 1];
     }
     if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     out->n_rec = nrec;

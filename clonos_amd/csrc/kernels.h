@@ -297,9 +297,11 @@ struct SmallPlanArg {  // 3 KiB: with the other arguments inside the 4 KiB kerne
   TileDesc tiles[kZSmallArgTiles];
   SpanDesc spans[kZSmallArgSpans];
 };
+// per_tile: a block per tile (spans of any number of tiles; 2 n_tiles <= kZSmallSpans) instead
+// of a wave per span (spans of at most kZSmallTiles tiles).
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
-                        const SmallPlanArg* plan = nullptr);
+                        const SmallPlanArg* plan = nullptr, bool per_tile = false);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one

@@ -12,10 +12,11 @@ from test_gpu_decode import assert_span_equal
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _small_up_to_8_tiles(monkeypatch):
-    """These tests hold spans of up to 8 tiles on the single launch (the default takes 2)."""
-    monkeypatch.setenv("CLONOS_SMALL_MAXTILES", "8")
+@pytest.fixture(autouse=True, params=["8", "1"], ids=["wave_per_span", "block_per_tile"])
+def _small_mode(request, monkeypatch):
+    """Every test twice: spans of up to 8 tiles on the wave-per-span launch (the default takes
+    2), then spans of 2 tiles or more on the block-per-tile launch (k_decode_small_tiles)."""
+    monkeypatch.setenv("CLONOS_SMALL_MAXTILES", request.param)
 
 
 def _eng(**kw):
@@ -209,11 +210,14 @@ def test_pooled_capacity_exceeded_is_decoded_again_sized():
             assert_span_equal(dec, s, data[l])
 
 
-def test_multi_tile_spans_default_to_three_pass(monkeypatch):
-    """By default the single launch takes spans of at most 2 tiles: a batch of 16 config-2
-    logs of ~45 KB (config 5's failed main logs, 6 tiles each) goes three-pass -- one wave
-    per span would walk its six tiles in a row -- with the same result."""
+@pytest.mark.parametrize("per_tile", [True, False])
+def test_multi_tile_spans_default_to_block_per_tile(monkeypatch, per_tile):
+    """By default a wave per span takes spans of at most 2 tiles: a batch of 16 config-2 logs of
+    ~45 KB (config 5's failed main logs, 6 tiles each) goes to the block-per-tile single launch
+    -- or, with it turned off (CLONOS_SMALL_TILES=0), three-pass -- with the same result."""
     monkeypatch.delenv("CLONOS_SMALL_MAXTILES")
+    if not per_tile:
+        monkeypatch.setenv("CLONOS_SMALL_TILES", "0")
     rng = np.random.default_rng(0xC5)
     from clonos_amd import CausalLogID
     with _eng() as eng:
@@ -226,7 +230,10 @@ def test_multi_tile_spans_default_to_three_pass(monkeypatch):
             logs.append(lg)
         eng.kernel_stats_reset()
         dec = eng.decode_logs(logs[:16], [0] * 16)
-        assert _launches(eng, "decode_small") == 0 and _launches(eng, "decode_count") == 1
+        if per_tile:
+            assert _launches(eng, "decode_small") == 1 and _launches(eng, "decode_count") == 0
+        else:
+            assert _launches(eng, "decode_small") == 0 and _launches(eng, "decode_count") == 1
         for s, b in enumerate(bufs):
             assert_span_equal(dec, s, b)
         eng.kernel_stats_reset()
