@@ -241,7 +241,11 @@ int clg_consumer_seek_batch(clg_engine* e, const clg_slice_req* reqs, const int3
 
 /* ---- checkpoint completion fan-out (JobCausalLogImpl.notifyCheckpointComplete :230-246) --
  * CAS on the job's latestCompletedCheckpoint; if newer, truncates every open log of that
- * job (other jobs' logs are untouched). */
+ * job (other jobs' logs are untouched).  Queued asynchronous decodes (clg_decode_logs_async)
+ * whose start epochs are all >= checkpoint_id stay queued: the truncation drops only bytes
+ * below the checkpoint, and the segments it frees return to the pool once those decodes are
+ * waited for.  A queued decode from an earlier epoch (or appends not yet flushed) is
+ * completed first, as by any other call that needs the engine exclusively. */
 int clg_truncate_all(clg_engine* e, uint32_t job, int64_t checkpoint_id, int32_t* applied);
 
 /* ---- batched decode (SimpleDeterminantEncoder.decodeNext over whole spans) -------------
@@ -292,8 +296,8 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
  * are not to be read, until the clg_decode_wait that pairs with this call returns, which
  * completes the decode (fallback paths included) and returns its status.  Every other call
  * that needs the engine exclusively completes the pending decodes first (their statuses are
- * kept for clg_decode_wait); clg_slice_batch into device memory with CLG_F_ASYNC_SLICE and
- * the consumer seeks leave them pending.
+ * kept for clg_decode_wait); clg_slice_batch into device memory with CLG_F_ASYNC_SLICE, the
+ * consumer seeks, and clg_truncate_all at or below every start epoch leave them pending.
  * Up to CLG_DECODE_MAX_INFLIGHT decodes may be queued before the first is waited for, so the
  * GPU runs decode i+1 while the host completes decode i; give each its own output arrays.
  * One more is CLG_E_STATE (no decode's status is ever dropped). */
