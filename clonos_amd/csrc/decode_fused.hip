@@ -2461,118 +2461,27 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
 
 // ---------------------------------------------------------------------------------
 // Small batches in one launch (config 1: an epoch of 44 logs, 73 KB, where the three-pass
-// sequence's ~15 queue operations cost more than the decode).  One wave per span: it counts
-// the span's tiles in order (count_staged: the first tile enters at the span start, each next
-// one at its predecessor's exit), publishes the span's counts, sums the counts of every
-// earlier span (look-back: earlier blocks were dispatched first and never wait on later ones,
-// so the waits end), then emits the tiles (emit_tile) from that base.  A span whose chain
-// goes wrong -- an invalid record, a Serializable record (no tables here) -- flags the batch
-// and the host decodes it the usual way, which classifies the error; a wait past
-// kZSpinLimit flags it too.  res: see launch_decode_small (kernels.h).
+// sequence's ~15 queue operations cost more than the decode; config 5's replay-prep decode:
+// 16 main logs of ~45 KB, 6 tiles each).  A block per tile: every block stages its tile and
+// walks it speculatively at once; then it takes its entry from the tile before's published
+// exit (the span start for a span's first tile) -- only the merge of the true chain is serial
+// along a span -- publishes its exit and counts, sums every earlier tile's counts (look-back:
+// blocks wait only on lower ones, dispatched first, so the waits end) and emits its tile from
+// the image it holds.  A tile whose chain goes wrong -- an invalid record, a Serializable
+// record (no tables here) -- flags the batch and the host decodes it the usual way, which
+// classifies the error; a wait past kZSpinLimit flags it too.  agg: counts at [t], exits at
+// [nt + t]; res: see launch_decode_small (kernels.h), res[3 + s] for the spans with tiles (the
+// host fills the empty ones).
 // ---------------------------------------------------------------------------------
 constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ull << 62) - 1;
 
-__device__ __forceinline__ void decode_small(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                             uint32_t n_spans, const FusedCtl& ctl, const DecodeOut& out, uint64_t* agg,
-                                             uint64_t* agg_next, uint64_t* res) {
-  __shared__ EmitLds<false, true> L;  // its image serves the count pass too
-  __shared__ uint64_t s_cnt[kZSmallTiles];
-  const uint32_t s = blockIdx.x, lane = threadIdx.x;
-  // developer diagnostics (CLONOS_SMALL_PROF): per span, shader-clock and 100 MHz real-time stamps
-  // at the start, after the count, after the look-back and at the end
-  auto stamp = [&](uint32_t i) {
-    if (ctl.prof && lane == 0) {
-      ctl.prof[(uint64_t)s * 8 + 2 * i] = __builtin_amdgcn_s_memtime();
-      ctl.prof[(uint64_t)s * 8 + 2 * i + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-  };
-  stamp(0);
-  FusedCtl cc = ctl;  // count_tile's own stamps (ZPHASE, per tile) after the spans'
-  cc.prof = ctl.prof ? ctl.prof + (uint64_t)n_spans * 8 : nullptr;
-  // the next call's look-back words, all kZSmallSpans of them (the host alternates the two buffers)
-  for (uint32_t j = s + n_spans * lane; j < kZSmallSpans; j += 64u * n_spans) agg_next[j] = 0;
-  const SpanDesc sd = spans[s];
-  uint64_t mine = 0, x = 0, bm[2] = {0, 0};
-  bool bad = sd.n_tiles > kZSmallTiles;
-  for (uint32_t k = 0; k < sd.n_tiles && !bad; ++k) {
-    const uint32_t t = sd.first_tile + k;
-    const ZTile z = ztile(tiles, spans, t, lane);
-    uint64_t c = 0;
-    if (k) __syncthreads();  // the image is reused (the last tile's stays for emit)
-    const uint32_t why = count_staged<false>(tiles, spans, cc, L.img, nullptr, lane, t, z, k ? x : z.td.span_off,
-                                             kZCanon, nullptr, &x, &c, nullptr, false, 0xFFFFFFFFu, bm);
-    bad = why != 0u;
-    if (lane == 0) s_cnt[k] = c;
-    mine += c;
-  }
-  stamp(1);
-  if (lane == 0) st_agent(&agg[s], kZAggSet | (bad ? kZAggBad : 0ull) | mine);
-  // look-back: every earlier span's counts
-  uint64_t pre = 0;
-  bool any_bad = bad;
-  for (uint32_t j0 = 0; j0 < s && !any_bad; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    uint64_t v = 0;
-    if (j < s) {  // a short poll: the waits here are a span's count (microseconds), not a batch's
-      const uint64_t w0 = __builtin_amdgcn_s_memtime();
-      while (!((v = ld_agent(&agg[j])) & kZAggSet)) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
-          v = kZAggSet | kZAggBad;
-          break;
-        }
-      }
-    }
-    any_bad = __any((v & kZAggBad) != 0ull);
-    uint64_t c = v & kZAggCnt;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    pre += c;
-  }
-  if (any_bad) {
-    if (lane == 0) __hip_atomic_store(res + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  stamp(2);
-  __syncthreads();  // s_cnt
-  uint64_t b = pre;
-  for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) b += s_cnt[k];
-  if (sd.n_tiles) {  // the last tile first: its image and bitmap are still here
-    emit_tile<false, true>(tiles, spans, cc, out, sd.first_tile + sd.n_tiles - 1, lane, b, L, bm);
-    b += s_cnt[sd.n_tiles - 1];
-  }
-  uint64_t e = pre;
-  for (uint32_t k = 0; k + 1 < sd.n_tiles; ++k) {
-    __syncthreads();
-    emit_tile<false, true>(tiles, spans, cc, out, sd.first_tile + k, lane, e, L);
-    e += s_cnt[k];
-  }
-  stamp(3);
-  if (lane == 0) {
-    res[3 + s] = pre;
-    if (s + 1 == n_spans) {
-      res[0] = b & ((1ull << 31) - 1);
-      res[1] = b >> 31;
-    }
-  }
-}
-
-// The same single launch with a block per tile, for small batches whose spans run over more
-// tiles (config 5's replay-prep decode: 16 main logs of ~45 KB, 6 tiles each, which the
-// three-pass sequence decoded in ~0.1 ms of launches and queue gaps).  Every block stages its
-// tile and walks it speculatively at once; then it takes its entry from the tile before's
-// published exit (the span start for a span's first tile), finishes the count, publishes its
-// exit and counts, sums every earlier tile's counts (look-back) and emits its tile from the
-// image it holds.  Blocks wait only on lower ones (dispatched first), so the waits end.  agg:
-// counts at [t], exits at [nt + t] (nt <= kZSmallSpans / 2).  res[3 + s] for the spans with
-// tiles (the host fills the empty ones).
 __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ tiles,
                                                    const SpanDesc* __restrict__ spans, uint32_t nt, const FusedCtl& ctl,
                                                    const DecodeOut& out, uint64_t* agg, uint64_t* agg_next,
                                                    uint64_t* res) {
   __shared__ EmitLds<false, true> L;
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
-  for (uint32_t j = t + nt * lane; j < kZSmallSpans; j += 64u * nt) agg_next[j] = 0;
+  for (uint32_t j = t + nt * lane; j < kZSmallAggWords; j += 64u * nt) agg_next[j] = 0;
   const ZTile z = ztile(tiles, spans, t, lane);
   const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
   stage_image(z.td, z.sd, t, tiles, L.img, lane, z.hi, &n1);
@@ -2662,40 +2571,18 @@ __global__ __launch_bounds__(64) void k_decode_small_tiles_arg(const SmallPlanAr
   decode_small_tiles(plan.tiles, plan.spans, n_tiles, ctl, out, agg, agg_next, res);
 }
 
-__global__ __launch_bounds__(64) void k_decode_small(const TileDesc* __restrict__ tiles,
-                                                     const SpanDesc* __restrict__ spans, uint32_t n_spans, FusedCtl ctl,
-                                                     DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
-  decode_small(tiles, spans, n_spans, ctl, out, agg, agg_next, res);
-}
-// The plan in the kernel arguments (read through the argument segment's address).
-__global__ __launch_bounds__(64) void k_decode_small_arg(const SmallPlanArg plan, uint32_t n_spans, FusedCtl ctl,
-                                                         DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res) {
-  decode_small(plan.tiles, plan.spans, n_spans, ctl, out, agg, agg_next, res);
-}
-
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
-                        const SmallPlanArg* plan, bool per_tile) {
+                        const SmallPlanArg* plan) {
   if (!n_spans) return CLG_OK;
+  if (!n_tiles || n_tiles > kZSmallTilesMax) return CLG_E_INVALID_ARG;
   ctl.n_tiles = n_tiles;
-  if (per_tile) {
-    if (!n_tiles || 2 * n_tiles > kZSmallSpans) return CLG_E_INVALID_ARG;
-    if (plan) {
-      if (n_tiles > kZSmallArgTiles || n_spans > kZSmallArgSpans) return CLG_E_INVALID_ARG;
-      hipLaunchKernelGGL(k_decode_small_tiles_arg, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, *plan, n_tiles, ctl,
-                         out, agg, agg_next, res);
-    } else {
-      hipLaunchKernelGGL(k_decode_small_tiles, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_tiles,
-                         ctl, out, agg, agg_next, res);
-    }
-    return launch_status(hipGetLastError());
-  }
   if (plan) {
     if (n_tiles > kZSmallArgTiles || n_spans > kZSmallArgSpans) return CLG_E_INVALID_ARG;
-    hipLaunchKernelGGL(k_decode_small_arg, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, *plan, n_spans, ctl, out,
-                       agg, agg_next, res);
+    hipLaunchKernelGGL(k_decode_small_tiles_arg, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, *plan, n_tiles, ctl,
+                       out, agg, agg_next, res);
   } else {
-    hipLaunchKernelGGL(k_decode_small, dim3(n_spans), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_spans,
+    hipLaunchKernelGGL(k_decode_small_tiles, dim3(n_tiles), dim3(64), 0, (hipStream_t)stream, d_tiles, d_spans, n_tiles,
                        ctl, out, agg, agg_next, res);
   }
   return launch_status(hipGetLastError());

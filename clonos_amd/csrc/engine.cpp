@@ -552,7 +552,7 @@ struct clg_engine {
   uint32_t plan_slot = 0;  // the slot stage_plan / enqueue_plan use (launch_fused sets it)
   DevBuf d_stage, d_desc, d_pieces, d_tiles, d_spans, d_agg, d_conv, d_tres, d_sres, d_totals, d_out;
   std::vector<uint64_t> tab_at;  // clg_get_determinants_batch: a log's place in the segment table (UINT64_MAX: none)
-  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_rprof, d_jpos, d_jlen, d_jn, d_defer;
+  DevBuf d_fconv, d_lanes, d_sums, d_fres, d_flags, d_dbg, d_prof, d_rprof, d_prof2, d_jpos, d_jlen, d_jn, d_defer;
   DevBuf d_o_off, d_o_tag, d_o_v0, d_o_widx, d_o_wrc, d_o_wv1, d_o_wvo, d_o_wvl, d_o_wsub;
   DevBuf d_zctl, d_ztiles, d_zbits;  // fast decode: control words, tiles, record-start bitmaps
   DevBuf d_zjpos, d_zjlen, d_zjn, d_zjwork;  // fast decode: Serializable length tables (phase 3)
@@ -2112,8 +2112,8 @@ struct clg_engine {
     return finish_out(out, nrec, nwide);
   }
   // ---------------------------------------------------------------- small batches
-  // A batch of at most kSmallBytes in spans of at most kZSmallTiles tiles, without
-  // Serializable tables, decodes in ONE launch (k_decode_small, decode_fused.hip): the plan
+  // A batch of at most kSmallBytes and clg::kZSmallTilesMax tiles, without Serializable
+  // tables, decodes in ONE launch (k_decode_small_tiles, decode_fused.hip): the plan
   // goes up in one copy, and the kernel writes host outputs straight into pinned memory, so
   // the call is copy + launch + one wait -- the three-pass sequence is about 15 queue
   // operations, which for config 1 (44 logs, 73 KB) cost more than the decode.  A span that
@@ -2134,31 +2134,14 @@ struct clg_engine {
   DevBuf d_small;
   clg::SmallPlanArg small_arg;
   bool small_flip = false;
-  // Tiles per span the single launch takes: its wave counts and emits a span's tiles one
-  // after another, so a span of 6 tiles (config 5's 45 KB main logs) is a chain of six tile
-  // walks on one wave while the three-pass path spreads them over the GPU (config 1's logs
-  // are one tile).  CLONOS_SMALL_MAXTILES (read at engine creation) overrides: tuning, tests.
-  const uint32_t small_max_tiles = [] {
-    const char* v = getenv("CLONOS_SMALL_MAXTILES");
-    return std::min<uint32_t>(v ? uint32_t(atoi(v)) : 2u, clg::kZSmallTiles);
-  }();
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
         p.only)
       return false;
     if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
-    bool long_span = false;
-    for (const auto& sd : p.spans) long_span |= sd.n_tiles > small_max_tiles;
-    // spans over more tiles: a block per tile (k_decode_small_tiles), up to its look-back size
-    return !long_span || (small_tiles && 2ull * p.n_tiles <= kSmallSpans);
+    return p.n_tiles <= clg::kZSmallTilesMax;
   }
-  // The per-tile single launch for batches with longer spans (CLONOS_SMALL_TILES=0 turns it
-  // off: a developer switch; such batches then take the three-pass path)
-  const bool small_tiles = [] {
-    const char* v = getenv("CLONOS_SMALL_TILES");
-    return !(v && atoi(v) == 0);
-  }();
   // CLG_MEM_MAPPED outputs: every array's device address (false: one is not registered, or
   // its cap / wcap elements reach past its registered range -- the caller's staging path then)
   static bool mapped_outputs(const clg_decoded& out, clg::DecodeOut* o) {
@@ -2200,8 +2183,11 @@ struct clg_engine {
     reset_result(out);
     host_tiles(p);
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
-    bool per_tile = false;  // (small_ok: spans over more tiles than a wave takes -> a block per tile)
-    for (const auto& sd : p.spans) per_tile |= sd.n_tiles > small_max_tiles;
+    if (nt == 0) {  // every span empty: no records, and no launch (a grid of zero blocks is invalid)
+      if (span_rec_base) std::fill(span_rec_base, span_rec_base + ns + 1, uint64_t(0));
+      out->n_rec = out->n_wide = 0;
+      return CLG_OK;
+    }
     // the plan: in the launch's arguments when it fits (no copy queued), else one copy
     static const int small_mode = [] {  // developer switch: bit 0 no argument plan
       const char* v = getenv("CLONOS_SMALL_MODE");
@@ -2240,15 +2226,17 @@ struct clg_engine {
     CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
     uint64_t* res = h_small_res.as<uint64_t>();
     res[0] = res[1] = res[2] = 0;
-    // look-back words: two buffers of kSmallSpans, zeroed once; each call zeroes the other
+    // look-back words: two buffers of kZSmallAggWords, zeroed once; each call zeroes the other;
+    // then the per-tile counts
+    constexpr size_t kAgg = clg::kZSmallAggWords;
     if (!d_small.p) {
-      CHK(d_small.ensure((2 * size_t(kSmallSpans) + clg::kZSmallTiles * size_t(kSmallSpans)) * 8));
-      HIPCHK(hipMemsetAsync(d_small.p, 0, 2 * size_t(kSmallSpans) * 8, stream));
+      CHK(d_small.ensure((2 * kAgg + clg::kZSmallTilesMax) * 8));
+      HIPCHK(hipMemsetAsync(d_small.p, 0, 2 * kAgg * 8, stream));
     }
-    uint64_t* agg = d_small.as<uint64_t>() + (small_flip ? kSmallSpans : 0);
-    uint64_t* agg_next = d_small.as<uint64_t>() + (small_flip ? 0 : kSmallSpans);
+    uint64_t* agg = d_small.as<uint64_t>() + (small_flip ? kAgg : 0);
+    uint64_t* agg_next = d_small.as<uint64_t>() + (small_flip ? 0 : kAgg);
     small_flip = !small_flip;
-    uint64_t* cnt = d_small.as<uint64_t>() + 2 * size_t(kSmallSpans);
+    uint64_t* cnt = d_small.as<uint64_t>() + 2 * kAgg;
     clg::FusedCtl ctl{};
     ctl.cnt = cnt;
     ctl.bits = d_zbits.as<uint64_t>();
@@ -2263,8 +2251,8 @@ struct clg_engine {
     ctl.warm = (small_warm >= 0 ? uint32_t(small_warm) : 32u) | (small_stagger ? 0u : (1u << 31));
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
-      CHK(d_prof.ensure(size_t(ns + nt) * 64));
-      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(ns + nt) * 64, stream));
+      CHK(d_prof.ensure(size_t(nt) * 64));
+      HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
       ctl.prof = d_prof.as<uint64_t>();
     }
     std::optional<HostTimer> hsub(std::in_place, this, "host_small_submit");  // (CLONOS_HOST_PROF sub-stages)
@@ -2278,25 +2266,16 @@ struct clg_engine {
     }
     CHK(clg::launch_decode_small(reinterpret_cast<const clg::TileDesc*>(d_plan.p), nt,
                                  reinterpret_cast<const clg::SpanDesc*>(d_plan.as<uint8_t>() + L.o_spans), ns, ctl, o,
-                                 agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr, per_tile));
+                                 agg, agg_next, res, stream, arg_plan ? &small_arg : nullptr));
     if (timing) HIPCHK(hipEventRecord(eb, stream));
     hsub.emplace(this, "host_small_wait");
     HIPCHK(hipStreamSynchronize(stream));
     hsub.emplace(this, "host_small_finish");
-    if (sprof) {
-      std::vector<uint64_t> hp(size_t(ns + nt) * 8);
+    if (sprof) {  // per tile (count_tile's stamps): walk, merge, counts ticks; merge steps, passes
+      std::vector<uint64_t> hp(size_t(nt) * 8);
       HIPCHK(hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost));
-      uint64_t r0 = ~0ull;
-      for (uint32_t s = 0; s < ns; ++s) r0 = std::min(r0, hp[s * 8 + 1]);
-      for (uint32_t s = 0; s < ns; ++s) {  // per span: start, then each phase's ticks and us
-        const uint64_t* q = &hp[s * 8];
-        fprintf(stderr, "[clonos] small decode span %u: start %.2f us  count %llu/%.2f  lookback %llu/%.2f  emit %llu/%.2f\n",
-                s, (q[1] - r0) / 100.0, (unsigned long long)(q[2] - q[0]), (q[3] - q[1]) / 100.0,
-                (unsigned long long)(q[4] - q[2]), (q[5] - q[3]) / 100.0, (unsigned long long)(q[6] - q[4]),
-                (q[7] - q[5]) / 100.0);
-      }
-      for (uint32_t t = 0; t < nt; ++t) {  // per tile (count_tile): walk, merge, counts ticks; merge steps, passes
-        const uint64_t* q = &hp[(ns + t) * 8];
+      for (uint32_t t = 0; t < nt; ++t) {
+        const uint64_t* q = &hp[size_t(t) * 8];
         fprintf(stderr, "[clonos] small decode tile %u: walk %llu  merge %llu  counts %llu  steps %llu/%llu  passes %llu\n", t,
                 (unsigned long long)(q[2] - q[1]), (unsigned long long)(q[3] - q[2]), (unsigned long long)(q[4] - q[3]),
                 (unsigned long long)(q[5] & 0xFFFFF), (unsigned long long)((q[5] >> 20) & 0xFFFFF),
@@ -2313,9 +2292,8 @@ struct clg_engine {
     if (span_rec_base) {
       for (uint32_t s = 0; s < ns; ++s) span_rec_base[s] = res[3 + s] & kRecMask;
       span_rec_base[ns] = nrec;
-      if (per_tile)  // (the kernel writes the spans with tiles: an empty span starts where the next one does)
-        for (uint32_t s = ns; s-- > 0;)
-          if (!p.spans[s].n_tiles) span_rec_base[s] = span_rec_base[s + 1];
+      for (uint32_t s = ns; s-- > 0;)  // (the kernel writes the spans with tiles: an empty one starts where the next does)
+        if (!p.spans[s].n_tiles) span_rec_base[s] = span_rec_base[s + 1];
     }
     if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     out->n_rec = nrec;
@@ -2800,10 +2778,24 @@ struct clg_engine {
       }
     }
     CHK(timed("robust_jser", 0, [&] { return clg::launch_jser_fill(dt, nt, ds, J, stream); }));
+    uint64_t* prof2 = nullptr;  // developer diagnostics: the deferred scan's phase stamps (CLONOS_ROBUST_PHASES)
+    if (J.prof && d_prof2.ensure(std::max<size_t>(1, nt) * 64) == CLG_OK) {
+      prof2 = d_prof2.as<uint64_t>();
+      hipMemsetAsync(prof2, 0, size_t(nt) * 64, stream);
+    }
     CHK(timed("robust_scan_deferred", 0, [&] {
       return clg::launch_fast_scan(dt, nt, ds, d_fconv.as<uint32_t>(), J, 1, d_lanes.as<clg::LaneSeg>(),
-                                   d_sums.as<clg::TileSum>(), dbg, nullptr, stream);
+                                   d_sums.as<clg::TileSum>(), dbg, prof2, stream);
     }));
+    if (prof2) {
+      std::vector<uint64_t> hp(size_t(nt) * 8);
+      hipMemcpyAsync(hp.data(), prof2, hp.size() * 8, hipMemcpyDeviceToHost, stream);
+      hipStreamSynchronize(stream);
+      if (FILE* fp = fopen((std::string(rprof_path) + ".scan").c_str(), "wb")) {
+        fwrite(hp.data(), 8, hp.size(), fp);
+        fclose(fp);
+      }
+    }
     CHK(timed("robust_resolve", uint64_t(nt) * 32, [&] {
       return clg::launch_fast_resolve(dt, ds, ns, d_fconv.as<uint32_t>(), d_lanes.as<clg::LaneSeg>(),
                                       d_sums.as<clg::TileSum>(), J, d_fres.as<clg::FastRes>(),

@@ -281,27 +281,26 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
 // per tile); CLG_E_DEVICE as 0.
 uint32_t decode_count_grid(bool jser, uint32_t n_tiles);
 
-// Small batches in one launch (k_decode_small): one wave per span counts the span's tiles,
-// publishes its counts, sums every earlier span's (look-back), emits.  Spans of at most
-// kZSmallTiles tiles, batches without Serializable tables.  Results go to `res` (host-mapped
-// pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any span failed
-// (the host then decodes the batch the usual way), res[3 + s] span s's first record.  agg: kZSmallSpans zeroed
-// words; the kernel zeroes all of agg_next for the next call (the host alternates two buffers,
-// so no memset is queued).  plan (host memory, optional): a plan of at most kZSmallArgTiles
-// tiles and kZSmallArgSpans spans goes in the launch's own arguments instead of d_tiles /
-// d_spans, so no copy is queued before the launch.
-constexpr uint32_t kZSmallTiles = 8;
-constexpr uint32_t kZSmallSpans = 4096;  // spans per small batch at most (look-back buffer size)
+// Small batches in one launch (k_decode_small_tiles): a block per tile counts the tile from
+// its predecessor's published exit, publishes its own exit and counts, sums every earlier
+// tile's (look-back), emits.  Batches without Serializable tables.  Results go to `res`
+// (host-mapped pinned memory or device): res[0] records, res[1] wide rows, res[2] != 0 when any
+// tile failed (the host then decodes the batch the usual way), res[3 + s] span s's first record
+// (spans with tiles).  agg: kZSmallAggWords zeroed words; the kernel zeroes all of agg_next for
+// the next call (the host alternates two buffers, so no memset is queued).  plan (host memory,
+// optional): a plan of at most kZSmallArgTiles tiles and kZSmallArgSpans spans goes in the
+// launch's own arguments instead of d_tiles / d_spans, so no copy is queued before the launch.
+constexpr uint32_t kZSmallSpans = 4096;     // spans per small batch at most
+constexpr uint32_t kZSmallTilesMax = 4096;  // tiles per small batch at most
+constexpr uint32_t kZSmallAggWords = 2 * kZSmallTilesMax;  // look-back words per buffer: counts, exits
 constexpr uint32_t kZSmallArgTiles = 64, kZSmallArgSpans = 64;
 struct SmallPlanArg {  // 3 KiB: with the other arguments inside the 4 KiB kernel-argument limit
   TileDesc tiles[kZSmallArgTiles];
   SpanDesc spans[kZSmallArgSpans];
 };
-// per_tile: a block per tile (spans of any number of tiles; 2 n_tiles <= kZSmallSpans) instead
-// of a wave per span (spans of at most kZSmallTiles tiles).
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
-                        const SmallPlanArg* plan = nullptr, bool per_tile = false);
+                        const SmallPlanArg* plan = nullptr);
 
 // ---- gather (delta slice) -------------------------------------------------------
 // A piece copies len bytes from src to out + dst; the source range lies inside one

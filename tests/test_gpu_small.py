@@ -1,5 +1,6 @@
-"""GPU: the single-launch small-batch decode (k_decode_small: one wave per span, look-back over
-the earlier spans' counts, host outputs written straight into pinned memory) == the CPU
+"""GPU: the single-launch small-batch decode (k_decode_small_tiles: a block per tile, each
+entering at its predecessor's published exit, look-back over the earlier tiles' counts, host
+outputs written straight into pinned memory) == the CPU
 oracle's decodeNext loop, bit-exact; batches it does not finish (an invalid record, a
 Serializable record) fall back to the three-pass path with the same result."""
 import numpy as np
@@ -10,13 +11,6 @@ from clonos_amd import ClonosError, Engine, synth
 from test_gpu_decode import assert_span_equal
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.fixture(autouse=True, params=["8", "1"], ids=["wave_per_span", "block_per_tile"])
-def _small_mode(request, monkeypatch):
-    """Every test twice: spans of up to 8 tiles on the wave-per-span launch (the default takes
-    2), then spans of 2 tiles or more on the block-per-tile launch (k_decode_small_tiles)."""
-    monkeypatch.setenv("CLONOS_SMALL_MAXTILES", request.param)
 
 
 def _eng(**kw):
@@ -69,6 +63,28 @@ def test_small_random_spans_multi_tile(seed, seg):
         for s, b in enumerate(bufs):
             assert_span_equal(dec, s, b)
         assert dec.span_rec_base[-1] == dec.n_rec
+
+
+@pytest.mark.parametrize("n_spans", [1, 7])
+def test_small_all_empty_spans_need_no_launch(n_spans):
+    """A batch of empty spans (a log truncated to its end, an empty replay batch) has no
+    tiles: no records, every span starts at 0, and nothing is launched."""
+    from clonos_amd import CausalLogID
+    with _eng() as eng:
+        logs = [eng.open_log(CausalLogID.main(i)) for i in range(n_spans)]
+        eng.kernel_stats_reset()
+        dec = eng.decode_logs(logs, [0] * n_spans)
+        assert dec.n_rec == 0 and list(dec.span_rec_base) == [0] * (n_spans + 1)
+        assert _launches(eng, "decode_small") == 0 and _launches(eng, "decode_count") == 0
+        dec = eng.decode_host(b"", [(0, 0)] * n_spans)
+        assert dec.n_rec == 0 and list(dec.span_rec_base) == [0] * (n_spans + 1)
+        # a non-empty batch after it still decodes on the small path
+        rng = np.random.default_rng(9)
+        b = synth.random_log(300, rng, allow_serializable=False)
+        logs[0].appendDeterminant(b, 0)
+        dec = eng.decode_logs(logs, [0] * n_spans)
+        assert_span_equal(dec, 0, b)
+        assert _launches(eng, "decode_small") == 1
 
 
 def test_small_host_input_spans():
@@ -210,17 +226,15 @@ def test_pooled_capacity_exceeded_is_decoded_again_sized():
             assert_span_equal(dec, s, data[l])
 
 
-@pytest.mark.parametrize("per_tile", [True, False])
-def test_multi_tile_spans_default_to_block_per_tile(monkeypatch, per_tile):
-    """By default a wave per span takes spans of at most 2 tiles: a batch of 16 config-2 logs of
-    ~45 KB (config 5's failed main logs, 6 tiles each) goes to the block-per-tile single launch
-    -- or, with it turned off (CLONOS_SMALL_TILES=0), three-pass -- with the same result."""
-    monkeypatch.delenv("CLONOS_SMALL_MAXTILES")
-    if not per_tile:
-        monkeypatch.setenv("CLONOS_SMALL_TILES", "0")
+@pytest.mark.parametrize("decode", ["auto", "three_pass"])
+def test_multi_tile_spans_take_the_single_launch(decode):
+    """A batch of 16 config-2 logs of ~45 KB (config 5's failed main logs, 6 tiles each) goes to
+    the single launch (a block per tile; the chain's merge is the only serial part along a span)
+    -- or, with it turned off (decode="three_pass"), three-pass -- with the same result."""
+    per_tile = decode == "auto"
     rng = np.random.default_rng(0xC5)
     from clonos_amd import CausalLogID
-    with _eng() as eng:
+    with _eng(decode=decode) as eng:
         bufs = [synth.config2_log(8000, rng)[0].tobytes() for _ in range(16)]
         small = [synth.config2_log(900, rng)[0].tobytes() for _ in range(4)]  # <= 2 tiles each
         logs = []
@@ -238,6 +252,6 @@ def test_multi_tile_spans_default_to_block_per_tile(monkeypatch, per_tile):
             assert_span_equal(dec, s, b)
         eng.kernel_stats_reset()
         dec = eng.decode_logs(logs[16:], [0] * 4)
-        assert _launches(eng, "decode_small") == 1
+        assert _launches(eng, "decode_small") == (1 if per_tile else 0)
         for s, b in enumerate(small):
             assert_span_equal(dec, s, b)

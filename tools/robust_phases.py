@@ -35,3 +35,8 @@ for q in (50, 90, 99):
 ok = p[:, 3] > 0
 print("jser per tile: candidates", round(float(p[ok, 4].mean()), 1), "general", round(float(p[ok, 5].mean()), 2),
       "max lane", round(float(p[ok, 6].mean()), 2))
+q = np.fromfile(out + ".scan", np.uint64).reshape(-1, 8).astype(np.int64)
+ok = np.all(q[:, :7] > 0, axis=1)
+d = np.diff(q[ok][:, :7], axis=1)
+print(f"deferred scan tiles {ok.sum()}:", {nm: round(float(d[:, i].mean()), 1) for i, nm in
+      enumerate(["stage", "tables", "bfs", "keep", "parse", "chain"])})
