@@ -38,6 +38,7 @@
 // Record layouts: SimpleDeterminantEncoder.java:124-323.
 #include "dev_common.h"
 #include "jser_device.h"
+#include "jser_flat.h"
 
 namespace clg {
 
@@ -2619,49 +2620,10 @@ __device__ __forceinline__ uint32_t z4(const uint32_t* T, uint32_t q) {
 }
 __device__ __forceinline__ uint32_t be16_12(uint32_t v) { return ((v >> 8) & 0xFFu) << 8 | ((v >> 16) & 0xFFu); }
 
-// Record length of the common stream shape, inline and call-free: one TC_OBJECT whose
-// class and superclasses are fresh TC_CLASSDESCs with flags SC_SERIALIZABLE only, primitive
-// fields only and an empty annotation (java.lang.Boolean, Integer, Long, ...); its class
-// data is then the fields' primitive values.  0: some other shape (the general walker
-// decides), or the stream leaves the LDS image.  Grammar: Java Object Serialization
-// Specification 6.4 (newObject, newClassDesc, classDescInfo, fieldDesc, nowrclass).
+// Record length of the common stream shape (jser_flat.h), from the LDS image: 0 = some
+// other shape (the general walker decides), or the stream leaves the image.
 __device__ __forceinline__ uint32_t jser_flat_len(const uint32_t* T, uint32_t a, uint32_t img_end) {
-  uint32_t p = a + 5;  // after the tag and AC ED 00 05
-  if (p + 1 > img_end || (z4(T, p) & 0xFFu) != jser::TC_OBJECT) return 0u;
-  ++p;
-  uint32_t data = 0;
-  for (int depth = 0;; ++depth) {
-    if (p + 1 > img_end || depth > 8) return 0u;
-    const uint32_t v = z4(T, p);  // [TC_CLASSDESC][className length u16] or [TC_NULL]
-    const uint32_t b = v & 0xFFu;
-    if (b == jser::TC_NULL) {  // no (further) superclass
-      ++p;
-      break;
-    }
-    if (b != jser::TC_CLASSDESC || p + 3 > img_end) return 0u;
-    p += 3 + be16_12(v) + 8;  // className, serialVersionUID
-    if (p + 3 > img_end) return 0u;
-    const uint32_t f = z4(T, p);  // [flags][field count u16]
-    if ((f & 0xFFu) != jser::SC_SERIALIZABLE) return 0u;
-    const uint32_t nf = be16_12(f);
-    if (nf & 0x8000u) return 0u;
-    p += 3;
-    for (uint32_t i = 0; i < nf; ++i) {
-      if (p + 3 > img_end) return 0u;
-      const uint32_t fv = z4(T, p);  // [typecode][fieldName length u16]
-      const uint32_t tc = fv & 0xFFu;
-      // primitive sizes: B 1, C 2, D 8, F 4, I 4, J 8, S 2, Z 1
-      const uint32_t sz = tc == 'B' || tc == 'Z' ? 1u : tc == 'C' || tc == 'S' ? 2u : tc == 'I' || tc == 'F' ? 4u
-                          : tc == 'J' || tc == 'D' ? 8u : 0u;
-      if (!sz) return 0u;
-      data += sz;
-      p += 3 + be16_12(fv);
-    }
-    if (p + 1 > img_end || (z4(T, p) & 0xFFu) != jser::TC_ENDBLOCKDATA) return 0u;
-    ++p;
-  }
-  p += data;
-  return p <= img_end ? p - a : 0u;
+  return jser_flat_len_t([T](uint32_t q) { return z4(T, q); }, a, img_end);
 }
 
 __device__ __forceinline__ bool zmagic(const uint32_t* T, uint32_t a) {
@@ -2842,14 +2804,167 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   }
 }
 
-// Persistent grid: block b takes tiles b, b + G, ...
+// The same table from the write path's candidates (kernels.h SideCar), without reading the
+// tile: its segment's entries inside the tile, those of unknown length kept only where the
+// magic is there (read from HBM: a prefix at a chunk's end, or a stream running past it),
+// ranked by position; lengths the writer measured are used when the stream ends inside the
+// span, every other candidate goes to the general walker (which then decides as it would for
+// the scan's candidates).  false: the tile is not in the pool, its segment's list overflowed
+// or it holds more than kZSideKept candidates -- the caller scans it (nothing written but
+// the scratch).  Wave-uniform; `scr`: the wave's own 2 kZSideKept words of LDS.
+constexpr uint32_t kZSideKept = 256;  // candidates of one tile a wave ranks in LDS
+__device__ __forceinline__ bool side_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                          const FusedCtl& ctl, uint32_t* scr, const uint32_t t, const uint32_t lane,
+                                          bool* flagged) {
+  const SideCar& S = ctl.side;
+  const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
+  const TileDesc td = tiles[t];
+  const uintptr_t ab = (uintptr_t)td.abase, pb = (uintptr_t)S.pool;
+  if (ab < pb || ab - pb >= S.pool_bytes) return false;
+  const uint64_t off = ab - pb;
+  const uint32_t seg = (uint32_t)(off / S.seg_bytes), so0 = (uint32_t)(off % S.seg_bytes);
+  const uint32_t n = (uint32_t)gp(S.hdr)[seg];
+  if (n > S.cap) return false;
+  const ZTile z = ztile(tiles, spans, t, lane);
+  const uint64_t c1 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
+  const uint32_t lo = so0 + z.lo, hi = so0 + z.hi;  // the tile's bytes, as segment positions
+  const CLG_GLOBAL uint32_t* ent = gp(S.ent) + (size_t)seg * S.cap;
+  uint32_t* s_a = scr;               // kept candidates: image coordinate
+  uint32_t* s_c = scr + kZSideKept;  // and length code
+  uint32_t kept = 0;
+  for (uint32_t k0 = 0; k0 < n; k0 += 64u) {  // wave-uniform: kept entries compacted in list order
+    const uint32_t k = k0 + lane;
+    bool keep = false;
+    uint32_t a = 0, code = 0;
+    if (k < n) {
+      const uint32_t e = ent[k];
+      const uint32_t pos = e & 0xFFFFu;
+      code = e >> 16;
+      a = pos - so0;
+      keep = pos >= lo && pos < hi && a + 5u <= z.end_a;
+      if (keep && code == kSideUnknown) {
+        ZStreamBytes acc{nullptr, a, 0u, z.lo, z.td.span_off, tiles, t, z.sd.first_tile + z.sd.n_tiles};
+        keep = acc(0) == CLG_TAG_SERIALIZABLE && acc(1) == 0xAC && acc(2) == 0xED && acc(3) == 0x00 && acc(4) == 0x05;
+      }
+    }
+    const uint64_t m = __ballot(keep);
+    if (keep) {
+      const uint32_t i = kept + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (i < kZSideKept) {
+        s_a[i] = a;
+        s_c[i] = code;
+      }
+    }
+    kept += (uint32_t)__popcll(m);
+  }
+  if (kept > kZSideKept) return false;
+  const uint64_t c2 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS stores before its reads
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t total = kept;
+  uint32_t ob = 0;
+  if (lane == 0) {  // as jser_tile: the batch flag, the overflow arena, the tile's count
+    uint32_t nn = total;
+    if (total > kZJCap) {  // (the batch flag: set once per block by the caller, k_decode_jser_side)
+      ob = atomicAdd(ctl.jwork + 1, total - kZJCap);
+      if (ob + (total - kZJCap) > ctl.jovf_cap) {
+        raise_abort(ctl, 6, t);
+        nn = kZJCap;
+      } else {
+        gp(ctl.jbase)[t] = ob;
+      }
+    }
+    gp(ctl.jn)[t] = nn;
+  }
+  ob = __shfl(ob, 0);
+  const bool ovf_ok = total <= kZJCap || ob + (total - kZJCap) <= ctl.jovf_cap;
+  *flagged = *flagged || total;
+  uint32_t ngen = 0;  // (diagnostics)
+  for (uint32_t i0 = 0; i0 < total; i0 += 64u) {  // wave-uniform: one work-list reservation per pass
+    const uint32_t i = i0 + lane;
+    const bool on = i < total;
+    const uint32_t a = on ? s_a[i] : 0u, code = on ? s_c[i] : 0u;
+    uint32_t r = 0;  // rank by position (a list is in position order but for chunks of one launch)
+    if (on)
+      for (uint32_t j = 0; j < total; ++j) {
+        const uint32_t b = s_a[j];
+        r += b < a || (b == a && j < i) ? 1u : 0u;
+      }
+    uint64_t sl = ~0ull;
+    if (on && r < kZJCap) sl = (uint64_t)t * kZJCap + r;
+    else if (on && ovf_ok) sl = (uint64_t)ctl.n_tiles * kZJCap + ob + (r - kZJCap);
+    const bool known = code != kSideUnknown && a + code <= z.end_a;
+    const bool gen = sl != ~0ull && !known;  // the general walker measures it (jser_tile's measure)
+    const uint64_t gm = __ballot(gen);
+    uint32_t wb = 0;
+    if (gm && lane == 0) wb = atomicAdd(ctl.jwork, (uint32_t)__popcll(gm));
+    wb = __shfl(wb, 0);
+    ngen += (uint32_t)__popcll(gm);
+    if (sl == ~0ull) continue;
+    gp(ctl.jpos)[sl] = a;
+    if (!gen) {
+      gp(ctl.jlen)[sl] = code;
+    } else {
+      gp(ctl.jlen)[sl] = kZJGeneral;
+      const uint32_t w = wb + (uint32_t)__popcll(gm & ((1ull << lane) - 1ull));
+      if (w < ctl.jwork_cap) {
+        ctl.jwork[2 + w] = (uint32_t)sl;
+        ctl.jwork[2 + ctl.jwork_cap + w] = t;
+      } else {
+        raise_abort(ctl, 6, t);
+      }
+    }
+  }
+  if (ctl.prof && lane == 0) {  // developer diagnostics: start; descriptor+header, entries, rank+tables
+    const uint64_t c3 = __builtin_amdgcn_s_memtime();
+    ctl.prof[(uint64_t)t * 8 + 6] = c0;
+    ctl.prof[(uint64_t)t * 8 + 7] = (c1 - c0) | (c2 - c1) << 21 | (c3 - c2) << 42 | (uint64_t)(ngen < 31 ? ngen : 31) << 59;
+  }
+  return true;
+}
+
+// The tiles the sidecar does not serve (side_tile false), for k_decode_jser: [0] their
+// count, then the tiles (after the general walker's work list; [0] zeroed per batch).
+__device__ __forceinline__ uint32_t* side_scan_list(const FusedCtl& ctl) { return ctl.jwork + 2 + 2 * ctl.jwork_cap; }
+
+// Phase 3 from the sidecars: a wave per tile, four to a block, persistent over the tiles;
+// tiles it cannot serve are listed for the scan.  Per tile the work is a few dependent
+// loads (descriptor, list header, entries), so many waves are resident to overlap them.
+__global__ __launch_bounds__(256) void k_decode_jser_side(const TileDesc* __restrict__ tiles,
+                                                          const SpanDesc* __restrict__ spans, FusedCtl ctl) {
+  __shared__ uint32_t s_scr[4][2 * kZSideKept];
+  __shared__ uint32_t s_flag;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t* list = side_scan_list(ctl);
+  if (threadIdx.x == 0) s_flag = 0;
+  __syncthreads();
+  bool flagged = false;
+  for (uint32_t t = blockIdx.x * 4u + wv; t < ctl.n_tiles; t += gridDim.x * 4u) {
+    if (!side_tile(tiles, spans, ctl, s_scr[wv], t, lane, &flagged) && lane == 0) {
+      const uint32_t i = atomicAdd(list, 1u);
+      list[1 + i] = t;
+    }
+  }
+  if (flagged && lane == 0) s_flag = 1;
+  __syncthreads();
+  // "the batch holds Serializable records" (the host's table hint): one store per block at most,
+  // and none once another block's is visible -- a store per wave to this one word queued
+  // behind each other and stalled the waves' next loads (the kernel 0.37 against 0.17 ms)
+  if (threadIdx.x == 0 && s_flag && !ld_agent32(ctl.abort + 7))
+    __hip_atomic_store(ctl.abort + 7, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Persistent grid: block b takes tiles b, b + G, ... (with the sidecar: the listed tiles)
 __global__ __launch_bounds__(64) void k_decode_jser(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                     FusedCtl ctl) {
   __shared__ uint32_t s_img[kZJRows * kZPitch];
   __shared__ uint32_t s_cand[kZJCap];
   bool flagged = false;
-  for (uint32_t t = blockIdx.x; t < ctl.n_tiles; t += gridDim.x) {
-    jser_tile(tiles, spans, ctl, s_img, s_cand, t, threadIdx.x, &flagged);
+  const uint32_t* list = ctl.side.hdr ? side_scan_list(ctl) : nullptr;
+  const uint32_t n = list ? min(ld_agent32(list), ctl.n_tiles) : ctl.n_tiles;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    jser_tile(tiles, spans, ctl, s_img, s_cand, list ? list[1 + i] : i, threadIdx.x, &flagged);
     __syncthreads();  // the image is reused by the next tile
   }
 }
@@ -3005,6 +3120,20 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
         return CLG_E_DEVICE;
       jres = per_cu * cus;
+    }
+    if (ctl.side.hdr) {
+      static int sres = 0;  // blocks the device keeps resident for the sidecar kernel
+      if (!sres) {
+        int dev = 0, per_cu = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_jser_side, 256, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 || cus < 1)
+          return CLG_E_DEVICE;
+        sres = per_cu * cus;
+      }
+      const uint32_t nb = (nt + 3u) / 4u;
+      ZLAUNCH(k_decode_jser_side, dim3(nb < (uint32_t)sres ? nb : (uint32_t)sres), dim3(256), 0, st, d_tiles, d_spans,
+              ctl);
     }
     ZLAUNCH(k_decode_jser, dim3(nt < (uint32_t)jres ? nt : (uint32_t)jres), dim3(64), 0, st,
                        d_tiles, d_spans, ctl);

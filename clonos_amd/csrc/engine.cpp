@@ -527,6 +527,16 @@ struct clg_engine {
   void* pool_alloc = nullptr;  // pool minus the guard bytes either side
   uint8_t* pool = nullptr;
   std::vector<uint32_t> free_segs;
+  // The write path's Serializable candidates per segment (kernels.h SideCar; hdr null: none,
+  // every decode tile is scanned), and each segment's life stamp: bumped whenever the segment
+  // leaves the free list, carried by the chunks written into it.
+  clg::SideCar side{};
+  void* side_alloc = nullptr;
+  std::vector<uint32_t> seg_life;
+  const clg::SideCar* side_arg() const { return side.hdr ? &side : nullptr; }
+  // a chunk's life word: the segment's life (31 bits) | 1 << 31 when the request's bytes go on
+  // in the next chunk (contiguous in the source: the writer measures streams across it)
+  uint32_t life_word(uint32_t seg, bool more) const { return (seg_life[seg] & 0x7FFFFFFFu) | (more ? 0x80000000u : 0u); }
   // the in-flight (data) log's own pool (clg_config.ifl_*)
   void* ifl_alloc = nullptr;
   uint8_t* ifl_pool = nullptr;
@@ -739,6 +749,7 @@ struct clg_engine {
       return fail(CLG_E_NOSPACE, "segment pool exhausted (need %zu, free %zu)", need, free_segs.size());
     for (size_t i = 0; i < need; ++i) {
       l.segs.push_back(free_segs.back());
+      ++seg_life[free_segs.back()];
       free_segs.pop_back();
     }
     return CLG_OK;
@@ -819,7 +830,7 @@ struct clg_engine {
       while (left) {
         const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
         const uint32_t take = uint32_t(std::min<size_t>(left, C() - so));
-        ch[n++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, 0};
+        ch[n++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, life_word(l.segs[si], left > take)};
         p += int32_t(take);
         src += take;
         left -= take;
@@ -832,7 +843,7 @@ struct clg_engine {
     HIPCHK(hipMemcpyAsync(d_stage.p, hs, total, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(d_desc.p, ch, n * sizeof(clg::ScatterChunk), hipMemcpyHostToDevice, stream));
     CHK(timed("append_scatter", 2 * total, [&] {
-      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(n), d_stage.as<uint8_t>(), stream);
+      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(n), d_stage.as<uint8_t>(), stream, side_arg());
     }));
     // the pinned staging buffers are reused by the next flush: wait for the copies
     HIPCHK(hipStreamSynchronize(stream));
@@ -917,7 +928,7 @@ struct clg_engine {
       while (left) {
         const uint32_t si = uint32_t(p) / C(), so = uint32_t(p) % C();
         const uint32_t take = std::min<uint32_t>(left, C() - so);
-        ch[nch++] = clg::ScatterChunk{seg_addr(l->segs[si]) + so, src, take, 0};
+        ch[nch++] = clg::ScatterChunk{seg_addr(l->segs[si]) + so, src, take, life_word(l->segs[si], left > take)};
         p += int32_t(take);
         src += take;
         left -= take;
@@ -933,7 +944,7 @@ struct clg_engine {
     CHK(d_desc.ensure(db));
     HIPCHK(hipMemcpyAsync(d_desc.p, h_desc.p, db, hipMemcpyHostToDevice, stream));
     CHK(timed("upstream_scatter", 2 * total, [&] {
-      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream);
+      return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream, side_arg());
     }));
     return sync();  // the caller's buffer and the pinned descriptors are free again
   }
@@ -1058,7 +1069,11 @@ struct clg_engine {
         }
         if (!u.need && !u.num_new) continue;
         Log& l = logs[r[i].log];
-        for (uint32_t j = 0; j < u.need; ++j) l.segs.push_back(free_segs[top - 1 - (u.seg_from + j)]);  // pop order
+        for (uint32_t j = 0; j < u.need; ++j) {  // pop order
+          const uint32_t sg = free_segs[top - 1 - (u.seg_from + j)];
+          l.segs.push_back(sg);
+          ++seg_life[sg];  // (each segment is taken by one part)
+        }
         if (!u.num_new) continue;
         int32_t p = l.writer;
         uint64_t src = r[i].src_off + (r[i].len - uint32_t(u.num_new));
@@ -1067,7 +1082,7 @@ struct clg_engine {
         while (left) {
           const uint32_t si = uint32_t(p) / Cb, so = uint32_t(p) % Cb;
           const uint32_t take = std::min<uint32_t>(left, Cb - so);
-          ch[c++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, 0};
+          ch[c++] = clg::ScatterChunk{seg_addr(l.segs[si]) + so, src, take, life_word(l.segs[si], left > take)};
           p += int32_t(take);
           src += take;
           left -= take;
@@ -1089,7 +1104,7 @@ struct clg_engine {
       return true;
     }
     if ((*out_st = timed("upstream_scatter", 2 * total, [&] {
-           return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream);
+           return clg::launch_scatter(d_desc.as<clg::ScatterChunk>(), uint32_t(nch), bytes, stream, side_arg());
          })) != CLG_OK)
       return true;
     *out_st = sync();
@@ -1921,7 +1936,7 @@ struct clg_engine {
       CHK(d_zjpos.ensure((size_t(nt) * clg::kZJCap + zjovf_cap) * 4));
       CHK(d_zjlen.ensure((size_t(nt) * clg::kZJCap + zjovf_cap) * 4));
       CHK(d_zjn.ensure(size_t(nt) * 8));  // jn, jbase
-      CHK(d_zjwork.ensure((2 * size_t(jwork_cap) + 2) * 4));
+      CHK(d_zjwork.ensure((2 * size_t(jwork_cap) + 3 + size_t(nt)) * 4));  // (+ the sidecar's scan list)
     }
     clg::FusedCtl ctl{w, w + o_cnt, w + o_cnt + nt, w + o_cnt + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
@@ -1943,6 +1958,7 @@ struct clg_engine {
     ctl.rep = ab + 8;
     ctl.lb = w + o_lb;
     ctl.lean = !jser && (lean_env() >= 0 ? lean_env() != 0 : lean_hint) ? 1u : 0u;
+    ctl.side = side;
     // the scan writes the result into the pinned read-back buffer itself (no copy queued after
     // emit) while the spans are few: each span_hi is its own write across the bus, and for
     // config 4's 66 k spans those took 2.5 ms -- there one copy after emit reads them back
@@ -1984,6 +2000,8 @@ struct clg_engine {
         pa.r[4] = clg::PrepRange{d_zerr.as<uint32_t>(), nullptr, keep_errors ? nsw * 2 : 0, 0xFFFFFFFFu, 0};
         pa.r[5] = clg::PrepRange{jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, jser ? 2u : 0u, 0, 0};
         pa.r[6] = clg::PrepRange{d_ztiles.as<uint32_t>(), reinterpret_cast<const uint32_t*>(d_plan.p), runs ? 0 : L.tb / 4, 0, 0};
+        pa.r[7] = clg::PrepRange{jser ? d_zjwork.as<uint32_t>() + 2 + 2 * size_t(jwork_cap) : nullptr, nullptr,
+                                 jser && side.hdr ? 1u : 0u, 0, 0};  // the sidecar's scan-list count
         CHK(clg::launch_decode_prep(pa, stream));
       }
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
@@ -3013,6 +3031,19 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   e->pool = static_cast<uint8_t*>(p) + kPoolGuard;
   e->free_segs.resize(cfg->pool_segments);
   for (uint32_t i = 0; i < cfg->pool_segments; ++i) e->free_segs[i] = cfg->pool_segments - 1 - i;
+  e->seg_life.assign(cfg->pool_segments, 0u);
+  // the sidecar: C / 64 entries per segment (256 for 16 KiB: config 3 averages ~100), its
+  // positions 16 bits (segments up to 64 KiB); CLONOS_SIDECAR=0 turns it off (developer A/B)
+  const char* sc = getenv("CLONOS_SIDECAR");
+  if (cfg->segment_bytes <= 65536u && cfg->pool_segments && !(sc && atoi(sc) == 0)) {
+    const uint32_t cap = std::min<uint32_t>(clg::kSideCapMax, std::max<uint32_t>(8u, cfg->segment_bytes / 64u));
+    const size_t hb = size_t(cfg->pool_segments) * 8, eb = size_t(cfg->pool_segments) * cap * 4;
+    HIPCHK(hipMalloc(&p, hb + eb));
+    e->side_alloc = p;
+    HIPCHK(hipMemset(p, 0, hb));  // life 0: every segment's first chunk starts its list
+    e->side = clg::SideCar{static_cast<uint64_t*>(p), reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + hb),
+                           e->pool, pool_bytes, cfg->segment_bytes, cap};
+  }
   e->ifl_C = cfg->ifl_segment_bytes ? cfg->ifl_segment_bytes : 32768u;
   const uint32_t ifl_n = cfg->ifl_pool_segments ? cfg->ifl_pool_segments : 4096u;
   if (e->ifl_C % 16) return fail(CLG_E_INVALID_ARG, "ifl_segment_bytes must be a multiple of 16");
@@ -3044,6 +3075,7 @@ void clg_engine_destroy(clg_engine* e) {
   for (auto ev : e->zdone)
     if (ev) hipEventDestroy(ev);
   if (e->pool_alloc) hipFree(e->pool_alloc);
+  if (e->side_alloc) hipFree(e->side_alloc);
   if (e->ifl_alloc) hipFree(e->ifl_alloc);
   hipStreamDestroy(e->stream);
   if (e->gstream) hipStreamDestroy(e->gstream);
@@ -3121,6 +3153,7 @@ int clg_log_open(clg_engine* e, uint32_t job, const clg_causal_log_id* id, uint3
   l.open = true;
   if (e->free_segs.empty()) return fail(CLG_E_NOSPACE, "segment pool exhausted");
   l.segs.push_back(e->free_segs.back());  // ctor addComponent() :102
+  ++e->seg_life[e->free_segs.back()];
   e->free_segs.pop_back();
   const uint32_t h = uint32_t(e->logs.size());  // handles are never reused: a stale one is CLG_E_NO_LOG
   e->logs.push_back(std::move(l));

@@ -185,6 +185,27 @@ constexpr uint32_t kZRegion = 128;
 constexpr uint32_t kZTile = 64 * kZRegion;  // 8192
 constexpr uint32_t kZHalo = 64;             // bytes of the span's next tile staged after a tile
 
+// Serializable candidates recorded where the log bytes are written (k_scatter), so the
+// decode need not read the whole log to find them.  Per pool segment: hdr[s] = life << 32 |
+// entries, and ent[s * cap + i] = position in the segment (low 16 bits) | code << 16, code the
+// record length of the "03 AC ED 00 05" stream there (TC_STRING and flat objects complete
+// inside the written chunk) or kSideUnknown (another shape, a stream running past the chunk,
+// or a prefix of the magic at the chunk's end: the decode verifies the magic and walks the
+// stream).  `life` is the host's count of the segment's allocations (31 bits): the first
+// chunk of a new life resets the count.  A stream running past its chunk is measured on the
+// request's next chunks' bytes (contiguous in the source) when the chunk says it goes on.  entries > cap: the list overflowed, the decode scans the
+// segment's tiles.  Segments of more than 64 KiB carry no sidecar (hdr null).
+constexpr uint32_t kSideUnknown = 0xFFFFu;
+constexpr uint32_t kSideCapMax = 1024;  // entries per segment at most (C / 64, 64 KiB segments)
+struct SideCar {
+  uint64_t* hdr;
+  uint32_t* ent;
+  const uint8_t* pool;  // the segment pool (a tile outside it is scanned)
+  uint64_t pool_bytes;
+  uint32_t seg_bytes;
+  uint32_t cap;
+};
+
 struct FusedCtl {
   uint64_t* st_x;     // per tile: 1<<63 | exit (span offset) the successor enters at
   uint64_t* cnt;      // per tile: wide<<31 | records
@@ -207,7 +228,8 @@ struct FusedCtl {
   uint32_t jser;
   uint32_t jwork_cap;  // capacity of the general-walker work list
   uint32_t* jwork;     // [0]: items, [1]: overflow entries taken, then [2, 2 + cap): the items'
-                       // table slots, [2 + cap, 2 + 2 cap): their tiles
+                       // table slots, [2 + cap, 2 + 2 cap): their tiles; with the sidecar then
+                       // [2 + 2 cap]: tiles to scan, and those tiles (n_tiles words)
   uint32_t warm;    // speculative warm-up bytes before each region (| 1 << 31: not staggered by lane)
   JArena jar;       // the stream walker's spill arena (k_decode_jser_general)
   // Per-span fallback: a tile whose chain goes wrong (reasons 1-3, 5) sets span_bad[span]
@@ -245,6 +267,9 @@ struct FusedCtl {
   uint64_t* lb;
   uint64_t* h_res;
   uint32_t lean;  // batches without tables: the lean speculative walk (wide tags step one byte)
+  // The write path's Serializable candidates (SideCar, below): phase 3 builds a tile's table
+  // from its segment's list instead of scanning the tile (hdr null: every tile is scanned).
+  SideCar side;
 };
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile in LDS (more: the overflow arena)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
@@ -317,7 +342,8 @@ struct ScatterChunk {
   uint8_t* dst;        // inside one segment
   uint64_t src;        // offset into the staged upload buffer
   uint32_t len;
-  uint32_t pad;
+  uint32_t life;       // causal-log chunks: the segment's life stamp (SideCar, 31 bits) | 1 << 31:
+                       // the request goes on in the next chunk, its source bytes contiguous
 };
 
 // ---- device-side planning ---------------------------------------------------------
@@ -343,7 +369,7 @@ int launch_expand_tiles(const SegSpan* d_spans, uint32_t n_spans, uint32_t n_til
                         const uint8_t* pool, uint32_t seg_bytes, uint32_t unit, TileDesc* d_out, void* stream);
 // The fast decode's set-up in one launch: n_tiles tiles expanded from the runs (as
 // k_expand_tiles; 0: none), then each word range r[] copied from src or filled with val.
-constexpr int kPrepRanges = 7;
+constexpr int kPrepRanges = 8;
 struct PrepRange {
   uint32_t* dst;
   const uint32_t* src;  // null: fill
@@ -364,7 +390,9 @@ struct PrepArgs {
 int launch_decode_prep(PrepArgs a, void* stream);
 
 // ---- launchers (kernels.hip) -----------------------------------------------------------
-int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream);
+// side: the causal pool's sidecar (null: no candidates recorded, e.g. in-flight log buffers)
+int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream,
+                   const SideCar* side = nullptr);
 int launch_gather(const GatherPiece* d_pieces, uint32_t n, uint8_t* d_out, void* stream);
 // Robust pipeline (per-byte DP transfer tables); runs only on spans whose flag is set
 // (d_span_flags == nullptr: all spans).

@@ -17,6 +17,7 @@
 
 #include "../../include/clonos_engine.h"
 #include "dev_slow.h"
+#include "jser_flat.h"
 
 namespace clg {
 
@@ -88,17 +89,148 @@ __device__ __forceinline__ void copy_range(const uint8_t* src, uint8_t* dst, uin
 }
 
 // ==================================================================================
+// The write path's Serializable candidates (kernels.h SideCar): every "03 AC ED 00 05" of a
+// chunk -- the tag of a Serializable record and the stream magic, SimpleDeterminantEncoder
+// .java:316-341 -- with the record length where the stream's shape is one the decode measures
+// inline and it ends inside the chunk; a prefix of the magic at the chunk's end is listed
+// with an unknown length (the decode checks the magic against the bytes after it).
+// ==================================================================================
+constexpr uint64_t kMagic5 = 0x0500EDAC03ull;  // 03 AC ED 00 05, little-endian
+
+// Bytes q .. q+7 of the chunk s[0, len) little-endian, zero at and past len (q < len).  Only
+// aligned dwords holding a byte of the chunk are loaded, so no load leaves its pages.
+__device__ __forceinline__ uint64_t chunk8(const uint8_t* s, uint32_t len, uint32_t q) {
+  const uintptr_t b = (uintptr_t)s + q, a = b & ~(uintptr_t)3, e = (uintptr_t)s + len;
+  uint32_t d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) d[k] = a + 4u * k < e ? *reinterpret_cast<const uint32_t*>(a + 4u * k) : 0u;
+  const uint32_t sh = (uint32_t)(b & 3) * 8u;
+  const uint64_t lo = (uint64_t)d[0] | (uint64_t)d[1] << 32;
+  uint64_t v = sh ? (lo >> sh) | ((uint64_t)d[2] << (64u - sh)) : lo;
+  const uint32_t vb = len - q;
+  if (vb < 8) v &= (1ull << (8u * vb)) - 1ull;
+  return v;
+}
+
+// Record length of the full candidate at p (the decode's inline shapes: TC_STRING, flat
+// objects), or kSideUnknown: another shape, or the stream runs past the chunk.
+__device__ __forceinline__ uint32_t side_len(const uint8_t* s, uint32_t len, uint32_t p) {
+  if (p + 8 > len) return kSideUnknown;
+  auto rd4 = [s, len](uint32_t q) -> uint32_t { return q < len ? (uint32_t)chunk8(s, len, q) : 0u; };
+  const uint32_t v = rd4(p + 5);
+  uint32_t L = 0;
+  if ((v & 0xFFu) == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+    L = 8u + jf_be16_12(v);
+    if (p + L > len) L = 0;
+  } else if ((v & 0xFFu) == jser::TC_OBJECT) {
+    L = jser_flat_len_t(rd4, p, len);
+  }
+  return L && L < kSideUnknown ? L : kSideUnknown;
+}
+
+// One wave records chunk ch's candidates in its segment's list.  One pass over the chunk's
+// dwords (eight loads in flight per lane; a dword and the next one hold every candidate
+// starting in it) compacts the candidates' positions, in order, into the wave's LDS (`pos`,
+// S.cap words); one reservation in the header (its life checked: a new life starts the list
+// again); then a lane per candidate measures its stream and writes the entry.
+__device__ __forceinline__ void side_record(const ScatterChunk* __restrict__ chunks, uint32_t c, uint32_t n,
+                                            const ScatterChunk& ch, const uint8_t* s, const SideCar& S, uint32_t lane,
+                                            uint32_t* pos) {
+  const uint64_t off = (uint64_t)(ch.dst - S.pool);
+  const uint32_t seg = (uint32_t)(off / S.seg_bytes), so = (uint32_t)(off % S.seg_bytes), len = ch.len;
+  const uint32_t life = ch.life & 0x7FFFFFFFu;
+  // the request's bytes after this chunk (contiguous in the source), up to 64 KiB: the next
+  // chunks while each says the request goes on (at most four descriptors read)
+  uint32_t avail = len;
+  {
+    uint32_t more = ch.life >> 31, k = c + 1;
+    while (more && k < n && k <= c + 4 && avail - len < 65536u) {
+      const ScatterChunk nx = chunks[k++];
+      avail += nx.len;
+      more = nx.life >> 31;
+    }
+  }
+  const uintptr_t A0 = (uintptr_t)s & ~(uintptr_t)3;
+  const uint32_t lead = (uint32_t)((uintptr_t)s - A0);  // chunk bytes start at byte `lead` of dword 0
+  const uint32_t nd = (lead + len + 3u) >> 2;    // dwords holding a byte of the chunk
+  const uint32_t na = (lead + avail + 3u) >> 2;  // ... of the request's bytes from the chunk on
+  constexpr int kU = 8;
+  uint32_t total = 0;
+  for (uint32_t d0 = 0; d0 < nd; d0 += 64u * kU) {
+    uint32_t w[kU], x[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const uint32_t d = d0 + 64u * k + lane;
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(A0) + d;
+      w[k] = d < nd ? q[0] : 0u;
+      x[k] = d < nd && d + 1 < na ? q[1] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const uint32_t d = d0 + 64u * k + lane;
+      const uint64_t v = (uint64_t)w[k] | (uint64_t)x[k] << 32;
+      uint32_t c = 0;  // candidate's chunk position + 1 (at most one per dword: a second 03 within
+                       // four bytes of a first would lie inside that one's magic)
+#pragma unroll
+      for (uint32_t sh = 0; sh < 4; ++sh) {
+        const int64_t p = (int64_t)(4u * d + sh) - (int64_t)lead;
+        if (c || p < 0 || p >= (int64_t)len) continue;
+        const uint32_t kb = avail - (uint32_t)p < 5u ? avail - (uint32_t)p : 5u;  // magic bytes written
+        const uint64_t m = (1ull << (8u * kb)) - 1ull;
+        if (((v >> (8u * sh)) & m) == (kMagic5 & m)) c = (uint32_t)p + 1u;
+      }
+      const uint64_t bm = __ballot(c != 0);
+      if (c) {
+        const uint32_t i = total + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        if (i < S.cap) pos[i] = c - 1u;
+      }
+      total += (uint32_t)__popcll(bm);
+    }
+  }
+  uint32_t base = 0;
+  if (lane == 0) {
+    uint64_t* h = S.hdr + seg;
+    uint64_t old = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const bool same = (uint32_t)(old >> 32) == life;
+      if (same && !total) break;  // nothing to add, the life already stamped
+      const uint64_t nw = same ? old + total : ((uint64_t)life << 32 | total);
+      if (__hip_atomic_compare_exchange_strong(h, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        base = same ? (uint32_t)old : 0u;
+        break;
+      }
+    }
+  }
+  if (!total) return;
+  base = __shfl(base, 0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS stores before its reads
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t* ent = S.ent + (size_t)seg * S.cap;
+  for (uint32_t i = lane; i < total && base + i < S.cap; i += 64u) {
+    const uint32_t p = pos[i];
+    ent[base + i] = (so + p) | (p + 5u <= avail ? side_len(s, avail, p) : kSideUnknown) << 16;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next chunk's stores
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ==================================================================================
 // Append scatter: one wave per chunk (chunks are at most one segment; config 4's are
-// mostly a few hundred bytes), 16-byte stores.
+// mostly a few hundred bytes), 16-byte stores; causal-log chunks then record their
+// Serializable candidates (S.hdr set).
 // ==================================================================================
 __global__ __launch_bounds__(256) void k_scatter(const ScatterChunk* __restrict__ chunks, uint32_t n,
-                                                 const uint8_t* __restrict__ src) {
+                                                 const uint8_t* __restrict__ src, const SideCar S) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  __shared__ uint32_t s_pos[4][kSideCapMax];  // per wave: its chunk's candidates (S.cap <= kSideCapMax)
   for (uint32_t c = wave; c < n; c += nwaves) {
     const ScatterChunk ch = chunks[c];
     copy_range<64>(src + ch.src, ch.dst, ch.len, lane);
+    if (S.hdr) side_record(chunks, c, n, ch, src + ch.src, S, lane, s_pos[threadIdx.x >> 6]);
   }
 }
 
@@ -793,10 +925,16 @@ const char* take_launch_error() {
 
 static int ok(hipError_t e) { return launch_status(e); }
 
-int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream) {
+int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_src, void* stream, const SideCar* side) {
   if (!n) return CLG_OK;
   const uint32_t blocks = min((n + 3) / 4, 4096u);
-  hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_chunks, n, d_src);
+  SideCar S{};
+  if (side && side->hdr) {
+    if (!side->pool || !side->seg_bytes || side->seg_bytes > 65536u || !side->cap || side->cap > kSideCapMax)
+      return CLG_E_INVALID_ARG;
+    S = *side;
+  }
+  hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_chunks, n, d_src, S);
   return ok(hipGetLastError());
 }
 
