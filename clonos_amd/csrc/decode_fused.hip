@@ -2880,17 +2880,25 @@ __device__ __forceinline__ bool side_tile(const TileDesc* __restrict__ tiles, co
   ob = __shfl(ob, 0);
   const bool ovf_ok = total <= kZJCap || ob + (total - kZJCap) <= ctl.jovf_cap;
   *flagged = *flagged || total;
+  // in position order already (the usual case: a list is out of order only where chunks of one
+  // launch wrote one segment), else ranked
+  bool sorted = true;
+  for (uint32_t i = lane; i < total; i += 64u)
+    if (i && s_a[i - 1] >= s_a[i]) sorted = false;
+  sorted = __ballot(!sorted) == 0;
   uint32_t ngen = 0;  // (diagnostics)
   for (uint32_t i0 = 0; i0 < total; i0 += 64u) {  // wave-uniform: one work-list reservation per pass
     const uint32_t i = i0 + lane;
     const bool on = i < total;
     const uint32_t a = on ? s_a[i] : 0u, code = on ? s_c[i] : 0u;
-    uint32_t r = 0;  // rank by position (a list is in position order but for chunks of one launch)
-    if (on)
+    uint32_t r = i;  // rank by position
+    if (on && !sorted) {
+      r = 0;
       for (uint32_t j = 0; j < total; ++j) {
         const uint32_t b = s_a[j];
         r += b < a || (b == a && j < i) ? 1u : 0u;
       }
+    }
     uint64_t sl = ~0ull;
     if (on && r < kZJCap) sl = (uint64_t)t * kZJCap + r;
     else if (on && ovf_ok) sl = (uint64_t)ctl.n_tiles * kZJCap + ob + (r - kZJCap);
