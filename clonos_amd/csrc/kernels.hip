@@ -129,32 +129,27 @@ __device__ __forceinline__ uint32_t side_len(const uint8_t* s, uint32_t len, uin
 }
 
 // One wave records chunk ch's candidates in its segment's list.  One pass over the chunk's
-// dwords (eight loads in flight per lane; a dword and the next one hold every candidate
+// dwords (four dwords' loads in flight per lane; a dword and the next one hold every candidate
 // starting in it) compacts the candidates' positions, in order, into the wave's LDS (`pos`,
 // S.cap words); one reservation in the header (its life checked: a new life starts the list
 // again); then a lane per candidate measures its stream and writes the entry.
+// nx: the next chunk's descriptor when the request goes on into it (loaded by the caller
+// before the copy), else len 0.
 __device__ __forceinline__ void side_record(const ScatterChunk* __restrict__ chunks, uint32_t c, uint32_t n,
-                                            const ScatterChunk& ch, const uint8_t* s, const SideCar& S, uint32_t lane,
-                                            uint32_t* pos) {
+                                            const ScatterChunk& ch, const ScatterChunk& nx, const uint8_t* s,
+                                            const SideCar& S, uint32_t lane, uint32_t* pos) {
   const uint64_t off = (uint64_t)(ch.dst - S.pool);
   const uint32_t seg = (uint32_t)(off / S.seg_bytes), so = (uint32_t)(off % S.seg_bytes), len = ch.len;
   const uint32_t life = ch.life & 0x7FFFFFFFu;
-  // the request's bytes after this chunk (contiguous in the source), up to 64 KiB: the next
-  // chunks while each says the request goes on (at most four descriptors read)
-  uint32_t avail = len;
-  {
-    uint32_t more = ch.life >> 31, k = c + 1;
-    while (more && k < n && k <= c + 4 && avail - len < 65536u) {
-      const ScatterChunk nx = chunks[k++];
-      avail += nx.len;
-      more = nx.life >> 31;
-    }
-  }
+  // the request's bytes from this chunk through the next (contiguous in the source): enough to
+  // see a magic the chunk's end cuts (the next chunk is a whole segment, at least 16 bytes, or
+  // the request's last)
+  uint32_t avail = len + nx.len;
   const uintptr_t A0 = (uintptr_t)s & ~(uintptr_t)3;
   const uint32_t lead = (uint32_t)((uintptr_t)s - A0);  // chunk bytes start at byte `lead` of dword 0
   const uint32_t nd = (lead + len + 3u) >> 2;    // dwords holding a byte of the chunk
   const uint32_t na = (lead + avail + 3u) >> 2;  // ... of the request's bytes from the chunk on
-  constexpr int kU = 8;
+  constexpr int kU = 4;
   uint32_t total = 0;
   for (uint32_t d0 = 0; d0 < nd; d0 += 64u * kU) {
     uint32_t w[kU], x[kU];
@@ -168,13 +163,19 @@ __device__ __forceinline__ void side_record(const ScatterChunk* __restrict__ chu
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
       const uint32_t d = d0 + 64u * k + lane;
+      // a magic starting in dword d has its ED byte in bytes 2-3 of d or 0-1 of d + 1; only a
+      // prefix of it cut by the request's end ("03", "03 AC") has none: the exact test runs
+      // only where one of those can be
+      const uint32_t ed = ((w[k] >> 16) | (x[k] << 16)) ^ 0xEDEDEDEDu;
+      const bool maybe = d < nd && (((ed - 0x01010101u) & ~ed & 0x80808080u) || 4u * d + 8u > lead + avail);
+      if (!__ballot(maybe)) continue;
       const uint64_t v = (uint64_t)w[k] | (uint64_t)x[k] << 32;
       uint32_t c = 0;  // candidate's chunk position + 1 (at most one per dword: a second 03 within
                        // four bytes of a first would lie inside that one's magic)
 #pragma unroll
       for (uint32_t sh = 0; sh < 4; ++sh) {
         const int64_t p = (int64_t)(4u * d + sh) - (int64_t)lead;
-        if (c || p < 0 || p >= (int64_t)len) continue;
+        if (!maybe || c || p < 0 || p >= (int64_t)len) continue;
         const uint32_t kb = avail - (uint32_t)p < 5u ? avail - (uint32_t)p : 5u;  // magic bytes written
         const uint64_t m = (1ull << (8u * kb)) - 1ull;
         if (((v >> (8u * sh)) & m) == (kMagic5 & m)) c = (uint32_t)p + 1u;
@@ -187,6 +188,10 @@ __device__ __forceinline__ void side_record(const ScatterChunk* __restrict__ chu
       total += (uint32_t)__popcll(bm);
     }
   }
+  // A chunk that does not start its segment and holds no candidate has nothing to do: the
+  // segment's first chunk of this life (at offset 0: segments fill from their start) stamps
+  // the life; config 4's appends are mostly such chunks
+  if (!total && so) return;
   uint32_t base = 0;
   if (lane == 0) {
     uint64_t* h = S.hdr + seg;
@@ -204,6 +209,15 @@ __device__ __forceinline__ void side_record(const ScatterChunk* __restrict__ chu
   }
   if (!total) return;
   base = __shfl(base, 0);
+  // for the lengths: the request's bytes up to 64 KiB past the chunk (at most four descriptors)
+  {
+    uint32_t more = nx.life >> 31, k = c + 2;
+    while (more && k < n && k <= c + 4 && avail - len < 65536u) {
+      const ScatterChunk nk = chunks[k++];
+      avail += nk.len;
+      more = nk.life >> 31;
+    }
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the wave's LDS stores before its reads
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -226,11 +240,13 @@ __global__ __launch_bounds__(256) void k_scatter(const ScatterChunk* __restrict_
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  __shared__ uint32_t s_pos[4][kSideCapMax];  // per wave: its chunk's candidates (S.cap <= kSideCapMax)
+  extern __shared__ uint32_t s_pos[];  // per wave: its chunk's candidates, S.cap words (dynamic: 0 without S)
   for (uint32_t c = wave; c < n; c += nwaves) {
     const ScatterChunk ch = chunks[c];
+    ScatterChunk nx{nullptr, 0, 0, 0};  // (loaded before the copy: its latency under the copy's)
+    if (S.hdr && (ch.life >> 31) && c + 1 < n) nx = chunks[c + 1];
     copy_range<64>(src + ch.src, ch.dst, ch.len, lane);
-    if (S.hdr) side_record(chunks, c, n, ch, src + ch.src, S, lane, s_pos[threadIdx.x >> 6]);
+    if (S.hdr) side_record(chunks, c, n, ch, nx, src + ch.src, S, lane, s_pos + (threadIdx.x >> 6) * S.cap);
   }
 }
 
@@ -934,7 +950,8 @@ int launch_scatter(const ScatterChunk* d_chunks, uint32_t n, const uint8_t* d_sr
       return CLG_E_INVALID_ARG;
     S = *side;
   }
-  hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_chunks, n, d_src, S);
+  hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(256), S.hdr ? 4u * 4u * S.cap : 0u, (hipStream_t)stream, d_chunks, n,
+                     d_src, S);
   return ok(hipGetLastError());
 }
 
