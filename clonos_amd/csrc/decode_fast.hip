@@ -607,6 +607,68 @@ __device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* ge
   return p - a;
 }
 
+// A tile's table from the write path's sidecar (kernels.h SideCar): its segment's entries
+// inside the tile, taken when every one has a length the writer measured that ends inside the
+// span (the record length; the table holds the stream's, one less), ranked by position when
+// the list is out of order.  false: not applicable -- outside the pool, an overflowed list,
+// a candidate of unknown length or cut by the span's end (the caller scans the tile).
+// Block-uniform (one wave); s_a, s_c: kJserCap words of LDS each.
+__device__ __forceinline__ bool jfill_side(const TileDesc& td, const SpanDesc& sd, uint32_t t, const JserTabs& J,
+                                           uint32_t lane, uint32_t* s_a, uint32_t* s_c) {
+  const SideCar& S = J.side;
+  const uintptr_t ab = (uintptr_t)td.abase, pb = (uintptr_t)S.pool;
+  if (!S.hdr || ab < pb || ab - pb >= S.pool_bytes) return false;
+  const uint64_t off = ab - pb;
+  const uint32_t seg = (uint32_t)(off / S.seg_bytes), so0 = (uint32_t)(off % S.seg_bytes);
+  const uint32_t n = (uint32_t)S.hdr[seg];
+  if (n > S.cap) return false;
+  const uint32_t lo = so0 + td.delta, hi = lo + td.len;
+  const uint64_t end_a = sd.len - td.span_off + td.delta;  // the span's end, image coordinate
+  const uint32_t* ent = S.ent + (size_t)seg * S.cap;
+  uint32_t kept = 0;
+  bool bad = false;
+  for (uint32_t k0 = 0; k0 < n; k0 += 64u) {
+    const uint32_t k = k0 + lane;
+    bool in = false;
+    uint32_t a = 0, code = 0;
+    if (k < n) {
+      const uint32_t e = ent[k];
+      const uint32_t pos = e & 0xFFFFu;
+      code = e >> 16;
+      in = pos >= lo && pos < hi;
+      a = pos - so0;
+      bad = bad || (in && (code == kSideUnknown || (uint64_t)a + code > end_a));
+    }
+    const uint64_t m = __ballot(in);
+    if (in) {
+      const uint32_t i = kept + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (i < (uint32_t)kJserCap) {
+        s_a[i] = a;
+        s_c[i] = code;
+      }
+    }
+    kept += (uint32_t)__popcll(m);
+  }
+  if (__ballot(bad) || kept > (uint32_t)kJserCap) return false;
+  __syncthreads();
+  bool sorted = true;
+  for (uint32_t i = lane; i < kept; i += 64u)
+    if (i && s_a[i - 1] >= s_a[i]) sorted = false;
+  sorted = __ballot(!sorted) == 0;
+  for (uint32_t i = lane; i < kept; i += 64u) {
+    const uint32_t a = s_a[i];
+    uint32_t r = i;
+    if (!sorted) {
+      r = 0;
+      for (uint32_t j = 0; j < kept; ++j) r += s_a[j] < a || (s_a[j] == a && j < i) ? 1u : 0u;
+    }
+    J.pos[(uint64_t)t * kJserCap + r] = a;
+    J.len[(uint64_t)t * kJserCap + r] = s_c[i] - 1u;
+  }
+  if (lane == 0) J.n[t] = kept;
+  return true;
+}
+
 __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                   JserTabs J) {
   __shared__ uint32_t s_tile[kImageDwords];
@@ -617,6 +679,8 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   // deferred tiles, and the successor of a deferred tile (its segment crossing the tile
   // end, and its next-tile points, may land on Serializable records there)
   if (!J.defer[t] && !(t > sd.first_tile && J.defer[t - 1])) return;
+  if (jfill_side(td, sd, t, J, lane, s_tile, s_tile + kJserCap)) return;
+  __syncthreads();  // (the image's words were the sidecar path's scratch)
   CLG_JPHASE(0);
   SpanReader sr{tiles, sd.first_tile, sd.first_tile + sd.n_tiles, t, sd.len, J.ar};
   stage_tile(s_tile, td, sr, lane);

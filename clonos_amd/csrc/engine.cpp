@@ -2768,6 +2768,7 @@ struct clg_engine {
     clg::JArena jar;
     CHK(jarena_reset(&jar));
     clg::JserTabs J{d_jpos.as<uint32_t>(), d_jlen.as<uint32_t>(), d_jn.as<uint32_t>(), d_defer.as<uint32_t>(), jar};
+    J.side = side;  // (k_jser_fill takes a tile's table from the sidecar where it can)
     const char* rprof_path = getenv("CLONOS_ROBUST_PHASES");  // developer diagnostics (stamps per tile)
     if (rprof_path && d_rprof.ensure(std::max<size_t>(1, nt) * 16 * 8) == CLG_OK) {
       J.prof = d_rprof.as<uint64_t>();

@@ -152,6 +152,27 @@ struct JArena {
 constexpr int kCands = CLG_FCANDS;  // candidate entries per region (covers every fixed-layout record; <= 64)
 constexpr int kJserCap = 256;  // Serializable stream-length table entries per tile
 
+// Serializable candidates recorded where the log bytes are written (k_scatter), so the
+// decode need not read the whole log to find them.  Per pool segment: hdr[s] = life << 32 |
+// entries, and ent[s * cap + i] = position in the segment (low 16 bits) | code << 16, code the
+// record length of the "03 AC ED 00 05" stream there (TC_STRING and flat objects complete
+// inside the written chunk) or kSideUnknown (another shape, a stream running past the chunk,
+// or a prefix of the magic at the chunk's end: the decode verifies the magic and walks the
+// stream).  `life` is the host's count of the segment's allocations (31 bits): the first
+// chunk of a new life resets the count.  A stream running past its chunk is measured on the
+// request's next chunks' bytes (contiguous in the source) when the chunk says it goes on.  entries > cap: the list overflowed, the decode scans the
+// segment's tiles.  Segments of more than 64 KiB carry no sidecar (hdr null).
+constexpr uint32_t kSideUnknown = 0xFFFFu;
+constexpr uint32_t kSideCapMax = 1024;  // entries per segment at most (C / 64, 64 KiB segments)
+struct SideCar {
+  uint64_t* hdr;
+  uint32_t* ent;
+  const uint8_t* pool;  // the segment pool (a tile outside it is scanned)
+  uint64_t pool_bytes;
+  uint32_t seg_bytes;
+  uint32_t cap;
+};
+
 // Serializable stream lengths per tile, sorted by position (aligned coordinates):
 // pos/len[t * kJserCap + i], n[t] entries (n > kJserCap: overflow, span falls back);
 // defer[t] = 1 if the tile's scan met a "03 AC ED 00 05" pattern before the tables existed.
@@ -162,6 +183,7 @@ struct JserTabs {
   uint32_t* defer;
   JArena ar;
   uint64_t* prof = nullptr;  // developer diagnostics: 16 s_memtime stamps per tile (fill 0-7, emit 8-15)
+  SideCar side{};            // the write path's candidates (k_jser_fill takes a tile's table from them)
 };
 
 // Fused convergence + segment pass.  mode 0: every tile (tiles meeting a Serializable
@@ -184,27 +206,6 @@ int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
 constexpr uint32_t kZRegion = 128;
 constexpr uint32_t kZTile = 64 * kZRegion;  // 8192
 constexpr uint32_t kZHalo = 64;             // bytes of the span's next tile staged after a tile
-
-// Serializable candidates recorded where the log bytes are written (k_scatter), so the
-// decode need not read the whole log to find them.  Per pool segment: hdr[s] = life << 32 |
-// entries, and ent[s * cap + i] = position in the segment (low 16 bits) | code << 16, code the
-// record length of the "03 AC ED 00 05" stream there (TC_STRING and flat objects complete
-// inside the written chunk) or kSideUnknown (another shape, a stream running past the chunk,
-// or a prefix of the magic at the chunk's end: the decode verifies the magic and walks the
-// stream).  `life` is the host's count of the segment's allocations (31 bits): the first
-// chunk of a new life resets the count.  A stream running past its chunk is measured on the
-// request's next chunks' bytes (contiguous in the source) when the chunk says it goes on.  entries > cap: the list overflowed, the decode scans the
-// segment's tiles.  Segments of more than 64 KiB carry no sidecar (hdr null).
-constexpr uint32_t kSideUnknown = 0xFFFFu;
-constexpr uint32_t kSideCapMax = 1024;  // entries per segment at most (C / 64, 64 KiB segments)
-struct SideCar {
-  uint64_t* hdr;
-  uint32_t* ent;
-  const uint8_t* pool;  // the segment pool (a tile outside it is scanned)
-  uint64_t pool_bytes;
-  uint32_t seg_bytes;
-  uint32_t cap;
-};
 
 struct FusedCtl {
   uint64_t* st_x;     // per tile: 1<<63 | exit (span offset) the successor enters at

@@ -60,9 +60,9 @@ def _cuts(rng, n: int, hi: int = 300):
     return cuts
 
 
-def _engine(monkeypatch, side: bool, seg: int, pool: int = 8192) -> Engine:
+def _engine(monkeypatch, side: bool, seg: int, pool: int = 8192, decode: str = "auto") -> Engine:
     monkeypatch.setenv("CLONOS_SIDECAR", "1" if side else "0")
-    return Engine(segment_bytes=seg, pool_segments=pool)
+    return Engine(segment_bytes=seg, pool_segments=pool, decode=decode)
 
 
 def _write_host(eng, logs, blobs, rng):
@@ -223,3 +223,20 @@ def test_config3_epochs_equal_with_and_without_the_sidecar(monkeypatch):
                 assert_span_equal(dec, s, b"".join(epochs[(e + v) % 4] for e in range(4)))
     for k in outs[0]:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("seg", [256, 16384])
+@pytest.mark.parametrize("side", [True, False], ids=["sidecar", "scan"])
+def test_robust_pipeline_tables_from_the_sidecar(monkeypatch, seg, side):
+    """The robust pipeline's table fill (k_jser_fill) takes a deferred tile's table from the
+    sidecar when every candidate's length is known, else scans the tile: both bit-exact."""
+    rng = np.random.default_rng(seg + side)
+    with _engine(monkeypatch, side, seg, decode="robust") as eng:
+        logs = [eng.open_log(CausalLogID.main(v)) for v in range(5)]
+        blobs = [_mixed(rng, int(rng.integers(300, 1200))) for _ in range(5)]
+        _write_host(eng, logs[:3], blobs[:3], rng)
+        _write_device(eng, logs[3:], blobs[3:], rng)
+        for _ in range(2):
+            dec = eng.decode_logs(logs, [0] * 5)
+            for s_, b in enumerate(blobs):
+                assert_span_equal(dec, s_, b)
