@@ -3466,7 +3466,9 @@ int clg_consumer_seek(clg_engine* e, uint32_t h, clg_channel_id c, int64_t epoch
 }
 
 int clg_upstream_delta_batch(clg_engine* e, clg_delta_req* reqs, uint32_t n, const uint8_t* bytes, uint32_t in_kind) {
-  ENGINE_GUARD(e);
+  ENGINE_GUARD_KEEP(e);
+  clg_engine::HostTimer ht(e, "host_abi_upstream");  // (CLONOS_HOST_PROF: lock held to here; settle and the call)
+  e->settle();
   if (n && (!reqs || !bytes)) return fail(CLG_E_INVALID_ARG, "null argument");
   return e->upstream_batch(reqs, n, bytes, in_kind);
 }
