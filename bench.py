@@ -856,10 +856,38 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
         eng.decode_logs_device(handles, starts, dec, base)
     assert dec.n_rec == n_det and dec.err_status == 0
     torch.cuda.synchronize()
+    t0 = _t.perf_counter()
+    for _ in range(steps):  # one decode at a time (the host's planning and completion between them)
+        eng.decode_logs_device(handles, starts, dec, base)
+    torch.cuda.synchronize()
+    el_sync = (_t.perf_counter() - t0) / steps
+    # the step as config 2 runs it: two decodes in flight (CLG_DECODE_MAX_INFLIGHT), each with its
+    # own outputs, so the GPU does not wait for the host between decodes
+    dec2 = _lib.Decoded()
+    o2 = [torch.empty_like(t) for t in o] + [torch.empty_like(t) for t in ow]
+    dec2.off, dec2.tag, dec2.v0 = [t.data_ptr() for t in o2[:3]]
+    dec2.w_idx, dec2.w_rc, dec2.w_v1, dec2.w_var_off, dec2.w_var_len, dec2.w_sub = [t.data_ptr() for t in o2[3:]]
+    dec2.cap, dec2.wcap, dec2.out_kind = cap, wcap, _lib.CLG_MEM_DEVICE
+    pairs, queued = [(dec, base), (dec2, np.zeros_like(base))], []
+
+    def run_async(k):
+        for i in range(k):
+            if len(queued) == 2:
+                eng.decode_wait()
+                d_ = queued.pop(0)
+                assert d_.n_rec == n_det and d_.err_status == 0
+            d_, b_ = pairs[i % 2]
+            eng.decode_logs_device_async(handles, starts, d_, b_)
+            queued.append(d_)
+        while queued:
+            eng.decode_wait()
+            d_ = queued.pop(0)
+            assert d_.n_rec == n_det and d_.err_status == 0
+    run_async(2)  # warm-up
+    torch.cuda.synchronize()
     eng.kernel_stats_reset()
     t0 = _t.perf_counter()
-    for _ in range(steps):
-        eng.decode_logs_device(handles, starts, dec, base)
+    run_async(steps)
     torch.cuda.synchronize()
     el = (_t.perf_counter() - t0) / steps
     st = eng.kernel_stats()
@@ -903,6 +931,7 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     out = {"workload": f"config3: {n_logs} subtask logs x {n_epochs} epochs x {per_epoch} mixed determinants "
                        "(incl. Serializable, BufferBuilt), decode", "log_bytes": total, "determinants": n_det,
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
+           "ms_per_step_one_at_a_time": round(el_sync * 1e3, 4),
            "log_gbs": round(total / el / 1e9, 2), "algo_gbs": round(algo / el / 1e9, 1),
            "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern,
            "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)},

@@ -13,7 +13,7 @@ python3 - <<'P'
 import json
 d=[json.loads(l) for l in open("gpurun_out/full/bench.json") if l.startswith("{")][-1]
 print("value", d["value"], "ms", d["ms_per_step"], "roof", d["roofline"]["frac"], "cpu", d["cpu_baseline"]["value"])
-print("c3", d["config3"]["ms_per_step"], "robust", d["config3"]["robust_pipeline"]["ms_per_step"])
+print("c3", d["config3"]["ms_per_step"], d["config3"].get("ms_per_step_one_at_a_time"), d["config3"]["hbm_frac"], "robust", d["config3"]["robust_pipeline"]["ms_per_step"])
 print("c4", d["config4"]["ms_per_step"], "c5", d["config5"]["latency_ms"], d["config5"]["phase_ms_max_over_ranks"])
 print("c1", {k: v for k, v in d["config1"].items() if "ms" in k})
 P
