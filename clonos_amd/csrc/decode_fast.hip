@@ -578,8 +578,8 @@ __device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* ge
   for (int depth = 0;; ++depth) {
     if (p + 1 > a + lim || depth > 8) return 0u;
     const uint32_t c = b(p);  // [TC_CLASSDESC][className length u16] or [TC_NULL]
-    if (c == jser::TC_NULL) {  // no (further) superclass
-      ++p;
+    if (c == jser::TC_NULL && depth > 0) {  // no (further) superclass (a null class of the object
+      ++p;                                   // itself: the walker, which rejects it)
       break;
     }
     if (c != jser::TC_CLASSDESC || p + 3 > a + lim) return 0u;

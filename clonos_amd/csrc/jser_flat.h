@@ -6,7 +6,8 @@
 // Object Serialization Specification 6.4 (newObject, newClassDesc, classDescInfo, fieldDesc,
 // nowrclass); the records are SimpleDeterminantEncoder.java:316-341's.  Shared by the decode
 // (bytes from the LDS image) and the write path's sidecar (bytes from the staged chunk), so
-// both give the same length for the same bytes.
+// both give the same length for the same bytes; compiled for the host by
+// tests/jser_walker_host.cpp, where tests/test_jser_reference.py holds it to the oracle.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,13 +16,13 @@
 
 namespace clg {
 
-__device__ __forceinline__ uint32_t jf_be16_12(uint32_t v) { return ((v >> 8) & 0xFFu) << 8 | ((v >> 16) & 0xFFu); }
+__host__ __device__ __forceinline__ uint32_t jf_be16_12(uint32_t v) { return ((v >> 8) & 0xFFu) << 8 | ((v >> 16) & 0xFFu); }
 
 // rd4(q): bytes q .. q+3 little-endian (bytes at or past `end` may be anything).  a: the
 // record's tag byte ("03", then AC ED 00 05).  Returns the record length, or 0: some other
 // shape (the general walker decides), or the stream does not end before `end`.
 template <class Rd4>
-__device__ __forceinline__ uint32_t jser_flat_len_t(Rd4&& rd4, uint32_t a, uint32_t end) {
+__host__ __device__ __forceinline__ uint32_t jser_flat_len_t(Rd4&& rd4, uint32_t a, uint32_t end) {
   uint32_t p = a + 5;  // after the tag and AC ED 00 05
   if (p + 1 > end || (rd4(p) & 0xFFu) != jser::TC_OBJECT) return 0u;
   ++p;
@@ -30,8 +31,8 @@ __device__ __forceinline__ uint32_t jser_flat_len_t(Rd4&& rd4, uint32_t a, uint3
     if (p + 1 > end || depth > 8) return 0u;
     const uint32_t v = rd4(p);  // [TC_CLASSDESC][className length u16] or [TC_NULL]
     const uint32_t b = v & 0xFFu;
-    if (b == jser::TC_NULL) {  // no (further) superclass
-      ++p;
+    if (b == jser::TC_NULL && depth > 0) {  // no (further) superclass (the object's own class
+      ++p;                                   // null: not a stream the JDK reads -- the walker says so)
       break;
     }
     if (b != jser::TC_CLASSDESC || p + 3 > end) return 0u;

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../clonos_amd/csrc/jser_device.h"
+#include "../clonos_amd/csrc/jser_flat.h"
 
 namespace {
 struct HostBytes {
@@ -38,4 +39,16 @@ extern "C" int64_t walker_stream_len(const uint8_t* p, uint64_t n, uint64_t aren
   const int64_t r = clg::jser::stream_len(at, n, ar);
   if (spilled) *spilled = used;
   return r;
+}
+
+// The inline flat-object length (clonos_amd/csrc/jser_flat.h) of the record rec[0, n) (tag
+// byte first): the record length, or 0 (another shape, or the stream does not end in n).
+extern "C" uint32_t flat_record_len(const uint8_t* rec, uint32_t n) {
+  auto rd4 = [rec, n](uint32_t q) -> uint32_t {
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k)
+      if (q + k < n) v |= uint32_t(rec[q + k]) << (8 * k);
+    return v;
+  };
+  return clg::jser_flat_len_t(rd4, 0u, n);
 }

@@ -240,3 +240,27 @@ def test_robust_pipeline_tables_from_the_sidecar(monkeypatch, seg, side):
             dec = eng.decode_logs(logs, [0] * 5)
             for s_, b in enumerate(blobs):
                 assert_span_equal(dec, s_, b)
+
+
+@pytest.mark.parametrize("mode", ["sidecar", "scan", "robust", "host"])
+def test_object_with_a_null_class_is_an_error(monkeypatch, mode):
+    """03 AC ED 00 05 73 70: a TC_OBJECT whose class descriptor is TC_NULL is no stream the JDK
+    reads (the reference's decodeNext throws); the inline flat-object parser once took it for a
+    7-byte record.  Every path reports the oracle's error at its offset."""
+    rng = np.random.default_rng(17)
+    bad = b"\x03\xac\xed\x00\x05\x73\x70"
+    blob = synth.random_log(200, rng, allow_serializable=False) + _ser(rng) + bad + \
+        synth.random_log(30, rng, allow_serializable=False)
+    st, _, eo, et = O.decode(blob)
+    assert st != 0
+    with _engine(monkeypatch, mode != "scan", 16384, decode="robust" if mode == "robust" else "auto") as eng:
+        for _ in range(2):  # (the second batch with the table hint set)
+            with pytest.raises(_lib.ClonosError) as ex:
+                if mode == "host":
+                    eng.decode_host(blob)
+                else:
+                    lg = eng.open_log(CausalLogID.main(int(rng.integers(0, 1 << 30))))
+                    lg.appendDeterminant(blob, 0)
+                    eng.sync()
+                    eng.decode_logs([lg], [0])
+            assert (ex.value.status, ex.value.err_off, ex.value.err_tag) == (st, eo, et)

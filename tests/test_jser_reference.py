@@ -39,11 +39,14 @@ def walker(tmp_path_factory):
     lib = C.CDLL(so)
     lib.walker_stream_len.restype = C.c_int64
     lib.walker_stream_len.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
+    lib.flat_record_len.restype = C.c_uint32
+    lib.flat_record_len.argtypes = [C.c_char_p, C.c_uint32]
 
     def run(b: bytes, arena: int = 1 << 22):
         used = C.c_uint64()
         r = lib.walker_stream_len(b, len(b), arena, C.byref(used))
         return r, used.value
+    run.flat = lambda rec: lib.flat_record_len(rec, len(rec))
     return run
 
 
@@ -173,3 +176,37 @@ def test_many_handles_and_descriptors(walker):
     assert r1 == -2
     r2, used = walker(s, 1 << 20)
     assert r2 == len(s) and used > 4 * 5300
+
+
+def test_flat_parser_agrees_with_the_oracle(walker):
+    """The inline flat-object parser (jser_flat.h) that both the decode and the write path's
+    sidecar trust for lengths: on every reference stream, the flat shapes the synthetic
+    configs write, and seeded mutations, a length it gives is the oracle's record length
+    (1 + the stream's), and a stream it cannot finish inside the bytes gives 0 (the walker
+    decides)."""
+    from clonos_amd import determinants as D
+    rng = random.Random(0xF1A7)
+    shapes = [D.jser_boolean(True), D.jser_boolean(False), D.jser_integer(-7), D.jser_integer(2 ** 31 - 1),
+              D.jser_long(-(2 ** 62)), D.jser_long(12345)]
+    base = list(STREAMS) + shapes
+    streams = list(base)
+    for k in range(3000):
+        s = bytearray(rng.choice(base))
+        op = k % 3
+        if op == 0:
+            s[rng.randrange(4, len(s))] = rng.randrange(256)
+        elif op == 1:
+            s = s[:rng.randrange(4, len(s) + 1)]
+        streams.append(bytes(s))
+    n_flat = 0
+    for s in streams:
+        rec = b"\x03" + s + bytes([0x70, 0x00, 0x78, 0xAC, 0xED])  # (a tail: the stream ends where it ends)
+        L = walker.flat(rec)
+        if L:
+            n_flat += 1
+            assert O.jser_len(rec[1:]) == L - 1, (s.hex(), L)
+            assert walker.flat(rec[:L]) == L  # the bytes up to its end suffice
+            assert walker.flat(rec[:L - 1]) == 0  # one short: not finished inside the bytes
+    for s in shapes:
+        assert walker.flat(b"\x03" + s) == 1 + len(s)
+    assert n_flat > 100
