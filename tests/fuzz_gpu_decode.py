@@ -29,10 +29,31 @@ ap.add_argument("--seed", type=int, default=1)
 args = ap.parse_args()
 
 
+def flat_mutant(rng):
+    """A Serializable record of one of the flat shapes the inline parsers measure, mutated where
+    those parsers decide: a byte of the stream flipped or replaced by a grammar code (TC_NULL,
+    TC_CLASSDESC, TC_ENDBLOCKDATA, a field typecode), or the stream cut short."""
+    s = bytearray(rng.choice([D.jser_boolean(True), D.jser_integer(int(rng.integers(-99, 99))),
+                              D.jser_long(int(rng.integers(0, 1 << 40))), D.jser_string("s" * int(rng.integers(0, 20)))]))
+    op = int(rng.integers(0, 3))
+    q = int(rng.integers(4, len(s)))
+    if op == 0:
+        s[q] = int(rng.integers(0, 256))
+    elif op == 1:
+        s[q] = int(rng.choice([0x70, 0x71, 0x72, 0x73, 0x74, 0x78, ord("I"), ord("Z"), ord("J"), ord("["), 0x00, 0x01, 0x02]))
+    else:
+        s = s[:q]
+    return D.encode(D.SerializableDeterminant(bytes(s)))
+
+
 def span_bytes(rng):
-    k = int(rng.integers(0, 10))
+    k = int(rng.integers(0, 11))
     if k == 0:
         return b""
+    if k == 10:  # mutated flat Serializable shapes among ordinary records
+        return b"".join(flat_mutant(rng) if rng.random() < 0.2 else
+                        D.encode(synth.random_determinant(rng, allow_serializable=False))
+                        for _ in range(int(rng.integers(1, 200))))
     if k <= 4:
         return synth.random_log(int(rng.integers(1, 3000)), rng)
     if k == 5:  # config-3 epoch piece
