@@ -567,9 +567,25 @@ __device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* ge
     return 0u;
   }
   const uint32_t tc = b(a + 5);
-  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+  // bytes [q, q + n) as readUTF takes them (modified UTF-8, jser_flat.h jf_mutf; byte by byte:
+  // the reader is not asked for bytes past them)
+  auto mutf = [&](uint32_t q, uint32_t n) {
+    for (uint32_t i = 0; i < n;) {
+      const uint32_t b1 = b(q + i);
+      if (b1 < 0x80u) {
+        ++i;
+        continue;
+      }
+      const uint32_t k = (b1 >> 5) == 6u ? 2u : (b1 >> 4) == 14u ? 3u : 0u;
+      if (!k || n - i < k || (b(q + i + 1) & 0xC0u) != 0x80u || (k == 3u && (b(q + i + 2) & 0xC0u) != 0x80u))
+        return false;
+      i += k;
+    }
+    return true;
+  };
+  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][modified UTF-8]
     const uint64_t L = 8ull + u16(a + 6);
-    return L <= avail ? (uint32_t)L : 0u;
+    return L <= avail && mutf(a + 8, (uint32_t)L - 8u) ? (uint32_t)L : 0u;
   }
   *general = true;
   if (tc != jser::TC_OBJECT) return 0u;
@@ -583,8 +599,9 @@ __device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* ge
       break;
     }
     if (c != jser::TC_CLASSDESC || p + 3 > a + lim) return 0u;
-    p += 3 + u16(p + 1) + 8;  // className, serialVersionUID
-    if (p + 3 > a + lim) return 0u;
+    const uint32_t nq = p + 3, nl = u16(p + 1);
+    p += 3 + nl + 8;  // className, serialVersionUID
+    if (p + 3 > a + lim || !mutf(nq, nl)) return 0u;
     if (b(p) != jser::SC_SERIALIZABLE) return 0u;
     const uint32_t nf = u16(p + 1);
     if (nf & 0x8000u) return 0u;
@@ -596,7 +613,9 @@ __device__ uint32_t jser_inline_len_r(R& r, uint32_t a, uint64_t avail, bool* ge
                           : ft == 'J' || ft == 'D' ? 8u : 0u;
       if (!sz) return 0u;
       data += sz;
-      p += 3 + u16(p + 1);
+      const uint32_t fq = p + 3, fl = u16(p + 1);
+      p += 3 + fl;
+      if (p > a + lim || !mutf(fq, fl)) return 0u;  // the field name
     }
     if (p + 1 > a + lim || b(p) != jser::TC_ENDBLOCKDATA) return 0u;
     ++p;

@@ -2637,9 +2637,14 @@ __device__ __forceinline__ uint32_t jser_inline_len(const uint32_t* T, uint32_t 
   const uint32_t v = z4(T, a + 5);
   const uint32_t tc = v & 0xFFu;
   *general = false;
-  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+  if (tc == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][modified UTF-8]
     const uint64_t L = 8ull + be16_12(v);
-    return L <= avail ? (uint32_t)L : 0u;
+    if (L > avail) return 0u;
+    if ((uint64_t)a + L > img_end) {  // its bytes past the image: the walker checks them
+      *general = true;
+      return 0u;
+    }
+    return jf_mutf([T](uint32_t q) { return z4(T, q); }, a + 8u, (uint32_t)L - 8u) ? (uint32_t)L : 0u;
   }
   const uint32_t fl = tc == jser::TC_OBJECT ? jser_flat_len(T, a, img_end) : 0u;
   if (fl) return fl <= avail ? fl : 0u;

@@ -86,7 +86,9 @@ __host__ __device__ inline bool grow(const A& ar, T*& p, uint32_t& cap, uint32_t
   return true;
 }
 
-// F: callable returning the byte at stream offset k (k < avail), as int.  A: spill
+// F: callable returning the byte at stream offset k (k < avail), as int; the walk asks for
+// offsets in non-decreasing order (the device readers keep a forward-only cursor over the
+// span's tiles: an offset before it would be read out of bounds).  A: spill
 // allocator (take(bytes) -> pointer or null).  Returns the stream length (magic through
 // the end of the first object), kJsInvalid or kJsSpill.
 template <class F, class A>
@@ -140,6 +142,33 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
     pos += 4;
     return (int32_t)v;
   };
+  // bytes [pos, pos + l) (present) as readUTF takes them: modified UTF-8, JDK 8
+  // BlockDataInputStream.readUTFBody -- units 0xxxxxxx, 110xxxxx 10xxxxxx, 1110xxxx 10xxxxxx
+  // 10xxxxxx, none cut by the length; anything else is UTFDataFormatException.  Every byte read
+  // once, in order; *c01 (optional): the first two (0 past the end)
+  auto mutf = [&](uint64_t l, uint32_t* c01 = nullptr) -> bool {
+    uint32_t first = 0;
+    for (uint64_t i = 0; i < l;) {
+      const uint32_t b1 = (uint32_t)at(pos + i);
+      if (i == 0) first = b1;
+      if (b1 < 0x80u) {
+        if (i == 1) first |= b1 << 8;
+        ++i;
+        continue;
+      }
+      const uint64_t k = (b1 >> 5) == 6u ? 2u : (b1 >> 4) == 14u ? 3u : 0u;
+      if (!k || l - i < k) return false;
+      if (i == 1) first |= b1 << 8;
+      for (uint64_t j = 1; j < k; ++j) {
+        const uint32_t bj = (uint32_t)at(pos + i + j);
+        if (i + j == 1) first |= bj << 8;
+        if ((bj & 0xC0u) != 0x80u) return false;
+      }
+      i += k;
+    }
+    if (c01) *c01 = first;
+    return true;
+  };
 
   // Termination: every step consumes bytes, pushes a frame that will, pops, or advances a
   // frame's bounded state (class index < chain length <= kMaxChain); no step bound needed.
@@ -172,6 +201,7 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
             JS_NEED(2);
             const uint32_t l = u16();
             JS_NEED(l);
+            if (!mutf(l)) JS_FAIL;
             pos += l;
             break;
           }
@@ -180,7 +210,7 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
             JS_NEED(8);
             const uint64_t hi = (uint32_t)s32(), lo = (uint32_t)s32();
             const uint64_t l = hi << 32 | lo;
-            if (l > avail - pos) JS_FAIL;
+            if (l > avail - pos || !mutf(l)) JS_FAIL;  // readLongUTF
             pos += l;
             break;
           }
@@ -265,7 +295,9 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
             JS_NEED(2);
             const uint32_t l = u16();
             JS_NEED(l);
-            const uint8_t c0 = l > 0 ? (uint8_t)at(pos) : 0, c1 = l > 1 ? (uint8_t)at(pos + 1) : 0;
+            uint32_t c01 = 0;  // (its first two bytes, read by the check: readers only go forwards)
+            if (!mutf(l, &c01)) JS_FAIL;  // the class name
+            const uint8_t c0 = (uint8_t)c01, c1 = (uint8_t)(c01 >> 8);
             pos += l;
             JS_NEED(8);
             pos += 8;  // serialVersionUID
@@ -292,6 +324,7 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
               JS_NEED(2);
               const uint32_t l = u16();
               JS_NEED(l);
+              if (!mutf(l)) JS_FAIL;  // an interface name
               pos += l;
             }
             f.d = di;
@@ -309,6 +342,7 @@ __host__ __device__ __noinline__ int64_t stream_len(F& at, uint64_t avail, const
             JS_NEED(2);
             const uint32_t l = u16();
             JS_NEED(l);
+            if (!mutf(l)) JS_FAIL;
             pos += l;  // field name
             const bool obj = t == 'L' || t == '[';
             if (!obj && !(t == 'B' || t == 'C' || t == 'D' || t == 'F' || t == 'I' || t == 'J' || t == 'S' || t == 'Z'))

@@ -18,6 +18,30 @@ namespace clg {
 
 __host__ __device__ __forceinline__ uint32_t jf_be16_12(uint32_t v) { return ((v >> 8) & 0xFFu) << 8 | ((v >> 16) & 0xFFu); }
 
+// Bytes [q, q + len) as readUTF takes them (all present): modified UTF-8, JDK 8
+// ObjectInputStream.BlockDataInputStream.readUTFBody -- units 0xxxxxxx, 110xxxxx 10xxxxxx,
+// 1110xxxx 10xxxxxx 10xxxxxx, none cut by the length (else UTFDataFormatException).  Four
+// ASCII bytes at a time.
+template <class Rd4>
+__host__ __device__ __forceinline__ bool jf_mutf(Rd4&& rd4, uint32_t q, uint32_t len) {
+  for (uint32_t i = 0; i < len;) {
+    const uint32_t w = rd4(q + i);
+    if (len - i >= 4u && !(w & 0x80808080u)) {
+      i += 4u;
+      continue;
+    }
+    const uint32_t b1 = w & 0xFFu;
+    if (b1 < 0x80u) {
+      ++i;
+      continue;
+    }
+    const uint32_t k = (b1 >> 5) == 6u ? 2u : (b1 >> 4) == 14u ? 3u : 0u;
+    if (!k || len - i < k || ((w >> 8) & 0xC0u) != 0x80u || (k == 3u && ((w >> 16) & 0xC0u) != 0x80u)) return false;
+    i += k;
+  }
+  return true;
+}
+
 // rd4(q): bytes q .. q+3 little-endian (bytes at or past `end` may be anything).  a: the
 // record's tag byte ("03", then AC ED 00 05).  Returns the record length, or 0: some other
 // shape (the general walker decides), or the stream does not end before `end`.
@@ -36,8 +60,9 @@ __host__ __device__ __forceinline__ uint32_t jser_flat_len_t(Rd4&& rd4, uint32_t
       break;
     }
     if (b != jser::TC_CLASSDESC || p + 3 > end) return 0u;
-    p += 3 + jf_be16_12(v) + 8;  // className, serialVersionUID
-    if (p + 3 > end) return 0u;
+    const uint32_t nq = p + 3, nl = jf_be16_12(v);
+    p += 3 + nl + 8;  // className, serialVersionUID
+    if (p + 3 > end || !jf_mutf(rd4, nq, nl)) return 0u;
     const uint32_t f = rd4(p);  // [flags][field count u16]
     if ((f & 0xFFu) != jser::SC_SERIALIZABLE) return 0u;
     const uint32_t nf = jf_be16_12(f);
@@ -52,7 +77,9 @@ __host__ __device__ __forceinline__ uint32_t jser_flat_len_t(Rd4&& rd4, uint32_t
                           : tc == 'J' || tc == 'D' ? 8u : 0u;
       if (!sz) return 0u;
       data += sz;
-      p += 3 + jf_be16_12(fv);
+      const uint32_t fq = p + 3, fl = jf_be16_12(fv);
+      p += 3 + fl;
+      if (p > end || !jf_mutf(rd4, fq, fl)) return 0u;  // the field name
     }
     if (p + 1 > end || (rd4(p) & 0xFFu) != jser::TC_ENDBLOCKDATA) return 0u;
     ++p;

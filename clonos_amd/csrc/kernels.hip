@@ -119,9 +119,9 @@ __device__ __forceinline__ uint32_t side_len(const uint8_t* s, uint32_t len, uin
   auto rd4 = [s, len](uint32_t q) -> uint32_t { return q < len ? (uint32_t)chunk8(s, len, q) : 0u; };
   const uint32_t v = rd4(p + 5);
   uint32_t L = 0;
-  if ((v & 0xFFu) == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][utf8]
+  if ((v & 0xFFu) == jser::TC_STRING) {  // [03][AC ED 00 05][74][len u16][modified UTF-8]
     L = 8u + jf_be16_12(v);
-    if (p + L > len) L = 0;
+    if (p + L > len || !jf_mutf(rd4, p + 8u, L - 8u)) L = 0;  // (malformed: the decode's walker rejects it)
   } else if ((v & 0xFFu) == jser::TC_OBJECT) {
     L = jser_flat_len_t(rd4, p, len);
   }

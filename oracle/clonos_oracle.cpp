@@ -59,9 +59,24 @@ struct JWalker {
   bool u16(uint32_t& v) { if (!need(2)) return false; v = (uint32_t(b[pos]) << 8) | b[pos + 1]; pos += 2; return true; }
   bool s32(int32_t& v) { if (!need(4)) return false; v = int32_t(be32(b + pos)); pos += 4; return true; }
   bool skip(uint64_t k) { if (k > n - pos) return false; pos += size_t(k); return true; }
-  bool utf(std::string* out) {
+  // Modified UTF-8 as JDK 8 reads it (ObjectInputStream.BlockDataInputStream.readUTFBody /
+  // readUTFSpan): every unit 0xxxxxxx, 110xxxxx 10xxxxxx or 1110xxxx 10xxxxxx 10xxxxxx, none
+  // cut by the length; anything else throws UTFDataFormatException.
+  static bool mutf(const uint8_t* s, uint64_t len) {
+    for (uint64_t i = 0; i < len;) {
+      const uint8_t b1 = s[i];
+      if (b1 < 0x80) { ++i; continue; }
+      const uint64_t k = (b1 >> 5) == 6 ? 2 : (b1 >> 4) == 14 ? 3 : 0;
+      if (!k || len - i < k) return false;
+      for (uint64_t j = 1; j < k; ++j)
+        if ((s[i + j] & 0xC0) != 0x80) return false;
+      i += k;
+    }
+    return true;
+  }
+  bool utf(std::string* out) {  // readUTF
     uint32_t len;
-    if (!u16(len) || !need(len)) return false;
+    if (!u16(len) || !need(len) || !mutf(b + pos, len)) return false;
     if (out) out->assign(reinterpret_cast<const char*>(b + pos), len);
     pos += len;
     return true;
@@ -205,7 +220,7 @@ struct JWalker {
         if (!need(8)) return false;
         uint64_t len = be64(b + pos);
         pos += 8;
-        return skip(len);
+        return len <= n - pos && mutf(b + pos, len) && skip(len);  // readLongUTF
       }
       case TC_CLASSDESC: case TC_PROXYCLASSDESC: {
         pos--;

@@ -30,6 +30,23 @@ class DecodeError(Exception):
 # Java serialization stream length (recursive descent; independent of the C++ walker)
 # --------------------------------------------------------------------------------------
 MAX_DEPTH = 512  # open obj() calls: the JVM's StackOverflowError, which the reference does not catch
+
+
+def _mutf(b):
+    """Modified UTF-8 as JDK 8's ObjectInputStream reads it (readUTFBody / readUTFSpan): units
+    0xxxxxxx, 110xxxxx 10xxxxxx, 1110xxxx 10xxxxxx 10xxxxxx, none cut by the length; else
+    UTFDataFormatException."""
+    i, n = 0, len(b)
+    while i < n:
+        b1 = b[i]
+        if b1 < 0x80:
+            i += 1
+            continue
+        k = 2 if b1 >> 5 == 6 else 3 if b1 >> 4 == 14 else 0
+        if not k or n - i < k or any(b[i + j] & 0xC0 != 0x80 for j in range(1, k)):
+            raise ValueError("utf")
+        i += k
+    return b
 MAX_CHAIN = 256  # classes in one object's hierarchy (longer: a cyclic superclass chain)
 
 
@@ -60,8 +77,8 @@ class _J:
     def s32(self):
         return struct.unpack(">i", self.take(4))[0]
 
-    def utf(self):
-        return self.take(self.u16())
+    def utf(self):  # readUTF: modified UTF-8 (JDK 8 BlockDataInputStream.readUTFBody)
+        return _mutf(self.take(self.u16()))
 
     def class_desc(self):
         tc = self.u8()
@@ -164,7 +181,7 @@ class _J:
             return
         if tc == 0x7C:
             self.handles.append("s")
-            self.take(struct.unpack(">Q", self.take(8))[0])
+            _mutf(self.take(struct.unpack(">Q", self.take(8))[0]))  # readLongUTF
             return
         if tc in (0x72, 0x7D):
             self.p -= 1

@@ -11,9 +11,15 @@
 #include "../clonos_amd/csrc/jser_flat.h"
 
 namespace {
+uint64_t g_backwards = 0;  // reads before an earlier one: the device readers' cursors only go forwards
 struct HostBytes {
   const uint8_t* p;
-  int operator()(uint64_t k) const { return p[k]; }
+  uint64_t hi = 0;
+  int operator()(uint64_t k) {
+    if (k < hi) ++g_backwards;
+    hi = k > hi ? k : hi;
+    return p[k];
+  }
 };
 struct HostArena {  // bump allocator over a fixed buffer, like the device arena
   uint8_t* base;
@@ -52,3 +58,7 @@ extern "C" uint32_t flat_record_len(const uint8_t* rec, uint32_t n) {
   };
   return clg::jser_flat_len_t(rd4, 0u, n);
 }
+
+// Reads the walker made at an offset before an earlier read's, since the library loaded (the
+// device readers step through the span's tiles forwards only: such a read is out of bounds).
+extern "C" uint64_t walker_backward_reads() { return g_backwards; }

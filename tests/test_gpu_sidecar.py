@@ -242,13 +242,26 @@ def test_robust_pipeline_tables_from_the_sidecar(monkeypatch, seg, side):
                 assert_span_equal(dec, s_, b)
 
 
+_BAD_STREAMS = {
+    # a TC_OBJECT whose class descriptor is TC_NULL (the inline flat parser once took it for a
+    # 7-byte record)
+    "null_class": b"\x03\xac\xed\x00\x05\x73\x70",
+    # malformed modified UTF-8 (JDK 8 readUTF: UTFDataFormatException) in a string, in a class
+    # name and in a field name of a flat object
+    "utf_string": b"\x03\xac\xed\x00\x05\x74\x00\x03a\xc3z",
+    "utf_class": D.encode(D.SerializableDeterminant(D.jser_integer(5)))[:9] + b"\xff" +
+    D.encode(D.SerializableDeterminant(D.jser_integer(5)))[10:],  # (byte 9: the name's first)
+    "utf_field": b"\x03\xac\xed\x00\x05\x73\x72\x00\x01K" + bytes(8) + b"\x02\x00\x01I\x00\x02f\x80\x78\x70" + bytes(4),
+}
+
+
+@pytest.mark.parametrize("kind", sorted(_BAD_STREAMS))
 @pytest.mark.parametrize("mode", ["sidecar", "scan", "robust", "host"])
-def test_object_with_a_null_class_is_an_error(monkeypatch, mode):
-    """03 AC ED 00 05 73 70: a TC_OBJECT whose class descriptor is TC_NULL is no stream the JDK
-    reads (the reference's decodeNext throws); the inline flat-object parser once took it for a
-    7-byte record.  Every path reports the oracle's error at its offset."""
+def test_streams_the_jdk_rejects_are_errors(monkeypatch, mode, kind):
+    """Serializable records JDK 8's ObjectInputStream fails on (the reference's decodeNext
+    throws): every path reports the oracle's error at its offset."""
     rng = np.random.default_rng(17)
-    bad = b"\x03\xac\xed\x00\x05\x73\x70"
+    bad = _BAD_STREAMS[kind]
     blob = synth.random_log(200, rng, allow_serializable=False) + _ser(rng) + bad + \
         synth.random_log(30, rng, allow_serializable=False)
     st, _, eo, et = O.decode(blob)

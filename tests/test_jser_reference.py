@@ -47,6 +47,8 @@ def walker(tmp_path_factory):
         r = lib.walker_stream_len(b, len(b), arena, C.byref(used))
         return r, used.value
     run.flat = lambda rec: lib.flat_record_len(rec, len(rec))
+    lib.walker_backward_reads.restype = C.c_uint64
+    run.backward_reads = lib.walker_backward_reads
     return run
 
 
@@ -210,3 +212,38 @@ def test_flat_parser_agrees_with_the_oracle(walker):
     for s in shapes:
         assert walker.flat(b"\x03" + s) == 1 + len(s)
     assert n_flat > 100
+
+
+def test_modified_utf8_as_jdk8_reads_it(walker):
+    """readUTF / readLongUTF (JDK 8 BlockDataInputStream.readUTFBody): units 0xxxxxxx,
+    110xxxxx 10xxxxxx, 1110xxxx 10xxxxxx 10xxxxxx, none cut by the length, else
+    UTFDataFormatException -- in a TC_STRING, a TC_LONGSTRING, a class name and a field name.
+    Oracle, pyref and the device walker agree; the inline flat parser gives no length for a
+    malformed name (the walker decides)."""
+    good = [b"abc", b"", b"\xc0\x80", b"\xc3\xa9t\xc3\xa9", b"\xe2\x82\xac", b"\x00\x7f", b"\xef\xbf\xbf"]
+    bad = [b"\x80", b"a\xbf", b"\xc3", b"\xc3a", b"\xe2\x82", b"\xe2\x82a", b"\xe2a\xac", b"\xf0\x9f\x98\x80",
+           b"\xff", b"ab\xf8", b"\xed\xa0"]
+    for body, ok in [(x, True) for x in good] + [(x, False) for x in bad]:
+        s1 = MAGIC + b"\x74" + _utf(body)                                    # TC_STRING
+        s2 = MAGIC + b"\x7c" + struct.pack(">Q", len(body)) + body           # TC_LONGSTRING
+        name = b"C" + body
+        s3 = MAGIC + b"\x73\x72" + _utf(name) + bytes(8) + b"\x02\x00\x01I" + _utf(b"v") + b"\x78\x70" + bytes(4)
+        s4 = MAGIC + b"\x73\x72" + _utf(b"K") + bytes(8) + b"\x02\x00\x01I" + _utf(b"f" + body) + b"\x78\x70" + bytes(4)
+        for s in (s1, s2, s3, s4):
+            n = _agree(walker, s)
+            assert (n == len(s)) == ok, (body, s.hex(), n)
+        for s in (s3, s4):
+            L = walker.flat(b"\x03" + s)
+            assert L == (1 + len(s) if ok else 0), (body, s.hex(), L)
+
+
+def test_walker_reads_forwards_only(walker):
+    """The device readers (ZStreamBytes, the robust pipeline's span reader) keep a cursor over
+    the span's tiles that only moves forwards, so the walker must ask for offsets in
+    non-decreasing order; a class name once was checked before its first two bytes were read
+    back (an out-of-bounds read on the GPU).  Every stream this module walks, counted."""
+    test_modified_utf8_as_jdk8_reads_it(walker)
+    test_mutations_agree(walker)
+    for s in STREAMS:
+        walker(s)
+    assert walker.backward_reads() == 0
