@@ -1131,11 +1131,10 @@ struct ZTile {
   uint32_t lo, hi, end_a, rs, re;
   bool first, last;  // first / last tile of its span
 };
-__device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans, uint32_t t,
-                                       uint32_t lane) {
+__device__ __forceinline__ ZTile ztile_of(const TileDesc& td, const SpanDesc& sd, uint32_t t, uint32_t lane) {
   ZTile z;
-  z.td = tiles[t];
-  z.sd = spans[z.td.span];
+  z.td = td;
+  z.sd = sd;
   z.first = t == z.sd.first_tile;
   z.last = t + 1 == z.sd.first_tile + z.sd.n_tiles;
   z.lo = z.td.delta;
@@ -1146,6 +1145,11 @@ __device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const
   z.rs = r0 < z.lo ? z.lo : (r0 > z.hi ? z.hi : r0);
   z.re = r0 + kZRegion > z.hi ? z.hi : r0 + kZRegion;
   return z;
+}
+__device__ __forceinline__ ZTile ztile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans, uint32_t t,
+                                       uint32_t lane) {
+  const TileDesc td = tiles[t];
+  return ztile_of(td, spans[td.span], t, lane);
 }
 
 // Build the map in place over the tile's rows of the image (every lane of the wave calls it:
@@ -2818,19 +2822,20 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
 // or it holds more than kZSideKept candidates -- the caller scans it (nothing written but
 // the scratch).  Wave-uniform; `scr`: the wave's own 2 kZSideKept words of LDS.
 constexpr uint32_t kZSideKept = 256;  // candidates of one tile a wave ranks in LDS
+// td: tile t's descriptor (the caller loads it a tile ahead).
 __device__ __forceinline__ bool side_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
-                                          const FusedCtl& ctl, uint32_t* scr, const uint32_t t, const uint32_t lane,
-                                          bool* flagged) {
+                                          const FusedCtl& ctl, uint32_t* scr, const uint32_t t, const TileDesc& td,
+                                          const uint32_t lane, bool* flagged) {
   const SideCar& S = ctl.side;
   const uint64_t c0 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
-  const TileDesc td = tiles[t];
   const uintptr_t ab = (uintptr_t)td.abase, pb = (uintptr_t)S.pool;
   if (ab < pb || ab - pb >= S.pool_bytes) return false;
   const uint64_t off = ab - pb;
   const uint32_t seg = (uint32_t)(off / S.seg_bytes), so0 = (uint32_t)(off % S.seg_bytes);
   const uint32_t n = (uint32_t)gp(S.hdr)[seg];
+  const SpanDesc sd = spans[td.span];  // (issued with the header's load)
   if (n > S.cap) return false;
-  const ZTile z = ztile(tiles, spans, t, lane);
+  const ZTile z = ztile_of(td, sd, t, lane);
   const uint64_t c1 = ctl.prof ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t lo = so0 + z.lo, hi = so0 + z.hi;  // the tile's bytes, as segment positions
   const CLG_GLOBAL uint32_t* ent = gp(S.ent) + (size_t)seg * S.cap;
@@ -2953,11 +2958,16 @@ __global__ __launch_bounds__(256) void k_decode_jser_side(const TileDesc* __rest
   if (threadIdx.x == 0) s_flag = 0;
   __syncthreads();
   bool flagged = false;
-  for (uint32_t t = blockIdx.x * 4u + wv; t < ctl.n_tiles; t += gridDim.x * 4u) {
-    if (!side_tile(tiles, spans, ctl, s_scr[wv], t, lane, &flagged) && lane == 0) {
+  const uint32_t stride = gridDim.x * 4u;
+  uint32_t t = blockIdx.x * 4u + wv;
+  TileDesc td = tiles[t < ctl.n_tiles ? t : 0];
+  for (; t < ctl.n_tiles; t += stride) {
+    const TileDesc tdn = tiles[t + stride < ctl.n_tiles ? t + stride : t];  // the next tile's, a tile ahead
+    if (!side_tile(tiles, spans, ctl, s_scr[wv], t, td, lane, &flagged) && lane == 0) {
       const uint32_t i = atomicAdd(list, 1u);
       list[1 + i] = t;
     }
+    td = tdn;
   }
   if (flagged && lane == 0) s_flag = 1;
   __syncthreads();
