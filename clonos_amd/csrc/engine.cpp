@@ -3039,11 +3039,15 @@ int clg_engine_create(const clg_config* cfg, clg_engine** out) {
   if (cfg->segment_bytes <= 65536u && cfg->pool_segments && !(sc && atoi(sc) == 0)) {
     const uint32_t cap = std::min<uint32_t>(clg::kSideCapMax, std::max<uint32_t>(8u, cfg->segment_bytes / 64u));
     const size_t hb = size_t(cfg->pool_segments) * 8, eb = size_t(cfg->pool_segments) * cap * 4;
-    HIPCHK(hipMalloc(&p, hb + eb));
-    e->side_alloc = p;
-    HIPCHK(hipMemset(p, 0, hb));  // life 0: every segment's first chunk starts its list
-    e->side = clg::SideCar{static_cast<uint64_t*>(p), reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + hb),
-                           e->pool, pool_bytes, cfg->segment_bytes, cap};
+    // (no room beside a pool sized to the HBM: the engine runs without it, the decode scans)
+    if (hipMalloc(&p, hb + eb) == hipSuccess) {
+      e->side_alloc = p;
+      HIPCHK(hipMemset(p, 0, hb));  // life 0: every segment's first chunk starts its list
+      e->side = clg::SideCar{static_cast<uint64_t*>(p), reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + hb),
+                             e->pool, pool_bytes, cfg->segment_bytes, cap};
+    } else {
+      (void)hipGetLastError();  // (the failed allocation is not the engine's error)
+    }
   }
   e->ifl_C = cfg->ifl_segment_bytes ? cfg->ifl_segment_bytes : 32768u;
   const uint32_t ifl_n = cfg->ifl_pool_segments ? cfg->ifl_pool_segments : 4096u;
