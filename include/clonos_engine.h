@@ -96,7 +96,9 @@ typedef struct clg_causal_log_id {
 
 typedef struct clg_config {
   uint32_t segment_bytes;  /* determinantBufferSize (NettyConfig.java:86-89); 16384 by default */
-  uint32_t pool_segments;  /* segments preallocated in HBM (pool = segment_bytes * pool_segments) */
+  uint32_t pool_segments;  /* segments preallocated in HBM (pool = segment_bytes * pool_segments);
+                              beside it, for segments up to 64 KiB, the Serializable records' positions
+                              per segment (segment_bytes / 16 + 8 bytes each, ~6 %; none if HBM is short) */
   int32_t device;          /* HIP device ordinal */
   int32_t sharing_depth;   /* determinantSharingDepth (-1 = full sharing, 0 = logging off) */
   uint32_t flags;          /* CLG_F_* */
