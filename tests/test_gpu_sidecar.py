@@ -277,3 +277,17 @@ def test_streams_the_jdk_rejects_are_errors(monkeypatch, mode, kind):
                     eng.sync()
                     eng.decode_logs([lg], [0])
             assert (ex.value.status, ex.value.err_off, ex.value.err_tag) == (st, eo, et)
+
+
+def test_segments_past_64k_carry_no_sidecar(monkeypatch):
+    """Segments over 64 KiB hold positions a 16-bit entry cannot name: such an engine keeps no
+    lists and scans every tile, bit-exact as with them."""
+    rng = np.random.default_rng(131)
+    with _engine(monkeypatch, True, 131072, pool=256) as eng:
+        logs = [eng.open_log(CausalLogID.main(v)) for v in range(3)]
+        blobs = [_mixed(rng, int(rng.integers(2000, 6000))) for _ in range(3)]
+        _write_host(eng, logs, blobs, rng)
+        for _ in range(2):
+            dec = eng.decode_logs(logs, [0, 0, 0])
+            for s_, b in enumerate(blobs):
+                assert_span_equal(dec, s_, b)
