@@ -155,13 +155,16 @@ constexpr int kJserCap = 256;  // Serializable stream-length table entries per t
 // Serializable candidates recorded where the log bytes are written (k_scatter), so the
 // decode need not read the whole log to find them.  Per pool segment: hdr[s] = life << 32 |
 // entries, and ent[s * cap + i] = position in the segment (low 16 bits) | code << 16, code the
-// record length of the "03 AC ED 00 05" stream there (TC_STRING and flat objects complete
-// inside the written chunk) or kSideUnknown (another shape, a stream running past the chunk,
-// or a prefix of the magic at the chunk's end: the decode verifies the magic and walks the
-// stream).  `life` is the host's count of the segment's allocations (31 bits): the first
-// chunk of a new life resets the count.  A stream running past its chunk is measured on the
-// request's next chunks' bytes (contiguous in the source) when the chunk says it goes on.  entries > cap: the list overflowed, the decode scans the
-// segment's tiles.  Segments of more than 64 KiB carry no sidecar (hdr null).
+// record length of the "03 AC ED 00 05" stream there (TC_STRING and flat objects that end
+// inside the request's written bytes, strings well-formed) or kSideUnknown (another shape, a
+// stream running past the request, or a prefix of the magic at its end: the decode verifies
+// the magic and walks the stream).  A stream running past its chunk is measured on the
+// request's next chunks' bytes (contiguous in the source) when the chunk says it goes on.
+// `life` is the host's count of the segment's allocations (31 bits).  The chunk at a
+// segment's offset 0 -- every life's first, segments filling from their start -- stamps it,
+// resetting the list; a later chunk of that life with no candidate touches nothing.
+// entries > cap: the list overflowed, the decode scans the segment's tiles.  Segments of
+// more than 64 KiB carry no sidecar (hdr null).
 constexpr uint32_t kSideUnknown = 0xFFFFu;
 constexpr uint32_t kSideCapMax = 1024;  // entries per segment at most (C / 64, 64 KiB segments)
 struct SideCar {
