@@ -2290,7 +2290,13 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
         old = __shfl(old, 0);
         if (old == 1u || z.last) break;  // resynchronised, or the span ends
         if (old == 2u && !zero && ++disagree > kZWalkDisagree) {  // chains that do not meet: the span goes robust
-          if (lane == 0) mark_bad(ctl, 3, t, z.td.span);
+          if (lane == 0) {
+            mark_bad(ctl, 3, t, z.td.span);
+            if (ctl.dbg) {  // developer diagnostics (CLONOS_FUSED_DEBUG): the walk that gave up
+              ctl.dbg[9] = 0xD15A; ctl.dbg[10] = f; ctl.dbg[11] = t; ctl.dbg[12] = (uint32_t)(xs - z.td.span_off);
+              ctl.dbg[13] = (uint32_t)(x - z.td.span_off); ctl.dbg[14] = z.td.span; ctl.dbg[15] = disagree;
+            }
+          }
           break;
         }
         xs = x;

@@ -2098,6 +2098,10 @@ struct clg_engine {
         ev_pool.push_back(r.pb);
       }
       *aborted = true;
+      static const char* kWhy[7] = {nullptr, "decode_abort_bad", "decode_abort_end", "decode_abort_exit",
+                                    "decode_abort_timeout", "decode_abort_serializable", "decode_abort_overflow"};
+      for (int k = 1; k <= 6; ++k)  // (which reasons: the bench line lists them beside the kernels)
+        if (hab[k]) stats[kWhy[k]].launches++;
       // Serializable records were met without tables: other aborts may be consequences
       // (entries guessed across them), so the tables decide; a second abort goes robust
       // (a table arena that was full, now grown: the same, once)
@@ -2113,6 +2117,9 @@ struct clg_engine {
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
         fprintf(stderr, "[clonos] tile %u reason %u x_pub %u x_true %u e_true %u lo %u hi %u end_a %u\n", hd[1], hd[2],
                 hd[3], hd[4], hd[5], hd[6], hd[7], hd[8]);
+        if (hd[9] == 0xD15A)
+          fprintf(stderr, "[clonos] repair walk from tile %u gave up at tile %u (entry %u exit %u, span %u, %u disagreements)\n",
+                  hd[10], hd[11], hd[12], hd[13], hd[14], hd[15]);
         for (int l = 0; l < 64; ++l) {
           const uint32_t* d = &hd[16 + 8 * l];
           fprintf(stderr, "  lane %2d rs %5u re %5u spec_exit %5u spec_bad %5u canon_exit %5u canon_bad %u entry %5u exit %5u bad %u\n",
