@@ -920,6 +920,21 @@ __device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// A word another block polls (a published exit, a look-back aggregate): a 2-bit state (0: not
+// published) in bits 63:62 and again in 31:30, a 60-bit value in 61:32 (high 30 bits) and 29:0.
+// Store and load are single dwordx2 accesses, yet a poll in the count pass once read a
+// published high half beside the zeroed low half (a chunk entering at span offset 0: the
+// repair walk gave up, config 2, about 1 batch in 30), so a word whose two states differ is
+// taken as not (yet) published and polled again.
+__device__ __forceinline__ uint64_t pk_word(uint32_t state, uint64_t v) {
+  const uint32_t h = state << 30 | ((uint32_t)(v >> 30) & 0x3FFFFFFFu), l = state << 30 | ((uint32_t)v & 0x3FFFFFFFu);
+  return (uint64_t)h << 32 | l;
+}
+__device__ __forceinline__ uint32_t pk_state(uint64_t w) {
+  const uint32_t h = (uint32_t)(w >> 62), l = ((uint32_t)w >> 30) & 3u;
+  return h == l ? h : 0u;
+}
+__device__ __forceinline__ uint64_t pk_val(uint64_t w) { return ((w >> 32) & 0x3FFFFFFFull) << 30 | (w & 0x3FFFFFFFull); }
 // abort[0]: nonzero once any tile aborted (polled by waiting tiles); abort[r], r = 1..4:
 // ~(lowest tile that aborted for reason r), for diagnostics.
 // An invalid record at span offset so on a true chain of span `span` (the lowest one wins).
@@ -1471,7 +1486,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
         ctl.dbg[1] = t; ctl.dbg[2] = reason; ctl.dbg[3] = must_exit; ctl.dbg[4] = x_true; ctl.dbg[5] = e_true;
         ctl.dbg[6] = lo; ctl.dbg[7] = z.hi; ctl.dbg[8] = end_a;
       }
-      uint32_t* d = ctl.dbg + 16 + 8 * lane;
+      uint32_t* d = ctl.dbg + 24 + 8 * lane;
       d[0] = rs; d[1] = re; d[2] = sp.exit; d[3] = sp.bad; d[4] = sp.first; d[5] = 0; d[6] = entry;
       d[7] = r.exit | r.bad << 31;
     }
@@ -1596,7 +1611,7 @@ __global__ __launch_bounds__(256) void k_decode_spans(const SpanDesc* __restrict
 // between count and emit beside the slice gather, and the read-back copy another ~45 us (its
 // blit kernel waits for CU slots too).  Each host write is its own bus transaction, though: for
 // config 4's 66 k spans they took 2.5 ms, so many-span batches copy the words back instead.
-constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 1ull << 63, kLbVal = kLbAgg - 1;
+constexpr uint32_t kLbAgg = 1u, kLbPre = 2u;  // pk_word states: block aggregate, inclusive prefix
 __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict__ tiles,
                                                      const SpanDesc* __restrict__ spans, uint32_t n_spans,
                                                      FusedCtl ctl) {
@@ -1635,13 +1650,14 @@ __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict_
     uint64_t* W = ctl.lb + 1;
     uint64_t pre = 0;
     if (blk == 0) {
-      st_agent(&W[0], kLbPre | total);
+      st_agent(&W[0], pk_word(kLbPre, total));
     } else {
-      st_agent(&W[blk], kLbAgg | total);
+      st_agent(&W[blk], pk_word(kLbAgg, total));
       const uint64_t t0 = __builtin_amdgcn_s_memtime();
       for (uint32_t j = blk - 1;;) {
         const uint64_t x = ld_agent(&W[j]);
-        if (!(x & (kLbAgg | kLbPre))) {
+        const uint32_t st = pk_state(x);
+        if (!st) {
           if (__builtin_amdgcn_s_memtime() - t0 > kZSpinLimit) {  // (cannot happen: earlier tickets run)
             raise_abort(ctl, 4, 0u);  // a wait timed out: the batch goes robust
             if (hab) {
@@ -1653,11 +1669,11 @@ __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict_
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
-        pre += x & kLbVal;
-        if (x & kLbPre) break;
+        pre += pk_val(x);
+        if (st == kLbPre) break;
         --j;
       }
-      st_agent(&W[blk], kLbPre | (pre + total));
+      st_agent(&W[blk], pk_word(kLbPre, pre + total));
     }
     gp(ctl.boff)[blk] = pre;
     s_pre = pre;
@@ -2251,7 +2267,7 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
       return;
     }
     uint64_t xs = xe & ~kZExValid;
-    if (xs != (ld_agent(&ctl.st_x[f - 1]) & ~(1ull << 63))) {  // entered elsewhere: walk from the true exit
+    if (xs != pk_val(ld_agent(&ctl.st_x[f - 1]))) {  // entered elsewhere: walk from the true exit
       uint32_t disagree = 0;
       for (uint32_t t = f; t < ctl.n_tiles; ++t) {
         const ZTile z = ztile(tiles, spans, t, lane);
@@ -2286,6 +2302,11 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
           const uint64_t o = ld_agent(&ctl.ex[t]);
           old = o == xv ? 1u : (o & kZExValid) ? 2u : 0u;  // 1 the same, 2 another exit, 0 none
           st_agent(&ctl.ex[t], xv);
+          if (ctl.dbg) {  // developer diagnostics (CLONOS_FUSED_DEBUG): who wrote ex[t], from which entry
+            uint64_t* w = reinterpret_cast<uint64_t*>(ctl.dbg + kZDbgTiles) + 2 * (uint64_t)t;
+            w[0] = xs;
+            w[1] = 2ull << 60 | (uint64_t)blockIdx.x << 32 | (uint64_t)(f & 0xFFFFFF) << 4 | old;
+          }
         }
         old = __shfl(old, 0);
         if (old == 1u || z.last) break;  // resynchronised, or the span ends
@@ -2349,7 +2370,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl, ctl.lean != 0u)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
       x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
-      if (lane == 0) st_agent(&ctl.st_x[t1 - 1], (1ull << 63) | (z.td.span_off + (x_pub - z.lo)));
+      if (lane == 0) st_agent(&ctl.st_x[t1 - 1], pk_word(2u, z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
   }
@@ -2378,14 +2399,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       const uint64_t w0 = __builtin_amdgcn_s_memtime();
       for (;;) {
         v = ld_agent(&ctl.st_x[t - 1]);
-        if (v) break;
+        // published, and not before this tile: an exit of the tile before lies in this one or
+        // later.  A chunk once entered at span offset 0 from a word read as published (about 1
+        // batch in 30 on config 2; the word held the right exit afterwards): such a read is
+        // not taken, the poll goes on
+        if (pk_state(v) && pk_val(v) >= z.td.span_off) break;
+        if (pk_state(v) && ctl.dbg && lane == 0) {  // developer diagnostics: the reads not taken
+          if (atomicAdd(ctl.dbg + 16, 1u) == 0u) {
+            ctl.dbg[17] = t; ctl.dbg[18] = (uint32_t)v; ctl.dbg[19] = (uint32_t)(v >> 32);
+            ctl.dbg[20] = (uint32_t)z.td.span_off; ctl.dbg[21] = nb;
+          }
+        }
         if (ld_agent32(ctl.abort + 4)) return;  // another wait timed out: the batch goes robust
         if (!backoff(nb, w0)) {
           if (lane == 0) raise_abort(ctl, 4, t);
           return;
         }
       }
-      xs = v & ~(1ull << 63);
+      xs = pk_val(v);
       sus_span = z.td.span;
     }
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
@@ -2400,6 +2431,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       x_prev = x;
       if (lane == 0) {
         st_agent(&ctl.ex[t], kZExValid | x);
+        if (ctl.dbg) {  // developer diagnostics (CLONOS_FUSED_DEBUG): who wrote ex[t], from which entry
+          uint64_t* w = reinterpret_cast<uint64_t*>(ctl.dbg + kZDbgTiles) + 2 * (uint64_t)t;
+          w[0] = xs;
+          w[1] = 1ull << 60 | (uint64_t)blockIdx.x << 32 | (uint64_t)(t0 & 0xFFFFFF) << 4 | why;
+        }
         if (why == 3u) {  // the chunk holding the next tile entered elsewhere (empty chunks skipped)
           uint32_t c = blockIdx.x + 1;
           while (chunk_first(ctl, c + 1, K, gridDim.x) == t1) ++c;
@@ -2484,7 +2520,7 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
 // [nt + t]; res: see launch_decode_small (kernels.h), res[3 + s] for the spans with tiles (the
 // host fills the empty ones).
 // ---------------------------------------------------------------------------------
-constexpr uint64_t kZAggSet = 1ull << 63, kZAggBad = 1ull << 62, kZAggCnt = (1ull << 62) - 1;
+constexpr uint32_t kZAggSet = 2u, kZAggBad = 3u;  // pk_word states: published, published and bad
 
 __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ tiles,
                                                    const SpanDesc* __restrict__ spans, uint32_t nt, const FusedCtl& ctl,
@@ -2508,18 +2544,18 @@ __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ 
     uint64_t v = 0;
     if (lane == 0) {
       const uint64_t w0 = __builtin_amdgcn_s_memtime();
-      while (!((v = ld_agent(&agg[nt + t - 1])) & kZAggSet)) {
+      while (!pk_state(v = ld_agent(&agg[nt + t - 1]))) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
-          v = kZAggSet | kZAggBad;
+          v = pk_word(kZAggBad, 0);
           break;
         }
       }
     }
     v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-    bad = (v & kZAggBad) != 0ull;
-    xs = v & kZAggCnt;
+    bad = pk_state(v) == kZAggBad;
+    xs = pk_val(v);
   }
   uint64_t c = 0, x = 0, bm[2] = {0, 0};
   if (!bad) {
@@ -2531,8 +2567,8 @@ __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ 
     bad = why != 0u;
   }
   if (lane == 0) {
-    st_agent(&agg[nt + t], kZAggSet | (bad ? kZAggBad : 0ull) | (x & kZAggCnt));
-    st_agent(&agg[t], kZAggSet | (bad ? kZAggBad : 0ull) | c);
+    st_agent(&agg[nt + t], pk_word(bad ? kZAggBad : kZAggSet, x));
+    st_agent(&agg[t], pk_word(bad ? kZAggBad : kZAggSet, c));
   }
   // look-back: every earlier tile's counts
   uint64_t pre = 0;
@@ -2542,16 +2578,16 @@ __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ 
     uint64_t v = 0;
     if (j < t) {
       const uint64_t w0 = __builtin_amdgcn_s_memtime();
-      while (!((v = ld_agent(&agg[j])) & kZAggSet)) {
+      while (!pk_state(v = ld_agent(&agg[j]))) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memtime() - w0 >= kZSpinLimit) {
-          v = kZAggSet | kZAggBad;
+          v = pk_word(kZAggBad, 0);
           break;
         }
       }
     }
-    any_bad = __any((v & kZAggBad) != 0ull);
-    uint64_t cj = v & kZAggCnt;
+    any_bad = __any(pk_state(v) == kZAggBad);
+    uint64_t cj = pk_val(v);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cj += __shfl_xor(cj, off);
     pre += cj;

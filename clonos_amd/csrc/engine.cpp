@@ -1929,7 +1929,7 @@ struct clg_engine {
     CHK(h_zres.ensure((2 * size_t(ns) + 5) * 8));
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
-    if (zdbg) CHK(d_dbg.ensure(16 * 4 + 64 * 32));
+    if (zdbg) CHK(d_dbg.ensure(clg::kZDbgTiles * 4 + size_t(nt) * 16));
     if (prof_path) CHK(d_prof.ensure(size_t(nt) * 64));
     const uint32_t jwork_cap = std::max<uint32_t>(uint32_t(nt) * 16 + 1024, zjwork_min);
     if (jser) {
@@ -2004,7 +2004,7 @@ struct clg_engine {
                                  jser && side.hdr ? 1u : 0u, 0, 0};  // the sidecar's scan-list count
         CHK(clg::launch_decode_prep(pa, stream));
       }
-      if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, 16 * 4 + 64 * 32, stream));
+      if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, clg::kZDbgTiles * 4 + size_t(nt) * 16, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
       if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
@@ -2088,6 +2088,13 @@ struct clg_engine {
       grown = used[0] > r.ctl.jwork_cap || used[1] > r.ctl.jovf_cap;
       stats["decode_jser_grow"].launches++;
     }
+    if (zdbg) {  // count-pass chunk entries read as published but before their tile (not taken)
+      uint32_t w8[8];
+      hipMemcpy(w8, d_dbg.as<uint32_t>() + 16, sizeof(w8), hipMemcpyDeviceToHost);
+      if (w8[0])
+        fprintf(stderr, "[clonos] %u chunk-entry reads not taken; first: tile %u word %08x%08x tile span offset %u (poll %u)\n",
+                w8[0], w8[1], w8[3], w8[2], w8[4], w8[5]);
+    }
     if (hab[0] || spilled) {
       if (ea) {
         ev_pool.push_back(ea);
@@ -2113,15 +2120,32 @@ struct clg_engine {
                 "timeout=%d serializable=%d overflow=%d\n", nt, int(jser), int(~hab[1]), int(~hab[2]), int(~hab[3]),
                 int(~hab[4]), int(~hab[5]), int(~hab[6]));
       if (zdbg) {
-        std::vector<uint32_t> hd(16 + 64 * 8);
+        std::vector<uint32_t> hd(clg::kZDbgTiles);
         hipMemcpy(hd.data(), d_dbg.p, hd.size() * 4, hipMemcpyDeviceToHost);
         fprintf(stderr, "[clonos] tile %u reason %u x_pub %u x_true %u e_true %u lo %u hi %u end_a %u\n", hd[1], hd[2],
                 hd[3], hd[4], hd[5], hd[6], hd[7], hd[8]);
-        if (hd[9] == 0xD15A)
+        if (hd[9] == 0xD15A) {
           fprintf(stderr, "[clonos] repair walk from tile %u gave up at tile %u (entry %u exit %u, span %u, %u disagreements)\n",
                   hd[10], hd[11], hd[12], hd[13], hd[14], hd[15]);
+          {  // who wrote the exits before the walk (site 1 the count pass, 2 a repair walk)
+            const uint32_t f = hd[10];
+            std::vector<uint64_t> pp(size_t(p.n_tiles) * 2);
+            hipMemcpy(pp.data(), d_dbg.as<uint8_t>() + clg::kZDbgTiles * 4, pp.size() * 8, hipMemcpyDeviceToHost);
+            for (uint32_t t = f >= 10 ? f - 10 : 0; t <= std::min(hd[11] + 1, p.n_tiles - 1); ++t) {
+              const uint64_t w = pp[size_t(t) * 2 + 1];
+              uint64_t exv = 0, stx = 0;
+              hipMemcpy(&exv, r.ctl.ex + t, 8, hipMemcpyDeviceToHost);
+              hipMemcpy(&stx, r.ctl.st_x + t, 8, hipMemcpyDeviceToHost);
+              fprintf(stderr, "[clonos]   tile %u: ex writer site %llu block %llu (chunk first / walk start %llu, why/old %llu) "
+                      "entry %llu ex %llx st_x %llx\n",
+                      t, (unsigned long long)(w >> 60), (unsigned long long)((w >> 32) & 0xFFFFFFF),
+                      (unsigned long long)((w >> 4) & 0xFFFFFF), (unsigned long long)(w & 15),
+                      (unsigned long long)pp[size_t(t) * 2], (unsigned long long)exv, (unsigned long long)stx);
+            }
+          }
+        }
         for (int l = 0; l < 64; ++l) {
-          const uint32_t* d = &hd[16 + 8 * l];
+          const uint32_t* d = &hd[24 + 8 * l];
           fprintf(stderr, "  lane %2d rs %5u re %5u spec_exit %5u spec_bad %5u canon_exit %5u canon_bad %u entry %5u exit %5u bad %u\n",
                   l, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7] & 0x7FFFFFFFu, d[7] >> 31);
         }

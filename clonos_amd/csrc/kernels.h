@@ -207,11 +207,12 @@ int launch_fast_emit(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* 
 // (record / wide bases per tile and per span), emit (SoA).  Any anomaly raises *abort and
 // the host re-decodes the batch with the robust pipeline above.
 constexpr uint32_t kZRegion = 128;
+constexpr uint32_t kZDbgTiles = 24 + 64 * 8;  // FusedCtl.dbg: the per-tile words' start (u32 index)
 constexpr uint32_t kZTile = 64 * kZRegion;  // 8192
 constexpr uint32_t kZHalo = 64;             // bytes of the span's next tile staged after a tile
 
 struct FusedCtl {
-  uint64_t* st_x;     // per tile: 1<<63 | exit (span offset) the successor enters at
+  uint64_t* st_x;     // per tile: pk_word(2, exit (span offset) the successor enters at)
   uint64_t* cnt;      // per tile: wide<<31 | records
   uint64_t* base;     // per tile: exclusive prefix of cnt inside its block of 1024 tiles
   uint64_t* boff;     // per block of 1024 tiles: exclusive prefix of the block totals
@@ -219,7 +220,10 @@ struct FusedCtl {
   uint64_t* span_lo;  // per span: base at its first tile
   uint64_t* span_hi;  // per span: base past its last tile
   uint32_t* abort;    // [8]: flag, then ~(first tile) per abort reason 1..4 (4 = wait timed out)
-  uint32_t* dbg;      // optional diagnostics (CLONOS_FUSED_DEBUG): first aborting tile's lane state
+  uint32_t* dbg;      // optional diagnostics (CLONOS_FUSED_DEBUG): [0, 16) the first aborting tile and
+                      // a repair walk that gave up, [16, 24) chunk-entry reads not taken, [24, ..)
+                      // the first aborting tile's lane state, then from word kZDbgTiles per tile the
+                      // writer of its ex word and its entry
   uint64_t* prof;     // optional per-tile phase stamps (CLONOS_SCAN_PHASES): s_memtime x 8
   uint32_t n_tiles;
   uint32_t nodep;     // developer timing mode (CLONOS_FUSED_NODEP): tiles independent, output invalid
@@ -264,7 +268,8 @@ struct FusedCtl {
   uint32_t* jbase;
   uint32_t jovf_cap;
   // The one-launch scan (phase 5, k_decode_scan): lb[0] a ticket counter, lb[1 + b] block b's
-  // look-back word (1 << 62 | its total, then 1 << 63 | its inclusive prefix); all zeroed per
+  // look-back word (pk_word state 1 and its total, then state 2 and its inclusive prefix; the
+  // state is held in both halves, see decode_fused.hip); all zeroed per
   // batch.  h_res: host memory the host reads the batch's result from -- span_hi at
   // [n_spans + s], the abort words as u32 at [2 n_spans] -- written by that kernel, so no
   // read-back copy is queued (null: none).
