@@ -22,6 +22,8 @@ HEADERS = [
     os.path.join(CSRC, "jser_device.h"),
     os.path.join(CSRC, "dev_common.h"),
     os.path.join(CSRC, "dev_slow.h"),
+    os.path.join(CSRC, "jser_flat.h"),
+    os.path.join(CSRC, "handoff.h"),
     os.path.join(ROOT, "include", "clonos_engine.h"),
 ]
 ARCH = os.environ.get("CLONOS_OFFLOAD_ARCH", "gfx950")

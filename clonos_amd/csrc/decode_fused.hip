@@ -39,6 +39,7 @@
 #include "dev_common.h"
 #include "jser_device.h"
 #include "jser_flat.h"
+#include "handoff.h"
 
 namespace clg {
 
@@ -920,21 +921,7 @@ __device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
 __device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// A word another block polls (a published exit, a look-back aggregate): a 2-bit state (0: not
-// published) in bits 63:62 and again in 31:30, a 60-bit value in 61:32 (high 30 bits) and 29:0.
-// Store and load are single dwordx2 accesses, yet a poll in the count pass once read a
-// published high half beside the zeroed low half (a chunk entering at span offset 0: the
-// repair walk gave up, config 2, about 1 batch in 30), so a word whose two states differ is
-// taken as not (yet) published and polled again.
-__device__ __forceinline__ uint64_t pk_word(uint32_t state, uint64_t v) {
-  const uint32_t h = state << 30 | ((uint32_t)(v >> 30) & 0x3FFFFFFFu), l = state << 30 | ((uint32_t)v & 0x3FFFFFFFu);
-  return (uint64_t)h << 32 | l;
-}
-__device__ __forceinline__ uint32_t pk_state(uint64_t w) {
-  const uint32_t h = (uint32_t)(w >> 62), l = ((uint32_t)w >> 30) & 3u;
-  return h == l ? h : 0u;
-}
-__device__ __forceinline__ uint64_t pk_val(uint64_t w) { return ((w >> 32) & 0x3FFFFFFFull) << 30 | (w & 0x3FFFFFFFull); }
+// The words other blocks poll: pk_word / pk_state / pk_val (handoff.h).
 // abort[0]: nonzero once any tile aborted (polled by waiting tiles); abort[r], r = 1..4:
 // ~(lowest tile that aborted for reason r), for diagnostics.
 // An invalid record at span offset so on a true chain of span `span` (the lowest one wins).
