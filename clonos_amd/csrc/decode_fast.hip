@@ -707,9 +707,6 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   const TileGeom g{td.delta, td.delta + td.len};
   const uint32_t rs = g.rs((int)lane), re = g.re((int)lane);
   const uint32_t nm = re > rs ? count_magic(s_tile, rs, re) : 0u;
-#ifndef CLG_JFILL_EXP
-#define CLG_JFILL_EXP 0  // developer A/B: 1 stage + count only, 2 no stream parse
-#endif
   uint32_t ex = nm;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -720,7 +717,7 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
   uint32_t idx = ex - nm;
   if (lane == 0) J.n[t] = total;
   CLG_JPHASE(2);
-  if (total == 0 || CLG_JFILL_EXP == 1) return;
+  if (total == 0) return;
   // pass 1: the candidates count_magic found, in position order, into LDS by table index:
   // dwords holding a 03 byte, then their bytes (a byte-by-byte pass over the region read every
   // byte from LDS)
@@ -751,7 +748,7 @@ __global__ __launch_bounds__(64) void k_jser_fill(const TileDesc* __restrict__ t
     const uint32_t a = s_cand[i];
     const uint64_t avail = sd.len - (td.span_off + (a - td.delta));
     bool general = false;
-    int64_t L = CLG_JFILL_EXP == 2 ? 80 : jser_inline_len_r(tr, a, avail, &general);  // the common shapes inline
+    int64_t L = jser_inline_len_r(tr, a, avail, &general);  // the common shapes inline
     ncand += 1;
     ngen += general;
     if (general) {
@@ -1248,10 +1245,7 @@ __global__ __launch_bounds__(64) void k_fast_emit(const TileDesc* __restrict__ t
     }
     __syncthreads();
     CLG_JPHASE(11);
-#ifndef CLG_EMIT_EXP
-#define CLG_EMIT_EXP 0  // developer A/B: 1 no phase B
-#endif
-    const uint32_t nw = CLG_EMIT_EXP == 1 ? 0u : total - w0 < (uint32_t)kEmitCap ? total - w0 : (uint32_t)kEmitCap;
+    const uint32_t nw = total - w0 < (uint32_t)kEmitCap ? total - w0 : (uint32_t)kEmitCap;
     for (uint32_t i0 = 0; i0 < nw; i0 += 64) {  // phase B
       const uint32_t i = i0 + lane;
       const bool act = i < nw;

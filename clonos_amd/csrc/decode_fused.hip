@@ -43,40 +43,20 @@
 
 namespace clg {
 
-// LDS image: row r holds aligned bytes [kZRegion r, kZRegion (r + 1)) at a pitch of kZPitch
-// dwords; with pads (kZPad > 0) the kZPad dwords after a row repeat the first kZPad dwords of
-// the next row, so up to four consecutive dwords read from any dword of a row stay inside its
-// pitch, and with a pitch of 35 dwords (co-prime with the 32 banks) the lanes' row walks start
-// on distinct banks.  The default is no pads: the image is the bytes themselves (an address is
-// the aligned coordinate, two VALU fewer per walk step), the warm-ups start 4 (lane & 7)
-// bytes apart instead (warm_start), and build_lm reads column-wise.  Rows: the tile, then the
-// halo + zero pad.
+// LDS image: row r holds aligned bytes [kZRegion r, kZRegion (r + 1)), unpadded: the image
+// is the bytes themselves (an address is the aligned coordinate).  Rows of 35 dwords with pad
+// dwords repeating the next row's head spread the lanes' row walks over the banks, but cost
+// two VALU per walk step; without them config-2 count took 0.179 -> 0.164 ms and config-3 emit
+// 0.363 -> 0.335 ms (round 4), and round 5 measured it again (0.150 against 0.170 ms).  The
+// warm-ups are staggered instead (warm_start), and build_lm reads column-wise.  Rows: the tile,
+// then the halo + zero pad.
 constexpr uint32_t kZRowDw = kZRegion / 4;  // 32
-#ifndef CLG_ZPAD
-#define CLG_ZPAD 0  // 3: rows at a 35-dword pitch (measured: config-2 count 0.179 -> 0.164 ms, config-3 emit
-                    // 0.363 -> 0.335 ms without pads; tools/ab.sh)
-#endif
-constexpr uint32_t kZPad = CLG_ZPAD;
-constexpr uint32_t kZPitch = kZRowDw + kZPad;
+constexpr uint32_t kZPitch = kZRowDw;
 constexpr uint32_t kZRows = kZTile / kZRegion + 2;
 constexpr uint32_t kZImgDw = kZRows * kZPitch;
-#ifndef CLG_COUNT_LM
-#define CLG_COUNT_LM 1  // 1: the count pass with Serializable tables walks a step-code map (build_lm)
-#endif
-#ifndef CLG_WARM_PRED
-#define CLG_WARM_PRED 0  // 1: the speculative warm-up as straight-line predicated steps (kZWarmUnroll per test)
-#endif
-[[maybe_unused]] constexpr int kZWarmUnroll = 4;
-#ifndef CLG_COUNT_PREFETCH
-#define CLG_COUNT_PREFETCH 0  // 1: the count pass without tables issues the next tile's loads during a walk
-                              // (measured: config-2 count 0.185 against 0.175 ms without; 127 VGPRs)
-#endif
 constexpr uint32_t kZWin = 1024;                       // emit: record starts staged per window (16-bit entries)
 constexpr uint32_t kZEmitWin = 512;                    // emit: 32-bit entries, the same 2 KiB of LDS
-#ifndef CLG_EMIT_PAIR
-#define CLG_EMIT_PAIR 1  // 2 measured the same (config-2 emit 0.220 ms either way, config 3 0.329 / 0.331)
-#endif
-constexpr int kZEmitPair = CLG_EMIT_PAIR;              // emit: records per lane per pass (loads hoisted)
+constexpr int kZEmitPair = 1;  // emit: records per lane per pass (2, the loads hoisted: the same, round 4)
 constexpr uint32_t kZCanon = 0xFFFFFFFFu;              // entry marker: not on the canonical chain
 constexpr uint32_t kZCanonLanes = 16;                  // regions (2 KiB) the canonical chain spans
 constexpr int kZSer = -2;                              // Serializable stream: walker needed
@@ -85,18 +65,14 @@ constexpr uint32_t kZTiny = kZTinySpan;                // small whole spans: a l
 // ---------------------------------------------------------------------------------
 // Wave-wide sums, scans and lane shifts through DPP (cross-lane moves inside the VALU): a
 // __shfl is a ds_bpermute, an LDS round trip each, and the count pass's per-tile reductions
-// were six of them in a row (CLG_DPP=0: the __shfl forms, for A/B).
+// were six of them in a row (the DPP forms: -2 % on count and emit, round 4).
 // ---------------------------------------------------------------------------------
-#ifndef CLG_DPP
-#define CLG_DPP 1
-#endif
 template <int kCtrl>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, false);
 }
 // inclusive scan over the 64 lanes (row_shr 1/2/4/8, then row_bcast 15 / 31)
 __device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, uint32_t lane) {
-#if CLG_DPP
   const uint32_t rl = lane & 15u;
   uint32_t t;
   t = dpp_mov<0x111>(v);
@@ -112,18 +88,9 @@ __device__ __forceinline__ uint32_t wave_scan_u32(uint32_t v, uint32_t lane) {
   t = dpp_mov<0x143>(v);
   if (lane >= 32u) v += t;
   return v;
-#else
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(v, off);
-    if ((int)lane >= off) v += y;
-  }
-  return v;
-#endif
 }
 // the sum over the 64 lanes, in every lane
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#if CLG_DPP
   v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_mov<0x124>(v);  // row_ror:4
@@ -131,19 +98,10 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   v += dpp_mov<0x142>(v);  // row_bcast:15
   v += dpp_mov<0x143>(v);  // row_bcast:31 (lane 63 holds the total)
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-#else
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-#endif
 }
 // lane l gets lane l - 1's value (lane 0: its own)
 __device__ __forceinline__ uint32_t wave_prev_u32(uint32_t v) {
-#if CLG_DPP
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);  // wave_shr:1
-#else
-  return __shfl_up(v, 1);
-#endif
 }
 __device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
 
@@ -166,7 +124,7 @@ __device__ __forceinline__ Bits bge(const Bits& b, uint32_t i) {
 __device__ __forceinline__ Bits bor(const Bits& a, const Bits& b) { return Bits{a.lo | b.lo, a.hi | b.hi}; }
 __device__ __forceinline__ uint32_t bcount(const Bits& b) { return (uint32_t)(__popcll(b.lo) + __popcll(b.hi)); }
 
-__device__ __forceinline__ uint32_t rk(uint32_t k) { return k + kZPad * (k >> 5); }  // dword k -> LDS dword
+__device__ __forceinline__ uint32_t rk(uint32_t k) { return k; }  // dword k -> LDS dword
 __device__ __forceinline__ uint32_t rb(uint32_t a) { return 4u * rk(a >> 2) + (a & 3u); }  // byte a -> LDS byte
 __device__ __forceinline__ uint32_t zb(const uint32_t* T, uint32_t a) { return (T[rk(a >> 2)] >> (8u * (a & 3u))) & 0xFFu; }
 __device__ __forceinline__ uint32_t zbe32(const uint32_t* T, uint32_t a) {
@@ -187,17 +145,8 @@ struct ZBytes {
 __device__ __forceinline__ uint32_t fld_be32(const ZBytes& b, uint32_t k) { return zbe32(b.T, b.base + k); }
 __device__ __forceinline__ uint64_t fld_be64(const ZBytes& b, uint32_t k) { return zbe64(b.T, b.base + k); }
 
-// LDS byte offset of aligned coordinate a (rows of 128 bytes at a pitch of 140 bytes):
-// a + 12 (a >> 7) in one full-rate op (left to itself the compiler picks v_mad_u64_u32).
-__device__ __forceinline__ uint32_t zoff(uint32_t a) {
-  if constexpr (kZPad == 0) {
-    return a;
-  } else {
-    uint32_t off;
-    asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(off) : "v"(a >> 7), "v"(a), "i"(4 * kZPad));
-    return off;
-  }
-}
+// LDS byte offset of aligned coordinate a (the unpadded image: a itself).
+__device__ __forceinline__ uint32_t zoff(uint32_t a) { return a; }
 typedef const __attribute__((address_space(3))) uint8_t lds_u8;
 typedef const __attribute__((address_space(3))) uint32_t lds_u32;
 // Byte a of the LDS image: one ds_read_u8.
@@ -442,22 +391,10 @@ __device__ __forceinline__ SpecR spec_walk_t(const uint32_t* T, uint32_t ws, uin
   {
     constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
     constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
-#if CLG_WARM_PRED
-    // straight-line steps, lanes past rs standing still: no branch per step, one wave-wide
-    // test per kZWarmUnroll steps
-    while (__any(q < rs)) {
-#pragma unroll
-      for (int k = 0; k < kZWarmUnroll; ++k) {
-        const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
-        q = q < rs ? q + (L > 1u ? L : 1u) : q;
-      }
-    }
-#else
     while (q < rs) {
       const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(zb8(T, q), 12u)) & 0xFFu;
       q += L > 1u ? L : 1u;
     }
-#endif
   }
   s.first = q;
   const uint32_t mid = re < r0 + 64u ? re : r0 + 64u;
@@ -524,140 +461,12 @@ __device__ __forceinline__ SpecR lm_spec_walk(const uint32_t* M, uint32_t ws, ui
   return s;
 }
 
-// ---------------------------------------------------------------------------------
-// Two chains per lane in lockstep (CLG_SPEC_PAIR).  A walk step is one dependent LDS read
-// and a few VALU, so a lane's walk is a chain of read latencies.  The region's two 64-byte
-// halves are walked at once: chain A warms up before rs and walks the low half, chain B warms
-// up before the high half (wsb; its warm-up covers the low half's bytes) and walks the high
-// half; each step issues both reads before using either.  Where A's exit is a start of B's
-// chain the two are one chain from there on (a step is a function of the position), so the
-// region's bitmaps are A's low half and B's high half from that start: the result equals
-// spec_walk_t's exactly.  Where it is not (B's warm-up did not meet A's chain), A goes on
-// through the high half alone, as spec_walk_t would.
-// ---------------------------------------------------------------------------------
-#ifndef CLG_SPEC_PAIR
-#define CLG_SPEC_PAIR 0  // measured slower: config-2 count 0.161 -> 0.209 ms, config 3 0.365 -> 0.45 (the walk is
-                         // issue-bound, not latency-bound: the second chain's VALU cost more than its overlap saved)
-#endif
 // the lean warm-up step: fixed-length tags, one byte past wide ones
 __device__ __forceinline__ uint32_t warm_len(uint32_t tg) {
   constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16;  // tags 0..3 (Serializable: 0)
   constexpr uint32_t kHi = 5u << 24;                  // tags 4..7 (wide: 0)
   const uint32_t L = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
   return L > 1u ? L : 1u;
-}
-// spec_step's length rule for a tag already read (0: step one byte); *wide for a wide record
-template <bool J, bool SAFE>
-__device__ __forceinline__ uint32_t spec_len_tag(const uint32_t* T, uint32_t q, uint32_t tg, uint32_t end_a, const JL& jl,
-                                                 bool* wide) {
-  constexpr uint32_t kLo = 2u | 9u << 8 | 5u << 16 | (J ? 0x40u : 0u) << 24;  // tags 0..3
-  constexpr uint32_t kHi = 0x40u | 0x40u << 8 | 0x40u << 16 | 5u << 24;       // tags 4..7
-  const uint32_t c = __builtin_amdgcn_perm(kHi, kLo, min(tg, 12u)) & 0xFFu;
-  uint32_t L = c;
-  *wide = false;
-  if (c >= 0x40u) {  // rare: the length needs fields of the record
-    if (tg == CLG_TAG_IGNORE_CHECKPOINT) {
-      L = 13;
-    } else if (J && tg == CLG_TAG_SERIALIZABLE) {
-      L = jl_len(jl, q);
-      L = L <= (uint32_t)kZSpecMax ? L : 0u;
-    } else {
-      L = zspec_var(T, q, end_a, tg);
-    }
-    if (!SAFE) L = q + L <= end_a ? L : 0u;
-    *wide = L != 0u;
-  } else if (!SAFE) {
-    L = q + L <= end_a ? L : 0u;
-  }
-  return L;
-}
-// the region's bitmaps from chain A (low half, exit qa) and chain B (high half from mid, its
-// exit qb), or A continued through the high half (step(q, sb, wb) -> next q)
-template <class Step>
-__device__ __forceinline__ SpecR pair_join(SpecR s, uint32_t mid, uint32_t re, uint32_t r0, uint32_t qa, uint32_t qb,
-                                           uint64_t sba, uint64_t wba, uint64_t sbb, uint64_t wbb, Step&& step) {
-  s.sb.lo = sba;
-  s.wb.lo = wba;
-  if (qa >= re) {  // A's last record reaches past the region: no start of the high half is A's
-    s.sb.hi = s.wb.hi = 0;
-    s.exit = qa;
-  } else if ((sbb >> (qa - mid)) & 1ull) {  // A meets B at qa: B's chain from there
-    const uint64_t m = ~0ull << (qa - mid);
-    s.sb.hi = sbb & m;
-    s.wb.hi = wbb & m;
-    s.exit = qb;
-  } else {  // B's warm-up missed A's chain: A alone through the high half (rare)
-    uint64_t sh = 0, wh = 0;
-    uint32_t q = qa;
-    while (q < re) q = step(q, sh, wh);
-    s.sb.hi = sh;
-    s.wb.hi = wh;
-    s.exit = q;
-  }
-  s.bad = spec_bad(s, r0);
-  return s;
-}
-template <bool J, bool SAFE>
-__device__ __forceinline__ SpecR spec_walk_pair(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                uint32_t end_a, uint32_t r0, const JL& jl) {
-  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
-  const uint32_t mid = r0 + 64u;  // (the caller: rs < mid < re)
-  uint32_t qa = ws, qb = wsb;
-  while (qa < rs || qb < mid) {  // both warm-ups
-    const uint32_t ta = zb8(T, qa < rs ? qa : rs), tb = zb8(T, qb < mid ? qb : mid);
-    qa = qa < rs ? qa + warm_len(ta) : qa;
-    qb = qb < mid ? qb + warm_len(tb) : qb;
-  }
-  s.first = qa;
-  uint64_t sba = 0, wba = 0, sbb = 0, wbb = 0;
-  while (qa < mid || qb < re) {  // A over the low half, B over the high half
-    const bool ia = qa < mid, ib = qb < re;
-    const uint32_t pa = ia ? qa : rs, pb = ib ? qb : mid;
-    const uint32_t ta = zb8(T, pa), tb = zb8(T, pb);
-    bool wa, wb;
-    const uint32_t La = spec_len_tag<J, SAFE>(T, pa, ta, end_a, jl, &wa);
-    const uint32_t Lb = spec_len_tag<J, SAFE>(T, pb, tb, end_a, jl, &wb);
-    const uint64_t ma = ia ? 1ull << (qa & 63u) : 0ull, mb = ib ? 1ull << (qb & 63u) : 0ull;
-    sba |= ma;
-    sbb |= mb;
-    wba |= wa ? ma : 0ull;
-    wbb |= wb ? mb : 0ull;
-    qa = ia ? qa + (La > 1u ? La : 1u) : qa;
-    qb = ib ? qb + (Lb > 1u ? Lb : 1u) : qb;
-  }
-  return pair_join(s, mid, re, r0, qa, qb, sba, wba, sbb, wbb, [&](uint32_t q, uint64_t& sh, uint64_t& wh) {
-    return spec_step<J, SAFE>(T, q, end_a, jl, sh, wh);
-  });
-}
-// the same over the step-code map (lm_spec_walk's rule)
-__device__ __forceinline__ SpecR lm_spec_walk_pair(const uint32_t* M, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                   uint32_t r0) {
-  SpecR s{{0, 0}, {0, 0}, rs, rs, 0};
-  const uint32_t mid = r0 + 64u;
-  uint32_t qa = ws, qb = wsb;
-  while (qa < rs || qb < mid) {
-    const uint32_t ca = lm8(M, qa < rs ? qa : rs) & 0x7Fu, cb = lm8(M, qb < mid ? qb : mid) & 0x7Fu;
-    qa = qa < rs ? qa + (ca > 1u ? ca : 1u) : qa;
-    qb = qb < mid ? qb + (cb > 1u ? cb : 1u) : qb;
-  }
-  s.first = qa;
-  uint64_t sba = 0, wba = 0, sbb = 0, wbb = 0;
-  while (qa < mid || qb < re) {
-    const bool ia = qa < mid, ib = qb < re;
-    const uint32_t ca = lm8(M, ia ? qa : rs), cb = lm8(M, ib ? qb : mid);
-    if (ia) {
-      sba |= 1ull << (qa & 63u);
-      wba |= (uint64_t)(ca >> 7) << (qa & 63u);
-      qa += (ca & 0x7Fu) > 1u ? (ca & 0x7Fu) : 1u;
-    }
-    if (ib) {
-      sbb |= 1ull << (qb & 63u);
-      wbb |= (uint64_t)(cb >> 7) << (qb & 63u);
-      qb += (cb & 0x7Fu) > 1u ? (cb & 0x7Fu) : 1u;
-    }
-  }
-  return pair_join(s, mid, re, r0, qa, qb, sba, wba, sbb, wbb,
-                   [&](uint32_t q, uint64_t& sh, uint64_t& wh) { return lm_step(M, q, sh, wh); });
 }
 
 // ---------------------------------------------------------------------------------
@@ -700,44 +509,18 @@ __device__ __forceinline__ SpecR lean_walk(const uint32_t* T, uint32_t ws, uint3
   return s;
 }
 
-#ifndef CLG_SPEC_PAIR_CHECK
-#define CLG_SPEC_PAIR_CHECK 0  // developer check: every paired walk against the single one (printf)
-#endif
-template <bool J>
-__device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair, bool lean);
-#if CLG_SPEC_PAIR_CHECK
-__device__ uint32_t g_pair_mismatch;
-#endif
+// The region's speculative walk: over the step-code map (batches with tables), the lean walk,
+// or spec_walk_t.  (Two chains per lane in lockstep -- the region's halves walked at once --
+// was measured slower, config-2 count 0.161 -> 0.209 ms: the walk is issue-bound, and the
+// second chain's VALU cost more than its overlap saved; round 4.)  wsb is unused.
 template <bool J>
 __device__ __forceinline__ SpecR spec_walk_fast(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool lean = false) {
-  // pairs where the region reaches well into its high half
-  const bool pair = CLG_SPEC_PAIR && rs < r0 + 64u && re >= r0 + 80u;
-#if CLG_SPEC_PAIR_CHECK
-  const SpecR a = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair, false);
-  const SpecR b = spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, false, false);
-  if (a.sb.lo != b.sb.lo || a.sb.hi != b.sb.hi || a.wb.lo != b.wb.lo || a.wb.hi != b.wb.hi || a.first != b.first ||
-      a.exit != b.exit || a.bad != b.bad) {
-    if (atomicAdd(&g_pair_mismatch, 1u) < 8u)
-      printf("[clonos] spec pair mismatch: r0 %u rs %u re %u ws %u wsb %u exit %u/%u first %u/%u bad %u/%u\n", r0, rs,
-             re, ws, wsb, a.exit, b.exit, a.first, b.first, a.bad, b.bad);
-  }
-  return b;
-#else
-  return spec_walk_fast1<J>(T, ws, wsb, rs, re, end_a, r0, jl, pair, lean);
-#endif
-}
-template <bool J>
-__device__ __forceinline__ SpecR spec_walk_fast1(const uint32_t* T, uint32_t ws, uint32_t wsb, uint32_t rs, uint32_t re,
-                                                 uint32_t end_a, uint32_t r0, const JL& jl, bool pair, bool lean) {
-  if (J && jl.lm) return pair ? lm_spec_walk_pair(jl.lm, ws, wsb, rs, re, r0) : lm_spec_walk(jl.lm, ws, rs, re, r0);
+  if (J && jl.lm) return lm_spec_walk(jl.lm, ws, rs, re, r0);
   if (!J && lean) return re + 16u <= end_a ? lean_walk<true>(T, ws, rs, re, end_a, r0) : lean_walk<false>(T, ws, rs, re, end_a, r0);
   // lanes whose records cannot run past the span end (all but the last tile's) skip the test
-  if (re + 16u <= end_a)
-    return pair ? spec_walk_pair<J, true>(T, ws, wsb, rs, re, end_a, r0, jl) : spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl);
-  return pair ? spec_walk_pair<J, false>(T, ws, wsb, rs, re, end_a, r0, jl)
-              : spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
+  if (re + 16u <= end_a) return spec_walk_t<J, true>(T, ws, rs, re, end_a, r0, jl);
+  return spec_walk_t<J, false>(T, ws, rs, re, end_a, r0, jl);
 }
 
 // True chain from entry e (e >= rs) merged with the speculative chain: walk until the true
@@ -836,9 +619,6 @@ __device__ __forceinline__ Res merge_walk_r(const uint32_t* T, uint32_t re, uint
 // takes that one record (merge_walk_r's step) and the loop goes on.  merge_walk_r's nested
 // rare branches cost about twice the VALU and SALU of this loop per step (the count pass's
 // ISA), and the merges are the count pass's second-largest phase after the speculative walk.
-#ifndef CLG_LEAN_MERGE
-#define CLG_LEAN_MERGE 1  // 0: lean batches merge with merge_walk_r (A/B)
-#endif
 __device__ __forceinline__ Res merge_walk_lean(const uint32_t* T, uint32_t re, uint32_t end_a, uint32_t e,
                                                const SpecR& s) {
   Res r{{0, 0}, {0, 0}, e, 0, 0, 0};
@@ -1104,13 +884,6 @@ __device__ __forceinline__ void stage_finish(const TileDesc& td, const SpanDesc&
     bb[rb(img_end + lane)] = 0;  // zero pad (64 bytes) so 16-byte reads near the end are defined
   }
   __syncthreads();
-  if constexpr (kZPad > 0) {
-    for (uint32_t i = lane; i < (kRows - 1) * kZPad; i += 64) {  // pads repeat the next row's head
-      const uint32_t row = i / kZPad, j = i - row * kZPad;
-      s_img[row * kZPitch + kZRowDw + j] = s_img[(row + 1) * kZPitch + j];
-    }
-    __syncthreads();
-  }
 }
 
 
@@ -1173,7 +946,7 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
   // The lane's dwords: its row (dword j of row `lane`), or without row pads (pitch 32, where a
   // row-per-lane read puts all 32 lanes of a group on one bank) dword 64 j + lane of the tile,
   // so the lanes of a read touch 64 consecutive dwords.
-  constexpr bool kCols = kZPad == 0;
+  constexpr bool kCols = true;  // (the unpadded image)
   // (kCols) bit j: the row of dword 64 j + lane, 2 j + (lane >> 5), meets the tile (rows from 0,
   // since lo < 16, to (hi - 1) >> 7)
   const int32_t jmax = z.hi > z.lo ? ((int32_t)((z.hi - 1u) >> 7) - (int32_t)(lane >> 5)) >> 1 : -1;
@@ -1216,14 +989,9 @@ __device__ __forceinline__ void build_lm(const ZTile& z, uint32_t* T, uint32_t* 
     list[k] = a | code << 16;
   }
   __syncthreads();  // every lane has read the image
-  if (kZPad == 0) {
 #pragma unroll
-    for (uint32_t j = 0; j < kZRowDw; ++j)
-      if ((onm >> j) & 1u) T[64u * j + lane] = c[j];
-  } else if (on) {
-#pragma unroll
-    for (uint32_t j = 0; j < kZRowDw; ++j) T[lane * kZPitch + j] = c[j];
-  }
+  for (uint32_t j = 0; j < kZRowDw; ++j)
+    if ((onm >> j) & 1u) T[64u * j + lane] = c[j];
   __syncthreads();  // the rows hold codes: the candidates' go over them
   for (uint32_t k = lane; k < n; k += 64) {
     const uint32_t e = list[k];
@@ -1359,22 +1127,17 @@ __device__ __forceinline__ uint32_t canon_exit_r(const ZTile& z, const uint32_t*
 
 // Where lane `lane`'s speculative warm-up starts, warm bytes before its region start rs.
 // Without row pads every region starts on bank 0, so the lanes' first reads would all hit
-// one bank: there the warm-up grows by 4 (lane & 7) bytes, putting eight start banks in each
-// group of lanes (the walk is a function of the tile's bytes either way).
-#ifndef CLG_WARM_STAGGER
-#define CLG_WARM_STAGGER 1  // 0: 4 (lane & 7) bytes; 1: 4 ((lane >> 1) & 15); 2: 4 ((lane >> 1) & 7)
-#endif
+// one bank: the warm-up grows by 4 ((lane >> 1) & 15) bytes (the walk is a function of the
+// tile's bytes either way).
 constexpr uint32_t kZWarmFlat = 1u << 31;  // FusedCtl::warm flag: no stagger (a lone wave: latency first)
 __device__ __forceinline__ uint32_t warm_start(uint32_t rs, uint32_t lo, uint32_t warm, uint32_t lane) {
   // Regions start 32 dwords apart, so the lanes' first reads hit banks 0 and 32 only (by lane
   // parity) and, walking at similar speeds, keep colliding.  The stagger's dword offsets
   // spread them: (lane >> 1) & 15 with the parity gives 32 banks (config-2 count 0.165 ->
   // 0.153 ms against lane & 7's 8 banks; tools/ab.sh), at 30 B more warm-up on average.
-  // (3: (lane >> 1) & 31, every lane's first read on its own bank, at 30 B more warm-up again)
-  const uint32_t st = CLG_WARM_STAGGER == 1 ? ((lane >> 1) & 15u)
-                      : CLG_WARM_STAGGER == 2 ? ((lane >> 1) & 7u)
-                      : CLG_WARM_STAGGER == 3 ? ((lane >> 1) & 31u) : (lane & 7u);
-  const uint32_t w = (warm & kZWarmFlat) ? (warm & ~kZWarmFlat) : (kZPad == 0 ? warm + 4u * st : warm);
+  // ((lane >> 1) & 31, every lane's first read on its own bank, costs 30 B more warm-up again)
+  const uint32_t st = (lane >> 1) & 15u;
+  const uint32_t w = (warm & kZWarmFlat) ? (warm & ~kZWarmFlat) : warm + 4u * st;
   return rs >= lo + w ? rs - w : lo;
 }
 
@@ -1414,7 +1177,7 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
   auto merge = [&](uint32_t from) -> Res {
     if (rs >= re) return Res{{0, 0}, {0, 0}, from, 0, 0, 0};
     if (J && jl.lm) return merge_walk_lm(s_img, re, end_a, from, sp, jl, g);
-    if (!J && CLG_LEAN_MERGE && ctl.lean) return merge_walk_lean(s_img, re, end_a, from, sp);
+    if (!J && ctl.lean) return merge_walk_lean(s_img, re, end_a, from, sp);
     return merge_walk_r<J>(s_img, re, end_a, from, sp, jl);
   };
   Res r = merge(entry);
@@ -1478,7 +1241,6 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
       d[7] = r.exit | r.bad << 31;
     }
   }
-  if (ctl.nodep) reason = 0;
   // an invalid record on the true chain with errors kept (ctl.span_err): the tile's counts and
   // bits cover the records before it -- the lanes below the failing one, and its starts before
   // the failing record -- so that a confirmed error costs its span no second decode
@@ -1611,7 +1373,8 @@ __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict_
   __syncthreads();
   const uint32_t blk = s_blk;
   volatile uint32_t* hab = ctl.h_res ? reinterpret_cast<volatile uint32_t*>(ctl.h_res + 2ull * n_spans) : nullptr;
-  if (blk == 0 && hab && tid < 10u) hab[tid] = ld_agent32(ctl.abort + tid);  // final: count and repair ran
+  if (blk == 0 && hab && tid < kZAbortWords) hab[tid] = ld_agent32(ctl.abort + tid);  // final: count and repair ran
+  if (blk == 0 && hab && ctl.jwork && tid < 2u) hab[kZAbortWords + tid] = ld_agent32(ctl.jwork + tid);  // table work used
   if (ld_agent32(ctl.abort)) return;  // (every block: nothing writes it during this kernel)
   const uint32_t i0 = blk * kZScanBlock + tid * 4u;
   uint64_t v[4], sum = 0;
@@ -1660,6 +1423,7 @@ __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict_
         if (st == kLbPre) break;
         --j;
       }
+      if ((ctl.perturb >> 16) && blk == 1) ++pre;  // (test switch: a wrong look-back result; 0 in production)
       st_agent(&W[blk], pk_word(kLbPre, pre + total));
     }
     gp(ctl.boff)[blk] = pre;
@@ -1678,6 +1442,24 @@ __global__ __launch_bounds__(256) void k_decode_scan(const TileDesc* __restrict_
       gp(ctl.span_hi)[sp] = hi;
       if (ctl.h_res) reinterpret_cast<volatile uint64_t*>(ctl.h_res)[n_spans + sp] = hi;
     }
+  }
+}
+
+// The look-back above, checked after it (emit, a kernel boundary later: every word final):
+// block k's offset must equal block k - 1's final inclusive prefix.  Block 0's offset is 0 and
+// each block's total is summed from the counts locally, so when every block k >= 1 passes,
+// by induction every offset is the sum of the totals before it -- whatever value a look-back
+// poll read.  A mismatch aborts the batch, which the host decodes again (rep[2] counts it;
+// emit's stores so far are overwritten then).  One lane of emit's block for tile 1024 k.
+__device__ __forceinline__ void lookback_check(const FusedCtl& ctl, uint32_t k) {
+  const uint64_t w = ld_agent(ctl.lb + k);  // W[k - 1] (W = lb + 1)
+  if (pk_state(w) == kLbPre && pk_val(w) == ld_agent(&ctl.boff[k])) return;
+  atomicAdd(ctl.rep + 2, 1u);
+  __hip_atomic_store(ctl.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ctl.h_res) {  // (the scan copied the abort words into the host's read-back already)
+    volatile uint32_t* hab = reinterpret_cast<volatile uint32_t*>(ctl.h_res + 2ull * ctl.n_spans);
+    hab[10] = 1u;
+    hab[0] = 1u;
   }
 }
 
@@ -2019,7 +1801,8 @@ __global__ __launch_bounds__(64) void k_decode_emit(const TileDesc* __restrict__
                                                     FusedCtl ctl, DecodeOut out) {
   __shared__ EmitLds<J> L;
   const uint32_t t = blockIdx.x, lane = threadIdx.x;
-  if (ld_agent32(ctl.abort)) return;
+  if (ld_agent32(ctl.abort)) return;  // (then the scan returned before its look-back too)
+  if (ctl.lb_check && t && t % kZScanBlock == 0 && lane == 0) lookback_check(ctl, t / kZScanBlock);
   if (ctl.skip_bad && gp(ctl.span_bad)[tiles[t].span]) return;  // the robust output fills this span
   if (ctl.span_err && tiles[t].span_off > gp(ctl.span_err)[tiles[t].span]) return;  // past a kept error
   emit_tile<J>(tiles, spans, ctl, out, t, lane, gp(ctl.base)[t] + gp(ctl.boff)[t / kZScanBlock], L);
@@ -2162,10 +1945,7 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
                                                  const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_j, uint32_t lane,
                                                  uint32_t t, const ZTile& z, uint64_t xs, uint32_t must_exit,
                                                  const SpecR* walked, uint64_t* x, uint64_t* cnt_out = nullptr,
-                                                 StagePre* pf = nullptr, bool pf_ready = false,
-                                                 uint32_t pf_next = 0xFFFFFFFFu, uint64_t* bm_out = nullptr,
-                                                 uint64_t* fail_so = nullptr) {
-  constexpr bool kLm = CLG_COUNT_LM != 0;
+                                                 uint64_t* bm_out = nullptr, uint64_t* fail_so = nullptr) {
   const uint32_t nt = ctl.n_tiles;
   const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
   const uint64_t ee = xs - z.td.span_off + z.lo;
@@ -2173,19 +1953,11 @@ __device__ __forceinline__ uint32_t count_staged(const TileDesc* __restrict__ ti
   JL jl{nullptr, nullptr, nullptr};
   JLPre pre{};
   if (J) pre = jl_prefetch(ctl, t, lane);
-  if (pf) {  // staged from registers; then tile pf_next's loads go out, to land during this walk
-    if (!pf_ready) stage_issue(z.td, z.sd, t, lane, z.hi, &n1, *pf);
-    stage_finish(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1, *pf);
-    if (pf_next < nt) {
-      const TileDesc td2 = tiles[pf_next], n2 = tiles[pf_next + 1 < nt ? pf_next + 1 : pf_next];
-      stage_issue(td2, spans[td2.span], pf_next, lane, td2.delta + td2.len, &n2, *pf);
-    }
-  } else {
-    stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
-  }
-  if (J && kLm) build_lm(z, s_img, s_j, lane);
-  if (J && kLm) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
-  else if (J) jl = load_jl(ctl, t, s_j, lane, nullptr, &pre);
+  // (the next tile's loads issued during this walk were slower: config-2 count 0.185 against
+  // 0.175 ms, 127 VGPRs; round 4)
+  stage_image(z.td, z.sd, t, tiles, s_img, lane, z.hi, &n1);
+  if (J) build_lm(z, s_img, s_j, lane);  // the image becomes the step-code map
+  if (J) jl = load_jl_map(ctl, t, s_j, lane, s_img, pre);
   uint32_t x_true, fa = 0xFFFFFFFFu;
   const uint32_t why = count_tile<J>(t, z, e_true, must_exit, ctl, s_img, lane, &x_true, jl, tiles, walked, cnt_out,
                                      bm_out, fail_so ? &fa : nullptr);
@@ -2241,11 +2013,23 @@ __device__ __forceinline__ bool zero_tile_walk(const ZTile& z, uint64_t xs, cons
   return true;
 }
 
+// Whether chunk c (first tile f) entered at a published exit other than the true exit of the
+// tile before it.  Read after the count pass (a kernel boundary), from the words the count
+// pass stored: the entry the chunk actually took (ent[c]) and the tile before's exit (ex[f-1];
+// not valid: that tile failed, and its span is the chunk's first).  Independent of how the
+// count pass's poll of st_x went.
+__device__ __forceinline__ bool wrong_entry(const FusedCtl& ctl, uint32_t c, uint32_t f) {
+  const uint64_t e = ld_agent(&ctl.ent[c]);
+  if (!pk_state(e) || f == 0) return false;  // (the chunk started its span, or never counted)
+  const uint64_t xe = ld_agent(&ctl.ex[f - 1]);
+  return !(xe & kZExValid) || (xe & ~kZExValid) != pk_val(e);
+}
+
 // Chunk c's request (k_decode_repair).  *walk_end: past the last tile a walk reached.
 template <bool J>
 __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                             const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_j, uint32_t lane,
-                                            uint32_t f, uint32_t ce, uint32_t* walk_end) {
+                                            uint32_t c, uint32_t f, uint32_t ce, uint32_t* walk_end) {
   if (f == 0 || f >= ce || tiles[f].span_off == 0) return;  // the chunk starts its span
   if (f >= *walk_end) {  // (else a walk has rewritten this chunk's entry already)
     const uint64_t xe = ld_agent(&ctl.ex[f - 1]);
@@ -2254,7 +2038,10 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
       return;
     }
     uint64_t xs = xe & ~kZExValid;
-    if (xs != pk_val(ld_agent(&ctl.st_x[f - 1]))) {  // entered elsewhere: walk from the true exit
+    // the entry the chunk took (or, never stored, the published exit it would have taken)
+    const uint64_t e = ld_agent(&ctl.ent[c]);
+    const uint64_t taken = pk_state(e) ? pk_val(e) : pk_val(ld_agent(&ctl.st_x[f - 1]));
+    if (xs != taken) {  // entered elsewhere: walk from the true exit
       uint32_t disagree = 0;
       for (uint32_t t = f; t < ctl.n_tiles; ++t) {
         const ZTile z = ztile(tiles, spans, t, lane);
@@ -2270,7 +2057,7 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
           zero = true;  // a run of Order(channel 0) records: settled without a walk
         } else {
           why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, kZCanon, nullptr, &x, nullptr, nullptr,
-                                false, 0xFFFFFFFFu, nullptr, &fso);
+                                &fso);
           __syncthreads();  // the image is reused
           if (why == 1u && lane == 0) note_error(ctl, z.td.span, fso);  // (the walk's entry is the true one)
         }
@@ -2326,18 +2113,14 @@ __device__ __forceinline__ void serve_chunk(const TileDesc* __restrict__ tiles, 
 // 0.376 ms on the config-3 subset, count<false> (88 VGPRs) unaffected.  The same bound on
 // k_decode_jser made it slower (0.26 to 0.28 ms), so that kernel keeps its 150.
 // Waves per SIMD the count kernel is compiled for (its VGPR bound): 4 (128 VGPRs), except with
-// tables and no row pads, where 128 VGPRs spilled into the walks (config-3 count +60 %) -- 3.
-#ifndef CLG_COUNT_J_WAVES
-#define CLG_COUNT_J_WAVES 0  // developer switch: waves per SIMD for count<J> (0: the default below)
-#endif
+// tables, where 128 VGPRs spilled into the walks (config-3 count +60 %) -- 3.
 template <bool J>
-constexpr int kZCountWaves = (J && CLG_COUNT_J_WAVES) ? CLG_COUNT_J_WAVES : ((J && kZPad == 0) ? 3 : 4);
+constexpr int kZCountWaves = J ? 3 : 4;
 template <bool J>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves<J>))) void k_decode_count(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                                      FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  constexpr bool kLm = CLG_COUNT_LM != 0;  // J: the image becomes the step-code map (build_lm)
   const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
   JL jl{nullptr, nullptr, nullptr};
   const uint32_t K = (nt + gridDim.x - 1) / gridDim.x;
@@ -2349,26 +2132,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
     const ZTile z = ztile(tiles, spans, t1 - 1, lane);
     if (!z.last && t1 < nt) {
       stage_image(z.td, z.sd, t1 - 1, tiles, s_img, lane, z.hi);
-      if (J && kLm) build_lm(z, s_img, s_j, lane);
-      if (J && kLm) jl = load_jl_map(ctl, t1 - 1, s_j, lane, s_img, jl_prefetch(ctl, t1 - 1, lane));
-      else if (J) jl = load_jl(ctl, t1 - 1, s_j, lane);
+      if (J) build_lm(z, s_img, s_j, lane);  // the image becomes the step-code map
+      if (J) jl = load_jl_map(ctl, t1 - 1, s_j, lane, s_img, jl_prefetch(ctl, t1 - 1, lane));
       const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane);
       const uint32_t wsb = warm_start(lane * kZRegion + 64u, z.lo, ctl.warm, lane);
       sp_last = z.rs < z.re ? spec_walk_fast<J>(s_img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl, ctl.lean != 0u)
                             : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
       x_pub = canon_exit_r<J>(z, s_img, sp_last, lane, jl, tiles, t1 - 1);
-      if (lane == 0) st_agent(&ctl.st_x[t1 - 1], pk_word(2u, z.td.span_off + (x_pub - z.lo)));
+      // An exit is the first record start at or past the tile end.  One before it is a fault
+      // of the canonical walk: publish the tile end instead (a guess; this chunk's last tile
+      // checks it against its true exit and files a repair when they differ), and count it.
+      if (x_pub < z.hi) {
+        if (lane == 0) atomicAdd(ctl.rep + 3, 1u);
+        x_pub = z.hi;
+      }
+      // (64-bit: the exit's span offset, never wrapped)
+      if (lane == 0) st_agent(&ctl.st_x[t1 - 1], pk_word(2u, (uint64_t)z.td.span_off + (x_pub - z.lo)));
       __syncthreads();
     }
   }
   uint64_t x_prev = 0;  // previous tile's exit, span offset
   uint32_t bad_span = 0xFFFFFFFFu;  // a span whose chain went wrong: its later tiles are skipped
   uint32_t sus_span = 0xFFFFFFFFu;  // the chunk's first span, entered at a published exit
-  // without tables (88-93 VGPRs) the next tile's loads are issued during this tile's walk:
-  // its 32 VGPRs fit below 128, the 4 waves per SIMD the LDS allows anyway
-  constexpr bool kPre = !J && CLG_COUNT_PREFETCH != 0;
-  StagePre pf;
-  uint32_t pf_t = 0xFFFFFFFFu;  // the tile whose loads pf holds
   for (uint32_t t = t0; t < t1; ++t) {
     const ZTile z = ztile(tiles, spans, t, lane);
     if (z.td.span == bad_span) continue;  // (wave-uniform) the host decodes that span robustly
@@ -2376,7 +2161,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
       continue;  // (wave-uniform) pass 0 counted this small whole span
     if (ctl.prof && lane == 0) ctl.prof[(uint64_t)t * 8] = __builtin_amdgcn_s_memtime();
     uint64_t xs;
-    if (z.first || ctl.nodep) {
+    if (z.first) {
       xs = z.td.span_off;  // a span starts on a record boundary
     } else if (t > t0) {
       xs = x_prev;
@@ -2403,17 +2188,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kZCountWaves
           return;
         }
       }
-      xs = pk_val(v);
+      xs = pk_val(v) + (ctl.perturb & 0xFFFFu);  // (perturb: a test switch, 0 in production)
       sus_span = z.td.span;
+      // the entry taken, for k_decode_repair's check against the true exit before it
+      if (lane == 0) st_agent(&ctl.ent[blockIdx.x], pk_word(2u, xs));
     }
     const bool reuse = t + 1 == t1 && x_pub != kZCanon;
     uint64_t x;
-    const uint32_t nxt = t + 1 < t1 ? t + 1 : 0xFFFFFFFFu;
     uint64_t fso = ~0ull;
     const uint32_t why = count_staged<J>(tiles, spans, ctl, s_img, s_j, lane, t, z, xs, t + 1 == t1 ? x_pub : kZCanon,
-                                         reuse ? &sp_last : nullptr, &x, nullptr, kPre ? &pf : nullptr, pf_t == t, nxt,
-                                         nullptr, &fso);
-    pf_t = nxt;
+                                         reuse ? &sp_last : nullptr, &x, nullptr, nullptr, &fso);
     if (why == 0u || why == 3u) {
       x_prev = x;
       if (lane == 0) {
@@ -2461,26 +2245,27 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
                                                       FusedCtl ctl) {
   __shared__ uint32_t s_img[kZImgDw];
   __shared__ uint32_t s_j[J ? 2 * kZJBitsDw + kZJCap : 1];
-  // nothing to do, or the batch goes again anyway (4 a wait timed out, 5 Serializable records
-  // without tables: again with them, 6 a table overflowed)
-  if (ctl.nodep || !ld_agent32(ctl.rep + 1) || ld_agent32(ctl.abort + 4) || ld_agent32(ctl.abort + 5) ||
-      ld_agent32(ctl.abort + 6))
-    return;
+  // the batch goes again anyway (4 a wait timed out, 5 Serializable records without tables:
+  // again with them, 6 a table overflowed)
+  if (ld_agent32(ctl.abort + 4) || ld_agent32(ctl.abort + 5) || ld_agent32(ctl.abort + 6)) return;
   const uint32_t G = gridDim.x, b = blockIdx.x, lane = threadIdx.x, K = (ctl.n_tiles + G - 1) / G;
-  if (!gp(ctl.rep_flag)[b]) return;
   const uint32_t fb = chunk_first(ctl, b, K, G);
   if (fb >= chunk_first(ctl, b + 1, K, G)) return;  // (an empty chunk is never asked for)
+  // chunk c needs serving: a request filed by the count pass, or an entry other than the true
+  // exit before it (every block checks its own chunk: two words; the usual batch stops here)
+  auto need = [&](uint32_t c, uint32_t f) -> bool { return gp(ctl.rep_flag)[c] || wrong_entry(ctl, c, f); };
+  if (!need(b, fb)) return;
   const uint32_t span = tiles[fb].span;
-  // an earlier flagged chunk of the same span: that chunk's block serves this one
+  // an earlier chunk of the same span needing service: that chunk's block serves this one
   for (uint32_t hi = b; hi > 0;) {
     const uint32_t lo = hi > 64u ? hi - 64u : 0u, k = lo + lane;
     const bool in = k < hi;
     const uint32_t ft = in ? chunk_first(ctl, k, K, G) : 0u;
     const uint32_t kt = in ? chunk_first(ctl, k + 1, K, G) : 0u;
-    // a chunk's flag is for its first tile's span: chunk k counts when that is this span (an
+    // a chunk's need is for its first tile's span: chunk k counts when that is this span (an
     // empty chunk: no tiles, the scan goes on past it)
     const bool empty = in && kt == ft, same = in && !empty && tiles[ft].span == span;
-    if (__any(same && gp(ctl.rep_flag)[k])) return;
+    if (__any(same && need(k, ft))) return;
     if (!__all(!in || empty || same)) break;  // the span starts inside [lo, hi)
     hi = lo;
   }
@@ -2489,7 +2274,13 @@ __global__ __launch_bounds__(64) void k_decode_repair(const TileDesc* __restrict
     const uint32_t f = chunk_first(ctl, c, K, G), ce = chunk_first(ctl, c + 1, K, G);
     if (f >= ce) continue;
     if (tiles[f].span != span) break;
-    if (gp(ctl.rep_flag)[c]) serve_chunk<J>(tiles, spans, ctl, s_img, s_j, lane, f, ce, &walk_end);
+    if (!gp(ctl.rep_flag)[c]) {
+      if (!wrong_entry(ctl, c, f)) continue;
+      // counted (the bench line and the tests read it) where the tile before has an exit: else
+      // it failed, and its span is bad already
+      if (lane == 0 && (ld_agent(&ctl.ex[f - 1]) & kZExValid)) atomicAdd(ctl.rep, 1u);
+    }
+    serve_chunk<J>(tiles, spans, ctl, s_img, s_j, lane, c, f, ce, &walk_end);
   }
 }
 
@@ -2542,7 +2333,7 @@ __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ 
     v = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     bad = pk_state(v) == kZAggBad;
-    xs = pk_val(v);
+    xs = pk_val(v) + (ctl.perturb & 0xFFFFu);  // (perturb: a test switch, 0 in production)
   }
   uint64_t c = 0, x = 0, bm[2] = {0, 0};
   if (!bad) {
@@ -2585,6 +2376,14 @@ __device__ __forceinline__ void decode_small_tiles(const TileDesc* __restrict__ 
   }
   emit_tile<false, true>(tiles, spans, ctl, out, t, lane, pre, L, bm);
   if (lane == 0) {
+    // the hand-offs this tile took, for the host to check once the kernel is done (every tile
+    // but a span's first entered at the exit of the tile before; every base is the one before
+    // it plus that tile's counts): entry | exit << 32 (span offsets, a small span < 4 GiB),
+    // base, counts
+    uint64_t* ck = res + 3 + ctl.n_spans + 3ull * t;
+    ck[0] = (uint64_t)(uint32_t)xs | (uint64_t)(uint32_t)x << 32;
+    ck[1] = pre;
+    ck[2] = c;
     if (z.first) res[3 + z.td.span] = pre;
     if (t + 1 == nt) {
       res[0] = (pre + c) & ((1ull << 31) - 1);
@@ -2689,9 +2488,6 @@ constexpr int kZJReg = 4;  // candidates a lane keeps in registers (more: second
 constexpr uint32_t kZJGeneral = 0xFFFFFFFFu;  // jlen placeholder: k_decode_jser_general fills it
 constexpr uint32_t kZJHalo = 1024;  // phase 3 halo: streams starting near the tile end stay in LDS
 constexpr uint32_t kZJRows = (kZTile + 15 + kZJHalo + 64 + 127) / 128 + 1;
-#ifndef CLG_JSER_ROT
-#define CLG_JSER_ROT 1  // rotated magic-scan row reads (A/B on MI355X, lane & 31: jser 0.262 vs 0.262 ms, config-3 subset)
-#endif
 __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
                                           const FusedCtl& ctl, uint32_t* s_img, uint32_t* s_cand, const uint32_t t,
                                           const uint32_t lane, bool* flagged) {
@@ -2703,8 +2499,8 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   const uint64_t after = z.td.span_off + z.td.len;
   const uint64_t rem = z.sd.len > after ? z.sd.len - after : 0;
   const uint32_t img_end = z.hi + (rem < (uint64_t)kZJHalo ? (uint32_t)rem : kZJHalo);
-  // candidates in the lane's region (row `lane` of the image, dwords 35 lane + j; j = 32..34
-  // are the row's pad = the next row's head).  First a mask of the row's dwords holding an
+  // candidates in the lane's region (row `lane` of the image, dwords 32 lane + j; j = 32..33
+  // are the next row's head).  First a mask of the row's dwords holding an
   // ED byte (rare outside the magic), branch-free; then only the dwords where a magic could
   // start (its ED byte, at +2, lies in that dword or the next) are tested at their four
   // byte offsets for "03 AC ED 00 05" -- a loop over a few set bits per lane, where testing
@@ -2713,12 +2509,11 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
   const uint32_t r0 = lane * kZRegion;
   const uint32_t* row = s_img + lane * kZPitch;
   uint64_t edm = 0;  // bit j: dword j (0..33) holds an ED byte
-#if CLG_JSER_ROT
-  // Without row pads the rows start 32 dwords apart, so reading dword j of every row at once
+  // The rows start 32 dwords apart, so reading dword j of every row at once
   // hits two banks (a 32-way conflict: 7.4 cycles per LDS instruction).  Each lane starts its
   // pass at its own dword and wraps: lane l reads bank 32 (l & 1) + (j + (l >> 1)) mod 34, so
   // the 64 reads of one instruction fall on distinct banks but for wrapped dwords 32-33
-  const uint32_t rot = kZPad == 0 ? ((lane >> 1) & 31u) : 0u;
+  const uint32_t rot = (lane >> 1) & 31u;
   for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
     uint32_t D[17], J[17];
 #pragma unroll
@@ -2733,18 +2528,6 @@ __device__ __forceinline__ void jser_tile(const TileDesc* __restrict__ tiles, co
       edm |= (((e - 0x01010101u) & ~e & 0x80808080u) ? 1ull : 0ull) << J[j];
     }
   }
-#else
-  for (uint32_t j0 = 0; j0 < kZRowDw + 2u; j0 += 17u) {  // two slices of 17 dwords (registers)
-    uint32_t D[17];
-#pragma unroll
-    for (uint32_t j = 0; j < 17; ++j) D[j] = row[j0 + j];
-#pragma unroll
-    for (uint32_t j = 0; j < 17; ++j) {
-      const uint32_t e = D[j] ^ 0xEDEDEDEDu;
-      edm |= (((e - 0x01010101u) & ~e & 0x80808080u) ? 1ull : 0ull) << (j0 + j);
-    }
-  }
-#endif
   uint64_t sm = (edm | (edm >> 1)) & 0xFFFFFFFFull;  // dwords where a magic may start
   while (sm) {
     const uint32_t j = (uint32_t)__builtin_ctzll(sm);

@@ -1,5 +1,7 @@
-// dev_common.h -- device helpers shared by the decode kernels (no calls, no Java
-// serialization walker: kernels that include only this header stay call-free).
+// dev_common.h -- device helpers shared by the decode kernels (no Java serialization
+// walker).  One out-of-line function: span_byte_at, the far byte read behind TileReader --
+// a kernel that reads bytes past its tile's image makes that call.  It is static, so every
+// translation unit has its own copy (no duplicate device symbols under -fgpu-rdc).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,8 +52,10 @@ struct SpanReader {
 };
 
 // A byte of the span through a fresh span reader, out of line: inlined at every byte the
-// stream parsers read, the tile search made the table fill's code several times larger.
-__device__ __noinline__ int span_byte_at(const TileDesc* tiles, uint32_t t0, uint32_t t1, uint32_t cur, uint64_t len,
+// stream parsers read, the tile search made the table fill's code several times larger.  The
+// search starts at the caller's tile hint `cur` (TileReader passes its reader's, which this
+// call does not move: the search goes either way from it, so a stale hint costs steps only).
+static __device__ __noinline__ int span_byte_at(const TileDesc* tiles, uint32_t t0, uint32_t t1, uint32_t cur, uint64_t len,
                                          uint64_t o) {
   SpanReader r{tiles, t0, t1, cur, len, JArena{}};
   return r.at(o);

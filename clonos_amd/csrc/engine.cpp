@@ -1396,7 +1396,11 @@ struct clg_engine {
     uint32_t n_tiny = 0;                // whole spans of one tile and at most kZTinySpan bytes
     uint32_t unit = 0;                  // device-planning tile window
     const std::vector<uint32_t>* only = nullptr;  // plan only these spans (ascending), as spans 0, 1, ...
+    // a builder that could not plan a log (a queued decode's re-plan after a rebase found its
+    // range gone): the decode fails with this status instead of decoding an empty span
+    int status = CLG_OK;
     void reset() {  // empty, capacity kept (a config-4 plan is ~4 MB: fresh pages cost page faults)
+      status = CLG_OK;
       tiles.clear();
       spans.clear();
       runs.clear();
@@ -1769,11 +1773,7 @@ struct clg_engine {
   // running on gstream only read log segments, and every call that writes segments waits for
   // gstream first (flush, upstream deltas, the in-flight pool).  Measured on MI355X (config-2
   // step, 3 runs each, tools/ab_env.sh): 0.79 ms against 0.83 ms when the completion also
-  // drained gstream.  CLONOS_DECODE_OWN_WAIT=0 restores the full wait (developer switch).
-  static bool own_wait() {
-    static const bool v = !(getenv("CLONOS_DECODE_OWN_WAIT") && atoi(getenv("CLONOS_DECODE_OWN_WAIT")) == 0);
-    return v;
-  }
+  // drained gstream.
   bool settling = false;  // settle() is completing an asynchronous decode
   int finish_out(clg_decoded* out, uint64_t nrec, uint64_t nwide) {
     out->n_rec = nrec;
@@ -1807,7 +1807,7 @@ struct clg_engine {
           if (parts[i].n) HIPCHK(hipMemcpyAsync(parts[i].dst, parts[i].src, parts[i].n, hipMemcpyDeviceToHost, stream));
       }
     }
-    if (settling && own_wait() && out->out_kind == CLG_MEM_DEVICE) {
+    if (settling && out->out_kind == CLG_MEM_DEVICE) {
       collect_timings(true);  // (finish_fused waited for the run's read-back, which follows emit)
     } else {
       CHK(sync());
@@ -1882,6 +1882,7 @@ struct clg_engine {
     clg::FusedCtl ctl{};
     clg::DecodeOut o{};
     bool span_local = false;
+    bool lookback_bad = false;  // emit found a scan offset other than its predecessor's prefix
     // its decode slot (read-back buffer, staged plan, jser arena note), and for a queued
     // decode the event after its read-back, which its completion waits for (not the stream:
     // a later decode may be queued behind it)
@@ -1901,7 +1902,7 @@ struct clg_engine {
     const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
     const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
     // pass 0 (small whole spans, a lane each) for batches without Serializable tables
-    const bool tiny = p.n_tiny && !jser && !prof_path && !getenv("CLONOS_FUSED_NODEP");
+    const bool tiny = p.n_tiny && !jser && !prof_path;
     std::optional<HostTimer> hsub(std::in_place, this, "host_launch_chunks");  // (CLONOS_HOST_PROF sub-stages)
     if (chunked) count_chunks(p, G, tiny, chunk_buf);
     PlanLayout L;
@@ -1916,17 +1917,18 @@ struct clg_engine {
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
     // words: st_x[nt] ex[nt] rep_flag[nt] (u8) cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] |
-    // abort[8] rep[2] (u32); bits apart.  st_x, ex and rep_flag are zeroed per batch.
+    // abort[8] rep[4] (u32) | lb: ticket, look-back[nb] | ent[G]; bits apart.  st_x, ex,
+    // rep_flag, the abort and repair words, lb and ent are zeroed per batch.
     const size_t nbk = (size_t(nt) + 1023) / 1024, fw = (size_t(nt) + 7) / 8;
-    const size_t o_cnt = 2 * size_t(nt) + fw;
-    const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), o_lb = o_ab + 5;
-    const size_t words = o_lb + 1 + nbk;  // (the one-launch scan's ticket and look-back words)
+    const size_t o_cnt = 2 * size_t(nt) + fw, n_ab = clg::kZAbortWords / 2;
+    const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), o_lb = o_ab + n_ab;
+    const size_t o_ent = o_lb + 1 + nbk, words = o_ent + std::max<size_t>(1, G);
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
     CHK(d_zerr.ensure(std::max<size_t>(1, ns) * 8));
     PinBuf& h_zres = h_zres_s[r->slot];
-    CHK(h_zres.ensure((2 * size_t(ns) + 5) * 8));
+    CHK(h_zres.ensure((2 * size_t(ns) + n_ab + 1) * 8));  // (+ the table work counters)
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     if (zdbg) CHK(d_dbg.ensure(clg::kZDbgTiles * 4 + size_t(nt) * 16));
@@ -1941,7 +1943,6 @@ struct clg_engine {
     clg::FusedCtl ctl{w, w + o_cnt, w + o_cnt + nt, w + o_cnt + 2 * size_t(nt), d_zbits.as<uint64_t>(), w + o_span,
                       w + o_span + ns, ab,
                       zdbg ? d_dbg.as<uint32_t>() : nullptr, prof_path ? d_prof.as<uint64_t>() : nullptr, nt,
-                      getenv("CLONOS_FUSED_NODEP") ? 1u : 0u,
                       jser ? d_zjpos.as<uint32_t>() : nullptr, jser ? d_zjlen.as<uint32_t>() : nullptr,
                       jser ? d_zjn.as<uint32_t>() : nullptr, jser ? 1u : 0u, jwork_cap,
                       jser ? d_zjwork.as<uint32_t>() : nullptr, spec_warm(jser), clg::JArena{}};
@@ -1956,6 +1957,10 @@ struct clg_engine {
     ctl.ex = w + nt;
     ctl.rep_flag = reinterpret_cast<uint8_t*>(w + 2 * size_t(nt));
     ctl.rep = ab + 8;
+    ctl.ent = w + o_ent;
+    ctl.perturb = fused_perturb;
+    ctl.lb_check = 1;
+    ctl.n_spans = ns;
     ctl.lb = w + o_lb;
     ctl.lean = !jser && (lean_env() >= 0 ? lean_env() != 0 : lean_hint) ? 1u : 0u;
     ctl.side = side;
@@ -1964,7 +1969,7 @@ struct clg_engine {
     // config 4's 66 k spans those took 2.5 ms -- there one copy after emit reads them back
     const bool host_res = ns <= kHostResSpans;
     ctl.h_res = host_res ? h_zres.as<uint64_t>() : nullptr;
-    memset(h_zres.p, 0, (2 * size_t(ns) + 5) * 8);  // (a batch without tiles runs no scan)
+    memset(h_zres.p, 0, (2 * size_t(ns) + n_ab + 1) * 8);  // (a batch without tiles runs no scan)
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -1995,7 +2000,7 @@ struct clg_engine {
         pa.r[0] = clg::PrepRange{d_spans.as<uint32_t>(), reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_spans),
                                  L.sb / 4, 0, 0};
         pa.r[1] = clg::PrepRange{reinterpret_cast<uint32_t*>(w), nullptr, o_cnt * 2, 0, 0};
-        pa.r[2] = clg::PrepRange{ab, nullptr, 10 + 2 * (1 + nbk), 0, 0};  // abort words, repair counters, look-back
+        pa.r[2] = clg::PrepRange{ab, nullptr, clg::kZAbortWords + 2 * (1 + nbk + std::max<size_t>(1, G)), 0, 0};  // abort words, repair counters, look-back, entries
         pa.r[3] = clg::PrepRange{d_zbad.as<uint32_t>(), nullptr, nsw, 0, 0};
         pa.r[4] = clg::PrepRange{d_zerr.as<uint32_t>(), nullptr, keep_errors ? nsw * 2 : 0, 0xFFFFFFFFu, 0};
         pa.r[5] = clg::PrepRange{jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, jser ? 2u : 0u, 0, 0};
@@ -2019,9 +2024,12 @@ struct clg_engine {
       // the span ranges and abort words: in h_zres already (the scan wrote them) or read back
       // now (emit ran right behind the scan: it returns at once when the batch aborted, and its
       // stores are bounded by the output capacity)
-      if (!host_res)  // span_hi and the abort words (adjacent; the host derives the ranges from span_hi)
-        HIPCHK(hipMemcpyAsync(h_zres.as<uint64_t>() + ns, ctl.span_hi, (size_t(ns) + 5) * 8, hipMemcpyDeviceToHost,
+      if (!host_res) {  // span_hi and the abort words (adjacent; the host derives the ranges from span_hi)
+        HIPCHK(hipMemcpyAsync(h_zres.as<uint64_t>() + ns, ctl.span_hi, (size_t(ns) + n_ab) * 8, hipMemcpyDeviceToHost,
                               stream));
+        if (jser)  // the table work counters beside them (the scan copies them when it writes h_res)
+          HIPCHK(hipMemcpyAsync(h_zres.as<uint64_t>() + 2 * size_t(ns) + n_ab, ctl.jwork, 8, hipMemcpyDeviceToHost, stream));
+      }
       if (jser) CHK(jarena_note(r->note()));
       if (r->slot) {
         if (!zdone[r->slot]) HIPCHK(hipEventCreateWithFlags(&zdone[r->slot], hipEventDisableTiming));
@@ -2076,13 +2084,16 @@ struct clg_engine {
     const uint32_t* hab = reinterpret_cast<const uint32_t*>(hz + 2 * size_t(ns));
     if (jser) jser_hint = hab[7] != 0;  // keep building tables while batches hold Serializable records
     if (hab[9]) stats["decode_chunk_repair"].launches += hab[9];  // repair requests the count pass served
+    if (hab[8]) stats["decode_entry_repair"].launches += hab[8];  // chunks walked again for a wrong entry
+    if (hab[11]) stats["decode_canon_before_end"].launches += hab[11];  // canonical exits inside their tile
     const bool spilled = jser && jarena_spilled(r.note());  // a stream walk found the spill arena full
     if (spilled) CHK(jarena_grow());
     // Serializable tables: the overflow arena or the walker's work list was full (reason 6)
     bool grown = false;
     if (jser && hab[6]) {
-      uint32_t used[2];
-      HIPCHK(hipMemcpy(used, d_zjwork.p, 8, hipMemcpyDeviceToHost));
+      // the work list's and the overflow arena's use, from this run's own read-back (a later
+      // decode queued behind it may have zeroed the device words already)
+      const uint32_t used[2] = {hab[clg::kZAbortWords], hab[clg::kZAbortWords + 1]};
       if (used[0] > r.ctl.jwork_cap) zjwork_min = std::max(zjwork_min, 2 * used[0]);
       if (used[1] > zjovf_cap) zjovf_cap = std::max<uint32_t>(2 * used[1], 2 * zjovf_cap);
       grown = used[0] > r.ctl.jwork_cap || used[1] > r.ctl.jovf_cap;
@@ -2113,7 +2124,9 @@ struct clg_engine {
       // (entries guessed across them), so the tables decide; a second abort goes robust
       // (a table arena that was full, now grown: the same, once)
       *need_jser = (!jser && hab[5] && !spilled) || (jser && (spilled || grown));
-      r.span_local = !*need_jser && !spilled && !hab[4] && !hab[6];
+      r.span_local = !*need_jser && !spilled && !hab[4] && !hab[6] && !hab[10];
+      r.lookback_bad = hab[10] != 0;
+      if (hab[10]) stats["decode_lookback_check"].launches++;  // a look-back read gave a wrong offset
       zlast = r;
       if (getenv("CLONOS_FUSED_DEBUG"))
         fprintf(stderr, "[clonos] fused decode aborted (%u tiles, jser %d): first tile per reason bad=%d end=%d exit=%d "
@@ -2175,6 +2188,12 @@ struct clg_engine {
   // Decode errors kept on the fast path (FusedCtl::span_err; CLONOS_KEEP_ERRORS=0 turns it off,
   // a developer switch): a span whose error the full rules confirm keeps the fast run's records
   // before it, and only spans whose chains went wrong otherwise go to the robust pipeline.
+  // Test switch (CLONOS_FUSED_PERTURB, FusedCtl::perturb): wrong chunk entries and a wrong
+  // look-back result, which the checks must catch (k_decode_repair, run_small, emit).
+  const uint32_t fused_perturb = [] {
+    const char* v = getenv("CLONOS_FUSED_PERTURB");
+    return v ? uint32_t(strtoul(v, nullptr, 0)) : 0u;
+  }();
   const bool keep_errors = [] {
     const char* v = getenv("CLONOS_KEEP_ERRORS");
     return !(v && atoi(v) == 0);
@@ -2226,6 +2245,23 @@ struct clg_engine {
     p.unit = 0;
   }
   static uint32_t segtab_at(const DecodePlan& p, uint64_t i) { return p.segtab[size_t(i)]; }
+  // The small path's hand-offs, checked once its kernel is done: every tile but a span's first
+  // entered at the exit the tile before it published, and every tile's base is the one before
+  // it plus that tile's counts (the kernel's per-tile words: entry | exit << 32, base, counts).
+  // A mismatch -- a poll that read a wrong word -- sends the batch the usual way.
+  bool small_handoffs_ok(const DecodePlan& p, const uint64_t* res) {
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    const uint64_t* ck = res + 3 + ns;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint64_t* k = ck + 3 * size_t(t);
+      const bool first = p.tiles[t].span_off == 0;
+      if ((t == 0 ? k[1] != 0 : k[1] != k[-2] + k[-1]) || (!first && uint32_t(k[0]) != uint32_t(k[-3] >> 32))) {
+        stats["decode_small_handoff"].launches++;
+        return false;
+      }
+    }
+    return true;
+  }
   int run_small(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base, bool* aborted) {
     HostTimer ht(this, "host_decode_small");
     *aborted = false;
@@ -2238,11 +2274,7 @@ struct clg_engine {
       return CLG_OK;
     }
     // the plan: in the launch's arguments when it fits (no copy queued), else one copy
-    static const int small_mode = [] {  // developer switch: bit 0 no argument plan
-      const char* v = getenv("CLONOS_SMALL_MODE");
-      return v ? atoi(v) : 0;
-    }();
-    const bool arg_plan = !(small_mode & 1) && nt <= clg::kZSmallArgTiles && ns <= clg::kZSmallArgSpans;
+    const bool arg_plan = nt <= clg::kZSmallArgTiles && ns <= clg::kZSmallArgSpans;
     PlanLayout L;
     if (arg_plan) {
       memcpy(small_arg.tiles, p.tiles.data(), size_t(nt) * sizeof(clg::TileDesc));
@@ -2272,7 +2304,7 @@ struct clg_engine {
     }
     // scratch: per-tile counts and record-start bitmaps, per-span look-back words
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
-    CHK(h_small_res.ensure((3 + size_t(ns)) * 8));
+    CHK(h_small_res.ensure((3 + size_t(ns) + 3 * size_t(nt)) * 8));  // (+ the per-tile hand-off words)
     uint64_t* res = h_small_res.as<uint64_t>();
     res[0] = res[1] = res[2] = 0;
     // look-back words: two buffers of kZSmallAggWords, zeroed once; each call zeroes the other;
@@ -2290,14 +2322,12 @@ struct clg_engine {
     ctl.cnt = cnt;
     ctl.bits = d_zbits.as<uint64_t>();
     ctl.n_tiles = nt;
-    static const int small_warm = [] {  // developer switch: the small path's warm-up bytes
-      const char* v = getenv("CLONOS_SMALL_WARM");
-      return v ? atoi(v) : -1;
-    }();
-    // warm-up 32 B: a lone wave per span waits on every step, and shorter warm-ups cost fewer
-    // merges than they save (config 1: the kernel 65 -> 62 us at 32 or 16 B, 63 at 48)
-    static const bool small_stagger = getenv("CLONOS_SMALL_STAGGER") != nullptr;  // developer switch
-    ctl.warm = (small_warm >= 0 ? uint32_t(small_warm) : 32u) | (small_stagger ? 0u : (1u << 31));
+    ctl.n_spans = ns;
+    ctl.perturb = fused_perturb;
+    // warm-up 32 B, not staggered: a lone wave per span waits on every step, and shorter
+    // warm-ups cost fewer merges than they save (config 1: the kernel 65 -> 62 us at 32 or 16 B,
+    // 63 at 48)
+    ctl.warm = 32u | (1u << 31);
     const bool sprof = getenv("CLONOS_SMALL_PROF") != nullptr;  // developer diagnostics: phase stamps
     if (sprof) {
       CHK(d_prof.ensure(size_t(nt) * 64));
@@ -2331,7 +2361,7 @@ struct clg_engine {
                 (unsigned long long)(q[5] >> 40));
       }
     }
-    if (res[2]) {
+    if (res[2] || !small_handoffs_ok(p, res)) {
       if (timing) timings.push_back(PendingTiming{"decode_small", ea, eb, 0});
       *aborted = true;
       return CLG_OK;
@@ -2376,6 +2406,7 @@ struct clg_engine {
         HostTimer hp(this, "host_decode_plan");
         build(pf, clg::kZTile);
       }
+      CHK(plan_ok(pf));
       bool aborted = false, need_jser = false;
       if (small_ok(pf, log_bytes, out)) {
         CHK(run_small(pf, log_bytes, out, span_rec_base, &aborted));
@@ -2388,7 +2419,12 @@ struct clg_engine {
     }
     DecodePlan p;
     build(p, uint32_t(clg::kTile));
+    CHK(plan_ok(p));
     return run_decode(p, log_bytes, out, span_rec_base);
+  }
+  int plan_ok(const DecodePlan& p) {
+    return p.status == CLG_OK ? CLG_OK
+                              : fail(p.status, "a queued decode's log range is gone (truncated past its start epoch)");
   }
 
   // Per-span fallback after a fast run whose chains went wrong in some spans only (a
@@ -2476,6 +2512,7 @@ struct clg_engine {
       DecodePlan sp;
       sp.only = &bad;
       build(sp, uint32_t(clg::kTile));
+      CHK(plan_ok(sp));
       clg_decoded so{};
       so.off = s_off;
       so.tag = s_tag;
@@ -2534,6 +2571,7 @@ struct clg_engine {
     HIPCHK(hipMemcpyAsync(d_sf_meta.p, meta.data(), mb, hipMemcpyHostToDevice, stream));
     clg::FusedCtl ctl = zlast.ctl;
     ctl.skip_bad = 1;
+    ctl.lb_check = 0;  // (the three-launch scan below: no look-back words)
     ctl.chunk = nullptr;  // (the count pass's chunk table is not staged again: scan and emit never read it)
     auto* zt = d_ztiles.as<clg::TileDesc>();
     auto* zs = d_spans.as<clg::SpanDesc>();
@@ -2546,7 +2584,7 @@ struct clg_engine {
     const clg::DecodeOut sc{s_off, s_tag, s_v0, s_widx, s_wrc, s_wv1, s_wvo, s_wvl, s_wsub, RC, WC};
     CHK(clg::launch_sf_place(reinterpret_cast<const clg::SfPlace*>(d_sf_meta.as<uint8_t>() + o_place), nb, sc, zlast.o,
                              ctl, stream));
-    CHK(h_zres_s[0].ensure((2 * size_t(ns) + 5) * 8));
+    CHK(h_zres_s[0].ensure((2 * size_t(ns) + clg::kZAbortWords / 2) * 8));
     uint64_t* hz = h_zres_s[0].as<uint64_t>();
     HIPCHK(hipMemcpyAsync(hz, ctl.span_lo, (2 * size_t(ns) + 4) * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -2573,6 +2611,12 @@ struct clg_engine {
   int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                   bool need_jser) {
     bool aborted = true, nj = false;
+    // a look-back read gave a wrong offset (emit's check): the fast path once more, as it was
+    if (zlast.lookback_bad && !need_jser) {
+      CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, zlast.jser, &nj));
+      if (!aborted) return CLG_OK;
+      need_jser = nj;
+    }
     // with the tables; again (at most twice) while a table arena was full and has grown
     for (int tries = 0; need_jser && tries < 3; ++tries) {
       stats["decode_jser_retry"].launches++;
@@ -2588,6 +2632,7 @@ struct clg_engine {
     stats["decode_fallback"].launches++;
     DecodePlan p;
     build(p, uint32_t(clg::kTile));
+    CHK(plan_ok(p));
     return run_decode(p, log_bytes, out, span_rec_base);
   }
 
@@ -2662,6 +2707,7 @@ struct clg_engine {
       HostTimer hp(this, "host_decode_plan");
       build(pf, clg::kZTile);
     }
+    CHK(plan_ok(pf));
     const bool queue = fast && !pf.spans.empty() && fused_fits(pf);
     // what the queued decodes' completions need must not be overwritten by this one's kernels:
     // host outputs go through shared staging arrays, and a scratch buffer that has to grow
@@ -3716,7 +3762,10 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
     for (uint32_t i = 0; i < uint32_t(hs.size()); ++i) {
       int32_t s = st[i], b = nb[i];
       const Log& l = e->logs[hs[i]];
-      if (gen != e->rebase_gen && l.depth != 0 && e->determinants_range(l, eps[i], &s, &b) != CLG_OK) s = b = 0;
+      if (gen != e->rebase_gen && l.depth != 0 && e->determinants_range(l, eps[i], &s, &b) != CLG_OK) {
+        p.status = CLG_E_STATE;  // (the settle-on-truncate rule makes this unreachable)
+        s = b = 0;
+      }
       e->plan_log_span(p, l, s, b, i, T);
     }
   };
@@ -3802,7 +3851,7 @@ static int replay_prepare(clg_engine* e, const clg_replay_vertex* v, uint32_t n,
       z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
       return z ^ (z >> 31);
     };
-    return mix(mix(uint64_t(uint16_t(k.v)) | uint64_t(k.main) << 16 | uint64_t(uint8_t(k.sub)) << 24 ^ uint64_t(k.lo)) ^
+    return mix(mix(uint64_t(uint16_t(k.v)) | uint64_t(k.main) << 16 | (uint64_t(uint8_t(k.sub)) << 24 ^ uint64_t(k.lo))) ^
                uint64_t(k.hi));
   };
   auto same = [](const IdKey& a, const IdKey& b) {

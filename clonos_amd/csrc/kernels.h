@@ -226,7 +226,6 @@ struct FusedCtl {
                       // writer of its ex word and its entry
   uint64_t* prof;     // optional per-tile phase stamps (CLONOS_SCAN_PHASES): s_memtime x 8
   uint32_t n_tiles;
-  uint32_t nodep;     // developer timing mode (CLONOS_FUSED_NODEP): tiles independent, output invalid
   // Serializable record lengths per tile (phase 3, k_decode_jser), sorted by position:
   // jpos/jlen[t * kZJCap + i] (aligned coordinate, record length or 0 for an invalid
   // stream), jn[t] entries.  jser = 1: the tables exist and the passes use them.
@@ -254,10 +253,25 @@ struct FusedCtl {
   uint32_t tiny;  // pass 0 ran (k_decode_count_tiny): small whole spans are counted already
   // Chunk-boundary repair (k_decode_count files, k_decode_repair serves): ex[t] = 1 << 63 |
   // the tile's exit (span offset), 0 while unknown; rep_flag[c] = 1: chunk c needs a check;
-  // rep[1]: requests filed (rep[0] unused).  All zeroed per batch.
+  // ent[c] = pk_word(2, the span offset chunk c's first tile entered at) when it entered at a
+  // published exit (0: it did not).  k_decode_repair compares every such entry with the true
+  // exit ex[] of the tile before, after the count pass, so a chunk that took a wrong entry is
+  // walked again whatever the hand-off read returned.  rep[0]: chunks served for a wrong
+  // entry, rep[1]: requests filed, rep[2]: look-back checks failed (k_decode_emit; the batch
+  // is decoded again), rep[3]: canonical exits found before their tile's end (published as
+  // the tile end, a guess the repair checks).  All zeroed per batch.
   uint64_t* ex;
   uint8_t* rep_flag;
   uint32_t* rep;
+  uint64_t* ent;
+  // Test switch (CLONOS_FUSED_PERTURB): bits 15:0 are added to every chunk entry taken from a
+  // published exit (and every small-path entry) -- the wrong entries the checks must catch;
+  // bit 16 makes scan block 1's look-back result one record too high.  0 in production.
+  uint32_t perturb;
+  // 1: the one-launch scan (k_decode_scan) computed boff, and emit checks each block's
+  // look-back result against its predecessor's final word (lb).  0: the three-launch scan.
+  uint32_t lb_check;
+  uint32_t n_spans;  // (the abort words' place in h_res)
   // Decode errors kept on the fast path: span_err[s] = the lowest span offset where a true
   // chain of span s met an invalid record (~0: none; atomicMin), and the tile holding it
   // writes the counts and start bits of the records before it.  null: off.
@@ -280,6 +294,7 @@ struct FusedCtl {
   // from its segment's list instead of scanning the tile (hdr null: every tile is scanned).
   SideCar side;
 };
+constexpr uint32_t kZAbortWords = 12;  // abort[8] rep[4] (u32), adjacent
 constexpr uint32_t kZJCap = 256;  // Serializable candidates per tile in LDS (more: the overflow arena)
 constexpr uint32_t kZScanBlock = 1024;  // tiles per workgroup of the offsets scan
 constexpr uint32_t kZTinySpan = 1024;   // whole spans up to this many bytes: pass 0, a lane each

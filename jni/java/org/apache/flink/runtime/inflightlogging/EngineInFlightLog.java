@@ -48,6 +48,9 @@ public class EngineInFlightLog implements InFlightLog {
 	// a checkpoint completed while a batch waited for pool space: truncated right after the
 	// batch is accepted (Long.MIN_VALUE: none), so the notifier never waits for the batch
 	private long pendingTruncation = Long.MIN_VALUE;
+	// that truncation's failure, kept apart from the batch's append status: the caller clears
+	// an accepted batch first (the engine holds its buffers), then raises it (CLG_OK: none)
+	private int truncationStatus = CLG_OK;
 
 	public EngineInFlightLog(ClonosEngine engine) {
 		this(engine, CLG_IFL_IN_MEMORY);
@@ -77,6 +80,7 @@ public class EngineInFlightLog implements InFlightLog {
 		if (n > STAGE_BYTES) { // larger than the stage: a batch of its own
 			ByteBuffer direct = nio.isDirect() ? nio.slice() : ByteBuffer.allocateDirect(n).put(nio.duplicate());
 			check(submit(new long[]{epochID}, new int[]{n}, direct, 1));
+			raiseTruncation();
 			return;
 		}
 		stage.put(nio.duplicate());
@@ -96,6 +100,14 @@ public class EngineInFlightLog implements InFlightLog {
 			staged = 0;
 		}
 		check(st);
+		raiseTruncation();
+	}
+
+	/** A deferred truncation that failed in submit(): raised once its batch is cleared. */
+	private void raiseTruncation() {
+		int t = truncationStatus;
+		truncationStatus = CLG_OK;
+		check(t);
 	}
 
 	/** The engine appended the batch: CLG_OK, or CLG_E_STATE (spillable log() while replaying
@@ -128,7 +140,9 @@ public class EngineInFlightLog implements InFlightLog {
 	// The batch's arrays and bytes are the live stage while it waits (wait() releases the
 	// monitor): nothing else touches them until it returns (log() and flush() wait for the
 	// submit, notifyCheckpointComplete leaves the stage to pendingTruncation).  Returns the
-	// engine's status; the caller clears what was accepted, then raises.
+	// append's status alone; the caller clears what was accepted, then raises it and then a
+	// failed deferred truncation (truncationStatus; the truncation stays pending, so the next
+	// accepted batch applies it again).
 	private int submit(long[] epochs, int[] lens, ByteBuffer bytes, int n) {
 		submitting = true;
 		try {
@@ -140,12 +154,13 @@ public class EngineInFlightLog implements InFlightLog {
 				waitQuietly();
 			}
 			long cp = pendingTruncation;
-			pendingTruncation = Long.MIN_VALUE;
 			if (cp != Long.MIN_VALUE && accepted(st)) {
 				// the batch was logged before the notification: its epochs below cp go too
 				int tst = nIflNotifyCheckpointComplete(engine.handle(), ifl, cp);
-				if (st == CLG_OK) {
-					st = tst;
+				if (tst == CLG_OK) {
+					pendingTruncation = Long.MIN_VALUE;
+				} else {
+					truncationStatus = tst;
 				}
 			}
 			return st; // CLG_E_STATE: spillable log() while replaying without an iterator (:98-99, NPE)
