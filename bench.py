@@ -387,11 +387,29 @@ def main():
             "config4": c4,
             "config5": c5,
             "config1": c1,
+            "distributed": dist_info(torch, dist, world, rehearse),
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def dist_info(torch, dist, world, rehearse):
+    """What the process group was, so a scaling record shows how many ranks the collectives
+    saw: torch.distributed's world size and backend ("nccl" is RCCL on ROCm), and the RCCL
+    version torch was built against."""
+    info = {"world_size": dist.get_world_size() if dist.is_initialized() else world,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "transport": "gloo rehearsal (every rank on GPU 0)" if rehearse else
+                         ("RCCL over xGMI" if world > 1 else "one rank (no collective in the config-2 step)"),
+            "rccl_version": None, "hip_version": getattr(torch.version, "hip", None)}
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # (reported, not fatal: the version is a label)
+        info["rccl_version"] = f"unavailable: {type(e).__name__}"
+    return info
 
 
 def config4(args, torch, dev, rank, world, dist, rehearse, main_records=4096, sub_records=64):
