@@ -1267,11 +1267,13 @@ __device__ __forceinline__ uint32_t count_tile(const uint32_t t, const ZTile& z,
     bm_out[0] = r.bm.lo;
     bm_out[1] = r.bm.hi;
   }
-  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  u64x2 out_bits;
-  out_bits.x = r.bm.lo;
-  out_bits.y = r.bm.hi;
-  gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = out_bits;
+  if (!bm_out) {  // (bm_out: the caller emits from registers -- the small and one-pass decodes)
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 out_bits;
+    out_bits.x = r.bm.lo;
+    out_bits.y = r.bm.hi;
+    gp(reinterpret_cast<u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane] = out_bits;
+  }
   ZPHASE(4);
 #undef ZPHASE
   return reason;
@@ -2404,6 +2406,186 @@ __global__ __launch_bounds__(64) void k_decode_small_tiles_arg(const SmallPlanAr
   decode_small_tiles(plan.tiles, plan.spans, n_tiles, ctl, out, agg, agg_next, res);
 }
 
+// ---------------------------------------------------------------------------------
+// One pass for large batches without Serializable tables (config 2: 64 logs of 5.5 MB).  A
+// block per tile, dispatched in tile order, counts its tile, takes its record base by a
+// decoupled look-back and emits from the image and start bitmap it still holds: the log is
+// read once and no bitmap goes through HBM (the three passes read the log twice and write and
+// read 1 KiB of bitmap per tile), and a wave's chain walk can run beside another's emit stores.
+// The true chain's entry is the canonical exit the tile before publishes right after its
+// speculative walk (canon_exit_r: the speculative chain over that tile's last 2 KiB, which
+// does not depend on its entry), so no tile waits for another's true chain.  Every tile then
+// checks that its own true exit equals the canonical exit it published (count_tile's
+// must_exit).  Whatever the fast rules do not settle in one tile -- a mismatch there (a record
+// longer than the canonical walk's reach crossing a tile end), an invalid record, a record past
+// the span end, a Serializable record -- aborts the batch, and the host decodes it with the
+// three passes, which repair chunk entries and keep errors.  Blocks wait only on lower blocks,
+// dispatched before them, so every wait ends; a wait past kZSpinLimit aborts.
+// Words (zeroed by the prep kernel): st_x[t] = pk_word(2, tile t's canonical exit), ex[t] =
+// its look-back word (kLbAgg: its packed counts, kLbPre: its inclusive prefix, kZOneBad: it
+// aborted), ent[] the counts of finished blocks.  After its emit each tile reads again the two
+// words it took -- the tile before's exit and final prefix, which must equal its entry and its
+// base -- and aborts the batch on a difference; the last block to finish copies the abort
+// words into the host's read-back.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kZOneBad = 3u;
+// A wait here is short (the tile before is a block dispatched just before this one, at the same
+// phase): a fixed short sleep between polls, not the count pass's doubling backoff -- which,
+// escalating to ~15 us per poll, made every tile's three waits cost more than its work.
+__device__ __forceinline__ bool one_wait(uint64_t w0) {
+  __builtin_amdgcn_s_sleep(2);
+  return __builtin_amdgcn_s_memtime() - w0 < kZSpinLimit;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ uint64_t first_lane_u64(uint64_t v) {
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32 | (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__global__ __launch_bounds__(64) void k_decode_one(const TileDesc* __restrict__ tiles, const SpanDesc* __restrict__ spans,
+                                                   FusedCtl ctl, DecodeOut out) {
+  __shared__ EmitLds<false, false> L;
+  const uint32_t lane = threadIdx.x, nt = ctl.n_tiles;
+  // (tiles in block order: an XCD-aware order -- chunks of 64 consecutive tiles per XCD, so that a
+  // tile's predecessor ran on its own XCD -- measured slower, 0.61 against 0.58 ms)
+  const uint32_t t = blockIdx.x;
+  uint32_t why = ld_agent32(ctl.abort) ? 4u : 0u;  // (another tile aborted the batch: nothing to do)
+  // developer diagnostics (CLONOS_SCAN_PHASES): per tile, s_memrealtime (100 MHz) at the phase
+  // boundaries, in the second half of ctl.prof (the first holds count_tile's stamps);
+  // tools/one_pass_phases.py reads them
+#define OSTAMP(k) \
+  if (ctl.prof && lane == 0) ctl.prof[(uint64_t)(nt + t) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  OSTAMP(0);
+  if (ctl.prof && lane == 0)
+    ctl.prof[(uint64_t)(nt + t) * 8 + 7] = (uint64_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) << 32;
+  if (!why) {
+    const ZTile z = ztile(tiles, spans, t, lane);
+    const TileDesc n1 = tiles[t + 1 < nt ? t + 1 : t];
+    stage_image(z.td, z.sd, t, tiles, L.img, lane, z.hi, &n1);
+    const JL jl{nullptr, nullptr, nullptr};
+    const uint32_t ws = warm_start(z.rs, z.lo, ctl.warm, lane);
+    const uint32_t wsb = warm_start(lane * kZRegion + 64u, z.lo, ctl.warm, lane);
+    const SpecR sp = z.rs < z.re ? spec_walk_fast<false>(L.img, ws, wsb, z.rs, z.re, z.end_a, lane * kZRegion, jl,
+                                                         ctl.lean != 0u)
+                                 : SpecR{{0, 0}, {0, 0}, z.rs, z.rs, 0};
+    // the successor's entry, published before this tile's own wait
+    uint32_t x_pub = kZCanon;
+    if (!z.last) {
+      x_pub = canon_exit_r<false>(z, L.img, sp, lane, jl, tiles, t);
+      if (x_pub < z.hi) {  // (an exit lies at or past the tile end; see k_decode_count)
+        if (lane == 0) atomicAdd(ctl.rep + 3, 1u);
+        x_pub = z.hi;
+      }
+      if (lane == 0) st_agent(&ctl.st_x[t], pk_word(2u, (uint64_t)z.td.span_off + (x_pub - z.lo)));
+    }
+    OSTAMP(1);
+    // this tile's entry: the span start, or the tile before's canonical exit (one lane polls)
+    uint64_t xs = z.td.span_off;
+    if (!z.first) {
+      uint64_t v = 0;
+      if (lane == 0) {
+        const uint64_t w0 = __builtin_amdgcn_s_memtime();
+        for (;;) {
+          v = ld_agent(&ctl.st_x[t - 1]);
+          if (pk_state(v) && pk_val(v) >= z.td.span_off) break;
+          if (ld_agent32(ctl.abort) || !one_wait(w0)) {
+            v = 0;
+            break;
+          }
+        }
+      }
+      v = first_lane_u64(v);
+      if (!pk_state(v)) why = 4u;
+      xs = pk_val(v) + (ctl.perturb & 0xFFFFu);  // (perturb: a test switch, 0 in production)
+    }
+    OSTAMP(2);
+    uint64_t c = 0, bm[2] = {0, 0};
+    if (!why) {
+      const uint64_t ee = xs - z.td.span_off + z.lo;
+      const uint32_t e_true = ee > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ee;
+      uint32_t x_true;
+      why = count_tile<false>(t, z, e_true, x_pub, ctl, L.img, lane, &x_true, jl, tiles, &sp, &c, bm);
+    }
+    OSTAMP(3);
+    // counts published, then the base: look back over the tiles before, 64 at a time
+    uint64_t pre = 0;
+    if (!why) {
+      if (lane == 0) st_agent(&ctl.ex[t], pk_word(t == 0 ? kLbPre : kLbAgg, c));
+      const uint64_t w0 = __builtin_amdgcn_s_memtime();
+      for (uint32_t hi = t; hi > 0;) {  // window: tiles hi - 1, hi - 2, ... (lane 0 the nearest)
+        const bool in = lane < hi;
+        const uint64_t v = in ? ld_agent(&ctl.ex[hi - 1 - lane]) : pk_word(kLbPre, 0);
+        const uint32_t st = pk_state(v);
+        const uint64_t m_pre = __ballot(st == kLbPre), m_bad = __ballot(st == kZOneBad), m_none = __ballot(st == 0u);
+        const uint32_t f = m_pre ? (uint32_t)__builtin_ctzll(m_pre) : 64u;  // the nearest prefix
+        const uint64_t upto = f >= 63u ? ~0ull : (2ull << f) - 1ull;   // lanes 0 .. f
+        if (m_bad & upto) {
+          why = 4u;
+          break;
+        }
+        if (m_none & upto) {  // not all published yet: the same window again
+          if (ld_agent32(ctl.abort) || !one_wait(w0)) {
+            why = 4u;
+            break;
+          }
+          continue;
+        }
+        pre += wave_sum_u64(lane <= f ? pk_val(v) : 0ull);
+        if (f < 64u) break;
+        hi = hi > 64u ? hi - 64u : 0u;
+      }
+      if (!why) {
+        if ((ctl.perturb >> 16) && t == 1) ++pre;  // (test switch: a wrong look-back result)
+        if (lane == 0 && t) st_agent(&ctl.ex[t], pk_word(kLbPre, pre + c));
+        if (z.last && lane == 0) {  // the span's record range ends here
+          gp(ctl.span_hi)[z.td.span] = pre + c;
+          if (ctl.h_res) reinterpret_cast<volatile uint64_t*>(ctl.h_res)[ctl.n_spans + z.td.span] = pre + c;
+        }
+        OSTAMP(4);
+        emit_tile<false, false>(tiles, spans, ctl, out, t, lane, pre, L, bm);
+        OSTAMP(5);
+        // the words taken, read again: the tile before's exit and its final prefix
+        if (lane == 0 && t) {
+          if (!z.first && pk_val(ld_agent(&ctl.st_x[t - 1])) != xs) why = 7u;
+          uint64_t w;
+          const uint64_t w2 = __builtin_amdgcn_s_memtime();
+          while (pk_state(w = ld_agent(&ctl.ex[t - 1])) != kLbPre) {
+            if (pk_state(w) == kZOneBad || ld_agent32(ctl.abort) || !one_wait(w2)) break;
+          }
+          if (pk_state(w) == kLbPre && pk_val(w) != pre) why = 7u;
+        }
+        why = __shfl(why, 0);
+      }
+    }
+    if (why && lane == 0) {  // (7: a word taken differed from its final value; rep[2] counts it)
+      if (why == 7u) atomicAdd(ctl.rep + 2, 1u);
+      st_agent(&ctl.ex[t], pk_word(kZOneBad, 0));
+      raise_abort(ctl, why == 7u ? 4u : why, t);
+      __threadfence();  // (the abort words before this block's count below)
+    }
+  }
+  OSTAMP(6);
+#undef OSTAMP
+  // the last block to finish copies the abort words into the host's read-back.  Finished
+  // blocks are counted in 64 shards (tile t in shard t & 63, each on its own 128-byte line of
+  // the zeroed ent words), and a shard's last block counts the shard: one counter taking every
+  // block's returning atomic held the blocks ~70 ns each, serialised (3.6 ms for 43 k tiles)
+  if (lane == 0 && ctl.h_res) {
+    uint32_t* shard = reinterpret_cast<uint32_t*>(ctl.ent) + 32u * (t & 63u);
+    const uint32_t in_shard = (nt - (t & 63u) + 63u) >> 6;
+    if (atomicAdd(shard, 1u) + 1u == in_shard) {
+      const uint32_t shards = nt < 64u ? nt : 64u;
+      if (atomicAdd(reinterpret_cast<uint32_t*>(ctl.ent) + 32u * 64u, 1u) + 1u == shards) {
+        __threadfence();
+        volatile uint32_t* hab = reinterpret_cast<volatile uint32_t*>(ctl.h_res + 2ull * ctl.n_spans);
+        for (uint32_t k = 0; k < kZAbortWords; ++k) hab[k] = ld_agent32(ctl.abort + k);
+      }
+    }
+  }
+}
+
 int launch_decode_small(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDesc* d_spans, uint32_t n_spans,
                         FusedCtl ctl, DecodeOut out, uint64_t* agg, uint64_t* agg_next, uint64_t* res, void* stream,
                         const SmallPlanArg* plan) {
@@ -2932,6 +3114,9 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
     }
   } else if (phase == 4) {
     ZLAUNCH(k_decode_count_tiny, dim3((nt + 63) / 64), dim3(64), 0, st, d_tiles, d_spans, ctl);
+  } else if (phase == 6) {  // the one-pass decode (no tables; ctl.lb, st_x and ex zeroed)
+    if (ctl.jser) return CLG_E_INVALID_ARG;
+    ZLAUNCH(k_decode_one, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
   } else if (phase == 5) {  // scan, block offsets and span ranges in one launch (ctl.lb zeroed)
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     ZLAUNCH(k_decode_scan, dim3(nb), dim3(256), 0, st, d_tiles, d_spans, n_spans, ctl);

@@ -1883,6 +1883,7 @@ struct clg_engine {
     clg::DecodeOut o{};
     bool span_local = false;
     bool lookback_bad = false;  // emit found a scan offset other than its predecessor's prefix
+    bool one = false;           // the one-pass decode (k_decode_one) ran, not the three passes
     // its decode slot (read-back buffer, staged plan, jser arena note), and for a queued
     // decode the event after its read-back, which its completion waits for (not the stream:
     // a later decode may be queued behind it)
@@ -1891,18 +1892,33 @@ struct clg_engine {
     int note() const { return slot ? int(1 + slot) : 0; }
   };
   FusedRun zlast;  // the last finished fast run
+  // The one-pass decode (k_decode_one, decode_fused.hip): off by default, since on MI355X it is
+  // slower than the three passes (config 2: 0.58 against 0.43 ms, DESIGN.md section 4, "One
+  // pass").  CLONOS_ONE_PASS=1 uses it for batches of more than kZSmallTilesMax tiles without
+  // tables or small whole spans; =2 for every batch the three passes would take (the tests).
+  // An abort goes to the three passes (after_abort), and so does a run with allow_one cleared.
+  const int one_pass = [] {
+    const char* v = getenv("CLONOS_ONE_PASS");
+    return v ? atoi(v) : 0;
+  }();
+  bool allow_one = true;
   int launch_fused(DecodePlan& p, uint64_t log_bytes, clg_decoded* out, bool jser, FusedRun* r) {
     HostTimer ht(this, "host_decode_launch");
     const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
     r->log_bytes = log_bytes;
     r->jser = jser;
     // chunks of equal cost when blocks take several tiles of spans of different sizes
-    const uint32_t G = clg::decode_count_grid(jser, nt);
-    const bool chunked = G && nt > G && ns > 1;
     const bool zdbg = getenv("CLONOS_FUSED_DEBUG") != nullptr;
     const char* prof_path = getenv("CLONOS_SCAN_PHASES");  // developer diagnostics: phase stamps
     // pass 0 (small whole spans, a lane each) for batches without Serializable tables
     const bool tiny = p.n_tiny && !jser && !prof_path;
+    // (default: logs in segments of at least two tiles, or host input -- tiles of a few hundred
+    // bytes give canonical exits from too few bytes, which often miss, and the batch goes again)
+    const bool one = one_pass && allow_one && !jser && !p.n_tiny && !zdbg &&
+                     ((nt > clg::kZSmallTilesMax && (p.runs.empty() || C() >= 2 * clg::kZTile)) || one_pass == 2);
+    r->one = one;
+    const uint32_t G = clg::decode_count_grid(jser, nt);
+    const bool chunked = G && nt > G && ns > 1 && !one;
     std::optional<HostTimer> hsub(std::in_place, this, "host_launch_chunks");  // (CLONOS_HOST_PROF sub-stages)
     if (chunked) count_chunks(p, G, tiny, chunk_buf);
     PlanLayout L;
@@ -1922,7 +1938,9 @@ struct clg_engine {
     const size_t nbk = (size_t(nt) + 1023) / 1024, fw = (size_t(nt) + 7) / 8;
     const size_t o_cnt = 2 * size_t(nt) + fw, n_ab = clg::kZAbortWords / 2;
     const size_t o_span = o_cnt + 2 * size_t(nt) + nbk, o_ab = o_span + 2 * size_t(ns), o_lb = o_ab + n_ab;
-    const size_t o_ent = o_lb + 1 + nbk, words = o_ent + std::max<size_t>(1, G);
+    // (ent: G words for the count pass's chunks, or the one-pass decode's 65 counters, 128 B apart)
+    const size_t n_ent = std::max<size_t>(one ? 65 * 16 : 1, G);
+    const size_t o_ent = o_lb + 1 + nbk, words = o_ent + n_ent;
     CHK(d_zctl.ensure(words * 8));
     CHK(d_zbits.ensure(std::max<size_t>(1, nt) * 64 * 16));
     CHK(d_zbad.ensure(std::max<size_t>(1, ns) * 4));
@@ -1932,7 +1950,7 @@ struct clg_engine {
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     if (zdbg) CHK(d_dbg.ensure(clg::kZDbgTiles * 4 + size_t(nt) * 16));
-    if (prof_path) CHK(d_prof.ensure(size_t(nt) * 64));
+    if (prof_path) CHK(d_prof.ensure(size_t(nt) * (one ? 128 : 64)));  // (one pass: its phase stamps too)
     const uint32_t jwork_cap = std::max<uint32_t>(uint32_t(nt) * 16 + 1024, zjwork_min);
     if (jser) {
       CHK(d_zjpos.ensure((size_t(nt) * clg::kZJCap + zjovf_cap) * 4));
@@ -1951,7 +1969,7 @@ struct clg_engine {
     ctl.jovf_cap = zjovf_cap;
     ctl.span_bad = d_zbad.as<uint32_t>();
     ctl.skip_bad = 0;
-    ctl.span_err = keep_errors ? d_zerr.as<uint64_t>() : nullptr;
+    ctl.span_err = keep_errors && !one ? d_zerr.as<uint64_t>() : nullptr;  // (one pass: errors abort it)
     ctl.chunk = chunked ? reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_chunk) : nullptr;
     ctl.tiny = tiny ? 1u : 0u;
     ctl.ex = w + nt;
@@ -2000,7 +2018,7 @@ struct clg_engine {
         pa.r[0] = clg::PrepRange{d_spans.as<uint32_t>(), reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_spans),
                                  L.sb / 4, 0, 0};
         pa.r[1] = clg::PrepRange{reinterpret_cast<uint32_t*>(w), nullptr, o_cnt * 2, 0, 0};
-        pa.r[2] = clg::PrepRange{ab, nullptr, clg::kZAbortWords + 2 * (1 + nbk + std::max<size_t>(1, G)), 0, 0};  // abort words, repair counters, look-back, entries
+        pa.r[2] = clg::PrepRange{ab, nullptr, clg::kZAbortWords + 2 * (1 + nbk + n_ent), 0, 0};  // abort words, repair counters, look-back, entries
         pa.r[3] = clg::PrepRange{d_zbad.as<uint32_t>(), nullptr, nsw, 0, 0};
         pa.r[4] = clg::PrepRange{d_zerr.as<uint32_t>(), nullptr, keep_errors ? nsw * 2 : 0, 0xFFFFFFFFu, 0};
         pa.r[5] = clg::PrepRange{jser ? d_zjwork.as<uint32_t>() : nullptr, nullptr, jser ? 2u : 0u, 0, 0};
@@ -2010,10 +2028,16 @@ struct clg_engine {
         CHK(clg::launch_decode_prep(pa, stream));
       }
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, clg::kZDbgTiles * 4 + size_t(nt) * 16, stream));
-      if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * 64, stream));
+      if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * (one ? 128 : 64), stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
       if (tiny) CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 4));  // small whole spans
+      if (one) {  // count, look-back and emit in one launch
+        if (ev) HIPCHK(hipEventRecord(ev[2], stream));
+        CHK(clg::launch_decode_fused(zt, nt, zs, ns, ctl, o, stream, 6));
+        if (ev) HIPCHK(hipEventRecord(ev[3], stream));
+      }
       for (int ph : {3, 0, 5, 2}) {  // jser tables, count, offsets (one launch), emit
+        if (one) break;
         if (ph == 3 && !jser) continue;
         const int k = ph == 3 ? 0 : ph == 0 ? 1 : ph == 5 ? 2 : 3;
         if (ev) HIPCHK(hipEventRecord(ev[2 * k], stream));
@@ -2044,7 +2068,11 @@ struct clg_engine {
       for (auto& e : evp) e = get_event();
     }
     CHK(enqueue(timing ? ev : nullptr, timing ? evp : nullptr));
-    if (timing) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
+    if (timing && one) {  // the one kernel's duration: its bytes need the record count (finish_fused)
+      ev_pool.insert(ev_pool.end(), {ev[0], ev[1], ev[4], ev[5], ev[6], ev[7]});
+      r->ea = ev[2];
+      r->eb = ev[3];
+    } else if (timing) {  // per-kernel durations, read back by sync(); emit's bytes need the record count
       if (jser) timings.push_back(PendingTiming{"decode_jser", ev[0], ev[1], log_bytes});
       else ev_pool.insert(ev_pool.end(), {ev[0], ev[1]});
       timings.push_back(PendingTiming{"decode_count", ev[2], ev[3], log_bytes});
@@ -2074,7 +2102,7 @@ struct clg_engine {
     }
     HostTimer ht(this, "host_decode_finish");
     if (const char* prof_path = getenv("CLONOS_SCAN_PHASES")) {
-      std::vector<uint64_t> hp(size_t(nt) * 8);
+      std::vector<uint64_t> hp(size_t(nt) * (r.one ? 16 : 8));
       hipMemcpy(hp.data(), d_prof.p, hp.size() * 8, hipMemcpyDeviceToHost);
       if (FILE* fp = fopen(prof_path, "wb")) {
         fwrite(hp.data(), 8, hp.size(), fp);
@@ -2124,7 +2152,8 @@ struct clg_engine {
       // (entries guessed across them), so the tables decide; a second abort goes robust
       // (a table arena that was full, now grown: the same, once)
       *need_jser = (!jser && hab[5] && !spilled) || (jser && (spilled || grown));
-      r.span_local = !*need_jser && !spilled && !hab[4] && !hab[6] && !hab[10];
+      r.span_local = !r.one && !*need_jser && !spilled && !hab[4] && !hab[6] && !hab[10];
+      if (r.one) stats["decode_one_abort"].launches++;  // (the three passes decode it again)
       r.lookback_bad = hab[10] != 0;
       if (hab[10]) stats["decode_lookback_check"].launches++;  // a look-back read gave a wrong offset
       zlast = r;
@@ -2168,7 +2197,7 @@ struct clg_engine {
     uint64_t nrec = 0, nwide = 0;
     span_totals(p, hz, span_rec_base, &nrec, &nwide);
     if (!jser) lean_hint = nwide * 16 < nrec;
-    if (ea) timings.push_back(PendingTiming{"decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
+    if (ea) timings.push_back(PendingTiming{r.one ? "decode_one" : "decode_emit", ea, eb, log_bytes + 13 * nrec + 25 * nwide});
     // the pipeline's algorithmic bytes: log bytes read + the SoA rows
     if (r.pa) timings.push_back(PendingTiming{"decode_pipeline", r.pa, r.pb, log_bytes + 13 * nrec + 25 * nwide});
     return finish_out(out, nrec, nwide);
@@ -2611,6 +2640,15 @@ struct clg_engine {
   int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                   bool need_jser) {
     bool aborted = true, nj = false;
+    // the one-pass decode aborted (a case its rules leave to the three passes): those
+    if (zlast.one) {
+      allow_one = false;
+      const int st = run_fused(pf, log_bytes, out, span_rec_base, &aborted, zlast.jser || need_jser, &nj);
+      allow_one = true;
+      CHK(st);
+      if (!aborted) return CLG_OK;
+      need_jser = nj;
+    }
     // a look-back read gave a wrong offset (emit's check): the fast path once more, as it was
     if (zlast.lookback_bad && !need_jser) {
       CHK(run_fused(pf, log_bytes, out, span_rec_base, &aborted, zlast.jser, &nj));

@@ -25,11 +25,18 @@ def have_gpu():
     return _have_gpu()
 
 
-@pytest.fixture(params=["auto", "robust"])
-def engine(request):
-    """A fresh engine on cuda:0 with small segments (exercise segment boundaries), once
-    with the fast three-pass decode (robust pipeline on abort) and once robust-only."""
+@pytest.fixture(params=["auto", "robust", "one_pass"])
+def engine(request, monkeypatch):
+    """A fresh engine on cuda:0 with small segments (exercise segment boundaries): with the
+    fast decode (single-launch small path, one-pass or three-pass decode, robust pipeline on
+    abort), robust-only, and with the one-pass decode forced onto every batch it may take
+    (CLONOS_ONE_PASS=2, no small path; its aborts go to the three passes)."""
     from clonos_amd import Engine
-    e = Engine(segment_bytes=256, pool_segments=1 << 16, timing=True, decode=request.param)
+    if request.param == "one_pass":
+        monkeypatch.setenv("CLONOS_ONE_PASS", "2")
+        e = Engine(segment_bytes=256, pool_segments=1 << 16, timing=True, decode="three_pass")
+        monkeypatch.delenv("CLONOS_ONE_PASS")
+    else:
+        e = Engine(segment_bytes=256, pool_segments=1 << 16, timing=True, decode=request.param)
     yield e
     e.close()
