@@ -1625,7 +1625,7 @@ __device__ __forceinline__ void emit_tile(const TileDesc* __restrict__ tiles, co
   const uint32_t end_a = ea > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)ea;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   // bm_in: the lane's bitmap words straight from the count, the image still staged in L.img
-  // (the single-launch small decode); else both from memory
+  // (the single-launch small decode and the one pass); else both from memory
   u64x2 bits = bm_in ? u64x2{bm_in[0], bm_in[1]} : gp(reinterpret_cast<const u64x2*>(ctl.bits))[(uint64_t)t * 64 + lane];
   if (lane * kZRegion >= hi) bits = u64x2{0, 0};  // past the tile (the lane path of small spans skips them)
   JLPre pre{};
@@ -3117,6 +3117,7 @@ int launch_decode_fused(const TileDesc* d_tiles, uint32_t n_tiles, const SpanDes
   } else if (phase == 6) {  // the one-pass decode (no tables; ctl.lb, st_x and ex zeroed)
     if (ctl.jser) return CLG_E_INVALID_ARG;
     ZLAUNCH(k_decode_one, dim3(nt), dim3(64), 0, st, d_tiles, d_spans, ctl, out);
+
   } else if (phase == 5) {  // scan, block offsets and span ranges in one launch (ctl.lb zeroed)
     const uint32_t nb = (n_tiles + kZScanBlock - 1) / kZScanBlock;
     ZLAUNCH(k_decode_scan, dim3(nb), dim3(256), 0, st, d_tiles, d_spans, n_spans, ctl);
