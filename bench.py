@@ -844,9 +844,19 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
         return np.concatenate([epochs[e][:k], np.frombuffer(rec, np.uint8), epochs[e][k:]])
     special = {(37, 4): with_long(4, long_tt), (181, 7): with_long(7, long_js)}  # (log, epoch) -> bytes
 
-    def build_engine(variant, decode="auto"):
-        e_ = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
-                    timing=True, ifl_pool_segments=16, decode=decode)
+    def build_engine(variant, decode="auto", sidecar=True):
+        old = os.environ.get("CLONOS_SIDECAR")
+        if not sidecar:
+            os.environ["CLONOS_SIDECAR"] = "0"  # (read when the engine opens)
+        try:
+            e_ = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
+                        timing=True, ifl_pool_segments=16, decode=decode)
+        finally:
+            if not sidecar:
+                if old is None:
+                    del os.environ["CLONOS_SIDECAR"]
+                else:
+                    os.environ["CLONOS_SIDECAR"] = old
         ls = []
         for v in range(n_logs):  # every log: the epoch sequence rotated, so layouts differ per log
             log = e_.open_log(CausalLogID.main(v))
@@ -856,7 +866,15 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
             ls.append(log)
         e_.sync()
         return e_, ls
+
+    def write_cost(e_):
+        """The write path's kernel time for the whole log (every byte reaches HBM through
+        k_scatter once; with the sidecar it also lists the Serializable candidates)."""
+        st_ = e_.kernel_stats()
+        ks = [st_.get(n, {"launches": 0, "ms": 0.0}) for n in ("upstream_scatter", "append_scatter")]
+        return {"launches": sum(k["launches"] for k in ks), "ms_total": round(sum(k["ms"] for k in ks), 4)}
     eng, logs = build_engine("clean")
+    writer = {"with_sidecar": write_cost(eng)}
     cap = n_det + 16  # (the long-record variant holds two records more)
     o = [torch.empty(cap, dtype=torch.int32, device=dev), torch.empty(cap, dtype=torch.uint8, device=dev),
          torch.empty(cap, dtype=torch.int64, device=dev)]
@@ -941,6 +959,14 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
             return ms, paths, kms
         finally:
             e_.close()
+    # the write path without the sidecar, for the cost it moves from the decode to the writer
+    e_ns, _ = build_engine("clean", sidecar=False)
+    writer["without_sidecar"] = write_cost(e_ns)
+    e_ns.close()
+    writer["sidecar_ms_per_step"] = round(writer["with_sidecar"]["ms_total"] - writer["without_sidecar"]["ms_total"], 4)
+    writer["note"] = ("k_scatter time to write the whole config-3 log (0.9 GB, 2 560 upstream deltas), with and without "
+                      "the Serializable candidate lists; the difference is the decode work moved to the writer, "
+                      "paid once per byte written (one decode step's worth)")
     # the robust pipeline alone (the fallback's throughput) and the long-record batch
     rob_ms, _, rob_k = timed_decode("clean", "robust", n_det)
     # the long-record batch against the clean one through the same harness (a fresh engine each)
@@ -951,7 +977,7 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
            "wide_records": n_wide, "ms_per_step": round(el * 1e3, 4), "determinants_per_s": round(n_det / el, 1),
            "ms_per_step_one_at_a_time": round(el_sync * 1e3, 4),
            "log_gbs": round(total / el / 1e9, 2), "algo_gbs": round(algo / el / 1e9, 1),
-           "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern,
+           "hbm_frac": round(algo / el / 1e9 / HBM_PEAK_GBS, 4), "kernels": kern, "writer": writer,
            "truncate_all": {"logs": n_logs, "checkpoint": n_epochs // 2, "latency_ms": round(trunc_ms, 4)},
            "robust_pipeline": {"ms_per_step": round(rob_ms, 4), "determinants_per_s": round(n_det / rob_ms * 1e3, 1),
                                "log_gbs": round(total / rob_ms / 1e6, 2), "kernels_ms": rob_k},
