@@ -963,10 +963,55 @@ def config3(args, torch, dev, n_logs=256, n_epochs=10, per_epoch=40000, steps=5)
     e_ns, _ = build_engine("clean", sidecar=False)
     writer["without_sidecar"] = write_cost(e_ns)
     e_ns.close()
-    writer["sidecar_ms_per_step"] = round(writer["with_sidecar"]["ms_total"] - writer["without_sidecar"]["ms_total"], 4)
-    writer["note"] = ("k_scatter time to write the whole config-3 log (0.9 GB, 2 560 upstream deltas), with and without "
-                      "the Serializable candidate lists; the difference is the decode work moved to the writer, "
-                      "paid once per byte written (one decode step's worth)")
+    writer["per_call_latency_us"] = {k: round(v["ms_total"] * 1e3 / max(1, v["launches"]), 2) for k, v in writer.items()}
+
+    def batched_write(sidecar):
+        """The same 0.9 GB written as one device-input upstream batch per epoch (256 deltas
+        each, clg_upstream_delta_batch from HBM): the writer's throughput, where the per-call
+        figures above are one wave's latency per chunk."""
+        from clonos_amd import dist as X
+        old = os.environ.get("CLONOS_SIDECAR")
+        if not sidecar:
+            os.environ["CLONOS_SIDECAR"] = "0"
+        try:
+            e_ = Engine(segment_bytes=seg, pool_segments=n_logs * ((per_log + seg - 1) // seg + n_epochs + 1) + 64,
+                        timing=True, ifl_pool_segments=16)
+        finally:
+            if not sidecar:
+                if old is None:
+                    del os.environ["CLONOS_SIDECAR"]
+                else:
+                    os.environ["CLONOS_SIDECAR"] = old
+        try:
+            ls = [e_.open_log(CausalLogID.main(v)) for v in range(n_logs)]
+            blob = np.concatenate(epochs)
+            eoff = np.concatenate([[0], np.cumsum([int(x.size) for x in epochs])]).astype(np.uint64)
+            d_blob = torch.from_numpy(blob).to(dev)
+            torch.cuda.synchronize()
+            e_.kernel_stats_reset()
+            t0 = _t.perf_counter()
+            for e in range(n_epochs):
+                req = np.zeros(n_logs, X.DELTA_REQ)
+                req["log"] = [l.handle for l in ls]
+                req["epoch"] = e
+                k = (np.arange(n_logs) + e) % n_epochs  # (each log's epoch sequence rotated, as above)
+                req["src_off"] = eoff[k]
+                req["len"] = (eoff[k + 1] - eoff[k]).astype(np.uint32)
+                e_.upstream_delta_batch(req.ctypes.data, n_logs, d_blob.data_ptr(), _lib.CLG_MEM_DEVICE)
+            torch.cuda.synchronize()
+            wall = (_t.perf_counter() - t0) * 1e3
+            return dict(write_cost(e_), wall_ms=round(wall, 3), gbs=round(total / (wall * 1e-3) / 1e9, 2))
+        finally:
+            e_.close()
+    writer["batched_with_sidecar"] = batched_write(True)
+    writer["batched_without_sidecar"] = batched_write(False)
+    writer["sidecar_ms_per_step"] = round(writer["batched_with_sidecar"]["ms_total"] -
+                                          writer["batched_without_sidecar"]["ms_total"], 4)
+    writer["note"] = ("k_scatter time to write the whole config-3 log (0.9 GB) with and without the Serializable "
+                      "candidate lists (the decode work moved to the writer, paid once per byte written: one decode "
+                      "step's worth): as 2 560 one-log calls (per-call latency: one wave per 16 KiB chunk measures "
+                      "its candidates) and as 10 batched device-input calls of 256 deltas (throughput); "
+                      "sidecar_ms_per_step from the batched figures")
     # the robust pipeline alone (the fallback's throughput) and the long-record batch
     rob_ms, _, rob_k = timed_decode("clean", "robust", n_det)
     # the long-record batch against the clean one through the same harness (a fresh engine each)

@@ -1,7 +1,7 @@
 """GPU decode fuzzer (a checker, run by hand on a GPU box; not collected by pytest):
 random batches of spans -- every tag, Serializable streams, long records, zero runs, dense
-short strings, byte flips that make decode errors -- decoded by the engine (auto, the three-pass path and the robust
-pipeline alone), and the same bytes as logs in 4 KiB HBM segments delivered over a few
+short strings, byte flips that make decode errors -- decoded by the engine (auto, the three-pass path, the one-pass
+decode forced (CLONOS_ONE_PASS=2) and the robust pipeline alone), and the same bytes as logs in 4 KiB HBM segments delivered over a few
 epochs (decode_logs from a random start epoch), compared with the C++ oracle's decodeNext
 loop span by span: bit-exact records, or the lowest failing span's (status, offset, tag).  Prints one JSON line per
 round; stops at the first mismatch with its seed.
@@ -152,6 +152,9 @@ rng0 = np.random.default_rng(args.seed)
 engines = {"auto": Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True),
            "three_pass": Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True, decode="three_pass"),
            "robust": Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True, decode="robust")}
+os.environ["CLONOS_ONE_PASS"] = "2"  # (read when an engine opens: the one-pass decode on every batch it may take)
+engines["one_pass"] = Engine(segment_bytes=16384, pool_segments=1 << 15, timing=True, decode="three_pass")
+del os.environ["CLONOS_ONE_PASS"]
 log_eng = Engine(segment_bytes=4096, pool_segments=1 << 19, timing=True)  # logs over 4 KiB segments
 t_end = time.time() + args.minutes * 60
 rnd = 0
