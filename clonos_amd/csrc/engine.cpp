@@ -1932,6 +1932,7 @@ struct clg_engine {
     hsub.emplace(this, "host_launch_enqueue");
     clg::DecodeOut o{};
     CHK(prep_out(out, &o));
+    hsub->lap("host_enq_out");
     // words: st_x[nt] ex[nt] rep_flag[nt] (u8) cnt[nt] base[nt] boff[nb] | span_lo[ns] span_hi[ns] |
     // abort[8] rep[4] (u32) | lb: ticket, look-back[nb] | ent[G]; bits apart.  st_x, ex,
     // rep_flag, the abort and repair words, lb and ent are zeroed per batch.
@@ -1947,6 +1948,7 @@ struct clg_engine {
     CHK(d_zerr.ensure(std::max<size_t>(1, ns) * 8));
     PinBuf& h_zres = h_zres_s[r->slot];
     CHK(h_zres.ensure((2 * size_t(ns) + n_ab + 1) * 8));  // (+ the table work counters)
+    hsub->lap("host_enq_bufs");
     uint64_t* w = d_zctl.as<uint64_t>();
     uint32_t* ab = reinterpret_cast<uint32_t*>(w + o_ab);
     if (zdbg) CHK(d_dbg.ensure(clg::kZDbgTiles * 4 + size_t(nt) * 16));
@@ -1988,6 +1990,7 @@ struct clg_engine {
     const bool host_res = ns <= kHostResSpans;
     ctl.h_res = host_res ? h_zres.as<uint64_t>() : nullptr;
     memset(h_zres.p, 0, (2 * size_t(ns) + n_ab + 1) * 8);  // (a batch without tiles runs no scan)
+    hsub->lap("host_enq_memset");
     r->ctl = ctl;
     r->o = o;
     auto* zt = d_ztiles.as<clg::TileDesc>();
@@ -2003,6 +2006,7 @@ struct clg_engine {
       // table, and the zeroed control words (st_x, ex, rep_flag; abort words and repair
       // counters; bad-span flags; kept-error offsets ~0; the jser work counters)
       HIPCHK(hipMemcpyAsync(d_plan.p, h_plan_s[plan_slot].p, L.hb, hipMemcpyHostToDevice, stream));
+      hsub->lap("host_enq_h2d");
       {
         clg::PrepArgs pa{};
         const bool runs = !p.runs.empty();
@@ -2027,6 +2031,7 @@ struct clg_engine {
                                  jser && side.hdr ? 1u : 0u, 0, 0};  // the sidecar's scan-list count
         CHK(clg::launch_decode_prep(pa, stream));
       }
+      hsub->lap("host_enq_prep");
       if (zdbg) HIPCHK(hipMemsetAsync(d_dbg.p, 0, clg::kZDbgTiles * 4 + size_t(nt) * 16, stream));
       if (prof_path) HIPCHK(hipMemsetAsync(d_prof.p, 0, size_t(nt) * (one ? 128 : 64), stream));
       if (evp) HIPCHK(hipEventRecord(evp[0], stream));
@@ -2045,6 +2050,7 @@ struct clg_engine {
         if (ev) HIPCHK(hipEventRecord(ev[2 * k + 1], stream));
       }
       if (evp) HIPCHK(hipEventRecord(evp[1], stream));
+      hsub->lap("host_enq_kernels");
       // the span ranges and abort words: in h_zres already (the scan wrote them) or read back
       // now (emit ran right behind the scan: it returns at once when the batch aborted, and its
       // stores are bounded by the output capacity)
@@ -2054,6 +2060,7 @@ struct clg_engine {
         if (jser)  // the table work counters beside them (the scan copies them when it writes h_res)
           HIPCHK(hipMemcpyAsync(h_zres.as<uint64_t>() + 2 * size_t(ns) + n_ab, ctl.jwork, 8, hipMemcpyDeviceToHost, stream));
       }
+      hsub->lap("host_enq_d2h");
       if (jser) CHK(jarena_note(r->note()));
       if (r->slot) {
         if (!zdone[r->slot]) HIPCHK(hipEventCreateWithFlags(&zdone[r->slot], hipEventDisableTiming));
