@@ -1399,8 +1399,20 @@ struct clg_engine {
     // a builder that could not plan a log (a queued decode's re-plan after a rebase found its
     // range gone): the decode fails with this status instead of decoding an empty span
     int status = CLG_OK;
+    // plan_parallel wrote the runs, segment table and spans straight into the pinned plan
+    // buffer of decode slot stage_slot (stage_plan then adds only the chunk table); runs and
+    // segtab stay empty, their sizes are n_runs / n_segs.  A re-launch of the plan (an abort's
+    // fallbacks) re-plans it from its builder first (unstage).
+    bool staged = false;
+    uint32_t stage_slot = 0;
+    size_t n_runs = 0, n_segs = 0;
+    size_t run_count() const { return staged ? n_runs : runs.size(); }
+    size_t seg_count() const { return staged ? n_segs : segtab.size(); }
     void reset() {  // empty, capacity kept (a config-4 plan is ~4 MB: fresh pages cost page faults)
       status = CLG_OK;
+      staged = false;
+      stage_slot = 0;
+      n_runs = n_segs = 0;
       tiles.clear();
       spans.clear();
       runs.clear();
@@ -1517,7 +1529,11 @@ struct clg_engine {
   // and sizes, then the parts' offsets, then each part writes its entries in place.  false:
   // not applicable (no device planning) or a log failed -- the caller runs the serial loop,
   // which reports the error.
-  bool plan_parallel(DecodePlan& p, const uint32_t* log, const int64_t* start_epoch, uint32_t n, uint64_t* total) {
+  // stage >= 0: the runs, segment table and spans go straight into that decode slot's pinned
+  // plan buffer (DecodePlan::staged; the spans into p.spans too, which the host reads), so the
+  // launch copies nothing on the host but the chunk table.
+  bool plan_parallel(DecodePlan& p, const uint32_t* log, const int64_t* start_epoch, uint32_t n, uint64_t* total,
+                     int stage = -1) {
     const uint32_t U = tile_unit(clg::kZTile), Cb = C();
     if (!U) return false;
     WorkPool* wp = workers();
@@ -1567,10 +1583,31 @@ struct clg_engine {
     p.reset();
     p.unit = U;
     p.spans.resize(n);
-    p.runs.resize(at[P].runs);
-    p.segtab.resize(at[P].segs);
     p.n_tiles = uint32_t(at[P].tiles);
     p.n_tiny = uint32_t(at[P].tiny);
+    clg::SegSpan* runs_out;
+    uint32_t* seg_out;
+    clg::SpanDesc* spans_copy = nullptr;
+    if (stage >= 0) {  // the layout stage_plan computes, room for the count pass's chunk table after it
+      PlanLayout L;
+      plan_layout(0, at[P].runs * sizeof(clg::SegSpan), at[P].segs * sizeof(uint32_t), size_t(n) * sizeof(clg::SpanDesc),
+                  (size_t(p.n_tiles) + 2) * sizeof(uint32_t), &L);
+      PinBuf& h = h_plan_s[stage];
+      if (h.ensure(L.hb + 64) != CLG_OK) return false;
+      uint8_t* hd = h.as<uint8_t>();
+      runs_out = reinterpret_cast<clg::SegSpan*>(hd + L.o_runs);
+      seg_out = reinterpret_cast<uint32_t*>(hd + L.o_seg);
+      spans_copy = reinterpret_cast<clg::SpanDesc*>(hd + L.o_spans);
+      p.staged = true;
+      p.stage_slot = uint32_t(stage);
+      p.n_runs = at[P].runs;
+      p.n_segs = at[P].segs;
+    } else {
+      p.runs.resize(at[P].runs);
+      p.segtab.resize(at[P].segs);
+      runs_out = p.runs.data();
+      seg_out = p.segtab.data();
+    }
     wp->run([&](unsigned k, unsigned) {
       uint64_t tile = at[k].tiles, run = at[k].runs, seg = at[k].segs;
       for (uint32_t i = k * per; i < std::min(n, (k + 1) * per); ++i) {
@@ -1578,10 +1615,11 @@ struct clg_engine {
         const int32_t start = st[i], len = nb[i];
         const uint32_t c = cnt_of(start, len);
         p.spans[i] = clg::SpanDesc{uint32_t(tile), c, uint64_t(len)};
+        if (spans_copy) spans_copy[i] = p.spans[i];
         if (c) {  // plan_log_span's device-planning entries
           const uint32_t s0 = uint32_t(start) / Cb, s1 = uint32_t(start + len - 1) / Cb + 1;
-          p.runs[run++] = clg::SegSpan{seg, uint32_t(start) - s0 * Cb, uint32_t(len), i, uint32_t(tile), 0};
-          std::copy(l.segs.begin() + s0, l.segs.begin() + s1, p.segtab.begin() + seg);
+          runs_out[run++] = clg::SegSpan{seg, uint32_t(start) - s0 * Cb, uint32_t(len), i, uint32_t(tile), 0};
+          std::copy(l.segs.begin() + s0, l.segs.begin() + s1, seg_out + seg);
           seg += s1 - s0;
         }
         tile += c;
@@ -1613,13 +1651,7 @@ struct clg_engine {
   // Host half: the plan's descriptors (and the count pass's chunk table, if any) into the
   // pinned plan buffer (its own: an asynchronous decode may still be uploading it while later
   // calls -- flush, slices -- stage theirs).
-  int stage_plan(const DecodePlan& p, DevBuf& dtiles, PlanLayout* L, const std::vector<uint32_t>* chunk = nullptr) {
-    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
-    CHK(dtiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
-    CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
-    const size_t tb = p.tiles.size() * sizeof(clg::TileDesc), rb = p.runs.size() * sizeof(clg::SegSpan),
-                 gb = p.segtab.size() * sizeof(uint32_t), sb = ns * sizeof(clg::SpanDesc),
-                 cb = chunk ? chunk->size() * sizeof(uint32_t) : 0;
+  static void plan_layout(size_t tb, size_t rb, size_t gb, size_t sb, size_t cb, PlanLayout* L) {
     L->tb = tb;
     L->sb = sb;
     L->o_runs = (tb + 15) & ~size_t(15);
@@ -1627,7 +1659,24 @@ struct clg_engine {
     L->o_spans = (L->o_seg + gb + 15) & ~size_t(15);
     L->o_chunk = (L->o_spans + sb + 15) & ~size_t(15);
     L->hb = L->o_chunk + cb;
+  }
+  int stage_plan(const DecodePlan& p, DevBuf& dtiles, PlanLayout* L, const std::vector<uint32_t>* chunk = nullptr) {
+    const uint32_t nt = p.n_tiles, ns = uint32_t(p.spans.size());
+    CHK(dtiles.ensure(std::max<size_t>(1, nt) * sizeof(clg::TileDesc)));
+    CHK(d_spans.ensure(ns * sizeof(clg::SpanDesc)));
+    const size_t cb = chunk ? chunk->size() * sizeof(uint32_t) : 0;
+    plan_layout(p.tiles.size() * sizeof(clg::TileDesc), p.run_count() * sizeof(clg::SegSpan),
+                p.seg_count() * sizeof(uint32_t), ns * sizeof(clg::SpanDesc), cb, L);
     PinBuf& h_plan = h_plan_s[plan_slot];
+    if (p.staged) {  // runs, segment table and spans are in place (plan_parallel): the chunk table
+      if (p.stage_slot != plan_slot || h_plan.cap < L->hb + 64)
+        return fail(CLG_E_STATE, "staged decode plan in slot %u, launched in slot %u", p.stage_slot, plan_slot);
+      CHK(d_plan.ensure(L->hb));
+      if (cb) memcpy(h_plan.as<uint8_t>() + L->o_chunk, chunk->data(), cb);
+      return CLG_OK;
+    }
+    const size_t tb = L->tb, rb = p.runs.size() * sizeof(clg::SegSpan), gb = p.segtab.size() * sizeof(uint32_t),
+                 sb = L->sb;
     CHK(h_plan.ensure(L->hb + 64));
     CHK(d_plan.ensure(L->hb));
     uint8_t* hd = h_plan.as<uint8_t>();
@@ -1915,7 +1964,7 @@ struct clg_engine {
     // (default: logs in segments of at least two tiles, or host input -- tiles of a few hundred
     // bytes give canonical exits from too few bytes, which often miss, and the batch goes again)
     const bool one = one_pass && allow_one && !jser && !p.n_tiny && !zdbg &&
-                     ((nt > clg::kZSmallTilesMax && (p.runs.empty() || C() >= 2 * clg::kZTile)) || one_pass == 2);
+                     ((nt > clg::kZSmallTilesMax && (!p.run_count() || C() >= 2 * clg::kZTile)) || one_pass == 2);
     r->one = one;
     const uint32_t G = clg::decode_count_grid(jser, nt);
     const bool chunked = G && nt > G && ns > 1 && !one;
@@ -2009,9 +2058,9 @@ struct clg_engine {
       hsub->lap("host_enq_h2d");
       {
         clg::PrepArgs pa{};
-        const bool runs = !p.runs.empty();
+        const bool runs = p.run_count() != 0;
         pa.runs = reinterpret_cast<const clg::SegSpan*>(d_plan.as<uint8_t>() + L.o_runs);
-        pa.n_runs = uint32_t(p.runs.size());
+        pa.n_runs = uint32_t(p.run_count());
         pa.n_tiles = runs ? nt : 0;
         pa.segtab = reinterpret_cast<const uint32_t*>(d_plan.as<uint8_t>() + L.o_seg);
         pa.pool = pool;
@@ -2240,7 +2289,7 @@ struct clg_engine {
   bool small_flip = false;
   bool small_ok(const DecodePlan& p, uint64_t log_bytes, const clg_decoded* out) const {
     if (!small_decode || jser_hint || p.spans.empty() || p.spans.size() > kSmallSpans || log_bytes > kSmallBytes ||
-        p.only)
+        p.only || p.staged)
       return false;
     if (out->out_kind == CLG_MEM_HOST && out->cap * 13 + out->wcap * 25 > kSmallHostOut) return false;
     if (out->out_kind == CLG_MEM_MAPPED && !mapped_outputs(*out, nullptr)) return false;
@@ -2647,6 +2696,11 @@ struct clg_engine {
   int after_abort(DecodePlan& pf, Build&& build, uint64_t log_bytes, clg_decoded* out, uint64_t* span_rec_base,
                   bool need_jser) {
     bool aborted = true, nj = false;
+    if (pf.staged) {  // its runs and segment table live only in the pinned buffer: planned again
+      pf.reset();
+      build(pf, clg::kZTile);
+      CHK(plan_ok(pf));
+    }
     // the one-pass decode aborted (a case its rules leave to the three passes): those
     if (zlast.one) {
       allow_one = false;
@@ -2760,8 +2814,8 @@ struct clg_engine {
     bool clash = !queue;
     for (const auto& d : pq)
       if (d.active && d.out->out_kind != CLG_MEM_DEVICE) clash = true;
-    if (queue && (pf.n_tiles > hw_tiles || pf.spans.size() > hw_spans || pf.runs.size() > hw_runs ||
-                  pf.segtab.size() > hw_segs || (jser_hint && !hw_jser)))
+    if (queue && (pf.n_tiles > hw_tiles || pf.spans.size() > hw_spans || pf.run_count() > hw_runs ||
+                  pf.seg_count() > hw_segs || (jser_hint && !hw_jser)))
       clash = true;
     if (clash) CHK(settle());
     if (!queue) {  // nothing to queue, or too large for the fast path: decoded now
@@ -2772,21 +2826,18 @@ struct clg_engine {
       return push_settled(decode(build, log_bytes, out, span_rec_base), out);
     }
     reset_result(out);
-    uint32_t slot = 1;  // a slot no queued decode holds
-    for (; slot < kSlots; ++slot) {
-      bool used = false;
-      for (const auto& d : pq)
-        if (d.active && d.run.slot == slot) used = true;
-      if (!used) break;
-    }
-    if (slot == kSlots) return fail(CLG_E_STATE, "no free decode slot");  // (cannot happen: bounded by the caller)
+    // a slot no queued decode holds: the one the plan was staged for (free still: planned in
+    // this call, and a settle above only frees slots)
+    const uint32_t slot = pf.staged ? pf.stage_slot : free_slot();
+    if (slot == 0 || slot >= kSlots || slot_used(slot))
+      return fail(CLG_E_STATE, "no free decode slot");  // (cannot happen: bounded by the caller)
     FusedRun r;
     r.slot = slot;
     CHK(launch_fused(pf, log_bytes, out, jser_hint, &r));
     hw_tiles = std::max<uint64_t>(hw_tiles, pf.n_tiles);
     hw_spans = std::max<uint64_t>(hw_spans, pf.spans.size());
-    hw_runs = std::max<uint64_t>(hw_runs, pf.runs.size());
-    hw_segs = std::max<uint64_t>(hw_segs, pf.segtab.size());
+    hw_runs = std::max<uint64_t>(hw_runs, pf.run_count());
+    hw_segs = std::max<uint64_t>(hw_segs, pf.seg_count());
     hw_jser = hw_jser || r.jser;
     PendingDecode d;
     d.active = true;
@@ -2801,6 +2852,16 @@ struct clg_engine {
     return CLG_OK;
   }
 
+  bool slot_used(uint32_t slot) const {
+    for (const auto& d : pq)
+      if (d.active && d.run.slot == slot) return true;
+    return false;
+  }
+  uint32_t free_slot() const {  // the first asynchronous decode slot no queued decode holds (kSlots: none)
+    uint32_t slot = 1;
+    while (slot < kSlots && slot_used(slot)) ++slot;
+    return slot;
+  }
   // Completes the queued decodes [0, upto] (all: upto = SIZE_MAX), oldest first.
   int settle(size_t upto = SIZE_MAX) {
     for (size_t i = 0; i < pq.size() && i <= upto; ++i) {
@@ -3733,7 +3794,7 @@ int clg_decode_logs(clg_engine* e, const uint32_t* log, const int64_t* start_epo
   }
   {
     clg_engine::HostTimer ht(e, "host_decode_plan");
-    if (!(n >= clg_engine::kParallelLogs && e->fused_decode && e->plan_parallel(pf, log, start_epoch, n, &total))) {
+    if (!(n >= clg_engine::kParallelLogs && e->fused_decode && e->plan_parallel(pf, log, start_epoch, n, &total, 0))) {
       total = 0;
       pf.reset();
       for (uint32_t i = 0; i < n; ++i) {
@@ -3777,7 +3838,8 @@ int clg_decode_logs_async(clg_engine* e, const uint32_t* log, const int64_t* sta
     clg_engine::HostTimer ht(e, "host_decode_plan");
     e->zst.assign(n, 0);  // (plan_parallel's ranges go here)
     e->znb.assign(n, 0);
-    planned = e->plan_parallel(pf, log, start_epoch, n, &total);
+    const uint32_t fs = e->free_slot();  // (the plan is staged for that slot)
+    planned = e->plan_parallel(pf, log, start_epoch, n, &total, fs < clg_engine::kSlots ? int(fs) : -1);
   }
   if (planned) {
     st.assign(e->zst.begin(), e->zst.begin() + n);
