@@ -635,3 +635,53 @@ def test_many_span_decode_chunked_on_host_threads():
             got = eng.decode_logs_async(logs, [0] * n_logs).wait()
             for f in ("off", "tag", "v0", "w_idx", "w_rc", "w_v1", "w_var_off", "w_var_len", "w_sub", "span_rec_base"):
                 np.testing.assert_array_equal(getattr(got, f), getattr(dec, f), err_msg=f)
+
+
+@pytest.mark.parametrize("case", ["error", "serializable"])
+def test_many_span_staged_plan_fallbacks(case):
+    """A 9000-log decode whose plan is staged straight into the decode slot's pinned buffer
+    (engine.cpp plan_parallel, DecodePlan::staged), synchronous and queued, when the fast run
+    aborts and the fallbacks plan the batch again from its builder: a decode error in one log
+    (the oracle's status, span, offset and tag; kept on the fast path or decoded by the per-span
+    fallback), or Serializable records in a few logs while the engine's last batches had none
+    (the fast run without tables aborts, the batch goes again with them): every sampled span
+    equals the oracle's."""
+    from test_gpu_decode import assert_span_equal
+    rng = np.random.default_rng(94 if case == "error" else 95)
+    n_logs, seg = 9000, 4096
+    with Engine(segment_bytes=seg, pool_segments=n_logs * 4, timing=True, ifl_pool_segments=16) as eng:
+        logs, blobs = [], []
+        for v in range(n_logs):
+            lg = eng.open_log(CausalLogID.main(v))
+            b = synth.random_log(int(rng.integers(1, 300)), rng, allow_serializable=False)
+            if case == "error" and v == 4321:
+                b = b[:len(b) // 2] + b"\x08" + b[len(b) // 2:]  # tag 8: decodeNext rejects it
+            if case == "serializable" and v % 1500 == 7:
+                b = b + synth.random_log(40, rng, allow_serializable=True) + D.encode(
+                    D.SerializableDeterminant(D.jser_string("s" * 20)))
+            lg.processUpstreamDelta(b, 0, 0)
+            logs.append(lg)
+            blobs.append(b)
+        bad = [(s, O.decode(b)) for s, b in enumerate(blobs)]
+        bad = [(s, r) for s, r in bad if r[0] != 0]
+        sample = sorted(set(list(range(0, n_logs, 89)) + [7, 1507, 4321, n_logs - 1]))
+        for mode in ("async", "sync", "async"):  # (the first decode of the Serializable case aborts)
+            if case == "error":
+                s, (st, _, eo, et) = bad[0]
+                with pytest.raises(ClonosError) as ex:
+                    if mode == "sync":
+                        eng.decode_logs(logs, [0] * n_logs)
+                    else:
+                        eng.decode_logs_async(logs, [0] * n_logs).wait()
+                assert (ex.value.status, ex.value.err_span, ex.value.err_off, ex.value.err_tag) == (st, s, eo, et)
+            else:
+                assert not bad
+                dec = eng.decode_logs(logs, [0] * n_logs) if mode == "sync" else \
+                    eng.decode_logs_async(logs, [0] * n_logs).wait()
+                for s in sample:
+                    assert_span_equal(dec, s, blobs[s])
+        ks = eng.kernel_stats()
+        if case == "error":  # the fallbacks ran: the error kept, or its span decoded apart
+            assert "decode_kept_errors" in ks or "decode_span_fallback" in ks, sorted(ks)
+        else:  # the fast run without tables aborted, and ran again with them
+            assert "decode_jser_retry" in ks, sorted(ks)
