@@ -1442,7 +1442,8 @@ struct clg_engine {
     return std::max(1, n);
   }
   // Host threads for the per-log loops: CLONOS_HOST_THREADS, else up to 16 of the usable CPUs.
-  // Config 4's step on one box (tools/r5_call6.sh): 2.49 ms with 16 against 3.1-3.4 ms with 8.
+  // Config 4's step on one box (round 5): 2.49 ms with 16 against 3.1-3.4 ms with 8; round 6,
+  // median of four each: 2.09 / 2.20 / 2.40 ms with 16 / 14 / 12.
   WorkPool* workers() {
     if (!host_pool) {
       const char* v = getenv("CLONOS_HOST_THREADS");
