@@ -1871,7 +1871,8 @@ struct clg_engine {
 
   // Speculative warm-up bytes before each lane's region (CLONOS_WARM overrides; tuning aid).
   // Measured on MI355X (tools/r3_warm.sh): 96 B is best for short fixed-length records
-  // (config 2: count 0.176 ms at 96 B, 0.194 at 64, 0.182 at 128).  With Serializable
+  // (config 2: count 0.176 ms at 96 B, 0.194 at 64, 0.182 at 128; round 6, with the lean walk
+  // and the staggered starts, 64-128 B within 2 %: pipeline 0.430-0.437 ms).  With Serializable
   // tables the count pass walks the step-code map, whose steps no longer diverge on wide
   // records, and 48-128 B are best too (config-3 subset: 0.43-0.44 ms, 0.451 at 16 B).
   static uint32_t spec_warm(bool /*jser*/) {
